@@ -1,0 +1,236 @@
+/*
+ * optiland_rt.h -- C ABI of the MI355X sequential real-ray-trace core.
+ *
+ * This library replaces the per-surface Python loop of the reference
+ *   optiland/surfaces/surface_group.py:232-244      SurfaceGroup.trace(rays, skip)
+ *   optiland/surfaces/standard_surface.py:186-233   Surface.trace (real-ray branch)
+ * together with the ray construction it is fed by
+ *   optiland/rays/ray_generator.py:28-106            RayGenerator.generate_rays
+ *   optiland/fields/field_types.py:139-180           AngleField.get_ray_origins
+ * and the image-space propagate in optiland/raytrace/real_ray_tracer.py:84-89.
+ *
+ * Everything here is plain C: device pointers, sizes and a hipStream_t (passed as
+ * void* so the header does not need HIP headers). Every pointer named "device" must
+ * point to device (HBM) memory owned by the caller. Calls are asynchronous on the
+ * given stream; nothing in this library allocates, frees or synchronises, so any call
+ * can be captured in a hipGraph.
+ *
+ * Floating-point: fp64 throughout, compiled with -ffp-contract=off so that every
+ * +,-,*,/,sqrt is evaluated in the same order and rounding as the reference NumPy
+ * backend (see DESIGN.md "Parity").
+ */
+#ifndef OPTILAND_RT_H
+#define OPTILAND_RT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ORT_ABI_VERSION 1
+#define ORT_MAX_SURFACES 64
+
+/* ---- geometry kinds ----------------------------------- */
+enum ort_geometry { /* see optiland/geometries */
+  ORT_GEOM_PLANE = 0,        /* plane.py:61-98                                     */
+  ORT_GEOM_STANDARD = 1,     /* standard.py:73-167 (sphere / conic)                */
+  ORT_GEOM_EVEN_ASPHERE = 2, /* even_asphere.py:82-129 + newton_raphson.py:119-168 */
+  ORT_GEOM_ODD_ASPHERE = 3,  /* odd_asphere.py:73-130 + newton_raphson.py:119-168  */
+  ORT_GEOM_ZERNIKE = 4       /* zernike.py:133-246 + zernike/base.py:42-299        */
+};
+
+/* ---- surface flags ------------------------------------------------------------ */
+enum ort_surface_flags {
+  ORT_SURF_REFLECTIVE = 1u << 0, /* interaction_model.is_reflective (material "mirror") */
+  ORT_SURF_RADIUS_INF = 1u << 1, /* standard.py:100-103 plane branch of a conic guess   */
+  ORT_SURF_APERTURE = 1u << 2,   /* radial physical aperture: physical_apertures/radial.py */
+  ORT_SURF_RECORD = 1u << 3      /* snapshot the ray state after this surface (_record)  */
+};
+
+/* ---- coordinate-system op (coordinate_system.py:73-107, real_rays.py:90-130) ---- */
+enum ort_cs_kind {
+  ORT_CS_TRANSLATE = 0, /* p = (dx, dy, dz)                         rays/base.py:28-42 */
+  ORT_CS_ROT_X = 1,     /* p = (cos a, sin a)                       real_rays.py:90-102 */
+  ORT_CS_ROT_Y = 2,     /*                                          real_rays.py:104-116 */
+  ORT_CS_ROT_Z = 3      /*                                          real_rays.py:118-130 */
+};
+
+typedef struct ort_cs_op {
+  int32_t kind;
+  int32_t reserved;
+  double p[3];
+} ort_cs_op; /* 32 bytes */
+
+/* One traced surface (the object surface is not in the table: it only records,
+ * object_surface.py:56-72). Localize = cs ops [cs_loc_off, +n_cs_loc) applied in
+ * order; globalize = [cs_glob_off, +n_cs_glob) applied in order. */
+typedef struct ort_surface {
+  double radius;      /* R (may be +-inf)                                            */
+  double conic;       /* k                                                           */
+  double tol;         /* Newton tolerance            newton_raphson.py:58-61         */
+  double norm_radius; /* Zernike normalisation radius zernike.py:91-116             */
+  double ap_rmax2;    /* r_max**2 of a radial aperture  radial.py:50-63              */
+  double ap_rmin2;    /* r_min**2                                                    */
+  int32_t geometry;   /* enum ort_geometry                                           */
+  int32_t flags;      /* enum ort_surface_flags                                      */
+  int32_t max_iter;   /* Newton max_iter                                             */
+  int32_t n_coef;     /* asphere coefficients / Zernike terms                        */
+  int32_t coef_off;   /* offset into lens.coef (asphere) or lens.zern (Zernike)      */
+  int32_t mat_pre;    /* column of n_tab/alpha_tab for material_pre                  */
+  int32_t mat_post;   /* column for material_post                                    */
+  int32_t cs_loc_off;
+  int32_t n_cs_loc;
+  int32_t cs_glob_off;
+  int32_t n_cs_glob;
+  int32_t rec_slot;   /* slot in the record buffer when ORT_SURF_RECORD              */
+} ort_surface; /* 96 bytes */
+
+/* One Zernike term: c * norm * R_n^|m|(rho) * {cos m phi | sin |m| phi}
+ * (zernike/base.py:42-68, 228-299). Radial coefficients a_k (for rho^(n-2k)) and
+ * derivative coefficients d_k (for rho^(n-2k-1)) live in lens.coef at rad_off and
+ * rad_off + n_rad. */
+typedef struct ort_zernike_term {
+  double c;
+  double norm;
+  int32_t n;
+  int32_t m;
+  int32_t rad_off;
+  int32_t n_rad;
+} ort_zernike_term; /* 32 bytes */
+
+/* The lowered lens (all pointers are device pointers). */
+typedef struct ort_lens {
+  const ort_surface* surfaces;
+  const ort_cs_op* cs_ops;
+  const double* coef;
+  const ort_zernike_term* zern;
+  const double* n_tab;     /* [n_lambda][n_mat] refractive index n(lambda)          */
+  const double* alpha_tab; /* [n_lambda][n_mat] 4*pi*k/lambda (0 when k == 0)       */
+  int32_t n_surfaces;      /* traced surfaces S (<= ORT_MAX_SURFACES)               */
+  int32_t n_lambda;
+  int32_t n_mat;
+  int32_t final_mat;       /* material_post of the last surface (image space); < 0:  *
+                            * no image-space propagate (bare SurfaceGroup.trace)     */
+  uint32_t geometry_mask;  /* OR of (1u << geometry) over the surfaces; selects the  */
+  int32_t reserved;        /* kernel specialisation (no Newton code for sphere lenses) */
+  double final_thickness;  /* real_ray_tracer.py:84-89 image-space propagate distance */
+} ort_lens;
+
+/* Ray state, structure of arrays, one double per ray per attribute (device). */
+typedef struct ort_rays {
+  double* x;
+  double* y;
+  double* z;
+  double* L;
+  double* M;
+  double* N;
+  double* i;
+  double* opd;
+} ort_rays;
+
+/* Per (field, wavelength) segment parameters for in-kernel ray generation
+ * (ray_generator.py:71-89 + field_types.py:160-172, infinite object, AngleField,
+ * or field_types.py:173-181 finite object). Host scalars are computed in NumPy. */
+enum ort_gen_mode { ORT_GEN_INFINITE = 0, ORT_GEN_FINITE = 1 };
+typedef struct ort_segment {
+  double epd;      /* EPD (paraxial.py:232-297)                                     */
+  double epl;      /* EPL (paraxial.py:207-230)                                     */
+  double vx, vy;   /* 1 - vignetting factor                                         */
+  double x_off;    /* infinite: -tan(radians(field_x)) * (offset + EPL); finite: x0 */
+  double y_off;
+  double z0;       /* starting plane z                                              */
+  int32_t lambda_idx;
+  int32_t mode;    /* enum ort_gen_mode                                             */
+} ort_segment; /* 64 bytes */
+
+/* A batch of rays: n_rays rays split into consecutive segments of seg_len rays (the
+ * reference's field-major layout real_ray_tracer.py:74-77, generalised to (field,
+ * wavelength) pairs). Rays also fall into "Newton groups" of group_len consecutive rays:
+ * one group is one reference trace call, over which the reference's global Newton stop
+ * rule (newton_raphson.py:148) applies. Usually group_len == seg_len (one Optic.trace per
+ * (field, wavelength)); trace_generic uses seg_len 1 and group_len n_rays.
+ * seg may be NULL: then every ray uses lambda index 0 and no ray generation is possible. */
+typedef struct ort_batch {
+  int64_t n_rays;
+  int64_t seg_len;        /* >= 1                                                    */
+  int64_t group_len;      /* >= 1                                                    */
+  int32_t n_seg;          /* entries in seg (>= ceil(n_rays / seg_len) when seg set) */
+  int32_t pupil_per_ray;  /* px/py hold n_rays points (1) or seg_len points tiled (0) */
+  const ort_segment* seg; /* device                                                   */
+} ort_batch;
+
+/* Newton semantics (newton_raphson.py:137-166). */
+enum ort_newton_mode {
+  /* Every ray performs exactly sched[s] updates at Newton surface s, and the kernel
+   * reports per surface the AND over rays of the "converged at update j" bitmask and
+   * the max over rays of the last non-converged update index, so the host can verify
+   * that sched[s] equals the reference's global stopping index
+   * (max|f| < tol over ALL rays). See ort_newton_stat. */
+  ORT_NEWTON_SCHEDULE = 0,
+  /* Per-wavefront early exit: a wave stops when all of its 64 lanes have
+   * |f| < tol (or max_iter). Faster, not bit-identical to the global criterion. */
+  ORT_NEWTON_WAVE = 1
+};
+
+typedef struct ort_newton_stat {
+  uint64_t conv_mask;  /* AND over rays: bit j set when |f(t_j)| < tol (j < 64)      */
+  int32_t last_bad;    /* max over rays of the largest j <= sched with |f(t_j)| >= tol
+                          or NaN; -1 when every ray converged at every j              */
+  int32_t max_updates; /* ORT_NEWTON_WAVE: max updates any wave performed            */
+} ort_newton_stat; /* 16 bytes */
+
+typedef struct ort_options {
+  int32_t newton_mode;   /* enum ort_newton_mode                                     */
+  int32_t start_surface; /* SurfaceGroup.trace skip, counted in traced surfaces (>= 0) */
+  /* ORT_NEWTON_SCHEDULE: device int32 [n_groups][n_surfaces], updates per Newton group
+   * and surface (entries of non-Newton surfaces are ignored). NULL means "max_iter"
+   * everywhere. */
+  const int32_t* sched;
+} ort_options;
+
+/* status bits written with atomicOr into *status (device int32) */
+enum ort_status {
+  ORT_STATUS_ZERNIKE_RANGE = 1u << 0 /* zernike.py:234-246 ValueError              */
+};
+
+/* ---- entry points ------------------------------------------------------------- */
+
+int ort_abi_version(void);
+
+/* Trace rays_in through the lens, writing rays_out (may alias rays_in for an in-place
+ * trace, as the reference mutates RealRays in place). rec (nullable) receives
+ * [n_rec][8][n_rays] doubles (x,y,z,L,M,N,i,opd) after every surface flagged
+ * ORT_SURF_RECORD, at its rec_slot (standard_surface.py:266-286). newton_stat
+ * (nullable; device, [n_groups][n_surfaces] entries, n_groups =
+ * ceil(n_rays / group_len)) and status (nullable;
+ * device int32) are initialised by this call. Returns 0, or a negative ort_error. */
+int ort_trace_sequential(const ort_lens* lens, const ort_rays* rays_in, ort_rays* rays_out,
+                         const ort_batch* batch, const ort_options* opt, double* rec,
+                         ort_newton_stat* newton_stat, int32_t* status, void* stream);
+
+/* Generate rays from pupil samples and trace them in one launch (the pupil
+ * coordinates are the only per-ray input: 16 bytes per ray). With pupil_per_ray == 0,
+ * px, py hold seg_len pupil points shared by every segment (real_ray_tracer.py:74-77:
+ * Px tiled over fields). */
+int ort_trace_pupil(const ort_lens* lens, const double* px, const double* py,
+                    ort_rays* rays_out, const ort_batch* batch, const ort_options* opt,
+                    double* rec, ort_newton_stat* newton_stat, int32_t* status,
+                    void* stream);
+
+/* Ray generation only (ray_generator.py:28-106): fills rays_out from pupil points. */
+int ort_generate_rays(const double* px, const double* py, ort_rays* rays_out,
+                      const ort_batch* batch, void* stream);
+
+/* Error codes */
+enum ort_error {
+  ORT_OK = 0,
+  ORT_ERR_ARG = -1,      /* null pointer / bad size                                   */
+  ORT_ERR_SURFACES = -2, /* n_surfaces outside [0, ORT_MAX_SURFACES]                  */
+  ORT_ERR_LAUNCH = -3    /* hipGetLastError() after launch                            */
+};
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OPTILAND_RT_H */

@@ -1,0 +1,110 @@
+"""NumPy mirrors of the C structs in include/optiland_rt.h.
+
+The host builds the lowered lens as NumPy structured arrays with exactly the C
+layout, so `arr.tobytes()` is the device image of the table. Offsets are asserted
+against the header sizes in tests/test_abi.py.
+"""
+
+from __future__ import annotations
+
+import numpy as np
+
+ABI_VERSION = 1
+MAX_SURFACES = 64
+
+# enum ort_geometry
+GEOM_PLANE = 0
+GEOM_STANDARD = 1
+GEOM_EVEN_ASPHERE = 2
+GEOM_ODD_ASPHERE = 3
+GEOM_ZERNIKE = 4
+NEWTON_GEOMETRIES = (GEOM_EVEN_ASPHERE, GEOM_ODD_ASPHERE, GEOM_ZERNIKE)
+
+# enum ort_surface_flags
+SURF_REFLECTIVE = 1 << 0
+SURF_RADIUS_INF = 1 << 1
+SURF_APERTURE = 1 << 2
+SURF_RECORD = 1 << 3
+
+# enum ort_cs_kind
+CS_TRANSLATE = 0
+CS_ROT_X = 1
+CS_ROT_Y = 2
+CS_ROT_Z = 3
+
+# enum ort_gen_mode
+GEN_INFINITE = 0
+GEN_FINITE = 1
+
+# enum ort_newton_mode
+NEWTON_SCHEDULE = 0
+NEWTON_WAVE = 1
+
+# enum ort_status
+STATUS_ZERNIKE_RANGE = 1 << 0
+
+CS_OP = np.dtype(
+    [("kind", "<i4"), ("reserved", "<i4"), ("p", "<f8", (3,))], align=True
+)
+assert CS_OP.itemsize == 32
+
+SURFACE = np.dtype(
+    [
+        ("radius", "<f8"),
+        ("conic", "<f8"),
+        ("tol", "<f8"),
+        ("norm_radius", "<f8"),
+        ("ap_rmax2", "<f8"),
+        ("ap_rmin2", "<f8"),
+        ("geometry", "<i4"),
+        ("flags", "<i4"),
+        ("max_iter", "<i4"),
+        ("n_coef", "<i4"),
+        ("coef_off", "<i4"),
+        ("mat_pre", "<i4"),
+        ("mat_post", "<i4"),
+        ("cs_loc_off", "<i4"),
+        ("n_cs_loc", "<i4"),
+        ("cs_glob_off", "<i4"),
+        ("n_cs_glob", "<i4"),
+        ("rec_slot", "<i4"),
+    ],
+    align=True,
+)
+assert SURFACE.itemsize == 96
+
+ZERNIKE_TERM = np.dtype(
+    [
+        ("c", "<f8"),
+        ("norm", "<f8"),
+        ("n", "<i4"),
+        ("m", "<i4"),
+        ("rad_off", "<i4"),
+        ("n_rad", "<i4"),
+    ],
+    align=True,
+)
+assert ZERNIKE_TERM.itemsize == 32
+
+SEGMENT = np.dtype(
+    [
+        ("epd", "<f8"),
+        ("epl", "<f8"),
+        ("vx", "<f8"),
+        ("vy", "<f8"),
+        ("x_off", "<f8"),
+        ("y_off", "<f8"),
+        ("z0", "<f8"),
+        ("lambda_idx", "<i4"),
+        ("mode", "<i4"),
+    ],
+    align=True,
+)
+assert SEGMENT.itemsize == 64
+
+NEWTON_STAT = np.dtype(
+    [("conv_mask", "<u8"), ("last_bad", "<i4"), ("max_updates", "<i4")], align=True
+)
+assert NEWTON_STAT.itemsize == 16
+
+RAY_FIELDS = ("x", "y", "z", "L", "M", "N", "i", "opd")

@@ -1,0 +1,518 @@
+// ort_core.h -- per-ray fp64 arithmetic of the sequential real-ray trace.
+//
+// Every function here is a scalar, per-ray restatement of one reference formula, in
+// the reference's evaluation order (NumPy evaluates each expression left to right with
+// one IEEE rounding per operation; this file is compiled with -ffp-contract=off so the
+// compiler may not fuse a*b+c). The wave-level control (Newton convergence votes,
+// segment lookup, record stores) lives in ort_trace.hip; this header has no
+// intrinsics so it can also be compiled for the host by the test-only checker
+// (tests/hostcheck/).
+//
+// Reference files are cited as path:line under optiland/.
+#pragma once
+
+#include <math.h>
+#include <stdint.h>
+
+#include "../../include/optiland_rt.h"
+
+#ifndef ORT_HD
+#define ORT_HD __host__ __device__
+#endif
+#define ORT_INLINE ORT_HD inline __attribute__((always_inline))
+
+
+namespace ort {
+
+// att accumulates the absorption exponent sum(-alpha t 1e3) (homogeneous.py:54); the
+// intensity is i * exp(att), evaluated once per ray instead of once per surface
+// (exp(a)exp(b) vs exp(a+b): a few ulps relative, see DESIGN.md Parity).
+struct Ray {
+  double x, y, z, L, M, N, i, opd, att;
+};
+
+ORT_INLINE double intensity(const Ray& r) { return r.att == 0.0 ? r.i : r.i * exp(r.att); }
+
+// ---------------------------------------------------------------------------------
+// ray generation: rays/ray_generator.py:71-106 + fields/field_types.py:160-181
+// ---------------------------------------------------------------------------------
+ORT_INLINE Ray generate_ray(const ort_segment& s, double px, double py) {
+  Ray r;
+  double x0, y0;
+  if (s.mode == ORT_GEN_INFINITE) {
+    x0 = px * s.epd / 2.0 * s.vx + s.x_off;  // field_types.py:166
+    y0 = py * s.epd / 2.0 * s.vy + s.y_off;  // field_types.py:167
+  } else {
+    x0 = s.x_off;
+    y0 = s.y_off;
+  }
+  const double z0 = s.z0;
+  const double x1 = px * s.epd * s.vx / 2.0;  // ray_generator.py:76
+  const double y1 = py * s.epd * s.vy / 2.0;  // ray_generator.py:77
+  const double z1 = s.epl;
+  const double dx = x1 - x0, dy = y1 - y0, dz = z1 - z0;
+  double mag = sqrt(dx * dx + dy * dy + dz * dz);  // :80
+  const bool is_zero = mag < 1e-9;                  // :82
+  mag = is_zero ? 1.0 : mag;
+  r.L = is_zero ? 0.0 : dx / mag;
+  r.M = is_zero ? 0.0 : dy / mag;
+  r.N = is_zero ? 1.0 : dz / mag;
+  r.x = x0;
+  r.y = y0;
+  r.z = z0;
+  r.i = 1.0;  // no apodization: be.ones_like(Px)
+  r.opd = 0.0;
+  r.att = 0.0;
+  return r;
+}
+
+// ---------------------------------------------------------------------------------
+// coordinate systems: coordinate_system.py:73-107, rays/base.py:28-42,
+// rays/real_rays.py:90-130 (cos/sin precomputed on the host)
+// ---------------------------------------------------------------------------------
+ORT_INLINE void apply_cs_op(Ray& r, const ort_cs_op& op) {
+  const double a = op.p[0], b = op.p[1], c = op.p[2];
+  switch (op.kind) {
+    case ORT_CS_TRANSLATE:
+      r.x = r.x + a;
+      r.y = r.y + b;
+      r.z = r.z + c;
+      break;
+    case ORT_CS_ROT_X: {
+      const double y = r.y * a - r.z * b, z = r.y * b + r.z * a;
+      const double M = r.M * a - r.N * b, N = r.M * b + r.N * a;
+      r.y = y; r.z = z; r.M = M; r.N = N;
+    } break;
+    case ORT_CS_ROT_Y: {
+      const double x = r.x * a + r.z * b, z = -r.x * b + r.z * a;
+      const double L = r.L * a + r.N * b, N = -r.L * b + r.N * a;
+      r.x = x; r.z = z; r.L = L; r.N = N;
+    } break;
+    default: {  // ORT_CS_ROT_Z
+      const double x = r.x * a - r.y * b, y = r.x * b + r.y * a;
+      const double L = r.L * a - r.M * b, M = r.L * b + r.M * a;
+      r.x = x; r.y = y; r.L = L; r.M = M;
+    } break;
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// intersections
+// ---------------------------------------------------------------------------------
+// plane.py:61-77
+ORT_INLINE double distance_plane(const Ray& r) { return -r.z / r.N; }
+
+// standard.py:89-140
+ORT_INLINE double distance_conic(const Ray& r, double R, double k, bool radius_inf) {
+  if (radius_inf) {
+    const double Ns = fabs(r.N) > 1e-14 ? r.N : 1e-14;
+    return -r.z / Ns;
+  }
+  const double N2 = r.N * r.N;
+  const double a = k * N2 + r.L * r.L + r.M * r.M + N2;
+  // 2*k*N*z + 2*L*x + 2*M*y - 2*N*R + 2*N*z: every "2*" is an exact scaling
+  const double b = 2.0 * k * r.N * r.z + 2.0 * r.L * r.x + 2.0 * r.M * r.y -
+                   2.0 * r.N * R + 2.0 * r.N * r.z;
+  const double z2 = r.z * r.z;
+  const double c = k * z2 - 2.0 * R * r.z + r.x * r.x + r.y * r.y + z2;
+  const double d = b * b - 4.0 * a * c;
+  const double sd = sqrt(d);
+  const double a2 = 2.0 * a;
+  const double t1 = (-b + sd) / a2;
+  const double t2 = (-b - sd) / a2;
+  const double z1 = r.z + t1 * r.N;
+  const double zz2 = r.z + t2 * r.N;
+  double t = fabs(z1) <= fabs(zz2) ? t1 : t2;
+  if (a == 0.0) t = -c / b;
+  return t;
+}
+
+// standard.py:154-167
+ORT_INLINE void normal_conic(double x, double y, double R, double k, double& nx, double& ny,
+                             double& nz) {
+  const double r2 = x * x + y * y;
+  const double denom = R * sqrt(1.0 - (1.0 + k) * r2 / (R * R));
+  const double dfdx = x / denom;
+  const double dfdy = y / denom;
+  const double mag = sqrt(dfdx * dfdx + dfdy * dfdy + 1.0);  // dfdz**2 = (-1)**2 = 1
+  nx = dfdx / mag;
+  ny = dfdy / mag;
+  nz = -1.0 / mag;
+}
+
+// base conic sag, standard.py:73-87 (shared by every Newton geometry)
+ORT_INLINE double sag_conic(double r2, double R, double k) {
+  return r2 / (R * (1.0 + sqrt(1.0 - (1.0 + k) * r2 / (R * R))));
+}
+
+// x**p for the small integer exponents the asphere sums use. NumPy squares exactly
+// for p == 2 and returns x for p == 1 and 1 for p == 0 (fast scalar power); other
+// exponents go through libm pow in the reference and through repeated products here
+// (1-ulp-level differences on a small correction term; see DESIGN.md Parity).
+ORT_INLINE double ipow(double x, int p) {
+  if (p == 0) return 1.0;
+  if (p < 0) return 1.0 / ipow(x, -p);
+  double r = x;
+#pragma unroll 1
+  for (int q = 1; q < p; ++q) r = r * x;
+  return r;
+}
+
+// even_asphere.py:82-98
+template <class PD>
+ORT_INLINE double sag_even(double x, double y, double R, double k, PD C, int nc) {
+  const double r2 = x * x + y * y;
+  double z = sag_conic(r2, R, k);
+  double rp = r2;  // r2 ** (i + 1)
+  for (int i = 0; i < nc; ++i) {
+    z = z + C[i] * rp;
+    rp = rp * r2;
+  }
+  return z;
+}
+
+// even_asphere.py:100-129
+template <class PD>
+ORT_INLINE void normal_even(double x, double y, double R, double k, PD C, int nc,
+                            double& nx, double& ny, double& nz) {
+  const double r2 = x * x + y * y;
+  const double denom = R * sqrt(1.0 - (1.0 + k) * r2 / (R * R));
+  double dfdx = x / denom;
+  double dfdy = y / denom;
+  double rp = 1.0;  // r2 ** i
+  for (int i = 0; i < nc; ++i) {
+    const double f = 2.0 * (double)(i + 1);
+    dfdx = dfdx + f * x * C[i] * rp;
+    dfdy = dfdy + f * y * C[i] * rp;
+    rp = rp * r2;
+  }
+  const double mag = sqrt(dfdx * dfdx + dfdy * dfdy + 1.0);
+  nx = dfdx / mag;
+  ny = dfdy / mag;
+  nz = -1.0 / mag;
+}
+
+// odd_asphere.py:73-89
+template <class PD>
+ORT_INLINE double sag_odd(double x, double y, double R, double k, PD C, int nc) {
+  const double r2 = x * x + y * y;
+  const double r = sqrt(r2);
+  double z = sag_conic(r2, R, k);
+  double rp = r;  // r ** (i + 1)
+  for (int i = 0; i < nc; ++i) {
+    z = z + C[i] * rp;
+    rp = rp * r;
+  }
+  return z;
+}
+
+// odd_asphere.py:91-130 (non-finite per-term slopes are zeroed, :112-122)
+template <class PD>
+ORT_INLINE void normal_odd(double x, double y, double R, double k, PD C, int nc,
+                           double& nx, double& ny, double& nz) {
+  const double r2 = x * x + y * y;
+  const double r = sqrt(r2);
+  const double denom = R * sqrt(1.0 - (1.0 + k) * r2 / (R * R));
+  double dfdx = x / denom;
+  double dfdy = y / denom;
+  double rp = 1.0 / r;  // r ** (i - 1): 1/r, 1, r, r*r, r*r*r, ...
+  for (int i = 0; i < nc; ++i) {
+    const double f = (double)(i + 1);
+    double xt = f * x * C[i] * rp;
+    double yt = f * y * C[i] * rp;
+    if (!isfinite(xt)) xt = 0.0;
+    if (!isfinite(yt)) yt = 0.0;
+    rp = (i == 0) ? 1.0 : (i == 1 ? r : rp * r);
+    dfdx = dfdx + xt;
+    dfdy = dfdy + yt;
+  }
+  const double mag = sqrt(dfdx * dfdx + dfdy * dfdy + 1.0);
+  nx = dfdx / mag;
+  ny = dfdy / mag;
+  nz = -1.0 / mag;
+}
+
+// ---- Zernike: geometries/zernike.py:133-246 + zernike/base.py:42-299 ----------------
+// R_n^|m|(rho) = sum_k a_k rho^(n-2k)         (base.py:228-253)
+template <class PD>
+ORT_INLINE double zern_radial(PD a, int n, int nr, double rho) {
+  double v = 0.0;
+#pragma unroll 1
+  for (int k = 0; k < nr; ++k) v = v + a[k] * ipow(rho, n - 2 * k);
+  return v;
+}
+// dR/drho = sum_k d_k rho^(n-2k-1)            (base.py:272-299)
+template <class PD>
+ORT_INLINE double zern_radial_deriv(PD d, int n, int nr, double rho) {
+  double v = 0.0;
+#pragma unroll 1
+  for (int k = 0; k < nr; ++k) {
+    if (n - 2 * k < 0) continue;
+    const double p = (n - 2 * k - 1) >= 0 ? ipow(rho, n - 2 * k - 1) : 0.0;
+    v = v + d[k] * p;
+  }
+  return v;
+}
+
+// cos(m phi), sin(m phi) for m >= 0 from cos phi, sin phi by the angle-addition
+// recurrence (the reference evaluates cos(m * atan2(y, x)); a few ulps apart, see
+// DESIGN.md Parity). phi = atan2(yn, xn) gives cos phi = xn / rho, sin phi = yn / rho,
+// and atan2(0, 0) = 0 at rho == 0.
+ORT_INLINE void cos_sin_m(int m, double c1, double s1, double& cm, double& sm) {
+  double c = 1.0, s = 0.0;
+#pragma unroll 1
+  for (int q = 0; q < m; ++q) {
+    const double cn = c * c1 - s * s1;
+    s = s * c1 + c * s1;
+    c = cn;
+  }
+  cm = c;
+  sm = s;
+}
+
+ORT_INLINE void polar_unit(double xn, double yn, double rho, double& c1, double& s1) {
+  if (rho > 0.0) {
+    c1 = xn / rho;
+    s1 = yn / rho;
+  } else {
+    c1 = 1.0;
+    s1 = 0.0;
+  }
+}
+
+// zernike.py:133-161 (sets range_error on |x/R_norm| > 1 or |y/R_norm| > 1)
+template <class PD, class PZ>
+ORT_INLINE double sag_zernike(double x, double y, double R, double k, double Rn, PZ T, int nt,
+                              PD coef, bool& range_error) {
+  const double xn = x / Rn;
+  const double yn = y / Rn;
+  if (fabs(xn) > 1.0 || fabs(yn) > 1.0) range_error = true;  // zernike.py:234-246
+  const double rho = sqrt(xn * xn + yn * yn);
+  double c1, s1;
+  polar_unit(xn, yn, rho, c1, s1);
+  const double r2 = x * x + y * y;
+  double z = sag_conic(r2, R, k);
+  double total = 0.0;  // python sum() starts at int 0; 0 + t == t exactly
+  for (int j = 0; j < nt; ++j) {
+    const ort_zernike_term t = T[j];
+    const double rad = zern_radial(coef + t.rad_off, t.n, t.n_rad, rho);
+    double cm, sm;
+    cos_sin_m(t.m >= 0 ? t.m : -t.m, c1, s1, cm, sm);
+    const double az = t.m >= 0 ? cm : sm;  // base.py:206-226
+    total = total + t.c * t.norm * rad * az;
+  }
+  return z + total;
+}
+
+// zernike.py:163-231 (the normal omits the normalisation constant: reference quirk)
+template <class PD, class PZ>
+ORT_INLINE void normal_zernike(double x, double y, double R, double k, double Rn, PZ T, int nt,
+                               PD coef, double& nx, double& ny, double& nz) {
+  const double r2 = x * x + y * y;
+  const double denominator = R * sqrt(1.0 - (1.0 + k) * r2 / (R * R));
+  double dzdx = x / denominator;
+  double dzdy = y / denominator;
+  const double eps = 1e-14;
+  const double xn = x / Rn;
+  const double yn = y / Rn;
+  const double rho = sqrt(xn * xn + yn * yn);
+  double c1, s1;
+  polar_unit(xn, yn, rho, c1, s1);
+  const double Rn2 = Rn * Rn;
+  // (the reference returns zeros when EVERY rho is 0; per ray (x/Rn^2)/(0+eps) = 0 too)
+  const double drho_dx = (x / Rn2) / (rho + eps);
+  const double drho_dy = (y / Rn2) / (rho + eps);
+  const double rho2e = rho * rho + eps;
+  const double inv_rn = 1.0 / Rn;
+  const double dphi_dx = -(yn) / rho2e * inv_rn;
+  const double dphi_dy = +(xn) / rho2e * inv_rn;
+  for (int j = 0; j < nt; ++j) {
+    const ort_zernike_term t = T[j];
+    if (t.c == 0.0) continue;
+    const PD a = coef + t.rad_off;
+    const double rt = zern_radial(a, t.n, t.n_rad, rho);
+    const double rd = zern_radial_deriv(a + t.n_rad, t.n, t.n_rad, rho);
+    const int am = t.m >= 0 ? t.m : -t.m;
+    double cm, sm;
+    cos_sin_m(am, c1, s1, cm, sm);
+    double dr, dp;
+    if (t.m == 0) {  // base.py:128-137
+      dr = rd;
+      dp = 0.0;
+    } else if (t.m > 0) {
+      dr = rd * cm;
+      dp = (double)(-t.m) * rt * sm;
+    } else {
+      dr = rd * sm;
+      dp = (double)am * rt * cm;
+    }
+    dzdx = dzdx + t.c * (dr * drho_dx + dp * dphi_dx);
+    dzdy = dzdy + t.c * (dr * drho_dy + dp * dphi_dy);
+  }
+  double norm = sqrt(dzdx * dzdx + dzdy * dzdy + 1.0);
+  norm = norm < eps ? 1.0 : norm;
+  nx = dzdx / norm;
+  ny = dzdy / norm;
+  nz = -1.0 / norm;
+}
+
+// Sag and normal of a Newton-iterated geometry (EvenAsphere / OddAsphere / Zernike).
+// KM is a bitmask of the Newton kinds compiled in (KM_EVEN | KM_ODD | KM_ZERN): a lens
+// only pays registers for the kinds it contains.
+enum : unsigned { KM_EVEN = 1u, KM_ODD = 2u, KM_ZERN = 4u };
+
+template <unsigned KM, class PD, class PZ>
+ORT_INLINE double newton_sag(const ort_surface& s, PD coef, PZ zern, double x, double y,
+                             bool& range_error) {
+  const PD C = coef + s.coef_off;
+  if constexpr ((KM & KM_EVEN) != 0) {
+    if (KM == KM_EVEN || s.geometry == ORT_GEOM_EVEN_ASPHERE)
+      return sag_even(x, y, s.radius, s.conic, C, s.n_coef);
+  }
+  if constexpr ((KM & KM_ODD) != 0) {
+    if ((KM & ~KM_ODD) == 0 || s.geometry == ORT_GEOM_ODD_ASPHERE)
+      return sag_odd(x, y, s.radius, s.conic, C, s.n_coef);
+  }
+  if constexpr ((KM & KM_ZERN) != 0) {
+    return sag_zernike(x, y, s.radius, s.conic, s.norm_radius, zern + s.coef_off, s.n_coef,
+                       coef, range_error);
+  }
+  return NAN;
+}
+
+template <unsigned KM, class PD, class PZ>
+ORT_INLINE void newton_normal(const ort_surface& s, PD coef, PZ zern, double x, double y,
+                              double& nx, double& ny, double& nz) {
+  const PD C = coef + s.coef_off;
+  if constexpr ((KM & KM_EVEN) != 0) {
+    if (KM == KM_EVEN || s.geometry == ORT_GEOM_EVEN_ASPHERE) {
+      normal_even(x, y, s.radius, s.conic, C, s.n_coef, nx, ny, nz);
+      return;
+    }
+  }
+  if constexpr ((KM & KM_ODD) != 0) {
+    if ((KM & ~KM_ODD) == 0 || s.geometry == ORT_GEOM_ODD_ASPHERE) {
+      normal_odd(x, y, s.radius, s.conic, C, s.n_coef, nx, ny, nz);
+      return;
+    }
+  }
+  if constexpr ((KM & KM_ZERN) != 0) {
+    normal_zernike(x, y, s.radius, s.conic, s.norm_radius, zern + s.coef_off, s.n_coef, coef,
+                   nx, ny, nz);
+    return;
+  }
+  nx = ny = nz = NAN;
+}
+
+// newton_raphson.py:140-146: residual f(t) = sag(P(t)) - z(t)
+template <unsigned KM, class PD, class PZ>
+ORT_INLINE double newton_residual(const ort_surface& s, PD coef, PZ zern, const Ray& r,
+                                  double t, bool& range_error) {
+  const double xi = r.x + t * r.L;
+  const double yi = r.y + t * r.M;
+  const double zi = r.z + t * r.N;
+  return newton_sag<KM, PD, PZ>(s, coef, zern, xi, yi, range_error) - zi;
+}
+
+// newton_raphson.py:154-166: t_new = t - f / f'(t)
+template <unsigned KM, class PD, class PZ>
+ORT_INLINE double newton_update(const ort_surface& s, PD coef, PZ zern, const Ray& r,
+                                double t, double f) {
+  const double xi = r.x + t * r.L;
+  const double yi = r.y + t * r.M;
+  double nx, ny, nz;
+  newton_normal<KM, PD, PZ>(s, coef, zern, xi, yi, nx, ny, nz);
+  const double nzs = fabs(nz) > 1e-14 ? nz : 1e-14;
+  const double fx = -nx / nzs;
+  const double fy = -ny / nzs;
+  const double df = fx * r.L + fy * r.M - r.N;
+  const double dfs = fabs(df) > 1e-14 ? df : 1e-14;
+  return t - f / dfs;
+}
+
+// ---------------------------------------------------------------------------------
+// per-surface physics
+// ---------------------------------------------------------------------------------
+// propagation/homogeneous.py:30-57 (alpha = 4 pi k / w, applied only when k > 0)
+ORT_INLINE void propagate(Ray& r, double t, double alpha) {
+  r.x = r.x + t * r.L;
+  r.y = r.y + t * r.M;
+  r.z = r.z + t * r.N;
+  if (alpha > 0.0) r.att = r.att + -alpha * t * 1e3;
+}
+
+// surfaces/standard_surface.py:218
+ORT_INLINE void add_opd(Ray& r, double t, double n_pre) { r.opd = r.opd + fabs(t * n_pre); }
+
+// physical_apertures/radial.py:50-63 + rays/real_rays.py:132-139
+ORT_INLINE void clip_radial(Ray& r, double rmax2, double rmin2) {
+  const double radius2 = r.x * r.x + r.y * r.y;
+  const bool inside = (radius2 <= rmax2) && (radius2 >= rmin2);
+  if (!inside) {
+    r.i = 0.0;
+    r.att = 0.0;
+  }
+}
+
+// rays/real_rays.py:511-547: sign(dot) flip (np.sign: 0 -> 0, NaN -> NaN), |dot|
+ORT_INLINE double align_normal(const Ray& r, double& nx, double& ny, double& nz) {
+  const double dot = r.L * nx + r.M * ny + r.N * nz;
+  const double sgn = dot > 0.0 ? 1.0 : (dot < 0.0 ? -1.0 : (dot == dot ? 0.0 : dot));
+  nx = nx * sgn;
+  ny = ny * sgn;
+  nz = nz * sgn;
+  return fabs(dot);
+}
+
+// rays/real_rays.py:141-163
+ORT_INLINE void refract(Ray& r, double nx, double ny, double nz, double n1, double n2) {
+  const double u = n1 / n2;
+  const double dot = align_normal(r, nx, ny, nz);
+  const double root = sqrt(1.0 - u * u * (1.0 - dot * dot));
+  const double L0 = r.L, M0 = r.M, N0 = r.N;
+  r.L = u * L0 + nx * root - u * nx * dot;
+  r.M = u * M0 + ny * root - u * ny * dot;
+  r.N = u * N0 + nz * root - u * nz * dot;
+}
+
+// rays/real_rays.py:165-181
+ORT_INLINE void reflect(Ray& r, double nx, double ny, double nz) {
+  const double dot = align_normal(r, nx, ny, nz);
+  r.L = r.L - 2.0 * dot * nx;
+  r.M = r.M - 2.0 * dot * ny;
+  r.N = r.N - 2.0 * dot * nz;
+}
+
+// surface normal at the current (local) ray position
+template <unsigned KM, class PD, class PZ>
+ORT_INLINE void surface_normal(const ort_surface& s, PD coef, PZ zern, const Ray& r,
+                               double& nx, double& ny, double& nz) {
+  switch (s.geometry) {
+    case ORT_GEOM_PLANE:  // plane.py:79-98
+      nx = 0.0; ny = 0.0; nz = 1.0;
+      break;
+    case ORT_GEOM_STANDARD:
+      normal_conic(r.x, r.y, s.radius, s.conic, nx, ny, nz);
+      break;
+    default:
+      newton_normal<KM, PD, PZ>(s, coef, zern, r.x, r.y, nx, ny, nz);
+  }
+}
+
+// everything in Surface.trace after the distance t is known
+// (standard_surface.py:215-231 minus localize/globalize)
+template <unsigned KM, class PD, class PZ>
+ORT_INLINE void finish_surface(Ray& r, const ort_surface& s, PD coef, PZ zern, double t,
+                               double n_pre, double n_post, double alpha_pre) {
+  propagate(r, t, alpha_pre);
+  add_opd(r, t, n_pre);
+  if (s.flags & ORT_SURF_APERTURE) clip_radial(r, s.ap_rmax2, s.ap_rmin2);
+  double nx, ny, nz;
+  surface_normal<KM, PD, PZ>(s, coef, zern, r, nx, ny, nz);
+  if (s.flags & ORT_SURF_REFLECTIVE)
+    reflect(r, nx, ny, nz);
+  else
+    refract(r, nx, ny, nz, n_pre, n_post);
+}
+
+}  // namespace ort

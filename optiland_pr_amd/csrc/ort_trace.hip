@@ -1,0 +1,440 @@
+// ort_trace.hip -- MI355X (gfx950) kernels of the sequential real-ray trace + C ABI.
+//
+// One ray per lane, all surfaces fused in one launch. The ray state
+// (x, y, z, L, M, N, i, opd) stays in VGPRs from the first surface to the image; the
+// surface table is wave-uniform (indexed by the loop counter) so every surface
+// parameter is fetched with scalar loads into SGPRs. Per-ray HBM traffic is one read of
+// the inputs (64 B of rays, or 16 B of pupil coordinates) and one 64 B write.
+//
+// Newton surfaces (even/odd asphere, Zernike) follow the reference's GLOBAL stopping
+// rule (newton_raphson.py:148: break when max|f| < tol over all rays of the trace call)
+// by speculate-and-verify: every ray performs exactly sched[group][s] updates and
+// reports, per group and surface, the AND of its "converged at update j" bits and the
+// last update index at which it was not converged; the host checks the schedule
+// against those and re-launches on a mismatch (rare). ORT_NEWTON_WAVE instead stops a
+// wave as soon as its 64 lanes have converged (approximate, faster).
+//
+// Compiled with -ffp-contract=off: see ort_core.h.
+
+#include <hip/hip_runtime.h>
+
+#include "ort_core.h"
+
+namespace {
+
+constexpr int kBlock = 256;
+
+// Lens tables are read-only for the whole launch and indexed by wave-uniform values, so
+// they are read through the constant address space: the compiler then emits scalar
+// loads (s_load -> SGPRs) instead of per-lane vector loads.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define ORT_CONST_AS __attribute__((address_space(4)))
+#else
+#define ORT_CONST_AS
+#endif
+template <class T>
+using cptr = const ORT_CONST_AS T*;
+template <class T>
+__device__ inline cptr<T> cst(const T* p) {
+  return (cptr<T>)(p);
+}
+using PD = cptr<double>;
+using PZ = cptr<ort_zernike_term>;
+
+// Kernel specialisation bits: bits 0-2 = Newton kinds present (ort::KM_*), bit 3 = rays
+// generated in-kernel from pupil coordinates.
+enum : uint32_t {
+  F_KM = 7u,
+  F_GEN = 1u << 3,
+  F_REC = 1u << 4,  // some surfaces are recorded (standard_surface.py:266-286)
+};
+
+struct KArgs {
+  // lens
+  const ort_surface* surf;
+  const ort_cs_op* cs;
+  const double* coef;
+  const ort_zernike_term* zern;
+  const double* n_tab;
+  const double* alpha_tab;
+  int32_t n_surf;
+  int32_t n_lambda;
+  int32_t n_mat;
+  int32_t final_mat;
+  double final_thickness;
+  // rays
+  ort_rays in;
+  ort_rays out;
+  const double* px;
+  const double* py;
+  // batch
+  int64_t n_rays;
+  int64_t seg_len;
+  int64_t group_len;
+  const ort_segment* seg;
+  int32_t n_seg;
+  int32_t pupil_per_ray;
+  // options
+  int32_t newton_mode;
+  int32_t start_surface;
+  const int32_t* sched;
+  // outputs
+  double* rec;
+  ort_newton_stat* stats;
+  int32_t* status;
+};
+
+__device__ inline uint64_t wave_and_u64(uint64_t v) {
+  for (int o = 32; o > 0; o >>= 1) v &= __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ inline int wave_max_i32(int v) {
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Table lookup n_tab[lam][mat]: a uniform scalar load when the lens is traced at one
+// wavelength (the common case), else a per-lane load of the small L1-resident table.
+__device__ inline double tab(const double* t, int n_lambda, int n_mat, int lam, int mat) {
+  if (n_lambda == 1) return cst(t)[mat];
+  return t[lam * n_mat + mat];
+}
+
+// Newton refinement of t at surface s for one lane (newton_raphson.py:119-168).
+template <uint32_t FEAT>
+__device__ inline double newton_distance(const KArgs& a, const ort_surface& s, int si,
+                                         const ort::Ray& r, bool active, int64_t group,
+                                         bool group_uniform, bool& range_error) {
+  double t = ort::distance_conic(r, s.radius, s.conic, (s.flags & ORT_SURF_RADIUS_INF) != 0);
+  const double tol = s.tol;
+  const int max_iter = s.max_iter;
+  if (a.newton_mode == ORT_NEWTON_WAVE) {
+    // Per-wave global rule: every lane of the wave does the same number of updates,
+    // the wave stops at the first j where all its (non-NaN) lanes have |f| < tol.
+    int j = 0;
+    for (; j < max_iter; ++j) {
+      bool rerr = false;
+      const double f = ort::newton_residual<(FEAT & F_KM)>(s, cst(a.coef), cst(a.zern), r, t, rerr);
+      if (active && rerr) range_error = true;
+      const bool conv = !active || !(fabs(f) >= tol);
+      if (__all(conv)) break;
+      t = ort::newton_update<(FEAT & F_KM)>(s, cst(a.coef), cst(a.zern), r, t, f);
+    }
+    if (a.stats && (threadIdx.x & 63) == 0)
+      atomicMax(&a.stats[(group_uniform ? group : 0) * a.n_surf + si].max_updates, j);
+    return t;
+  }
+  // ORT_NEWTON_SCHEDULE: exactly U updates, plus the check evaluation at j = U.
+  const int U = a.sched ? a.sched[group * a.n_surf + si] : max_iter;
+  uint64_t mask = 0;
+  int last_bad = -1;
+  for (int j = 0;; ++j) {
+    const bool lane_on = active && j <= U;
+    if (!__any(lane_on)) break;
+    if (lane_on) {
+      bool rerr = false;
+      const double f = ort::newton_residual<(FEAT & F_KM)>(s, cst(a.coef), cst(a.zern), r, t, rerr);
+      // the reference evaluates sag at j = 0..U-1 always, and at j = U only when the
+      // loop broke there (U < max_iter)
+      if (rerr && (j < U || U < max_iter)) range_error = true;
+      const bool conv = fabs(f) < tol;  // NaN never converges (np.max propagates NaN)
+      if (conv && j < 64) mask |= 1ull << j;
+      if (!conv) last_bad = j;
+      if (j < U) t = ort::newton_update<(FEAT & F_KM)>(s, cst(a.coef), cst(a.zern), r, t, f);
+    }
+  }
+  if (a.stats) {
+    if (!active) {
+      mask = ~0ull;
+      last_bad = -1;
+    }
+    ort_newton_stat* st = &a.stats[group * a.n_surf + si];
+    if (group_uniform) {
+      mask = wave_and_u64(mask);
+      last_bad = wave_max_i32(last_bad);
+      if ((threadIdx.x & 63) == 0) {
+        if (mask != ~0ull) atomicAnd((unsigned long long*)&st->conv_mask, (unsigned long long)mask);
+        if (last_bad >= 0) atomicMax(&st->last_bad, last_bad);
+      }
+    } else if (active) {
+      if (mask != ~0ull) atomicAnd((unsigned long long*)&st->conv_mask, (unsigned long long)mask);
+      if (last_bad >= 0) atomicMax(&st->last_bad, last_bad);
+    }
+  }
+  return t;
+}
+
+template <uint32_t FEAT>
+__global__ __launch_bounds__(kBlock) void trace_kernel(const KArgs a) {
+  const int64_t rid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const bool active = rid < a.n_rays;
+  const int64_t r_ld = active ? rid : 0;  // inactive lanes compute on ray 0, store nothing
+
+  // segment / wavelength / Newton group of this ray
+  const int64_t sidx = a.seg ? r_ld / a.seg_len : 0;
+  int lam = 0;
+  ort::Ray r;
+  if constexpr (FEAT & F_GEN) {
+    const ort_segment sg = a.seg[sidx];
+    lam = sg.lambda_idx;
+    const int64_t p = a.pupil_per_ray ? r_ld : (r_ld - sidx * a.seg_len);
+    r = ort::generate_ray(sg, a.px[p], a.py[p]);
+  } else {
+    if (a.seg) lam = a.seg[sidx].lambda_idx;
+    r.x = a.in.x[r_ld];
+    r.y = a.in.y[r_ld];
+    r.z = a.in.z[r_ld];
+    r.L = a.in.L[r_ld];
+    r.M = a.in.M[r_ld];
+    r.N = a.in.N[r_ld];
+    r.i = a.in.i[r_ld];
+    r.opd = a.in.opd[r_ld];
+    r.att = 0.0;
+  }
+  int64_t group = 0;
+  bool group_uniform = true;
+  if constexpr ((FEAT & F_KM) != 0) {
+    group = r_ld / a.group_len;
+    const int64_t g0 = __shfl(group, 0, 64);
+    group_uniform = __all(group == g0);
+  }
+  bool range_error = false;
+
+  for (int si = a.start_surface; si < a.n_surf; ++si) {
+    const ort_surface s = cst(a.surf)[si];
+    for (int c = 0; c < s.n_cs_loc; ++c) ort::apply_cs_op(r, cst(a.cs)[s.cs_loc_off + c]);
+    double t;
+    if (s.geometry == ORT_GEOM_PLANE) {
+      t = ort::distance_plane(r);
+    } else if (s.geometry == ORT_GEOM_STANDARD) {
+      t = ort::distance_conic(r, s.radius, s.conic, (s.flags & ORT_SURF_RADIUS_INF) != 0);
+    } else {
+      if constexpr ((FEAT & F_KM) != 0) {
+        t = newton_distance<FEAT>(a, s, si, r, active, group, group_uniform, range_error);
+      } else {
+        t = __builtin_nan("");  // unreachable: the host sets geometry_mask
+      }
+    }
+    const double n_pre = tab(a.n_tab, a.n_lambda, a.n_mat, lam, s.mat_pre);
+    const double n_post = tab(a.n_tab, a.n_lambda, a.n_mat, lam, s.mat_post);
+    const double alpha = tab(a.alpha_tab, a.n_lambda, a.n_mat, lam, s.mat_pre);
+    if constexpr ((FEAT & F_KM) != 0) {
+      ort::finish_surface<(FEAT & F_KM)>(r, s, cst(a.coef), cst(a.zern), t, n_pre, n_post, alpha);
+    } else {
+      // closed-form geometries only: plane / conic normal inline
+      ort::propagate(r, t, alpha);
+      ort::add_opd(r, t, n_pre);
+      if (s.flags & ORT_SURF_APERTURE) ort::clip_radial(r, s.ap_rmax2, s.ap_rmin2);
+      double nx, ny, nz;
+      if (s.geometry == ORT_GEOM_PLANE) {
+        nx = 0.0; ny = 0.0; nz = 1.0;
+      } else {
+        ort::normal_conic(r.x, r.y, s.radius, s.conic, nx, ny, nz);
+      }
+      if (s.flags & ORT_SURF_REFLECTIVE)
+        ort::reflect(r, nx, ny, nz);
+      else
+        ort::refract(r, nx, ny, nz, n_pre, n_post);
+    }
+    for (int c = 0; c < s.n_cs_glob; ++c) ort::apply_cs_op(r, cst(a.cs)[s.cs_glob_off + c]);
+    if constexpr ((FEAT & F_REC) != 0) {
+      if ((s.flags & ORT_SURF_RECORD) && active) {
+        double* base = a.rec + (int64_t)s.rec_slot * 8 * a.n_rays + rid;
+        base[0 * a.n_rays] = r.x;
+        base[1 * a.n_rays] = r.y;
+        base[2 * a.n_rays] = r.z;
+        base[3 * a.n_rays] = r.L;
+        base[4 * a.n_rays] = r.M;
+        base[5 * a.n_rays] = r.N;
+        base[6 * a.n_rays] = ort::intensity(r);
+        base[7 * a.n_rays] = r.opd;
+      }
+    }
+  }
+  // real_ray_tracer.py:84-89: image-space propagate by the last surface's thickness
+  // (final_mat < 0: plain SurfaceGroup.trace, no propagate)
+  if (a.final_mat >= 0)
+    ort::propagate(r, a.final_thickness,
+                   tab(a.alpha_tab, a.n_lambda, a.n_mat, lam, a.final_mat));
+
+  if constexpr ((FEAT & ort::KM_ZERN) != 0) {
+    if (range_error && active && a.status) atomicOr(a.status, (int)ORT_STATUS_ZERNIKE_RANGE);
+  }
+  if (!active) return;
+  a.out.x[rid] = r.x;
+  a.out.y[rid] = r.y;
+  a.out.z[rid] = r.z;
+  a.out.L[rid] = r.L;
+  a.out.M[rid] = r.M;
+  a.out.N[rid] = r.N;
+  a.out.i[rid] = ort::intensity(r);
+  a.out.opd[rid] = r.opd;
+}
+
+__global__ __launch_bounds__(kBlock) void generate_kernel(const KArgs a) {
+  const int64_t rid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (rid >= a.n_rays) return;
+  const int64_t sidx = rid / a.seg_len;
+  const ort_segment sg = a.seg[sidx];
+  const int64_t p = a.pupil_per_ray ? rid : (rid - sidx * a.seg_len);
+  const ort::Ray r = ort::generate_ray(sg, a.px[p], a.py[p]);
+  a.out.x[rid] = r.x;
+  a.out.y[rid] = r.y;
+  a.out.z[rid] = r.z;
+  a.out.L[rid] = r.L;
+  a.out.M[rid] = r.M;
+  a.out.N[rid] = r.N;
+  a.out.i[rid] = r.i;
+  a.out.opd[rid] = r.opd;
+}
+
+typedef void (*KernelFn)(const KArgs);
+
+template <uint32_t FEAT>
+KernelFn pick() {
+  return trace_kernel<FEAT>;
+}
+
+KernelFn select_kernel(uint32_t feat) {
+  switch (feat) {
+#define ORT_CASE(F) \
+  case (F):         \
+    return pick<(F)>();
+#define ORT_CASES(G) ORT_CASE(G | 0) ORT_CASE(G | 1) ORT_CASE(G | 2) ORT_CASE(G | 3) \
+    ORT_CASE(G | 4) ORT_CASE(G | 5) ORT_CASE(G | 6) ORT_CASE(G | 7)
+    ORT_CASES(0)
+    ORT_CASES(F_GEN)
+    ORT_CASES(F_REC)
+    ORT_CASES(F_REC | F_GEN)
+#undef ORT_CASES
+#undef ORT_CASE
+    default:
+      return nullptr;
+  }
+}
+
+int fill_args(KArgs& a, const ort_lens* lens, const ort_batch* batch, const ort_options* opt,
+              double* rec, ort_newton_stat* stats, int32_t* status, uint32_t& feat) {
+  if (!lens || !batch || !opt) return ORT_ERR_ARG;
+  if (lens->n_surfaces < 0 || lens->n_surfaces > ORT_MAX_SURFACES) return ORT_ERR_SURFACES;
+  if (lens->n_surfaces > 0 && (!lens->surfaces || !lens->n_tab || !lens->alpha_tab))
+    return ORT_ERR_ARG;
+  if (batch->n_rays < 0 || batch->seg_len < 1 || batch->group_len < 1) return ORT_ERR_ARG;
+  if (lens->n_lambda < 1 || lens->n_mat < 1) return ORT_ERR_ARG;
+  if (opt->start_surface < 0) return ORT_ERR_ARG;
+  a.surf = lens->surfaces;
+  a.cs = lens->cs_ops;
+  a.coef = lens->coef;
+  a.zern = lens->zern;
+  a.n_tab = lens->n_tab;
+  a.alpha_tab = lens->alpha_tab;
+  a.n_surf = lens->n_surfaces;
+  a.n_lambda = lens->n_lambda;
+  a.n_mat = lens->n_mat;
+  a.final_mat = lens->final_mat;
+  a.final_thickness = lens->final_thickness;
+  a.n_rays = batch->n_rays;
+  a.seg_len = batch->seg_len;
+  a.group_len = batch->group_len;
+  a.seg = batch->seg;
+  a.n_seg = batch->n_seg;
+  a.pupil_per_ray = batch->pupil_per_ray;
+  a.newton_mode = opt->newton_mode;
+  a.start_surface = opt->start_surface;
+  a.sched = opt->sched;
+  a.rec = rec;
+  a.stats = stats;
+  a.status = status;
+  feat = 0;
+  if (lens->geometry_mask & (1u << ORT_GEOM_EVEN_ASPHERE)) feat |= ort::KM_EVEN;
+  if (lens->geometry_mask & (1u << ORT_GEOM_ODD_ASPHERE)) feat |= ort::KM_ODD;
+  if (lens->geometry_mask & (1u << ORT_GEOM_ZERNIKE)) feat |= ort::KM_ZERN;
+  if (rec) feat |= F_REC;
+  if (opt->newton_mode != ORT_NEWTON_SCHEDULE && opt->newton_mode != ORT_NEWTON_WAVE)
+    return ORT_ERR_ARG;
+  return ORT_OK;
+}
+
+int launch(const KArgs& a, uint32_t feat, hipStream_t stream) {
+  if (a.n_rays == 0) return ORT_OK;
+  KernelFn fn = select_kernel(feat);
+  if (!fn) return ORT_ERR_ARG;
+  const int64_t blocks = (a.n_rays + kBlock - 1) / kBlock;
+  if (blocks > 0x7fffffff) return ORT_ERR_ARG;
+  hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(kBlock), 0, stream, a);
+  return hipGetLastError() == hipSuccess ? ORT_OK : ORT_ERR_LAUNCH;
+}
+
+int init_outputs(const KArgs& a, hipStream_t stream) {
+  if (a.stats) {
+    const int64_t groups = (a.n_rays + a.group_len - 1) / a.group_len;
+    // conv_mask = ~0, last_bad = -1, max_updates = -1 (all 0xFF bytes)
+    if (hipMemsetAsync(a.stats, 0xFF, (size_t)(groups > 0 ? groups : 1) * a.n_surf *
+                                          sizeof(ort_newton_stat),
+                       stream) != hipSuccess)
+      return ORT_ERR_LAUNCH;
+  }
+  if (a.status && hipMemsetAsync(a.status, 0, sizeof(int32_t), stream) != hipSuccess)
+    return ORT_ERR_LAUNCH;
+  return ORT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ort_abi_version(void) { return ORT_ABI_VERSION; }
+
+int ort_trace_sequential(const ort_lens* lens, const ort_rays* rays_in, ort_rays* rays_out,
+                         const ort_batch* batch, const ort_options* opt, double* rec,
+                         ort_newton_stat* newton_stat, int32_t* status, void* stream) {
+  if (!rays_in || !rays_out) return ORT_ERR_ARG;
+  KArgs a{};
+  uint32_t feat = 0;
+  int rc = fill_args(a, lens, batch, opt, rec, newton_stat, status, feat);
+  if (rc) return rc;
+  a.in = *rays_in;
+  a.out = *rays_out;
+  hipStream_t s = (hipStream_t)stream;
+  if ((rc = init_outputs(a, s))) return rc;
+  return launch(a, feat, s);
+}
+
+int ort_trace_pupil(const ort_lens* lens, const double* px, const double* py,
+                    ort_rays* rays_out, const ort_batch* batch, const ort_options* opt,
+                    double* rec, ort_newton_stat* newton_stat, int32_t* status,
+                    void* stream) {
+  if (!px || !py || !rays_out || !batch || !batch->seg) return ORT_ERR_ARG;
+  KArgs a{};
+  uint32_t feat = 0;
+  int rc = fill_args(a, lens, batch, opt, rec, newton_stat, status, feat);
+  if (rc) return rc;
+  a.px = px;
+  a.py = py;
+  a.out = *rays_out;
+  feat |= F_GEN;
+  hipStream_t s = (hipStream_t)stream;
+  if ((rc = init_outputs(a, s))) return rc;
+  return launch(a, feat, s);
+}
+
+int ort_generate_rays(const double* px, const double* py, ort_rays* rays_out,
+                      const ort_batch* batch, void* stream) {
+  if (!px || !py || !rays_out || !batch || !batch->seg || batch->seg_len < 1)
+    return ORT_ERR_ARG;
+  KArgs a{};
+  a.px = px;
+  a.py = py;
+  a.out = *rays_out;
+  a.n_rays = batch->n_rays;
+  a.seg_len = batch->seg_len;
+  a.seg = batch->seg;
+  a.pupil_per_ray = batch->pupil_per_ray;
+  if (a.n_rays == 0) return ORT_OK;
+  const int64_t blocks = (a.n_rays + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(generate_kernel, dim3((unsigned)blocks), dim3(kBlock), 0,
+                     (hipStream_t)stream, a);
+  return hipGetLastError() == hipSuccess ? ORT_OK : ORT_ERR_LAUNCH;
+}
+
+}  // extern "C"

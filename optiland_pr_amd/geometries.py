@@ -1,0 +1,221 @@
+"""Surface geometries (parameter holders lowered into the kernel's surface table).
+
+Mirrors optiland/geometries/{plane,standard,newton_raphson,even_asphere,odd_asphere,
+zernike}.py: same class names, constructor arguments and defaults. The arithmetic
+(sag, intersection distance, normal) runs only in the HIP kernel
+(optiland_pr_amd/csrc/ort_core.h); these classes just describe the surface.
+"""
+
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+from . import _abi
+from .coordinate_system import CoordinateSystem
+
+
+class BaseGeometry:
+    """geometries/base.py:14-110."""
+
+    geometry_id: int = -1
+
+    def __init__(self, coordinate_system: CoordinateSystem):
+        self.cs = coordinate_system
+
+    def flip(self):
+        raise NotImplementedError
+
+    # lowering hooks ------------------------------------------------------------------
+    def lower_params(self):
+        """-> (radius, conic, tol, max_iter, norm_radius, coefficients list)."""
+        raise NotImplementedError
+
+    def zernike_terms(self):
+        return None
+
+
+class Plane(BaseGeometry):
+    """geometries/plane.py:19-98 (t = -z/N, normal (0,0,1))."""
+
+    geometry_id = _abi.GEOM_PLANE
+
+    def __init__(self, coordinate_system):
+        super().__init__(coordinate_system)
+        self.radius = np.inf
+        self.is_symmetric = True
+
+    def flip(self):
+        pass
+
+    def lower_params(self):
+        return np.inf, 0.0, 0.0, 0, 1.0, []
+
+
+class StandardGeometry(BaseGeometry):
+    """geometries/standard.py:19-167 (sphere / conic, closed form)."""
+
+    geometry_id = _abi.GEOM_STANDARD
+
+    def __init__(self, coordinate_system, radius, conic=0.0):
+        super().__init__(coordinate_system)
+        self.radius = float(radius)
+        self.k = float(conic)
+        self.is_symmetric = True
+
+    def flip(self):
+        self.radius = -self.radius
+
+    def lower_params(self):
+        return self.radius, self.k, 0.0, 0, 1.0, []
+
+
+class NewtonRaphsonGeometry(StandardGeometry):
+    """geometries/newton_raphson.py:43-168 (conic initial guess + Newton refinement)."""
+
+    def __init__(self, coordinate_system, radius, conic=0.0, tol=1e-10, max_iter=100):
+        super().__init__(coordinate_system, radius, conic)
+        self.tol = float(tol)
+        self.max_iter = int(max_iter)
+
+
+class EvenAsphere(NewtonRaphsonGeometry):
+    """geometries/even_asphere.py:28-129: conic + sum_i C_i r^(2(i+1))."""
+
+    geometry_id = _abi.GEOM_EVEN_ASPHERE
+
+    def __init__(self, coordinate_system, radius, conic=0.0, tol=1e-10, max_iter=100,
+                 coefficients=None):
+        super().__init__(coordinate_system, radius, conic, tol, max_iter)
+        self.coefficients = list(coefficients) if coefficients is not None else []
+        self.is_symmetric = True
+
+    def lower_params(self):
+        return (self.radius, self.k, self.tol, self.max_iter, 1.0,
+                [float(c) for c in self.coefficients])
+
+
+class OddAsphere(EvenAsphere):
+    """geometries/odd_asphere.py:20-130: conic + sum_i C_i r^(i+1)."""
+
+    geometry_id = _abi.GEOM_ODD_ASPHERE
+
+
+_ZERNIKE_TYPES = ("standard", "noll", "fringe")
+
+
+def _index_to_number(kind, n, m):
+    """zernike/standard.py:47-60, noll.py:59-78, fringe.py:53-68."""
+    if kind == "standard":
+        if (n - m) % 2 == 0:
+            return (n * (n + 2) + m) // 2
+        return None
+    if kind == "noll":
+        if (n - m) % 2 == 0:
+            mod = n % 4
+            if (m > 0 and mod <= 1) or (m < 0 and mod >= 2):
+                c = 0
+            elif (m >= 0 and mod >= 2) or (m <= 0 and mod <= 1):
+                c = 1
+            return int(n * (n + 1) / 2 + np.abs(m) + c)
+        return None
+    if kind == "fringe":
+        if (n - m) % 2 == 0:
+            return int((1 + (n + abs(m)) / 2) ** 2 - 2 * abs(m) + (1 - np.sign(m)) / 2)
+        return None
+    raise ValueError(kind)
+
+
+def _norm_constant(kind, n, m):
+    """standard.py:63-75 / noll.py:44-56: sqrt((2n+2)/(1+delta_m0)); fringe.py:38-50: 1."""
+    if kind == "fringe":
+        return np.array(1)
+    denominator = 2 if m == 0 else 1
+    return np.sqrt(np.array((2 * n + 2) / denominator))
+
+
+def zernike_indices(kind, n_indices):
+    """zernike/base.py:143-192 (_generate_indices): (n, m) sorted by the scheme's
+    coefficient number."""
+    numbers_present = np.full(n_indices + 1, False)
+    numbers_present[0] = _index_to_number(kind, 0, 0) != 0
+    number, indices = [], []
+    n, m = 0, 0
+    while not all(numbers_present):
+        num = _index_to_number(kind, n, m)
+        if num is not None:
+            number.append(num)
+            indices.append((n, m))
+            if num <= n_indices:
+                numbers_present[num] = True
+        if m == n:
+            n += 1
+            m = -n
+        else:
+            m += 1
+    srt = [e for _, e in sorted(zip(number, indices, strict=False))]
+    return srt[:n_indices]
+
+
+def _gamma(x):
+    try:
+        from scipy.special import gamma
+
+        return gamma(x)
+    except ImportError:  # pragma: no cover
+        return np.float64(math.gamma(float(x)))
+
+
+def radial_coefficients(n, m_abs):
+    """Host precompute of the reference's per-term factorial weights.
+
+    _radial_term (zernike/base.py:228-253): coeff_k = (-1)**k * num / denom,
+    num = factorial(n-k), denom = k! * ((n+m)/2-k)! * ((n-m)/2-k)!, with
+    be.factorial = scipy.special.gamma(n+1) (backend/numpy_backend.py:135-136).
+    _radial_derivative (:272-299): d_k = (-1)**k * (num / denom) * (n - 2k).
+    """
+    s_max = (n - m_abs) // 2 + 1
+    nn = np.array(n)
+    ma = np.array(m_abs)
+    a, d = [], []
+    for k in range(s_max):
+        num = _gamma(nn - k + 1)
+        denom = _gamma(k + 1) * _gamma((nn + ma) // 2 - k + 1) * _gamma((nn - ma) // 2 - k + 1)
+        a.append(float((-1) ** k * num / denom))
+        factor = n - 2 * k
+        d.append(float((-1) ** k * (num / denom) * factor))
+    return a, d
+
+
+class ZernikePolynomialGeometry(NewtonRaphsonGeometry):
+    """geometries/zernike.py:33-246: conic + sum_j c_j N_nm R_n^|m|(rho) {cos|sin}(m phi)."""
+
+    geometry_id = _abi.GEOM_ZERNIKE
+
+    def __init__(self, coordinate_system, radius, conic=0.0, tol=1e-10, max_iter=100,
+                 coefficients=None, zernike_type="standard", norm_radius=1):
+        super().__init__(coordinate_system, radius, conic, tol, max_iter)
+        if zernike_type not in _ZERNIKE_TYPES:
+            raise ValueError(
+                "Zernike type must be one of 'standard', 'noll', or 'fringe', got "
+                f"{zernike_type}")
+        if norm_radius <= 0:
+            raise ValueError(f"Normalization radius must be positive, got {norm_radius}")
+        self.coefficients = np.atleast_1d(
+            np.asarray(coefficients if coefficients is not None else [], dtype=np.float64))
+        self.zernike_type = zernike_type
+        self.norm_radius = float(norm_radius)
+        self.is_symmetric = False
+
+    def lower_params(self):
+        return self.radius, self.k, self.tol, self.max_iter, self.norm_radius, []
+
+    def zernike_terms(self):
+        """-> list of (c, norm, n, m, a_k list, d_k list) in coefficient order."""
+        idx = zernike_indices(self.zernike_type, len(self.coefficients))
+        out = []
+        for (n, m), c in zip(idx, self.coefficients, strict=True):
+            a, d = radial_coefficients(n, abs(m))
+            out.append((float(c), float(_norm_constant(self.zernike_type, n, m)), n, m, a, d))
+        return out

@@ -1,0 +1,226 @@
+"""Lowering: SurfaceGroup + wavelengths -> the kernel's packed lens table (host, NumPy).
+
+The reference walks Python objects per surface per call (surface_group.py:232-244) and
+evaluates n/k per ray with a cache keyed on the whole wavelength array
+(materials/base.py:73-119). Here a lens is lowered ONCE per (surface group,
+wavelength set) into a few KB of structured arrays (include/optiland_rt.h layout):
+
+  surfaces  [S]            ort_surface    geometry id, R, k, tol, flags, offsets
+  cs_ops    [n_ops]        ort_cs_op      localize/globalize translate/rotate ops
+  coef      [n_coef]       double         asphere C_i; Zernike radial a_k / d_k
+  zern      [n_terms]      ort_zernike_term
+  n_tab     [n_lambda][M]  double         n(material, lambda)
+  alpha_tab [n_lambda][M]  double         4*pi*k/lambda (homogeneous.py:49-54)
+
+and segment descriptors (ort_segment) carrying the ray-generation scalars
+(ray_generator.py:49-106, field_types.py:139-181) per (field, wavelength).
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _abi
+from .geometries import NewtonRaphsonGeometry, ZernikePolynomialGeometry
+from .surfaces import ObjectSurface
+
+
+@dataclass
+class LensTable:
+    surfaces: np.ndarray
+    cs_ops: np.ndarray
+    coef: np.ndarray
+    zern: np.ndarray
+    n_tab: np.ndarray
+    alpha_tab: np.ndarray
+    wavelengths: list
+    final_mat: int
+    final_thickness: float
+    materials: list = field(default_factory=list)
+    n_rec: int = 0
+    rec_surfaces: list = field(default_factory=list)  # traced-surface indices recorded
+
+    @property
+    def n_surfaces(self):
+        return int(self.surfaces.shape[0])
+
+    @property
+    def newton_surfaces(self):
+        return [i for i, s in enumerate(self.surfaces)
+                if int(s["geometry"]) in _abi.NEWTON_GEOMETRIES]
+
+    @property
+    def has_zernike(self):
+        return bool(np.any(self.surfaces["geometry"] == _abi.GEOM_ZERNIKE))
+
+
+def lower_surface_group(surface_group, wavelengths, record=False, skip_object=True):
+    """Lower every traced surface (index >= 1) of `surface_group`.
+
+    record: False, True (all traced surfaces) or an iterable of traced-surface
+    indices (0-based within the traced surfaces) to snapshot (standard_surface.py:266-286).
+    """
+    surfs = [s for s in surface_group.surfaces if not isinstance(s, ObjectSurface)]
+    if len(surfs) > _abi.MAX_SURFACES:
+        raise ValueError(f"at most {_abi.MAX_SURFACES} surfaces are supported")
+    wavelengths = [float(w) for w in np.atleast_1d(wavelengths)]
+
+    mats, mat_index = [], {}
+
+    def mat_id(m):
+        key = m.key()
+        if key not in mat_index:
+            mat_index[key] = len(mats)
+            mats.append(m)
+        return mat_index[key]
+
+    if record is True:
+        rec_set = list(range(len(surfs)))
+    elif record:
+        rec_set = sorted(int(i) for i in record)
+    else:
+        rec_set = []
+
+    table = np.zeros(len(surfs), dtype=_abi.SURFACE)
+    ops, coef, zern = [], [], []
+    for si, s in enumerate(surfs):
+        g = s.geometry
+        R, k, tol, max_iter, norm_radius, cc = g.lower_params()
+        row = table[si]
+        row["geometry"] = g.geometry_id
+        row["radius"] = R
+        row["conic"] = k
+        row["tol"] = tol
+        row["max_iter"] = max_iter
+        row["norm_radius"] = norm_radius
+        flags = 0
+        if s.is_reflective:
+            flags |= _abi.SURF_REFLECTIVE
+        if isinstance(g, NewtonRaphsonGeometry) or g.geometry_id == _abi.GEOM_STANDARD:
+            if np.isinf(R):
+                flags |= _abi.SURF_RADIUS_INF
+        if s.aperture is not None:
+            flags |= _abi.SURF_APERTURE
+            row["ap_rmax2"] = s.aperture.r_max**2  # radial.py:62
+            row["ap_rmin2"] = s.aperture.r_min**2
+        if si in rec_set:
+            flags |= _abi.SURF_RECORD
+            row["rec_slot"] = rec_set.index(si)
+        else:
+            row["rec_slot"] = -1
+        row["flags"] = flags
+        if isinstance(g, ZernikePolynomialGeometry):
+            terms = g.zernike_terms()
+            row["coef_off"] = len(zern)
+            row["n_coef"] = len(terms)
+            for (c, norm, n, m, a, d) in terms:
+                zern.append((c, norm, n, m, len(coef), len(a)))
+                coef.extend(a)
+                coef.extend(d)
+        else:
+            row["coef_off"] = len(coef)
+            row["n_coef"] = len(cc)
+            coef.extend(cc)
+        row["mat_pre"] = mat_id(s.material_pre)
+        row["mat_post"] = mat_id(s.material_post)
+        loc = g.cs.localize_ops()
+        glob = g.cs.globalize_ops()
+        row["cs_loc_off"] = len(ops)
+        row["n_cs_loc"] = len(loc)
+        ops.extend(loc)
+        row["cs_glob_off"] = len(ops)
+        row["n_cs_glob"] = len(glob)
+        ops.extend(glob)
+
+    final = surfs[-1]
+    final_mat = mat_id(final.material_post)
+
+    cs = np.zeros(max(1, len(ops)), dtype=_abi.CS_OP)
+    for i, (kind, p) in enumerate(ops):
+        cs[i]["kind"] = kind
+        cs[i]["p"] = p
+    z = np.zeros(max(1, len(zern)), dtype=_abi.ZERNIKE_TERM)
+    for i, (c, norm, n, m, off, nr) in enumerate(zern):
+        z[i] = (c, norm, n, m, off, nr)
+
+    n_tab = np.zeros((len(wavelengths), len(mats)))
+    alpha_tab = np.zeros((len(wavelengths), len(mats)))
+    for j, w in enumerate(wavelengths):
+        for mi, m in enumerate(mats):
+            n_tab[j, mi] = m.n_scalar(w)
+            kv = m.k_scalar(w)
+            # homogeneous.py:49-54: applied only when k > 0; alpha = 4*pi*k/w
+            alpha_tab[j, mi] = (4 * np.pi * np.float64(kv) / np.float64(w)) if kv > 0 else 0.0
+    return LensTable(
+        surfaces=table,
+        cs_ops=cs,
+        coef=np.array(coef if coef else [0.0], dtype=np.float64),
+        zern=z,
+        n_tab=n_tab,
+        alpha_tab=alpha_tab,
+        wavelengths=wavelengths,
+        final_mat=final_mat,
+        final_thickness=float(final.thickness),
+        materials=mats,
+        n_rec=len(rec_set),
+        rec_surfaces=rec_set,
+    )
+
+
+# --------------------------------------------------------------------------------------
+# ray-generation scalars per (field, wavelength) segment
+# --------------------------------------------------------------------------------------
+def _starting_z_offset(optic):
+    """field_types.py:223-235."""
+    z = optic.surface_group.positions[1:-1]
+    offset = optic.paraxial.EPD()
+    return offset - np.min(z)
+
+
+def segment_params(optic, Hx, Hy, lambda_idx, EPL=None, EPD=None):
+    """One ort_segment for field (Hx, Hy): ray_generator.py:49-89 + AngleField /
+    ObjectHeightField.get_ray_origins (field_types.py:139-181, 255-275)."""
+    seg = np.zeros((), dtype=_abi.SEGMENT)
+    if optic.obj_space_telecentric:
+        raise ValueError("telecentric object space is out of scope for the trace core")
+    vxf, vyf = optic.fields.get_vig_factor(Hx, Hy)
+    vx = 1 - np.array(vxf)
+    vy = 1 - np.array(vyf)
+    EPL = optic.paraxial.EPL() if EPL is None else EPL
+    EPD = optic.paraxial.EPD() if EPD is None else EPD
+    max_field = optic.fields.max_field
+    field_x = max_field * Hx
+    field_y = max_field * Hy
+    obj = optic.object_surface
+    if optic.field_type == "angle":
+        if obj.is_infinite:
+            offset = _starting_z_offset(optic)
+            x = -np.tan(np.radians(field_x)) * (offset + EPL)
+            y = -np.tan(np.radians(field_y)) * (offset + EPL)
+            z = optic.surface_group.positions[1] - offset
+            seg["mode"] = _abi.GEN_INFINITE
+            seg["x_off"], seg["y_off"] = float(x), float(y)
+            seg["z0"] = float(np.ravel(z)[0])
+        else:
+            z0 = float(np.ravel(optic.surface_group.positions[0])[0])
+            seg["mode"] = _abi.GEN_FINITE
+            seg["x_off"] = float(-np.tan(np.radians(field_x)) * (EPL - z0))
+            seg["y_off"] = float(-np.tan(np.radians(field_y)) * (EPL - z0))
+            seg["z0"] = z0
+    elif optic.field_type == "object_height":
+        if obj.is_infinite:
+            raise ValueError("Object surface is at infinity.")
+        seg["mode"] = _abi.GEN_FINITE
+        seg["x_off"] = float(np.array(field_x))
+        seg["y_off"] = float(np.array(field_y))
+        seg["z0"] = float(obj.geometry.cs.z)  # plane object: sag 0 (field_types.py:273)
+    else:
+        raise ValueError(f"field type {optic.field_type!r} not supported")
+    seg["epd"] = float(EPD)
+    seg["epl"] = float(EPL)
+    seg["vx"] = float(vx)
+    seg["vy"] = float(vy)
+    seg["lambda_idx"] = int(lambda_idx)
+    return seg

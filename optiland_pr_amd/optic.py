@@ -1,0 +1,108 @@
+"""Optic: the lens system object (host side).
+
+Mirrors the slice of optiland/optic/optic.py the ray-trace path uses:
+add_surface / set_aperture / set_field_type / add_field / add_wavelength /
+update_paraxial / trace (optic.py:584-609) / trace_generic (:611-632), plus
+paraxial, fields, wavelengths, surface_group, object_surface, image_surface,
+primary_wavelength, n().
+
+Optic.trace and trace_generic run on the MI355X: rays are generated and traced by the
+HIP kernels; the returned RealRays hold device (torch) tensors.
+"""
+
+from __future__ import annotations
+
+import numpy as np
+
+from .fields import Aperture, Field, FieldGroup, WavelengthGroup
+from .paraxial import Paraxial
+from .surfaces import ObjectSurface, SurfaceGroup
+
+
+class Optic:
+    def __init__(self, name: str | None = None):
+        self.name = name
+        self.surface_group = SurfaceGroup()
+        self.fields = FieldGroup()
+        self.wavelengths = WavelengthGroup()
+        self.aperture = None
+        self.field_type = None
+        self.paraxial = Paraxial(self)
+        self.obj_space_telecentric = False
+        self.polarization = "ignore"
+        self.apodization = None
+        self._lowered = None  # lowering cache (raytrace.LoweredLens), reset on edits
+
+    # -- building ---------------------------------------------------------------------
+    def add_surface(self, new_surface=None, surface_type="standard", comment="",
+                    index=None, is_stop=False, material="air", **kwargs):
+        self._lowered = None
+        self.surface_group.add_surface(new_surface=new_surface, surface_type=surface_type,
+                                       comment=comment, index=index, is_stop=is_stop,
+                                       material=material, **kwargs)
+
+    def add_field(self, y, x=0.0, vx=0.0, vy=0.0):
+        self.fields.add_field(Field(x, y, vx, vy))
+
+    def add_wavelength(self, value, is_primary=False, unit="um"):
+        self.wavelengths.add_wavelength(value=value, is_primary=is_primary, unit=unit)
+
+    def set_aperture(self, aperture_type, value):
+        self._lowered = None
+        self.aperture = Aperture(aperture_type, value)
+
+    def set_field_type(self, field_type):
+        """optic.py:298-318: 'angle' | 'object_height'."""
+        if field_type not in ("angle", "object_height"):
+            raise ValueError(f"field type {field_type!r} is not supported by the trace core")
+        self.field_type = field_type
+
+    def invalidate(self):
+        """Drop cached device tables after editing surfaces in place."""
+        self._lowered = None
+
+    # -- properties -------------------------------------------------------------------
+    @property
+    def primary_wavelength(self):
+        return self.wavelengths.primary_wavelength.value
+
+    @property
+    def object_surface(self):
+        for s in self.surface_group.surfaces:
+            if isinstance(s, ObjectSurface):
+                return s
+        return None
+
+    @property
+    def image_surface(self):
+        return self.surface_group.surfaces[-1] if self.surface_group.surfaces else None
+
+    def n(self, wavelength="primary"):
+        if wavelength == "primary":
+            wavelength = self.primary_wavelength
+        return self.surface_group.n(wavelength)
+
+    # -- optic_updater.py:192-240 --
+    def update_paraxial(self):
+        ya, _ = self.paraxial.marginal_ray()
+        yb, _ = self.paraxial.chief_ray()
+        ya = np.abs(np.ravel(ya))
+        yb = np.abs(np.ravel(yb))
+        for k, s in enumerate(self.surface_group.surfaces):
+            s.set_semi_aperture(r_max=ya[k] + yb[k])
+            if s.surface_type == "zernike":
+                s.geometry.norm_radius = float(s.semi_aperture * 1.25)
+        self._lowered = None
+
+    # -- tracing ----------------------------------------------------------------------
+    def trace(self, Hx, Hy, wavelength, num_rays=100, distribution="hexapolar"):
+        """optic.py:584-609 -> RealRayTracer.trace (HIP)."""
+        from .raytrace import RealRayTracer
+
+        return RealRayTracer(self).trace(Hx, Hy, wavelength, num_rays, distribution)
+
+    def trace_generic(self, Hx, Hy, Px, Py, wavelength):
+        """optic.py:611-632 -> RealRayTracer.trace_generic (HIP)."""
+        from .raytrace import RealRayTracer
+
+        return RealRayTracer(self).trace_generic(Hx, Hy, Px, Py, wavelength)

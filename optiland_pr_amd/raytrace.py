@@ -1,0 +1,455 @@
+"""Device-side driver of the sequential trace: RealRays on HBM, lens upload, launches.
+
+Mirrors optiland/raytrace/real_ray_tracer.py (RealRayTracer.trace / trace_generic) and
+the SurfaceGroup.trace seam (surfaces/surface_group.py:232-244). PyTorch-ROCm is used
+only for device memory and the current HIP stream; all arithmetic is in
+liboptiland_rt.so (include/optiland_rt.h).
+
+Newton surfaces: the reference stops iterating when max|f| < tol over ALL rays of the
+trace call (newton_raphson.py:148). The kernel runs a schedule of update counts per
+Newton group (= one reference trace call) and reports, per group and surface, the AND of
+the per-ray "converged at update j" bits and the last non-converged update. The host
+checks the schedule is exactly the reference's stopping index and re-launches with the
+corrected schedule when it is not (speculate-and-verify; the schedule is cached per
+lens and field/wavelength key, so a repeated trace is one launch + one 16-byte-per-
+surface read-back).
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _abi, _native
+from .distribution import BaseDistribution, create_distribution
+from .lowering import LensTable, lower_surface_group, segment_params
+
+try:
+    import torch
+except ImportError:  # pragma: no cover
+    torch = None
+
+
+class ZernikeRangeError(ValueError):
+    pass
+
+
+_ZERNIKE_MSG = ("Zernike coordinates must be normalized to [-1, 1]. Consider updating the "
+                "normalization radius to 1.1x the surface aperture.")
+
+
+def get_device():
+    """The HIP device the trace runs on (torch's "cuda" device on ROCm). No fallback."""
+    if torch is None or not torch.cuda.is_available():
+        raise RuntimeError(
+            "optiland_pr_amd traces on an MI355X (HIP) device; torch.cuda.is_available() is "
+            "False. There is no CPU fallback.")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def _ptr(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else C.c_void_p(0)
+
+
+def _stream_handle():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _to_device_bytes(arr: np.ndarray, device):
+    buf = np.frombuffer(np.ascontiguousarray(arr).tobytes(), dtype=np.uint8).copy()
+    return torch.from_numpy(buf).to(device)
+
+
+# --------------------------------------------------------------------------------------
+# rays
+# --------------------------------------------------------------------------------------
+class RealRays:
+    """rays/real_rays.py:22-88 on HBM: SoA float64 tensors x,y,z,L,M,N,i,w,opd."""
+
+    def __init__(self, x, y, z, L, M, N, intensity, wavelength, opd=None, device=None):
+        dev = device or get_device()
+
+        def T(v):
+            return torch.as_tensor(np.atleast_1d(v) if not torch.is_tensor(v) else v,
+                                   dtype=torch.float64, device=dev).reshape(-1).contiguous()
+
+        self.x, self.y, self.z = T(x), T(y), T(z)
+        self.L, self.M, self.N = T(L), T(M), T(N)
+        n = self.x.numel()
+        self.i = T(intensity)
+        if self.i.numel() == 1 and n > 1:
+            self.i = self.i.expand(n).contiguous()
+        self.w = T(wavelength)
+        if self.w.numel() == 1 and n > 1:
+            self.w = self.w.expand(n).contiguous()
+        self.opd = torch.zeros_like(self.x) if opd is None else T(opd)
+        self.is_normalized = True
+
+    @classmethod
+    def empty(cls, n, wavelength, device=None):
+        dev = device or get_device()
+        r = cls.__new__(cls)
+        for a in _abi.RAY_FIELDS:
+            setattr(r, a, torch.empty(n, dtype=torch.float64, device=dev))
+        r.w = torch.full((n,), float(wavelength), dtype=torch.float64, device=dev)
+        r.is_normalized = True
+        return r
+
+    def __len__(self):
+        return self.x.numel()
+
+    def c_struct(self):
+        return _native.ort_rays(*(getattr(self, a).data_ptr() for a in _abi.RAY_FIELDS))
+
+    def numpy(self):
+        return {a: getattr(self, a).detach().cpu().numpy() for a in (*_abi.RAY_FIELDS, "w")}
+
+
+# --------------------------------------------------------------------------------------
+# lens upload
+# --------------------------------------------------------------------------------------
+class DeviceLens:
+    """A LensTable resident in HBM (a few KB) plus the Newton schedule cache."""
+
+    def __init__(self, table: LensTable, device=None):
+        self.table = table
+        self.device = device or get_device()
+        d = self.device
+        self.surfaces = _to_device_bytes(table.surfaces, d)
+        self.cs_ops = _to_device_bytes(table.cs_ops, d)
+        self.coef = torch.as_tensor(table.coef, dtype=torch.float64, device=d)
+        self.zern = _to_device_bytes(table.zern, d)
+        self.n_tab = torch.as_tensor(np.ascontiguousarray(table.n_tab), dtype=torch.float64, device=d)
+        self.alpha_tab = torch.as_tensor(np.ascontiguousarray(table.alpha_tab),
+                                         dtype=torch.float64, device=d)
+        mask = 0
+        for g in np.unique(table.surfaces["geometry"]):
+            mask |= 1 << int(g)
+        self.geometry_mask = mask
+        self.c = _native.ort_lens(
+            self.surfaces.data_ptr(), self.cs_ops.data_ptr(), self.coef.data_ptr(),
+            self.zern.data_ptr(), self.n_tab.data_ptr(), self.alpha_tab.data_ptr(),
+            table.n_surfaces, len(table.wavelengths), table.n_tab.shape[1], table.final_mat,
+            mask, 0, table.final_thickness)
+        self.newton = table.newton_surfaces
+        self.sched_cache: dict = {}
+
+    # -- Newton schedule speculate / verify ---------------------------------------------
+    def initial_schedule(self, keys):
+        S = self.table.n_surfaces
+        sched = np.zeros((len(keys), S), dtype=np.int32)
+        dflt = self.sched_cache.get("_default")
+        for g, k in enumerate(keys):
+            cached = self.sched_cache.get(k)
+            if cached is not None:
+                sched[g] = cached
+            elif dflt is not None:
+                sched[g] = dflt
+            else:
+                for s in self.newton:
+                    sched[g, s] = min(3, int(self.table.surfaces[s]["max_iter"]))
+        return sched
+
+    def verify(self, sched, stats):
+        """-> (ok, new_sched). stats: NEWTON_STAT [n_groups][S]."""
+        ok = True
+        new = sched.copy()
+        for g in range(sched.shape[0]):
+            for s in self.newton:
+                U = int(sched[g, s])
+                max_iter = int(self.table.surfaces[s]["max_iter"])
+                mask = int(stats[g, s]["conv_mask"])
+                last_bad = int(stats[g, s]["last_bad"])
+                below = mask & ((1 << min(U, 64)) - 1)
+                if below:  # every ray had |f| < tol before update U: the reference stops there
+                    new[g, s] = (below & -below).bit_length() - 1
+                    ok = False
+                    break
+                if U < max_iter and last_bad >= U:  # not all converged at U: it goes on
+                    new[g, s] = max_iter if U >= 8 else min(max_iter, max(2 * U + 2, 8))
+                    ok = False
+                    break
+        return ok, new
+
+    def remember(self, keys, sched):
+        for g, k in enumerate(keys):
+            self.sched_cache[k] = sched[g].copy()
+        self.sched_cache["_default"] = sched.max(axis=0)
+
+
+def lens_for(optic_or_group, wavelengths, record=False):
+    """Lowered + uploaded lens, cached on the Optic (invalidated by Optic edits)."""
+    host = optic_or_group
+    sg = getattr(host, "surface_group", host)
+    key = (tuple(float(w) for w in wavelengths), record if isinstance(record, bool) else tuple(record))
+    cache = getattr(host, "_lowered", None)
+    if not isinstance(cache, dict):
+        cache = {}
+        try:
+            host._lowered = cache
+        except AttributeError:
+            pass
+    if key not in cache:
+        cache[key] = DeviceLens(lower_surface_group(sg, wavelengths, record=record))
+    return cache[key]
+
+
+# --------------------------------------------------------------------------------------
+# launches
+# --------------------------------------------------------------------------------------
+def _run(dlens: DeviceLens, launch, n_rays, group_len, keys, newton_mode="reference",
+         with_status=True):
+    """Run `launch(opt, stats, status)` under the Newton speculate-and-verify protocol."""
+    dev = dlens.device
+    S = dlens.table.n_surfaces
+    n_groups = max(1, -(-n_rays // group_len))
+    need_status = with_status and dlens.table.has_zernike
+    status = torch.zeros(1, dtype=torch.int32, device=dev) if need_status else None
+    if not dlens.newton or n_rays == 0:
+        opt = _native.ort_options(_abi.NEWTON_SCHEDULE, 0, None)
+        launch(opt, None, status)
+        _raise_status(status)
+        return
+    if newton_mode == "wave":
+        stats = torch.empty(n_groups * S * _abi.NEWTON_STAT.itemsize, dtype=torch.uint8, device=dev)
+        opt = _native.ort_options(_abi.NEWTON_WAVE, 0, None)
+        launch(opt, stats, status)
+        _raise_status(status)
+        return
+    if len(keys) != n_groups:
+        keys = [("group", g) for g in range(n_groups)]
+    sched = dlens.initial_schedule(keys)
+    stats = torch.empty(n_groups * S * _abi.NEWTON_STAT.itemsize, dtype=torch.uint8, device=dev)
+    for _ in range(64):
+        sched_dev = torch.from_numpy(sched.reshape(-1).copy()).to(dev)
+        opt = _native.ort_options(_abi.NEWTON_SCHEDULE, 0, sched_dev.data_ptr())
+        launch(opt, stats, status)
+        st = stats.cpu().numpy().view(_abi.NEWTON_STAT).reshape(n_groups, S)
+        ok, new = dlens.verify(sched, st)
+        if ok:
+            dlens.remember(keys, sched)
+            _raise_status(status)
+            return
+        sched = new
+    raise RuntimeError("Newton schedule did not settle")
+
+
+def _raise_status(status):
+    if status is None:
+        return
+    v = int(status.item())
+    if v & _abi.STATUS_ZERNIKE_RANGE:
+        raise ZernikeRangeError(_ZERNIKE_MSG)
+
+
+def trace_pupil(dlens: DeviceLens, segments: np.ndarray, px, py, out: RealRays, n_rays,
+                seg_len, group_len, pupil_per_ray=False, keys=(), rec=None,
+                newton_mode="reference", start_surface=0):
+    """Generate + trace in one launch (ort_trace_pupil)."""
+    lib = _native.load()
+    dev = dlens.device
+    seg_dev = _to_device_bytes(segments, dev)
+    batch = _native.ort_batch(n_rays, seg_len, group_len, len(segments), int(pupil_per_ray),
+                              seg_dev.data_ptr())
+    out_c = out.c_struct()
+
+    def launch(opt, stats, status):
+        opt.start_surface = start_surface
+        rc = lib.ort_trace_pupil(C.byref(dlens.c), _ptr(px), _ptr(py), C.byref(out_c),
+                                 C.byref(batch), C.byref(opt), _ptr(rec), _ptr(stats),
+                                 _ptr(status), _stream_handle())
+        _native.check(rc, "ort_trace_pupil")
+
+    _run(dlens, launch, n_rays, group_len, list(keys), newton_mode)
+    return seg_dev
+
+
+def trace_rays(dlens: DeviceLens, rays_in: RealRays, rays_out: RealRays, group_len=None,
+               keys=(), rec=None, newton_mode="reference", start_surface=0, segments=None,
+               seg_len=None):
+    """Trace resident rays (ort_trace_sequential); rays_out may be rays_in (in place)."""
+    lib = _native.load()
+    n = len(rays_in)
+    group_len = group_len or max(n, 1)
+    seg_dev = None
+    if segments is not None:
+        seg_dev = _to_device_bytes(segments, dlens.device)
+        batch = _native.ort_batch(n, seg_len, group_len, len(segments), 0, seg_dev.data_ptr())
+    else:
+        batch = _native.ort_batch(n, max(n, 1), group_len, 0, 0, None)
+    in_c, out_c = rays_in.c_struct(), rays_out.c_struct()
+
+    def launch(opt, stats, status):
+        opt.start_surface = start_surface
+        rc = lib.ort_trace_sequential(C.byref(dlens.c), C.byref(in_c), C.byref(out_c),
+                                      C.byref(batch), C.byref(opt), _ptr(rec), _ptr(stats),
+                                      _ptr(status), _stream_handle())
+        _native.check(rc, "ort_trace_sequential")
+
+    if rays_in is rays_out and dlens.newton and newton_mode != "wave":
+        # a schedule miss re-runs the launch: keep the input
+        src = RealRays.__new__(RealRays)
+        for a in (*_abi.RAY_FIELDS, "w"):
+            setattr(src, a, getattr(rays_in, a).clone())
+        in_c = src.c_struct()
+    _run(dlens, launch, n, group_len, list(keys), newton_mode)
+    return seg_dev
+
+
+def generate_rays(segments, px, py, out: RealRays, n_rays, seg_len, pupil_per_ray=False):
+    lib = _native.load()
+    seg_dev = _to_device_bytes(segments, out.x.device)
+    batch = _native.ort_batch(n_rays, seg_len, n_rays, len(segments), int(pupil_per_ray),
+                              seg_dev.data_ptr())
+    out_c = out.c_struct()
+    rc = lib.ort_generate_rays(_ptr(px), _ptr(py), C.byref(out_c), C.byref(batch),
+                               _stream_handle())
+    _native.check(rc, "ort_generate_rays")
+    return seg_dev
+
+
+# --------------------------------------------------------------------------------------
+# reference-shaped entry points
+# --------------------------------------------------------------------------------------
+def _validate_normalized(x, y, kind):
+    """real_ray_tracer.py:135-152."""
+    xa, ya = np.asarray(x, dtype=np.float64), np.asarray(y, dtype=np.float64)
+    if not (np.all((xa >= -1) & (xa <= 1)) and np.all((ya >= -1) & (ya <= 1))):
+        raise ValueError(f"Normalized {kind} coordinates must be within (-1, 1)")
+
+
+def _record_into(sg, rec, n, rec_surfaces, rays0=None):
+    """Fill Surface.x/y/z/L/M/N/intensity/opd (standard_surface.py:266-286) from a record
+    buffer [n_rec][8][n] (device tensors, no copy)."""
+    from .surfaces import ObjectSurface
+
+    traced = [s for s in sg.surfaces if not isinstance(s, ObjectSurface)]
+    names = ("x", "y", "z", "L", "M", "N", "intensity", "opd")
+    if rays0 is not None:
+        obj = sg.surfaces[0]
+        for nm, a in zip(names, _abi.RAY_FIELDS, strict=True):
+            setattr(obj, nm, getattr(rays0, a))
+    view = rec.view(len(rec_surfaces), 8, n) if rec is not None else None
+    for slot, si in enumerate(rec_surfaces):
+        for f, nm in enumerate(names):
+            setattr(traced[si], nm, view[slot, f])
+
+
+class RealRayTracer:
+    """raytrace/real_ray_tracer.py:23-133 running on the MI355X."""
+
+    def __init__(self, optic):
+        self.optic = optic
+
+    def trace(self, Hx, Hy, wavelength, num_rays=100, distribution="hexapolar",
+              newton_mode="reference"):
+        optic = self.optic
+        _validate_normalized(Hx, Hy, "field")
+        if isinstance(distribution, str):
+            distribution = create_distribution(distribution)
+            distribution.generate_points(num_rays)
+        if not isinstance(distribution, BaseDistribution) and not hasattr(distribution, "x"):
+            raise ValueError("Invalid distribution type.")
+        Px = np.asarray(distribution.x, dtype=np.float64)
+        Py = np.asarray(distribution.y, dtype=np.float64)
+        Hx = np.atleast_1d(np.asarray(Hx, dtype=np.float64))
+        Hy = np.atleast_1d(np.asarray(Hy, dtype=np.float64))
+        Hx, Hy = np.broadcast_arrays(Hx, Hy)
+        record = optic.surface_group.record
+        dlens = lens_for(optic, [wavelength], record=True if record == "all" else False)
+        EPL, EPD = optic.paraxial.EPL(), optic.paraxial.EPD()
+        segs = np.stack([segment_params(optic, float(hx), float(hy), 0, EPL, EPD)
+                         for hx, hy in zip(Hx, Hy, strict=True)])
+        n_p = Px.size
+        n = n_p * len(segs)
+        dev = dlens.device
+        px = torch.as_tensor(Px, device=dev)
+        py = torch.as_tensor(Py, device=dev)
+        out = RealRays.empty(n, wavelength, device=dev)
+        rec = None
+        if record == "all":
+            rec = torch.empty(dlens.table.n_rec * 8 * n, dtype=torch.float64, device=dev)
+        keys = [("trace", tuple(np.round(Hx, 15)), tuple(np.round(Hy, 15)), float(wavelength), n_p)]
+        trace_pupil(dlens, segs, px, py, out, n, n_p, n, keys=keys, rec=rec,
+                    newton_mode=newton_mode)
+        self._record(dlens, out, rec, n, segs, px, py, n_p)
+        return out
+
+    def trace_generic(self, Hx, Hy, Px, Py, wavelength, newton_mode="reference"):
+        """real_ray_tracer.py:99-133: per-ray field and pupil coordinates."""
+        optic = self.optic
+        _validate_normalized(Hx, Hy, "field")
+        _validate_normalized(Px, Py, "pupil")
+        Hx, Hy, Px, Py = (np.atleast_1d(np.asarray(v, dtype=np.float64)) for v in (Hx, Hy, Px, Py))
+        Hx, Hy, Px, Py = np.broadcast_arrays(Hx, Hy, Px, Py)
+        n = Hx.size
+        # vignetting is applied to the pupil here AND inside generate_rays (reference)
+        vig = [optic.fields.get_vig_factor(hx, hy) for hx, hy in zip(Hx, Hy, strict=True)]
+        vxs = np.array([v[0] for v in vig])
+        vys = np.array([v[1] for v in vig])
+        Px = Px * (1 - vxs)
+        Py = Py * (1 - vys)
+        record = optic.surface_group.record
+        dlens = lens_for(optic, [wavelength], record=True if record == "all" else False)
+        EPL, EPD = optic.paraxial.EPL(), optic.paraxial.EPD()
+        uniq = {}
+        segs = np.empty(n, dtype=_abi.SEGMENT)
+        for r in range(n):
+            k = (float(Hx[r]), float(Hy[r]))
+            if k not in uniq:
+                uniq[k] = segment_params(optic, k[0], k[1], 0, EPL, EPD)
+            segs[r] = uniq[k]
+        dev = dlens.device
+        px = torch.as_tensor(np.ascontiguousarray(Px), device=dev)
+        py = torch.as_tensor(np.ascontiguousarray(Py), device=dev)
+        out = RealRays.empty(n, wavelength, device=dev)
+        rec = None
+        if record == "all":
+            rec = torch.empty(dlens.table.n_rec * 8 * n, dtype=torch.float64, device=dev)
+        trace_pupil(dlens, segs, px, py, out, n, 1, n, pupil_per_ray=True,
+                    keys=[("generic", float(wavelength), n)], rec=rec, newton_mode=newton_mode)
+        self._record(dlens, out, rec, n, segs, px, py, 1, pupil_per_ray=True)
+        return out
+
+    def _record(self, dlens, out, rec, n, segs, px, py, seg_len, pupil_per_ray=False):
+        sg = self.optic.surface_group
+        if rec is not None:
+            rays0 = RealRays.empty(n, 0.0, device=dlens.device)
+            generate_rays(segs, px, py, rays0, n, seg_len, pupil_per_ray)
+            _record_into(sg, rec, n, dlens.table.rec_surfaces, rays0)
+        else:
+            sg.reset()
+            # image-surface record only (what SpotDiagram reads: surface_group.x[-1, :])
+            img = sg.surfaces[-1]
+            for nm, a in zip(("x", "y", "z", "L", "M", "N", "intensity", "opd"),
+                             _abi.RAY_FIELDS, strict=True):
+                setattr(img, nm, getattr(out, a))
+
+
+def trace_surface_group(sg, rays: RealRays, skip=0, newton_mode="reference"):
+    """SurfaceGroup.trace(rays, skip) (surface_group.py:232-244): in-place trace of
+    resident RealRays through the traced surfaces (no image-space propagate)."""
+    w = torch.unique(rays.w)
+    if w.numel() != 1:
+        raise ValueError("SurfaceGroup.trace on the MI355X core expects one wavelength per "
+                         "call (the reference traces one wavelength per Optic.trace)")
+    wl = float(w.item())
+    table = lower_surface_group(sg, [wl], record=(sg.record == "all"))
+    # SurfaceGroup.trace does not include the image-space propagate of RealRayTracer
+    table.final_mat = -1
+    dlens = DeviceLens(table, device=rays.x.device)
+    rec = None
+    n = len(rays)
+    if sg.record == "all":
+        rec = torch.empty(table.n_rec * 8 * n, dtype=torch.float64, device=rays.x.device)
+    rays0 = None
+    if rec is not None:
+        rays0 = RealRays.__new__(RealRays)
+        for a in (*_abi.RAY_FIELDS, "w"):
+            setattr(rays0, a, getattr(rays, a).clone())
+    trace_rays(dlens, rays, rays, rec=rec, newton_mode=newton_mode,
+               start_surface=max(int(skip) - 1, 0))
+    if rec is not None:
+        _record_into(sg, rec, n, table.rec_surfaces, rays0)
+    return rays

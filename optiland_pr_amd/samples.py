@@ -1,0 +1,206 @@
+"""Sample lenses (prescriptions restated from optiland/samples/objectives.py:46-173 and
+docs/examples/Tutorial_7d_Three_Mirror_Anastigmat.ipynb), plus the synthetic variants
+the benchmark configs and parity fixtures use (BASELINE.json configs).
+
+Each builder mirrors tests/golden/gen_golden.py's reference-API builder of the same name.
+"""
+
+from __future__ import annotations
+
+import numpy as np
+
+from .optic import Optic
+from .surfaces import RadialAperture
+
+
+class CookeTriplet(Optic):
+    """samples/objectives.py:46-72."""
+
+    def __init__(self):
+        super().__init__()
+        self.add_surface(index=0, radius=np.inf, thickness=np.inf)
+        self.add_surface(index=1, radius=22.01359, thickness=3.25896, material="SK16")
+        self.add_surface(index=2, radius=-435.76044, thickness=6.00755)
+        self.add_surface(index=3, radius=-22.21328, thickness=0.99997, material=("F2", "schott"))
+        self.add_surface(index=4, radius=20.29192, thickness=4.75041, is_stop=True)
+        self.add_surface(index=5, radius=79.68360, thickness=2.95208, material="SK16")
+        self.add_surface(index=6, radius=-18.39533, thickness=42.20778)
+        self.add_surface(index=7)
+        self.set_aperture(aperture_type="EPD", value=10)
+        self.set_field_type(field_type="angle")
+        self.add_field(y=0)
+        self.add_field(y=14)
+        self.add_field(y=20)
+        self.add_wavelength(value=0.48)
+        self.add_wavelength(value=0.55, is_primary=True)
+        self.add_wavelength(value=0.65)
+
+
+class DoubleGauss(Optic):
+    """samples/objectives.py:75-114 (8 spheres + 3 planes + image; S = 12)."""
+
+    def __init__(self):
+        super().__init__()
+        self.add_surface(index=0, radius=np.inf, thickness=np.inf)
+        self.add_surface(index=1, radius=56.20238, thickness=8.75, material="N-SSK2")
+        self.add_surface(index=2, radius=152.28580, thickness=0.5)
+        self.add_surface(index=3, radius=37.68262, thickness=12.5, material="N-SK2")
+        self.add_surface(index=4, radius=np.inf, thickness=3.8, material=("F5", "schott"))
+        self.add_surface(index=5, radius=24.23130, thickness=16.369445)
+        self.add_surface(index=6, radius=np.inf, thickness=13.747957, is_stop=True)
+        self.add_surface(index=7, radius=-28.37731, thickness=3.8, material=("F5", "schott"))
+        self.add_surface(index=8, radius=np.inf, thickness=11, material="N-SK16")
+        self.add_surface(index=9, radius=-37.92546, thickness=0.5)
+        self.add_surface(index=10, radius=177.41176, thickness=7, material="N-SK16")
+        self.add_surface(index=11, radius=-79.41143, thickness=61.487536)
+        self.add_surface(index=12)
+        self.set_aperture(aperture_type="imageFNO", value=5)
+        self.set_field_type(field_type="angle")
+        self.add_field(y=0)
+        self.add_field(y=10)
+        self.add_field(y=14)
+        self.add_wavelength(value=0.4861)
+        self.add_wavelength(value=0.5876, is_primary=True)
+        self.add_wavelength(value=0.6563)
+
+
+_RT_ROWS = [
+    # radius, thickness, material, is_stop  (samples/objectives.py:117-173)
+    (np.inf, np.inf, None, False),
+    (1.69111096, 0.08259680, "N-SK10", False),
+    (0.94414496, 0.8, None, False),
+    (4.32100401, 0.080256, "SK15", False),
+    (1.78117621, 0.5, None, False),
+    (2.64050282, 0.27638160, "BASF2", False),
+    (-3.86177348, 0.1, None, False),
+    (1.05627661, 0.2, "FK3", False),
+    (-4.06933311, 0.2001384, None, False),
+    (np.inf, 0.06688, None, True),
+    (-2.61246583, 0.064372, ("SF15", "hikari"), False),
+    (0.99117409, 0.3, None, False),
+    (9.03045960, 0.18743120, "N-LAK12", False),
+    (-1.35680743, 2.35130547, None, False),
+]
+
+
+def _reverse_telephoto(lens: Optic, aspheres=None, kind="even_asphere"):
+    aspheres = aspheres or {}
+    for k, (R, t, mat, stop) in enumerate(_RT_ROWS):
+        kw = dict(index=k, radius=R, thickness=t, is_stop=stop)
+        if mat is not None:
+            kw["material"] = mat
+        if k in aspheres:
+            kw.update(surface_type=kind, conic=0.0, coefficients=aspheres[k])
+        lens.add_surface(**kw)
+    lens.add_surface(index=len(_RT_ROWS))
+    lens.set_aperture(aperture_type="EPD", value=0.3)
+    lens.set_field_type(field_type="angle")
+    lens.add_field(y=0)
+    lens.add_field(y=21)
+    lens.add_field(y=30)
+    lens.add_wavelength(value=0.4861)
+    lens.add_wavelength(value=0.5876, is_primary=True)
+    lens.add_wavelength(value=0.6563)
+    return lens
+
+
+class ReverseTelephoto(Optic):
+    """samples/objectives.py:117-173 (S = 14)."""
+
+    def __init__(self):
+        super().__init__()
+        _reverse_telephoto(self)
+
+
+class ReverseTelephotoAsphere(Optic):
+    """Config 3 "even-asphere wide-angle" (SURVEY 8d.3): ReverseTelephoto with surfaces 2
+    and 13 as even aspheres (k = 0, C = [0.02, -0.01, 0.005] / [0.01, 0.005, -0.002])."""
+
+    def __init__(self):
+        super().__init__()
+        _reverse_telephoto(self, {2: [0.02, -0.01, 0.005], 13: [0.01, 0.005, -0.002]})
+
+
+class ReverseTelephotoOddAsphere(Optic):
+    """ReverseTelephoto with surface 4 an odd asphere (odd_asphere.py coverage)."""
+
+    def __init__(self):
+        super().__init__()
+        _reverse_telephoto(self, {4: [0.0, 0.003, -0.002, 0.001]}, kind="odd_asphere")
+
+
+class ThreeMirrorAnastigmat(Optic):
+    """Tutorial_7d_Three_Mirror_Anastigmat.ipynb cell 1: three tilted/decentred Zernike
+    mirrors (config 5), fixed coefficients."""
+
+    def __init__(self, zernike_type="fringe",
+                 coefficients=(0, 0, 0, 1e-4, 2e-4, -1e-4, 5e-5, 0, 0, 3e-5)):
+        super().__init__(name="TMA")
+        self.set_aperture(aperture_type="EPD", value=10)
+        self.set_field_type(field_type="angle")
+        self.add_field(y=0)
+        self.add_field(y=+1.5)
+        self.add_field(y=-1.5)
+        self.add_wavelength(value=0.486)
+        self.add_wavelength(value=0.587, is_primary=True)
+        self.add_wavelength(value=0.656)
+        self.add_surface(index=0, radius=np.inf, thickness=np.inf)
+        common = dict(conic=0, material="mirror", surface_type="zernike",
+                      coefficients=list(coefficients), zernike_type=zernike_type)
+        self.add_surface(index=1, radius=-100, thickness=-20, rx=np.radians(-15.0),
+                         is_stop=True, **common)
+        self.add_surface(index=2, radius=-100, thickness=+20, rx=np.radians(-10.0),
+                         dy=-11.5, **common)
+        self.add_surface(index=3, radius=-100, thickness=-22, rx=np.radians(-1.0), dy=-15,
+                         **common)
+        self.add_surface(index=4, dy=-19.3)
+        self.update_paraxial()
+
+
+class CookeTripletApertures(CookeTriplet):
+    """CookeTriplet with radial clear apertures on surfaces 3 and 5 (clip coverage)."""
+
+    def __init__(self):
+        super().__init__()
+        self.surface_group.surfaces[3].aperture = RadialAperture(r_max=4.5)
+        self.surface_group.surfaces[5].aperture = RadialAperture(r_max=8.0, r_min=0.4)
+
+
+class DecenteredTriplet(Optic):
+    """Cooke-like triplet with a tilted/decentred element (rotate_x/y/z coverage)."""
+
+    def __init__(self):
+        super().__init__()
+        self.add_surface(index=0, radius=np.inf, thickness=np.inf)
+        self.add_surface(index=1, radius=22.01359, thickness=3.25896, material="SK16")
+        self.add_surface(index=2, radius=-435.76044, thickness=6.00755)
+        self.add_surface(index=3, radius=-22.21328, thickness=0.99997,
+                         material=("F2", "schott"), dx=0.05, dy=-0.1, rx=0.01, ry=-0.02,
+                         rz=0.3)
+        self.add_surface(index=4, radius=20.29192, thickness=4.75041, is_stop=True, dy=-0.1,
+                         rx=0.01)
+        self.add_surface(index=5, radius=79.68360, thickness=2.95208, material="SK16",
+                         conic=-0.5)
+        self.add_surface(index=6, radius=-18.39533, thickness=42.20778, conic=1.2)
+        self.add_surface(index=7)
+        self.set_aperture(aperture_type="EPD", value=10)
+        self.set_field_type(field_type="angle")
+        self.add_field(y=0)
+        self.add_field(y=14)
+        self.add_field(x=5, y=20)
+        self.add_wavelength(value=0.55, is_primary=True)
+
+
+# name -> builder, matching tests/golden/gen_golden.py CASES
+GOLDEN_LENSES = {
+    "cooke": CookeTriplet,
+    "dg": DoubleGauss,
+    "rt": ReverseTelephoto,
+    "rt_asph": ReverseTelephotoAsphere,
+    "rt_odd": ReverseTelephotoOddAsphere,
+    "tma_fringe": lambda: ThreeMirrorAnastigmat("fringe"),
+    "tma_standard": lambda: ThreeMirrorAnastigmat("standard"),
+    "tma_noll": lambda: ThreeMirrorAnastigmat("noll"),
+    "cooke_aperture": CookeTripletApertures,
+    "decentered": DecenteredTriplet,
+}

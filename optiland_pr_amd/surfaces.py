@@ -1,0 +1,293 @@
+"""Surfaces and the surface group.
+
+Mirrors optiland/surfaces/{standard_surface,object_surface,surface_group}.py and the
+factories in optiland/surfaces/factories/*.py (add_surface keyword semantics:
+radius / conic / thickness / dx / dy / x / y / z / rx / ry / rz / material /
+surface_type / coefficients / aperture / tol / max_iter / norm_radius / zernike_type).
+
+`SurfaceGroup.trace(rays, skip=0)` is the drop-in seam (surface_group.py:232-244): it
+lowers the group into the kernel's surface table and runs the HIP trace; there is no
+per-surface Python loop and no CPU path.
+"""
+
+from __future__ import annotations
+
+import numpy as np
+
+from .coordinate_system import CoordinateSystem
+from .geometries import (
+    EvenAsphere,
+    OddAsphere,
+    Plane,
+    StandardGeometry,
+    ZernikePolynomialGeometry,
+)
+from .materials import BaseMaterial, IdealMaterial, configure_material
+
+
+class RadialAperture:
+    """physical_apertures/radial.py:24-90: clip (i = 0) outside r_min <= r <= r_max."""
+
+    def __init__(self, r_max, r_min=0):
+        self.r_max = float(r_max)
+        self.r_min = float(r_min)
+
+    def scale(self, scale_factor):
+        self.r_max = self.r_max * scale_factor
+        self.r_min = self.r_min * scale_factor
+
+
+def configure_aperture(aperture):
+    """physical_apertures/radial.py:9-22."""
+    if aperture is None:
+        return None
+    if isinstance(aperture, (int, float)):
+        return RadialAperture(r_max=aperture / 2)
+    if isinstance(aperture, RadialAperture):
+        return aperture
+    raise ValueError(
+        f"Invalid `aperture` provided: {aperture}. Only radial apertures are lowered "
+        "to the MI355X trace core."
+    )
+
+
+class Surface:
+    """standard_surface.py:32-233 (the real-ray branch of Surface.trace runs in HIP)."""
+
+    def __init__(self, previous_surface, material_post, geometry, is_stop=False,
+                 aperture=None, surface_type=None, comment="", is_reflective=False):
+        self.geometry = geometry
+        self.previous_surface = previous_surface
+        self._material_post = material_post
+        self.is_stop = is_stop
+        self.aperture = configure_aperture(aperture)
+        self.semi_aperture = None
+        self.surface_type = surface_type
+        self.comment = comment
+        self.is_reflective = is_reflective
+        self.thickness = 0.0
+        self.reset()
+
+    @property
+    def material_pre(self):
+        return (self.previous_surface.material_post if self.previous_surface is not None
+                else self.material_post)
+
+    @property
+    def material_post(self):
+        if self._material_post is None:  # mirror: material_post = material_pre
+            return self.material_pre
+        return self._material_post
+
+    @material_post.setter
+    def material_post(self, m):
+        self._material_post = m
+
+    def set_semi_aperture(self, r_max):
+        self.semi_aperture = r_max
+
+    def reset(self):
+        for a in ("x", "y", "z", "L", "M", "N", "intensity", "opd"):
+            setattr(self, a, np.empty(0))
+
+
+class ObjectSurface(Surface):
+    """object_surface.py:19-72: records only, no intersection."""
+
+    def __init__(self, geometry, material_post, comment=""):
+        super().__init__(None, material_post, geometry, comment=comment)
+
+    @property
+    def is_infinite(self):
+        return bool(np.isinf(self.geometry.cs.z))
+
+
+def _make_geometry(surface_type, cs, kw):
+    """surfaces/factories/geometry_factory.py:58-389 with geometry_configs.py defaults."""
+    st = surface_type or "standard"
+    radius = kw.get("radius", np.inf)
+    conic = kw.get("conic", 0.0)
+    if st == "standard":
+        if np.isinf(radius):
+            return Plane(cs)
+        return StandardGeometry(cs, radius, conic)
+    if st == "plane":
+        return Plane(cs)
+    if st == "even_asphere":
+        return EvenAsphere(cs, radius, conic, kw.get("tol", 1e-6), kw.get("max_iter", 100),
+                           kw.get("coefficients", []))
+    if st == "odd_asphere":
+        return OddAsphere(cs, radius, conic, kw.get("tol", 1e-6), kw.get("max_iter", 100),
+                          kw.get("coefficients", []))
+    if st == "zernike":
+        return ZernikePolynomialGeometry(
+            cs, radius, conic, kw.get("tol", 1e-6), kw.get("max_iter", 100),
+            kw.get("coefficients", []), kw.get("zernike_type", "fringe"),
+            kw.get("norm_radius", 1.0))
+    raise ValueError(
+        f"Surface type {st!r} is not lowered to the MI355X trace core "
+        "(supported: standard, plane, even_asphere, odd_asphere, zernike).")
+
+
+class SurfaceGroup:
+    """surface_group.py:30-330."""
+
+    def __init__(self):
+        self.surfaces: list[Surface] = []
+        self.use_absolute_cs = False
+        # per-surface snapshots (standard_surface.py:266-286): None = image surface only,
+        # "all" = every surface (8 x 8 B per ray per surface of HBM writes)
+        self.record = None
+
+    # -- properties (surface_group.py:95-217) --
+    @property
+    def num_surfaces(self):
+        return len(self.surfaces)
+
+    @property
+    def positions(self):
+        return np.array([s.geometry.cs.position_in_gcs[2] for s in self.surfaces]).reshape(-1, 1)
+
+    @property
+    def radii(self):
+        return np.array([s.geometry.radius for s in self.surfaces], dtype=np.float64)
+
+    @property
+    def stop_index(self):
+        for i, s in enumerate(self.surfaces):
+            if s.is_stop:
+                return i
+        raise ValueError("No stop surface found.")
+
+    def n(self, wavelength):
+        return np.array([s.material_post.n_scalar(wavelength) for s in self.surfaces])
+
+    def _stack(self, attr):
+        vals = [getattr(s, attr) for s in self.surfaces]
+        if any(hasattr(v, "device") for v in vals):
+            import torch
+
+            n = max(int(v.numel()) if hasattr(v, "numel") else len(v) for v in vals)
+            dev = next(v.device for v in vals if hasattr(v, "device"))
+            rows = [v if hasattr(v, "device") and v.numel() == n
+                    else torch.full((n,), float("nan"), dtype=torch.float64, device=dev)
+                    for v in vals]
+            return torch.stack(rows)
+        return np.stack([np.asarray(v) for v in vals])
+
+    @property
+    def x(self):
+        return self._stack("x")
+
+    @property
+    def y(self):
+        return self._stack("y")
+
+    @property
+    def z(self):
+        return self._stack("z")
+
+    @property
+    def L(self):
+        return self._stack("L")
+
+    @property
+    def M(self):
+        return self._stack("M")
+
+    @property
+    def N(self):
+        return self._stack("N")
+
+    @property
+    def intensity(self):
+        return self._stack("intensity")
+
+    @property
+    def opd(self):
+        return self._stack("opd")
+
+    def reset(self):
+        for s in self.surfaces:
+            s.reset()
+
+    # -- building (surface_group.py:246-330 + factories) --
+    def add_surface(self, new_surface=None, surface_type="standard", comment="",
+                    index=None, is_stop=False, material="air", **kwargs):
+        if new_surface is None:
+            if index is None:
+                raise ValueError("Must define index when defining surface.")
+            if index > len(self.surfaces):
+                raise IndexError("Surface index cannot be greater than number of surfaces.")
+            new_surface = self._create(surface_type, comment, index, is_stop, material, kwargs)
+        new_surface.thickness = kwargs.get("thickness", 0.0)
+        if index is None:
+            index = len(self.surfaces)
+        if index < 0:
+            raise IndexError(f"Index {index} cannot be negative.")
+        if index == 0 and len(self.surfaces) > 0:
+            raise ValueError("Surface index cannot be zero after first surface is created.")
+        self.surfaces.insert(index, new_surface)
+        self._relink()
+        if not self.use_absolute_cs and index < len(self.surfaces) - 1:
+            self._update_coordinate_systems(index)
+        if new_surface.is_stop:
+            for i, s in enumerate(self.surfaces):
+                s.is_stop = i == index
+
+    def _relink(self):
+        for i, s in enumerate(self.surfaces):
+            s.previous_surface = self.surfaces[i - 1] if i > 0 else None
+
+    def _update_coordinate_systems(self, start_index):
+        for i in range(max(start_index, 1), len(self.surfaces)):
+            if i == 1:
+                z = 0.0
+            else:
+                prev = self.surfaces[i - 1]
+                z = prev.geometry.cs.z + prev.thickness
+            self.surfaces[i].geometry.cs.z = z
+
+    def _create(self, surface_type, comment, index, is_stop, material, kw):
+        # coordinate_system_factory.py:28-93
+        if "z" in kw:
+            if "thickness" in kw:
+                raise ValueError('Cannot define both "thickness" and "z".')
+            if "dx" in kw or "dy" in kw:
+                raise ValueError('Cannot define "dx" or "dy" when using absolute "x", "y", "z".')
+            x, y, z = kw.get("x", 0), kw.get("y", 0), kw["z"]
+            self.use_absolute_cs = True
+        else:
+            if self.use_absolute_cs:
+                raise ValueError('Cannot pass "thickness" after defining "x", "y", "z" '
+                                 "position for a previous surface.")
+            thickness = kw.get("thickness", 0)
+            x, y = kw.get("dx", 0), kw.get("dy", 0)
+            if index == 0:
+                z = -thickness
+            elif index == 1:
+                z = 0
+            else:
+                prev = self.surfaces[index - 1]
+                z = prev.geometry.cs.z + prev.thickness
+        cs = CoordinateSystem(x=x, y=y, z=z, rx=kw.get("rx", 0), ry=kw.get("ry", 0),
+                              rz=kw.get("rz", 0))
+        # material_factory.py:22-62
+        is_reflective = isinstance(material, str) and material == "mirror"
+        material_post = configure_material(material)
+        geometry = _make_geometry(surface_type, cs, kw)
+        if index == 0:
+            s = ObjectSurface(geometry, material_post, comment)
+            s.thickness = kw.get("thickness", 0.0)
+            return s
+        if kw.get("phase_profile") is not None or surface_type in ("paraxial", "grating"):
+            raise ValueError(f"interaction for surface_type={surface_type!r} is out of scope")
+        return Surface(None, material_post, geometry, is_stop=is_stop,
+                       aperture=kw.get("aperture"), surface_type=surface_type,
+                       comment=comment, is_reflective=is_reflective)
+
+    def trace(self, rays, skip=0):
+        """surface_group.py:232-244: trace `rays` (RealRays, device) in place."""
+        from .raytrace import trace_surface_group
+
+        return trace_surface_group(self, rays, skip=skip)

@@ -1,0 +1,465 @@
+"""ORACLE -- NumPy CPU restatement of the reference's sequential real-ray trace.
+
+TEST INFRASTRUCTURE ONLY. Only tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg may import this module, and only as the checker / CPU baseline.
+The product path (optiland_pr_amd) never imports it and has no CPU fallback.
+
+It restates, formula by formula and in the same evaluation order, the reference
+(PriUVBio/optiland_Pr, Optiland 0.5.8 fork) NumPy-backend hot path:
+
+  ray_generator.py:28-106, field_types.py:139-180      ray construction
+  surface_group.py:232-244, standard_surface.py:186-233 surface loop
+  coordinate_system.py:73-107, real_rays.py:90-130     localize / globalize
+  plane.py:61-98, standard.py:73-167                   closed-form intersections
+  newton_raphson.py:119-168                            Newton refinement (global stop)
+  even_asphere.py:82-129, odd_asphere.py:73-130        asphere sag / normal
+  zernike.py:133-246, zernike/base.py:42-299           Zernike sag / normal
+  homogeneous.py:30-57                                 propagate + absorption
+  standard_surface.py:218                              OPD accumulation
+  physical_apertures/radial.py:50-63, real_rays.py:132-139  radial clip
+  real_rays.py:141-181, 511-547                        refract / reflect
+  real_ray_tracer.py:84-89                             image-space propagate
+
+Input is the lowered lens (optiland_pr_amd._abi structured arrays: the same bytes the
+GPU reads). Pinned against the reference's own outputs by tests/test_oracle_golden.py
+(fixtures made by tests/golden/gen_golden.py from /root/reference).
+"""
+
+from __future__ import annotations
+
+import warnings
+
+import numpy as np
+
+# layout constants (data format shared with the product; no compute is imported)
+from optiland_pr_amd import _abi
+
+
+class ZernikeRangeError(ValueError):
+    pass
+
+
+# --------------------------------------------------------------------------------------
+# rays
+# --------------------------------------------------------------------------------------
+class Rays:
+    """SoA ray state (real_rays.py:46-88)."""
+
+    __slots__ = ("x", "y", "z", "L", "M", "N", "i", "opd")
+
+    def __init__(self, x, y, z, L, M, N, i, opd=None):
+        self.x, self.y, self.z = (np.array(a, dtype=np.float64) for a in (x, y, z))
+        self.L, self.M, self.N = (np.array(a, dtype=np.float64) for a in (L, M, N))
+        self.i = np.array(i, dtype=np.float64)
+        self.opd = np.zeros_like(self.x) if opd is None else np.array(opd, dtype=np.float64)
+
+    def copy(self):
+        return Rays(self.x, self.y, self.z, self.L, self.M, self.N, self.i, self.opd)
+
+    def take(self, sl):
+        return Rays(*(getattr(self, a)[sl] for a in _abi.RAY_FIELDS))
+
+    def as_dict(self):
+        return {a: getattr(self, a) for a in _abi.RAY_FIELDS}
+
+
+def generate_rays(seg, px, py):
+    """ray_generator.py:49-106 with AngleField.get_ray_origins field_types.py:139-181.
+
+    seg: one _abi.SEGMENT record (host scalars EPD, EPL, vx, vy, x_off, y_off, z0)."""
+    epd, epl = float(seg["epd"]), float(seg["epl"])
+    vx, vy = float(seg["vx"]), float(seg["vy"])
+    if int(seg["mode"]) == _abi.GEN_INFINITE:
+        x0 = px * epd / 2 * vx + float(seg["x_off"])  # field_types.py:166
+        y0 = py * epd / 2 * vy + float(seg["y_off"])  # field_types.py:167
+    else:
+        x0 = np.full_like(px, float(seg["x_off"]))  # field_types.py:173-178
+        y0 = np.full_like(px, float(seg["y_off"]))
+    z0 = np.full_like(px, float(seg["z0"]))
+    x1 = px * epd * vx / 2  # ray_generator.py:76
+    y1 = py * epd * vy / 2  # ray_generator.py:77
+    z1 = np.full_like(px, epl)
+    mag = np.sqrt((x1 - x0) ** 2 + (y1 - y0) ** 2 + (z1 - z0) ** 2)  # :80
+    is_zero = mag < 1e-9
+    mag = np.where(is_zero, 1.0, mag)
+    L = np.where(is_zero, 0.0, (x1 - x0) / mag)
+    M = np.where(is_zero, 0.0, (y1 - y0) / mag)
+    N = np.where(is_zero, 1.0, (z1 - z0) / mag)
+    return Rays(x0, y0, z0, L, M, N, np.ones_like(px))
+
+
+# --------------------------------------------------------------------------------------
+# coordinate systems
+# --------------------------------------------------------------------------------------
+def apply_cs(r: Rays, ops):
+    """Apply lowered localize/globalize ops in order (coordinate_system.py:73-107)."""
+    for op in ops:
+        k = int(op["kind"])
+        p = op["p"]
+        if k == _abi.CS_TRANSLATE:  # rays/base.py:39-42
+            r.x = r.x + p[0]
+            r.y = r.y + p[1]
+            r.z = r.z + p[2]
+        elif k == _abi.CS_ROT_X:  # real_rays.py:96-102
+            c, s = p[0], p[1]
+            r.y, r.z, r.M, r.N = (r.y * c - r.z * s, r.y * s + r.z * c,
+                                  r.M * c - r.N * s, r.M * s + r.N * c)
+        elif k == _abi.CS_ROT_Y:  # real_rays.py:110-116
+            c, s = p[0], p[1]
+            r.x, r.z, r.L, r.N = (r.x * c + r.z * s, -r.x * s + r.z * c,
+                                  r.L * c + r.N * s, -r.L * s + r.N * c)
+        elif k == _abi.CS_ROT_Z:  # real_rays.py:124-130
+            c, s = p[0], p[1]
+            r.x, r.y, r.L, r.M = (r.x * c - r.y * s, r.x * s + r.y * c,
+                                  r.L * c - r.M * s, r.L * s + r.M * c)
+        else:
+            raise ValueError(f"bad cs op {k}")
+
+
+# --------------------------------------------------------------------------------------
+# geometries
+# --------------------------------------------------------------------------------------
+def distance_plane(r: Rays):
+    with warnings.catch_warnings():  # plane.py:73-75
+        warnings.simplefilter("ignore")
+        return -r.z / r.N
+
+
+def distance_conic(r: Rays, R, k, radius_inf):
+    """standard.py:89-140."""
+    if radius_inf:
+        N_safe = np.where(np.abs(r.N) > 1e-14, r.N, 1e-14)
+        return -r.z / N_safe
+    a = k * r.N**2 + r.L**2 + r.M**2 + r.N**2
+    b = 2 * k * r.N * r.z + 2 * r.L * r.x + 2 * r.M * r.y - 2 * r.N * R + 2 * r.N * r.z
+    c = k * r.z**2 - 2 * R * r.z + r.x**2 + r.y**2 + r.z**2
+    d = b**2 - 4 * a * c
+    with warnings.catch_warnings(), np.errstate(all="ignore"):
+        warnings.simplefilter("ignore")
+        t1 = (-b + np.sqrt(d)) / (2 * a)
+        t2 = (-b - np.sqrt(d)) / (2 * a)
+        z1 = r.z + t1 * r.N
+        z2 = r.z + t2 * r.N
+        t = np.where(np.abs(z1) <= np.abs(z2), t1, t2)
+        t = np.where(a == 0, -c / b, t)
+    return t
+
+
+def normal_conic(x, y, R, k):
+    """standard.py:154-167."""
+    r2 = x**2 + y**2
+    denom = R * np.sqrt(1 - (1 + k) * r2 / R**2)
+    dfdx = x / denom
+    dfdy = y / denom
+    dfdz = -1
+    mag = np.sqrt(dfdx**2 + dfdy**2 + dfdz**2)
+    return dfdx / mag, dfdy / mag, dfdz / mag
+
+
+def sag_even(x, y, R, k, C):
+    """even_asphere.py:82-98."""
+    r2 = x**2 + y**2
+    z = r2 / (R * (1 + np.sqrt(1 - (1 + k) * r2 / R**2)))
+    for i, Ci in enumerate(C):
+        z = z + Ci * r2 ** (i + 1)
+    return z
+
+
+def normal_even(x, y, R, k, C):
+    """even_asphere.py:100-129."""
+    r2 = x**2 + y**2
+    denom = R * np.sqrt(1 - (1 + k) * r2 / R**2)
+    dfdx = x / denom
+    dfdy = y / denom
+    for i, Ci in enumerate(C):
+        dfdx = dfdx + 2 * (i + 1) * x * Ci * r2**i
+        dfdy = dfdy + 2 * (i + 1) * y * Ci * r2**i
+    mag = np.sqrt(dfdx**2 + dfdy**2 + 1)
+    return dfdx / mag, dfdy / mag, -1 / mag
+
+
+def sag_odd(x, y, R, k, C):
+    """odd_asphere.py:73-89."""
+    r2 = np.array(x**2 + y**2)
+    r = np.sqrt(r2)
+    z = r2 / (R * (1 + np.sqrt(1 - (1 + k) * r2 / R**2)))
+    for i, Ci in enumerate(C):
+        z = z + Ci * r ** (i + 1)
+    return z
+
+
+def normal_odd(x, y, R, k, C):
+    """odd_asphere.py:91-130 (non-finite per-term slopes zeroed)."""
+    r2 = x**2 + y**2
+    r = np.sqrt(r2)
+    denom = R * np.sqrt(1 - (1 + k) * r2 / R**2)
+    dfdx = x / denom
+    dfdy = y / denom
+    with warnings.catch_warnings(), np.errstate(all="ignore"):
+        warnings.simplefilter("ignore")
+        for i, Ci in enumerate(C):
+            x_term = (i + 1) * x * Ci * r ** (i - 1)
+            y_term = (i + 1) * y * Ci * r ** (i - 1)
+            x_term[~np.isfinite(x_term)] = 0
+            y_term[~np.isfinite(y_term)] = 0
+            dfdx = dfdx + x_term
+            dfdy = dfdy + y_term
+    mag = np.sqrt(dfdx**2 + dfdy**2 + 1)
+    return dfdx / mag, dfdy / mag, -1 / mag
+
+
+def _radial(coef, term, r):
+    """zernike/base.py:228-253: sum_k a_k r^(n-2k), a_k precomputed on the host."""
+    n = int(term["n"])
+    off, nr = int(term["rad_off"]), int(term["n_rad"])
+    value = np.zeros_like(r)
+    for kk in range(nr):
+        value = value + coef[off + kk] * (r ** np.array(n - 2 * kk))
+    return value
+
+
+def _radial_derivative(coef, term, r):
+    """zernike/base.py:272-299: sum_k d_k r^(n-2k-1) (d_k has (-1)^k (n-k)!/.. * (n-2k))."""
+    n = int(term["n"])
+    off, nr = int(term["rad_off"]), int(term["n_rad"])
+    value = np.zeros_like(r)
+    for kk in range(nr):
+        if n - 2 * kk < 0:
+            continue
+        power_term = r ** np.array(n - 2 * kk - 1) if (n - 2 * kk - 1) >= 0 else 0
+        value = value + coef[off + nr + kk] * power_term
+    return value
+
+
+def sag_zernike(x, y, R, k, terms, coef, norm_radius):
+    """zernike.py:133-161 (standard/noll/fringe differ only in (n,m) order and norm)."""
+    x_norm = x / norm_radius
+    y_norm = y / norm_radius
+    if np.any(np.abs(x_norm) > 1) or np.any(np.abs(y_norm) > 1):  # zernike.py:234-246
+        raise ZernikeRangeError(
+            "Zernike coordinates must be normalized to [-1, 1]. Consider updating the "
+            "normalization radius to 1.1x the surface aperture."
+        )
+    rho = np.sqrt(x_norm**2 + y_norm**2)
+    phi = np.arctan2(y_norm, x_norm)
+    r2 = x**2 + y**2
+    z = r2 / (R * (1 + np.sqrt(1 - (1 + k) * r2 / R**2)))
+    # BaseZernike.poly: python sum() of terms, starting at int 0 (base.py:87-101)
+    total = 0
+    for t in terms:
+        m = int(t["m"])
+        az = np.cos(np.array(m) * phi) if m >= 0 else np.sin(np.abs(np.array(m)) * phi)
+        total = total + float(t["c"]) * float(t["norm"]) * _radial(coef, t, rho) * az
+    z += total
+    return z
+
+
+def normal_zernike(x, y, R, k, terms, coef, norm_radius):
+    """zernike.py:163-231 (the normal omits the normalisation constant: reference quirk)."""
+    r2 = x**2 + y**2
+    denominator = R * np.sqrt(1 - (1 + k) * r2 / R**2)
+    dzdx = x / denominator
+    dzdy = y / denominator
+    eps = 1e-14
+    x_norm = x / norm_radius
+    y_norm = y / norm_radius
+    rho = np.sqrt(x_norm**2 + y_norm**2)
+    phi = np.arctan2(y_norm, x_norm)
+    if np.all(rho == 0):
+        drho_dx = np.zeros_like(x)
+        drho_dy = np.zeros_like(y)
+    else:
+        drho_dx = (x / (norm_radius**2)) / (rho + eps)
+        drho_dy = (y / (norm_radius**2)) / (rho + eps)
+    dphi_dx = -(y_norm) / (rho**2 + eps) * (1.0 / norm_radius)
+    dphi_dy = +(x_norm) / (rho**2 + eps) * (1.0 / norm_radius)
+    for t in terms:
+        c = float(t["c"])
+        if c == 0:
+            continue
+        m = int(t["m"])
+        rt = _radial(coef, t, rho)
+        rd = _radial_derivative(coef, t, rho)
+        if m == 0:  # base.py:128-137
+            dr, dphi = rd, 0.0
+        elif m > 0:
+            dr = rd * np.cos(m * phi)
+            dphi = -m * rt * np.sin(m * phi)
+        else:
+            dr = rd * np.sin(abs(m) * phi)
+            dphi = abs(m) * rt * np.cos(abs(m) * phi)
+        dzdx += c * (dr * drho_dx + dphi * dphi_dx)
+        dzdy += c * (dr * drho_dy + dphi * dphi_dy)
+    nx = +dzdx
+    ny = +dzdy
+    norm = np.sqrt(nx**2 + ny**2 + 1)
+    norm = np.where(norm < eps, 1.0, norm)
+    return nx / norm, ny / norm, -np.ones_like(x) / norm
+
+
+def _geometry_fns(table, s):
+    g = int(s["geometry"])
+    R, k = float(s["radius"]), float(s["conic"])
+    off, nc = int(s["coef_off"]), int(s["n_coef"])
+    if g == _abi.GEOM_EVEN_ASPHERE:
+        C = [float(c) for c in table.coef[off:off + nc]]
+        return (lambda x, y: sag_even(x, y, R, k, C)), (lambda x, y: normal_even(x, y, R, k, C))
+    if g == _abi.GEOM_ODD_ASPHERE:
+        C = [float(c) for c in table.coef[off:off + nc]]
+        return (lambda x, y: sag_odd(x, y, R, k, C)), (lambda x, y: normal_odd(x, y, R, k, C))
+    if g == _abi.GEOM_ZERNIKE:
+        terms = table.zern[off:off + nc]
+        nr = float(s["norm_radius"])
+        return ((lambda x, y: sag_zernike(x, y, R, k, terms, table.coef, nr)),
+                (lambda x, y: normal_zernike(x, y, R, k, terms, table.coef, nr)))
+    raise ValueError(g)
+
+
+def distance_newton(r: Rays, table, s, sched=None):
+    """newton_raphson.py:119-168. Returns (t, updates). The stop test is GLOBAL over all
+    rays of this trace call: max(|f|) < tol (NaN never passes). If sched is given,
+    exactly that many updates are made instead."""
+    sag, normal = _geometry_fns(table, s)
+    t = distance_conic(r, float(s["radius"]), float(s["conic"]),
+                       bool(int(s["flags"]) & _abi.SURF_RADIUS_INF))
+    tol, max_iter = float(s["tol"]), int(s["max_iter"])
+    updates = 0
+    for it in range(max_iter):
+        if sched is not None and it >= sched:
+            break
+        x_int = r.x + t * r.L
+        y_int = r.y + t * r.M
+        z_int = r.z + t * r.N
+        f_t = sag(x_int, y_int) - z_int
+        if sched is None and np.max(np.abs(f_t)) < tol:
+            break
+        nx, ny, nz = normal(x_int, y_int)
+        nz_safe = np.where(np.abs(nz) > 1e-14, nz, 1e-14)
+        fx = -nx / nz_safe
+        fy = -ny / nz_safe
+        df_dt = fx * r.L + fy * r.M - r.N
+        safe_df_dt = np.where(np.abs(df_dt) > 1e-14, df_dt, 1e-14)
+        t = t - f_t / safe_df_dt
+        updates += 1
+    return t, updates
+
+
+def surface_normal(r: Rays, table, s):
+    g = int(s["geometry"])
+    if g == _abi.GEOM_PLANE:  # plane.py:79-98
+        return np.zeros_like(r.x), np.zeros_like(r.x), np.ones_like(r.x)
+    if g == _abi.GEOM_STANDARD:
+        return normal_conic(r.x, r.y, float(s["radius"]), float(s["conic"]))
+    return _geometry_fns(table, s)[1](r.x, r.y)
+
+
+# --------------------------------------------------------------------------------------
+# propagation / interaction
+# --------------------------------------------------------------------------------------
+def propagate(r: Rays, t, alpha):
+    """homogeneous.py:30-57; alpha = 4*pi*k/w precomputed (k>0 <=> alpha>0)."""
+    r.x = r.x + t * r.L
+    r.y = r.y + t * r.M
+    r.z = r.z + t * r.N
+    if alpha > 0:
+        r.i = r.i * np.exp(-alpha * t * 1e3)
+
+
+def _align(r: Rays, nx, ny, nz):
+    """real_rays.py:511-547."""
+    dot = r.L * nx + r.M * ny + r.N * nz
+    sgn = np.sign(dot)
+    return nx * sgn, ny * sgn, nz * sgn, np.abs(dot)
+
+
+def refract(r: Rays, nx, ny, nz, n1, n2):
+    """real_rays.py:141-163."""
+    u = n1 / n2
+    nx, ny, nz, dot = _align(r, nx, ny, nz)
+    with np.errstate(invalid="ignore"):
+        root = np.sqrt(1 - u**2 * (1 - dot**2))
+    L0, M0, N0 = r.L, r.M, r.N
+    r.L = u * L0 + nx * root - u * nx * dot
+    r.M = u * M0 + ny * root - u * ny * dot
+    r.N = u * N0 + nz * root - u * nz * dot
+
+
+def reflect(r: Rays, nx, ny, nz):
+    """real_rays.py:165-181."""
+    nx, ny, nz, dot = _align(r, nx, ny, nz)
+    r.L = r.L - 2 * dot * nx
+    r.M = r.M - 2 * dot * ny
+    r.N = r.N - 2 * dot * nz
+
+
+# --------------------------------------------------------------------------------------
+# the trace
+# --------------------------------------------------------------------------------------
+class TraceResult:
+    def __init__(self, rays, records, newton_updates):
+        self.rays = rays
+        self.records = records  # {surface index (traced, 0-based): Rays}
+        self.newton_updates = newton_updates  # {surface index: updates}
+
+
+def trace_segment(table, rays: Rays, lam: int, record=False, sched=None, start=0):
+    """One reference trace call: SurfaceGroup.trace (surface_group.py:232-244) over the
+    traced surfaces, then the image-space propagate (real_ray_tracer.py:84-89).
+    `rays` is modified in place (the reference mutates RealRays)."""
+    r = rays
+    records = {}
+    updates = {}
+    n_tab = table.n_tab[lam]
+    a_tab = table.alpha_tab[lam]
+    for si in range(start, len(table.surfaces)):
+        s = table.surfaces[si]
+        g = int(s["geometry"])
+        flags = int(s["flags"])
+        apply_cs(r, table.cs_ops[int(s["cs_loc_off"]):int(s["cs_loc_off"]) + int(s["n_cs_loc"])])
+        if g == _abi.GEOM_PLANE:
+            t = distance_plane(r)
+        elif g == _abi.GEOM_STANDARD:
+            t = distance_conic(r, float(s["radius"]), float(s["conic"]),
+                               bool(flags & _abi.SURF_RADIUS_INF))
+        else:
+            t, updates[si] = distance_newton(
+                r, table, s, None if sched is None else sched.get(si))
+        mp, mq = int(s["mat_pre"]), int(s["mat_post"])
+        propagate(r, t, float(a_tab[mp]))
+        r.opd = r.opd + np.abs(t * n_tab[mp])  # standard_surface.py:218
+        if flags & _abi.SURF_APERTURE:  # radial.py:50-63 + real_rays.py:132-139
+            radius2 = r.x**2 + r.y**2
+            inside = (radius2 <= float(s["ap_rmax2"])) & (radius2 >= float(s["ap_rmin2"]))
+            r.i = np.where(~inside, np.zeros_like(r.i), r.i)
+        nx, ny, nz = surface_normal(r, table, s)
+        if flags & _abi.SURF_REFLECTIVE:
+            reflect(r, nx, ny, nz)
+        else:
+            refract(r, nx, ny, nz, n_tab[mp], n_tab[mq])
+        apply_cs(r, table.cs_ops[int(s["cs_glob_off"]):int(s["cs_glob_off"]) + int(s["n_cs_glob"])])
+        if record:
+            records[si] = r.copy()
+    if table.final_mat >= 0:
+        # real_ray_tracer.py:84-89 always propagates (by 0 for the samples), and applies
+        # absorption only when k>0 of the image-space material.
+        propagate(r, table.final_thickness, float(a_tab[table.final_mat]))
+    return TraceResult(r, records, updates)
+
+
+def trace_batch(table, rays: Rays, batch_lambda, seg_len, record=False):
+    """Trace a batch of consecutive segments, each one reference trace call."""
+    n = rays.x.size
+    out = {a: np.empty(n) for a in _abi.RAY_FIELDS}
+    ups = []
+    recs = []
+    nseg = max(1, len(batch_lambda))
+    for sg in range(nseg):
+        sl = slice(sg * seg_len, min(n, (sg + 1) * seg_len))
+        sub = rays.take(sl)
+        res = trace_segment(table, sub, int(batch_lambda[sg]) if len(batch_lambda) else 0,
+                            record=record)
+        for a in _abi.RAY_FIELDS:
+            out[a][sl] = getattr(res.rays, a)
+        ups.append(res.newton_updates)
+        recs.append(res.records)
+    return Rays(**{a: out[a] for a in ("x", "y", "z", "L", "M", "N", "i")}, opd=out["opd"]), ups, recs
