@@ -388,7 +388,8 @@ int ort_abi_version(void) { return ORT_ABI_VERSION; }
 int ort_trace_sequential(const ort_lens* lens, const ort_rays* rays_in, ort_rays* rays_out,
                          const ort_batch* batch, const ort_options* opt, double* rec,
                          ort_newton_stat* newton_stat, int32_t* status, void* stream) {
-  if (!rays_in || !rays_out) return ORT_ERR_ARG;
+  if (!rays_in || !rays_out || !batch) return ORT_ERR_ARG;
+  if (batch->n_rays == 0) return ORT_OK;
   KArgs a{};
   uint32_t feat = 0;
   int rc = fill_args(a, lens, batch, opt, rec, newton_stat, status, feat);
@@ -404,7 +405,9 @@ int ort_trace_pupil(const ort_lens* lens, const double* px, const double* py,
                     ort_rays* rays_out, const ort_batch* batch, const ort_options* opt,
                     double* rec, ort_newton_stat* newton_stat, int32_t* status,
                     void* stream) {
-  if (!px || !py || !rays_out || !batch || !batch->seg) return ORT_ERR_ARG;
+  if (!rays_out || !batch) return ORT_ERR_ARG;
+  if (batch->n_rays == 0) return ORT_OK;
+  if (!px || !py || !batch->seg) return ORT_ERR_ARG;
   KArgs a{};
   uint32_t feat = 0;
   int rc = fill_args(a, lens, batch, opt, rec, newton_stat, status, feat);
@@ -420,8 +423,9 @@ int ort_trace_pupil(const ort_lens* lens, const double* px, const double* py,
 
 int ort_generate_rays(const double* px, const double* py, ort_rays* rays_out,
                       const ort_batch* batch, void* stream) {
-  if (!px || !py || !rays_out || !batch || !batch->seg || batch->seg_len < 1)
-    return ORT_ERR_ARG;
+  if (!rays_out || !batch) return ORT_ERR_ARG;
+  if (batch->n_rays == 0) return ORT_OK;
+  if (!px || !py || !batch->seg || batch->seg_len < 1) return ORT_ERR_ARG;
   KArgs a{};
   a.px = px;
   a.py = py;

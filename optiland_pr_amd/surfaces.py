@@ -25,6 +25,15 @@ from .geometries import (
 from .materials import BaseMaterial, IdealMaterial, configure_material
 
 
+def _torch_or_none():
+    try:
+        import torch
+
+        return torch
+    except ImportError:  # pragma: no cover
+        return None
+
+
 class RadialAperture:
     """physical_apertures/radial.py:24-90: clip (i = 0) outside r_min <= r <= r_max."""
 
@@ -164,12 +173,12 @@ class SurfaceGroup:
 
     def _stack(self, attr):
         vals = [getattr(s, attr) for s in self.surfaces]
-        if any(hasattr(v, "device") for v in vals):
-            import torch
-
-            n = max(int(v.numel()) if hasattr(v, "numel") else len(v) for v in vals)
-            dev = next(v.device for v in vals if hasattr(v, "device"))
-            rows = [v if hasattr(v, "device") and v.numel() == n
+        torch = _torch_or_none()
+        if torch is not None and any(torch.is_tensor(v) for v in vals):
+            n = max(int(v.numel()) if torch.is_tensor(v) else len(v) for v in vals)
+            dev = next(v.device for v in vals if torch.is_tensor(v))
+            # surfaces without a record (only the image surface is recorded by default)
+            rows = [v if torch.is_tensor(v) and v.numel() == n
                     else torch.full((n,), float("nan"), dtype=torch.float64, device=dev)
                     for v in vals]
             return torch.stack(rows)

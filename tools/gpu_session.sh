@@ -1,0 +1,30 @@
+#!/bin/bash
+# One GPU-box session: parity tests, smoke, bench (+ optional rocprof). Each GPU step has
+# its own time limit; a crash / abort / timeout ends the session (test FAILURES do not).
+# usage: bash tools/gpu_session.sh [tests|smoke|bench|prof|pmc]...
+set -u
+cd "$(dirname "$0")/.."
+mkdir -p gpurun_out
+export PYTHONDONTWRITEBYTECODE=1
+run() {  # run <name> <seconds> <cmd...>
+  local name=$1 secs=$2; shift 2
+  echo "== $name: $*" | tee -a gpurun_out/session.log
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc" | tee -a gpurun_out/session.log
+  tail -5 "gpurun_out/$name.log" | tee -a gpurun_out/session.log
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "abort session (rc=$rc)"; exit $rc; fi
+  return 0
+}
+for step in "$@"; do
+  case $step in
+    tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -x -rf ;;
+    testsall) run pytest_gpu 900 python -m pytest tests -m gpu -q -rf ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 600 python bench.py ;;
+    benchq) run bench 600 python bench.py --steps 20 --warmup 3 ;;
+    prof) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
+          run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --no-cpu --steps 20 --warmup 3 ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
