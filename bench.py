@@ -78,7 +78,7 @@ def main():
     from optiland_pr_amd import _native
     from optiland_pr_amd.distribution import RandomDistribution
     from optiland_pr_amd.lowering import segment_params
-    from optiland_pr_amd.raytrace import RealRays, lens_for, trace_pupil
+    from optiland_pr_amd.raytrace import RealRays, lens_for, trace_pupil, upload_segments
     from optiland_pr_amd.samples import DoubleGauss
 
     _native.load()
@@ -92,10 +92,11 @@ def main():
     px = torch.as_tensor(np.ascontiguousarray(d.x), device=dev)
     py = torch.as_tensor(np.ascontiguousarray(d.y), device=dev)
     seg = np.stack([segment_params(lens, Hx, Hy, 0)])
+    seg_dev = upload_segments(seg, dev)
     out = RealRays.empty(R, wl, device=dev)
 
     def step():
-        trace_pupil(dl, seg, px, py, out, R, R, R)
+        trace_pupil(dl, seg_dev, px, py, out, R, R, R)
 
     for _ in range(args.warmup):
         step()
@@ -124,8 +125,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    units = world * R * S  # ray-surface intersections processed by all ranks
-    value = units / elapsed
+    units = world * R * S  # ray-surface intersections per step, all ranks
+    value = units * args.steps / elapsed
     ms_per_step = elapsed / args.steps * 1e3
 
     if rank == 0:

@@ -243,14 +243,20 @@ def _raise_status(status):
         raise ZernikeRangeError(_ZERNIKE_MSG)
 
 
-def trace_pupil(dlens: DeviceLens, segments: np.ndarray, px, py, out: RealRays, n_rays,
+def upload_segments(segments: np.ndarray, device):
+    """Copy ort_segment descriptors to HBM once (reusable across launches)."""
+    return _to_device_bytes(np.asarray(segments, dtype=_abi.SEGMENT), device)
+
+
+def trace_pupil(dlens: DeviceLens, segments, px, py, out: RealRays, n_rays,
                 seg_len, group_len, pupil_per_ray=False, keys=(), rec=None,
                 newton_mode="reference", start_surface=0):
-    """Generate + trace in one launch (ort_trace_pupil)."""
+    """Generate + trace in one launch (ort_trace_pupil). `segments` is a host SEGMENT array
+    or the device tensor returned by upload_segments (no per-call copy)."""
     lib = _native.load()
-    dev = dlens.device
-    seg_dev = _to_device_bytes(segments, dev)
-    batch = _native.ort_batch(n_rays, seg_len, group_len, len(segments), int(pupil_per_ray),
+    seg_dev = segments if torch.is_tensor(segments) else upload_segments(segments, dlens.device)
+    n_seg = seg_dev.numel() // _abi.SEGMENT.itemsize
+    batch = _native.ort_batch(n_rays, seg_len, group_len, n_seg, int(pupil_per_ray),
                               seg_dev.data_ptr())
     out_c = out.c_struct()
 

@@ -24,7 +24,12 @@ for step in "$@"; do
     bench) run bench 600 python bench.py ;;
     benchq) run bench 600 python bench.py --steps 20 --warmup 3 ;;
     prof) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
-          run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --no-cpu --steps 20 --warmup 3 ;;
+          run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --no-cpu --steps 20 --warmup 3 ;;
+    pmc) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
+         run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --no-cpu --steps 10 --warmup 2
+         run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --no-cpu --steps 10 --warmup 2
+         run pmc_valu 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_INSTS_SALU GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d gpurun_out/pmc_valu -o run -- python3 bench.py --no-cpu --steps 10 --warmup 2 ;;
+    counters) run counters 120 rocprofv3 -L ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
