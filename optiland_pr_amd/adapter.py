@@ -1,0 +1,222 @@
+"""Drop-in adapter for the reference package (Optiland, `import optiland`).
+
+`install()` replaces optiland.surfaces.surface_group.SurfaceGroup.trace
+(surface_group.py:232-244) -- the seam SURVEY 8b names -- with the MI355X trace when:
+  * the rays are RealRays (not Paraxial/Polarized) held as torch float64 tensors on the
+    HIP device (be.set_backend("torch"); be.set_device("cuda"); be.set_precision("float64")),
+  * every traced surface is lowerable (plane / standard / even / odd asphere / Zernike
+    geometry, refractive-reflective interaction without coating or BSDF, radial or no
+    aperture, homogeneous propagation),
+  * autograd is not requested on the ray tensors.
+Otherwise the original Python loop runs unchanged. The rays are traced IN PLACE (the
+reference mutates its RealRays) and every surface's record (_record,
+standard_surface.py:266-286) is filled from the kernel's record buffer.
+
+`lower_reference_group()` turns reference objects into the same LensTable bytes the
+native host API produces (tested equal in tests/test_adapter.py).
+"""
+
+from __future__ import annotations
+
+import numpy as np
+
+from . import _abi
+from .geometries import (
+    EvenAsphere,
+    OddAsphere,
+    Plane,
+    StandardGeometry,
+    ZernikePolynomialGeometry,
+)
+from .coordinate_system import CoordinateSystem
+from .materials import BaseMaterial
+
+_ORIGINAL = {}
+
+
+class Unsupported(Exception):
+    pass
+
+
+class _RefMaterial(BaseMaterial):
+    """Wraps a reference material: n/k come from the reference's own material code."""
+
+    def __init__(self, m):
+        self.m = m
+
+    def _calculate_n(self, w):
+        return np.asarray(_np(self.m.n(w)), dtype=np.float64) * np.ones_like(w)
+
+    def _calculate_k(self, w):
+        return np.asarray(_np(self.m.k(w)), dtype=np.float64) * np.ones_like(w)
+
+    def key(self):
+        # same dedup keys as the native materials (materials.py), so tables match
+        m = self.m
+        if type(m).__name__ == "IdealMaterial":
+            return ("ideal", _f(m.index), _f(m.absorp))
+        fn = getattr(m, "filename", None)
+        if fn:
+            import os
+
+            return ("glass", fn.split("database" + os.sep)[-1])
+        return ("ref", id(m))
+
+
+def _np(v):
+    try:
+        import torch
+
+        if torch.is_tensor(v):
+            return v.detach().cpu().numpy()
+    except ImportError:  # pragma: no cover
+        pass
+    return np.asarray(v)
+
+
+def _f(v):
+    return float(np.ravel(_np(v))[0])
+
+
+def _cs(ref_cs):
+    parent = None if ref_cs.reference_cs is None else _cs(ref_cs.reference_cs)
+    return CoordinateSystem(_f(ref_cs.x), _f(ref_cs.y), _f(ref_cs.z), _f(ref_cs.rx),
+                            _f(ref_cs.ry), _f(ref_cs.rz), reference_cs=parent)
+
+
+def _geometry(g):
+    name = type(g).__name__
+    cs = _cs(g.cs)
+    if name == "Plane":
+        return Plane(cs)
+    if name == "StandardGeometry":
+        return StandardGeometry(cs, _f(g.radius), _f(g.k))
+    if name == "EvenAsphere":
+        return EvenAsphere(cs, _f(g.radius), _f(g.k), g.tol, g.max_iter,
+                           [float(_f(c)) for c in g.coefficients])
+    if name == "OddAsphere":
+        return OddAsphere(cs, _f(g.radius), _f(g.k), g.tol, g.max_iter,
+                          [float(_f(c)) for c in g.coefficients])
+    if name == "ZernikePolynomialGeometry":
+        return ZernikePolynomialGeometry(cs, _f(g.radius), _f(g.k), g.tol, g.max_iter,
+                                         np.ravel(_np(g.coefficients)), g.zernike_type,
+                                         _f(g.norm_radius))
+    raise Unsupported(name)
+
+
+class _Surf:
+    """Duck-typed stand-in for optiland_pr_amd.surfaces.Surface during lowering."""
+
+    def __init__(self, geometry, pre, post, is_reflective, aperture, thickness):
+        self.geometry = geometry
+        self.material_pre = pre
+        self.material_post = post
+        self.is_reflective = is_reflective
+        self.aperture = aperture
+        self.thickness = thickness
+
+
+class _Group:
+    def __init__(self, surfaces):
+        self.surfaces = surfaces
+
+
+def lower_reference_group(ref_group, wavelengths, record=False):
+    """Reference SurfaceGroup -> LensTable (raises Unsupported when not lowerable)."""
+    from .lowering import lower_surface_group
+    from .surfaces import RadialAperture
+
+    mats = {}
+
+    def mat(m):
+        if id(m) not in mats:
+            mats[id(m)] = _RefMaterial(m)
+        return mats[id(m)]
+
+    surfs = []
+    for s in ref_group.surfaces[1:]:
+        im = s.interaction_model
+        if type(im).__name__ != "RefractiveReflectiveModel":
+            raise Unsupported(type(im).__name__)
+        if getattr(im, "coating", None) is not None or getattr(im, "bsdf", None) is not None:
+            raise Unsupported("coating/bsdf")
+        for m in (s.material_pre, s.material_post):
+            if type(m.propagation_model).__name__ != "HomogeneousPropagation":
+                raise Unsupported("propagation model")
+        ap = None
+        if s.aperture is not None:
+            if type(s.aperture).__name__ != "RadialAperture":
+                raise Unsupported(type(s.aperture).__name__)
+            ap = RadialAperture(_f(s.aperture.r_max), _f(s.aperture.r_min))
+        surfs.append(_Surf(_geometry(s.geometry), mat(s.material_pre), mat(s.material_post),
+                           bool(im.is_reflective), ap, _f(s.thickness)))
+    # lower_surface_group skips ObjectSurface instances; pass the traced surfaces only
+    return lower_surface_group(_Group(surfs), wavelengths, record=record)
+
+
+def install():
+    """Patch optiland's SurfaceGroup.trace (idempotent). Returns the patched class."""
+    from optiland.surfaces import surface_group as sg_mod
+
+    cls = sg_mod.SurfaceGroup
+    if "trace" in _ORIGINAL:
+        return cls
+    _ORIGINAL["trace"] = cls.trace
+
+    def trace(self, rays, skip=0):
+        try:
+            return _trace_on_mi355x(self, rays, skip)
+        except Unsupported:
+            return _ORIGINAL["trace"](self, rays, skip)
+
+    cls.trace = trace
+    return cls
+
+
+def uninstall():
+    from optiland.surfaces import surface_group as sg_mod
+
+    if "trace" in _ORIGINAL:
+        sg_mod.SurfaceGroup.trace = _ORIGINAL.pop("trace")
+
+
+def _trace_on_mi355x(group, rays, skip):
+    import torch
+
+    from .raytrace import DeviceLens, RealRays, trace_rays
+
+    if type(rays).__name__ != "RealRays":
+        raise Unsupported(type(rays).__name__)
+    x = rays.x
+    if not (torch.is_tensor(x) and x.is_cuda and x.dtype == torch.float64):
+        raise Unsupported("rays must be float64 torch tensors on the HIP device")
+    if any(getattr(rays, a).requires_grad for a in ("x", "y", "z", "L", "M", "N")):
+        raise Unsupported("autograd")
+    w = torch.unique(rays.w)
+    if w.numel() != 1:
+        raise Unsupported("several wavelengths in one call")
+    table = lower_reference_group(group, [float(w.item())], record=True)
+    table.final_mat = -1  # SurfaceGroup.trace has no image-space propagate
+    dl = DeviceLens(table, device=x.device)
+    mine = RealRays.__new__(RealRays)
+    n = x.numel()
+    for a in _abi.RAY_FIELDS:
+        setattr(mine, a, getattr(rays, a).contiguous())
+    mine.w = rays.w
+    rec = torch.empty(table.n_rec * 8 * n, dtype=torch.float64, device=x.device)
+    group.reset()
+    obj = group.surfaces[0]
+    snap = {a: getattr(mine, a).clone() for a in _abi.RAY_FIELDS}
+    trace_rays(dl, mine, mine, rec=rec, start_surface=max(int(skip) - 1, 0))
+    for a in _abi.RAY_FIELDS:
+        setattr(rays, a, getattr(mine, a))
+    view = rec.view(table.n_rec, 8, n)
+    names = ("x", "y", "z", "L", "M", "N", "intensity", "opd")
+    if skip == 0:
+        for nm, a in zip(names, _abi.RAY_FIELDS, strict=True):
+            setattr(obj, nm, snap[a])
+    for slot, si in enumerate(table.rec_surfaces):
+        s = group.surfaces[si + 1]
+        for f, nm in enumerate(names):
+            setattr(s, nm, view[slot, f])
+    return rays

@@ -1,0 +1,83 @@
+"""Host-side lens logic vs the reference's values (CPU): glass dispersion formulas,
+paraxial EPL/EPD/f2/XPL, surface positions, Zernike normalisation radii, n/k tables."""
+
+import json
+import os
+
+import numpy as np
+import pytest
+
+from optiland_pr_amd import _abi
+from optiland_pr_amd.materials import Material
+from optiland_pr_amd.samples import GOLDEN_LENSES
+from tests._cases import ALL_CASES, native_case
+from tests.conftest import REPO, load_golden
+
+
+def test_glass_formulas_match_reference():
+    db = json.load(open(os.path.join(REPO, "optiland_pr_amd", "data", "glasses.json")))
+    for key, e in db.items():
+        name, _, ref = key.partition("|")
+        m = Material(name, ref or None)
+        for w, n, k in zip(e["check_wavelength"], e["check_n"], e["check_k"], strict=True):
+            assert m.n_scalar(w) == n, (key, w)
+            assert m.k_scalar(w) == k, (key, w)
+
+
+def test_unknown_glass_raises():
+    with pytest.raises(ValueError):
+        Material("NOT-A-GLASS")
+
+
+@pytest.mark.parametrize("name", ALL_CASES)
+def test_paraxial_and_positions(name, golden_index):
+    meta = golden_index[name]
+    lens = GOLDEN_LENSES[name]()
+    g = load_golden(name)
+    assert lens.paraxial.EPL() == meta["EPL"]
+    assert lens.paraxial.EPD() == meta["EPD"]
+    assert lens.paraxial.f2() == meta["f2"]
+    assert lens.paraxial.XPL() == meta["XPL"]
+    np.testing.assert_array_equal(np.ravel(lens.surface_group.positions), g["positions"])
+    nr = [getattr(s.geometry, "norm_radius", np.nan) for s in lens.surface_group.surfaces]
+    np.testing.assert_array_equal(nr, meta["norm_radius"])
+
+
+@pytest.mark.parametrize("name", ALL_CASES)
+def test_material_tables(name, golden_index):
+    meta = golden_index[name]
+    _, table, _ = native_case(name, meta)
+    g = load_golden(name)
+    for s_idx, row in enumerate(table.surfaces):
+        for j in range(len(meta["wavelengths"])):
+            n_post = g["n_post"][j, s_idx + 1]
+            if not np.isnan(n_post):  # mirrors: material_post is material_pre
+                assert table.n_tab[j, int(row["mat_post"])] == n_post
+            k = g["k_post"][j, s_idx + 1]
+            a = table.alpha_tab[j, int(row["mat_post"])]
+            assert (a > 0) == (k > 0)
+            if k > 0:
+                assert a == 4 * np.pi * k / meta["wavelengths"][j]
+
+
+def test_field_and_pupil_validation():
+    from optiland_pr_amd.raytrace import _validate_normalized
+
+    with pytest.raises(ValueError, match="Normalized field coordinates"):
+        _validate_normalized(1.5, 0.0, "field")
+    with pytest.raises(ValueError, match="Normalized pupil coordinates"):
+        _validate_normalized(np.array([0.0, -1.01]), 0.0, "pupil")
+
+
+def test_surface_table_flags():
+    from optiland_pr_amd.lowering import lower_surface_group
+
+    lens = GOLDEN_LENSES["tma_fringe"]()
+    t = lower_surface_group(lens.surface_group, [0.587])
+    assert all(int(s["flags"]) & _abi.SURF_REFLECTIVE for s in t.surfaces[:3])
+    assert (t.surfaces["geometry"][:3] == _abi.GEOM_ZERNIKE).all()
+    assert t.zern.shape[0] == 30  # 10 terms x 3 mirrors
+    lens = GOLDEN_LENSES["cooke_aperture"]()
+    t = lower_surface_group(lens.surface_group, [0.55])
+    assert int(t.surfaces[2]["flags"]) & _abi.SURF_APERTURE
+    assert t.surfaces[2]["ap_rmax2"] == 4.5**2
