@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define ORT_ABI_VERSION 1
+#define ORT_ABI_VERSION 2
 #define ORT_MAX_SURFACES 64
 
 /* ---- geometry kinds ----------------------------------- */
@@ -45,7 +45,9 @@ enum ort_surface_flags {
   ORT_SURF_REFLECTIVE = 1u << 0, /* interaction_model.is_reflective (material "mirror") */
   ORT_SURF_RADIUS_INF = 1u << 1, /* standard.py:100-103 plane branch of a conic guess   */
   ORT_SURF_APERTURE = 1u << 2,   /* radial physical aperture: physical_apertures/radial.py */
-  ORT_SURF_RECORD = 1u << 3      /* snapshot the ray state after this surface (_record)  */
+  ORT_SURF_RECORD = 1u << 3,     /* snapshot the ray state after this surface (_record)  */
+  ORT_SURF_TRANSLATE = 1u << 4   /* the frame is a pure translation by cs_t (no rotation, */
+                                 /* no reference_cs): localize adds -cs_t, globalize +cs_t */
 };
 
 /* ---- coordinate-system op (coordinate_system.py:73-107, real_rays.py:90-130) ---- */
@@ -84,7 +86,19 @@ typedef struct ort_surface {
   int32_t cs_glob_off;
   int32_t n_cs_glob;
   int32_t rec_slot;   /* slot in the record buffer when ORT_SURF_RECORD              */
-} ort_surface; /* 96 bytes */
+  double cs_t[3];     /* vertex (x, y, z) when ORT_SURF_TRANSLATE (the op lists hold  */
+  double reserved;    /* the same translation for the general path)                   */
+} ort_surface; /* 128 bytes */
+
+/* Per (wavelength, surface) optical constants, read in the same scalar-load batch as
+ * the surface record (one round trip per surface instead of three dependent ones). */
+typedef struct ort_surface_optics {
+  double n_pre;     /* n of material_pre (standard_surface.py:218 OPD)                */
+  double u;         /* n_pre / n_post (real_rays.py:152); the same IEEE quotient the  */
+                    /* reference forms per ray                                        */
+  double alpha_pre; /* 4 pi k / lambda of material_pre, 0 when k == 0 (homogeneous.py) */
+  double reserved;
+} ort_surface_optics; /* 32 bytes */
 
 /* One Zernike term: c * norm * R_n^|m|(rho) * {cos m phi | sin |m| phi}
  * (zernike/base.py:42-68, 228-299). Radial coefficients a_k (for rho^(n-2k)) and
@@ -107,6 +121,7 @@ typedef struct ort_lens {
   const ort_zernike_term* zern;
   const double* n_tab;     /* [n_lambda][n_mat] refractive index n(lambda)          */
   const double* alpha_tab; /* [n_lambda][n_mat] 4*pi*k/lambda (0 when k == 0)       */
+  const ort_surface_optics* optics; /* [n_lambda][n_surfaces]                       */
   int32_t n_surfaces;      /* traced surfaces S (<= ORT_MAX_SURFACES)               */
   int32_t n_lambda;
   int32_t n_mat;

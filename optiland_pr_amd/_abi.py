@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import numpy as np
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 MAX_SURFACES = 64
 
 # enum ort_geometry
@@ -25,6 +25,7 @@ SURF_REFLECTIVE = 1 << 0
 SURF_RADIUS_INF = 1 << 1
 SURF_APERTURE = 1 << 2
 SURF_RECORD = 1 << 3
+SURF_TRANSLATE = 1 << 4
 
 # enum ort_cs_kind
 CS_TRANSLATE = 0
@@ -68,10 +69,17 @@ SURFACE = np.dtype(
         ("cs_glob_off", "<i4"),
         ("n_cs_glob", "<i4"),
         ("rec_slot", "<i4"),
+        ("cs_t", "<f8", (3,)),
+        ("reserved", "<f8"),
     ],
     align=True,
 )
-assert SURFACE.itemsize == 96
+assert SURFACE.itemsize == 128
+
+SURFACE_OPTICS = np.dtype(
+    [("n_pre", "<f8"), ("u", "<f8"), ("alpha_pre", "<f8"), ("reserved", "<f8")], align=True
+)
+assert SURFACE_OPTICS.itemsize == 32
 
 ZERNIKE_TERM = np.dtype(
     [

@@ -21,6 +21,7 @@ class ort_lens(C.Structure):
         ("zern", C.c_void_p),
         ("n_tab", C.c_void_p),
         ("alpha_tab", C.c_void_p),
+        ("optics", C.c_void_p),
         ("n_surfaces", C.c_int32),
         ("n_lambda", C.c_int32),
         ("n_mat", C.c_int32),
@@ -68,7 +69,8 @@ def load(path: str | None = None):
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = path or LIB_PATH
+    # ORT_LIB_PATH: load an alternative build (A/B timing of kernel variants)
+    p = path or os.environ.get("ORT_LIB_PATH") or LIB_PATH
     if not os.path.exists(p):
         raise NativeLibraryError(
             f"{p} is missing: build the HIP extension first "

@@ -34,6 +34,53 @@ struct Ray {
 ORT_INLINE double intensity(const Ray& r) { return r.att == 0.0 ? r.i : r.i * exp(r.att); }
 
 // ---------------------------------------------------------------------------------
+// Division by a shared divisor. gfx950 lowers an IEEE fp64 a / b to
+//   v_div_scale(b), v_rcp_f64, 2 x (fma, fma) Newton steps on the reciprocal,
+//   q0 = a * y, r = fma(-b, q0, a), v_div_fmas(r, y, q0), v_div_fixup
+// where the scale/fixup steps only act on extreme exponents, zeros, infinities and
+// NaNs. For several numerators over one divisor the reciprocal refinement is done once
+// and, inside a guarded exponent range where scale/fixup are identities, each quotient
+// is the same three operations -- bit-identical to a / b. Outside the range (and on
+// the host) it falls back to the plain division.
+// ---------------------------------------------------------------------------------
+struct SharedDiv {
+  double b, y;
+  bool ok;
+};
+
+ORT_INLINE bool div_range_ok(double v) {
+  const double av = fabs(v);
+  return av >= 0x1p-300 && av <= 0x1p300;  // false for 0, inf, NaN
+}
+
+ORT_INLINE SharedDiv shared_div(double b) {
+  SharedDiv d;
+  d.b = b;
+#if defined(__HIP_DEVICE_COMPILE__)
+  d.ok = div_range_ok(b);
+  double y = __builtin_amdgcn_rcp(b);
+  double e = fma(-b, y, 1.0);
+  y = fma(y, e, y);
+  e = fma(-b, y, 1.0);
+  y = fma(y, e, y);
+  d.y = y;
+#else
+  d.ok = false;
+  d.y = 0.0;
+#endif
+  return d;
+}
+
+ORT_INLINE double sdiv(double a, const SharedDiv& d) {
+  if (__builtin_expect(d.ok && div_range_ok(a), 1)) {
+    const double q0 = a * d.y;
+    const double r = fma(-d.b, q0, a);
+    return fma(r, d.y, q0);
+  }
+  return a / d.b;
+}
+
+// ---------------------------------------------------------------------------------
 // ray generation: rays/ray_generator.py:71-106 + fields/field_types.py:160-181
 // ---------------------------------------------------------------------------------
 ORT_INLINE Ray generate_ray(const ort_segment& s, double px, double py) {
@@ -54,9 +101,10 @@ ORT_INLINE Ray generate_ray(const ort_segment& s, double px, double py) {
   double mag = sqrt(dx * dx + dy * dy + dz * dz);  // :80
   const bool is_zero = mag < 1e-9;                  // :82
   mag = is_zero ? 1.0 : mag;
-  r.L = is_zero ? 0.0 : dx / mag;
-  r.M = is_zero ? 0.0 : dy / mag;
-  r.N = is_zero ? 1.0 : dz / mag;
+  const SharedDiv dm = shared_div(mag);
+  r.L = is_zero ? 0.0 : sdiv(dx, dm);
+  r.M = is_zero ? 0.0 : sdiv(dy, dm);
+  r.N = is_zero ? 1.0 : sdiv(dz, dm);
   r.x = x0;
   r.y = y0;
   r.z = z0;
@@ -109,17 +157,26 @@ ORT_INLINE double distance_conic(const Ray& r, double R, double k, bool radius_i
     return -r.z / Ns;
   }
   const double N2 = r.N * r.N;
-  const double a = k * N2 + r.L * r.L + r.M * r.M + N2;
-  // 2*k*N*z + 2*L*x + 2*M*y - 2*N*R + 2*N*z: every "2*" is an exact scaling
-  const double b = 2.0 * k * r.N * r.z + 2.0 * r.L * r.x + 2.0 * r.M * r.y -
-                   2.0 * r.N * R + 2.0 * r.N * r.z;
   const double z2 = r.z * r.z;
-  const double c = k * z2 - 2.0 * R * r.z + r.x * r.x + r.y * r.y + z2;
+  double a, b, c;
+  // 2*k*N*z + 2*L*x + 2*M*y - 2*N*R + 2*N*z: every "2*" is an exact scaling
+  if (k == 0.0) {
+    // sphere: k*N**2 = 0, 2*k*N*z = 0, k*z**2 = 0 and 0 + v == v, so the conic terms
+    // drop out without changing a bit (for finite rays)
+    a = r.L * r.L + r.M * r.M + N2;
+    b = 2.0 * r.L * r.x + 2.0 * r.M * r.y - 2.0 * r.N * R + 2.0 * r.N * r.z;
+    c = 0.0 - 2.0 * R * r.z + r.x * r.x + r.y * r.y + z2;
+  } else {
+    a = k * N2 + r.L * r.L + r.M * r.M + N2;
+    b = 2.0 * k * r.N * r.z + 2.0 * r.L * r.x + 2.0 * r.M * r.y - 2.0 * r.N * R +
+        2.0 * r.N * r.z;
+    c = k * z2 - 2.0 * R * r.z + r.x * r.x + r.y * r.y + z2;
+  }
   const double d = b * b - 4.0 * a * c;
   const double sd = sqrt(d);
-  const double a2 = 2.0 * a;
-  const double t1 = (-b + sd) / a2;
-  const double t2 = (-b - sd) / a2;
+  const SharedDiv a2 = shared_div(2.0 * a);
+  const double t1 = sdiv(-b + sd, a2);
+  const double t2 = sdiv(-b - sd, a2);
   const double z1 = r.z + t1 * r.N;
   const double zz2 = r.z + t2 * r.N;
   double t = fabs(z1) <= fabs(zz2) ? t1 : t2;
@@ -132,12 +189,14 @@ ORT_INLINE void normal_conic(double x, double y, double R, double k, double& nx,
                              double& nz) {
   const double r2 = x * x + y * y;
   const double denom = R * sqrt(1.0 - (1.0 + k) * r2 / (R * R));
-  const double dfdx = x / denom;
-  const double dfdy = y / denom;
+  const SharedDiv dd = shared_div(denom);
+  const double dfdx = sdiv(x, dd);
+  const double dfdy = sdiv(y, dd);
   const double mag = sqrt(dfdx * dfdx + dfdy * dfdy + 1.0);  // dfdz**2 = (-1)**2 = 1
-  nx = dfdx / mag;
-  ny = dfdy / mag;
-  nz = -1.0 / mag;
+  const SharedDiv dm = shared_div(mag);
+  nx = sdiv(dfdx, dm);
+  ny = sdiv(dfdy, dm);
+  nz = sdiv(-1.0, dm);
 }
 
 // base conic sag, standard.py:73-87 (shared by every Newton geometry)
@@ -464,9 +523,9 @@ ORT_INLINE double align_normal(const Ray& r, double& nx, double& ny, double& nz)
   return fabs(dot);
 }
 
-// rays/real_rays.py:141-163
-ORT_INLINE void refract(Ray& r, double nx, double ny, double nz, double n1, double n2) {
-  const double u = n1 / n2;
+// rays/real_rays.py:141-163; u = n1 / n2 comes from the host table (the same IEEE
+// quotient the reference forms per ray)
+ORT_INLINE void refract(Ray& r, double nx, double ny, double nz, double u) {
   const double dot = align_normal(r, nx, ny, nz);
   const double root = sqrt(1.0 - u * u * (1.0 - dot * dot));
   const double L0 = r.L, M0 = r.M, N0 = r.N;
@@ -503,7 +562,7 @@ ORT_INLINE void surface_normal(const ort_surface& s, PD coef, PZ zern, const Ray
 // (standard_surface.py:215-231 minus localize/globalize)
 template <unsigned KM, class PD, class PZ>
 ORT_INLINE void finish_surface(Ray& r, const ort_surface& s, PD coef, PZ zern, double t,
-                               double n_pre, double n_post, double alpha_pre) {
+                               double n_pre, double u, double alpha_pre) {
   propagate(r, t, alpha_pre);
   add_opd(r, t, n_pre);
   if (s.flags & ORT_SURF_APERTURE) clip_radial(r, s.ap_rmax2, s.ap_rmin2);
@@ -512,7 +571,7 @@ ORT_INLINE void finish_surface(Ray& r, const ort_surface& s, PD coef, PZ zern, d
   if (s.flags & ORT_SURF_REFLECTIVE)
     reflect(r, nx, ny, nz);
   else
-    refract(r, nx, ny, nz, n_pre, n_post);
+    refract(r, nx, ny, nz, u);
 }
 
 }  // namespace ort

@@ -17,6 +17,7 @@
 // Compiled with -ffp-contract=off: see ort_core.h.
 
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 
 #include "ort_core.h"
 
@@ -57,6 +58,7 @@ struct KArgs {
   const ort_zernike_term* zern;
   const double* n_tab;
   const double* alpha_tab;
+  const ort_surface_optics* optics;
   int32_t n_surf;
   int32_t n_lambda;
   int32_t n_mat;
@@ -98,6 +100,35 @@ __device__ inline int wave_max_i32(int v) {
 __device__ inline double tab(const double* t, int n_lambda, int n_mat, int lam, int mat) {
   if (n_lambda == 1) return cst(t)[mat];
   return t[lam * n_mat + mat];
+}
+
+// Optical constants of surface si at the ray's wavelength (same scalar-load batch as the
+// surface record when the lens is traced at one wavelength).
+__device__ inline ort_surface_optics optics_at(const KArgs& a, int lam, int si) {
+  if (a.n_lambda == 1) return cst(a.optics)[si];
+  return a.optics[lam * a.n_surf + si];
+}
+
+// localize / globalize (coordinate_system.py:73-107): pure translations inline,
+// general frames through the op list
+__device__ inline void localize(const KArgs& a, const ort_surface& s, ort::Ray& r) {
+  if (s.flags & ORT_SURF_TRANSLATE) {
+    r.x = r.x + -s.cs_t[0];
+    r.y = r.y + -s.cs_t[1];
+    r.z = r.z + -s.cs_t[2];
+    return;
+  }
+  for (int c = 0; c < s.n_cs_loc; ++c) ort::apply_cs_op(r, cst(a.cs)[s.cs_loc_off + c]);
+}
+
+__device__ inline void globalize(const KArgs& a, const ort_surface& s, ort::Ray& r) {
+  if (s.flags & ORT_SURF_TRANSLATE) {
+    r.x = r.x + s.cs_t[0];
+    r.y = r.y + s.cs_t[1];
+    r.z = r.z + s.cs_t[2];
+    return;
+  }
+  for (int c = 0; c < s.n_cs_glob; ++c) ort::apply_cs_op(r, cst(a.cs)[s.cs_glob_off + c]);
 }
 
 // Newton refinement of t at surface s for one lane (newton_raphson.py:119-168).
@@ -202,7 +233,8 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(const KArgs a) {
 
   for (int si = a.start_surface; si < a.n_surf; ++si) {
     const ort_surface s = cst(a.surf)[si];
-    for (int c = 0; c < s.n_cs_loc; ++c) ort::apply_cs_op(r, cst(a.cs)[s.cs_loc_off + c]);
+    const ort_surface_optics o = optics_at(a, lam, si);
+    localize(a, s, r);
     double t;
     if (s.geometry == ORT_GEOM_PLANE) {
       t = ort::distance_plane(r);
@@ -215,11 +247,9 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(const KArgs a) {
         t = __builtin_nan("");  // unreachable: the host sets geometry_mask
       }
     }
-    const double n_pre = tab(a.n_tab, a.n_lambda, a.n_mat, lam, s.mat_pre);
-    const double n_post = tab(a.n_tab, a.n_lambda, a.n_mat, lam, s.mat_post);
-    const double alpha = tab(a.alpha_tab, a.n_lambda, a.n_mat, lam, s.mat_pre);
+    const double n_pre = o.n_pre, u = o.u, alpha = o.alpha_pre;
     if constexpr ((FEAT & F_KM) != 0) {
-      ort::finish_surface<(FEAT & F_KM)>(r, s, cst(a.coef), cst(a.zern), t, n_pre, n_post, alpha);
+      ort::finish_surface<(FEAT & F_KM)>(r, s, cst(a.coef), cst(a.zern), t, n_pre, u, alpha);
     } else {
       // closed-form geometries only: plane / conic normal inline
       ort::propagate(r, t, alpha);
@@ -234,9 +264,9 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(const KArgs a) {
       if (s.flags & ORT_SURF_REFLECTIVE)
         ort::reflect(r, nx, ny, nz);
       else
-        ort::refract(r, nx, ny, nz, n_pre, n_post);
+        ort::refract(r, nx, ny, nz, u);
     }
-    for (int c = 0; c < s.n_cs_glob; ++c) ort::apply_cs_op(r, cst(a.cs)[s.cs_glob_off + c]);
+    globalize(a, s, r);
     if constexpr ((FEAT & F_REC) != 0) {
       if ((s.flags & ORT_SURF_RECORD) && active) {
         double* base = a.rec + (int64_t)s.rec_slot * 8 * a.n_rays + rid;
@@ -260,6 +290,86 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(const KArgs a) {
   if constexpr ((FEAT & ort::KM_ZERN) != 0) {
     if (range_error && active && a.status) atomicOr(a.status, (int)ORT_STATUS_ZERNIKE_RANGE);
   }
+  if (!active) return;
+  a.out.x[rid] = r.x;
+  a.out.y[rid] = r.y;
+  a.out.z[rid] = r.z;
+  a.out.L[rid] = r.L;
+  a.out.M[rid] = r.M;
+  a.out.N[rid] = r.N;
+  a.out.i[rid] = ort::intensity(r);
+  a.out.opd[rid] = r.opd;
+}
+
+// Closed-form lenses (planes, spheres, conics: no Newton surface) -- the DoubleGauss /
+// Cooke / ReverseTelephoto path. One ray per lane: at 52 VGPRs the kernel runs 8 waves
+// per SIMD, which hides the fp64 div/sqrt latency better than 2 or 4 rays per lane
+// (measured: 2 rays/lane 7% slower at 5 waves/SIMD, 4 rays/lane 28% slower).
+// Per surface: one batch of scalar loads (surface record + optics of this wavelength).
+template <uint32_t FEAT>
+__global__ __launch_bounds__(kBlock) void trace_closed_kernel(const KArgs a) {
+  const int64_t rid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const bool active = rid < a.n_rays;
+  const int64_t r_ld = active ? rid : 0;
+  int lam = 0;
+  ort::Ray r;
+  if constexpr ((FEAT & F_GEN) != 0) {
+    const int64_t sidx = a.n_seg == 1 ? 0 : r_ld / a.seg_len;
+    const ort_segment sg = a.n_seg == 1 ? cst(a.seg)[0] : a.seg[sidx];
+    lam = sg.lambda_idx;
+    const int64_t p = a.pupil_per_ray ? r_ld : (r_ld - sidx * a.seg_len);
+    r = ort::generate_ray(sg, a.px[p], a.py[p]);
+  } else {
+    if (a.seg) lam = a.seg[a.n_seg == 1 ? 0 : r_ld / a.seg_len].lambda_idx;
+    r.x = a.in.x[r_ld];
+    r.y = a.in.y[r_ld];
+    r.z = a.in.z[r_ld];
+    r.L = a.in.L[r_ld];
+    r.M = a.in.M[r_ld];
+    r.N = a.in.N[r_ld];
+    r.i = a.in.i[r_ld];
+    r.opd = a.in.opd[r_ld];
+    r.att = 0.0;
+  }
+  for (int si = a.start_surface; si < a.n_surf; ++si) {
+    const ort_surface s = cst(a.surf)[si];
+    const ort_surface_optics o = optics_at(a, lam, si);
+    localize(a, s, r);
+    const bool is_plane = s.geometry == ORT_GEOM_PLANE;
+    const double t = is_plane ? ort::distance_plane(r)
+                              : ort::distance_conic(r, s.radius, s.conic,
+                                                    (s.flags & ORT_SURF_RADIUS_INF) != 0);
+    ort::propagate(r, t, o.alpha_pre);
+    ort::add_opd(r, t, o.n_pre);
+    if (s.flags & ORT_SURF_APERTURE) ort::clip_radial(r, s.ap_rmax2, s.ap_rmin2);
+    double nx, ny, nz;
+    if (is_plane) {
+      nx = 0.0; ny = 0.0; nz = 1.0;
+    } else {
+      ort::normal_conic(r.x, r.y, s.radius, s.conic, nx, ny, nz);
+    }
+    if (s.flags & ORT_SURF_REFLECTIVE)
+      ort::reflect(r, nx, ny, nz);
+    else
+      ort::refract(r, nx, ny, nz, o.u);
+    globalize(a, s, r);
+    if constexpr ((FEAT & F_REC) != 0) {
+      if ((s.flags & ORT_SURF_RECORD) && active) {
+        double* b = a.rec + (int64_t)s.rec_slot * 8 * a.n_rays + rid;
+        b[0 * a.n_rays] = r.x;
+        b[1 * a.n_rays] = r.y;
+        b[2 * a.n_rays] = r.z;
+        b[3 * a.n_rays] = r.L;
+        b[4 * a.n_rays] = r.M;
+        b[5 * a.n_rays] = r.N;
+        b[6 * a.n_rays] = ort::intensity(r);
+        b[7 * a.n_rays] = r.opd;
+      }
+    }
+  }
+  if (a.final_mat >= 0)
+    ort::propagate(r, a.final_thickness,
+                   tab(a.alpha_tab, a.n_lambda, a.n_mat, lam, a.final_mat));
   if (!active) return;
   a.out.x[rid] = r.x;
   a.out.y[rid] = r.y;
@@ -317,7 +427,8 @@ int fill_args(KArgs& a, const ort_lens* lens, const ort_batch* batch, const ort_
               double* rec, ort_newton_stat* stats, int32_t* status, uint32_t& feat) {
   if (!lens || !batch || !opt) return ORT_ERR_ARG;
   if (lens->n_surfaces < 0 || lens->n_surfaces > ORT_MAX_SURFACES) return ORT_ERR_SURFACES;
-  if (lens->n_surfaces > 0 && (!lens->surfaces || !lens->n_tab || !lens->alpha_tab))
+  if (lens->n_surfaces > 0 &&
+      (!lens->surfaces || !lens->n_tab || !lens->alpha_tab || !lens->optics))
     return ORT_ERR_ARG;
   if (batch->n_rays < 0 || batch->seg_len < 1 || batch->group_len < 1) return ORT_ERR_ARG;
   if (lens->n_lambda < 1 || lens->n_mat < 1) return ORT_ERR_ARG;
@@ -328,6 +439,7 @@ int fill_args(KArgs& a, const ort_lens* lens, const ort_batch* batch, const ort_
   a.zern = lens->zern;
   a.n_tab = lens->n_tab;
   a.alpha_tab = lens->alpha_tab;
+  a.optics = lens->optics;
   a.n_surf = lens->n_surfaces;
   a.n_lambda = lens->n_lambda;
   a.n_mat = lens->n_mat;
@@ -355,9 +467,18 @@ int fill_args(KArgs& a, const ort_lens* lens, const ort_batch* batch, const ort_
   return ORT_OK;
 }
 
+// rays per lane of the closed-form kernel (ORT_RPL overrides, for A/B timing)
 int launch(const KArgs& a, uint32_t feat, hipStream_t stream) {
   if (a.n_rays == 0) return ORT_OK;
   KernelFn fn = select_kernel(feat);
+  if ((feat & F_KM) == 0) {  // closed-form lens
+    switch (feat & (F_GEN | F_REC)) {
+      case 0: fn = trace_closed_kernel<0>; break;
+      case F_GEN: fn = trace_closed_kernel<F_GEN>; break;
+      case F_REC: fn = trace_closed_kernel<F_REC>; break;
+      default: fn = trace_closed_kernel<F_GEN | F_REC>; break;
+    }
+  }
   if (!fn) return ORT_ERR_ARG;
   const int64_t blocks = (a.n_rays + kBlock - 1) / kBlock;
   if (blocks > 0x7fffffff) return ORT_ERR_ARG;

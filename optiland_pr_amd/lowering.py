@@ -47,6 +47,23 @@ class LensTable:
         return int(self.surfaces.shape[0])
 
     @property
+    def u_tab(self):
+        """[n_lambda][S] n_pre / n_post: the refraction ratio u of real_rays.py:152,
+        one IEEE division per (wavelength, surface) instead of one per ray."""
+        pre = self.n_tab[:, self.surfaces["mat_pre"]]
+        post = self.n_tab[:, self.surfaces["mat_post"]]
+        return np.ascontiguousarray(pre / post)
+
+    @property
+    def optics(self):
+        """[n_lambda][S] ort_surface_optics: n_pre, u, alpha_pre per (lambda, surface)."""
+        o = np.zeros((self.n_tab.shape[0], self.n_surfaces), dtype=_abi.SURFACE_OPTICS)
+        o["n_pre"] = self.n_tab[:, self.surfaces["mat_pre"]]
+        o["u"] = self.u_tab
+        o["alpha_pre"] = self.alpha_tab[:, self.surfaces["mat_pre"]]
+        return o
+
+    @property
     def newton_surfaces(self):
         return [i for i, s in enumerate(self.surfaces)
                 if int(s["geometry"]) in _abi.NEWTON_GEOMETRIES]
@@ -133,6 +150,13 @@ def lower_surface_group(surface_group, wavelengths, record=False, skip_object=Tr
         row["cs_glob_off"] = len(ops)
         row["n_cs_glob"] = len(glob)
         ops.extend(glob)
+        if (len(loc) == 1 and len(glob) == 1 and loc[0][0] == _abi.CS_TRANSLATE
+                and glob[0][0] == _abi.CS_TRANSLATE):
+            # pure translation: localize adds -t, globalize adds +t (exact negation)
+            t = glob[0][1]
+            if tuple(loc[0][1]) == (-t[0], -t[1], -t[2]):
+                row["flags"] = int(row["flags"]) | _abi.SURF_TRANSLATE
+                row["cs_t"] = t
 
     final = surfs[-1]
     final_mat = mat_id(final.material_post)

@@ -123,6 +123,7 @@ class DeviceLens:
         self.n_tab = torch.as_tensor(np.ascontiguousarray(table.n_tab), dtype=torch.float64, device=d)
         self.alpha_tab = torch.as_tensor(np.ascontiguousarray(table.alpha_tab),
                                          dtype=torch.float64, device=d)
+        self.optics = _to_device_bytes(table.optics, d)
         mask = 0
         for g in np.unique(table.surfaces["geometry"]):
             mask |= 1 << int(g)
@@ -130,6 +131,7 @@ class DeviceLens:
         self.c = _native.ort_lens(
             self.surfaces.data_ptr(), self.cs_ops.data_ptr(), self.coef.data_ptr(),
             self.zern.data_ptr(), self.n_tab.data_ptr(), self.alpha_tab.data_ptr(),
+            self.optics.data_ptr(),
             table.n_surfaces, len(table.wavelengths), table.n_tab.shape[1], table.final_mat,
             mask, 0, table.final_thickness)
         self.newton = table.newton_surfaces

@@ -29,7 +29,12 @@ for step in "$@"; do
          run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --no-cpu --steps 10 --warmup 2
          run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --no-cpu --steps 10 --warmup 2
          run pmc_valu 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_INSTS_SALU GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d gpurun_out/pmc_valu -o run -- python3 bench.py --no-cpu --steps 10 --warmup 2 ;;
+    pmcflops) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
+         run pmc_flops 600 rocprofv3 --pmc SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_FLOPS_FP64_TRANS SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES --kernel-trace --output-format csv -d gpurun_out/pmc_flops -o run -- python3 bench.py --no-cpu --steps 10 --warmup 2 ;;
+    pmcstall) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
+         run pmc_stall 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d gpurun_out/pmc_stall -o run -- python3 bench.py --no-cpu --steps 10 --warmup 2 ;;
     counters) run counters 120 rocprofv3 -L ;;
+    ab) run ab 900 bash tools/ab.sh $(ls optiland_pr_amd/lib/variants) ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
