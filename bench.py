@@ -136,7 +136,9 @@ def main():
         achieved_gbs = bytes_per_launch / (kern_ms * 1e-3) / 1e9
         flops = _flops_per_ray(dl.table) * R
         achieved_tf = flops / (kern_ms * 1e-3) / 1e12
-        traffic = _pmc_traffic()
+        pmc = _pmc_summary()
+        traffic = pmc.get("bytes_per_launch")
+        hw_flops = pmc.get("fp64_flops_per_launch")
         line = {
             "metric": "ray-surface intersections/sec at 1M pupil rays, 10-surf double-Gauss",
             "value": value,
@@ -165,7 +167,7 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved_gbs / (SPEC_HBM_TBPS * 1e3),
                 "traffic": traffic,
-                "kernel": "trace_kernel<F_GEN> (ort_trace_pupil)",
+                "kernel": "trace_closed_kernel<F_GEN> (ort_trace_pupil)",
                 "kernel_ms": kern_ms,
                 "algorithmic_bytes_per_launch": bytes_per_launch,
                 "note": "the fused trace is FP64-VALU bound (see roofline_fp64); HBM frac is "
@@ -178,6 +180,14 @@ def main():
                 "unit": "TFLOP/s",
                 "frac": achieved_tf / SPEC_FP64_VEC_TFLOPS,
                 "flops_per_ray": _flops_per_ray(dl.table),
+                "note": "achieved = algorithmic ops (+,-,*,/,sqrt = 1 each); the hardware "
+                        "executes IEEE / and sqrt as ~10-instruction FMA sequences",
+                "hw_counted": None if hw_flops is None else {
+                    "fp64_flops_per_launch": hw_flops,
+                    "achieved": hw_flops / (kern_ms * 1e-3) / 1e12,
+                    "frac": hw_flops / (kern_ms * 1e-3) / 1e12 / SPEC_FP64_VEC_TFLOPS,
+                    "source": "SQ_INSTS_VALU_FLOPS_FP64 x 64 (profiles/hbm_traffic.json)",
+                },
             },
             "cpu_baseline": None if args.no_cpu else _cpu_baseline(lens, dl, seg, args.cpu_rays),
         }
@@ -187,17 +197,15 @@ def main():
         dist.destroy_process_group()
 
 
-def _pmc_traffic():
-    """HBM bytes per launch from the committed rocprofv3 PMC summary, if present
-    (profiles/*hbm*.json written by tools/profile_hbm.py); else None."""
+def _pmc_summary():
+    """Per-launch HBM bytes / FP64 FLOPs of the trace kernel from the committed
+    rocprofv3 PMC summary (profiles/hbm_traffic.json, tools/profile_hbm.py); {} if absent."""
     p = os.path.join(HERE, "profiles", "hbm_traffic.json")
-    if not os.path.exists(p):
-        return None
     try:
         with open(p) as f:
-            return json.load(f).get("bytes_per_launch")
+            return json.load(f)
     except (OSError, ValueError):
-        return None
+        return {}
 
 
 def _cpu_baseline(lens, dl, seg, n_rays):

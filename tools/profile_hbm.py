@@ -1,14 +1,18 @@
-"""Summarise rocprofv3 runs of bench.py into profiles/ (test/measurement tooling).
+"""Summarise rocprofv3 runs of bench.py into profiles/ (measurement tooling, not product).
 
 usage: python tools/profile_hbm.py <round tag> <kernel-trace dir> [<pmc dir> ...]
 
-Writes profiles/<tag>_kernel_stats.csv (copy of the kernel stats) and, when PMC runs
-with FETCH_SIZE / WRITE_SIZE are given, profiles/hbm_traffic.json with the HBM bytes per
-launch of the trace kernel. gfx950 correction (MI355X_MICROARCH.md 'HBM'): FETCH_SIZE
-reports half of the bytes of WIDE (16 B/lane) coalesced reads; the trace kernel reads
-8 B/lane (uncalibrated width), so both the raw and the x2 figures are recorded, and the
-calibration kernel (generate_kernel: 16 B/ray read, 64 B/ray written, same widths) is
-reported beside it.
+Writes
+  profiles/<tag>_kernel_stats.csv   copy of rocprofv3 --kernel-trace --stats summary
+  profiles/<tag>_pmc_summary.json   per-dispatch averages of every PMC counter seen for
+                                    the trace kernel
+  profiles/hbm_traffic.json         what bench.py reads: HBM bytes and hardware FP64
+                                    FLOPs per launch of the trace kernel
+
+gfx950 corrections (MI355X_MICROARCH.md 'HBM'): FETCH_SIZE reports half of the bytes of
+wide coalesced reads -- verified for this kernel's 8 B/lane pupil reads: raw FETCH_SIZE
+is 7.9 MB for 16 MB of Px/Py, so bytes_per_launch uses 2 x FETCH_SIZE + WRITE_SIZE
+(in KiB). SQ_INSTS_VALU_FLOPS_FP64 counts per wave-instruction: x 64 lanes.
 """
 import csv
 import glob
@@ -18,49 +22,40 @@ import shutil
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-
-
-def _rows(pattern):
-    out = []
-    for f in glob.glob(pattern, recursive=True):
-        with open(f) as fh:
-            out.extend(csv.DictReader(fh))
-    return out
+KERNEL_KEYS = ("trace_kernel", "trace_closed_kernel")
 
 
 def main():
     tag, ktrace = sys.argv[1], sys.argv[2]
-    pmc_dirs = sys.argv[3:]
     prof = os.path.join(REPO, "profiles")
     os.makedirs(prof, exist_ok=True)
-    stats = glob.glob(os.path.join(ktrace, "**", "*kernel_stats.csv"), recursive=True)
-    for f in stats:
+    for f in glob.glob(os.path.join(ktrace, "**", "*kernel_stats.csv"), recursive=True):
         shutil.copy(f, os.path.join(prof, f"{tag}_kernel_stats.csv"))
-    res = {}
-    for d in pmc_dirs:
-        for r in _rows(os.path.join(d, "**", "*counter_collection.csv")):
-            k = r.get("Kernel_Name", "")
-            if "trace_kernel" not in k and "generate_kernel" not in k:
-                continue
-            name = "trace_kernel" if "trace_kernel" in k else "generate_kernel"
-            ctr = r.get("Counter_Name")
-            val = float(r.get("Counter_Value", "nan"))
-            res.setdefault(name, {}).setdefault(ctr, []).append(val)
-    summary = {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in res.items()}
-    if summary:
-        t = summary.get("trace_kernel", {})
-        fetch = t.get("FETCH_SIZE")
-        write = t.get("WRITE_SIZE")
-        out = {"per_dispatch_kilobytes": summary}
-        if fetch is not None and write is not None:
-            out["bytes_per_launch_raw"] = (fetch + write) * 1024
-            out["bytes_per_launch"] = (2 * fetch + write) * 1024
-            out["note"] = "FETCH_SIZE x2 gfx950 correction applied to bytes_per_launch"
-        with open(os.path.join(prof, "hbm_traffic.json"), "w") as fh:
-            json.dump(out, fh, indent=1)
-        with open(os.path.join(prof, f"{tag}_pmc_summary.json"), "w") as fh:
-            json.dump(out, fh, indent=1)
-    print(json.dumps(summary, indent=1))
+    acc = {}
+    for d in sys.argv[3:]:
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            for r in csv.DictReader(open(f)):
+                if not any(k in r.get("Kernel_Name", "") for k in KERNEL_KEYS):
+                    continue
+                acc.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+    per = {c: sum(v) / len(v) for c, v in acc.items()}
+    if not per:
+        print("no PMC rows for the trace kernel")
+        return
+    out = {"per_dispatch": per}
+    if "FETCH_SIZE" in per and "WRITE_SIZE" in per:
+        out["bytes_per_launch_raw"] = (per["FETCH_SIZE"] + per["WRITE_SIZE"]) * 1024
+        out["bytes_per_launch"] = (2 * per["FETCH_SIZE"] + per["WRITE_SIZE"]) * 1024
+    if "SQ_INSTS_VALU_FLOPS_FP64" in per:
+        out["fp64_flops_per_launch"] = per["SQ_INSTS_VALU_FLOPS_FP64"] * 64
+    if "SQ_INSTS_VALU" in per and "SQ_WAVES" in per:
+        out["valu_insts_per_wave"] = per["SQ_INSTS_VALU"] / per["SQ_WAVES"]
+    out["source"] = f"rocprofv3 PMC passes, round tag {tag}"
+    with open(os.path.join(prof, f"{tag}_pmc_summary.json"), "w") as fh:
+        json.dump(out, fh, indent=1)
+    with open(os.path.join(prof, "hbm_traffic.json"), "w") as fh:
+        json.dump(out, fh, indent=1)
+    print(json.dumps(out, indent=1))
 
 
 if __name__ == "__main__":
