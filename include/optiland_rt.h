@@ -233,6 +233,22 @@ int ort_trace_pupil(const ort_lens* lens, const double* px, const double* py,
                     double* rec, ort_newton_stat* newton_stat, int32_t* status,
                     void* stream);
 
+/* Backward of ort_trace_pupil w.r.t. Zernike coefficients: the vector-Jacobian product
+ *   grad[p] += sum_rays sum_f cotangent.f[ray] * d out.f[ray] / d c_p
+ * for the output fields f of rays_out (x, y, z, L, M, N, i, opd; a NULL cotangent field
+ * counts as zero). zern_param[j] maps Zernike term j of lens->zern (its coefficient
+ * lens->zern[j].c) to parameter p in [0, n_param), or < 0 for a constant term.
+ * opt must be ORT_NEWTON_SCHEDULE with the schedule the verified primal trace ran
+ * (the derivative is that of the unrolled Newton iteration, as torch autograd computes
+ * it through newton_raphson.py:137-166). grad is accumulated with device atomics: zero
+ * it first. Replaces reverse-mode torch autograd through the trace (SurfaceGroup.trace
+ * under the torch backend, driven by optimization/optimizer/torch/base.py:95-154 with
+ * variable/zernike_coeff.py:71-95 writing the coefficients). */
+int ort_trace_pupil_vjp(const ort_lens* lens, const double* px, const double* py,
+                        const ort_batch* batch, const ort_options* opt,
+                        const int32_t* zern_param, int32_t n_param,
+                        const ort_rays* cotangent, double* grad, void* stream);
+
 /* Ray generation only (ray_generator.py:28-106): fills rays_out from pupil points. */
 int ort_generate_rays(const double* px, const double* py, ort_rays* rays_out,
                       const ort_batch* batch, void* stream);

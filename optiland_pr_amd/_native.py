@@ -55,7 +55,8 @@ class ort_options(C.Structure):
     ]
 
 
-EXPORTS = ("ort_abi_version", "ort_trace_sequential", "ort_trace_pupil", "ort_generate_rays")
+EXPORTS = ("ort_abi_version", "ort_trace_sequential", "ort_trace_pupil", "ort_trace_pupil_vjp",
+           "ort_generate_rays")
 
 _lib = None
 
@@ -87,6 +88,10 @@ def load(path: str | None = None):
     lib.ort_trace_pupil.argtypes = [P(ort_lens), C.c_void_p, C.c_void_p, P(ort_rays),
                                     P(ort_batch), P(ort_options), C.c_void_p, C.c_void_p,
                                     C.c_void_p, C.c_void_p]
+    lib.ort_trace_pupil_vjp.restype = C.c_int
+    lib.ort_trace_pupil_vjp.argtypes = [P(ort_lens), C.c_void_p, C.c_void_p, P(ort_batch),
+                                        P(ort_options), C.c_void_p, C.c_int32, P(ort_rays),
+                                        C.c_void_p, C.c_void_p]
     lib.ort_generate_rays.restype = C.c_int
     lib.ort_generate_rays.argtypes = [C.c_void_p, C.c_void_p, P(ort_rays), P(ort_batch),
                                       C.c_void_p]

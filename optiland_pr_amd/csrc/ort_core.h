@@ -4,9 +4,14 @@
 // the reference's evaluation order (NumPy evaluates each expression left to right with
 // one IEEE rounding per operation; this file is compiled with -ffp-contract=off so the
 // compiler may not fuse a*b+c). The wave-level control (Newton convergence votes,
-// segment lookup, record stores) lives in ort_trace.hip; this header has no
-// intrinsics so it can also be compiled for the host by the test-only checker
-// (tests/hostcheck/).
+// segment lookup, record stores) lives in ort_trace.hip.
+//
+// The ray-dependent quantities are templated on a scalar type T: `double` for the
+// trace itself, and `Dual<P>` (value + P forward-mode tangents) for the derivative
+// kernels behind the autograd op (ort_trace_pupil_vjp). The value part of a Dual is
+// computed by the same operations in the same order, so it is bit-identical to the
+// double trace. Lens parameters (radius, conic, coefficients) stay `double`, except the
+// Zernike coefficients, which the derivative kernels seed with tangents (ZSeed).
 //
 // Reference files are cited as path:line under optiland/.
 #pragma once
@@ -21,17 +26,170 @@
 #endif
 #define ORT_INLINE ORT_HD inline __attribute__((always_inline))
 
-
 namespace ort {
 
+// ---------------------------------------------------------------------------------
+// forward-mode dual numbers (derivative kernels only)
+// ---------------------------------------------------------------------------------
+template <int P>
+struct Dual {
+  double v;
+  double d[P];
+  ORT_HD Dual() {}
+  ORT_HD Dual(double x) : v(x) {
+#pragma unroll
+    for (int k = 0; k < P; ++k) d[k] = 0.0;
+  }
+};
+
+// the double overloads stay visible next to the Dual ones below
+using ::exp;
+using ::fabs;
+using ::sqrt;
+
+ORT_INLINE double vv(double x) { return x; }
+template <int P>
+ORT_INLINE double vv(const Dual<P>& x) { return x.v; }
+
+template <int P>
+ORT_INLINE Dual<P> operator+(const Dual<P>& a, const Dual<P>& b) {
+  Dual<P> r;
+  r.v = a.v + b.v;
+#pragma unroll
+  for (int k = 0; k < P; ++k) r.d[k] = a.d[k] + b.d[k];
+  return r;
+}
+template <int P>
+ORT_INLINE Dual<P> operator+(const Dual<P>& a, double b) {
+  Dual<P> r = a;
+  r.v = a.v + b;
+  return r;
+}
+template <int P>
+ORT_INLINE Dual<P> operator+(double a, const Dual<P>& b) {
+  Dual<P> r = b;
+  r.v = a + b.v;
+  return r;
+}
+template <int P>
+ORT_INLINE Dual<P> operator-(const Dual<P>& a) {
+  Dual<P> r;
+  r.v = -a.v;
+#pragma unroll
+  for (int k = 0; k < P; ++k) r.d[k] = -a.d[k];
+  return r;
+}
+template <int P>
+ORT_INLINE Dual<P> operator-(const Dual<P>& a, const Dual<P>& b) {
+  Dual<P> r;
+  r.v = a.v - b.v;
+#pragma unroll
+  for (int k = 0; k < P; ++k) r.d[k] = a.d[k] - b.d[k];
+  return r;
+}
+template <int P>
+ORT_INLINE Dual<P> operator-(const Dual<P>& a, double b) {
+  Dual<P> r = a;
+  r.v = a.v - b;
+  return r;
+}
+template <int P>
+ORT_INLINE Dual<P> operator-(double a, const Dual<P>& b) {
+  Dual<P> r;
+  r.v = a - b.v;
+#pragma unroll
+  for (int k = 0; k < P; ++k) r.d[k] = -b.d[k];
+  return r;
+}
+template <int P>
+ORT_INLINE Dual<P> operator*(const Dual<P>& a, const Dual<P>& b) {
+  Dual<P> r;
+  r.v = a.v * b.v;
+#pragma unroll
+  for (int k = 0; k < P; ++k) r.d[k] = a.d[k] * b.v + a.v * b.d[k];
+  return r;
+}
+template <int P>
+ORT_INLINE Dual<P> operator*(const Dual<P>& a, double b) {
+  Dual<P> r;
+  r.v = a.v * b;
+#pragma unroll
+  for (int k = 0; k < P; ++k) r.d[k] = a.d[k] * b;
+  return r;
+}
+template <int P>
+ORT_INLINE Dual<P> operator*(double a, const Dual<P>& b) {
+  Dual<P> r;
+  r.v = a * b.v;
+#pragma unroll
+  for (int k = 0; k < P; ++k) r.d[k] = a * b.d[k];
+  return r;
+}
+template <int P>
+ORT_INLINE Dual<P> operator/(const Dual<P>& a, const Dual<P>& b) {
+  Dual<P> r;
+  r.v = a.v / b.v;
+  const double inv = 1.0 / b.v;
+#pragma unroll
+  for (int k = 0; k < P; ++k) r.d[k] = (a.d[k] - r.v * b.d[k]) * inv;
+  return r;
+}
+template <int P>
+ORT_INLINE Dual<P> operator/(const Dual<P>& a, double b) {
+  Dual<P> r;
+  r.v = a.v / b;
+  const double inv = 1.0 / b;
+#pragma unroll
+  for (int k = 0; k < P; ++k) r.d[k] = a.d[k] * inv;
+  return r;
+}
+template <int P>
+ORT_INLINE Dual<P> operator/(double a, const Dual<P>& b) {
+  Dual<P> r;
+  r.v = a / b.v;
+  const double s = -r.v / b.v;
+#pragma unroll
+  for (int k = 0; k < P; ++k) r.d[k] = s * b.d[k];
+  return r;
+}
+template <int P>
+ORT_INLINE Dual<P> sqrt(const Dual<P>& a) {
+  Dual<P> r;
+  r.v = ::sqrt(a.v);
+  const double h = 0.5 / r.v;
+#pragma unroll
+  for (int k = 0; k < P; ++k) r.d[k] = a.d[k] * h;
+  return r;
+}
+template <int P>
+ORT_INLINE Dual<P> fabs(const Dual<P>& a) {  // torch.abs backward: sign(a) * g
+  return a.v < 0.0 ? -a : (a.v > 0.0 ? a : Dual<P>(::fabs(a.v)));
+}
+template <int P>
+ORT_INLINE Dual<P> exp(const Dual<P>& a) {
+  Dual<P> r;
+  r.v = ::exp(a.v);
+#pragma unroll
+  for (int k = 0; k < P; ++k) r.d[k] = a.d[k] * r.v;
+  return r;
+}
+
+// ---------------------------------------------------------------------------------
+// ray state
+// ---------------------------------------------------------------------------------
 // att accumulates the absorption exponent sum(-alpha t 1e3) (homogeneous.py:54); the
 // intensity is i * exp(att), evaluated once per ray instead of once per surface
 // (exp(a)exp(b) vs exp(a+b): a few ulps relative, see DESIGN.md Parity).
-struct Ray {
-  double x, y, z, L, M, N, i, opd, att;
+template <class T>
+struct RayT {
+  T x, y, z, L, M, N, i, opd, att;
 };
+using Ray = RayT<double>;
 
-ORT_INLINE double intensity(const Ray& r) { return r.att == 0.0 ? r.i : r.i * exp(r.att); }
+template <class T>
+ORT_INLINE T intensity(const RayT<T>& r) {
+  return vv(r.att) == 0.0 ? r.i : r.i * exp(r.att);
+}
 
 // ---------------------------------------------------------------------------------
 // Division by a shared divisor. gfx950 lowers an IEEE fp64 a / b to
@@ -41,7 +199,8 @@ ORT_INLINE double intensity(const Ray& r) { return r.att == 0.0 ? r.i : r.i * ex
 // NaNs. For several numerators over one divisor the reciprocal refinement is done once
 // and, inside a guarded exponent range where scale/fixup are identities, each quotient
 // is the same three operations -- bit-identical to a / b. Outside the range (and on
-// the host) it falls back to the plain division.
+// the host) it falls back to the plain division. Dual numbers always divide plainly
+// (their value is then the same IEEE quotient).
 // ---------------------------------------------------------------------------------
 struct SharedDiv {
   double b, y;
@@ -49,7 +208,7 @@ struct SharedDiv {
 };
 
 ORT_INLINE bool div_range_ok(double v) {
-  const double av = fabs(v);
+  const double av = ::fabs(v);
   return av >= 0x1p-300 && av <= 0x1p300;  // false for 0, inf, NaN
 }
 
@@ -80,6 +239,43 @@ ORT_INLINE double sdiv(double a, const SharedDiv& d) {
   return a / d.b;
 }
 
+template <int P>
+struct PlainDiv {
+  Dual<P> b;
+};
+template <int P>
+ORT_INLINE PlainDiv<P> shared_div(const Dual<P>& b) {
+  return PlainDiv<P>{b};
+}
+template <int P>
+ORT_INLINE Dual<P> sdiv(const Dual<P>& a, const PlainDiv<P>& d) {
+  return a / d.b;
+}
+template <int P>
+ORT_INLINE Dual<P> sdiv(double a, const PlainDiv<P>& d) {
+  return a / d.b;
+}
+
+// Zernike coefficient tangent seeds for the derivative kernels: term j (global index in
+// lens.zern) is parameter param[j] (< 0: not differentiated); tangent slot k of this
+// launch is parameter p0 + k.
+struct ZSeed {
+  const int32_t* param;
+  int p0;
+};
+
+ORT_INLINE double zcoef(double c, int, const ZSeed&, double*) { return c; }
+template <int P>
+ORT_INLINE Dual<P> zcoef(double c, int j, const ZSeed& zs, Dual<P>*) {
+  Dual<P> r(c);
+  if (zs.param) {
+    const int p = zs.param[j] - zs.p0;
+#pragma unroll
+    for (int k = 0; k < P; ++k) r.d[k] = (p == k) ? 1.0 : 0.0;
+  }
+  return r;
+}
+
 // ---------------------------------------------------------------------------------
 // ray generation: rays/ray_generator.py:71-106 + fields/field_types.py:160-181
 // ---------------------------------------------------------------------------------
@@ -98,8 +294,8 @@ ORT_INLINE Ray generate_ray(const ort_segment& s, double px, double py) {
   const double y1 = py * s.epd * s.vy / 2.0;  // ray_generator.py:77
   const double z1 = s.epl;
   const double dx = x1 - x0, dy = y1 - y0, dz = z1 - z0;
-  double mag = sqrt(dx * dx + dy * dy + dz * dz);  // :80
-  const bool is_zero = mag < 1e-9;                  // :82
+  double mag = ::sqrt(dx * dx + dy * dy + dz * dz);  // :80
+  const bool is_zero = mag < 1e-9;                    // :82
   mag = is_zero ? 1.0 : mag;
   const SharedDiv dm = shared_div(mag);
   r.L = is_zero ? 0.0 : sdiv(dx, dm);
@@ -114,11 +310,21 @@ ORT_INLINE Ray generate_ray(const ort_segment& s, double px, double py) {
   return r;
 }
 
+template <class T>
+ORT_INLINE RayT<T> promote(const Ray& r) {
+  RayT<T> o;
+  o.x = T(r.x); o.y = T(r.y); o.z = T(r.z);
+  o.L = T(r.L); o.M = T(r.M); o.N = T(r.N);
+  o.i = T(r.i); o.opd = T(r.opd); o.att = T(r.att);
+  return o;
+}
+
 // ---------------------------------------------------------------------------------
 // coordinate systems: coordinate_system.py:73-107, rays/base.py:28-42,
 // rays/real_rays.py:90-130 (cos/sin precomputed on the host)
 // ---------------------------------------------------------------------------------
-ORT_INLINE void apply_cs_op(Ray& r, const ort_cs_op& op) {
+template <class T>
+ORT_INLINE void apply_cs_op(RayT<T>& r, const ort_cs_op& op) {
   const double a = op.p[0], b = op.p[1], c = op.p[2];
   switch (op.kind) {
     case ORT_CS_TRANSLATE:
@@ -127,18 +333,18 @@ ORT_INLINE void apply_cs_op(Ray& r, const ort_cs_op& op) {
       r.z = r.z + c;
       break;
     case ORT_CS_ROT_X: {
-      const double y = r.y * a - r.z * b, z = r.y * b + r.z * a;
-      const double M = r.M * a - r.N * b, N = r.M * b + r.N * a;
+      const T y = r.y * a - r.z * b, z = r.y * b + r.z * a;
+      const T M = r.M * a - r.N * b, N = r.M * b + r.N * a;
       r.y = y; r.z = z; r.M = M; r.N = N;
     } break;
     case ORT_CS_ROT_Y: {
-      const double x = r.x * a + r.z * b, z = -r.x * b + r.z * a;
-      const double L = r.L * a + r.N * b, N = -r.L * b + r.N * a;
+      const T x = r.x * a + r.z * b, z = -r.x * b + r.z * a;
+      const T L = r.L * a + r.N * b, N = -r.L * b + r.N * a;
       r.x = x; r.z = z; r.L = L; r.N = N;
     } break;
     default: {  // ORT_CS_ROT_Z
-      const double x = r.x * a - r.y * b, y = r.x * b + r.y * a;
-      const double L = r.L * a - r.M * b, M = r.L * b + r.M * a;
+      const T x = r.x * a - r.y * b, y = r.x * b + r.y * a;
+      const T L = r.L * a - r.M * b, M = r.L * b + r.M * a;
       r.x = x; r.y = y; r.L = L; r.M = M;
     } break;
   }
@@ -148,17 +354,21 @@ ORT_INLINE void apply_cs_op(Ray& r, const ort_cs_op& op) {
 // intersections
 // ---------------------------------------------------------------------------------
 // plane.py:61-77
-ORT_INLINE double distance_plane(const Ray& r) { return -r.z / r.N; }
+template <class T>
+ORT_INLINE T distance_plane(const RayT<T>& r) {
+  return -r.z / r.N;
+}
 
 // standard.py:89-140
-ORT_INLINE double distance_conic(const Ray& r, double R, double k, bool radius_inf) {
+template <class T>
+ORT_INLINE T distance_conic(const RayT<T>& r, double R, double k, bool radius_inf) {
   if (radius_inf) {
-    const double Ns = fabs(r.N) > 1e-14 ? r.N : 1e-14;
+    const T Ns = ::fabs(vv(r.N)) > 1e-14 ? r.N : T(1e-14);
     return -r.z / Ns;
   }
-  const double N2 = r.N * r.N;
-  const double z2 = r.z * r.z;
-  double a, b, c;
+  const T N2 = r.N * r.N;
+  const T z2 = r.z * r.z;
+  T a, b, c;
   // 2*k*N*z + 2*L*x + 2*M*y - 2*N*R + 2*N*z: every "2*" is an exact scaling
   if (k == 0.0) {
     // sphere: k*N**2 = 0, 2*k*N*z = 0, k*z**2 = 0 and 0 + v == v, so the conic terms
@@ -172,35 +382,36 @@ ORT_INLINE double distance_conic(const Ray& r, double R, double k, bool radius_i
         2.0 * r.N * r.z;
     c = k * z2 - 2.0 * R * r.z + r.x * r.x + r.y * r.y + z2;
   }
-  const double d = b * b - 4.0 * a * c;
-  const double sd = sqrt(d);
-  const SharedDiv a2 = shared_div(2.0 * a);
-  const double t1 = sdiv(-b + sd, a2);
-  const double t2 = sdiv(-b - sd, a2);
-  const double z1 = r.z + t1 * r.N;
-  const double zz2 = r.z + t2 * r.N;
-  double t = fabs(z1) <= fabs(zz2) ? t1 : t2;
-  if (a == 0.0) t = -c / b;
+  const T d = b * b - 4.0 * a * c;
+  const T sd = sqrt(d);
+  const auto a2 = shared_div(2.0 * a);
+  const T t1 = sdiv(-b + sd, a2);
+  const T t2 = sdiv(-b - sd, a2);
+  const T z1 = r.z + t1 * r.N;
+  const T zz2 = r.z + t2 * r.N;
+  T t = ::fabs(vv(z1)) <= ::fabs(vv(zz2)) ? t1 : t2;
+  if (vv(a) == 0.0) t = -c / b;
   return t;
 }
 
 // standard.py:154-167
-ORT_INLINE void normal_conic(double x, double y, double R, double k, double& nx, double& ny,
-                             double& nz) {
-  const double r2 = x * x + y * y;
-  const double denom = R * sqrt(1.0 - (1.0 + k) * r2 / (R * R));
-  const SharedDiv dd = shared_div(denom);
-  const double dfdx = sdiv(x, dd);
-  const double dfdy = sdiv(y, dd);
-  const double mag = sqrt(dfdx * dfdx + dfdy * dfdy + 1.0);  // dfdz**2 = (-1)**2 = 1
-  const SharedDiv dm = shared_div(mag);
+template <class T>
+ORT_INLINE void normal_conic(const T& x, const T& y, double R, double k, T& nx, T& ny, T& nz) {
+  const T r2 = x * x + y * y;
+  const T denom = R * sqrt(1.0 - (1.0 + k) * r2 / (R * R));
+  const auto dd = shared_div(denom);
+  const T dfdx = sdiv(x, dd);
+  const T dfdy = sdiv(y, dd);
+  const T mag = sqrt(dfdx * dfdx + dfdy * dfdy + 1.0);  // dfdz**2 = (-1)**2 = 1
+  const auto dm = shared_div(mag);
   nx = sdiv(dfdx, dm);
   ny = sdiv(dfdy, dm);
   nz = sdiv(-1.0, dm);
 }
 
 // base conic sag, standard.py:73-87 (shared by every Newton geometry)
-ORT_INLINE double sag_conic(double r2, double R, double k) {
+template <class T>
+ORT_INLINE T sag_conic(const T& r2, double R, double k) {
   return r2 / (R * (1.0 + sqrt(1.0 - (1.0 + k) * r2 / (R * R))));
 }
 
@@ -208,21 +419,22 @@ ORT_INLINE double sag_conic(double r2, double R, double k) {
 // for p == 2 and returns x for p == 1 and 1 for p == 0 (fast scalar power); other
 // exponents go through libm pow in the reference and through repeated products here
 // (1-ulp-level differences on a small correction term; see DESIGN.md Parity).
-ORT_INLINE double ipow(double x, int p) {
-  if (p == 0) return 1.0;
+template <class T>
+ORT_INLINE T ipow(const T& x, int p) {
+  if (p == 0) return T(1.0);
   if (p < 0) return 1.0 / ipow(x, -p);
-  double r = x;
+  T r = x;
 #pragma unroll 1
   for (int q = 1; q < p; ++q) r = r * x;
   return r;
 }
 
 // even_asphere.py:82-98
-template <class PD>
-ORT_INLINE double sag_even(double x, double y, double R, double k, PD C, int nc) {
-  const double r2 = x * x + y * y;
-  double z = sag_conic(r2, R, k);
-  double rp = r2;  // r2 ** (i + 1)
+template <class T, class PD>
+ORT_INLINE T sag_even(const T& x, const T& y, double R, double k, PD C, int nc) {
+  const T r2 = x * x + y * y;
+  T z = sag_conic(r2, R, k);
+  T rp = r2;  // r2 ** (i + 1)
   for (int i = 0; i < nc; ++i) {
     z = z + C[i] * rp;
     rp = rp * r2;
@@ -231,33 +443,33 @@ ORT_INLINE double sag_even(double x, double y, double R, double k, PD C, int nc)
 }
 
 // even_asphere.py:100-129
-template <class PD>
-ORT_INLINE void normal_even(double x, double y, double R, double k, PD C, int nc,
-                            double& nx, double& ny, double& nz) {
-  const double r2 = x * x + y * y;
-  const double denom = R * sqrt(1.0 - (1.0 + k) * r2 / (R * R));
-  double dfdx = x / denom;
-  double dfdy = y / denom;
-  double rp = 1.0;  // r2 ** i
+template <class T, class PD>
+ORT_INLINE void normal_even(const T& x, const T& y, double R, double k, PD C, int nc, T& nx,
+                            T& ny, T& nz) {
+  const T r2 = x * x + y * y;
+  const T denom = R * sqrt(1.0 - (1.0 + k) * r2 / (R * R));
+  T dfdx = x / denom;
+  T dfdy = y / denom;
+  T rp = T(1.0);  // r2 ** i
   for (int i = 0; i < nc; ++i) {
     const double f = 2.0 * (double)(i + 1);
     dfdx = dfdx + f * x * C[i] * rp;
     dfdy = dfdy + f * y * C[i] * rp;
     rp = rp * r2;
   }
-  const double mag = sqrt(dfdx * dfdx + dfdy * dfdy + 1.0);
+  const T mag = sqrt(dfdx * dfdx + dfdy * dfdy + 1.0);
   nx = dfdx / mag;
   ny = dfdy / mag;
   nz = -1.0 / mag;
 }
 
 // odd_asphere.py:73-89
-template <class PD>
-ORT_INLINE double sag_odd(double x, double y, double R, double k, PD C, int nc) {
-  const double r2 = x * x + y * y;
-  const double r = sqrt(r2);
-  double z = sag_conic(r2, R, k);
-  double rp = r;  // r ** (i + 1)
+template <class T, class PD>
+ORT_INLINE T sag_odd(const T& x, const T& y, double R, double k, PD C, int nc) {
+  const T r2 = x * x + y * y;
+  const T r = sqrt(r2);
+  T z = sag_conic(r2, R, k);
+  T rp = r;  // r ** (i + 1)
   for (int i = 0; i < nc; ++i) {
     z = z + C[i] * rp;
     rp = rp * r;
@@ -266,26 +478,26 @@ ORT_INLINE double sag_odd(double x, double y, double R, double k, PD C, int nc) 
 }
 
 // odd_asphere.py:91-130 (non-finite per-term slopes are zeroed, :112-122)
-template <class PD>
-ORT_INLINE void normal_odd(double x, double y, double R, double k, PD C, int nc,
-                           double& nx, double& ny, double& nz) {
-  const double r2 = x * x + y * y;
-  const double r = sqrt(r2);
-  const double denom = R * sqrt(1.0 - (1.0 + k) * r2 / (R * R));
-  double dfdx = x / denom;
-  double dfdy = y / denom;
-  double rp = 1.0 / r;  // r ** (i - 1): 1/r, 1, r, r*r, r*r*r, ...
+template <class T, class PD>
+ORT_INLINE void normal_odd(const T& x, const T& y, double R, double k, PD C, int nc, T& nx,
+                           T& ny, T& nz) {
+  const T r2 = x * x + y * y;
+  const T r = sqrt(r2);
+  const T denom = R * sqrt(1.0 - (1.0 + k) * r2 / (R * R));
+  T dfdx = x / denom;
+  T dfdy = y / denom;
+  T rp = 1.0 / r;  // r ** (i - 1): 1/r, 1, r, r*r, r*r*r, ...
   for (int i = 0; i < nc; ++i) {
     const double f = (double)(i + 1);
-    double xt = f * x * C[i] * rp;
-    double yt = f * y * C[i] * rp;
-    if (!isfinite(xt)) xt = 0.0;
-    if (!isfinite(yt)) yt = 0.0;
-    rp = (i == 0) ? 1.0 : (i == 1 ? r : rp * r);
+    T xt = f * x * C[i] * rp;
+    T yt = f * y * C[i] * rp;
+    if (!isfinite(vv(xt))) xt = T(0.0);
+    if (!isfinite(vv(yt))) yt = T(0.0);
+    rp = (i == 0) ? T(1.0) : (i == 1 ? r : rp * r);
     dfdx = dfdx + xt;
     dfdy = dfdy + yt;
   }
-  const double mag = sqrt(dfdx * dfdx + dfdy * dfdy + 1.0);
+  const T mag = sqrt(dfdx * dfdx + dfdy * dfdy + 1.0);
   nx = dfdx / mag;
   ny = dfdy / mag;
   nz = -1.0 / mag;
@@ -293,21 +505,21 @@ ORT_INLINE void normal_odd(double x, double y, double R, double k, PD C, int nc,
 
 // ---- Zernike: geometries/zernike.py:133-246 + zernike/base.py:42-299 ----------------
 // R_n^|m|(rho) = sum_k a_k rho^(n-2k)         (base.py:228-253)
-template <class PD>
-ORT_INLINE double zern_radial(PD a, int n, int nr, double rho) {
-  double v = 0.0;
+template <class T, class PD>
+ORT_INLINE T zern_radial(PD a, int n, int nr, const T& rho) {
+  T v = T(0.0);
 #pragma unroll 1
   for (int k = 0; k < nr; ++k) v = v + a[k] * ipow(rho, n - 2 * k);
   return v;
 }
 // dR/drho = sum_k d_k rho^(n-2k-1)            (base.py:272-299)
-template <class PD>
-ORT_INLINE double zern_radial_deriv(PD d, int n, int nr, double rho) {
-  double v = 0.0;
+template <class T, class PD>
+ORT_INLINE T zern_radial_deriv(PD d, int n, int nr, const T& rho) {
+  T v = T(0.0);
 #pragma unroll 1
   for (int k = 0; k < nr; ++k) {
     if (n - 2 * k < 0) continue;
-    const double p = (n - 2 * k - 1) >= 0 ? ipow(rho, n - 2 * k - 1) : 0.0;
+    const T p = (n - 2 * k - 1) >= 0 ? ipow(rho, n - 2 * k - 1) : T(0.0);
     v = v + d[k] * p;
   }
   return v;
@@ -317,11 +529,12 @@ ORT_INLINE double zern_radial_deriv(PD d, int n, int nr, double rho) {
 // recurrence (the reference evaluates cos(m * atan2(y, x)); a few ulps apart, see
 // DESIGN.md Parity). phi = atan2(yn, xn) gives cos phi = xn / rho, sin phi = yn / rho,
 // and atan2(0, 0) = 0 at rho == 0.
-ORT_INLINE void cos_sin_m(int m, double c1, double s1, double& cm, double& sm) {
-  double c = 1.0, s = 0.0;
+template <class T>
+ORT_INLINE void cos_sin_m(int m, const T& c1, const T& s1, T& cm, T& sm) {
+  T c = T(1.0), s = T(0.0);
 #pragma unroll 1
   for (int q = 0; q < m; ++q) {
-    const double cn = c * c1 - s * s1;
+    const T cn = c * c1 - s * s1;
     s = s * c1 + c * s1;
     c = cn;
   }
@@ -329,75 +542,77 @@ ORT_INLINE void cos_sin_m(int m, double c1, double s1, double& cm, double& sm) {
   sm = s;
 }
 
-ORT_INLINE void polar_unit(double xn, double yn, double rho, double& c1, double& s1) {
-  if (rho > 0.0) {
+template <class T>
+ORT_INLINE void polar_unit(const T& xn, const T& yn, const T& rho, T& c1, T& s1) {
+  if (vv(rho) > 0.0) {
     c1 = xn / rho;
     s1 = yn / rho;
   } else {
-    c1 = 1.0;
-    s1 = 0.0;
+    c1 = T(1.0);
+    s1 = T(0.0);
   }
 }
 
 // zernike.py:133-161 (sets range_error on |x/R_norm| > 1 or |y/R_norm| > 1)
-template <class PD, class PZ>
-ORT_INLINE double sag_zernike(double x, double y, double R, double k, double Rn, PZ T, int nt,
-                              PD coef, bool& range_error) {
-  const double xn = x / Rn;
-  const double yn = y / Rn;
-  if (fabs(xn) > 1.0 || fabs(yn) > 1.0) range_error = true;  // zernike.py:234-246
-  const double rho = sqrt(xn * xn + yn * yn);
-  double c1, s1;
+template <class T, class PD, class PZ>
+ORT_INLINE T sag_zernike(const T& x, const T& y, double R, double k, double Rn, PZ Tm, int t0,
+                         int nt, PD coef, const ZSeed& zs, bool& range_error) {
+  const T xn = x / Rn;
+  const T yn = y / Rn;
+  if (::fabs(vv(xn)) > 1.0 || ::fabs(vv(yn)) > 1.0) range_error = true;  // :234-246
+  const T rho = sqrt(xn * xn + yn * yn);
+  T c1, s1;
   polar_unit(xn, yn, rho, c1, s1);
-  const double r2 = x * x + y * y;
-  double z = sag_conic(r2, R, k);
-  double total = 0.0;  // python sum() starts at int 0; 0 + t == t exactly
+  const T r2 = x * x + y * y;
+  T z = sag_conic(r2, R, k);
+  T total = T(0.0);  // python sum() starts at int 0; 0 + t == t exactly
   for (int j = 0; j < nt; ++j) {
-    const ort_zernike_term t = T[j];
-    const double rad = zern_radial(coef + t.rad_off, t.n, t.n_rad, rho);
-    double cm, sm;
+    const ort_zernike_term t = Tm[t0 + j];
+    const T rad = zern_radial(coef + t.rad_off, t.n, t.n_rad, rho);
+    T cm, sm;
     cos_sin_m(t.m >= 0 ? t.m : -t.m, c1, s1, cm, sm);
-    const double az = t.m >= 0 ? cm : sm;  // base.py:206-226
-    total = total + t.c * t.norm * rad * az;
+    const T az = t.m >= 0 ? cm : sm;  // base.py:206-226
+    const T c = zcoef(t.c, t0 + j, zs, (T*)nullptr);
+    total = total + c * t.norm * rad * az;
   }
   return z + total;
 }
 
 // zernike.py:163-231 (the normal omits the normalisation constant: reference quirk)
-template <class PD, class PZ>
-ORT_INLINE void normal_zernike(double x, double y, double R, double k, double Rn, PZ T, int nt,
-                               PD coef, double& nx, double& ny, double& nz) {
-  const double r2 = x * x + y * y;
-  const double denominator = R * sqrt(1.0 - (1.0 + k) * r2 / (R * R));
-  double dzdx = x / denominator;
-  double dzdy = y / denominator;
+template <class T, class PD, class PZ>
+ORT_INLINE void normal_zernike(const T& x, const T& y, double R, double k, double Rn, PZ Tm,
+                               int t0, int nt, PD coef, const ZSeed& zs, T& nx, T& ny, T& nz) {
+  const T r2 = x * x + y * y;
+  const T denominator = R * sqrt(1.0 - (1.0 + k) * r2 / (R * R));
+  T dzdx = x / denominator;
+  T dzdy = y / denominator;
   const double eps = 1e-14;
-  const double xn = x / Rn;
-  const double yn = y / Rn;
-  const double rho = sqrt(xn * xn + yn * yn);
-  double c1, s1;
+  const T xn = x / Rn;
+  const T yn = y / Rn;
+  const T rho = sqrt(xn * xn + yn * yn);
+  T c1, s1;
   polar_unit(xn, yn, rho, c1, s1);
   const double Rn2 = Rn * Rn;
   // (the reference returns zeros when EVERY rho is 0; per ray (x/Rn^2)/(0+eps) = 0 too)
-  const double drho_dx = (x / Rn2) / (rho + eps);
-  const double drho_dy = (y / Rn2) / (rho + eps);
-  const double rho2e = rho * rho + eps;
+  const T drho_dx = (x / Rn2) / (rho + eps);
+  const T drho_dy = (y / Rn2) / (rho + eps);
+  const T rho2e = rho * rho + eps;
   const double inv_rn = 1.0 / Rn;
-  const double dphi_dx = -(yn) / rho2e * inv_rn;
-  const double dphi_dy = +(xn) / rho2e * inv_rn;
+  const T dphi_dx = -(yn) / rho2e * inv_rn;
+  const T dphi_dy = (xn) / rho2e * inv_rn;  // "+(x_norm)": unary plus
   for (int j = 0; j < nt; ++j) {
-    const ort_zernike_term t = T[j];
+    const ort_zernike_term t = Tm[t0 + j];
     if (t.c == 0.0) continue;
     const PD a = coef + t.rad_off;
-    const double rt = zern_radial(a, t.n, t.n_rad, rho);
-    const double rd = zern_radial_deriv(a + t.n_rad, t.n, t.n_rad, rho);
+    const T rt = zern_radial(a, t.n, t.n_rad, rho);
+    const T rd = zern_radial_deriv(a + t.n_rad, t.n, t.n_rad, rho);
     const int am = t.m >= 0 ? t.m : -t.m;
-    double cm, sm;
+    T cm, sm;
     cos_sin_m(am, c1, s1, cm, sm);
-    double dr, dp;
+    T dr, dp;
     if (t.m == 0) {  // base.py:128-137
       dr = rd;
-      dp = 0.0;
+      dp = T(0.0);
     } else if (t.m > 0) {
       dr = rd * cm;
       dp = (double)(-t.m) * rt * sm;
@@ -405,11 +620,12 @@ ORT_INLINE void normal_zernike(double x, double y, double R, double k, double Rn
       dr = rd * sm;
       dp = (double)am * rt * cm;
     }
-    dzdx = dzdx + t.c * (dr * drho_dx + dp * dphi_dx);
-    dzdy = dzdy + t.c * (dr * drho_dy + dp * dphi_dy);
+    const T c = zcoef(t.c, t0 + j, zs, (T*)nullptr);
+    dzdx = dzdx + c * (dr * drho_dx + dp * dphi_dx);
+    dzdy = dzdy + c * (dr * drho_dy + dp * dphi_dy);
   }
-  double norm = sqrt(dzdx * dzdx + dzdy * dzdy + 1.0);
-  norm = norm < eps ? 1.0 : norm;
+  T norm = sqrt(dzdx * dzdx + dzdy * dzdy + 1.0);
+  norm = vv(norm) < eps ? T(1.0) : norm;
   nx = dzdx / norm;
   ny = dzdy / norm;
   nz = -1.0 / norm;
@@ -420,9 +636,9 @@ ORT_INLINE void normal_zernike(double x, double y, double R, double k, double Rn
 // only pays registers for the kinds it contains.
 enum : unsigned { KM_EVEN = 1u, KM_ODD = 2u, KM_ZERN = 4u };
 
-template <unsigned KM, class PD, class PZ>
-ORT_INLINE double newton_sag(const ort_surface& s, PD coef, PZ zern, double x, double y,
-                             bool& range_error) {
+template <unsigned KM, class T, class PD, class PZ>
+ORT_INLINE T newton_sag(const ort_surface& s, PD coef, PZ zern, const ZSeed& zs, const T& x,
+                        const T& y, bool& range_error) {
   const PD C = coef + s.coef_off;
   if constexpr ((KM & KM_EVEN) != 0) {
     if (KM == KM_EVEN || s.geometry == ORT_GEOM_EVEN_ASPHERE)
@@ -433,15 +649,15 @@ ORT_INLINE double newton_sag(const ort_surface& s, PD coef, PZ zern, double x, d
       return sag_odd(x, y, s.radius, s.conic, C, s.n_coef);
   }
   if constexpr ((KM & KM_ZERN) != 0) {
-    return sag_zernike(x, y, s.radius, s.conic, s.norm_radius, zern + s.coef_off, s.n_coef,
-                       coef, range_error);
+    return sag_zernike(x, y, s.radius, s.conic, s.norm_radius, zern, s.coef_off, s.n_coef,
+                       coef, zs, range_error);
   }
-  return NAN;
+  return T(NAN);
 }
 
-template <unsigned KM, class PD, class PZ>
-ORT_INLINE void newton_normal(const ort_surface& s, PD coef, PZ zern, double x, double y,
-                              double& nx, double& ny, double& nz) {
+template <unsigned KM, class T, class PD, class PZ>
+ORT_INLINE void newton_normal(const ort_surface& s, PD coef, PZ zern, const ZSeed& zs,
+                              const T& x, const T& y, T& nx, T& ny, T& nz) {
   const PD C = coef + s.coef_off;
   if constexpr ((KM & KM_EVEN) != 0) {
     if (KM == KM_EVEN || s.geometry == ORT_GEOM_EVEN_ASPHERE) {
@@ -456,36 +672,36 @@ ORT_INLINE void newton_normal(const ort_surface& s, PD coef, PZ zern, double x, 
     }
   }
   if constexpr ((KM & KM_ZERN) != 0) {
-    normal_zernike(x, y, s.radius, s.conic, s.norm_radius, zern + s.coef_off, s.n_coef, coef,
-                   nx, ny, nz);
+    normal_zernike(x, y, s.radius, s.conic, s.norm_radius, zern, s.coef_off, s.n_coef, coef,
+                   zs, nx, ny, nz);
     return;
   }
-  nx = ny = nz = NAN;
+  nx = ny = nz = T(NAN);
 }
 
 // newton_raphson.py:140-146: residual f(t) = sag(P(t)) - z(t)
-template <unsigned KM, class PD, class PZ>
-ORT_INLINE double newton_residual(const ort_surface& s, PD coef, PZ zern, const Ray& r,
-                                  double t, bool& range_error) {
-  const double xi = r.x + t * r.L;
-  const double yi = r.y + t * r.M;
-  const double zi = r.z + t * r.N;
-  return newton_sag<KM, PD, PZ>(s, coef, zern, xi, yi, range_error) - zi;
+template <unsigned KM, class T, class PD, class PZ>
+ORT_INLINE T newton_residual(const ort_surface& s, PD coef, PZ zern, const ZSeed& zs,
+                             const RayT<T>& r, const T& t, bool& range_error) {
+  const T xi = r.x + t * r.L;
+  const T yi = r.y + t * r.M;
+  const T zi = r.z + t * r.N;
+  return newton_sag<KM>(s, coef, zern, zs, xi, yi, range_error) - zi;
 }
 
 // newton_raphson.py:154-166: t_new = t - f / f'(t)
-template <unsigned KM, class PD, class PZ>
-ORT_INLINE double newton_update(const ort_surface& s, PD coef, PZ zern, const Ray& r,
-                                double t, double f) {
-  const double xi = r.x + t * r.L;
-  const double yi = r.y + t * r.M;
-  double nx, ny, nz;
-  newton_normal<KM, PD, PZ>(s, coef, zern, xi, yi, nx, ny, nz);
-  const double nzs = fabs(nz) > 1e-14 ? nz : 1e-14;
-  const double fx = -nx / nzs;
-  const double fy = -ny / nzs;
-  const double df = fx * r.L + fy * r.M - r.N;
-  const double dfs = fabs(df) > 1e-14 ? df : 1e-14;
+template <unsigned KM, class T, class PD, class PZ>
+ORT_INLINE T newton_update(const ort_surface& s, PD coef, PZ zern, const ZSeed& zs,
+                           const RayT<T>& r, const T& t, const T& f) {
+  const T xi = r.x + t * r.L;
+  const T yi = r.y + t * r.M;
+  T nx, ny, nz;
+  newton_normal<KM>(s, coef, zern, zs, xi, yi, nx, ny, nz);
+  const T nzs = ::fabs(vv(nz)) > 1e-14 ? nz : T(1e-14);
+  const T fx = -nx / nzs;
+  const T fy = -ny / nzs;
+  const T df = fx * r.L + fy * r.M - r.N;
+  const T dfs = ::fabs(vv(df)) > 1e-14 ? df : T(1e-14);
   return t - f / dfs;
 }
 
@@ -493,7 +709,8 @@ ORT_INLINE double newton_update(const ort_surface& s, PD coef, PZ zern, const Ra
 // per-surface physics
 // ---------------------------------------------------------------------------------
 // propagation/homogeneous.py:30-57 (alpha = 4 pi k / w, applied only when k > 0)
-ORT_INLINE void propagate(Ray& r, double t, double alpha) {
+template <class T>
+ORT_INLINE void propagate(RayT<T>& r, const T& t, double alpha) {
   r.x = r.x + t * r.L;
   r.y = r.y + t * r.M;
   r.z = r.z + t * r.N;
@@ -501,22 +718,28 @@ ORT_INLINE void propagate(Ray& r, double t, double alpha) {
 }
 
 // surfaces/standard_surface.py:218
-ORT_INLINE void add_opd(Ray& r, double t, double n_pre) { r.opd = r.opd + fabs(t * n_pre); }
+template <class T>
+ORT_INLINE void add_opd(RayT<T>& r, const T& t, double n_pre) {
+  r.opd = r.opd + fabs(t * n_pre);
+}
 
 // physical_apertures/radial.py:50-63 + rays/real_rays.py:132-139
-ORT_INLINE void clip_radial(Ray& r, double rmax2, double rmin2) {
-  const double radius2 = r.x * r.x + r.y * r.y;
+template <class T>
+ORT_INLINE void clip_radial(RayT<T>& r, double rmax2, double rmin2) {
+  const double radius2 = vv(r.x * r.x + r.y * r.y);
   const bool inside = (radius2 <= rmax2) && (radius2 >= rmin2);
   if (!inside) {
-    r.i = 0.0;
-    r.att = 0.0;
+    r.i = T(0.0);
+    r.att = T(0.0);
   }
 }
 
 // rays/real_rays.py:511-547: sign(dot) flip (np.sign: 0 -> 0, NaN -> NaN), |dot|
-ORT_INLINE double align_normal(const Ray& r, double& nx, double& ny, double& nz) {
-  const double dot = r.L * nx + r.M * ny + r.N * nz;
-  const double sgn = dot > 0.0 ? 1.0 : (dot < 0.0 ? -1.0 : (dot == dot ? 0.0 : dot));
+template <class T>
+ORT_INLINE T align_normal(const RayT<T>& r, T& nx, T& ny, T& nz) {
+  const T dot = r.L * nx + r.M * ny + r.N * nz;
+  const double dv = vv(dot);
+  const double sgn = dv > 0.0 ? 1.0 : (dv < 0.0 ? -1.0 : (dv == dv ? 0.0 : dv));
   nx = nx * sgn;
   ny = ny * sgn;
   nz = nz * sgn;
@@ -525,49 +748,52 @@ ORT_INLINE double align_normal(const Ray& r, double& nx, double& ny, double& nz)
 
 // rays/real_rays.py:141-163; u = n1 / n2 comes from the host table (the same IEEE
 // quotient the reference forms per ray)
-ORT_INLINE void refract(Ray& r, double nx, double ny, double nz, double u) {
-  const double dot = align_normal(r, nx, ny, nz);
-  const double root = sqrt(1.0 - u * u * (1.0 - dot * dot));
-  const double L0 = r.L, M0 = r.M, N0 = r.N;
+template <class T>
+ORT_INLINE void refract(RayT<T>& r, T nx, T ny, T nz, double u) {
+  const T dot = align_normal(r, nx, ny, nz);
+  const T root = sqrt(1.0 - u * u * (1.0 - dot * dot));
+  const T L0 = r.L, M0 = r.M, N0 = r.N;
   r.L = u * L0 + nx * root - u * nx * dot;
   r.M = u * M0 + ny * root - u * ny * dot;
   r.N = u * N0 + nz * root - u * nz * dot;
 }
 
 // rays/real_rays.py:165-181
-ORT_INLINE void reflect(Ray& r, double nx, double ny, double nz) {
-  const double dot = align_normal(r, nx, ny, nz);
+template <class T>
+ORT_INLINE void reflect(RayT<T>& r, T nx, T ny, T nz) {
+  const T dot = align_normal(r, nx, ny, nz);
   r.L = r.L - 2.0 * dot * nx;
   r.M = r.M - 2.0 * dot * ny;
   r.N = r.N - 2.0 * dot * nz;
 }
 
 // surface normal at the current (local) ray position
-template <unsigned KM, class PD, class PZ>
-ORT_INLINE void surface_normal(const ort_surface& s, PD coef, PZ zern, const Ray& r,
-                               double& nx, double& ny, double& nz) {
+template <unsigned KM, class T, class PD, class PZ>
+ORT_INLINE void surface_normal(const ort_surface& s, PD coef, PZ zern, const ZSeed& zs,
+                               const RayT<T>& r, T& nx, T& ny, T& nz) {
   switch (s.geometry) {
     case ORT_GEOM_PLANE:  // plane.py:79-98
-      nx = 0.0; ny = 0.0; nz = 1.0;
+      nx = T(0.0); ny = T(0.0); nz = T(1.0);
       break;
     case ORT_GEOM_STANDARD:
       normal_conic(r.x, r.y, s.radius, s.conic, nx, ny, nz);
       break;
     default:
-      newton_normal<KM, PD, PZ>(s, coef, zern, r.x, r.y, nx, ny, nz);
+      newton_normal<KM>(s, coef, zern, zs, r.x, r.y, nx, ny, nz);
   }
 }
 
 // everything in Surface.trace after the distance t is known
 // (standard_surface.py:215-231 minus localize/globalize)
-template <unsigned KM, class PD, class PZ>
-ORT_INLINE void finish_surface(Ray& r, const ort_surface& s, PD coef, PZ zern, double t,
-                               double n_pre, double u, double alpha_pre) {
+template <unsigned KM, class T, class PD, class PZ>
+ORT_INLINE void finish_surface(RayT<T>& r, const ort_surface& s, PD coef, PZ zern,
+                               const ZSeed& zs, const T& t, double n_pre, double u,
+                               double alpha_pre) {
   propagate(r, t, alpha_pre);
   add_opd(r, t, n_pre);
   if (s.flags & ORT_SURF_APERTURE) clip_radial(r, s.ap_rmax2, s.ap_rmin2);
-  double nx, ny, nz;
-  surface_normal<KM, PD, PZ>(s, coef, zern, r, nx, ny, nz);
+  T nx, ny, nz;
+  surface_normal<KM>(s, coef, zern, zs, r, nx, ny, nz);
   if (s.flags & ORT_SURF_REFLECTIVE)
     reflect(r, nx, ny, nz);
   else

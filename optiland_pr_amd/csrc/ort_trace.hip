@@ -41,6 +41,7 @@ __device__ inline cptr<T> cst(const T* p) {
 }
 using PD = cptr<double>;
 using PZ = cptr<ort_zernike_term>;
+constexpr ort::ZSeed kNoSeed{nullptr, 0};
 
 // Kernel specialisation bits: bits 0-2 = Newton kinds present (ort::KM_*), bit 3 = rays
 // generated in-kernel from pupil coordinates.
@@ -111,7 +112,8 @@ __device__ inline ort_surface_optics optics_at(const KArgs& a, int lam, int si) 
 
 // localize / globalize (coordinate_system.py:73-107): pure translations inline,
 // general frames through the op list
-__device__ inline void localize(const KArgs& a, const ort_surface& s, ort::Ray& r) {
+template <class T>
+__device__ inline void localize(const KArgs& a, const ort_surface& s, ort::RayT<T>& r) {
   if (s.flags & ORT_SURF_TRANSLATE) {
     r.x = r.x + -s.cs_t[0];
     r.y = r.y + -s.cs_t[1];
@@ -121,7 +123,8 @@ __device__ inline void localize(const KArgs& a, const ort_surface& s, ort::Ray& 
   for (int c = 0; c < s.n_cs_loc; ++c) ort::apply_cs_op(r, cst(a.cs)[s.cs_loc_off + c]);
 }
 
-__device__ inline void globalize(const KArgs& a, const ort_surface& s, ort::Ray& r) {
+template <class T>
+__device__ inline void globalize(const KArgs& a, const ort_surface& s, ort::RayT<T>& r) {
   if (s.flags & ORT_SURF_TRANSLATE) {
     r.x = r.x + s.cs_t[0];
     r.y = r.y + s.cs_t[1];
@@ -145,11 +148,11 @@ __device__ inline double newton_distance(const KArgs& a, const ort_surface& s, i
     int j = 0;
     for (; j < max_iter; ++j) {
       bool rerr = false;
-      const double f = ort::newton_residual<(FEAT & F_KM)>(s, cst(a.coef), cst(a.zern), r, t, rerr);
+      const double f = ort::newton_residual<(FEAT & F_KM)>(s, cst(a.coef), cst(a.zern), kNoSeed, r, t, rerr);
       if (active && rerr) range_error = true;
       const bool conv = !active || !(fabs(f) >= tol);
       if (__all(conv)) break;
-      t = ort::newton_update<(FEAT & F_KM)>(s, cst(a.coef), cst(a.zern), r, t, f);
+      t = ort::newton_update<(FEAT & F_KM)>(s, cst(a.coef), cst(a.zern), kNoSeed, r, t, f);
     }
     if (a.stats && (threadIdx.x & 63) == 0)
       atomicMax(&a.stats[(group_uniform ? group : 0) * a.n_surf + si].max_updates, j);
@@ -164,14 +167,14 @@ __device__ inline double newton_distance(const KArgs& a, const ort_surface& s, i
     if (!__any(lane_on)) break;
     if (lane_on) {
       bool rerr = false;
-      const double f = ort::newton_residual<(FEAT & F_KM)>(s, cst(a.coef), cst(a.zern), r, t, rerr);
+      const double f = ort::newton_residual<(FEAT & F_KM)>(s, cst(a.coef), cst(a.zern), kNoSeed, r, t, rerr);
       // the reference evaluates sag at j = 0..U-1 always, and at j = U only when the
       // loop broke there (U < max_iter)
       if (rerr && (j < U || U < max_iter)) range_error = true;
       const bool conv = fabs(f) < tol;  // NaN never converges (np.max propagates NaN)
       if (conv && j < 64) mask |= 1ull << j;
       if (!conv) last_bad = j;
-      if (j < U) t = ort::newton_update<(FEAT & F_KM)>(s, cst(a.coef), cst(a.zern), r, t, f);
+      if (j < U) t = ort::newton_update<(FEAT & F_KM)>(s, cst(a.coef), cst(a.zern), kNoSeed, r, t, f);
     }
   }
   if (a.stats) {
@@ -249,7 +252,8 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(const KArgs a) {
     }
     const double n_pre = o.n_pre, u = o.u, alpha = o.alpha_pre;
     if constexpr ((FEAT & F_KM) != 0) {
-      ort::finish_surface<(FEAT & F_KM)>(r, s, cst(a.coef), cst(a.zern), t, n_pre, u, alpha);
+      ort::finish_surface<(FEAT & F_KM)>(r, s, cst(a.coef), cst(a.zern), kNoSeed, t, n_pre, u,
+                                         alpha);
     } else {
       // closed-form geometries only: plane / conic normal inline
       ort::propagate(r, t, alpha);
@@ -379,6 +383,114 @@ __global__ __launch_bounds__(kBlock) void trace_closed_kernel(const KArgs a) {
   a.out.N[rid] = r.N;
   a.out.i[rid] = ort::intensity(r);
   a.out.opd[rid] = r.opd;
+}
+
+// ---------------------------------------------------------------------------------
+// Vector-Jacobian product w.r.t. Zernike coefficients (the autograd backward of
+// ort_trace_pupil; reference: torch autograd through the unrolled trace,
+// backend/torch_backend.py + optimization/optimizer/torch/base.py:95-154).
+//
+// Forward mode: the ray state carries P tangents (ort::Dual<P>), one per coefficient of
+// this launch's parameter chunk, through exactly the Newton update counts of the primal
+// trace (opt.sched), so the derivative is that of the unrolled iteration the reference
+// differentiates. Each lane contracts its tangents with the ray cotangents; the wave
+// sums them with DPP/shuffles and one lane per wave adds P partial sums to grad.
+// ---------------------------------------------------------------------------------
+struct JArgs {
+  const int32_t* zparam;  // [n_zern_terms] parameter index per term, < 0: constant
+  int32_t n_param;
+  int32_t p0;             // first parameter of this launch
+  ort_rays cot;           // cotangents of the outputs (NULL field: zero)
+  double* grad;           // [n_param], accumulated with atomics
+};
+
+__device__ inline double wave_sum(double v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int P>
+__device__ inline void cot_acc(double (&acc)[P], const double* g, int64_t rid,
+                               const ort::Dual<P>& v) {
+  if (!g) return;
+  const double c = g[rid];
+#pragma unroll
+  for (int k = 0; k < P; ++k) acc[k] += c * v.d[k];
+}
+
+template <int P, uint32_t KM>
+__global__ __launch_bounds__(kBlock) void vjp_kernel(const KArgs a, const JArgs j) {
+  using D = ort::Dual<P>;
+  const int64_t rid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const bool active = rid < a.n_rays;
+  const int64_t r_ld = active ? rid : 0;
+  const int64_t sidx = r_ld / a.seg_len;
+  const ort_segment sg = a.seg[sidx];
+  const int lam = sg.lambda_idx;
+  const int64_t p = a.pupil_per_ray ? r_ld : (r_ld - sidx * a.seg_len);
+  ort::RayT<D> r = ort::promote<D>(ort::generate_ray(sg, a.px[p], a.py[p]));
+  const int64_t group = r_ld / a.group_len;
+  const ort::ZSeed zs{j.zparam, j.p0};
+
+  for (int si = a.start_surface; si < a.n_surf; ++si) {
+    const ort_surface s = cst(a.surf)[si];
+    const ort_surface_optics o = optics_at(a, lam, si);
+    localize(a, s, r);
+    D t;
+    if (s.geometry == ORT_GEOM_PLANE) {
+      t = ort::distance_plane(r);
+    } else {
+      t = ort::distance_conic(r, s.radius, s.conic, (s.flags & ORT_SURF_RADIUS_INF) != 0);
+      if (s.geometry != ORT_GEOM_STANDARD) {
+        // replay the primal's update count (newton_raphson.py:137-166)
+        const int U = a.sched ? a.sched[group * a.n_surf + si] : s.max_iter;
+        bool rerr = false;
+        for (int it = 0; it < U; ++it) {
+          const D f = ort::newton_residual<KM>(s, cst(a.coef), cst(a.zern), zs, r, t, rerr);
+          t = ort::newton_update<KM>(s, cst(a.coef), cst(a.zern), zs, r, t, f);
+        }
+      }
+    }
+    ort::finish_surface<KM>(r, s, cst(a.coef), cst(a.zern), zs, t, o.n_pre, o.u, o.alpha_pre);
+    globalize(a, s, r);
+  }
+  if (a.final_mat >= 0)
+    ort::propagate(r, D(a.final_thickness),
+                   tab(a.alpha_tab, a.n_lambda, a.n_mat, lam, a.final_mat));
+
+  double acc[P];
+#pragma unroll
+  for (int k = 0; k < P; ++k) acc[k] = 0.0;
+  if (active) {
+    cot_acc(acc, j.cot.x, rid, r.x);
+    cot_acc(acc, j.cot.y, rid, r.y);
+    cot_acc(acc, j.cot.z, rid, r.z);
+    cot_acc(acc, j.cot.L, rid, r.L);
+    cot_acc(acc, j.cot.M, rid, r.M);
+    cot_acc(acc, j.cot.N, rid, r.N);
+    if (j.cot.i) cot_acc(acc, j.cot.i, rid, ort::intensity(r));
+    cot_acc(acc, j.cot.opd, rid, r.opd);
+  }
+#pragma unroll
+  for (int k = 0; k < P; ++k) {
+    const double v = wave_sum(acc[k]);
+    if ((threadIdx.x & 63) == 0 && j.p0 + k < j.n_param && v != 0.0)
+      atomicAdd(&j.grad[j.p0 + k], v);
+  }
+}
+
+typedef void (*VjpFn)(const KArgs, const JArgs);
+
+template <int P>
+VjpFn pick_vjp(uint32_t km) {
+  switch (km) {
+    case ort::KM_ZERN: return vjp_kernel<P, ort::KM_ZERN>;
+    case ort::KM_ZERN | ort::KM_EVEN: return vjp_kernel<P, ort::KM_ZERN | ort::KM_EVEN>;
+    case ort::KM_ZERN | ort::KM_ODD: return vjp_kernel<P, ort::KM_ZERN | ort::KM_ODD>;
+    case ort::KM_ZERN | ort::KM_EVEN | ort::KM_ODD:
+      return vjp_kernel<P, ort::KM_ZERN | ort::KM_EVEN | ort::KM_ODD>;
+    default: return nullptr;
+  }
 }
 
 __global__ __launch_bounds__(kBlock) void generate_kernel(const KArgs a) {
@@ -540,6 +652,46 @@ int ort_trace_pupil(const ort_lens* lens, const double* px, const double* py,
   hipStream_t s = (hipStream_t)stream;
   if ((rc = init_outputs(a, s))) return rc;
   return launch(a, feat, s);
+}
+
+int ort_trace_pupil_vjp(const ort_lens* lens, const double* px, const double* py,
+                        const ort_batch* batch, const ort_options* opt,
+                        const int32_t* zern_param, int32_t n_param,
+                        const ort_rays* cotangent, double* grad, void* stream) {
+  if (!batch || !cotangent || n_param < 0) return ORT_ERR_ARG;
+  if (batch->n_rays == 0 || n_param == 0) return ORT_OK;
+  if (!px || !py || !batch->seg || !zern_param || !grad) return ORT_ERR_ARG;
+  KArgs a{};
+  uint32_t feat = 0;
+  int rc = fill_args(a, lens, batch, opt, nullptr, nullptr, nullptr, feat);
+  if (rc) return rc;
+  if (opt->newton_mode != ORT_NEWTON_SCHEDULE) return ORT_ERR_ARG;
+  if ((feat & ort::KM_ZERN) == 0) return ORT_ERR_ARG;  // no Zernike surface to seed
+  a.px = px;
+  a.py = py;
+  JArgs j{};
+  j.zparam = zern_param;
+  j.n_param = n_param;
+  j.cot = *cotangent;
+  j.grad = grad;
+  const int64_t blocks = (a.n_rays + kBlock - 1) / kBlock;
+  if (blocks > 0x7fffffff) return ORT_ERR_ARG;
+  const uint32_t km = feat & F_KM;
+  hipStream_t s = (hipStream_t)stream;
+  for (int p0 = 0; p0 < n_param;) {
+    const int left = n_param - p0;
+    // tangents per launch: ORT_VJP_TANGENTS overrides (A/B timing)
+    const char* e = getenv("ORT_VJP_TANGENTS");
+    const int pref = e ? atoi(e) : 4;
+    const int P = left >= 4 && pref >= 4 ? 4 : (left >= 2 && pref >= 2 ? 2 : 1);
+    VjpFn fn = P == 4 ? pick_vjp<4>(km) : (P == 2 ? pick_vjp<2>(km) : pick_vjp<1>(km));
+    if (!fn) return ORT_ERR_ARG;
+    j.p0 = p0;
+    hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(kBlock), 0, s, a, j);
+    if (hipGetLastError() != hipSuccess) return ORT_ERR_LAUNCH;
+    p0 += P;
+  }
+  return ORT_OK;
 }
 
 int ort_generate_rays(const double* px, const double* py, ort_rays* rays_out,

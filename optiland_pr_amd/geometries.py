@@ -8,6 +8,7 @@ zernike}.py: same class names, constructor arguments and defaults. The arithmeti
 
 from __future__ import annotations
 
+import functools
 import math
 
 import numpy as np
@@ -135,6 +136,7 @@ def _norm_constant(kind, n, m):
     return np.sqrt(np.array((2 * n + 2) / denominator))
 
 
+@functools.lru_cache(maxsize=None)
 def zernike_indices(kind, n_indices):
     """zernike/base.py:143-192 (_generate_indices): (n, m) sorted by the scheme's
     coefficient number."""
@@ -155,7 +157,7 @@ def zernike_indices(kind, n_indices):
         else:
             m += 1
     srt = [e for _, e in sorted(zip(number, indices, strict=False))]
-    return srt[:n_indices]
+    return tuple(srt[:n_indices])
 
 
 def _gamma(x):
@@ -167,6 +169,7 @@ def _gamma(x):
         return np.float64(math.gamma(float(x)))
 
 
+@functools.lru_cache(maxsize=None)
 def radial_coefficients(n, m_abs):
     """Host precompute of the reference's per-term factorial weights.
 
@@ -185,7 +188,7 @@ def radial_coefficients(n, m_abs):
         a.append(float((-1) ** k * num / denom))
         factor = n - 2 * k
         d.append(float((-1) ** k * (num / denom) * factor))
-    return a, d
+    return tuple(a), tuple(d)
 
 
 class ZernikePolynomialGeometry(NewtonRaphsonGeometry):
@@ -213,9 +216,12 @@ class ZernikePolynomialGeometry(NewtonRaphsonGeometry):
 
     def zernike_terms(self):
         """-> list of (c, norm, n, m, a_k list, d_k list) in coefficient order."""
-        idx = zernike_indices(self.zernike_type, len(self.coefficients))
+        coeffs = self.coefficients
+        if hasattr(coeffs, "detach"):  # torch tensor (autograd leaf, autodiff.py)
+            coeffs = coeffs.detach().cpu().numpy()
+        idx = zernike_indices(self.zernike_type, len(coeffs))
         out = []
-        for (n, m), c in zip(idx, self.coefficients, strict=True):
+        for (n, m), c in zip(idx, coeffs, strict=True):
             a, d = radial_coefficients(n, abs(m))
             out.append((float(c), float(_norm_constant(self.zernike_type, n, m)), n, m, a, d))
         return out

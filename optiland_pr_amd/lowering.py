@@ -72,6 +72,14 @@ class LensTable:
     def has_zernike(self):
         return bool(np.any(self.surfaces["geometry"] == _abi.GEOM_ZERNIKE))
 
+    def fingerprint(self):
+        """Bytes of everything the device reads: equal fingerprints trace identically."""
+        parts = [np.ascontiguousarray(a).tobytes() for a in
+                 (self.surfaces, self.cs_ops, self.coef, self.zern, self.n_tab, self.alpha_tab)]
+        parts.append(np.array([self.final_mat], dtype=np.int64).tobytes())
+        parts.append(np.array([self.final_thickness], dtype=np.float64).tobytes())
+        return b"".join(parts)
+
 
 def lower_surface_group(surface_group, wavelengths, record=False, skip_object=True):
     """Lower every traced surface (index >= 1) of `surface_group`.

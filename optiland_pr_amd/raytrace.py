@@ -21,7 +21,7 @@ import ctypes as C
 
 import numpy as np
 
-from . import _abi, _native
+from . import _abi, _native, autodiff
 from .distribution import BaseDistribution, create_distribution
 from .lowering import LensTable, lower_surface_group, segment_params
 
@@ -180,11 +180,18 @@ class DeviceLens:
         self.sched_cache["_default"] = sched.max(axis=0)
 
 
-def lens_for(optic_or_group, wavelengths, record=False):
-    """Lowered + uploaded lens, cached on the Optic (invalidated by Optic edits)."""
+def lens_for(optic_or_group, wavelengths, record=False, image_record=False):
+    """Lowered + uploaded lens, cached on the Optic.
+
+    The host lowering (~0.3 ms) runs on every call and the cached upload is reused only
+    when the lowered bytes are identical, so in-place edits the Optic does not see
+    (e.g. geometry.coefficients[i] = v, variable/zernike_coeff.py:71-95) are never
+    traced stale. image_record: no image-space propagate (final_mat = -1), i.e. the
+    outputs are the image-surface record surface_group.x[-1] (surface_group.py:232-244)."""
     host = optic_or_group
     sg = getattr(host, "surface_group", host)
-    key = (tuple(float(w) for w in wavelengths), record if isinstance(record, bool) else tuple(record))
+    key = (tuple(float(w) for w in wavelengths),
+           record if isinstance(record, bool) else tuple(record), bool(image_record))
     cache = getattr(host, "_lowered", None)
     if not isinstance(cache, dict):
         cache = {}
@@ -192,9 +199,20 @@ def lens_for(optic_or_group, wavelengths, record=False):
             host._lowered = cache
         except AttributeError:
             pass
-    if key not in cache:
-        cache[key] = DeviceLens(lower_surface_group(sg, wavelengths, record=record))
-    return cache[key]
+    table = lower_surface_group(sg, wavelengths, record=record)
+    if image_record:
+        table.final_mat = -1
+    fp = table.fingerprint()
+    hit = cache.get(key)
+    if hit is None or hit.fingerprint != fp:
+        old = hit
+        hit = DeviceLens(table)
+        hit.fingerprint = fp
+        if old is not None and old.table.surfaces.shape == table.surfaces.shape:
+            # an edited lens starts from the previous Newton schedules (verified anyway)
+            hit.sched_cache = old.sched_cache
+        cache[key] = hit
+    return hit
 
 
 # --------------------------------------------------------------------------------------
@@ -208,6 +226,7 @@ def _run(dlens: DeviceLens, launch, n_rays, group_len, keys, newton_mode="refere
     n_groups = max(1, -(-n_rays // group_len))
     need_status = with_status and dlens.table.has_zernike
     status = torch.zeros(1, dtype=torch.int32, device=dev) if need_status else None
+    dlens.last_schedule = None  # the verified [n_groups][S] update counts (VJP replay)
     if not dlens.newton or n_rays == 0:
         opt = _native.ort_options(_abi.NEWTON_SCHEDULE, 0, None)
         launch(opt, None, status)
@@ -231,6 +250,7 @@ def _run(dlens: DeviceLens, launch, n_rays, group_len, keys, newton_mode="refere
         ok, new = dlens.verify(sched, st)
         if ok:
             dlens.remember(keys, sched)
+            dlens.last_schedule = sched
             _raise_status(status)
             return
         sched = new
@@ -374,11 +394,14 @@ class RealRayTracer:
         dev = dlens.device
         px = torch.as_tensor(Px, device=dev)
         py = torch.as_tensor(Py, device=dev)
+        keys = [("trace", tuple(np.round(Hx, 15)), tuple(np.round(Hy, 15)), float(wavelength), n_p)]
+        if autodiff.wants_grad(optic):
+            return self._trace_grad(dlens, segs, px, py, n, n_p, wavelength, keys,
+                                    record == "all")
         out = RealRays.empty(n, wavelength, device=dev)
         rec = None
         if record == "all":
             rec = torch.empty(dlens.table.n_rec * 8 * n, dtype=torch.float64, device=dev)
-        keys = [("trace", tuple(np.round(Hx, 15)), tuple(np.round(Hy, 15)), float(wavelength), n_p)]
         trace_pupil(dlens, segs, px, py, out, n, n_p, n, keys=keys, rec=rec,
                     newton_mode=newton_mode)
         self._record(dlens, out, rec, n, segs, px, py, n_p)
@@ -418,6 +441,35 @@ class RealRayTracer:
         trace_pupil(dlens, segs, px, py, out, n, 1, n, pupil_per_ray=True,
                     keys=[("generic", float(wavelength), n)], rec=rec, newton_mode=newton_mode)
         self._record(dlens, out, rec, n, segs, px, py, 1, pupil_per_ray=True)
+        return out
+
+    def _trace_grad(self, dlens, segs, px, py, n, n_p, wavelength, keys, record_all):
+        """Optic.trace with torch-tensor Zernike coefficients that require grad (the
+        reference's torch-autograd path): returned rays and the image
+        record are autograd-connected to the coefficients (autodiff.py)."""
+        if float(dlens.table.final_thickness) != 0.0:
+            raise NotImplementedError("differentiable trace with a non-zero image-space "
+                                      "thickness (last surface) is not supported")
+        seg_dev = upload_segments(segs, dlens.device)
+        if record_all:  # non-differentiable records of every surface first
+            rec = torch.empty(dlens.table.n_rec * 8 * n, dtype=torch.float64, device=dlens.device)
+            tmp = RealRays.empty(n, wavelength, device=dlens.device)
+            trace_pupil(dlens, seg_dev, px, py, tmp, n, n_p, n, keys=keys, rec=rec)
+            self._record(dlens, tmp, rec, n, segs, px, py, n_p)
+        outs = autodiff.trace_pupil_grad(self.optic, dlens, seg_dev, px, py, n, n_p,
+                                         wavelength, keys)
+        out = RealRays.__new__(RealRays)
+        for a, t in zip(_abi.RAY_FIELDS, outs, strict=True):
+            setattr(out, a, t)
+        out.w = torch.full((n,), float(wavelength), dtype=torch.float64, device=dlens.device)
+        out.is_normalized = True
+        sg = self.optic.surface_group
+        if not record_all:
+            sg.reset()
+        img = sg.surfaces[-1]
+        for nm, a in zip(("x", "y", "z", "L", "M", "N", "intensity", "opd"),
+                         _abi.RAY_FIELDS, strict=True):
+            setattr(img, nm, getattr(out, a))
         return out
 
     def _record(self, dlens, out, rec, n, segs, px, py, seg_len, pupil_per_ray=False):

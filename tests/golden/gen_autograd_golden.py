@@ -1,0 +1,96 @@
+"""Gradient golden vectors (config 5): the REFERENCE's torch backend (CPU, float64)
+differentiating the Three-Mirror Anastigmat trace w.r.t. its Zernike coefficients.
+
+Test infrastructure only, run in the build container (never on the GPU box):
+
+    PYTHONPATH=tests/golden/shims:/root/reference PYTHONDONTWRITEBYTECODE=1 \
+        python tests/golden/gen_autograd_golden.py
+
+Writes tests/golden/autograd_tma.npz:
+  rms_*      RayOperand.rms_spot_size(optic, -1, 0, 1, 32, 0.587, "uniform")
+             (operand/ray.py:300-340) and d rms / d c for the coefficients of the three
+             Zernike mirrors (surfaces 1-3, 10 fringe coefficients each)
+  wsum_*     loss = sum_f sum_rays w_f * out_f over the image rays of Optic.trace at field
+             (0, -1) with seeded weights w_f (x, y, z, L, M, N, opd), and its gradient:
+             exercises every output's cotangent
+  Px, Py     the pupil samples (uniform 32 -> 812 points)
+
+Reference quirk recorded here: with be.grad_mode enabled (what TorchOptimizer does,
+optimizer/torch/base.py:50-53) the Zernike normal's factorial weights are built from
+requires-grad tensors and backward() fails with "derivative for aten::floor_divide is
+not implemented" (zernike/base.py:289). The gradients below are therefore taken with
+grad_mode off and the coefficient tensors as the only leaves requiring grad -- the same
+graph over the same values.
+"""
+
+from __future__ import annotations
+
+import os
+import sys
+
+sys.dont_write_bytecode = True
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+import gen_golden  # noqa: E402  (sets the numpy backend at import)
+import optiland.backend as be  # noqa: E402
+from optiland.distribution import create_distribution  # noqa: E402
+from optiland.optimization.operand.ray import RayOperand  # noqa: E402
+
+FIELDS = ("x", "y", "z", "L", "M", "N", "opd")
+
+
+def _leaf_coefficients(lens):
+    leaves = []
+    for si in (1, 2, 3):
+        geo = lens.surface_group.surfaces[si].geometry
+        c = geo.coefficients
+        c = c.detach() if torch.is_tensor(c) else torch.as_tensor(np.asarray(c))
+        t = c.clone().to(torch.float64).requires_grad_(True)
+        geo.coefficients = t
+        leaves.append(t)
+    return leaves
+
+
+def main():
+    be.set_backend("torch")
+    be.set_precision("float64")
+    out = {}
+
+    lens = gen_golden.tma("fringe")
+    leaves = _leaf_coefficients(lens)
+    rms = RayOperand.rms_spot_size(lens, -1, 0.0, 1.0, 32, 0.587, "uniform")
+    rms.backward()
+    out["rms_value"] = np.array(float(rms))
+    out["rms_grad"] = np.stack([t.grad.numpy().copy() for t in leaves])
+
+    lens = gen_golden.tma("fringe")
+    leaves = _leaf_coefficients(lens)
+    d = create_distribution("uniform")
+    d.generate_points(32)
+    px = np.asarray(d.x.detach() if torch.is_tensor(d.x) else d.x, dtype=np.float64)
+    py = np.asarray(d.y.detach() if torch.is_tensor(d.y) else d.y, dtype=np.float64)
+    rng = np.random.default_rng(1234)
+    w = {f: rng.standard_normal(px.size) for f in FIELDS}
+    rays = lens.trace(0.0, -1.0, 0.587, num_rays=32, distribution="uniform")
+    loss = 0.0
+    for f in FIELDS:
+        loss = loss + torch.sum(torch.as_tensor(w[f]) * getattr(rays, f))
+    loss.backward()
+    out["wsum_value"] = np.array(float(loss))
+    out["wsum_grad"] = np.stack([t.grad.numpy().copy() for t in leaves])
+    for f in FIELDS:
+        out[f"wsum_w_{f}"] = w[f]
+    out["Px"] = px
+    out["Py"] = py
+    np.savez_compressed(os.path.join(HERE, "autograd_tma.npz"), **out)
+    print("rms", out["rms_value"], "wsum", out["wsum_value"])
+    print(out["rms_grad"])
+
+
+if __name__ == "__main__":
+    main()
