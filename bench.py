@@ -1,9 +1,10 @@
 """Benchmark: ray-surface intersections/s, 10-surface double-Gauss, 1M pupil rays, fp64.
 
 BASELINE.json metric "ray-surface intersections/sec at 1M pupil rays, 10-surf
-double-Gauss" on configs[1]: DoubleGauss (samples/objectives.py:75-114; S = 12 traced
-surfaces = len(surfaces) - 1), 1,000,000 random pupil rays (numpy default_rng, seed 0 +
-rank), field Hy = 1 (14 deg), lambda = 0.5876 um, fp64.
+double-Gauss" on configs[1] (the default, --config 2): DoubleGauss
+(samples/objectives.py:75-114; S = 12 traced surfaces = len(surfaces) - 1), 1,000,000
+random pupil rays (numpy default_rng, seed 0 + rank), field Hy = 1 (14 deg),
+lambda = 0.5876 um, fp64.
 
 One step = one fused launch (ort_trace_pupil) that generates the rays from the resident
 pupil samples and traces them through every surface to the image plane, writing
@@ -11,10 +12,21 @@ x, y, z, L, M, N, i, opd to HBM: exactly RealRayTracer.trace's work
 (real_ray_tracer.py:37-97) for one (field, wavelength) on 1M rays.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--rays R] [--no-cpu]
+                    [--config {2,3,4,5}]
 
 N > 1: launched by torch.distributed.run, one process per GPU; every rank traces its
 own 1M-ray shard (weak scaling, no collective on the data path); the elapsed time is
-the max over ranks. value = N * R * S / time.
+the max over ranks. value = N * R * S * K / time.
+
+The other BASELINE configs are secondary measurements, same JSON shape:
+  --config 3  RT-asph (even aspheres, Newton sag): 5 fields x 3 lambda x 4M pupil rays
+              (60M rays, one launch, one Newton group per (field, lambda))
+  --config 4  ReverseTelephoto 7 fields x 7 lambda x 2M rays per pair (seed = pair),
+              98M rays sharded over the ranks (strong scaling) + all_gather of the image
+              (x, y) over RCCL
+  --config 5  TMA (3 Zernike mirrors), 1M random rays, Hy = 1: one optimisation step =
+              lens update + differentiable trace + rms_spot_size + backward (VJP kernel)
+              + Adam step on the 30 coefficients
 """
 
 from __future__ import annotations
@@ -37,7 +49,8 @@ SPEC_FP64_VEC_TFLOPS = 78.6  # AMD MI355X FP64 vector spec (not in the local gui
 
 def _flops_per_ray(table):
     """Algorithmic fp64 operations per ray (+,-,*,/,sqrt each 1) counted from
-    optiland_pr_amd/csrc/ort_core.h for the lowered surfaces (DESIGN.md 'Roofline')."""
+    optiland_pr_amd/csrc/ort_core.h for the lowered surfaces (DESIGN.md 'Roofline').
+    Closed-form surfaces only (the config-2 kernel)."""
     from optiland_pr_amd import _abi
 
     f = 20  # ray generation (ray_generator.py:71-89)
@@ -54,12 +67,210 @@ def _flops_per_ray(table):
     return f
 
 
+class Workload:
+    """One bench configuration: step() is the timed unit; units = intersections/step."""
+
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
+def _pupil(seed, n, dev, torch):
+    from optiland_pr_amd.distribution import RandomDistribution
+
+    d = RandomDistribution(seed=seed)
+    d.generate_points(n)
+    return (torch.as_tensor(np.ascontiguousarray(d.x), device=dev),
+            torch.as_tensor(np.ascontiguousarray(d.y), device=dev), d)
+
+
+def config2(args, dev, rank, world, torch):
+    from optiland_pr_amd.lowering import segment_params
+    from optiland_pr_amd.raytrace import RealRays, lens_for, trace_pupil, upload_segments
+    from optiland_pr_amd.samples import DoubleGauss
+
+    wl, Hx, Hy = 0.5876, 0.0, 1.0
+    lens = DoubleGauss()
+    dl = lens_for(lens, [wl])
+    S = dl.table.n_surfaces
+    R = args.rays
+    px, py, _ = _pupil(rank, R, dev, torch)  # rank 0 = the parity workload (seed 0)
+    seg = np.stack([segment_params(lens, Hx, Hy, 0)])
+    seg_dev = upload_segments(seg, dev)
+    out = RealRays.empty(R, wl, device=dev)
+
+    def step():
+        trace_pupil(dl, seg_dev, px, py, out, R, R, R)
+
+    def cpu():
+        return _cpu_trace(lens, dl, seg, args.cpu_rays, 1)
+
+    flops = _flops_per_ray(dl.table)
+    return Workload(
+        metric="ray-surface intersections/sec at 1M pupil rays, 10-surf double-Gauss",
+        unit="intersections/s", units=world * R * S, step=step, scaling="weak",
+        config={
+            "workload": "DoubleGauss (samples/objectives.py:75-114), 1 field Hy=1 (14 deg), "
+                        "lambda 0.5876 um, fused ray generation + 12-surface trace to image",
+            "rays_per_gpu": R, "surfaces": S, "intersections_per_step": world * R * S,
+            "parallelism": f"dp{world} (ray shards, no collective)"},
+        kernel="trace_closed_kernel<F_GEN> (ort_trace_pupil)", launches=1,
+        bytes_per_launch=R * (16 + 64), flops_per_ray=flops, pmc_file="hbm_traffic.json",
+        cpu=cpu, rays=R)
+
+
+def config3(args, dev, rank, world, torch):
+    from optiland_pr_amd.lowering import segment_params
+    from optiland_pr_amd.raytrace import RealRays, lens_for, trace_pupil, upload_segments
+    from optiland_pr_amd.samples import ReverseTelephotoAsphere
+
+    wls = [0.4861, 0.5876, 0.6563]
+    fields = [(0.0, float(h)) for h in np.linspace(0, 1, 5)]
+    lens = ReverseTelephotoAsphere()
+    dl = lens_for(lens, wls)
+    S = dl.table.n_surfaces
+    n_p = args.rays if args.rays != 1_000_000 else 4_000_000
+    px, py, _ = _pupil(rank, n_p, dev, torch)
+    EPL, EPD = lens.paraxial.EPL(), lens.paraxial.EPD()
+    seg = np.stack([segment_params(lens, hx, hy, wi, EPL, EPD)
+                    for hx, hy in fields for wi in range(len(wls))])
+    seg_dev = upload_segments(seg, dev)
+    n = n_p * len(seg)
+    out = RealRays.empty(n, 0.0, device=dev)
+    keys = [("bench3", k) for k in range(len(seg))]
+
+    def step():
+        trace_pupil(dl, seg_dev, px, py, out, n, n_p, n_p, keys=keys)
+
+    def cpu():
+        return _cpu_trace(lens, dl, seg, max(1, args.cpu_rays // 10), len(seg))
+
+    return Workload(
+        metric="ray-surface intersections/sec, RT-asph even-asphere (Newton sag), 5 fields x "
+               "3 lambda x 4M pupil rays",
+        unit="intersections/s", units=world * n * S, step=step, scaling="weak",
+        config={"workload": "ReverseTelephoto + even aspheres on surfaces 2, 13 (SURVEY 8d.3), "
+                            "5 fields x 3 lambda, one launch, Newton group per pair",
+                "rays_per_gpu": n, "pupil_per_pair": n_p, "surfaces": S,
+                "parallelism": f"dp{world} (ray shards, no collective)"},
+        kernel="trace_kernel<F_GEN|KM_EVEN> (ort_trace_pupil)", launches=1,
+        bytes_per_launch=n_p * 16 + n * 64, flops_per_ray=None, pmc_file="hbm_traffic_c3.json",
+        cpu=cpu, rays=n)
+
+
+def config4(args, dev, rank, world, torch):
+    from optiland_pr_amd import distributed
+    from optiland_pr_amd.lowering import segment_params
+    from optiland_pr_amd.raytrace import RealRays, lens_for, trace_pupil, upload_segments
+    from optiland_pr_amd.samples import ReverseTelephoto
+
+    wls = [float(w) for w in np.linspace(0.4861, 0.6563, 7)]
+    fields = [(0.0, float(h)) for h in np.linspace(0, 1, 7)]
+    lens = ReverseTelephoto()
+    dl = lens_for(lens, wls)
+    S = dl.table.n_surfaces
+    n_p = args.rays if args.rays != 1_000_000 else 2_000_000
+    EPL, EPD = lens.paraxial.EPL(), lens.paraxial.EPD()
+    pairs = [(hx, hy, wi) for hx, hy in fields for wi in range(len(wls))]
+    seg = np.stack([segment_params(lens, hx, hy, wi, EPL, EPD) for hx, hy, wi in pairs])
+    a, b = distributed.shard_range(n_p, rank, world)
+    n_loc = b - a
+    from optiland_pr_amd.distribution import RandomDistribution
+
+    pxs, pys = [], []
+    for k in range(len(pairs)):  # seed = pair index; this rank's slice of every pair
+        d = RandomDistribution(seed=k)
+        d.generate_points(n_p)
+        pxs.append(d.x[a:b])
+        pys.append(d.y[a:b])
+    px = torch.as_tensor(np.concatenate(pxs), device=dev)
+    py = torch.as_tensor(np.concatenate(pys), device=dev)
+    seg_dev = upload_segments(seg, dev)
+    n = n_loc * len(pairs)
+    out = RealRays.empty(n, 0.0, device=dev)
+
+    def step():
+        trace_pupil(dl, seg_dev, px, py, out, n, n_loc, n, pupil_per_ray=True)
+        if world > 1:
+            distributed.gather_image_plane(out.x, out.y, n_loc, len(pairs), n_p)
+
+    def cpu():
+        return _cpu_trace(lens, dl, seg, max(1, args.cpu_rays // 10), len(seg))
+
+    return Workload(
+        metric="ray-surface intersections/sec, ReverseTelephoto 7 fields x 7 lambda x 2M rays, "
+               "sharded + RCCL gather of image-plane hits",
+        unit="intersections/s", units=n_p * len(pairs) * S, step=step, scaling="strong",
+        config={"workload": "ReverseTelephoto (samples/objectives.py:117-173), 49 (field, "
+                            "lambda) pairs x 2M rays (seed = pair), all_gather of image x,y",
+                "rays_total": n_p * len(pairs), "surfaces": S,
+                "parallelism": f"dp{world} (pupil shards of every pair) + all_gather"},
+        kernel="trace_closed_kernel<F_GEN> (ort_trace_pupil)", launches=1,
+        bytes_per_launch=n * (16 + 64), flops_per_ray=None, pmc_file="hbm_traffic_c4.json",
+        cpu=cpu, rays=n)
+
+
+def config5(args, dev, rank, world, torch):
+    from optiland_pr_amd.operands import RayOperand
+    from optiland_pr_amd.samples import ThreeMirrorAnastigmat
+
+    R = args.rays
+    _, _, d = _pupil(rank, R, dev, torch)
+    lens = ThreeMirrorAnastigmat()
+    leaves = []
+    for si in (1, 2, 3):
+        g = lens.surface_group.surfaces[si].geometry
+        t = torch.tensor(np.asarray(g.coefficients), dtype=torch.float64, requires_grad=True)
+        g.coefficients = t
+        leaves.append(t)
+    opt = torch.optim.Adam(leaves, lr=1e-7)
+    S = 4
+    state = {}
+
+    def step():
+        opt.zero_grad()
+        loss = RayOperand.rms_spot_size(lens, -1, 0.0, 1.0, R, 0.587, d)
+        loss.backward()
+        opt.step()
+        state["loss"] = float(loss.detach())
+
+    def cpu():
+        from optiland_pr_amd.lowering import lower_surface_group, segment_params
+
+        table = lower_surface_group(lens.surface_group, [0.587])
+        seg = np.stack([segment_params(lens, 0.0, 1.0, 0)])
+
+        class _DL:
+            pass
+
+        dl = _DL()
+        dl.table = table
+        res = _cpu_trace(lens, dl, seg, max(1, args.cpu_rays // 10), 1)
+        res["sample"] += " (forward trace only: the oracle has no derivative path)"
+        return res
+
+    return Workload(
+        metric="TMA Zernike optimisation steps: ray-surface intersections/sec of forward + "
+               "backward (d rms_spot / d coeff) at 1M rays",
+        unit="intersections/s", units=world * R * S, step=step, scaling="weak",
+        config={"workload": "TMA (Tutorial_7d), 3 fringe-Zernike mirrors x 10 coefficients, "
+                            "1M random rays, Hy=1, lambda 0.587: lens update + trace + "
+                            "rms_spot_size + backward (VJP) + Adam",
+                "rays_per_gpu": R, "surfaces": S, "parameters": 30,
+                "parallelism": f"dp{world} (independent replicas)"},
+        kernel="vjp_kernel<4, KM_ZERN> (ort_trace_pupil_vjp)", launches=None,
+        bytes_per_launch=None, flops_per_ray=None, pmc_file=None, cpu=cpu, rays=R, state=state)
+
+
+CONFIGS = {2: config2, 3: config3, 4: config4, 5: config5}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--rays", type=int, default=1_000_000)
+    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-rays", type=int, default=1_000_000)
     args = ap.parse_args()
@@ -76,33 +287,15 @@ def main():
     dev = torch.device("cuda", local_rank if world > 1 else 0)
 
     from optiland_pr_amd import _native
-    from optiland_pr_amd.distribution import RandomDistribution
-    from optiland_pr_amd.lowering import segment_params
-    from optiland_pr_amd.raytrace import RealRays, lens_for, trace_pupil, upload_segments
-    from optiland_pr_amd.samples import DoubleGauss
 
     _native.load()
-    wl, Hx, Hy = 0.5876, 0.0, 1.0
-    lens = DoubleGauss()
-    dl = lens_for(lens, [wl])
-    S = dl.table.n_surfaces
-    R = args.rays
-    d = RandomDistribution(seed=rank)  # rank 0 = the parity workload (seed 0)
-    d.generate_points(R)
-    px = torch.as_tensor(np.ascontiguousarray(d.x), device=dev)
-    py = torch.as_tensor(np.ascontiguousarray(d.y), device=dev)
-    seg = np.stack([segment_params(lens, Hx, Hy, 0)])
-    seg_dev = upload_segments(seg, dev)
-    out = RealRays.empty(R, wl, device=dev)
-
-    def step():
-        trace_pupil(dl, seg_dev, px, py, out, R, R, R)
+    w = CONFIGS[args.config](args, dev, rank, world, torch)
 
     for _ in range(args.warmup):
-        step()
+        w.step()
     torch.cuda.synchronize()
 
-    # per-launch kernel time with HIP events on the stream the kernel is launched on
+    # per-step device time with HIP events on the stream the kernels are launched on
     # (torch's current stream: raytrace._stream_handle)
     stream = torch.cuda.current_stream()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -113,7 +306,7 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.steps):
         ev[k][0].record(stream)
-        step()
+        w.step()
         ev[k][1].record(stream)
     torch.cuda.synchronize()
     if world > 1:
@@ -125,113 +318,123 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    units = world * R * S  # ray-surface intersections per step, all ranks
-    value = units * args.steps / elapsed
+    value = w.units * args.steps / elapsed
     ms_per_step = elapsed / args.steps * 1e3
 
     if rank == 0:
-        # algorithmic HBM bytes per launch: 16 B/ray pupil in + 64 B/ray rays out
-        # (+ 64 B segment descriptor, negligible)
-        bytes_per_launch = R * (16 + 64)
-        achieved_gbs = bytes_per_launch / (kern_ms * 1e-3) / 1e9
-        flops = _flops_per_ray(dl.table) * R
-        achieved_tf = flops / (kern_ms * 1e-3) / 1e12
-        pmc = _pmc_summary()
-        traffic = pmc.get("bytes_per_launch")
-        hw_flops = pmc.get("fp64_flops_per_launch")
         line = {
-            "metric": "ray-surface intersections/sec at 1M pupil rays, 10-surf double-Gauss",
+            "metric": w.metric,
             "value": value,
-            "unit": "intersections/s",
+            "unit": w.unit,
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": w.scaling,
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (random pupil rays, numpy default_rng seed = rank)",
-            "config": {
-                "workload": "DoubleGauss (samples/objectives.py:75-114), 1 field Hy=1 (14 deg), "
-                            "lambda 0.5876 um, fused ray generation + 12-surface trace to image",
-                "rays_per_gpu": R,
-                "surfaces": S,
-                "intersections_per_step": units,
-                "parallelism": f"dp{world} (ray shards, no collective)",
-            },
-            "roofline": {
-                "bound": "hbm",
-                "achieved": achieved_gbs,
-                "peak": SPEC_HBM_TBPS * 1e3,
-                "unit": "GB/s",
-                "frac": achieved_gbs / (SPEC_HBM_TBPS * 1e3),
-                "traffic": traffic,
-                "kernel": "trace_closed_kernel<F_GEN> (ort_trace_pupil)",
-                "kernel_ms": kern_ms,
-                "algorithmic_bytes_per_launch": bytes_per_launch,
-                "note": "the fused trace is FP64-VALU bound (see roofline_fp64); HBM frac is "
-                        "reported because BASELINE asks for it",
-            },
-            "roofline_fp64": {
-                "bound": "fp64_valu",
-                "achieved": achieved_tf,
-                "peak": SPEC_FP64_VEC_TFLOPS,
-                "unit": "TFLOP/s",
-                "frac": achieved_tf / SPEC_FP64_VEC_TFLOPS,
-                "flops_per_ray": _flops_per_ray(dl.table),
-                "note": "achieved = algorithmic ops (+,-,*,/,sqrt = 1 each); the hardware "
-                        "executes IEEE / and sqrt as ~10-instruction FMA sequences",
-                "hw_counted": None if hw_flops is None else {
-                    "fp64_flops_per_launch": hw_flops,
-                    "achieved": hw_flops / (kern_ms * 1e-3) / 1e12,
-                    "frac": hw_flops / (kern_ms * 1e-3) / 1e12 / SPEC_FP64_VEC_TFLOPS,
-                    "source": "SQ_INSTS_VALU_FLOPS_FP64 x 64 (profiles/hbm_traffic.json)",
-                },
-            },
-            "cpu_baseline": None if args.no_cpu else _cpu_baseline(lens, dl, seg, args.cpu_rays),
+            "config": w.config,
+            "roofline": _roofline(w, kern_ms),
         }
+        if w.flops_per_ray is not None:
+            line["roofline_fp64"] = _roofline_fp64(w, kern_ms)
+        if getattr(w, "state", None):
+            line["config"]["final_loss"] = w.state.get("loss")
+        line["cpu_baseline"] = None if args.no_cpu or world > 1 else w.cpu()
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
 
 
-def _pmc_summary():
+def _roofline(w, kern_ms):
+    if w.bytes_per_launch is None:
+        return {"bound": "fp64_valu", "achieved": None, "peak": SPEC_FP64_VEC_TFLOPS,
+                "unit": "TFLOP/s", "frac": None, "traffic": None, "kernel": w.kernel,
+                "step_device_ms": kern_ms,
+                "note": "multi-launch optimisation step; per-kernel times in "
+                        "profiles/r01_config5_kernel_stats.csv"}
+    pmc = _pmc_summary(w.pmc_file)
+    achieved = w.bytes_per_launch / (kern_ms * 1e-3) / 1e9
+    return {
+        "bound": "hbm",
+        "achieved": achieved,
+        "peak": SPEC_HBM_TBPS * 1e3,
+        "unit": "GB/s",
+        "frac": achieved / (SPEC_HBM_TBPS * 1e3),
+        "traffic": pmc.get("bytes_per_launch"),
+        "kernel": w.kernel,
+        "kernel_ms": kern_ms,
+        "algorithmic_bytes_per_launch": w.bytes_per_launch,
+        "note": "the fused trace is FP64-VALU bound (see roofline_fp64); HBM frac is "
+                "reported because BASELINE asks for it",
+    }
+
+
+def _roofline_fp64(w, kern_ms):
+    pmc = _pmc_summary(w.pmc_file)
+    hw_flops = pmc.get("fp64_flops_per_launch")
+    achieved_tf = w.flops_per_ray * w.rays / (kern_ms * 1e-3) / 1e12
+    return {
+        "bound": "fp64_valu",
+        "achieved": achieved_tf,
+        "peak": SPEC_FP64_VEC_TFLOPS,
+        "unit": "TFLOP/s",
+        "frac": achieved_tf / SPEC_FP64_VEC_TFLOPS,
+        "flops_per_ray": w.flops_per_ray,
+        "note": "achieved = algorithmic ops (+,-,*,/,sqrt = 1 each); the hardware "
+                "executes IEEE / and sqrt as ~10-instruction FMA sequences",
+        "hw_counted": None if hw_flops is None else {
+            "fp64_flops_per_launch": hw_flops,
+            "achieved": hw_flops / (kern_ms * 1e-3) / 1e12,
+            "frac": hw_flops / (kern_ms * 1e-3) / 1e12 / SPEC_FP64_VEC_TFLOPS,
+            "source": f"SQ_INSTS_VALU_FLOPS_FP64 x 64 (profiles/{w.pmc_file})",
+        },
+    }
+
+
+def _pmc_summary(name):
     """Per-launch HBM bytes / FP64 FLOPs of the trace kernel from the committed
-    rocprofv3 PMC summary (profiles/hbm_traffic.json, tools/profile_hbm.py); {} if absent."""
-    p = os.path.join(HERE, "profiles", "hbm_traffic.json")
+    rocprofv3 PMC summary (profiles/<name>, tools/profile_hbm.py); {} if absent."""
+    if not name:
+        return {}
     try:
-        with open(p) as f:
+        with open(os.path.join(HERE, "profiles", name)) as f:
             return json.load(f)
     except (OSError, ValueError):
         return {}
 
 
-def _cpu_baseline(lens, dl, seg, n_rays):
+def _cpu_trace(lens, dl, seg, n_rays, n_pairs):
     """The oracle (NumPy restatement of the reference, oracle/trace_np.py) timed on this
-    host on the same workload: n_rays rays of the DoubleGauss, one process."""
+    host on a bounded sample of the same workload: n_rays pupil rays per pair for up to
+    3 of the workload's pairs, one process; reported per intersection."""
     from oracle import trace_np
     from optiland_pr_amd.distribution import RandomDistribution
 
     d = RandomDistribution(seed=0)
     d.generate_points(n_rays)
     px, py = np.asarray(d.x), np.asarray(d.y)
+    use = list(range(min(n_pairs, 3)))
     times = []
     for _ in range(2):
         t0 = time.perf_counter()
-        r = trace_np.generate_rays(seg[0], px, py)
-        trace_np.trace_segment(dl.table, r, 0)
+        for k in use:
+            r = trace_np.generate_rays(seg[k], px, py)
+            trace_np.trace_segment(dl.table, r, int(seg[k]["lambda_idx"]))
         times.append(time.perf_counter() - t0)
     t = min(times)
     S = dl.table.n_surfaces
     return {
-        "value": n_rays * S / t,
+        "value": n_rays * len(use) * S / t,
         "unit": "intersections/s",
         "cores": 1,
         "kind": "port",
-        "sample": f"{n_rays} DoubleGauss rays x {S} surfaces (generation + trace), NumPy "
-                  f"oracle, 1 process, best of 2: {t:.2f} s on {platform.processor() or platform.machine()}",
+        "sample": f"{n_rays} rays x {len(use)} (field, lambda) pair(s) x {S} surfaces "
+                  f"(generation + trace), NumPy oracle, 1 process, best of 2: {t:.2f} s on "
+                  f"{platform.processor() or platform.machine()}",
     }
 
 
