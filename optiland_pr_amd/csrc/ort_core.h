@@ -429,117 +429,99 @@ ORT_INLINE T ipow(const T& x, int p) {
   return r;
 }
 
-// even_asphere.py:82-98
+// The Newton step evaluates the sag AND the normal at the same point P(t)
+// (newton_raphson.py:140-146 then :154-166), so the geometries below evaluate both in one
+// pass: the conic square root sqrt(1 - (1 + k) r^2 / R^2) is the same IEEE expression in
+// the sag (standard.py:73-87) and in the normal's denominator and is computed once;
+// everything else keeps the reference's per-expression order. want_normal = false: the
+// sag alone (the convergence check after the last update).
+
+// even_asphere.py:82-98 (sag) + :100-129 (normal)
 template <class T, class PD>
-ORT_INLINE T sag_even(const T& x, const T& y, double R, double k, PD C, int nc) {
+ORT_INLINE T sagnorm_even(const T& x, const T& y, double R, double k, PD C, int nc,
+                          bool want_normal, T& nx, T& ny, T& nz) {
   const T r2 = x * x + y * y;
-  T z = sag_conic(r2, R, k);
+  const T q = sqrt(1.0 - (1.0 + k) * r2 / (R * R));
+  T z = r2 / (R * (1.0 + q));
   T rp = r2;  // r2 ** (i + 1)
   for (int i = 0; i < nc; ++i) {
     z = z + C[i] * rp;
     rp = rp * r2;
   }
+  if (want_normal) {
+    const T denom = R * q;
+    T dfdx = x / denom;
+    T dfdy = y / denom;
+    T rq = T(1.0);  // r2 ** i
+    for (int i = 0; i < nc; ++i) {
+      const double f = 2.0 * (double)(i + 1);
+      dfdx = dfdx + f * x * C[i] * rq;
+      dfdy = dfdy + f * y * C[i] * rq;
+      rq = rq * r2;
+    }
+    const T mag = sqrt(dfdx * dfdx + dfdy * dfdy + 1.0);
+    nx = dfdx / mag;
+    ny = dfdy / mag;
+    nz = -1.0 / mag;
+  }
   return z;
 }
 
-// even_asphere.py:100-129
+// odd_asphere.py:73-89 (sag) + :91-130 (normal; non-finite per-term slopes are zeroed,
+// :112-122)
 template <class T, class PD>
-ORT_INLINE void normal_even(const T& x, const T& y, double R, double k, PD C, int nc, T& nx,
-                            T& ny, T& nz) {
-  const T r2 = x * x + y * y;
-  const T denom = R * sqrt(1.0 - (1.0 + k) * r2 / (R * R));
-  T dfdx = x / denom;
-  T dfdy = y / denom;
-  T rp = T(1.0);  // r2 ** i
-  for (int i = 0; i < nc; ++i) {
-    const double f = 2.0 * (double)(i + 1);
-    dfdx = dfdx + f * x * C[i] * rp;
-    dfdy = dfdy + f * y * C[i] * rp;
-    rp = rp * r2;
-  }
-  const T mag = sqrt(dfdx * dfdx + dfdy * dfdy + 1.0);
-  nx = dfdx / mag;
-  ny = dfdy / mag;
-  nz = -1.0 / mag;
-}
-
-// odd_asphere.py:73-89
-template <class T, class PD>
-ORT_INLINE T sag_odd(const T& x, const T& y, double R, double k, PD C, int nc) {
+ORT_INLINE T sagnorm_odd(const T& x, const T& y, double R, double k, PD C, int nc,
+                         bool want_normal, T& nx, T& ny, T& nz) {
   const T r2 = x * x + y * y;
   const T r = sqrt(r2);
-  T z = sag_conic(r2, R, k);
+  const T q = sqrt(1.0 - (1.0 + k) * r2 / (R * R));
+  T z = r2 / (R * (1.0 + q));
   T rp = r;  // r ** (i + 1)
   for (int i = 0; i < nc; ++i) {
     z = z + C[i] * rp;
     rp = rp * r;
   }
+  if (want_normal) {
+    const T denom = R * q;
+    T dfdx = x / denom;
+    T dfdy = y / denom;
+    T rq = 1.0 / r;  // r ** (i - 1): 1/r, 1, r, r*r, r*r*r, ...
+    for (int i = 0; i < nc; ++i) {
+      const double f = (double)(i + 1);
+      T xt = f * x * C[i] * rq;
+      T yt = f * y * C[i] * rq;
+      if (!isfinite(vv(xt))) xt = T(0.0);
+      if (!isfinite(vv(yt))) yt = T(0.0);
+      rq = (i == 0) ? T(1.0) : (i == 1 ? r : rq * r);
+      dfdx = dfdx + xt;
+      dfdy = dfdy + yt;
+    }
+    const T mag = sqrt(dfdx * dfdx + dfdy * dfdy + 1.0);
+    nx = dfdx / mag;
+    ny = dfdy / mag;
+    nz = -1.0 / mag;
+  }
   return z;
 }
 
-// odd_asphere.py:91-130 (non-finite per-term slopes are zeroed, :112-122)
-template <class T, class PD>
-ORT_INLINE void normal_odd(const T& x, const T& y, double R, double k, PD C, int nc, T& nx,
-                           T& ny, T& nz) {
-  const T r2 = x * x + y * y;
-  const T r = sqrt(r2);
-  const T denom = R * sqrt(1.0 - (1.0 + k) * r2 / (R * R));
-  T dfdx = x / denom;
-  T dfdy = y / denom;
-  T rp = 1.0 / r;  // r ** (i - 1): 1/r, 1, r, r*r, r*r*r, ...
-  for (int i = 0; i < nc; ++i) {
-    const double f = (double)(i + 1);
-    T xt = f * x * C[i] * rp;
-    T yt = f * y * C[i] * rp;
-    if (!isfinite(vv(xt))) xt = T(0.0);
-    if (!isfinite(vv(yt))) yt = T(0.0);
-    rp = (i == 0) ? T(1.0) : (i == 1 ? r : rp * r);
-    dfdx = dfdx + xt;
-    dfdy = dfdy + yt;
-  }
-  const T mag = sqrt(dfdx * dfdx + dfdy * dfdy + 1.0);
-  nx = dfdx / mag;
-  ny = dfdy / mag;
-  nz = -1.0 / mag;
-}
-
 // ---- Zernike: geometries/zernike.py:133-246 + zernike/base.py:42-299 ----------------
-// R_n^|m|(rho) = sum_k a_k rho^(n-2k)         (base.py:228-253)
-template <class T, class PD>
-ORT_INLINE T zern_radial(PD a, int n, int nr, const T& rho) {
-  T v = T(0.0);
-#pragma unroll 1
-  for (int k = 0; k < nr; ++k) v = v + a[k] * ipow(rho, n - 2 * k);
-  return v;
-}
-// dR/drho = sum_k d_k rho^(n-2k-1)            (base.py:272-299)
-template <class T, class PD>
-ORT_INLINE T zern_radial_deriv(PD d, int n, int nr, const T& rho) {
-  T v = T(0.0);
-#pragma unroll 1
-  for (int k = 0; k < nr; ++k) {
-    if (n - 2 * k < 0) continue;
-    const T p = (n - 2 * k - 1) >= 0 ? ipow(rho, n - 2 * k - 1) : T(0.0);
-    v = v + d[k] * p;
-  }
-  return v;
-}
-
-// cos(m phi), sin(m phi) for m >= 0 from cos phi, sin phi by the angle-addition
-// recurrence (the reference evaluates cos(m * atan2(y, x)); a few ulps apart, see
-// DESIGN.md Parity). phi = atan2(yn, xn) gives cos phi = xn / rho, sin phi = yn / rho,
-// and atan2(0, 0) = 0 at rho == 0.
-template <class T>
-ORT_INLINE void cos_sin_m(int m, const T& c1, const T& s1, T& cm, T& sm) {
-  T c = T(1.0), s = T(0.0);
-#pragma unroll 1
-  for (int q = 0; q < m; ++q) {
-    const T cn = c * c1 - s * s1;
-    s = s * c1 + c * s1;
-    c = cn;
-  }
-  cm = c;
-  sm = s;
+// Per term (n, m), with a = |m|, rho = r / R_norm, phi = atan2(yn, xn):
+//   R_n^a(rho)   = sum_k a_k rho^(n-2k) = rho^a * P(rho^2)            (base.py:228-253)
+//   dR/drho      = sum_k d_k rho^(n-2k-1), terms with n-2k-1 < 0 dropped (:259-299)
+//                = rho^(a-1) * Q(rho^2)  (a >= 1),   rho * Q'(rho^2)  (a = 0)
+// P, Q by Horner in rho^2 from the host's a_k, d_k (highest power first), rho^a and
+// cos/sin(a phi) by one recurrence from cos phi = xn / rho, sin phi = yn / rho. The
+// reference sums libm powers term by term and takes cos/sin of a*atan2: rounding-level
+// differences (DESIGN.md Parity). A term whose coefficient is 0 adds exactly 0 to the
+// sag and is skipped by the reference's normal (zernike.py:213-214), so it is skipped
+// here -- unless the derivative kernels seed a tangent on it (the sag's derivative
+// w.r.t. that coefficient is not zero).
+ORT_INLINE bool zseeded(const ZSeed&, int, double*) { return false; }
+template <int P>
+ORT_INLINE bool zseeded(const ZSeed& zs, int j, Dual<P>*) {
+  if (!zs.param) return false;
+  const int p = zs.param[j] - zs.p0;
+  return p >= 0 && p < P;
 }
 
 template <class T>
@@ -547,88 +529,107 @@ ORT_INLINE void polar_unit(const T& xn, const T& yn, const T& rho, T& c1, T& s1)
   if (vv(rho) > 0.0) {
     c1 = xn / rho;
     s1 = yn / rho;
-  } else {
+  } else {  // atan2(0, 0) = 0
     c1 = T(1.0);
     s1 = T(0.0);
   }
 }
 
-// zernike.py:133-161 (sets range_error on |x/R_norm| > 1 or |y/R_norm| > 1)
+// sag (zernike.py:133-161; sets range_error on |x/R_norm| > 1 or |y/R_norm| > 1,
+// :234-246) and, with want_normal, the normal (zernike.py:163-231; the normal omits the
+// normalisation constant: reference quirk)
 template <class T, class PD, class PZ>
-ORT_INLINE T sag_zernike(const T& x, const T& y, double R, double k, double Rn, PZ Tm, int t0,
-                         int nt, PD coef, const ZSeed& zs, bool& range_error) {
+ORT_INLINE T sagnorm_zernike(const T& x, const T& y, double R, double k, double Rn, PZ Tm,
+                             int t0, int nt, PD coef, const ZSeed& zs, bool want_normal,
+                             bool& range_error, T& nx, T& ny, T& nz) {
   const T xn = x / Rn;
   const T yn = y / Rn;
-  if (::fabs(vv(xn)) > 1.0 || ::fabs(vv(yn)) > 1.0) range_error = true;  // :234-246
+  if (::fabs(vv(xn)) > 1.0 || ::fabs(vv(yn)) > 1.0) range_error = true;
   const T rho = sqrt(xn * xn + yn * yn);
   T c1, s1;
   polar_unit(xn, yn, rho, c1, s1);
+  const T rho2 = rho * rho;
   const T r2 = x * x + y * y;
-  T z = sag_conic(r2, R, k);
+  const T q = sqrt(1.0 - (1.0 + k) * r2 / (R * R));
+  const T z = r2 / (R * (1.0 + q));
   T total = T(0.0);  // python sum() starts at int 0; 0 + t == t exactly
+  // normal: conic part + chain rule through (rho, phi) with the reference's eps guards
+  const double eps = 1e-14;
+  T dzdx, dzdy, drho_dx, drho_dy, dphi_dx, dphi_dy;
+  if (want_normal) {
+    const T denominator = R * q;
+    dzdx = x / denominator;
+    dzdy = y / denominator;
+    const double Rn2 = Rn * Rn;
+    // (the reference returns zeros when EVERY rho is 0; per ray (x/Rn^2)/(0+eps) = 0 too)
+    drho_dx = (x / Rn2) / (rho + eps);
+    drho_dy = (y / Rn2) / (rho + eps);
+    const T rho2e = rho2 + eps;
+    const double inv_rn = 1.0 / Rn;
+    dphi_dx = -(yn) / rho2e * inv_rn;
+    dphi_dy = (xn) / rho2e * inv_rn;  // "+(x_norm)": unary plus
+  }
   for (int j = 0; j < nt; ++j) {
     const ort_zernike_term t = Tm[t0 + j];
-    const T rad = zern_radial(coef + t.rad_off, t.n, t.n_rad, rho);
-    T cm, sm;
-    cos_sin_m(t.m >= 0 ? t.m : -t.m, c1, s1, cm, sm);
+    if (t.c == 0.0 && !zseeded(zs, t0 + j, (T*)nullptr)) continue;
+    const int am = t.m >= 0 ? t.m : -t.m;
+    // cos(am phi), sin(am phi), rho^am, rho^(am-1)
+    T cm = T(1.0), sm = T(0.0), pm = T(1.0), pm1 = T(1.0);
+#pragma unroll 1
+    for (int qq = 0; qq < am; ++qq) {
+      const T cn = cm * c1 - sm * s1;
+      sm = sm * c1 + cm * s1;
+      cm = cn;
+      pm1 = pm;
+      pm = pm * rho;
+    }
+    const PD a = coef + t.rad_off;
+    T P = T(a[0]);
+#pragma unroll 1
+    for (int kk = 1; kk < t.n_rad; ++kk) P = P * rho2 + a[kk];
+    const T rt = P * pm;  // R_n^am(rho)
     const T az = t.m >= 0 ? cm : sm;  // base.py:206-226
     const T c = zcoef(t.c, t0 + j, zs, (T*)nullptr);
-    total = total + c * t.norm * rad * az;
+    total = total + c * t.norm * rt * az;
+    if (want_normal && t.c != 0.0) {
+      const PD d = a + t.n_rad;
+      T rd;
+      if (am > 0) {
+        T Q = T(d[0]);
+#pragma unroll 1
+        for (int kk = 1; kk < t.n_rad; ++kk) Q = Q * rho2 + d[kk];
+        rd = Q * pm1;
+      } else if (t.n_rad > 1) {
+        T Q = T(d[0]);
+#pragma unroll 1
+        for (int kk = 1; kk < t.n_rad - 1; ++kk) Q = Q * rho2 + d[kk];
+        rd = Q * rho;
+      } else {
+        rd = T(0.0);
+      }
+      T dr, dp;
+      if (t.m == 0) {  // base.py:124-136
+        dr = rd;
+        dp = T(0.0);
+      } else if (t.m > 0) {
+        dr = rd * cm;
+        dp = (double)(-t.m) * rt * sm;
+      } else {
+        dr = rd * sm;
+        dp = (double)am * rt * cm;
+      }
+      dzdx = dzdx + c * (dr * drho_dx + dp * dphi_dx);
+      dzdy = dzdy + c * (dr * drho_dy + dp * dphi_dy);
+    }
+  }
+  if (want_normal) {
+    T norm = sqrt(dzdx * dzdx + dzdy * dzdy + 1.0);
+    norm = vv(norm) < eps ? T(1.0) : norm;
+    nx = dzdx / norm;
+    ny = dzdy / norm;
+    nz = -1.0 / norm;
   }
   return z + total;
-}
-
-// zernike.py:163-231 (the normal omits the normalisation constant: reference quirk)
-template <class T, class PD, class PZ>
-ORT_INLINE void normal_zernike(const T& x, const T& y, double R, double k, double Rn, PZ Tm,
-                               int t0, int nt, PD coef, const ZSeed& zs, T& nx, T& ny, T& nz) {
-  const T r2 = x * x + y * y;
-  const T denominator = R * sqrt(1.0 - (1.0 + k) * r2 / (R * R));
-  T dzdx = x / denominator;
-  T dzdy = y / denominator;
-  const double eps = 1e-14;
-  const T xn = x / Rn;
-  const T yn = y / Rn;
-  const T rho = sqrt(xn * xn + yn * yn);
-  T c1, s1;
-  polar_unit(xn, yn, rho, c1, s1);
-  const double Rn2 = Rn * Rn;
-  // (the reference returns zeros when EVERY rho is 0; per ray (x/Rn^2)/(0+eps) = 0 too)
-  const T drho_dx = (x / Rn2) / (rho + eps);
-  const T drho_dy = (y / Rn2) / (rho + eps);
-  const T rho2e = rho * rho + eps;
-  const double inv_rn = 1.0 / Rn;
-  const T dphi_dx = -(yn) / rho2e * inv_rn;
-  const T dphi_dy = (xn) / rho2e * inv_rn;  // "+(x_norm)": unary plus
-  for (int j = 0; j < nt; ++j) {
-    const ort_zernike_term t = Tm[t0 + j];
-    if (t.c == 0.0) continue;
-    const PD a = coef + t.rad_off;
-    const T rt = zern_radial(a, t.n, t.n_rad, rho);
-    const T rd = zern_radial_deriv(a + t.n_rad, t.n, t.n_rad, rho);
-    const int am = t.m >= 0 ? t.m : -t.m;
-    T cm, sm;
-    cos_sin_m(am, c1, s1, cm, sm);
-    T dr, dp;
-    if (t.m == 0) {  // base.py:128-137
-      dr = rd;
-      dp = T(0.0);
-    } else if (t.m > 0) {
-      dr = rd * cm;
-      dp = (double)(-t.m) * rt * sm;
-    } else {
-      dr = rd * sm;
-      dp = (double)am * rt * cm;
-    }
-    const T c = zcoef(t.c, t0 + j, zs, (T*)nullptr);
-    dzdx = dzdx + c * (dr * drho_dx + dp * dphi_dx);
-    dzdy = dzdy + c * (dr * drho_dy + dp * dphi_dy);
-  }
-  T norm = sqrt(dzdx * dzdx + dzdy * dzdy + 1.0);
-  norm = vv(norm) < eps ? T(1.0) : norm;
-  nx = dzdx / norm;
-  ny = dzdy / norm;
-  nz = -1.0 / norm;
 }
 
 // Sag and normal of a Newton-iterated geometry (EvenAsphere / OddAsphere / Zernike).
@@ -637,66 +638,50 @@ ORT_INLINE void normal_zernike(const T& x, const T& y, double R, double k, doubl
 enum : unsigned { KM_EVEN = 1u, KM_ODD = 2u, KM_ZERN = 4u };
 
 template <unsigned KM, class T, class PD, class PZ>
-ORT_INLINE T newton_sag(const ort_surface& s, PD coef, PZ zern, const ZSeed& zs, const T& x,
-                        const T& y, bool& range_error) {
+ORT_INLINE T newton_sagnorm(const ort_surface& s, PD coef, PZ zern, const ZSeed& zs,
+                            const T& x, const T& y, bool want_normal, bool& range_error,
+                            T& nx, T& ny, T& nz) {
   const PD C = coef + s.coef_off;
   if constexpr ((KM & KM_EVEN) != 0) {
     if (KM == KM_EVEN || s.geometry == ORT_GEOM_EVEN_ASPHERE)
-      return sag_even(x, y, s.radius, s.conic, C, s.n_coef);
+      return sagnorm_even(x, y, s.radius, s.conic, C, s.n_coef, want_normal, nx, ny, nz);
   }
   if constexpr ((KM & KM_ODD) != 0) {
     if ((KM & ~KM_ODD) == 0 || s.geometry == ORT_GEOM_ODD_ASPHERE)
-      return sag_odd(x, y, s.radius, s.conic, C, s.n_coef);
+      return sagnorm_odd(x, y, s.radius, s.conic, C, s.n_coef, want_normal, nx, ny, nz);
   }
   if constexpr ((KM & KM_ZERN) != 0) {
-    return sag_zernike(x, y, s.radius, s.conic, s.norm_radius, zern, s.coef_off, s.n_coef,
-                       coef, zs, range_error);
+    return sagnorm_zernike(x, y, s.radius, s.conic, s.norm_radius, zern, s.coef_off,
+                           s.n_coef, coef, zs, want_normal, range_error, nx, ny, nz);
   }
+  nx = ny = nz = T(NAN);
   return T(NAN);
 }
 
 template <unsigned KM, class T, class PD, class PZ>
 ORT_INLINE void newton_normal(const ort_surface& s, PD coef, PZ zern, const ZSeed& zs,
                               const T& x, const T& y, T& nx, T& ny, T& nz) {
-  const PD C = coef + s.coef_off;
-  if constexpr ((KM & KM_EVEN) != 0) {
-    if (KM == KM_EVEN || s.geometry == ORT_GEOM_EVEN_ASPHERE) {
-      normal_even(x, y, s.radius, s.conic, C, s.n_coef, nx, ny, nz);
-      return;
-    }
-  }
-  if constexpr ((KM & KM_ODD) != 0) {
-    if ((KM & ~KM_ODD) == 0 || s.geometry == ORT_GEOM_ODD_ASPHERE) {
-      normal_odd(x, y, s.radius, s.conic, C, s.n_coef, nx, ny, nz);
-      return;
-    }
-  }
-  if constexpr ((KM & KM_ZERN) != 0) {
-    normal_zernike(x, y, s.radius, s.conic, s.norm_radius, zern, s.coef_off, s.n_coef, coef,
-                   zs, nx, ny, nz);
-    return;
-  }
-  nx = ny = nz = T(NAN);
+  bool rerr = false;  // the normal never raises (zernike.py:163-231)
+  (void)newton_sagnorm<KM>(s, coef, zern, zs, x, y, true, rerr, nx, ny, nz);
 }
 
-// newton_raphson.py:140-146: residual f(t) = sag(P(t)) - z(t)
+// One Newton evaluation at t (newton_raphson.py:140-146): returns f(t) = sag(P(t)) - z(t)
+// and, with want_normal, the normal at P(t) for the update.
 template <unsigned KM, class T, class PD, class PZ>
-ORT_INLINE T newton_residual(const ort_surface& s, PD coef, PZ zern, const ZSeed& zs,
-                             const RayT<T>& r, const T& t, bool& range_error) {
+ORT_INLINE T newton_eval(const ort_surface& s, PD coef, PZ zern, const ZSeed& zs,
+                         const RayT<T>& r, const T& t, bool want_normal, bool& range_error,
+                         T& nx, T& ny, T& nz) {
   const T xi = r.x + t * r.L;
   const T yi = r.y + t * r.M;
   const T zi = r.z + t * r.N;
-  return newton_sag<KM>(s, coef, zern, zs, xi, yi, range_error) - zi;
+  return newton_sagnorm<KM>(s, coef, zern, zs, xi, yi, want_normal, range_error, nx, ny, nz) -
+         zi;
 }
 
-// newton_raphson.py:154-166: t_new = t - f / f'(t)
-template <unsigned KM, class T, class PD, class PZ>
-ORT_INLINE T newton_update(const ort_surface& s, PD coef, PZ zern, const ZSeed& zs,
-                           const RayT<T>& r, const T& t, const T& f) {
-  const T xi = r.x + t * r.L;
-  const T yi = r.y + t * r.M;
-  T nx, ny, nz;
-  newton_normal<KM>(s, coef, zern, zs, xi, yi, nx, ny, nz);
+// newton_raphson.py:154-166: t_new = t - f / f'(t) from the normal at P(t)
+template <class T>
+ORT_INLINE T newton_step(const RayT<T>& r, const T& t, const T& f, const T& nx, const T& ny,
+                         const T& nz) {
   const T nzs = ::fabs(vv(nz)) > 1e-14 ? nz : T(1e-14);
   const T fx = -nx / nzs;
   const T fy = -ny / nzs;

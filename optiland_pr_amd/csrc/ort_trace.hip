@@ -148,11 +148,13 @@ __device__ inline double newton_distance(const KArgs& a, const ort_surface& s, i
     int j = 0;
     for (; j < max_iter; ++j) {
       bool rerr = false;
-      const double f = ort::newton_residual<(FEAT & F_KM)>(s, cst(a.coef), cst(a.zern), kNoSeed, r, t, rerr);
+      double nx, ny, nz;
+      const double f = ort::newton_eval<(FEAT & F_KM)>(s, cst(a.coef), cst(a.zern), kNoSeed, r,
+                                                      t, true, rerr, nx, ny, nz);
       if (active && rerr) range_error = true;
       const bool conv = !active || !(fabs(f) >= tol);
       if (__all(conv)) break;
-      t = ort::newton_update<(FEAT & F_KM)>(s, cst(a.coef), cst(a.zern), kNoSeed, r, t, f);
+      t = ort::newton_step(r, t, f, nx, ny, nz);
     }
     if (a.stats && (threadIdx.x & 63) == 0)
       atomicMax(&a.stats[(group_uniform ? group : 0) * a.n_surf + si].max_updates, j);
@@ -167,14 +169,17 @@ __device__ inline double newton_distance(const KArgs& a, const ort_surface& s, i
     if (!__any(lane_on)) break;
     if (lane_on) {
       bool rerr = false;
-      const double f = ort::newton_residual<(FEAT & F_KM)>(s, cst(a.coef), cst(a.zern), kNoSeed, r, t, rerr);
+      double nx, ny, nz;
+      const bool upd = j < U;  // sag + normal at P(t) for an update, the sag alone after
+      const double f = ort::newton_eval<(FEAT & F_KM)>(s, cst(a.coef), cst(a.zern), kNoSeed, r,
+                                                      t, upd, rerr, nx, ny, nz);
       // the reference evaluates sag at j = 0..U-1 always, and at j = U only when the
       // loop broke there (U < max_iter)
       if (rerr && (j < U || U < max_iter)) range_error = true;
       const bool conv = fabs(f) < tol;  // NaN never converges (np.max propagates NaN)
       if (conv && j < 64) mask |= 1ull << j;
       if (!conv) last_bad = j;
-      if (j < U) t = ort::newton_update<(FEAT & F_KM)>(s, cst(a.coef), cst(a.zern), kNoSeed, r, t, f);
+      if (upd) t = ort::newton_step(r, t, f, nx, ny, nz);
     }
   }
   if (a.stats) {
@@ -446,8 +451,10 @@ __global__ __launch_bounds__(kBlock) void vjp_kernel(const KArgs a, const JArgs 
         const int U = a.sched ? a.sched[group * a.n_surf + si] : s.max_iter;
         bool rerr = false;
         for (int it = 0; it < U; ++it) {
-          const D f = ort::newton_residual<KM>(s, cst(a.coef), cst(a.zern), zs, r, t, rerr);
-          t = ort::newton_update<KM>(s, cst(a.coef), cst(a.zern), zs, r, t, f);
+          D nx, ny, nz;
+          const D f = ort::newton_eval<KM>(s, cst(a.coef), cst(a.zern), zs, r, t, true, rerr,
+                                           nx, ny, nz);
+          t = ort::newton_step(r, t, f, nx, ny, nz);
         }
       }
     }
