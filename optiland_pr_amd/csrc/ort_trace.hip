@@ -96,6 +96,18 @@ __device__ inline int wave_max_i32(int v) {
   return v;
 }
 
+// Same-address atomics from every wave of a large grid serialise in L2, and almost every
+// wave would leave the value unchanged (the Newton statistics of one group agree across
+// its waves): read first (relaxed) and issue the atomic only when it changes something.
+__device__ inline void and_if_changes(uint64_t* p, uint64_t v) {
+  const uint64_t cur = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if ((cur & v) != cur) atomicAnd((unsigned long long*)p, (unsigned long long)v);
+}
+__device__ inline void max_if_changes(int32_t* p, int32_t v) {
+  const int32_t cur = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (v > cur) atomicMax(p, v);
+}
+
 // Table lookup n_tab[lam][mat]: a uniform scalar load when the lens is traced at one
 // wavelength (the common case), else a per-lane load of the small L1-resident table.
 __device__ inline double tab(const double* t, int n_lambda, int n_mat, int lam, int mat) {
@@ -157,7 +169,7 @@ __device__ inline double newton_distance(const KArgs& a, const ort_surface& s, i
       t = ort::newton_step(r, t, f, nx, ny, nz);
     }
     if (a.stats && (threadIdx.x & 63) == 0)
-      atomicMax(&a.stats[(group_uniform ? group : 0) * a.n_surf + si].max_updates, j);
+      max_if_changes(&a.stats[(group_uniform ? group : 0) * a.n_surf + si].max_updates, j);
     return t;
   }
   // ORT_NEWTON_SCHEDULE: exactly U updates, plus the check evaluation at j = U.
@@ -192,12 +204,12 @@ __device__ inline double newton_distance(const KArgs& a, const ort_surface& s, i
       mask = wave_and_u64(mask);
       last_bad = wave_max_i32(last_bad);
       if ((threadIdx.x & 63) == 0) {
-        if (mask != ~0ull) atomicAnd((unsigned long long*)&st->conv_mask, (unsigned long long)mask);
-        if (last_bad >= 0) atomicMax(&st->last_bad, last_bad);
+        if (mask != ~0ull) and_if_changes(&st->conv_mask, mask);
+        if (last_bad >= 0) max_if_changes(&st->last_bad, last_bad);
       }
     } else if (active) {
-      if (mask != ~0ull) atomicAnd((unsigned long long*)&st->conv_mask, (unsigned long long)mask);
-      if (last_bad >= 0) atomicMax(&st->last_bad, last_bad);
+      if (mask != ~0ull) and_if_changes(&st->conv_mask, mask);
+      if (last_bad >= 0) max_if_changes(&st->last_bad, last_bad);
     }
   }
   return t;
@@ -478,11 +490,19 @@ __global__ __launch_bounds__(kBlock) void vjp_kernel(const KArgs a, const JArgs 
     if (j.cot.i) cot_acc(acc, j.cot.i, rid, ort::intensity(r));
     cot_acc(acc, j.cot.opd, rid, r.opd);
   }
+  // wave sums -> LDS -> one atomic per block and parameter
+  __shared__ double part[kBlock / 64][P];
 #pragma unroll
   for (int k = 0; k < P; ++k) {
     const double v = wave_sum(acc[k]);
-    if ((threadIdx.x & 63) == 0 && j.p0 + k < j.n_param && v != 0.0)
-      atomicAdd(&j.grad[j.p0 + k], v);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6][k] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < P && j.p0 + (int)threadIdx.x < j.n_param) {
+    double v = 0.0;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) v += part[w][threadIdx.x];
+    if (v != 0.0) atomicAdd(&j.grad[j.p0 + threadIdx.x], v);
   }
 }
 
