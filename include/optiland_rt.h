@@ -249,6 +249,23 @@ int ort_trace_pupil_vjp(const ort_lens* lens, const double* px, const double* py
                         const int32_t* zern_param, int32_t n_param,
                         const ort_rays* cotangent, double* grad, void* stream);
 
+/* Per-geometry primitives of traced surface `surface` of `lens`, in the surface's local
+ * frame (no localize / globalize), for n points or rays:
+ *   ort_surface_sag_normal: sag(x, y) and the unit normal at (x, y)
+ *     (BaseGeometry.sag / surface_normal, e.g. standard.py:73-87, :154-167,
+ *     even_asphere.py:82-129, zernike.py:133-231); any output may be NULL.
+ *   ort_surface_distance: distance t along each ray to the surface (geometry.distance,
+ *     plane.py:61-77, standard.py:89-140, newton_raphson.py:119-168); Newton surfaces
+ *     follow the global stop rule over the n rays with opt / newton_stat exactly as
+ *     ort_trace_sequential with group_len = n (opt NULL: max_iter updates).
+ * status: ORT_STATUS_ZERNIKE_RANGE as for the trace (zernike.py:234-246). */
+int ort_surface_sag_normal(const ort_lens* lens, int32_t surface, const double* x,
+                           const double* y, int64_t n, double* sag, double* nx, double* ny,
+                           double* nz, int32_t* status, void* stream);
+int ort_surface_distance(const ort_lens* lens, int32_t surface, const ort_rays* rays,
+                         int64_t n, const ort_options* opt, double* t,
+                         ort_newton_stat* newton_stat, int32_t* status, void* stream);
+
 /* Ray generation only (ray_generator.py:28-106): fills rays_out from pupil points. */
 int ort_generate_rays(const double* px, const double* py, ort_rays* rays_out,
                       const ort_batch* batch, void* stream);

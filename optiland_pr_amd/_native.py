@@ -56,7 +56,7 @@ class ort_options(C.Structure):
 
 
 EXPORTS = ("ort_abi_version", "ort_trace_sequential", "ort_trace_pupil", "ort_trace_pupil_vjp",
-           "ort_generate_rays")
+           "ort_surface_sag_normal", "ort_surface_distance", "ort_generate_rays")
 
 _lib = None
 
@@ -92,6 +92,14 @@ def load(path: str | None = None):
     lib.ort_trace_pupil_vjp.argtypes = [P(ort_lens), C.c_void_p, C.c_void_p, P(ort_batch),
                                         P(ort_options), C.c_void_p, C.c_int32, P(ort_rays),
                                         C.c_void_p, C.c_void_p]
+    lib.ort_surface_sag_normal.restype = C.c_int
+    lib.ort_surface_sag_normal.argtypes = [P(ort_lens), C.c_int32, C.c_void_p, C.c_void_p,
+                                           C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p,
+                                           C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.ort_surface_distance.restype = C.c_int
+    lib.ort_surface_distance.argtypes = [P(ort_lens), C.c_int32, P(ort_rays), C.c_int64,
+                                         P(ort_options), C.c_void_p, C.c_void_p, C.c_void_p,
+                                         C.c_void_p]
     lib.ort_generate_rays.restype = C.c_int
     lib.ort_generate_rays.argtypes = [C.c_void_p, C.c_void_p, P(ort_rays), P(ort_batch),
                                       C.c_void_p]

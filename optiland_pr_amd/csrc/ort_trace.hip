@@ -506,6 +506,125 @@ __global__ __launch_bounds__(kBlock) void vjp_kernel(const KArgs a, const JArgs 
   }
 }
 
+// ---------------------------------------------------------------------------------
+// Geometry primitives of one surface in its local frame (geometries/*.py: sag(x, y),
+// surface_normal(rays), distance(rays)) -- the reference's per-geometry API, used by
+// its geometry tests and by analysis code that probes a surface.
+// ---------------------------------------------------------------------------------
+struct GArgs {
+  int32_t surface;
+  int32_t mode;  // 0: sag / normal at (x, y); 1: distance of the rays in a.in
+  const double* x;
+  const double* y;
+  double* sag;
+  double* nx;
+  double* ny;
+  double* nz;
+  double* t;
+};
+
+template <uint32_t KM>
+__global__ __launch_bounds__(kBlock) void geom_kernel(const KArgs a, const GArgs g) {
+  const int64_t rid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const bool active = rid < a.n_rays;
+  const int64_t r_ld = active ? rid : 0;
+  const ort_surface s = cst(a.surf)[g.surface];
+  bool range_error = false;
+  if (g.mode == 0) {
+    const double x = g.x[r_ld], y = g.y[r_ld];
+    double z, nx, ny, nz;
+    if (s.geometry == ORT_GEOM_PLANE) {  // plane.py:45-59, :79-98
+      z = 0.0;
+      nx = 0.0; ny = 0.0; nz = 1.0;
+    } else if (s.geometry == ORT_GEOM_STANDARD) {  // standard.py:73-87, :154-167
+      z = ort::sag_conic(x * x + y * y, s.radius, s.conic);
+      ort::normal_conic(x, y, s.radius, s.conic, nx, ny, nz);
+    } else {
+      if constexpr (KM != 0) {
+        z = ort::newton_sagnorm<KM>(s, cst(a.coef), cst(a.zern), kNoSeed, x, y, true,
+                                    range_error, nx, ny, nz);
+      } else {
+        z = nx = ny = nz = __builtin_nan("");
+      }
+    }
+    if (active) {
+      if (g.sag) g.sag[rid] = z;
+      if (g.nx) g.nx[rid] = nx;
+      if (g.ny) g.ny[rid] = ny;
+      if (g.nz) g.nz[rid] = nz;
+    }
+  } else {
+    ort::Ray r;
+    r.x = a.in.x[r_ld];
+    r.y = a.in.y[r_ld];
+    r.z = a.in.z[r_ld];
+    r.L = a.in.L[r_ld];
+    r.M = a.in.M[r_ld];
+    r.N = a.in.N[r_ld];
+    r.i = 1.0;
+    r.opd = 0.0;
+    r.att = 0.0;
+    double t;
+    if (s.geometry == ORT_GEOM_PLANE) {
+      t = ort::distance_plane(r);
+    } else if (s.geometry == ORT_GEOM_STANDARD) {
+      t = ort::distance_conic(r, s.radius, s.conic, (s.flags & ORT_SURF_RADIUS_INF) != 0);
+    } else {
+      if constexpr (KM != 0) {
+        t = newton_distance<KM>(a, s, g.surface, r, active, 0, true, range_error);
+      } else {
+        t = __builtin_nan("");
+      }
+    }
+    if (active && g.t) g.t[rid] = t;
+  }
+  if (range_error && active && a.status) atomicOr(a.status, (int)ORT_STATUS_ZERNIKE_RANGE);
+}
+
+typedef void (*GeomFn)(const KArgs, const GArgs);
+
+int fill_args(KArgs& a, const ort_lens* lens, const ort_batch* batch, const ort_options* opt,
+              double* rec, ort_newton_stat* stats, int32_t* status, uint32_t& feat);
+int init_outputs(const KArgs& a, hipStream_t stream);
+
+GeomFn pick_geom(uint32_t km) {
+  switch (km) {
+    case 0: return geom_kernel<0>;
+    case 1: return geom_kernel<1>;
+    case 2: return geom_kernel<2>;
+    case 3: return geom_kernel<3>;
+    case 4: return geom_kernel<4>;
+    case 5: return geom_kernel<5>;
+    case 6: return geom_kernel<6>;
+    default: return geom_kernel<7>;
+  }
+}
+
+int launch_geom(const ort_lens* lens, int32_t surface, int64_t n, const ort_rays* rays,
+                GArgs g, const ort_options* opt, ort_newton_stat* stats, int32_t* status,
+                hipStream_t stream) {
+  if (!lens || n < 0) return ORT_ERR_ARG;
+  if (n == 0) return ORT_OK;
+  if (surface < 0 || surface >= lens->n_surfaces) return ORT_ERR_ARG;
+  const ort_options dflt{ORT_NEWTON_SCHEDULE, 0, nullptr};
+  ort_batch b{};
+  b.n_rays = n;
+  b.seg_len = n;
+  b.group_len = n;  // one reference call: the Newton stop rule spans all n rays
+  KArgs a{};
+  uint32_t feat = 0;
+  int rc = fill_args(a, lens, &b, opt ? opt : &dflt, nullptr, stats, status, feat);
+  if (rc) return rc;
+  if (rays) a.in = *rays;
+  if ((rc = init_outputs(a, stream))) return rc;
+  const int64_t blocks = (n + kBlock - 1) / kBlock;
+  if (blocks > 0x7fffffff) return ORT_ERR_ARG;
+  g.surface = surface;
+  hipLaunchKernelGGL(pick_geom(feat & F_KM), dim3((unsigned)blocks), dim3(kBlock), 0, stream,
+                     a, g);
+  return hipGetLastError() == hipSuccess ? ORT_OK : ORT_ERR_LAUNCH;
+}
+
 typedef void (*VjpFn)(const KArgs, const JArgs);
 
 template <int P>
@@ -719,6 +838,33 @@ int ort_trace_pupil_vjp(const ort_lens* lens, const double* px, const double* py
     p0 += P;
   }
   return ORT_OK;
+}
+
+int ort_surface_sag_normal(const ort_lens* lens, int32_t surface, const double* x,
+                           const double* y, int64_t n, double* sag, double* nx, double* ny,
+                           double* nz, int32_t* status, void* stream) {
+  if (n > 0 && (!x || !y)) return ORT_ERR_ARG;
+  GArgs g{};
+  g.mode = 0;
+  g.x = x;
+  g.y = y;
+  g.sag = sag;
+  g.nx = nx;
+  g.ny = ny;
+  g.nz = nz;
+  return launch_geom(lens, surface, n, nullptr, g, nullptr, nullptr, status,
+                     (hipStream_t)stream);
+}
+
+int ort_surface_distance(const ort_lens* lens, int32_t surface, const ort_rays* rays,
+                         int64_t n, const ort_options* opt, double* t,
+                         ort_newton_stat* newton_stat, int32_t* status, void* stream) {
+  if (n > 0 && (!rays || !t)) return ORT_ERR_ARG;
+  GArgs g{};
+  g.mode = 1;
+  g.t = t;
+  return launch_geom(lens, surface, n, rays, g, opt, newton_stat, status,
+                     (hipStream_t)stream);
 }
 
 int ort_generate_rays(const double* px, const double* py, ort_rays* rays_out,

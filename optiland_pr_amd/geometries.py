@@ -36,6 +36,27 @@ class BaseGeometry:
     def zernike_terms(self):
         return None
 
+    # per-geometry API (geometries/base.py:61-110), evaluated on the MI355X in the
+    # geometry's local frame; results are float64 device tensors
+    def sag(self, x=0, y=0):
+        """Sag z(x, y) (e.g. standard.py:73-87, even_asphere.py:82-98)."""
+        from .raytrace import geometry_sag_normal
+
+        return geometry_sag_normal(self, x, y)[0]
+
+    def surface_normal(self, rays):
+        """Unit normal (nx, ny, nz) at the rays' (x, y) (e.g. standard.py:154-167)."""
+        from .raytrace import geometry_sag_normal
+
+        return geometry_sag_normal(self, rays.x, rays.y)[1:]
+
+    def distance(self, rays):
+        """Distance along each ray to the surface (plane.py:61-77, standard.py:89-140,
+        newton_raphson.py:119-168 with its global stop rule over `rays`)."""
+        from .raytrace import geometry_distance
+
+        return geometry_distance(self, rays)
+
 
 class Plane(BaseGeometry):
     """geometries/plane.py:19-98 (t = -z/N, normal (0,0,1))."""

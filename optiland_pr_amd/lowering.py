@@ -201,6 +201,18 @@ def lower_surface_group(surface_group, wavelengths, record=False, skip_object=Tr
     )
 
 
+def lower_geometry(geometry):
+    """One-surface table for a bare geometry (the per-geometry API: sag / surface_normal /
+    distance in the geometry's local frame; materials are placeholders)."""
+    from types import SimpleNamespace
+
+    from .materials import IdealMaterial
+    from .surfaces import Surface
+
+    surf = Surface(None, IdealMaterial(1.0), geometry)
+    return lower_surface_group(SimpleNamespace(surfaces=[surf]), [0.55])
+
+
 # --------------------------------------------------------------------------------------
 # ray-generation scalars per (field, wavelength) segment
 # --------------------------------------------------------------------------------------

@@ -513,3 +513,65 @@ def trace_surface_group(sg, rays: RealRays, skip=0, newton_mode="reference"):
     if rec is not None:
         _record_into(sg, rec, n, table.rec_surfaces, rays0)
     return rays
+
+
+# --------------------------------------------------------------------------------------
+# per-geometry primitives (geometries/*.py sag / surface_normal / distance)
+# --------------------------------------------------------------------------------------
+def _geometry_lens(geometry, device=None):
+    """One-surface DeviceLens for a bare geometry, reused while its lowering is unchanged."""
+    from .lowering import lower_geometry
+
+    table = lower_geometry(geometry)
+    fp = table.fingerprint()
+    hit = getattr(geometry, "_device_lens", None)
+    if hit is None or hit.fingerprint != fp:
+        hit = DeviceLens(table, device=device)
+        hit.fingerprint = fp
+        try:
+            geometry._device_lens = hit
+        except AttributeError:
+            pass
+    return hit
+
+
+def _as_device(v, dev):
+    if torch.is_tensor(v):
+        return v.to(device=dev, dtype=torch.float64).reshape(-1).contiguous()
+    return torch.as_tensor(np.atleast_1d(np.asarray(v, dtype=np.float64)),
+                           device=dev).reshape(-1).contiguous()
+
+
+def geometry_sag_normal(geometry, x, y):
+    """-> (sag, nx, ny, nz) device tensors at the local points (x, y) (broadcast)."""
+    lib = _native.load()
+    dl = _geometry_lens(geometry)
+    dev = dl.device
+    xs, ys = _as_device(x, dev), _as_device(y, dev)
+    xs, ys = torch.broadcast_tensors(xs, ys)
+    xs, ys = xs.contiguous(), ys.contiguous()
+    n = xs.numel()
+    out = [torch.empty(n, dtype=torch.float64, device=dev) for _ in range(4)]
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    rc = lib.ort_surface_sag_normal(C.byref(dl.c), 0, _ptr(xs), _ptr(ys), n,
+                                    *(_ptr(o) for o in out), _ptr(status), _stream_handle())
+    _native.check(rc, "ort_surface_sag_normal")
+    _raise_status(status)
+    return tuple(out)
+
+
+def geometry_distance(geometry, rays):
+    """-> t (device tensor) for RealRays in the geometry's local frame."""
+    lib = _native.load()
+    dl = _geometry_lens(geometry, device=rays.x.device)
+    n = len(rays)
+    t = torch.empty(n, dtype=torch.float64, device=dl.device)
+    rays_c = rays.c_struct()
+
+    def launch(opt, stats, status):
+        rc = lib.ort_surface_distance(C.byref(dl.c), 0, C.byref(rays_c), n, C.byref(opt),
+                                      _ptr(t), _ptr(stats), _ptr(status), _stream_handle())
+        _native.check(rc, "ort_surface_distance")
+
+    _run(dl, launch, n, max(n, 1), [("distance", n)])
+    return t

@@ -344,6 +344,23 @@ def distance_newton(r: Rays, table, s, sched=None):
     return t, updates
 
 
+def sag_surface(x, y, table, s):
+    """Geometry.sag(x, y): plane.py:45-59 (0), standard.py:73-87 (conic), Newton kinds
+    through their own sag (even_asphere.py:82-98, odd_asphere.py:73-89, zernike.py:133-161)."""
+    g = int(s["geometry"])
+    x = np.asarray(x, dtype=np.float64)
+    y = np.asarray(y, dtype=np.float64)
+    if g == _abi.GEOM_PLANE:
+        return np.zeros_like(y)
+    if g == _abi.GEOM_STANDARD:
+        R, k = float(s["radius"]), float(s["conic"])
+        r2 = x**2 + y**2
+        with np.errstate(invalid="ignore", divide="ignore"):
+            return r2 / (R * (1 + np.sqrt(1 - (1 + k) * r2 / R**2)))
+    with np.errstate(invalid="ignore", divide="ignore"):
+        return _geometry_fns(table, s)[0](x, y)
+
+
 def surface_normal(r: Rays, table, s):
     g = int(s["geometry"])
     if g == _abi.GEOM_PLANE:  # plane.py:79-98

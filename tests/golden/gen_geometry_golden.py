@@ -1,0 +1,154 @@
+"""Per-geometry golden vectors: the REFERENCE's geometries (optiland/geometries/*.py)
+evaluated on the inputs of its own geometry tests (tests/test_geometries.py:23-1230:
+same constructor arguments, points and rays) plus seeded random points and rays.
+
+Test infrastructure only, run in the build container (never on the GPU box):
+
+    PYTHONPATH=tests/golden/shims:/root/reference PYTHONDONTWRITEBYTECODE=1 \
+        python tests/golden/gen_geometry_golden.py
+
+Writes tests/golden/geometry.npz (arrays "<case>/<name>") and geometry.json (the
+geometry specs). Every case records sag(x, y) and the normal at (x, y) for its points,
+and distance(rays) for its rays (one reference call over all rays of the case, so the
+Newton global stop rule spans them).
+"""
+
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+sys.dont_write_bytecode = True
+
+import numpy as np  # noqa: E402
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+import optiland.backend as be  # noqa: E402
+from optiland import geometries  # noqa: E402
+from optiland.coordinate_system import CoordinateSystem  # noqa: E402
+from optiland.rays import RealRays  # noqa: E402
+
+be.set_backend("numpy")
+
+
+def _coeffs(d, kind):
+    start = 0 if kind == "standard" else 1
+    return [d.get(i, 0.0) for i in range(start, max(d) + 1 + start)]
+
+
+# name: (spec, extra literal points from the reference tests)
+SPECS = {
+    "plane": dict(kind="plane"),
+    "sphere": dict(kind="standard", radius=10.0, conic=0.0),
+    "parabola": dict(kind="standard", radius=-20.0, conic=-1.0),
+    "conic": dict(kind="standard", radius=27.0, conic=0.5),
+    "even_sag": dict(kind="even_asphere", radius=27.0, conic=0.0, coefficients=[1e-3, -1e-5]),
+    "even_dist": dict(kind="even_asphere", radius=-41.1, conic=0.0,
+                      coefficients=[1e-3, -1e-5, 1e-7]),
+    "even_norm": dict(kind="even_asphere", radius=10.0, conic=0.5, coefficients=[1e-2]),
+    "odd_sag": dict(kind="odd_asphere", radius=27.0, conic=0.0, coefficients=[1e-3, -1e-5]),
+    "odd_dist": dict(kind="odd_asphere", radius=-41.1, conic=0.0,
+                     coefficients=[1e-3, -1e-5, 1e-7]),
+    "odd_norm": dict(kind="odd_asphere", radius=10.0, conic=0.5, coefficients=[1e-2, -1e-5]),
+    "zern_standard": dict(kind="zernike", radius=22.0, conic=0.0, norm_radius=10.0,
+                          zernike_type="standard",
+                          coefficients=_coeffs({4: 0.5, 3: 0.2, 5: 0.3, 10: 0.1, 12: 0.2},
+                                               "standard")),
+    "zern_noll": dict(kind="zernike", radius=22.0, conic=0.0, norm_radius=10.0,
+                      zernike_type="noll",
+                      coefficients=_coeffs({4: 0.5, 5: 0.2, 6: 0.3, 11: 0.2, 15: 0.1}, "noll")),
+    "zern_fringe": dict(kind="zernike", radius=22.0, conic=0.0, norm_radius=10.0,
+                        zernike_type="fringe",
+                        coefficients=_coeffs({4: 0.5, 6: 0.2, 11: 0.3, 13: 0.2, 27: 0.1},
+                                             "fringe")),
+    "zern_fringe_conic": dict(kind="zernike", radius=-50.0, conic=-0.8, norm_radius=12.0,
+                              zernike_type="fringe",
+                              coefficients=[0.0, 1e-3, -2e-3, 5e-3, 1e-3, 0.0, 2e-4, -1e-4]),
+}
+
+
+def build(spec):
+    cs = CoordinateSystem()
+    k = spec["kind"]
+    if k == "plane":
+        return geometries.Plane(cs)
+    if k == "standard":
+        return geometries.StandardGeometry(cs, radius=spec["radius"], conic=spec["conic"])
+    if k == "even_asphere":
+        return geometries.EvenAsphere(cs, radius=spec["radius"], conic=spec["conic"],
+                                      coefficients=spec["coefficients"])
+    if k == "odd_asphere":
+        return geometries.OddAsphere(cs, radius=spec["radius"], conic=spec["conic"],
+                                     coefficients=spec["coefficients"])
+    if k == "zernike":
+        return geometries.ZernikePolynomialGeometry(
+            cs, radius=spec["radius"], conic=spec["conic"], coefficients=spec["coefficients"],
+            norm_radius=spec["norm_radius"], zernike_type=spec["zernike_type"])
+    raise ValueError(k)
+
+
+def points(name, spec, rng):
+    """Sag/normal evaluation points: the reference tests' points + seeded random ones
+    inside the surface's valid region."""
+    if spec["kind"] == "zernike":
+        g = np.linspace(-10, 10, 10) * spec["norm_radius"] / 10.0
+        X, Y = np.meshgrid(g, g)  # test_geometries.py:888-905
+        r = rng.uniform(-1, 1, size=(2, 64)) * spec["norm_radius"] / np.sqrt(2)
+        return np.concatenate([X.ravel(), r[0]]), np.concatenate([Y.ravel(), r[1]])
+    base_x = [0.0, 1.0, -2.0, 0.0, 3.0, 8.0, 1.0]
+    base_y = [0.0, 1.0, 3.0, 0.0, -7.0, 2.1, 2.0]
+    lim = 4.0 if spec.get("radius", 100.0) and abs(spec.get("radius", 100.0)) < 15 else 8.0
+    r = rng.uniform(-lim, lim, size=(2, 64))
+    return np.concatenate([base_x, r[0]]), np.concatenate([base_y, r[1]])
+
+
+def rays(name, spec, rng):
+    """Distance rays: the reference tests' rays (test_geometries.py:173-205, 275-310,
+    695-720) + seeded random rays starting in front of the vertex."""
+    x = [1.0, 1.0, 2.0, 1.0]
+    y = [2.0, 2.0, 3.0, 2.0]
+    z = [-3.0, -3.0, -4.0, -10.2]
+    L0, M0 = 0.222, -0.229
+    L = [0.0, 0.0, 0.0, L0]
+    M = [0.0, 0.0, 0.0, M0]
+    N = [1.0, 1.0, 1.0, float(np.sqrt(1 - L0**2 - M0**2))]
+    n = 48
+    lim = 2.5 if spec["kind"] == "zernike" else 3.0
+    rx = rng.uniform(-lim, lim, n)
+    ry = rng.uniform(-lim, lim, n)
+    rz = rng.uniform(-6.0, -1.0, n)
+    a = rng.uniform(-0.15, 0.15, (2, n))
+    rn = np.sqrt(1 - a[0] ** 2 - a[1] ** 2)
+    return (np.concatenate([x, rx]), np.concatenate([y, ry]), np.concatenate([z, rz]),
+            np.concatenate([L, a[0]]), np.concatenate([M, a[1]]), np.concatenate([N, rn]))
+
+
+def main():
+    rng = np.random.default_rng(2024)
+    arrays = {}
+    for name, spec in SPECS.items():
+        g = build(spec)
+        px, py = points(name, spec, rng)
+        arrays[f"{name}/x"] = px
+        arrays[f"{name}/y"] = py
+        arrays[f"{name}/sag"] = np.asarray(g.sag(px, py), dtype=np.float64) * np.ones_like(px)
+        rr = RealRays(px, py, np.zeros_like(px), np.zeros_like(px), np.zeros_like(px),
+                      np.ones_like(px), np.ones_like(px), np.ones_like(px))
+        nx, ny, nz = g.surface_normal(rr)
+        for k, v in (("nx", nx), ("ny", ny), ("nz", nz)):
+            arrays[f"{name}/{k}"] = np.asarray(v, dtype=np.float64) * np.ones_like(px)
+        rx, ry, rz, rL, rM, rN = rays(name, spec, rng)
+        for k, v in (("rx", rx), ("ry", ry), ("rz", rz), ("rL", rL), ("rM", rM), ("rN", rN)):
+            arrays[f"{name}/{k}"] = v
+        rr = RealRays(rx, ry, rz, rL, rM, rN, np.ones_like(rx), np.ones_like(rx))
+        arrays[f"{name}/t"] = np.asarray(g.distance(rr), dtype=np.float64) * np.ones_like(rx)
+    np.savez_compressed(os.path.join(HERE, "geometry.npz"), **arrays)
+    with open(os.path.join(HERE, "geometry.json"), "w") as f:
+        json.dump(SPECS, f, indent=1)
+    print(f"{len(SPECS)} geometry cases")
+
+
+if __name__ == "__main__":
+    main()

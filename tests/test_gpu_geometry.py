@@ -1,0 +1,75 @@
+"""GPU: the per-geometry API (geometry.sag / surface_normal / distance, backed by
+ort_surface_sag_normal / ort_surface_distance) against the reference's outputs on its
+own geometry-test inputs (tests/golden/geometry.npz; the oracle is pinned bit-exact to
+the same vectors in test_geometry_oracle.py).
+
+Tolerances: plane / conic bit-exact. Newton kinds: the sag and normal agree to rounding
+(r^k by products instead of libm pow; Zernike radial polynomials by Horner and the
+azimuth by recurrence): rtol 1e-12, atol 1e-13. Distances: the same Newton update count
+as the reference's global rule, so rounding-level too: rtol 1e-12, atol 1e-12.
+"""
+
+import numpy as np
+import pytest
+
+from tests._geometry_cases import CASES, NEWTON_KINDS, arrays, build, specs
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.fail("needs the MI355X")
+    from optiland_pr_amd import _native
+
+    _native.load()
+    return torch
+
+
+def _cmp(got, ref, exact):
+    got = got.cpu().numpy()
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    m = ~np.isnan(ref)
+    if exact:
+        np.testing.assert_array_equal(got[m], ref[m])
+    else:
+        np.testing.assert_allclose(got[m], ref[m], rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_geometry_api_matches_reference(torch, name):
+    from optiland_pr_amd.raytrace import RealRays
+
+    spec = specs()[name]
+    exact = spec["kind"] not in NEWTON_KINDS
+    g = build(spec)
+    a = arrays(name)
+    _cmp(g.sag(a["x"], a["y"]), a["sag"], exact)
+    rays = RealRays(a["x"], a["y"], 0 * a["x"], 0 * a["x"], 0 * a["x"], 1 + 0 * a["x"], 1.0, 0.55)
+    for got, k in zip(g.surface_normal(rays), ("nx", "ny", "nz"), strict=True):
+        _cmp(got, a[k], exact)
+    rays = RealRays(a["rx"], a["ry"], a["rz"], a["rL"], a["rM"], a["rN"], 1.0, 0.55)
+    _cmp(g.distance(rays), a["t"], exact)
+
+
+def test_zernike_range_error(torch):
+    from optiland_pr_amd.coordinate_system import CoordinateSystem
+    from optiland_pr_amd.geometries import ZernikePolynomialGeometry
+    from optiland_pr_amd.raytrace import ZernikeRangeError
+
+    g = ZernikePolynomialGeometry(CoordinateSystem(), radius=22.0, coefficients=[0.1, 0.2],
+                                  norm_radius=1.0, zernike_type="fringe")
+    g.sag(np.array([-1, -0.5, 0, 0.5, 1.0]), np.zeros(5))  # test_geometries.py:1182-1184
+    for x, y in ((-1.1, 0.0), (0.0, -1.1), (1.1, 0.0), (0.0, 1.1)):
+        with pytest.raises(ZernikeRangeError, match="Zernike coordinates must be normalized"):
+            g.sag(x, y)
+    assert issubclass(ZernikeRangeError, ValueError)
+
+
+def test_scalar_default_sag(torch):
+    g = build(specs()["even_sag"])
+    assert float(g.sag()) == 0.0
+    np.testing.assert_allclose(float(g.sag(1, 1)), 0.039022474574473776, rtol=1e-15)
