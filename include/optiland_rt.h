@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define ORT_ABI_VERSION 2
+#define ORT_ABI_VERSION 3
 #define ORT_MAX_SURFACES 64
 
 /* ---- geometry kinds ----------------------------------- */
@@ -37,8 +37,21 @@ enum ort_geometry { /* see optiland/geometries */
   ORT_GEOM_STANDARD = 1,     /* standard.py:73-167 (sphere / conic)                */
   ORT_GEOM_EVEN_ASPHERE = 2, /* even_asphere.py:82-129 + newton_raphson.py:119-168 */
   ORT_GEOM_ODD_ASPHERE = 3,  /* odd_asphere.py:73-130 + newton_raphson.py:119-168  */
-  ORT_GEOM_ZERNIKE = 4       /* zernike.py:133-246 + zernike/base.py:42-299        */
+  ORT_GEOM_ZERNIKE = 4,      /* zernike.py:133-246 + zernike/base.py:42-299        */
+  ORT_GEOM_POLYNOMIAL = 5,   /* polynomial.py:93-140 (XY polynomial)               */
+  ORT_GEOM_CHEBYSHEV = 6,    /* chebyshev.py:104-215                               */
+  ORT_GEOM_BICONIC = 7,      /* biconic.py:69-158                                  */
+  ORT_GEOM_TOROIDAL = 8      /* toroidal.py:75-233                                 */
 };
+/* Coefficient blocks in lens.coef at ort_surface.coef_off (n_coef doubles):
+ *   EVEN / ODD_ASPHERE  C_0 .. C_{n-1}
+ *   POLYNOMIAL          ni, nj, C[0][0], C[0][1], ..., C[ni-1][nj-1]  (x^i y^j, row-major)
+ *   CHEBYSHEV           ni, nj, norm_x, norm_y, C[0][0], ..., C[ni-1][nj-1]
+ *   BICONIC             cx, cy, kx, ky  (c = 1/R, 0 for an infinite or zero radius);
+ *                       ort_surface.radius / conic = R_x / k_x (the Newton start guess)
+ *   TOROIDAL            R_rot, c_yz, k_yz, has_yz (0/1), n_poly, alpha_1 .. alpha_n;
+ *                       ort_surface.radius = R_yz, conic = 0 (the Newton start guess)
+ * ZERNIKE uses lens.zern[coef_off .. coef_off + n_coef) instead. */
 
 /* ---- surface flags ------------------------------------------------------------ */
 enum ort_surface_flags {
@@ -206,7 +219,8 @@ typedef struct ort_options {
 
 /* status bits written with atomicOr into *status (device int32) */
 enum ort_status {
-  ORT_STATUS_ZERNIKE_RANGE = 1u << 0 /* zernike.py:234-246 ValueError              */
+  ORT_STATUS_ZERNIKE_RANGE = 1u << 0,  /* zernike.py:234-246 ValueError            */
+  ORT_STATUS_CHEBYSHEV_RANGE = 1u << 1 /* chebyshev.py:203-215 ValueError          */
 };
 
 /* ---- entry points ------------------------------------------------------------- */

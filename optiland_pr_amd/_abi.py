@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import numpy as np
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 MAX_SURFACES = 64
 
 # enum ort_geometry
@@ -18,7 +18,12 @@ GEOM_STANDARD = 1
 GEOM_EVEN_ASPHERE = 2
 GEOM_ODD_ASPHERE = 3
 GEOM_ZERNIKE = 4
-NEWTON_GEOMETRIES = (GEOM_EVEN_ASPHERE, GEOM_ODD_ASPHERE, GEOM_ZERNIKE)
+GEOM_POLYNOMIAL = 5
+GEOM_CHEBYSHEV = 6
+GEOM_BICONIC = 7
+GEOM_TOROIDAL = 8
+FREEFORM_GEOMETRIES = (GEOM_POLYNOMIAL, GEOM_CHEBYSHEV, GEOM_BICONIC, GEOM_TOROIDAL)
+NEWTON_GEOMETRIES = (GEOM_EVEN_ASPHERE, GEOM_ODD_ASPHERE, GEOM_ZERNIKE) + FREEFORM_GEOMETRIES
 
 # enum ort_surface_flags
 SURF_REFLECTIVE = 1 << 0
@@ -43,6 +48,7 @@ NEWTON_WAVE = 1
 
 # enum ort_status
 STATUS_ZERNIKE_RANGE = 1 << 0
+STATUS_CHEBYSHEV_RANGE = 1 << 1
 
 CS_OP = np.dtype(
     [("kind", "<i4"), ("reserved", "<i4"), ("p", "<f8", (3,))], align=True

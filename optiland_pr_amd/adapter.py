@@ -4,8 +4,8 @@
 (surface_group.py:232-244) -- the seam SURVEY 8b names -- with the MI355X trace when:
   * the rays are RealRays (not Paraxial/Polarized) held as torch float64 tensors on the
     HIP device (be.set_backend("torch"); be.set_device("cuda"); be.set_precision("float64")),
-  * every traced surface is lowerable (plane / standard / even / odd asphere / Zernike
-    geometry, refractive-reflective interaction without coating or BSDF, radial or no
+  * every traced surface is lowerable (plane / standard / even / odd asphere / Zernike /
+    XY-polynomial / Chebyshev / biconic / toroidal geometry, refractive-reflective interaction without coating or BSDF, radial or no
     aperture, homogeneous propagation),
   * autograd is not requested on the ray tensors.
 Otherwise the original Python loop runs unchanged. The rays are traced IN PLACE (the
@@ -22,10 +22,14 @@ import numpy as np
 
 from . import _abi
 from .geometries import (
+    BiconicGeometry,
+    ChebyshevPolynomialGeometry,
     EvenAsphere,
     OddAsphere,
     Plane,
+    PolynomialGeometry,
     StandardGeometry,
+    ToroidalGeometry,
     ZernikePolynomialGeometry,
 )
 from .coordinate_system import CoordinateSystem
@@ -101,6 +105,19 @@ def _geometry(g):
         return ZernikePolynomialGeometry(cs, _f(g.radius), _f(g.k), g.tol, g.max_iter,
                                          np.ravel(_np(g.coefficients)), g.zernike_type,
                                          _f(g.norm_radius))
+    if name == "PolynomialGeometry":
+        return PolynomialGeometry(cs, _f(g.radius), _f(g.k), g.tol, g.max_iter,
+                                  np.asarray(_np(g.coefficients), dtype=np.float64))
+    if name == "ChebyshevPolynomialGeometry":
+        return ChebyshevPolynomialGeometry(cs, _f(g.radius), _f(g.k), g.tol, g.max_iter,
+                                           np.asarray(_np(g.coefficients), dtype=np.float64),
+                                           _f(g.norm_x), _f(g.norm_y))
+    if name == "BiconicGeometry":
+        return BiconicGeometry(cs, _f(g.Rx), _f(g.Ry), _f(g.kx), _f(g.ky), g.tol, g.max_iter)
+    if name == "ToroidalGeometry":
+        return ToroidalGeometry(cs, _f(g.R_rot), _f(g.R_yz), _f(g.k_yz),
+                                [float(v) for v in np.ravel(_np(g.coeffs_poly_y))],
+                                g.tol, g.max_iter)
     raise Unsupported(name)
 
 

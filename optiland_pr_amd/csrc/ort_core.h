@@ -43,8 +43,11 @@ struct Dual {
 };
 
 // the double overloads stay visible next to the Dual ones below
+using ::acos;
+using ::cos;
 using ::exp;
 using ::fabs;
+using ::sin;
 using ::sqrt;
 
 ORT_INLINE double vv(double x) { return x; }
@@ -164,6 +167,33 @@ ORT_INLINE Dual<P> sqrt(const Dual<P>& a) {
 template <int P>
 ORT_INLINE Dual<P> fabs(const Dual<P>& a) {  // torch.abs backward: sign(a) * g
   return a.v < 0.0 ? -a : (a.v > 0.0 ? a : Dual<P>(::fabs(a.v)));
+}
+template <int P>
+ORT_INLINE Dual<P> cos(const Dual<P>& a) {
+  Dual<P> r;
+  r.v = ::cos(a.v);
+  const double s = -::sin(a.v);
+#pragma unroll
+  for (int k = 0; k < P; ++k) r.d[k] = a.d[k] * s;
+  return r;
+}
+template <int P>
+ORT_INLINE Dual<P> sin(const Dual<P>& a) {
+  Dual<P> r;
+  r.v = ::sin(a.v);
+  const double c = ::cos(a.v);
+#pragma unroll
+  for (int k = 0; k < P; ++k) r.d[k] = a.d[k] * c;
+  return r;
+}
+template <int P>
+ORT_INLINE Dual<P> acos(const Dual<P>& a) {
+  Dual<P> r;
+  r.v = ::acos(a.v);
+  const double s = -1.0 / ::sqrt(1.0 - a.v * a.v);
+#pragma unroll
+  for (int k = 0; k < P; ++k) r.d[k] = a.d[k] * s;
+  return r;
 }
 template <int P>
 ORT_INLINE Dual<P> exp(const Dual<P>& a) {
@@ -504,6 +534,239 @@ ORT_INLINE T sagnorm_odd(const T& x, const T& y, double R, double k, PD C, int n
   return z;
 }
 
+// ---- freeform Newton geometries (coefficient blocks: include/optiland_rt.h) ---------
+// x ** p for the reference's integer powers, as successive products (p <= 2 exact as
+// NumPy's fast paths; p >= 3 within an ulp of libm pow)
+template <class T>
+ORT_INLINE T np_sign(const T& v) {  // np.sign: 0 -> 0, NaN -> NaN
+  const double d = vv(v);
+  return T(d > 0.0 ? 1.0 : (d < 0.0 ? -1.0 : (d == d ? 0.0 : d)));
+}
+
+// polynomial.py:93-140: conic + sum_ij C_ij x^i y^j
+template <class T, class PD>
+ORT_INLINE T sagnorm_poly(const T& x, const T& y, double R, double k, PD B, bool want_normal,
+                          T& nx, T& ny, T& nz) {
+  const int ni = (int)B[0], nj = (int)B[1];
+  const PD C = B + 2;
+  const T r2 = x * x + y * y;
+  const T q = sqrt(1.0 - (1.0 + k) * r2 / (R * R));
+  T z = r2 / (R * (1.0 + q));
+  T xi = T(1.0);  // x ** i
+  for (int i = 0; i < ni; ++i) {
+    T yj = T(1.0);  // y ** j
+#pragma unroll 1
+    for (int j = 0; j < nj; ++j) {
+      z = z + C[i * nj + j] * xi * yj;
+      yj = yj * y;
+    }
+    xi = xi * x;
+  }
+  if (want_normal) {
+    const T denom = R * q;
+    T dzdx = x / denom;
+    T dzdy = y / denom;
+    T xm = T(1.0);  // x ** (i - 1)
+    for (int i = 1; i < ni; ++i) {
+      T yj = T(1.0);
+#pragma unroll 1
+      for (int j = 0; j < nj; ++j) {
+        dzdx = dzdx + (double)i * C[i * nj + j] * xm * yj;
+        yj = yj * y;
+      }
+      xm = xm * x;
+    }
+    T xi2 = T(1.0);
+    for (int i = 0; i < ni; ++i) {
+      T ym = T(1.0);  // y ** (j - 1)
+#pragma unroll 1
+      for (int j = 1; j < nj; ++j) {
+        dzdy = dzdy + (double)j * C[i * nj + j] * xi2 * ym;
+        ym = ym * y;
+      }
+      xi2 = xi2 * x;
+    }
+    const T norm = sqrt(dzdx * dzdx + dzdy * dzdy + 1.0);
+    nx = dzdx / norm;
+    ny = dzdy / norm;
+    nz = -1.0 / norm;
+  }
+  return z;
+}
+
+// chebyshev.py:104-202: T_n(u) = cos(n acos u), T_n'(u) = n sin(n acos u) / sqrt(1 - u^2)
+// (the 1/norm chain factor is omitted by the reference's normal; kept as is); only
+// non-zero coefficients contribute (chebyshev.py:126, 155). Range error on |u| > 1.
+template <class T>
+ORT_INLINE T cheb_t(int n, const T& u) {
+  return cos((double)n * acos(u));
+}
+template <class T>
+ORT_INLINE T cheb_dt(int n, const T& u) {
+  return (double)n * sin((double)n * acos(u)) / sqrt(1.0 - u * u);
+}
+
+template <class T, class PD>
+ORT_INLINE T sagnorm_cheb(const T& x, const T& y, double R, double k, PD B, bool want_normal,
+                          bool& range_error, T& nx, T& ny, T& nz) {
+  const int ni = (int)B[0], nj = (int)B[1];
+  const double norm_x = B[2], norm_y = B[3];
+  const PD C = B + 4;
+  const T xn = x / norm_x;
+  const T yn = y / norm_y;
+  if (::fabs(vv(xn)) > 1.0 || ::fabs(vv(yn)) > 1.0) range_error = true;
+  const T r2 = x * x + y * y;
+  const T q = sqrt(1.0 - (1.0 + k) * r2 / (R * R));
+  T z = r2 / (R * (1.0 + q));
+  T dzdx, dzdy;
+  if (want_normal) {
+    const T denom = R * q;
+    dzdx = x / denom;
+    dzdy = y / denom;
+  }
+  for (int i = 0; i < ni; ++i) {
+#pragma unroll 1
+    for (int j = 0; j < nj; ++j) {
+      const double c = C[i * nj + j];
+      if (c == 0.0) continue;
+      const T ti = cheb_t(i, xn), tj = cheb_t(j, yn);
+      z = z + c * ti * tj;
+      if (want_normal) {
+        dzdx = dzdx + cheb_dt(i, xn) * c * tj;
+        dzdy = dzdy + cheb_dt(j, yn) * c * ti;
+      }
+    }
+  }
+  if (want_normal) {
+    const T norm = sqrt(dzdx * dzdx + dzdy * dzdy + 1.0);
+    nx = dzdx / norm;
+    ny = dzdy / norm;
+    nz = -1.0 / norm;
+  }
+  return z;
+}
+
+// biconic.py:69-158: z = cx x^2 / (1 + sqrt(1 - (1 + kx) cx^2 x^2)) + (same in y), with
+// the reference's clamps
+template <class T>
+ORT_INLINE T biconic_profile(double c, double kk, const T& u) {
+  const T v = 1.0 - (1.0 + kk) * (c * c) * (u * u);
+  const T st = vv(v) < 1e-14 ? T(0.0) : v;
+  const T den = 1.0 + sqrt(st);
+  const T sden = ::fabs(vv(den)) < 1e-14 ? T(1e-14) : den;
+  return (c * (u * u)) / sden;
+}
+template <class T>
+ORT_INLINE T biconic_slope(double c, double kk, const T& u) {
+  const T v = 1.0 - (1.0 + kk) * (c * c) * (u * u);
+  const T st = vv(v) < 1e-14 ? T(1e-14) : v;
+  const T ds = sqrt(st);
+  const T sds = ::fabs(vv(ds)) < 1e-14 ? T(1e-14) : ds;
+  return (c * u) / sds;
+}
+
+template <class T, class PD>
+ORT_INLINE T sagnorm_biconic(const T& x, const T& y, PD B, bool want_normal, T& nx, T& ny,
+                             T& nz) {
+  const double cx = B[0], cy = B[1], kx = B[2], ky = B[3];
+  const T zx = cx == 0.0 ? T(0.0) : biconic_profile(cx, kx, x);
+  const T zy = cy == 0.0 ? T(0.0) : biconic_profile(cy, ky, y);
+  if (want_normal) {
+    const T dfdx = cx == 0.0 ? T(0.0) : biconic_slope(cx, kx, x);
+    const T dfdy = cy == 0.0 ? T(0.0) : biconic_slope(cy, ky, y);
+    const T mag = sqrt(dfdx * dfdx + dfdy * dfdy + 1.0);
+    const T smag = vv(mag) < 1e-14 ? T(1.0) : mag;
+    nx = dfdx / smag;
+    ny = dfdy / smag;
+    nz = -1.0 / smag;
+  }
+  return zx + zy;
+}
+
+// toroidal.py:75-233: Y-Z profile z_y(y) (conic + even polynomial in y) swept around an
+// axis at distance R_rot
+template <class T, class PD>
+ORT_INLINE T toroid_zy(PD B, const T& y, bool deriv) {
+  const double c = B[1], kk = B[2];
+  const bool has_yz = B[3] != 0.0;
+  const int np = (int)B[4];
+  const double eps = 1e-14;
+  const T y2 = y * y;
+  T z = T(0.0);
+  if (has_yz) {
+    const T v = 1.0 - (1.0 + kk) * (c * c) * y2;
+    if (!deriv) {  // _calculate_zy, toroidal.py:75-107
+      const T root = vv(v) < 0.0 ? T(0.0) : v;
+      const T den = 1.0 + sqrt(root);
+      const T sden = ::fabs(vv(den)) < eps ? T(eps) : den;
+      z = (c * y2) / sden;
+    } else {  // _calculate_zy_derivative, toroidal.py:109-141
+      const T root = vv(v) < eps ? T(eps) : v;
+      const T sq = sqrt(root);
+      const T ssq = ::fabs(vv(sq)) < eps ? T(eps) : sq;
+      z = (c * y) / ssq;
+    }
+  }
+  if (np > 0) {
+    T poly = T(0.0);
+    T cur = deriv ? y : y2;
+#pragma unroll 1
+    for (int i = 0; i < np; ++i) {
+      const double a = B[5 + i];
+      if (!deriv) {
+        poly = poly + a * cur;
+      } else {
+        const double pc = 2.0 * ((double)i + 1.0);
+        poly = poly + a * pc * cur;
+      }
+      cur = cur * y2;
+    }
+    z = z + poly;
+  }
+  return z;
+}
+
+template <class T, class PD>
+ORT_INLINE T sagnorm_toroidal(const T& x, const T& y, PD B, bool want_normal, T& nx, T& ny,
+                              T& nz) {
+  const double Rr = B[0];
+  const double eps = 1e-14;
+  const T zy = toroid_zy(B, y, false);
+  const bool rinf = isinf(Rr);
+  T z;
+  T term = T(INFINITY);
+  if (rinf) {
+    z = zy;
+  } else {
+    const T d = Rr - zy;
+    term = d * d - x * x;
+    z = vv(term) < 0.0 ? T(NAN) : zy + (d - np_sign(d) * sqrt(term));
+  }
+  if (want_normal) {
+    const T dzdy = toroid_zy(B, y, true);
+    T fx, fy;
+    if (rinf) {
+      fx = T(0.0);
+      fy = dzdy;
+    } else {
+      const bool valid = vv(term) >= 0.0;
+      const T st = valid ? term : T(eps);
+      const T sq = sqrt(st);
+      const T ssq = ::fabs(vv(sq)) < eps ? T(eps) : sq;
+      const double sR = Rr > 0.0 ? 1.0 : (Rr < 0.0 ? -1.0 : 0.0);
+      fx = valid ? sR * x / ssq : T(0.0);
+      fy = valid ? sR * (Rr - zy) * dzdy / ssq : T(0.0);
+    }
+    const T mag = sqrt(fx * fx + fy * fy + 1.0);
+    const T smag = vv(mag) < eps ? T(1.0) : mag;
+    const bool ok = vv(term) >= 0.0;
+    nx = ok ? fx / smag : T(0.0);
+    ny = ok ? fy / smag : T(0.0);
+    nz = ok ? -1.0 / smag : T(-1.0);
+  }
+  return z;
+}
+
 // ---- Zernike: geometries/zernike.py:133-246 + zernike/base.py:42-299 ----------------
 // Per term (n, m), with a = |m|, rho = r / R_norm, phi = atan2(yn, xn):
 //   R_n^a(rho)   = sum_k a_k rho^(n-2k) = rho^a * P(rho^2)            (base.py:228-253)
@@ -635,7 +898,9 @@ ORT_INLINE T sagnorm_zernike(const T& x, const T& y, double R, double k, double 
 // Sag and normal of a Newton-iterated geometry (EvenAsphere / OddAsphere / Zernike).
 // KM is a bitmask of the Newton kinds compiled in (KM_EVEN | KM_ODD | KM_ZERN): a lens
 // only pays registers for the kinds it contains.
-enum : unsigned { KM_EVEN = 1u, KM_ODD = 2u, KM_ZERN = 4u };
+// KM_FREE covers the freeform kinds (XY polynomial, Chebyshev, biconic, toroidal) with a
+// runtime switch.
+enum : unsigned { KM_EVEN = 1u, KM_ODD = 2u, KM_ZERN = 4u, KM_FREE = 8u };
 
 template <unsigned KM, class T, class PD, class PZ>
 ORT_INLINE T newton_sagnorm(const ort_surface& s, PD coef, PZ zern, const ZSeed& zs,
@@ -651,8 +916,25 @@ ORT_INLINE T newton_sagnorm(const ort_surface& s, PD coef, PZ zern, const ZSeed&
       return sagnorm_odd(x, y, s.radius, s.conic, C, s.n_coef, want_normal, nx, ny, nz);
   }
   if constexpr ((KM & KM_ZERN) != 0) {
-    return sagnorm_zernike(x, y, s.radius, s.conic, s.norm_radius, zern, s.coef_off,
-                           s.n_coef, coef, zs, want_normal, range_error, nx, ny, nz);
+    if ((KM & ~KM_ZERN) == 0 || s.geometry == ORT_GEOM_ZERNIKE)
+      return sagnorm_zernike(x, y, s.radius, s.conic, s.norm_radius, zern, s.coef_off,
+                             s.n_coef, coef, zs, want_normal, range_error, nx, ny, nz);
+  }
+  if constexpr ((KM & KM_FREE) != 0) {
+    switch (s.geometry) {
+      case ORT_GEOM_POLYNOMIAL:
+        return sagnorm_poly(x, y, s.radius, s.conic, C, want_normal, nx, ny, nz);
+      case ORT_GEOM_CHEBYSHEV: {
+        bool cerr = false;
+        const T z = sagnorm_cheb(x, y, s.radius, s.conic, C, want_normal, cerr, nx, ny, nz);
+        if (cerr) range_error = true;
+        return z;
+      }
+      case ORT_GEOM_BICONIC:
+        return sagnorm_biconic(x, y, C, want_normal, nx, ny, nz);
+      default:
+        return sagnorm_toroidal(x, y, C, want_normal, nx, ny, nz);
+    }
   }
   nx = ny = nz = T(NAN);
   return T(NAN);

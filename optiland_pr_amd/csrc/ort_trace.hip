@@ -43,12 +43,12 @@ using PD = cptr<double>;
 using PZ = cptr<ort_zernike_term>;
 constexpr ort::ZSeed kNoSeed{nullptr, 0};
 
-// Kernel specialisation bits: bits 0-2 = Newton kinds present (ort::KM_*), bit 3 = rays
+// Kernel specialisation bits: bits 0-3 = Newton kinds present (ort::KM_*), bit 4 = rays
 // generated in-kernel from pupil coordinates.
 enum : uint32_t {
-  F_KM = 7u,
-  F_GEN = 1u << 3,
-  F_REC = 1u << 4,  // some surfaces are recorded (standard_surface.py:266-286)
+  F_KM = 15u,
+  F_GEN = 1u << 4,
+  F_REC = 1u << 5,  // some surfaces are recorded (standard_surface.py:266-286)
 };
 
 struct KArgs {
@@ -146,11 +146,18 @@ __device__ inline void globalize(const KArgs& a, const ort_surface& s, ort::RayT
   for (int c = 0; c < s.n_cs_glob; ++c) ort::apply_cs_op(r, cst(a.cs)[s.cs_glob_off + c]);
 }
 
+// status bit of a normalisation-range error at surface s (zernike.py:234-246,
+// chebyshev.py:203-215: both raise ValueError in the reference)
+__device__ inline int range_bit(const ort_surface& s) {
+  return s.geometry == ORT_GEOM_CHEBYSHEV ? (int)ORT_STATUS_CHEBYSHEV_RANGE
+                                          : (int)ORT_STATUS_ZERNIKE_RANGE;
+}
+
 // Newton refinement of t at surface s for one lane (newton_raphson.py:119-168).
 template <uint32_t FEAT>
 __device__ inline double newton_distance(const KArgs& a, const ort_surface& s, int si,
                                          const ort::Ray& r, bool active, int64_t group,
-                                         bool group_uniform, bool& range_error) {
+                                         bool group_uniform, int& range_bits) {
   double t = ort::distance_conic(r, s.radius, s.conic, (s.flags & ORT_SURF_RADIUS_INF) != 0);
   const double tol = s.tol;
   const int max_iter = s.max_iter;
@@ -163,7 +170,7 @@ __device__ inline double newton_distance(const KArgs& a, const ort_surface& s, i
       double nx, ny, nz;
       const double f = ort::newton_eval<(FEAT & F_KM)>(s, cst(a.coef), cst(a.zern), kNoSeed, r,
                                                       t, true, rerr, nx, ny, nz);
-      if (active && rerr) range_error = true;
+      if (active && rerr) range_bits |= range_bit(s);
       const bool conv = !active || !(fabs(f) >= tol);
       if (__all(conv)) break;
       t = ort::newton_step(r, t, f, nx, ny, nz);
@@ -187,7 +194,7 @@ __device__ inline double newton_distance(const KArgs& a, const ort_surface& s, i
                                                       t, upd, rerr, nx, ny, nz);
       // the reference evaluates sag at j = 0..U-1 always, and at j = U only when the
       // loop broke there (U < max_iter)
-      if (rerr && (j < U || U < max_iter)) range_error = true;
+      if (rerr && (j < U || U < max_iter)) range_bits |= range_bit(s);
       const bool conv = fabs(f) < tol;  // NaN never converges (np.max propagates NaN)
       if (conv && j < 64) mask |= 1ull << j;
       if (!conv) last_bad = j;
@@ -249,7 +256,7 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(const KArgs a) {
     const int64_t g0 = __shfl(group, 0, 64);
     group_uniform = __all(group == g0);
   }
-  bool range_error = false;
+  int range_bits = 0;
 
   for (int si = a.start_surface; si < a.n_surf; ++si) {
     const ort_surface s = cst(a.surf)[si];
@@ -262,7 +269,7 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(const KArgs a) {
       t = ort::distance_conic(r, s.radius, s.conic, (s.flags & ORT_SURF_RADIUS_INF) != 0);
     } else {
       if constexpr ((FEAT & F_KM) != 0) {
-        t = newton_distance<FEAT>(a, s, si, r, active, group, group_uniform, range_error);
+        t = newton_distance<FEAT>(a, s, si, r, active, group, group_uniform, range_bits);
       } else {
         t = __builtin_nan("");  // unreachable: the host sets geometry_mask
       }
@@ -308,8 +315,8 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(const KArgs a) {
     ort::propagate(r, a.final_thickness,
                    tab(a.alpha_tab, a.n_lambda, a.n_mat, lam, a.final_mat));
 
-  if constexpr ((FEAT & ort::KM_ZERN) != 0) {
-    if (range_error && active && a.status) atomicOr(a.status, (int)ORT_STATUS_ZERNIKE_RANGE);
+  if constexpr ((FEAT & (ort::KM_ZERN | ort::KM_FREE)) != 0) {
+    if (range_bits && active && a.status) atomicOr(a.status, range_bits);
   }
   if (!active) return;
   a.out.x[rid] = r.x;
@@ -530,6 +537,7 @@ __global__ __launch_bounds__(kBlock) void geom_kernel(const KArgs a, const GArgs
   const int64_t r_ld = active ? rid : 0;
   const ort_surface s = cst(a.surf)[g.surface];
   bool range_error = false;
+  int range_bits = 0;
   if (g.mode == 0) {
     const double x = g.x[r_ld], y = g.y[r_ld];
     double z, nx, ny, nz;
@@ -571,14 +579,15 @@ __global__ __launch_bounds__(kBlock) void geom_kernel(const KArgs a, const GArgs
       t = ort::distance_conic(r, s.radius, s.conic, (s.flags & ORT_SURF_RADIUS_INF) != 0);
     } else {
       if constexpr (KM != 0) {
-        t = newton_distance<KM>(a, s, g.surface, r, active, 0, true, range_error);
+        t = newton_distance<KM>(a, s, g.surface, r, active, 0, true, range_bits);
       } else {
         t = __builtin_nan("");
       }
     }
     if (active && g.t) g.t[rid] = t;
   }
-  if (range_error && active && a.status) atomicOr(a.status, (int)ORT_STATUS_ZERNIKE_RANGE);
+  if (range_error) range_bits |= range_bit(s);
+  if (range_bits && active && a.status) atomicOr(a.status, range_bits);
 }
 
 typedef void (*GeomFn)(const KArgs, const GArgs);
@@ -589,14 +598,13 @@ int init_outputs(const KArgs& a, hipStream_t stream);
 
 GeomFn pick_geom(uint32_t km) {
   switch (km) {
-    case 0: return geom_kernel<0>;
-    case 1: return geom_kernel<1>;
-    case 2: return geom_kernel<2>;
-    case 3: return geom_kernel<3>;
-    case 4: return geom_kernel<4>;
-    case 5: return geom_kernel<5>;
-    case 6: return geom_kernel<6>;
-    default: return geom_kernel<7>;
+#define ORT_G(K) \
+  case (K):      \
+    return geom_kernel<(K)>;
+    ORT_G(0) ORT_G(1) ORT_G(2) ORT_G(3) ORT_G(4) ORT_G(5) ORT_G(6) ORT_G(7)
+    ORT_G(8) ORT_G(9) ORT_G(10) ORT_G(11) ORT_G(12) ORT_G(13) ORT_G(14)
+#undef ORT_G
+    default: return geom_kernel<15>;
   }
 }
 
@@ -629,12 +637,16 @@ typedef void (*VjpFn)(const KArgs, const JArgs);
 
 template <int P>
 VjpFn pick_vjp(uint32_t km) {
+  using namespace ort;
   switch (km) {
-    case ort::KM_ZERN: return vjp_kernel<P, ort::KM_ZERN>;
-    case ort::KM_ZERN | ort::KM_EVEN: return vjp_kernel<P, ort::KM_ZERN | ort::KM_EVEN>;
-    case ort::KM_ZERN | ort::KM_ODD: return vjp_kernel<P, ort::KM_ZERN | ort::KM_ODD>;
-    case ort::KM_ZERN | ort::KM_EVEN | ort::KM_ODD:
-      return vjp_kernel<P, ort::KM_ZERN | ort::KM_EVEN | ort::KM_ODD>;
+#define ORT_V(K) \
+  case (K):      \
+    return vjp_kernel<P, (K)>;
+    ORT_V(KM_ZERN) ORT_V(KM_ZERN | KM_EVEN) ORT_V(KM_ZERN | KM_ODD)
+    ORT_V(KM_ZERN | KM_EVEN | KM_ODD) ORT_V(KM_ZERN | KM_FREE)
+    ORT_V(KM_ZERN | KM_FREE | KM_EVEN) ORT_V(KM_ZERN | KM_FREE | KM_ODD)
+    ORT_V(KM_ZERN | KM_FREE | KM_EVEN | KM_ODD)
+#undef ORT_V
     default: return nullptr;
   }
 }
@@ -669,7 +681,9 @@ KernelFn select_kernel(uint32_t feat) {
   case (F):         \
     return pick<(F)>();
 #define ORT_CASES(G) ORT_CASE(G | 0) ORT_CASE(G | 1) ORT_CASE(G | 2) ORT_CASE(G | 3) \
-    ORT_CASE(G | 4) ORT_CASE(G | 5) ORT_CASE(G | 6) ORT_CASE(G | 7)
+    ORT_CASE(G | 4) ORT_CASE(G | 5) ORT_CASE(G | 6) ORT_CASE(G | 7) ORT_CASE(G | 8)  \
+    ORT_CASE(G | 9) ORT_CASE(G | 10) ORT_CASE(G | 11) ORT_CASE(G | 12) ORT_CASE(G | 13) \
+    ORT_CASE(G | 14) ORT_CASE(G | 15)
     ORT_CASES(0)
     ORT_CASES(F_GEN)
     ORT_CASES(F_REC)
@@ -719,6 +733,9 @@ int fill_args(KArgs& a, const ort_lens* lens, const ort_batch* batch, const ort_
   if (lens->geometry_mask & (1u << ORT_GEOM_EVEN_ASPHERE)) feat |= ort::KM_EVEN;
   if (lens->geometry_mask & (1u << ORT_GEOM_ODD_ASPHERE)) feat |= ort::KM_ODD;
   if (lens->geometry_mask & (1u << ORT_GEOM_ZERNIKE)) feat |= ort::KM_ZERN;
+  if (lens->geometry_mask & ((1u << ORT_GEOM_POLYNOMIAL) | (1u << ORT_GEOM_CHEBYSHEV) |
+                             (1u << ORT_GEOM_BICONIC) | (1u << ORT_GEOM_TOROIDAL)))
+    feat |= ort::KM_FREE;
   if (rec) feat |= F_REC;
   if (opt->newton_mode != ORT_NEWTON_SCHEDULE && opt->newton_mode != ORT_NEWTON_WAVE)
     return ORT_ERR_ARG;

@@ -246,3 +246,94 @@ class ZernikePolynomialGeometry(NewtonRaphsonGeometry):
             a, d = radial_coefficients(n, abs(m))
             out.append((float(c), float(_norm_constant(self.zernike_type, n, m)), n, m, a, d))
         return out
+
+
+class PolynomialGeometry(NewtonRaphsonGeometry):
+    """geometries/polynomial.py:33-140: conic + sum_ij C_ij x^i y^j (C as be.atleast_2d)."""
+
+    geometry_id = _abi.GEOM_POLYNOMIAL
+
+    def __init__(self, coordinate_system, radius, conic=0.0, tol=1e-10, max_iter=100,
+                 coefficients=None):
+        super().__init__(coordinate_system, radius, conic, tol, max_iter)
+        c = np.atleast_2d(np.asarray(coefficients if coefficients is not None else [],
+                                     dtype=np.float64))
+        if c.size == 0:
+            c = np.zeros((1, 1))
+        self.coefficients = c
+        self.is_symmetric = False
+
+    def lower_params(self):
+        c = np.atleast_2d(np.asarray(self.coefficients, dtype=np.float64))
+        block = [float(c.shape[0]), float(c.shape[1])] + [float(v) for v in c.ravel()]
+        return self.radius, self.k, self.tol, self.max_iter, 1.0, block
+
+
+class ChebyshevPolynomialGeometry(NewtonRaphsonGeometry):
+    """geometries/chebyshev.py:33-215: conic + sum_ij C_ij T_i(x/norm_x) T_j(y/norm_y)."""
+
+    geometry_id = _abi.GEOM_CHEBYSHEV
+
+    def __init__(self, coordinate_system, radius, conic=0.0, tol=1e-10, max_iter=100,
+                 coefficients=None, norm_x=1, norm_y=1):
+        super().__init__(coordinate_system, radius, conic, tol, max_iter)
+        self.coefficients = np.atleast_2d(np.asarray(
+            coefficients if coefficients is not None else [], dtype=np.float64))
+        self.norm_x = float(norm_x)
+        self.norm_y = float(norm_y)
+        self.is_symmetric = False
+
+    def lower_params(self):
+        c = np.atleast_2d(np.asarray(self.coefficients, dtype=np.float64))
+        if c.size == 0:
+            c = np.zeros((1, 0))
+        block = [float(c.shape[0]), float(c.shape[1]), float(self.norm_x),
+                 float(self.norm_y)] + [float(v) for v in c.ravel()]
+        return self.radius, self.k, self.tol, self.max_iter, 1.0, block
+
+
+class BiconicGeometry(NewtonRaphsonGeometry):
+    """geometries/biconic.py:29-158: separate conic profiles in x and y; the Newton start
+    guess is the (R_x, k_x) conic (newton_raphson.py:134)."""
+
+    geometry_id = _abi.GEOM_BICONIC
+
+    def __init__(self, coordinate_system, radius_x, radius_y, conic_x=0.0, conic_y=0.0,
+                 tol=1e-10, max_iter=100):
+        super().__init__(coordinate_system, radius_x, conic_x, tol, max_iter)
+        self.Rx = float(radius_x)
+        self.Ry = float(radius_y)
+        self.kx = float(conic_x)
+        self.ky = float(conic_y)
+        self.is_symmetric = False
+
+    @staticmethod
+    def _curv(r):
+        return 0.0 if (np.isinf(r) or r == 0) else 1.0 / r
+
+    def lower_params(self):
+        block = [self._curv(self.Rx), self._curv(self.Ry), self.kx, self.ky]
+        return self.radius, self.k, self.tol, self.max_iter, 1.0, block
+
+
+class ToroidalGeometry(NewtonRaphsonGeometry):
+    """geometries/toroidal.py:26-233: a Y-Z conic + even polynomial profile swept about an
+    axis at R_rot; the Newton start guess is the (R_yz, k = 0) sphere."""
+
+    geometry_id = _abi.GEOM_TOROIDAL
+
+    def __init__(self, coordinate_system, radius_x, radius_y, conic=0.0, coeffs_poly_y=None,
+                 tol=1e-10, max_iter=100):
+        super().__init__(coordinate_system, radius_y, 0.0, tol, max_iter)
+        self.R_rot = float(radius_x)
+        self.R_yz = float(radius_y)
+        self.k_yz = float(conic)
+        self.coeffs_poly_y = [float(c) for c in (coeffs_poly_y or [])]
+        self.is_symmetric = False
+
+    def lower_params(self):
+        has_yz = bool(np.isfinite(self.R_yz) and self.R_yz != 0)
+        c_yz = 1.0 / self.R_yz if has_yz else 0.0
+        block = [self.R_rot, c_yz, self.k_yz, 1.0 if has_yz else 0.0,
+                 float(len(self.coeffs_poly_y))] + self.coeffs_poly_y
+        return self.radius, self.k, self.tol, self.max_iter, 1.0, block

@@ -90,6 +90,11 @@ class Optic:
         yb = np.abs(np.ravel(yb))
         for k, s in enumerate(self.surface_group.surfaces):
             s.set_semi_aperture(r_max=ya[k] + yb[k])
+            # optic_updater.py:205-240 update_normalization
+            if hasattr(s.geometry, "norm_x"):
+                s.geometry.norm_x = float(s.semi_aperture * 1.25)
+            if hasattr(s.geometry, "norm_y"):
+                s.geometry.norm_y = float(s.semi_aperture * 1.25)
             if s.surface_type == "zernike":
                 s.geometry.norm_radius = float(s.semi_aperture * 1.25)
         self._lowered = None

@@ -192,6 +192,37 @@ class DecenteredTriplet(Optic):
 
 
 # name -> builder, matching tests/golden/gen_golden.py CASES
+class FreeformTriplet(Optic):
+    """Cooke-triplet layout with freeform surfaces (SURVEY 8f.3 coverage): a biconic
+    front, a toroidal rear of element 1, an XY-polynomial and a Chebyshev surface on
+    element 3 (normalisation set by update_paraxial, optic_updater.py:205-240)."""
+
+    def __init__(self):
+        super().__init__()
+        self.add_surface(index=0, radius=np.inf, thickness=np.inf)
+        self.add_surface(index=1, surface_type="biconic", radius_x=22.01359, radius_y=23.5,
+                         conic_x=-0.2, conic_y=0.1, thickness=3.25896, material="SK16")
+        self.add_surface(index=2, surface_type="toroidal", radius_x=-300.0,
+                         radius_y=-435.76044, conic=0.5, toroidal_coeffs_poly_y=[2e-6],
+                         thickness=6.00755)
+        self.add_surface(index=3, radius=-22.21328, thickness=0.99997, material=("F2", "schott"))
+        self.add_surface(index=4, radius=20.29192, thickness=4.75041, is_stop=True)
+        self.add_surface(index=5, surface_type="polynomial", radius=79.68360, conic=0.0,
+                         coefficients=[[0.0, 0.0, 2e-4], [0.0, 1e-5, 0.0], [1.5e-4, 0.0, 0.0]],
+                         thickness=2.95208, material="SK16")
+        self.add_surface(index=6, surface_type="chebyshev", radius=-18.39533, conic=0.0,
+                         coefficients=[[0.0, 1e-3, 2e-3], [5e-4, 0.0, 0.0], [1e-3, 0.0, 0.0]],
+                         thickness=42.20778)
+        self.add_surface(index=7)
+        self.set_aperture(aperture_type="EPD", value=10)
+        self.set_field_type(field_type="angle")
+        self.add_field(y=0)
+        self.add_field(y=14)
+        self.add_field(x=5, y=10)
+        self.add_wavelength(value=0.55, is_primary=True)
+        self.update_paraxial()
+
+
 GOLDEN_LENSES = {
     "cooke": CookeTriplet,
     "dg": DoubleGauss,
@@ -203,4 +234,5 @@ GOLDEN_LENSES = {
     "tma_noll": lambda: ThreeMirrorAnastigmat("noll"),
     "cooke_aperture": CookeTripletApertures,
     "decentered": DecenteredTriplet,
+    "freeform": FreeformTriplet,
 }

@@ -16,10 +16,14 @@ import numpy as np
 
 from .coordinate_system import CoordinateSystem
 from .geometries import (
+    BiconicGeometry,
+    ChebyshevPolynomialGeometry,
     EvenAsphere,
     OddAsphere,
     Plane,
+    PolynomialGeometry,
     StandardGeometry,
+    ToroidalGeometry,
     ZernikePolynomialGeometry,
 )
 from .materials import BaseMaterial, IdealMaterial, configure_material
@@ -133,9 +137,27 @@ def _make_geometry(surface_type, cs, kw):
             cs, radius, conic, kw.get("tol", 1e-6), kw.get("max_iter", 100),
             kw.get("coefficients", []), kw.get("zernike_type", "fringe"),
             kw.get("norm_radius", 1.0))
+    tol, max_iter = kw.get("tol", 1e-6), kw.get("max_iter", 100)
+    if st == "polynomial":
+        return PolynomialGeometry(cs, radius, conic, tol, max_iter, kw.get("coefficients", []))
+    if st == "chebyshev":
+        return ChebyshevPolynomialGeometry(cs, radius, conic, tol, max_iter,
+                                           kw.get("coefficients", []), kw.get("norm_x", 1.0),
+                                           kw.get("norm_y", 1.0))
+    if st == "biconic":
+        rx, ry = kw.get("radius_x", np.inf), kw.get("radius_y", np.inf)
+        kx, ky = kw.get("conic_x", 0.0), kw.get("conic_y", 0.0)
+        if np.isinf(rx) and np.isinf(ry) and kx == 0.0 and ky == 0.0:
+            return Plane(cs)  # geometry_factory.py _create_biconic
+        return BiconicGeometry(cs, rx, ry, kx, ky, tol, max_iter)
+    if st == "toroidal":
+        return ToroidalGeometry(cs, kw.get("radius_x", np.inf), kw.get("radius_y", np.inf),
+                                kw.get("conic", 0.0), kw.get("toroidal_coeffs_poly_y", []),
+                                tol, max_iter)
     raise ValueError(
-        f"Surface type {st!r} is not lowered to the MI355X trace core "
-        "(supported: standard, plane, even_asphere, odd_asphere, zernike).")
+        f"Surface type {st!r} is not lowered to the MI355X trace core (supported: "
+        "standard, plane, even_asphere, odd_asphere, zernike, polynomial, chebyshev, "
+        "biconic, toroidal).")
 
 
 class SurfaceGroup:

@@ -297,6 +297,187 @@ def normal_zernike(x, y, R, k, terms, coef, norm_radius):
     return nx / norm, ny / norm, -np.ones_like(x) / norm
 
 
+# ---- freeform Newton geometries ------------------------------------------------------
+def sag_poly(x, y, R, k, C):
+    """polynomial.py:93-108 (C: 2-D, be.atleast_2d)."""
+    r2 = x**2 + y**2
+    z = r2 / (R * (1 + np.sqrt(1 - (1 + k) * r2 / R**2)))
+    for i in range(len(C)):
+        for j in range(len(C[i])):
+            z = z + C[i][j] * (x**i) * (y**j)
+    return z
+
+
+def normal_poly(x, y, R, k, C):
+    """polynomial.py:111-140."""
+    r2 = x**2 + y**2
+    denom = R * np.sqrt(1 - (1 + k) * r2 / R**2)
+    dzdx = x / denom
+    dzdy = y / denom
+    for i in range(1, len(C)):
+        for j in range(len(C[i])):
+            dzdx = dzdx + i * C[i][j] * (x ** (i - 1)) * (y**j)
+    for i in range(len(C)):
+        for j in range(1, len(C[i])):
+            dzdy = dzdy + j * C[i][j] * (x**i) * (y ** (j - 1))
+    norm = np.sqrt(dzdx**2 + dzdy**2 + 1)
+    return dzdx / norm, dzdy / norm, -1 / norm
+
+
+class ChebyshevRangeError(ValueError):
+    pass
+
+
+def _cheb_validate(xn, yn):
+    """chebyshev.py:203-215."""
+    if np.any(np.abs(xn) > 1) or np.any(np.abs(yn) > 1):
+        raise ChebyshevRangeError("Chebyshev input coordinates must be normalized to [-1, 1]. "
+                                  "Consider updating the normalization factors.")
+
+
+def _cheb(n, x):
+    return np.cos(n * np.arccos(x))  # chebyshev.py:176-188
+
+
+def _cheb_d(n, x):
+    return n * np.sin(n * np.arccos(x)) / np.sqrt(1 - x**2)  # chebyshev.py:190-201
+
+
+def sag_cheb(x, y, R, k, C, norm_x, norm_y):
+    """chebyshev.py:104-129."""
+    xn = x / norm_x
+    yn = y / norm_y
+    _cheb_validate(xn, yn)
+    r2 = x**2 + y**2
+    z = r2 / (R * (1 + np.sqrt(1 - (1 + k) * r2 / R**2)))
+    for i, j in np.argwhere(C != 0):
+        z = z + C[i, j] * _cheb(i, xn) * _cheb(j, yn)
+    return z
+
+
+def normal_cheb(x, y, R, k, C, norm_x, norm_y):
+    """chebyshev.py:131-174."""
+    xn = x / norm_x
+    yn = y / norm_y
+    _cheb_validate(xn, yn)
+    r2 = x**2 + y**2
+    denom = R * np.sqrt(1 - (1 + k) * r2 / R**2)
+    dzdx = x / denom
+    dzdy = y / denom
+    for i, j in np.argwhere(C != 0):
+        dzdx = dzdx + (_cheb_d(i, xn) * C[i, j] * _cheb(j, yn))
+        dzdy = dzdy + (_cheb_d(j, yn) * C[i, j] * _cheb(i, xn))
+    norm = np.sqrt(dzdx**2 + dzdy**2 + 1)
+    return dzdx / norm, dzdy / norm, -1 / norm
+
+
+def sag_biconic(x, y, cx, cy, kx, ky):
+    """biconic.py:69-103 (cx, cy, kx, ky as the reference's 0-d arrays)."""
+    zx = np.zeros_like(x)
+    zy = np.zeros_like(y)
+    if not np.all(cx == 0):
+        v = 1.0 - (1.0 + kx) * cx**2 * x**2
+        st = np.where(v < 1e-14, 0.0, v)
+        den = 1.0 + np.sqrt(st)
+        zx = (cx * x**2) / np.where(np.abs(den) < 1e-14, 1e-14, den)
+    if not np.all(cy == 0):
+        v = 1.0 - (1.0 + ky) * cy**2 * y**2
+        st = np.where(v < 1e-14, 0.0, v)
+        den = 1.0 + np.sqrt(st)
+        zy = (cy * y**2) / np.where(np.abs(den) < 1e-14, 1e-14, den)
+    return zx + zy
+
+
+def normal_biconic(x, y, cx, cy, kx, ky):
+    """biconic.py:105-158."""
+    if np.all(cx == 0):
+        dfdx = np.zeros_like(x)
+    else:
+        v = 1.0 - (1.0 + kx) * cx**2 * x**2
+        ds = np.sqrt(np.where(v < 1e-14, 1e-14, v))
+        dfdx = (cx * x) / np.where(np.abs(ds) < 1e-14, 1e-14, ds)
+    if np.all(cy == 0):
+        dfdy = np.zeros_like(y)
+    else:
+        v = 1.0 - (1.0 + ky) * cy**2 * y**2
+        ds = np.sqrt(np.where(v < 1e-14, 1e-14, v))
+        dfdy = (cy * y) / np.where(np.abs(ds) < 1e-14, 1e-14, ds)
+    mag = np.sqrt(dfdx**2 + dfdy**2 + 1.0)
+    smag = np.where(mag < 1e-14, 1.0, mag)
+    return dfdx / smag, dfdy / smag, -1.0 / smag
+
+
+def _toroid_zy(y, R_yz, c, k, poly):
+    """toroidal.py:75-107 (_calculate_zy)."""
+    y2 = y**2
+    z_y = np.zeros_like(y)
+    if np.isfinite(R_yz) and R_yz != 0:
+        v = 1.0 - (1.0 + k) * c**2 * y2
+        root = np.where(v < 0, 0.0, v)
+        den = 1.0 + np.sqrt(root)
+        z_y = (c * y2) / np.where(np.abs(den) < 1e-14, 1e-14, den)
+    if len(poly) > 0:
+        p = np.zeros_like(y)
+        cur = y2
+        for a in poly:
+            p = p + a * cur
+            cur = cur * y2
+        z_y = z_y + p
+    return z_y
+
+
+def _toroid_dzy(y, R_yz, c, k, poly):
+    """toroidal.py:109-141 (_calculate_zy_derivative)."""
+    y2 = y**2
+    d = np.zeros_like(y)
+    if np.isfinite(R_yz) and R_yz != 0:
+        v = 1.0 - (1.0 + k) * c**2 * y2
+        sq = np.sqrt(np.where(v < 1e-14, 1e-14, v))
+        d = (c * y) / np.where(np.abs(sq) < 1e-14, 1e-14, sq)
+    if len(poly) > 0:
+        p = np.zeros_like(y)
+        cur = y
+        for i, a in enumerate(poly):
+            p = p + a * (2.0 * (i + 1.0)) * cur
+            cur = cur * y2
+        d = d + p
+    return d
+
+
+def sag_toroidal(x, y, R_rot, R_yz, c, k, poly):
+    """toroidal.py:143-167."""
+    z_y = _toroid_zy(y, R_yz, c, k, poly)
+    if np.isinf(R_rot):
+        return z_y
+    term = (R_rot - z_y) ** 2 - x**2
+    with np.errstate(invalid="ignore"):
+        return np.where(term < 0, np.nan,
+                        z_y + ((R_rot - z_y) - np.sign(R_rot - z_y) * np.sqrt(term)))
+
+
+def normal_toroidal(x, y, R_rot, R_yz, c, k, poly):
+    """toroidal.py:169-233."""
+    eps = 1e-14
+    z_y = _toroid_zy(y, R_yz, c, k, poly)
+    dz_dy = _toroid_dzy(y, R_yz, c, k, poly)
+    if np.isinf(R_rot):
+        fx = np.zeros_like(x)
+        fy = dz_dy
+        term = np.inf
+    else:
+        term = (R_rot - z_y) ** 2 - x**2
+        valid = term >= 0
+        sq = np.sqrt(np.where(valid, term, eps))
+        ssq = np.where(np.abs(sq) < eps, eps, sq)
+        fx = np.where(valid, np.sign(R_rot) * x / ssq, 0.0)
+        fy = np.where(valid, np.sign(R_rot) * (R_rot - z_y) * dz_dy / ssq, 0.0)
+    mag = np.sqrt(fx**2 + fy**2 + 1.0)
+    smag = np.where(mag < eps, 1.0, mag)
+    nx, ny, nz = fx / smag, fy / smag, -1.0 / smag
+    return (np.where(term >= 0, nx, 0.0), np.where(term >= 0, ny, 0.0),
+            np.where(term >= 0, nz, -1.0))
+
+
 def _geometry_fns(table, s):
     g = int(s["geometry"])
     R, k = float(s["radius"]), float(s["conic"])
@@ -312,6 +493,31 @@ def _geometry_fns(table, s):
         nr = float(s["norm_radius"])
         return ((lambda x, y: sag_zernike(x, y, R, k, terms, table.coef, nr)),
                 (lambda x, y: normal_zernike(x, y, R, k, terms, table.coef, nr)))
+    B = [float(c) for c in table.coef[off:off + nc]]
+    if g == _abi.GEOM_POLYNOMIAL:
+        ni, nj = int(B[0]), int(B[1])
+        C = np.array(B[2:2 + ni * nj]).reshape(ni, nj)
+        return (lambda x, y: sag_poly(x, y, R, k, C)), (lambda x, y: normal_poly(x, y, R, k, C))
+    if g == _abi.GEOM_CHEBYSHEV:
+        ni, nj = int(B[0]), int(B[1])
+        nx_, ny_ = np.array(B[2]), np.array(B[3])
+        C = np.array(B[4:4 + ni * nj]).reshape(ni, nj)
+        return ((lambda x, y: sag_cheb(x, y, R, k, C, nx_, ny_)),
+                (lambda x, y: normal_cheb(x, y, R, k, C, nx_, ny_)))
+    if g == _abi.GEOM_BICONIC:
+        cx, cy, kx, ky = (np.array(v) for v in B[:4])
+        return ((lambda x, y: sag_biconic(x, y, cx, cy, kx, ky)),
+                (lambda x, y: normal_biconic(x, y, cx, cy, kx, ky)))
+    if g == _abi.GEOM_TOROIDAL:
+        R_rot, c_yz, k_yz, has_yz, n_poly = B[:5]
+        poly = np.asarray(B[5:5 + int(n_poly)])
+        R_rot = np.array(R_rot)
+        # the reference keeps R_yz itself; only its finiteness / non-zero test matters here
+        R_yz = np.array(1.0 if has_yz else np.inf)
+        c = np.float64(c_yz)
+        k_ = np.array(k_yz)
+        return ((lambda x, y: sag_toroidal(x, y, R_rot, R_yz, c, k_, poly)),
+                (lambda x, y: normal_toroidal(x, y, R_rot, R_yz, c, k_, poly)))
     raise ValueError(g)
 
 

@@ -8,10 +8,14 @@ import numpy as np
 
 from optiland_pr_amd.coordinate_system import CoordinateSystem
 from optiland_pr_amd.geometries import (
+    BiconicGeometry,
+    ChebyshevPolynomialGeometry,
     EvenAsphere,
     OddAsphere,
     Plane,
+    PolynomialGeometry,
     StandardGeometry,
+    ToroidalGeometry,
     ZernikePolynomialGeometry,
 )
 
@@ -46,8 +50,22 @@ def build(spec):
                                          coefficients=spec["coefficients"],
                                          norm_radius=spec["norm_radius"],
                                          zernike_type=spec["zernike_type"])
+    if k == "polynomial":
+        return PolynomialGeometry(cs, radius=spec["radius"], conic=spec["conic"],
+                                  coefficients=spec["coefficients"])
+    if k == "chebyshev":
+        return ChebyshevPolynomialGeometry(cs, radius=spec["radius"], conic=spec["conic"],
+                                           coefficients=spec["coefficients"],
+                                           norm_x=spec["norm_x"], norm_y=spec["norm_y"])
+    if k == "biconic":
+        return BiconicGeometry(cs, radius_x=spec["radius_x"], radius_y=spec["radius_y"],
+                               conic_x=spec["conic_x"], conic_y=spec["conic_y"])
+    if k == "toroidal":
+        return ToroidalGeometry(cs, radius_x=spec["radius_x"], radius_y=spec["radius_y"],
+                                conic=spec["conic"], coeffs_poly_y=spec["coeffs_poly_y"])
     raise ValueError(k)
 
 
 CASES = sorted(specs())
-NEWTON_KINDS = ("even_asphere", "odd_asphere", "zernike")
+NEWTON_KINDS = ("even_asphere", "odd_asphere", "zernike", "polynomial", "chebyshev",
+                "biconic", "toroidal")

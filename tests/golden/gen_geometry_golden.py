@@ -66,6 +66,35 @@ SPECS = {
     "zern_fringe_conic": dict(kind="zernike", radius=-50.0, conic=-0.8, norm_radius=12.0,
                               zernike_type="fringe",
                               coefficients=[0.0, 1e-3, -2e-3, 5e-3, 1e-3, 0.0, 2e-4, -1e-4]),
+    "poly_sag": dict(kind="polynomial", radius=22.0, conic=0.0,
+                     coefficients=[[0.0, 1e-2, -2e-3], [0.1, 1e-2, -1e-3], [0.2, 1e-2, 0.0]]),
+    "poly_dist": dict(kind="polynomial", radius=-26.0, conic=0.1,
+                      coefficients=[[0.0, 1e-2, 2e-3], [0.1, -1e-2, 1e-3], [0.2, 1e-2, 2e-4]]),
+    "poly_1d": dict(kind="polynomial", radius=40.0, conic=-0.3,
+                    coefficients=[0.0, 2e-3, 1e-4, -3e-6]),
+    "cheb_sag": dict(kind="chebyshev", radius=22.0, conic=0.0, norm_x=10.0, norm_y=10.0,
+                     coefficients=[[0.0, 1e-2, -2e-3], [0.1, 1e-2, -1e-3], [0.2, 1e-2, 0.0]]),
+    "cheb_dist": dict(kind="chebyshev", radius=-26.0, conic=0.1, norm_x=10.0, norm_y=10.0,
+                      coefficients=[[0.0, 1e-2, -2e-3], [0.1, 1e-2, -1e-3], [0.2, 1e-2, 0.0]]),
+    "biconic": dict(kind="biconic", radius_x=10.0, radius_y=20.0, conic_x=0.5, conic_y=-0.5),
+    "biconic_conics": dict(kind="biconic", radius_x=10.0, radius_y=20.0, conic_x=-1.0,
+                           conic_y=0.5),
+    "biconic_rx_inf": dict(kind="biconic", radius_x=float("inf"), radius_y=20.0,
+                           conic_x=0.0, conic_y=0.0),
+    "biconic_ry_inf": dict(kind="biconic", radius_x=-15.0, radius_y=float("inf"),
+                           conic_x=0.2, conic_y=0.0),
+    "toroid": dict(kind="toroidal", radius_x=100.0, radius_y=50.0, conic=-0.5,
+                   coeffs_poly_y=[1e-5]),
+    "toroid_cyl_x": dict(kind="toroidal", radius_x=float("inf"), radius_y=-50.0, conic=0.0,
+                         coeffs_poly_y=[]),
+    "toroid_cyl_y": dict(kind="toroidal", radius_x=100.0, radius_y=float("inf"), conic=0.0,
+                         coeffs_poly_y=[]),
+    "toroid_no_x": dict(kind="toroidal", radius_x=float("inf"), radius_y=50.0, conic=-1.1,
+                        coeffs_poly_y=[1e-5, -2e-6]),
+    "toroid_no_y": dict(kind="toroidal", radius_x=100.0, radius_y=float("inf"), conic=-0.9,
+                        coeffs_poly_y=[1e-5, -2e-6]),
+    "toroid_neg": dict(kind="toroidal", radius_x=-30.0, radius_y=-20.0, conic=0.3,
+                       coeffs_poly_y=[2e-5, 1e-7]),
 }
 
 
@@ -86,6 +115,22 @@ def build(spec):
         return geometries.ZernikePolynomialGeometry(
             cs, radius=spec["radius"], conic=spec["conic"], coefficients=spec["coefficients"],
             norm_radius=spec["norm_radius"], zernike_type=spec["zernike_type"])
+    if k == "polynomial":
+        return geometries.PolynomialGeometry(cs, radius=spec["radius"], conic=spec["conic"],
+                                             coefficients=np.array(spec["coefficients"]))
+    if k == "chebyshev":
+        return geometries.ChebyshevPolynomialGeometry(
+            cs, radius=spec["radius"], conic=spec["conic"],
+            coefficients=np.array(spec["coefficients"]), norm_x=spec["norm_x"],
+            norm_y=spec["norm_y"])
+    if k == "biconic":
+        return geometries.BiconicGeometry(cs, radius_x=spec["radius_x"],
+                                          radius_y=spec["radius_y"], conic_x=spec["conic_x"],
+                                          conic_y=spec["conic_y"])
+    if k == "toroidal":
+        return geometries.ToroidalGeometry(cs, radius_x=spec["radius_x"],
+                                           radius_y=spec["radius_y"], conic=spec["conic"],
+                                           coeffs_poly_y=spec["coeffs_poly_y"])
     raise ValueError(k)
 
 
@@ -97,9 +142,15 @@ def points(name, spec, rng):
         X, Y = np.meshgrid(g, g)  # test_geometries.py:888-905
         r = rng.uniform(-1, 1, size=(2, 64)) * spec["norm_radius"] / np.sqrt(2)
         return np.concatenate([X.ravel(), r[0]]), np.concatenate([Y.ravel(), r[1]])
-    base_x = [0.0, 1.0, -2.0, 0.0, 3.0, 8.0, 1.0]
-    base_y = [0.0, 1.0, 3.0, 0.0, -7.0, 2.1, 2.0]
-    lim = 4.0 if spec.get("radius", 100.0) and abs(spec.get("radius", 100.0)) < 15 else 8.0
+    if spec["kind"] == "chebyshev":  # |x / norm| <= 1 (chebyshev.py:203-215)
+        base_x = [0.0, 1.0, -2.0, 0.0, 3.0, 8.0, 1.0, -2.0]
+        base_y = [0.0, 1.0, -7.0, 0.0, -7.0, 2.1, 2.0, 3.0]
+        r = rng.uniform(-9.5, 9.5, size=(2, 64))
+        return np.concatenate([base_x, r[0]]), np.concatenate([base_y, r[1]])
+    base_x = [0.0, 1.0, -2.0, 0.0, 3.0, 8.0, 1.0, -2.0, 10.0, -5.0]
+    base_y = [0.0, 1.0, 3.0, 0.0, -7.0, 2.1, 2.0, -7.0, 1.0, 1.0]
+    rad = min([abs(spec[k]) for k in ("radius", "radius_x", "radius_y") if k in spec] + [100.0])
+    lim = 4.0 if rad < 15 else 8.0
     r = rng.uniform(-lim, lim, size=(2, 64))
     return np.concatenate([base_x, r[0]]), np.concatenate([base_y, r[1]])
 
@@ -115,7 +166,7 @@ def rays(name, spec, rng):
     M = [0.0, 0.0, 0.0, M0]
     N = [1.0, 1.0, 1.0, float(np.sqrt(1 - L0**2 - M0**2))]
     n = 48
-    lim = 2.5 if spec["kind"] == "zernike" else 3.0
+    lim = 2.5 if spec["kind"] in ("zernike", "biconic") else 3.0
     rx = rng.uniform(-lim, lim, n)
     ry = rng.uniform(-lim, lim, n)
     rz = rng.uniform(-6.0, -1.0, n)

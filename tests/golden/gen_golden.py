@@ -172,6 +172,34 @@ def decentered():
     return lens
 
 
+def freeform():
+    """Cooke-triplet layout with a biconic, a toroidal, an XY-polynomial and a Chebyshev
+    surface (covers biconic.py, toroidal.py, polynomial.py, chebyshev.py on the trace)."""
+    lens = ref_optic.Optic()
+    lens.add_surface(index=0, radius=np.inf, thickness=np.inf)
+    lens.add_surface(index=1, surface_type="biconic", radius_x=22.01359, radius_y=23.5,
+                     conic_x=-0.2, conic_y=0.1, thickness=3.25896, material="SK16")
+    lens.add_surface(index=2, surface_type="toroidal", radius_x=-300.0, radius_y=-435.76044,
+                     conic=0.5, toroidal_coeffs_poly_y=[2e-6], thickness=6.00755)
+    lens.add_surface(index=3, radius=-22.21328, thickness=0.99997, material=("F2", "schott"))
+    lens.add_surface(index=4, radius=20.29192, thickness=4.75041, is_stop=True)
+    lens.add_surface(index=5, surface_type="polynomial", radius=79.68360, conic=0.0,
+                     coefficients=[[0.0, 0.0, 2e-4], [0.0, 1e-5, 0.0], [1.5e-4, 0.0, 0.0]],
+                     thickness=2.95208, material="SK16")
+    lens.add_surface(index=6, surface_type="chebyshev", radius=-18.39533, conic=0.0,
+                     coefficients=[[0.0, 1e-3, 2e-3], [5e-4, 0.0, 0.0], [1e-3, 0.0, 0.0]],
+                     thickness=42.20778)
+    lens.add_surface(index=7)
+    lens.set_aperture(aperture_type="EPD", value=10)
+    lens.set_field_type(field_type="angle")
+    lens.add_field(y=0)
+    lens.add_field(y=14)
+    lens.add_field(x=5, y=10)
+    lens.add_wavelength(value=0.55, is_primary=True)
+    lens.update_paraxial()
+    return lens
+
+
 CASES = {
     # name: (builder, fields [(Hx,Hy)], wavelengths, distribution, num)
     "cooke": (CookeTriplet, [(0, 0), (0, 0.7), (0, 1)], [0.48, 0.55, 0.65], "uniform", 32),
@@ -186,6 +214,7 @@ CASES = {
     "tma_noll": (lambda: tma("noll"), [(0, 1)], [0.587], "uniform", 24),
     "cooke_aperture": (cooke_aperture, [(0, 0), (0, 1)], [0.55], "uniform", 32),
     "decentered": (decentered, [(0, 0), (0, 1), (0.5, -0.5)], [0.55], "hexapolar", 8),
+    "freeform": (freeform, [(0, 0), (0, 1), (0.5, 0.7)], [0.48, 0.55, 0.65], "uniform", 24),
 }
 
 
@@ -388,6 +417,17 @@ def full_size_summaries():
 
 
 def main():
+    # --only NAME [NAME ...]: regenerate just those cases, keep the rest of index.json
+    only = sys.argv[sys.argv.index("--only") + 1:] if "--only" in sys.argv else None
+    if only:
+        with open(os.path.join(HERE, "index.json")) as f:
+            index = json.load(f)
+        for name in only:
+            builder, fields, wls, dist, num = CASES[name]
+            index[name] = generate_case(name, builder, fields, wls, dist, num)
+        with open(os.path.join(HERE, "index.json"), "w") as f:
+            json.dump(index, f, indent=1)
+        return
     glass_table()
     index = {}
     for name, (builder, fields, wls, dist, num) in CASES.items():

@@ -45,3 +45,28 @@ def test_reference_lowering_equals_native(ref, name, wls):
     np.testing.assert_array_equal(a.n_tab, b.n_tab)
     np.testing.assert_array_equal(a.alpha_tab, b.alpha_tab)
     assert a.final_mat == b.final_mat and a.final_thickness == b.final_thickness
+
+
+@pytest.mark.parametrize("name", ["freeform", "tma_fringe", "rt_asph"])
+def test_reference_lowering_equals_native_newton(ref, name):
+    """Newton geometries (incl. the freeform kinds): the adapter's lowering of the
+    reference lens equals the native lens's bytes, coefficient blocks included."""
+    import sys
+
+    from optiland_pr_amd.adapter import lower_reference_group
+    from optiland_pr_amd.lowering import lower_surface_group
+    from optiland_pr_amd.samples import GOLDEN_LENSES
+
+    sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
+    import gen_golden
+
+    builder = gen_golden.CASES[name][0]
+    ref_lens = builder()
+    native = GOLDEN_LENSES[name]()
+    wls = [0.55]
+    a = lower_reference_group(ref_lens.surface_group, wls)
+    b = lower_surface_group(native.surface_group, wls)
+    assert a.surfaces.tobytes() == b.surfaces.tobytes()
+    assert a.cs_ops.tobytes() == b.cs_ops.tobytes()
+    np.testing.assert_array_equal(a.coef, b.coef)
+    assert a.zern.tobytes() == b.zern.tobytes()
