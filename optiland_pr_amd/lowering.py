@@ -72,6 +72,12 @@ class LensTable:
     def has_zernike(self):
         return bool(np.any(self.surfaces["geometry"] == _abi.GEOM_ZERNIKE))
 
+    @property
+    def has_range_check(self):
+        """Surfaces whose sag raises on out-of-range normalised coordinates."""
+        g = self.surfaces["geometry"]
+        return bool(np.any((g == _abi.GEOM_ZERNIKE) | (g == _abi.GEOM_CHEBYSHEV)))
+
     def fingerprint(self):
         """Bytes of everything the device reads: equal fingerprints trace identically."""
         parts = [np.ascontiguousarray(a).tobytes() for a in

@@ -35,6 +35,12 @@ class ZernikeRangeError(ValueError):
     pass
 
 
+class ChebyshevRangeError(ValueError):
+    pass
+
+
+_CHEBYSHEV_MSG = ("Chebyshev input coordinates must be normalized to [-1, 1]. Consider "
+                  "updating the normalization factors.")  # chebyshev.py:203-215
 _ZERNIKE_MSG = ("Zernike coordinates must be normalized to [-1, 1]. Consider updating the "
                 "normalization radius to 1.1x the surface aperture.")
 
@@ -224,7 +230,7 @@ def _run(dlens: DeviceLens, launch, n_rays, group_len, keys, newton_mode="refere
     dev = dlens.device
     S = dlens.table.n_surfaces
     n_groups = max(1, -(-n_rays // group_len))
-    need_status = with_status and dlens.table.has_zernike
+    need_status = with_status and dlens.table.has_range_check
     status = torch.zeros(1, dtype=torch.int32, device=dev) if need_status else None
     dlens.last_schedule = None  # the verified [n_groups][S] update counts (VJP replay)
     if not dlens.newton or n_rays == 0:
@@ -263,6 +269,8 @@ def _raise_status(status):
     v = int(status.item())
     if v & _abi.STATUS_ZERNIKE_RANGE:
         raise ZernikeRangeError(_ZERNIKE_MSG)
+    if v & _abi.STATUS_CHEBYSHEV_RANGE:
+        raise ChebyshevRangeError(_CHEBYSHEV_MSG)
 
 
 def upload_segments(segments: np.ndarray, device):

@@ -73,3 +73,18 @@ def test_scalar_default_sag(torch):
     g = build(specs()["even_sag"])
     assert float(g.sag()) == 0.0
     np.testing.assert_allclose(float(g.sag(1, 1)), 0.039022474574473776, rtol=1e-15)
+
+
+def test_chebyshev_range_error(torch):
+    from optiland_pr_amd.coordinate_system import CoordinateSystem
+    from optiland_pr_amd.geometries import ChebyshevPolynomialGeometry
+    from optiland_pr_amd.raytrace import ChebyshevRangeError
+
+    g = ChebyshevPolynomialGeometry(CoordinateSystem(), radius=22.0,
+                                    coefficients=[[0.0, 1e-2], [0.1, 0.0]], norm_x=10,
+                                    norm_y=10)
+    g.sag(np.array([-10.0, 0.0, 10.0]), np.zeros(3))
+    for x, y in ((10.5, 0.0), (0.0, -10.5)):
+        with pytest.raises(ChebyshevRangeError, match="Chebyshev input coordinates must be"):
+            g.sag(x, y)
+    assert issubclass(ChebyshevRangeError, ValueError)
