@@ -17,13 +17,18 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 LIB_DIR = os.path.join(HERE, "lib")
 LIB_PATH = os.path.join(LIB_DIR, "liboptiland_rt.so")
-SOURCES = [os.path.join(HERE, "csrc", "ort_trace.hip")]
-DEPS = SOURCES + [os.path.join(HERE, "csrc", "ort_core.h"),
-                  os.path.join(REPO, "include", "optiland_rt.h")]
+CSRC = os.path.join(HERE, "csrc")
+# one translation unit per kernel family, compiled in parallel, linked into one .so
+SOURCES = [os.path.join(CSRC, f) for f in (
+    "ort_api.hip", "ort_k_closed.hip", "ort_k_trace.hip", "ort_k_trace_rec.hip",
+    "ort_k_vjp.hip", "ort_k_vjp1.hip", "ort_k_vjp2.hip", "ort_k_vjp4.hip", "ort_k_geom.hip")]
+HEADERS = [os.path.join(CSRC, "ort_core.h"), os.path.join(CSRC, "ort_kernels.h"),
+           os.path.join(REPO, "include", "optiland_rt.h")]
+DEPS = SOURCES + HEADERS
 
 # -ffp-contract=off: no a*b+c fusion, so each +,-,*,/ rounds exactly as NumPy does.
 HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-std=c++17", "-fPIC",
-               "-shared", "-Wno-unused-result"]
+               "-Wno-unused-result"]
 
 
 def hipcc():
@@ -33,24 +38,50 @@ def hipcc():
     raise RuntimeError("hipcc not found (ROCm is required to build the MI355X trace core)")
 
 
-def needs_build():
-    if not os.path.exists(LIB_PATH):
+def needs_build(out=None):
+    out = out or LIB_PATH
+    if not os.path.exists(out):
         return True
-    t = os.path.getmtime(LIB_PATH)
+    t = os.path.getmtime(out)
     return any(os.path.getmtime(d) > t for d in DEPS)
 
 
-def build(force=False, verbose=False):
-    if not force and not needs_build():
-        return LIB_PATH
-    os.makedirs(LIB_DIR, exist_ok=True)
-    tmp = LIB_PATH + ".tmp"
-    cmd = [hipcc(), *HIPCC_FLAGS, "-I", os.path.join(REPO, "include"), "-o", tmp, *SOURCES]
+def build(force=False, verbose=False, out=None, extra_flags=(), jobs=None):
+    """Compile every translation unit (in parallel) and link liboptiland_rt.so.
+    out / extra_flags: build a variant library elsewhere (A/B timing)."""
+    out = out or LIB_PATH
+    if not force and not needs_build(out):
+        return out
+    obj_dir = os.path.join(os.path.dirname(out), "obj" + ("" if out == LIB_PATH else "_" +
+                           os.path.splitext(os.path.basename(out))[0]))
+    os.makedirs(obj_dir, exist_ok=True)
+    cc = hipcc()
+    inc = ["-I", os.path.join(REPO, "include")]
+    procs, objs = [], []
+    jobs = jobs or min(len(SOURCES), max(1, os.cpu_count() or 1), 16)
+    pending = list(SOURCES)
+    failed = None
+    while pending or procs:
+        while pending and len(procs) < jobs:
+            src = pending.pop(0)
+            obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
+            objs.append(obj)
+            cmd = [cc, *HIPCC_FLAGS, *extra_flags, *inc, "-c", "-o", obj, src]
+            if verbose:
+                print(" ".join(cmd), file=sys.stderr)
+            procs.append((subprocess.Popen(cmd), src))
+        p, src = procs.pop(0)
+        if p.wait() != 0:
+            failed = src
+    if failed:
+        raise subprocess.CalledProcessError(1, f"hipcc {failed}")
+    tmp = out + ".tmp"
+    cmd = [cc, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", tmp, *objs]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(tmp, LIB_PATH)
-    return LIB_PATH
+    os.replace(tmp, out)
+    return out
 
 
 if __name__ == "__main__":

@@ -48,7 +48,30 @@ using ::cos;
 using ::exp;
 using ::fabs;
 using ::sin;
-using ::sqrt;
+
+// IEEE sqrt. gfx950 lowers a correctly rounded fp64 sqrt to v_rsq_f64 and two Goldschmidt
+// / Newton refinements wrapped in an input scaling (x < 2^-767) and a zero / +inf class
+// fix-up. For 2^-767 <= x < inf the wrappers are identities, so that range runs the
+// refinement alone -- the same instructions on the same values, bit-identical to sqrt(x)
+// -- and every other input (0, tiny, inf, NaN, negative) takes the full sequence.
+ORT_INLINE double sqrt(double x) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(ORT_NO_FAST_SQRT)
+  if (__builtin_expect(x >= 0x1p-767 && x < __builtin_inf(), 1)) {
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y;
+    double h = y * 0.5;
+    const double r = fma(-h, g, 0.5);
+    g = fma(g, r, g);
+    h = fma(h, r, h);
+    double d = fma(-g, g, x);
+    g = fma(d, h, g);
+    d = fma(-g, g, x);
+    g = fma(d, h, g);
+    return g;
+  }
+#endif
+  return ::sqrt(x);
+}
 
 ORT_INLINE double vv(double x) { return x; }
 template <int P>
@@ -158,7 +181,7 @@ ORT_INLINE Dual<P> operator/(double a, const Dual<P>& b) {
 template <int P>
 ORT_INLINE Dual<P> sqrt(const Dual<P>& a) {
   Dual<P> r;
-  r.v = ::sqrt(a.v);
+  r.v = sqrt(a.v);
   const double h = 0.5 / r.v;
 #pragma unroll
   for (int k = 0; k < P; ++k) r.d[k] = a.d[k] * h;
@@ -324,7 +347,7 @@ ORT_INLINE Ray generate_ray(const ort_segment& s, double px, double py) {
   const double y1 = py * s.epd * s.vy / 2.0;  // ray_generator.py:77
   const double z1 = s.epl;
   const double dx = x1 - x0, dy = y1 - y0, dz = z1 - z0;
-  double mag = ::sqrt(dx * dx + dy * dy + dz * dz);  // :80
+  double mag = sqrt(dx * dx + dy * dy + dz * dz);  // :80
   const bool is_zero = mag < 1e-9;                    // :82
   mag = is_zero ? 1.0 : mag;
   const SharedDiv dm = shared_div(mag);

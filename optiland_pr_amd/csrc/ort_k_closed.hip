@@ -1,0 +1,35 @@
+// ort_k_closed.hip -- closed-form-lens kernels and the generation-only kernel
+// (kernel templates: ort_kernels.h; compiled as its own translation unit)
+
+#include "ort_kernels.h"
+
+namespace ortk {
+__global__ __launch_bounds__(kBlock) void generate_kernel(const KArgs a) {
+  const int64_t rid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (rid >= a.n_rays) return;
+  const int64_t sidx = rid / a.seg_len;
+  const ort_segment sg = a.seg[sidx];
+  const int64_t p = a.pupil_per_ray ? rid : (rid - sidx * a.seg_len);
+  const ort::Ray r = ort::generate_ray(sg, a.px[p], a.py[p]);
+  a.out.x[rid] = r.x;
+  a.out.y[rid] = r.y;
+  a.out.z[rid] = r.z;
+  a.out.L[rid] = r.L;
+  a.out.M[rid] = r.M;
+  a.out.N[rid] = r.N;
+  a.out.i[rid] = r.i;
+  a.out.opd[rid] = r.opd;
+}
+
+KernelFn select_generate() { return generate_kernel; }
+
+KernelFn select_closed(uint32_t feat) {
+  switch (feat & (F_GEN | F_REC)) {
+    case 0: return trace_closed_kernel<0>;
+    case F_GEN: return trace_closed_kernel<F_GEN>;
+    case F_REC: return trace_closed_kernel<F_REC>;
+    default: return trace_closed_kernel<F_GEN | F_REC>;
+  }
+}
+
+}  // namespace ortk

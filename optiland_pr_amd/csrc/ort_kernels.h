@@ -1,4 +1,8 @@
-// ort_trace.hip -- MI355X (gfx950) kernels of the sequential real-ray trace + C ABI.
+// ort_kernels.h -- MI355X (gfx950) kernels of the sequential real-ray trace (templates).
+//
+// Shared by the kernel translation units (ort_k_*.hip, compiled in parallel, each
+// instantiating one family of specialisations) and the C ABI (ort_api.hip), which only
+// reaches kernels through the select_* functions declared at the end.
 //
 // One ray per lane, all surfaces fused in one launch. The ray state
 // (x, y, z, L, M, N, i, opd) stays in VGPRs from the first surface to the image; the
@@ -16,12 +20,14 @@
 //
 // Compiled with -ffp-contract=off: see ort_core.h.
 
+#pragma once
+
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 
 #include "ort_core.h"
 
-namespace {
+namespace ortk {
 
 constexpr int kBlock = 256;
 
@@ -335,7 +341,7 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(const KArgs a) {
 // (measured: 2 rays/lane 7% slower at 5 waves/SIMD, 4 rays/lane 28% slower).
 // Per surface: one batch of scalar loads (surface record + optics of this wavelength).
 template <uint32_t FEAT>
-__global__ __launch_bounds__(kBlock) void trace_closed_kernel(const KArgs a) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) void trace_closed_kernel(const KArgs a) {
   const int64_t rid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool active = rid < a.n_rays;
   const int64_t r_ld = active ? rid : 0;
@@ -590,318 +596,15 @@ __global__ __launch_bounds__(kBlock) void geom_kernel(const KArgs a, const GArgs
   if (range_bits && active && a.status) atomicOr(a.status, range_bits);
 }
 
+typedef void (*KernelFn)(const KArgs);
+typedef void (*VjpFn)(const KArgs, const JArgs);
 typedef void (*GeomFn)(const KArgs, const GArgs);
 
-int fill_args(KArgs& a, const ort_lens* lens, const ort_batch* batch, const ort_options* opt,
-              double* rec, ort_newton_stat* stats, int32_t* status, uint32_t& feat);
-int init_outputs(const KArgs& a, hipStream_t stream);
+// kernel selection (defined in the ort_k_*.hip translation units)
+KernelFn select_trace(uint32_t feat);      // Newton lenses, any F_GEN / F_REC  (ort_k_trace*.hip)
+KernelFn select_closed(uint32_t feat);     // closed-form lenses                (ort_k_closed.hip)
+KernelFn select_generate();                // ray generation only               (ort_k_closed.hip)
+VjpFn select_vjp(int tangents, uint32_t km);  // tangents 1, 2 or 4             (ort_k_vjp*.hip)
+GeomFn select_geom(uint32_t km);           // per-geometry primitives           (ort_k_geom.hip)
 
-GeomFn pick_geom(uint32_t km) {
-  switch (km) {
-#define ORT_G(K) \
-  case (K):      \
-    return geom_kernel<(K)>;
-    ORT_G(0) ORT_G(1) ORT_G(2) ORT_G(3) ORT_G(4) ORT_G(5) ORT_G(6) ORT_G(7)
-    ORT_G(8) ORT_G(9) ORT_G(10) ORT_G(11) ORT_G(12) ORT_G(13) ORT_G(14)
-#undef ORT_G
-    default: return geom_kernel<15>;
-  }
-}
-
-int launch_geom(const ort_lens* lens, int32_t surface, int64_t n, const ort_rays* rays,
-                GArgs g, const ort_options* opt, ort_newton_stat* stats, int32_t* status,
-                hipStream_t stream) {
-  if (!lens || n < 0) return ORT_ERR_ARG;
-  if (n == 0) return ORT_OK;
-  if (surface < 0 || surface >= lens->n_surfaces) return ORT_ERR_ARG;
-  const ort_options dflt{ORT_NEWTON_SCHEDULE, 0, nullptr};
-  ort_batch b{};
-  b.n_rays = n;
-  b.seg_len = n;
-  b.group_len = n;  // one reference call: the Newton stop rule spans all n rays
-  KArgs a{};
-  uint32_t feat = 0;
-  int rc = fill_args(a, lens, &b, opt ? opt : &dflt, nullptr, stats, status, feat);
-  if (rc) return rc;
-  if (rays) a.in = *rays;
-  if ((rc = init_outputs(a, stream))) return rc;
-  const int64_t blocks = (n + kBlock - 1) / kBlock;
-  if (blocks > 0x7fffffff) return ORT_ERR_ARG;
-  g.surface = surface;
-  hipLaunchKernelGGL(pick_geom(feat & F_KM), dim3((unsigned)blocks), dim3(kBlock), 0, stream,
-                     a, g);
-  return hipGetLastError() == hipSuccess ? ORT_OK : ORT_ERR_LAUNCH;
-}
-
-typedef void (*VjpFn)(const KArgs, const JArgs);
-
-template <int P>
-VjpFn pick_vjp(uint32_t km) {
-  using namespace ort;
-  switch (km) {
-#define ORT_V(K) \
-  case (K):      \
-    return vjp_kernel<P, (K)>;
-    ORT_V(KM_ZERN) ORT_V(KM_ZERN | KM_EVEN) ORT_V(KM_ZERN | KM_ODD)
-    ORT_V(KM_ZERN | KM_EVEN | KM_ODD) ORT_V(KM_ZERN | KM_FREE)
-    ORT_V(KM_ZERN | KM_FREE | KM_EVEN) ORT_V(KM_ZERN | KM_FREE | KM_ODD)
-    ORT_V(KM_ZERN | KM_FREE | KM_EVEN | KM_ODD)
-#undef ORT_V
-    default: return nullptr;
-  }
-}
-
-__global__ __launch_bounds__(kBlock) void generate_kernel(const KArgs a) {
-  const int64_t rid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (rid >= a.n_rays) return;
-  const int64_t sidx = rid / a.seg_len;
-  const ort_segment sg = a.seg[sidx];
-  const int64_t p = a.pupil_per_ray ? rid : (rid - sidx * a.seg_len);
-  const ort::Ray r = ort::generate_ray(sg, a.px[p], a.py[p]);
-  a.out.x[rid] = r.x;
-  a.out.y[rid] = r.y;
-  a.out.z[rid] = r.z;
-  a.out.L[rid] = r.L;
-  a.out.M[rid] = r.M;
-  a.out.N[rid] = r.N;
-  a.out.i[rid] = r.i;
-  a.out.opd[rid] = r.opd;
-}
-
-typedef void (*KernelFn)(const KArgs);
-
-template <uint32_t FEAT>
-KernelFn pick() {
-  return trace_kernel<FEAT>;
-}
-
-KernelFn select_kernel(uint32_t feat) {
-  switch (feat) {
-#define ORT_CASE(F) \
-  case (F):         \
-    return pick<(F)>();
-#define ORT_CASES(G) ORT_CASE(G | 0) ORT_CASE(G | 1) ORT_CASE(G | 2) ORT_CASE(G | 3) \
-    ORT_CASE(G | 4) ORT_CASE(G | 5) ORT_CASE(G | 6) ORT_CASE(G | 7) ORT_CASE(G | 8)  \
-    ORT_CASE(G | 9) ORT_CASE(G | 10) ORT_CASE(G | 11) ORT_CASE(G | 12) ORT_CASE(G | 13) \
-    ORT_CASE(G | 14) ORT_CASE(G | 15)
-    ORT_CASES(0)
-    ORT_CASES(F_GEN)
-    ORT_CASES(F_REC)
-    ORT_CASES(F_REC | F_GEN)
-#undef ORT_CASES
-#undef ORT_CASE
-    default:
-      return nullptr;
-  }
-}
-
-int fill_args(KArgs& a, const ort_lens* lens, const ort_batch* batch, const ort_options* opt,
-              double* rec, ort_newton_stat* stats, int32_t* status, uint32_t& feat) {
-  if (!lens || !batch || !opt) return ORT_ERR_ARG;
-  if (lens->n_surfaces < 0 || lens->n_surfaces > ORT_MAX_SURFACES) return ORT_ERR_SURFACES;
-  if (lens->n_surfaces > 0 &&
-      (!lens->surfaces || !lens->n_tab || !lens->alpha_tab || !lens->optics))
-    return ORT_ERR_ARG;
-  if (batch->n_rays < 0 || batch->seg_len < 1 || batch->group_len < 1) return ORT_ERR_ARG;
-  if (lens->n_lambda < 1 || lens->n_mat < 1) return ORT_ERR_ARG;
-  if (opt->start_surface < 0) return ORT_ERR_ARG;
-  a.surf = lens->surfaces;
-  a.cs = lens->cs_ops;
-  a.coef = lens->coef;
-  a.zern = lens->zern;
-  a.n_tab = lens->n_tab;
-  a.alpha_tab = lens->alpha_tab;
-  a.optics = lens->optics;
-  a.n_surf = lens->n_surfaces;
-  a.n_lambda = lens->n_lambda;
-  a.n_mat = lens->n_mat;
-  a.final_mat = lens->final_mat;
-  a.final_thickness = lens->final_thickness;
-  a.n_rays = batch->n_rays;
-  a.seg_len = batch->seg_len;
-  a.group_len = batch->group_len;
-  a.seg = batch->seg;
-  a.n_seg = batch->n_seg;
-  a.pupil_per_ray = batch->pupil_per_ray;
-  a.newton_mode = opt->newton_mode;
-  a.start_surface = opt->start_surface;
-  a.sched = opt->sched;
-  a.rec = rec;
-  a.stats = stats;
-  a.status = status;
-  feat = 0;
-  if (lens->geometry_mask & (1u << ORT_GEOM_EVEN_ASPHERE)) feat |= ort::KM_EVEN;
-  if (lens->geometry_mask & (1u << ORT_GEOM_ODD_ASPHERE)) feat |= ort::KM_ODD;
-  if (lens->geometry_mask & (1u << ORT_GEOM_ZERNIKE)) feat |= ort::KM_ZERN;
-  if (lens->geometry_mask & ((1u << ORT_GEOM_POLYNOMIAL) | (1u << ORT_GEOM_CHEBYSHEV) |
-                             (1u << ORT_GEOM_BICONIC) | (1u << ORT_GEOM_TOROIDAL)))
-    feat |= ort::KM_FREE;
-  if (rec) feat |= F_REC;
-  if (opt->newton_mode != ORT_NEWTON_SCHEDULE && opt->newton_mode != ORT_NEWTON_WAVE)
-    return ORT_ERR_ARG;
-  return ORT_OK;
-}
-
-// rays per lane of the closed-form kernel (ORT_RPL overrides, for A/B timing)
-int launch(const KArgs& a, uint32_t feat, hipStream_t stream) {
-  if (a.n_rays == 0) return ORT_OK;
-  KernelFn fn = select_kernel(feat);
-  if ((feat & F_KM) == 0) {  // closed-form lens
-    switch (feat & (F_GEN | F_REC)) {
-      case 0: fn = trace_closed_kernel<0>; break;
-      case F_GEN: fn = trace_closed_kernel<F_GEN>; break;
-      case F_REC: fn = trace_closed_kernel<F_REC>; break;
-      default: fn = trace_closed_kernel<F_GEN | F_REC>; break;
-    }
-  }
-  if (!fn) return ORT_ERR_ARG;
-  const int64_t blocks = (a.n_rays + kBlock - 1) / kBlock;
-  if (blocks > 0x7fffffff) return ORT_ERR_ARG;
-  hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(kBlock), 0, stream, a);
-  return hipGetLastError() == hipSuccess ? ORT_OK : ORT_ERR_LAUNCH;
-}
-
-int init_outputs(const KArgs& a, hipStream_t stream) {
-  if (a.stats) {
-    const int64_t groups = (a.n_rays + a.group_len - 1) / a.group_len;
-    // conv_mask = ~0, last_bad = -1, max_updates = -1 (all 0xFF bytes)
-    if (hipMemsetAsync(a.stats, 0xFF, (size_t)(groups > 0 ? groups : 1) * a.n_surf *
-                                          sizeof(ort_newton_stat),
-                       stream) != hipSuccess)
-      return ORT_ERR_LAUNCH;
-  }
-  if (a.status && hipMemsetAsync(a.status, 0, sizeof(int32_t), stream) != hipSuccess)
-    return ORT_ERR_LAUNCH;
-  return ORT_OK;
-}
-
-}  // namespace
-
-extern "C" {
-
-int ort_abi_version(void) { return ORT_ABI_VERSION; }
-
-int ort_trace_sequential(const ort_lens* lens, const ort_rays* rays_in, ort_rays* rays_out,
-                         const ort_batch* batch, const ort_options* opt, double* rec,
-                         ort_newton_stat* newton_stat, int32_t* status, void* stream) {
-  if (!rays_in || !rays_out || !batch) return ORT_ERR_ARG;
-  if (batch->n_rays == 0) return ORT_OK;
-  KArgs a{};
-  uint32_t feat = 0;
-  int rc = fill_args(a, lens, batch, opt, rec, newton_stat, status, feat);
-  if (rc) return rc;
-  a.in = *rays_in;
-  a.out = *rays_out;
-  hipStream_t s = (hipStream_t)stream;
-  if ((rc = init_outputs(a, s))) return rc;
-  return launch(a, feat, s);
-}
-
-int ort_trace_pupil(const ort_lens* lens, const double* px, const double* py,
-                    ort_rays* rays_out, const ort_batch* batch, const ort_options* opt,
-                    double* rec, ort_newton_stat* newton_stat, int32_t* status,
-                    void* stream) {
-  if (!rays_out || !batch) return ORT_ERR_ARG;
-  if (batch->n_rays == 0) return ORT_OK;
-  if (!px || !py || !batch->seg) return ORT_ERR_ARG;
-  KArgs a{};
-  uint32_t feat = 0;
-  int rc = fill_args(a, lens, batch, opt, rec, newton_stat, status, feat);
-  if (rc) return rc;
-  a.px = px;
-  a.py = py;
-  a.out = *rays_out;
-  feat |= F_GEN;
-  hipStream_t s = (hipStream_t)stream;
-  if ((rc = init_outputs(a, s))) return rc;
-  return launch(a, feat, s);
-}
-
-int ort_trace_pupil_vjp(const ort_lens* lens, const double* px, const double* py,
-                        const ort_batch* batch, const ort_options* opt,
-                        const int32_t* zern_param, int32_t n_param,
-                        const ort_rays* cotangent, double* grad, void* stream) {
-  if (!batch || !cotangent || n_param < 0) return ORT_ERR_ARG;
-  if (batch->n_rays == 0 || n_param == 0) return ORT_OK;
-  if (!px || !py || !batch->seg || !zern_param || !grad) return ORT_ERR_ARG;
-  KArgs a{};
-  uint32_t feat = 0;
-  int rc = fill_args(a, lens, batch, opt, nullptr, nullptr, nullptr, feat);
-  if (rc) return rc;
-  if (opt->newton_mode != ORT_NEWTON_SCHEDULE) return ORT_ERR_ARG;
-  if ((feat & ort::KM_ZERN) == 0) return ORT_ERR_ARG;  // no Zernike surface to seed
-  a.px = px;
-  a.py = py;
-  JArgs j{};
-  j.zparam = zern_param;
-  j.n_param = n_param;
-  j.cot = *cotangent;
-  j.grad = grad;
-  const int64_t blocks = (a.n_rays + kBlock - 1) / kBlock;
-  if (blocks > 0x7fffffff) return ORT_ERR_ARG;
-  const uint32_t km = feat & F_KM;
-  hipStream_t s = (hipStream_t)stream;
-  for (int p0 = 0; p0 < n_param;) {
-    const int left = n_param - p0;
-    // tangents per launch: ORT_VJP_TANGENTS overrides (A/B timing)
-    const char* e = getenv("ORT_VJP_TANGENTS");
-    const int pref = e ? atoi(e) : 4;
-    const int P = left >= 4 && pref >= 4 ? 4 : (left >= 2 && pref >= 2 ? 2 : 1);
-    VjpFn fn = P == 4 ? pick_vjp<4>(km) : (P == 2 ? pick_vjp<2>(km) : pick_vjp<1>(km));
-    if (!fn) return ORT_ERR_ARG;
-    j.p0 = p0;
-    hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(kBlock), 0, s, a, j);
-    if (hipGetLastError() != hipSuccess) return ORT_ERR_LAUNCH;
-    p0 += P;
-  }
-  return ORT_OK;
-}
-
-int ort_surface_sag_normal(const ort_lens* lens, int32_t surface, const double* x,
-                           const double* y, int64_t n, double* sag, double* nx, double* ny,
-                           double* nz, int32_t* status, void* stream) {
-  if (n > 0 && (!x || !y)) return ORT_ERR_ARG;
-  GArgs g{};
-  g.mode = 0;
-  g.x = x;
-  g.y = y;
-  g.sag = sag;
-  g.nx = nx;
-  g.ny = ny;
-  g.nz = nz;
-  return launch_geom(lens, surface, n, nullptr, g, nullptr, nullptr, status,
-                     (hipStream_t)stream);
-}
-
-int ort_surface_distance(const ort_lens* lens, int32_t surface, const ort_rays* rays,
-                         int64_t n, const ort_options* opt, double* t,
-                         ort_newton_stat* newton_stat, int32_t* status, void* stream) {
-  if (n > 0 && (!rays || !t)) return ORT_ERR_ARG;
-  GArgs g{};
-  g.mode = 1;
-  g.t = t;
-  return launch_geom(lens, surface, n, rays, g, opt, newton_stat, status,
-                     (hipStream_t)stream);
-}
-
-int ort_generate_rays(const double* px, const double* py, ort_rays* rays_out,
-                      const ort_batch* batch, void* stream) {
-  if (!rays_out || !batch) return ORT_ERR_ARG;
-  if (batch->n_rays == 0) return ORT_OK;
-  if (!px || !py || !batch->seg || batch->seg_len < 1) return ORT_ERR_ARG;
-  KArgs a{};
-  a.px = px;
-  a.py = py;
-  a.out = *rays_out;
-  a.n_rays = batch->n_rays;
-  a.seg_len = batch->seg_len;
-  a.seg = batch->seg;
-  a.pupil_per_ray = batch->pupil_per_ray;
-  if (a.n_rays == 0) return ORT_OK;
-  const int64_t blocks = (a.n_rays + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(generate_kernel, dim3((unsigned)blocks), dim3(kBlock), 0,
-                     (hipStream_t)stream, a);
-  return hipGetLastError() == hipSuccess ? ORT_OK : ORT_ERR_LAUNCH;
-}
-
-}  // extern "C"
+}  // namespace ortk

@@ -10,3 +10,4 @@ for rep in 1 2; do
     [ $rc -ne 0 ] && exit $rc
   done
 done
+exit 0
