@@ -77,6 +77,7 @@ int fill_args(KArgs& a, const ort_lens* lens, const ort_batch* batch, const ort_
                              (1u << ORT_GEOM_BICONIC) | (1u << ORT_GEOM_TOROIDAL)))
     feat |= ort::KM_FREE;
   if (rec) feat |= F_REC;
+  if (lens->n_lambda == 1) feat |= F_MONO;
   if (opt->newton_mode != ORT_NEWTON_SCHEDULE && opt->newton_mode != ORT_NEWTON_WAVE)
     return ORT_ERR_ARG;
   return ORT_OK;
@@ -84,7 +85,7 @@ int fill_args(KArgs& a, const ort_lens* lens, const ort_batch* batch, const ort_
 
 int launch(const KArgs& a, uint32_t feat, hipStream_t stream) {
   if (a.n_rays == 0) return ORT_OK;
-  KernelFn fn = (feat & F_KM) == 0 ? select_closed(feat) : select_trace(feat);
+  KernelFn fn = (feat & F_KM) == 0 ? select_closed(feat) : select_trace(feat & ~F_MONO);
   if (!fn) return ORT_ERR_ARG;
   const int64_t blocks = (a.n_rays + kBlock - 1) / kBlock;
   if (blocks > 0x7fffffff) return ORT_ERR_ARG;

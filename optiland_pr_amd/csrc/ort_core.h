@@ -56,21 +56,23 @@ using ::sin;
 // -- and every other input (0, tiny, inf, NaN, negative) takes the full sequence.
 ORT_INLINE double sqrt(double x) {
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(ORT_NO_FAST_SQRT)
-  if (__builtin_expect(x >= 0x1p-767 && x < __builtin_inf(), 1)) {
-    const double y = __builtin_amdgcn_rsq(x);
-    double g = x * y;
-    double h = y * 0.5;
-    const double r = fma(-h, g, 0.5);
-    g = fma(g, r, g);
-    h = fma(h, r, h);
-    double d = fma(-g, g, x);
-    g = fma(d, h, g);
-    d = fma(-g, g, x);
-    g = fma(d, h, g);
-    return g;
-  }
-#endif
+  // the refinement runs unconditionally (no data-dependent branch around the common
+  // case); the rare out-of-range lanes redo it with the full sequence
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y;
+  double h = y * 0.5;
+  const double r = fma(-h, g, 0.5);
+  g = fma(g, r, g);
+  h = fma(h, r, h);
+  double d = fma(-g, g, x);
+  g = fma(d, h, g);
+  d = fma(-g, g, x);
+  g = fma(d, h, g);
+  if (__builtin_expect(!(x >= 0x1p-767 && x < __builtin_inf()), 0)) g = ::sqrt(x);
+  return g;
+#else
   return ::sqrt(x);
+#endif
 }
 
 ORT_INLINE double vv(double x) { return x; }
@@ -284,12 +286,15 @@ ORT_INLINE SharedDiv shared_div(double b) {
 }
 
 ORT_INLINE double sdiv(double a, const SharedDiv& d) {
-  if (__builtin_expect(d.ok && div_range_ok(a), 1)) {
-    const double q0 = a * d.y;
-    const double r = fma(-d.b, q0, a);
-    return fma(r, d.y, q0);
-  }
+#if defined(__HIP_DEVICE_COMPILE__)
+  const double q0 = a * d.y;
+  const double r = fma(-d.b, q0, a);
+  double q = fma(r, d.y, q0);
+  if (__builtin_expect(!(d.ok && div_range_ok(a)), 0)) q = a / d.b;
+  return q;
+#else
   return a / d.b;
+#endif
 }
 
 template <int P>

@@ -24,11 +24,14 @@ __global__ __launch_bounds__(kBlock) void generate_kernel(const KArgs a) {
 KernelFn select_generate() { return generate_kernel; }
 
 KernelFn select_closed(uint32_t feat) {
-  switch (feat & (F_GEN | F_REC)) {
-    case 0: return trace_closed_kernel<0>;
-    case F_GEN: return trace_closed_kernel<F_GEN>;
-    case F_REC: return trace_closed_kernel<F_REC>;
-    default: return trace_closed_kernel<F_GEN | F_REC>;
+  switch (feat & (F_GEN | F_REC | F_MONO)) {
+#define ORT_C(F) \
+  case (F):      \
+    return trace_closed_kernel<(F)>;
+    ORT_C(0) ORT_C(F_GEN) ORT_C(F_REC) ORT_C(F_GEN | F_REC)
+    ORT_C(F_MONO) ORT_C(F_MONO | F_GEN) ORT_C(F_MONO | F_REC) ORT_C(F_MONO | F_GEN | F_REC)
+#undef ORT_C
+    default: return nullptr;
   }
 }
 

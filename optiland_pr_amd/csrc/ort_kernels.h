@@ -54,7 +54,8 @@ constexpr ort::ZSeed kNoSeed{nullptr, 0};
 enum : uint32_t {
   F_KM = 15u,
   F_GEN = 1u << 4,
-  F_REC = 1u << 5,  // some surfaces are recorded (standard_surface.py:266-286)
+  F_REC = 1u << 5,   // some surfaces are recorded (standard_surface.py:266-286)
+  F_MONO = 1u << 6,  // one wavelength in the lens tables (closed-form kernels only)
 };
 
 struct KArgs {
@@ -122,8 +123,12 @@ __device__ inline double tab(const double* t, int n_lambda, int n_mat, int lam, 
 }
 
 // Optical constants of surface si at the ray's wavelength (same scalar-load batch as the
-// surface record when the lens is traced at one wavelength).
+// surface record when the lens is traced at one wavelength). F_MONO makes that a
+// compile-time fact: with a run-time test the compiler merges both loads into one
+// per-lane vector load through a selected address, a dependent round trip per surface.
+template <uint32_t FEAT = 0>
 __device__ inline ort_surface_optics optics_at(const KArgs& a, int lam, int si) {
+  if constexpr ((FEAT & F_MONO) != 0) return cst(a.optics)[si];
   if (a.n_lambda == 1) return cst(a.optics)[si];
   return a.optics[lam * a.n_surf + si];
 }
@@ -367,7 +372,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
   }
   for (int si = a.start_surface; si < a.n_surf; ++si) {
     const ort_surface s = cst(a.surf)[si];
-    const ort_surface_optics o = optics_at(a, lam, si);
+    const ort_surface_optics o = optics_at<FEAT>(a, lam, si);
     localize(a, s, r);
     const bool is_plane = s.geometry == ORT_GEOM_PLANE;
     const double t = is_plane ? ort::distance_plane(r)
@@ -403,7 +408,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
   }
   if (a.final_mat >= 0)
     ort::propagate(r, a.final_thickness,
-                   tab(a.alpha_tab, a.n_lambda, a.n_mat, lam, a.final_mat));
+                   (FEAT & F_MONO) ? cst(a.alpha_tab)[a.final_mat]
+                                   : tab(a.alpha_tab, a.n_lambda, a.n_mat, lam, a.final_mat));
   if (!active) return;
   a.out.x[rid] = r.x;
   a.out.y[rid] = r.y;
