@@ -59,8 +59,8 @@ enum ort_surface_flags {
   ORT_SURF_RADIUS_INF = 1u << 1, /* standard.py:100-103 plane branch of a conic guess   */
   ORT_SURF_APERTURE = 1u << 2,   /* radial physical aperture: physical_apertures/radial.py */
   ORT_SURF_RECORD = 1u << 3,     /* snapshot the ray state after this surface (_record)  */
-  ORT_SURF_TRANSLATE = 1u << 4   /* the frame is a pure translation by cs_t (no rotation, */
-                                 /* no reference_cs): localize adds -cs_t, globalize +cs_t */
+  ORT_SURF_TRANSLATE = 1u << 4   /* informational: the frame is the translation cs_t only  */
+                                 /* (both op lists empty)                                  */
 };
 
 /* ---- coordinate-system op (coordinate_system.py:73-107, real_rays.py:90-130) ---- */
@@ -78,8 +78,9 @@ typedef struct ort_cs_op {
 } ort_cs_op; /* 32 bytes */
 
 /* One traced surface (the object surface is not in the table: it only records,
- * object_surface.py:56-72). Localize = cs ops [cs_loc_off, +n_cs_loc) applied in
- * order; globalize = [cs_glob_off, +n_cs_glob) applied in order. */
+ * object_surface.py:56-72). Localize = translate by -cs_t, then cs ops
+ * [cs_loc_off, +n_cs_loc) in order; globalize = cs ops [cs_glob_off, +n_cs_glob) in
+ * order, then translate by +cs_t. */
 typedef struct ort_surface {
   double radius;      /* R (may be +-inf)                                            */
   double conic;       /* k                                                           */
@@ -99,8 +100,9 @@ typedef struct ort_surface {
   int32_t cs_glob_off;
   int32_t n_cs_glob;
   int32_t rec_slot;   /* slot in the record buffer when ORT_SURF_RECORD              */
-  double cs_t[3];     /* vertex (x, y, z) when ORT_SURF_TRANSLATE (the op lists hold  */
-  double reserved;    /* the same translation for the general path)                   */
+  double cs_t[3];     /* root-frame translation: localize = x + -cs_t, then the loc    */
+                      /* ops; globalize = the glob ops, then x + cs_t                  */
+  double reserved;
 } ort_surface; /* 128 bytes */
 
 /* Per (wavelength, surface) optical constants, read in the same scalar-load batch as

@@ -133,28 +133,24 @@ __device__ inline ort_surface_optics optics_at(const KArgs& a, int lam, int si) 
   return a.optics[lam * a.n_surf + si];
 }
 
-// localize / globalize (coordinate_system.py:73-107): pure translations inline,
-// general frames through the op list
+// localize / globalize (coordinate_system.py:73-107): the root frame's translation
+// (cs_t) inline and unconditional, the rest (rotations, reference_cs chains) through the
+// op lists, which are empty for plain decentred surfaces (no branch, no register
+// shuffling around one)
 template <class T>
 __device__ inline void localize(const KArgs& a, const ort_surface& s, ort::RayT<T>& r) {
-  if (s.flags & ORT_SURF_TRANSLATE) {
-    r.x = r.x + -s.cs_t[0];
-    r.y = r.y + -s.cs_t[1];
-    r.z = r.z + -s.cs_t[2];
-    return;
-  }
+  r.x = r.x + -s.cs_t[0];
+  r.y = r.y + -s.cs_t[1];
+  r.z = r.z + -s.cs_t[2];
   for (int c = 0; c < s.n_cs_loc; ++c) ort::apply_cs_op(r, cst(a.cs)[s.cs_loc_off + c]);
 }
 
 template <class T>
 __device__ inline void globalize(const KArgs& a, const ort_surface& s, ort::RayT<T>& r) {
-  if (s.flags & ORT_SURF_TRANSLATE) {
-    r.x = r.x + s.cs_t[0];
-    r.y = r.y + s.cs_t[1];
-    r.z = r.z + s.cs_t[2];
-    return;
-  }
   for (int c = 0; c < s.n_cs_glob; ++c) ort::apply_cs_op(r, cst(a.cs)[s.cs_glob_off + c]);
+  r.x = r.x + s.cs_t[0];
+  r.y = r.y + s.cs_t[1];
+  r.z = r.z + s.cs_t[2];
 }
 
 // status bit of a normalisation-range error at surface s (zernike.py:234-246,

@@ -158,19 +158,22 @@ def lower_surface_group(surface_group, wavelengths, record=False, skip_object=Tr
         row["mat_post"] = mat_id(s.material_post)
         loc = g.cs.localize_ops()
         glob = g.cs.globalize_ops()
+        # localize starts with translate(-t) of the root frame and globalize ends with
+        # translate(+t) (coordinate_system.py:73-107): that pair lives in cs_t (the kernel
+        # adds -cs_t / +cs_t unconditionally), the op lists hold the rest
+        t = glob[-1][1]
+        assert loc[0][0] == _abi.CS_TRANSLATE and glob[-1][0] == _abi.CS_TRANSLATE
+        assert tuple(loc[0][1]) == (-t[0], -t[1], -t[2])
+        loc, glob = loc[1:], glob[:-1]
+        row["cs_t"] = t
         row["cs_loc_off"] = len(ops)
         row["n_cs_loc"] = len(loc)
         ops.extend(loc)
         row["cs_glob_off"] = len(ops)
         row["n_cs_glob"] = len(glob)
         ops.extend(glob)
-        if (len(loc) == 1 and len(glob) == 1 and loc[0][0] == _abi.CS_TRANSLATE
-                and glob[0][0] == _abi.CS_TRANSLATE):
-            # pure translation: localize adds -t, globalize adds +t (exact negation)
-            t = glob[0][1]
-            if tuple(loc[0][1]) == (-t[0], -t[1], -t[2]):
-                row["flags"] = int(row["flags"]) | _abi.SURF_TRANSLATE
-                row["cs_t"] = t
+        if not loc and not glob:
+            row["flags"] = int(row["flags"]) | _abi.SURF_TRANSLATE
 
     final = surfs[-1]
     final_mat = mat_id(final.material_post)

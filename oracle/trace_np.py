@@ -638,6 +638,9 @@ def trace_segment(table, rays: Rays, lam: int, record=False, sched=None, start=0
         s = table.surfaces[si]
         g = int(s["geometry"])
         flags = int(s["flags"])
+        # localize: translate(-t) of the root frame, then the remaining ops
+        ct = s["cs_t"]
+        r.x, r.y, r.z = r.x + -float(ct[0]), r.y + -float(ct[1]), r.z + -float(ct[2])
         apply_cs(r, table.cs_ops[int(s["cs_loc_off"]):int(s["cs_loc_off"]) + int(s["n_cs_loc"])])
         if g == _abi.GEOM_PLANE:
             t = distance_plane(r)
@@ -660,6 +663,7 @@ def trace_segment(table, rays: Rays, lam: int, record=False, sched=None, start=0
         else:
             refract(r, nx, ny, nz, n_tab[mp], n_tab[mq])
         apply_cs(r, table.cs_ops[int(s["cs_glob_off"]):int(s["cs_glob_off"]) + int(s["n_cs_glob"])])
+        r.x, r.y, r.z = r.x + float(ct[0]), r.y + float(ct[1]), r.z + float(ct[2])
         if record:
             records[si] = r.copy()
     if table.final_mat >= 0:
