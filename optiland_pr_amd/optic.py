@@ -99,6 +99,18 @@ class Optic:
                 s.geometry.norm_radius = float(s.semi_aperture * 1.25)
         self._lowered = None
 
+    # -- serialisation (optic.py:649-713; lensio.py) -----------------------------------
+    def to_dict(self):
+        from .lensio import optic_to_dict
+
+        return optic_to_dict(self)
+
+    @classmethod
+    def from_dict(cls, data):
+        from .lensio import optic_from_dict
+
+        return optic_from_dict(data)
+
     # -- tracing ----------------------------------------------------------------------
     def trace(self, Hx, Hy, wavelength, num_rays=100, distribution="hexapolar"):
         """optic.py:584-609 -> RealRayTracer.trace (HIP)."""

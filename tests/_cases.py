@@ -1,5 +1,7 @@
 """Shared helpers: rebuild a golden case with the NATIVE host API (optiland_pr_amd)."""
 
+import os
+
 import numpy as np
 
 from optiland_pr_amd import _abi
@@ -7,9 +9,24 @@ from optiland_pr_amd.lowering import lower_surface_group, segment_params
 from optiland_pr_amd.samples import GOLDEN_LENSES
 
 
+JSON_LENSES = {"json_cooke": "cooke_triplet", "json_heliar": "heliar",
+               "json_rt": "reverse_telephoto"}
+
+
+def build_lens(name):
+    """Native lens of a golden case: a sample class, or a reference JSON lens file read
+    with the native loader (optiland_pr_amd.lensio)."""
+    if name in JSON_LENSES:
+        from optiland_pr_amd.lensio import load_optiland_json
+
+        return load_optiland_json(os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                               "golden", "lenses", JSON_LENSES[name] + ".json"))
+    return GOLDEN_LENSES[name]()
+
+
 def native_case(name, meta, record=False):
     """-> (optic, LensTable, segments [n_pairs] (field-major, then wavelength), keys)."""
-    lens = GOLDEN_LENSES[name]()
+    lens = build_lens(name)
     wls = meta["wavelengths"]
     table = lower_surface_group(lens.surface_group, wls, record=record)
     EPL, EPD = lens.paraxial.EPL(), lens.paraxial.EPD()
@@ -22,7 +39,8 @@ def native_case(name, meta, record=False):
 
 # golden cases whose every traced surface is closed-form (plane / conic): the oracle and
 # the HIP kernel reproduce the reference bit for bit there
-CLOSED_FORM = ("cooke", "dg", "rt", "cooke_aperture", "decentered")
+CLOSED_FORM = ("cooke", "dg", "rt", "cooke_aperture", "decentered", "json_cooke",
+               "json_heliar", "json_rt")
 NEWTON = ("rt_asph", "rt_odd", "tma_fringe", "tma_standard", "tma_noll", "freeform")
 ALL_CASES = CLOSED_FORM + NEWTON
 

@@ -200,6 +200,15 @@ def freeform():
     return lens
 
 
+def json_lens(name):
+    """A lens file from the reference's docs/samples (copied as data to tests/golden/lenses),
+    loaded with the reference's own Optic.from_dict (optic.py:674-713)."""
+    def build():
+        with open(os.path.join(HERE, "lenses", name + ".json")) as f:
+            return ref_optic.Optic.from_dict(json.load(f))
+    return build
+
+
 CASES = {
     # name: (builder, fields [(Hx,Hy)], wavelengths, distribution, num)
     "cooke": (CookeTriplet, [(0, 0), (0, 0.7), (0, 1)], [0.48, 0.55, 0.65], "uniform", 32),
@@ -215,6 +224,10 @@ CASES = {
     "cooke_aperture": (cooke_aperture, [(0, 0), (0, 1)], [0.55], "uniform", 32),
     "decentered": (decentered, [(0, 0), (0, 1), (0.5, -0.5)], [0.55], "hexapolar", 8),
     "freeform": (freeform, [(0, 0), (0, 1), (0.5, 0.7)], [0.48, 0.55, 0.65], "uniform", 24),
+    "json_cooke": (json_lens("cooke_triplet"), [(0, 0), (0, 1)], [0.55], "uniform", 24),
+    "json_heliar": (json_lens("heliar"), [(0, 0), (0, 0.7), (0, 1)], [0.4861, 0.5876],
+                    "uniform", 24),
+    "json_rt": (json_lens("reverse_telephoto"), [(0, 0), (0, 1)], [0.5876], "uniform", 24),
 }
 
 
@@ -340,7 +353,8 @@ def glass_table():
     """Bake the dispersion data of every catalog glass the sample lenses use."""
     specs = [("SK16", None), ("F2", "schott"), ("N-SSK2", None), ("N-SK2", None),
              ("F5", "schott"), ("N-SK16", None), ("N-SK10", None), ("SK15", None),
-             ("BASF2", None), ("FK3", None), ("SF15", "hikari"), ("N-LAK12", None)]
+             ("BASF2", None), ("FK3", None), ("SF15", "hikari"), ("N-LAK12", None),
+             ("E-LLF6", None)]
     out = {}
     for name, ref in specs:
         m = Material(name, ref) if ref else Material(name)
@@ -418,6 +432,9 @@ def full_size_summaries():
 
 def main():
     # --only NAME [NAME ...]: regenerate just those cases, keep the rest of index.json
+    if "--glasses" in sys.argv:  # re-bake optiland_pr_amd/data/glasses.json only
+        glass_table()
+        return
     only = sys.argv[sys.argv.index("--only") + 1:] if "--only" in sys.argv else None
     if only:
         with open(os.path.join(HERE, "index.json")) as f:

@@ -10,7 +10,7 @@ import pytest
 from optiland_pr_amd import _abi
 from optiland_pr_amd.materials import Material
 from optiland_pr_amd.samples import GOLDEN_LENSES
-from tests._cases import ALL_CASES, native_case
+from tests._cases import ALL_CASES, build_lens, native_case
 from tests.conftest import REPO, load_golden
 
 
@@ -32,7 +32,7 @@ def test_unknown_glass_raises():
 @pytest.mark.parametrize("name", ALL_CASES)
 def test_paraxial_and_positions(name, golden_index):
     meta = golden_index[name]
-    lens = GOLDEN_LENSES[name]()
+    lens = build_lens(name)
     g = load_golden(name)
     assert lens.paraxial.EPL() == meta["EPL"]
     assert lens.paraxial.EPD() == meta["EPD"]
