@@ -33,7 +33,9 @@ from .materials import IdealMaterial, Material
 from .surfaces import ObjectSurface, RadialAperture, Surface
 
 _FIELD_TYPES = {"AngleField": "angle", "ObjectHeightField": "object_height",
-                "angle": "angle", "object_height": "object_height"}
+                "ParaxialImageHeightField": "paraxial_image_height",
+                "angle": "angle", "object_height": "object_height",
+                "paraxial_image_height": "paraxial_image_height"}
 
 
 def _f(v, default=0.0):

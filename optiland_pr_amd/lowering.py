@@ -225,6 +225,21 @@ def lower_geometry(geometry):
 # --------------------------------------------------------------------------------------
 # ray-generation scalars per (field, wavelength) segment
 # --------------------------------------------------------------------------------------
+def _unit_chief_rays(optic):
+    """ParaxialImageHeightField._trace_unit_chief_ray (field_types.py:461-479): y at the
+    image of a (y=0, u=1) ray from the stop, and y, u at the object of the same ray traced
+    backwards."""
+    sg = optic.surface_group
+    stop = sg.stop_index
+    pos = sg.positions
+    wl = optic.primary_wavelength
+    y, _ = optic.paraxial._trace_generic(y=0, u=1, z=pos[stop], wavelength=wl, skip=stop)
+    y_img = y[-1]
+    y, u = optic.paraxial._trace_generic(y=0, u=1, z=pos[-1] - pos[stop], wavelength=wl,
+                                         reverse=True, skip=sg.num_surfaces - stop)
+    return y_img, y[-1], u[-1]
+
+
 def _starting_z_offset(optic):
     """field_types.py:223-235."""
     z = optic.surface_group.positions[1:-1]
@@ -269,6 +284,28 @@ def segment_params(optic, Hx, Hy, lambda_idx, EPL=None, EPD=None):
         seg["x_off"] = float(np.array(field_x))
         seg["y_off"] = float(np.array(field_y))
         seg["z0"] = float(obj.geometry.cs.z)  # plane object: sag 0 (field_types.py:273)
+    elif optic.field_type == "paraxial_image_height":
+        # ParaxialImageHeightField.get_ray_origins (field_types.py:336-390): the object-side
+        # chief-ray slope / height that lands the paraxial chief ray at the target image
+        # height, from unit chief rays traced forward and backward from the stop
+        y_img_unit, y_obj_unit, u_obj_unit = _unit_chief_rays(optic)
+        if obj.is_infinite:
+            u_obj_y = u_obj_unit * (field_y / y_img_unit)
+            u_obj_x = u_obj_unit * (field_x / y_img_unit)
+            offset = _starting_z_offset(optic)
+            x = -u_obj_x * (offset + EPL)
+            y = -u_obj_y * (offset + EPL)
+            z = optic.surface_group.positions[1] - offset
+            seg["mode"] = _abi.GEN_INFINITE
+            seg["x_off"], seg["y_off"] = float(np.ravel(x)[0]), float(np.ravel(y)[0])
+            seg["z0"] = float(np.ravel(z)[0])
+        else:
+            y_obj = y_obj_unit * (field_y / y_img_unit)
+            x_obj = y_obj_unit * (field_x / y_img_unit)
+            seg["mode"] = _abi.GEN_FINITE
+            seg["x_off"] = float(np.ravel(x_obj)[0])
+            seg["y_off"] = float(np.ravel(y_obj)[0])
+            seg["z0"] = float(0.0 + obj.geometry.cs.z)  # plane object: sag 0
     else:
         raise ValueError(f"field type {optic.field_type!r} not supported")
     seg["epd"] = float(EPD)

@@ -52,8 +52,8 @@ class Optic:
         self.aperture = Aperture(aperture_type, value)
 
     def set_field_type(self, field_type):
-        """optic.py:298-318: 'angle' | 'object_height'."""
-        if field_type not in ("angle", "object_height"):
+        """optic.py:298-318: 'angle' | 'object_height' | 'paraxial_image_height'."""
+        if field_type not in ("angle", "object_height", "paraxial_image_height"):
             raise ValueError(f"field type {field_type!r} is not supported by the trace core")
         self.field_type = field_type
 

@@ -150,9 +150,14 @@ class Paraxial:
             scaling_factor = target_slope / u_obj_unit
         elif fd == "object_height":
             scaling_factor = self.optic.fields.max_y_field / y_obj_unit
+        elif fd == "paraxial_image_height":  # field_types.py:423-440
+            scaling_factor = self.optic.fields.max_y_field / y_img_unit
         else:
             raise NotImplementedError(fd)
-        y_obj_start = -(y_obj_unit * scaling_factor)
+        if fd == "paraxial_image_height":
+            y_obj_start = y_obj_unit * scaling_factor
+        else:
+            y_obj_start = -(y_obj_unit * scaling_factor)
         u_obj_start = u_obj_unit * scaling_factor
         if self.optic.object_surface.is_infinite:
             EPL = self.EPL()

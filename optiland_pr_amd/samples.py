@@ -223,6 +223,46 @@ class FreeformTriplet(Optic):
         self.update_paraxial()
 
 
+def _cooke_prescription(lens, object_thickness):
+    lens.add_surface(index=0, radius=np.inf, thickness=object_thickness)
+    lens.add_surface(index=1, radius=22.01359, thickness=3.25896, material="SK16")
+    lens.add_surface(index=2, radius=-435.76044, thickness=6.00755)
+    lens.add_surface(index=3, radius=-22.21328, thickness=0.99997, material=("F2", "schott"))
+    lens.add_surface(index=4, radius=20.29192, thickness=4.75041, is_stop=True)
+    lens.add_surface(index=5, radius=79.68360, thickness=2.95208, material="SK16")
+    lens.add_surface(index=6, radius=-18.39533, thickness=42.20778)
+    lens.add_surface(index=7)
+    lens.set_aperture(aperture_type="EPD", value=10)
+
+
+class CookeTripletImageHeight(Optic):
+    """Cooke triplet with fields given as paraxial image heights (ParaxialImageHeightField,
+    field_types.py:333-479), object at infinity."""
+
+    def __init__(self):
+        super().__init__()
+        _cooke_prescription(self, np.inf)
+        self.set_field_type(field_type="paraxial_image_height")
+        self.add_field(y=0)
+        self.add_field(y=10)
+        self.add_field(y=17)
+        self.add_wavelength(value=0.55, is_primary=True)
+
+
+class FiniteTripletImageHeight(Optic):
+    """The same triplet imaging an object 200 mm in front of it, fields as paraxial image
+    heights (the finite-conjugate branch of ParaxialImageHeightField)."""
+
+    def __init__(self):
+        super().__init__()
+        _cooke_prescription(self, 200.0)
+        self.set_field_type(field_type="paraxial_image_height")
+        self.add_field(y=0)
+        self.add_field(y=2)
+        self.add_field(y=4)
+        self.add_wavelength(value=0.55, is_primary=True)
+
+
 GOLDEN_LENSES = {
     "cooke": CookeTriplet,
     "dg": DoubleGauss,
@@ -235,4 +275,6 @@ GOLDEN_LENSES = {
     "cooke_aperture": CookeTripletApertures,
     "decentered": DecenteredTriplet,
     "freeform": FreeformTriplet,
+    "cooke_pih": CookeTripletImageHeight,
+    "finite_pih": FiniteTripletImageHeight,
 }

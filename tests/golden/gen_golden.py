@@ -200,6 +200,43 @@ def freeform():
     return lens
 
 
+def _cooke_prescription(lens, object_thickness):
+    lens.add_surface(index=0, radius=np.inf, thickness=object_thickness)
+    lens.add_surface(index=1, radius=22.01359, thickness=3.25896, material="SK16")
+    lens.add_surface(index=2, radius=-435.76044, thickness=6.00755)
+    lens.add_surface(index=3, radius=-22.21328, thickness=0.99997, material=("F2", "schott"))
+    lens.add_surface(index=4, radius=20.29192, thickness=4.75041, is_stop=True)
+    lens.add_surface(index=5, radius=79.68360, thickness=2.95208, material="SK16")
+    lens.add_surface(index=6, radius=-18.39533, thickness=42.20778)
+    lens.add_surface(index=7)
+    lens.set_aperture(aperture_type="EPD", value=10)
+
+
+def cooke_pih():
+    """Cooke triplet, fields as paraxial image heights (field_types.py:333-479), object at
+    infinity."""
+    lens = ref_optic.Optic()
+    _cooke_prescription(lens, np.inf)
+    lens.set_field_type(field_type="paraxial_image_height")
+    lens.add_field(y=0)
+    lens.add_field(y=10)
+    lens.add_field(y=17)
+    lens.add_wavelength(value=0.55, is_primary=True)
+    return lens
+
+
+def finite_pih():
+    """The triplet with the object 200 mm in front, fields as paraxial image heights."""
+    lens = ref_optic.Optic()
+    _cooke_prescription(lens, 200.0)
+    lens.set_field_type(field_type="paraxial_image_height")
+    lens.add_field(y=0)
+    lens.add_field(y=2)
+    lens.add_field(y=4)
+    lens.add_wavelength(value=0.55, is_primary=True)
+    return lens
+
+
 def json_lens(name):
     """A lens file from the reference's docs/samples (copied as data to tests/golden/lenses),
     loaded with the reference's own Optic.from_dict (optic.py:674-713)."""
@@ -228,6 +265,8 @@ CASES = {
     "json_heliar": (json_lens("heliar"), [(0, 0), (0, 0.7), (0, 1)], [0.4861, 0.5876],
                     "uniform", 24),
     "json_rt": (json_lens("reverse_telephoto"), [(0, 0), (0, 1)], [0.5876], "uniform", 24),
+    "cooke_pih": (cooke_pih, [(0, 0), (0, 0.6), (0.3, 1)], [0.55], "uniform", 24),
+    "finite_pih": (finite_pih, [(0, 0), (0, 1), (-0.4, 0.7)], [0.48, 0.55], "uniform", 24),
 }
 
 
