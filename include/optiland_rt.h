@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define ORT_ABI_VERSION 3
+#define ORT_ABI_VERSION 4
 #define ORT_MAX_SURFACES 64
 
 /* ---- geometry kinds ----------------------------------- */
@@ -249,21 +249,34 @@ int ort_trace_pupil(const ort_lens* lens, const double* px, const double* py,
                     double* rec, ort_newton_stat* newton_stat, int32_t* status,
                     void* stream);
 
-/* Backward of ort_trace_pupil w.r.t. Zernike coefficients: the vector-Jacobian product
- *   grad[p] += sum_rays sum_f cotangent.f[ray] * d out.f[ray] / d c_p
+/* Parameters of the backward pass. Parameter p (0 <= p < n_param) enters the trace
+ * through any of: the coefficient of Zernike term j of lens->zern (zern_param[j] == p),
+ * the radius / conic / vertex z of traced surface s (surf_tangent[(p*S + s)*3 + 0/1/2]
+ * = d value / d p; a thickness variable moves the vertices after it), the image-space
+ * propagation distance (final_tangent[p]). NULL tables contribute nothing. */
+typedef struct ort_vjp_params {
+  int32_t n_param;
+  int32_t reserved;
+  const int32_t* zern_param;   /* [n_zern_terms] parameter index per term, < 0: constant */
+  const double* surf_tangent;  /* [n_param][n_surfaces][3]                              */
+  const double* final_tangent; /* [n_param]                                             */
+} ort_vjp_params;
+
+/* Backward of ort_trace_pupil: the vector-Jacobian product
+ *   grad[p] += sum_rays sum_f cotangent.f[ray] * d out.f[ray] / d param_p
  * for the output fields f of rays_out (x, y, z, L, M, N, i, opd; a NULL cotangent field
- * counts as zero). zern_param[j] maps Zernike term j of lens->zern (its coefficient
- * lens->zern[j].c) to parameter p in [0, n_param), or < 0 for a constant term.
- * opt must be ORT_NEWTON_SCHEDULE with the schedule the verified primal trace ran
- * (the derivative is that of the unrolled Newton iteration, as torch autograd computes
- * it through newton_raphson.py:137-166). grad is accumulated with device atomics: zero
- * it first. Replaces reverse-mode torch autograd through the trace (SurfaceGroup.trace
- * under the torch backend, driven by optimization/optimizer/torch/base.py:95-154 with
- * variable/zernike_coeff.py:71-95 writing the coefficients). */
+ * counts as zero). opt must be ORT_NEWTON_SCHEDULE with the schedule the verified primal
+ * trace ran (the derivative is that of the unrolled Newton iteration, as torch autograd
+ * computes it through newton_raphson.py:137-166). grad is accumulated with device
+ * atomics: zero it first. Ray generation is not differentiated (the reference builds
+ * its paraxial quantities from detached copies, surface_group.py:143-153). Replaces
+ * reverse-mode torch autograd through the trace (SurfaceGroup.trace under the torch
+ * backend, driven by optimization/optimizer/torch/base.py:95-154; variables written by
+ * variable/{zernike_coeff,radius,conic,thickness}.py). */
 int ort_trace_pupil_vjp(const ort_lens* lens, const double* px, const double* py,
                         const ort_batch* batch, const ort_options* opt,
-                        const int32_t* zern_param, int32_t n_param,
-                        const ort_rays* cotangent, double* grad, void* stream);
+                        const ort_vjp_params* params, const ort_rays* cotangent,
+                        double* grad, void* stream);
 
 /* Per-geometry primitives of traced surface `surface` of `lens`, in the surface's local
  * frame (no localize / globalize), for n points or rays:

@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import numpy as np
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 MAX_SURFACES = 64
 
 # enum ort_geometry

@@ -47,6 +47,16 @@ class ort_batch(C.Structure):
     ]
 
 
+class ort_vjp_params(C.Structure):
+    _fields_ = [
+        ("n_param", C.c_int32),
+        ("reserved", C.c_int32),
+        ("zern_param", C.c_void_p),
+        ("surf_tangent", C.c_void_p),
+        ("final_tangent", C.c_void_p),
+    ]
+
+
 class ort_options(C.Structure):
     _fields_ = [
         ("newton_mode", C.c_int32),
@@ -90,7 +100,7 @@ def load(path: str | None = None):
                                     C.c_void_p, C.c_void_p]
     lib.ort_trace_pupil_vjp.restype = C.c_int
     lib.ort_trace_pupil_vjp.argtypes = [P(ort_lens), C.c_void_p, C.c_void_p, P(ort_batch),
-                                        P(ort_options), C.c_void_p, C.c_int32, P(ort_rays),
+                                        P(ort_options), P(ort_vjp_params), P(ort_rays),
                                         C.c_void_p, C.c_void_p]
     lib.ort_surface_sag_normal.restype = C.c_int
     lib.ort_surface_sag_normal.argtypes = [P(ort_lens), C.c_int32, C.c_void_p, C.c_void_p,

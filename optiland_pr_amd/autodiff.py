@@ -14,9 +14,13 @@ carry dual numbers through exactly the Newton update counts the primal ran, and 
 kernel contracts them with the incoming cotangents on the device. No torch graph is
 built over the per-ray arithmetic; torch only sees one autograd node per trace.
 
-Scope: Zernike coefficients of ZernikePolynomialGeometry surfaces (the reference's
-ZernikeCoefficientVariable). The image-surface record (surface_group.x[-1], ...) and
-the returned rays are differentiable; records of other surfaces are not.
+Parameters: Zernike coefficients, surface radius and conic (geometry.radius / .k) and
+thickness (Optic.set_thickness moves the later vertices), i.e. what the reference's
+ZernikeCoefficientVariable / RadiusVariable / ConicVariable / ThicknessVariable write.
+As in the reference, ray generation (EPL, EPD, ray origins) is not differentiated: its
+paraxial inputs are rebuilt from detached copies there (surface_group.py:143-153,
+backend be.array). The image-surface record (surface_group.x[-1], ...) and the returned
+rays are differentiable; records of other surfaces are not.
 """
 
 from __future__ import annotations
@@ -33,33 +37,56 @@ except ImportError:  # pragma: no cover
     torch = None
 
 
+def _is_leaf_param(v):
+    return torch is not None and torch.is_tensor(v) and v.requires_grad
+
+
 def zernike_parameters(optic):
     """[(traced-surface index, coefficient tensor)] for every Zernike surface whose
     coefficients are a torch tensor that requires grad (index into the lowered table)."""
+    return [(si, t) for kind, si, t in parameters(optic) if kind == "zernike"]
+
+
+def parameters(optic):
+    """[(kind, traced-surface index, tensor)]: every lens parameter that is a torch tensor
+    requiring grad -- what the reference's optimisation variables write
+    (variable/zernike_coeff.py:71-95, radius.py, conic.py, thickness.py through
+    optic_updater.py:37-86): Zernike coefficients ("zernike"), geometry.radius
+    ("radius"), geometry.k ("conic"), surface.thickness ("thickness")."""
     from .geometries import ZernikePolynomialGeometry
     from .surfaces import ObjectSurface
 
     if torch is None:
         return []
     sg = getattr(optic, "surface_group", optic)
-    traced = [s for s in sg.surfaces if not isinstance(s, ObjectSurface)]
     out = []
-    for si, s in enumerate(traced):
+    traced = 0
+    for s in sg.surfaces:
+        if isinstance(s, ObjectSurface):
+            if _is_leaf_param(getattr(s, "thickness", None)):
+                raise NotImplementedError("the object distance is not differentiated "
+                                          "(ray generation is not part of the backward)")
+            continue
         g = s.geometry
-        if isinstance(g, ZernikePolynomialGeometry):
-            c = g.coefficients
-            if torch.is_tensor(c) and c.requires_grad:
-                out.append((si, c))
+        if isinstance(g, ZernikePolynomialGeometry) and _is_leaf_param(g.coefficients):
+            out.append(("zernike", traced, g.coefficients))
+        if _is_leaf_param(getattr(g, "radius", None)):
+            out.append(("radius", traced, g.radius))
+        if _is_leaf_param(getattr(g, "k", None)):
+            out.append(("conic", traced, g.k))
+        if _is_leaf_param(getattr(s, "thickness", None)):
+            out.append(("thickness", traced, s.thickness))
+        traced += 1
     return out
 
 
 def wants_grad(optic):
-    return torch is not None and torch.is_grad_enabled() and bool(zernike_parameters(optic))
+    return torch is not None and torch.is_grad_enabled() and bool(parameters(optic))
 
 
 def parameter_map(table, params):
     """zern_param[j] for every Zernike term row j of the lowered table: index into the
-    concatenation of the parameter tensors, or -1."""
+    concatenation of the (Zernike) parameter tensors, or -1."""
     zp = np.full(max(1, len(table.zern)), -1, dtype=np.int32)
     off = 0
     for si, c in params:
@@ -73,12 +100,54 @@ def parameter_map(table, params):
     return zp, off
 
 
+def tangent_tables(table, params):
+    """Lay the parameters out for ort_vjp_params: -> (zern_param or None, surf_tangent
+    [n_param][S][3] or None, final_tangent [n_param] or None, n_param, sizes)."""
+    from . import _abi
+
+    S = table.n_surfaces
+    n_param = sum(int(t.numel()) for _, _, t in params)
+    zp = None
+    surf = None
+    final = None
+    off = 0
+    sizes = []
+    for kind, si, t in params:
+        n = int(t.numel())
+        sizes.append(n)
+        row = table.surfaces[si]
+        if kind == "zernike":
+            if zp is None:
+                zp = np.full(max(1, len(table.zern)), -1, dtype=np.int32)
+            if n != int(row["n_coef"]):
+                raise ValueError(f"surface {si}: {n} coefficients, lowered {int(row['n_coef'])}")
+            base = int(row["coef_off"])
+            zp[base:base + n] = np.arange(off, off + n, dtype=np.int32)
+        else:
+            if surf is None:
+                surf = np.zeros((n_param, S, 3), dtype=np.float64)
+            g = int(row["geometry"])
+            if kind in ("radius", "conic"):
+                if g in (_abi.GEOM_PLANE, _abi.GEOM_BICONIC, _abi.GEOM_TOROIDAL):
+                    raise NotImplementedError(f"surface {si}: {kind} of this geometry is "
+                                              "not a differentiable parameter here")
+                surf[off, si, 0 if kind == "radius" else 1] = 1.0
+            else:  # thickness after surface si moves every later vertex (set_thickness)
+                surf[off, si + 1:, 2] = 1.0
+                if si == S - 1:  # the image surface's thickness: the final propagate
+                    if final is None:
+                        final = np.zeros(n_param, dtype=np.float64)
+                    final[off] = 1.0
+        off += n
+    return zp, surf, final, n_param, sizes
+
+
 class _TracePupilFn(torch.autograd.Function if torch is not None else object):
-    """outputs (x, y, z, L, M, N, i, opd) of ort_trace_pupil as functions of the
-    coefficient tensors."""
+    """outputs (x, y, z, L, M, N, i, opd) of ort_trace_pupil as functions of the lens
+    parameter tensors."""
 
     @staticmethod
-    def forward(ctx, plan, *coeffs):
+    def forward(ctx, plan, *tensors):
         from .raytrace import RealRays, trace_pupil
 
         dl = plan["dlens"]
@@ -90,9 +159,8 @@ class _TracePupilFn(torch.autograd.Function if torch is not None else object):
         ctx.set_materialize_grads(False)
         ctx.sched_dev = (None if sched is None else
                          torch.from_numpy(np.ascontiguousarray(sched.reshape(-1))).to(dl.device))
-        ctx.shapes = [(c.numel(), c.shape, c.device, c.dtype) for c in coeffs]
-        outs = tuple(getattr(out, a) for a in _abi.RAY_FIELDS)
-        return outs
+        ctx.shapes = [(t.numel(), t.shape, t.device, t.dtype) for t in tensors]
+        return tuple(getattr(out, a) for a in _abi.RAY_FIELDS)
 
     @staticmethod
     def backward(ctx, *grads):
@@ -100,11 +168,9 @@ class _TracePupilFn(torch.autograd.Function if torch is not None else object):
         dl = plan["dlens"]
         n_param = plan["n_param"]
         g = torch.zeros(n_param, dtype=torch.float64, device=dl.device)
-        cot = []
-        for gr in grads:
-            cot.append(None if gr is None else gr.to(torch.float64).contiguous())
+        cot = [None if gr is None else gr.to(torch.float64).contiguous() for gr in grads]
         vjp(dl, plan["seg_dev"], plan["px"], plan["py"], plan["n"], plan["seg_len"],
-            ctx.sched_dev, plan["zparam_dev"], n_param, cot, g)
+            ctx.sched_dev, plan["tables"], n_param, cot, g)
         res = [None]
         off = 0
         for numel, shape, dev, dtype in ctx.shapes:
@@ -113,9 +179,10 @@ class _TracePupilFn(torch.autograd.Function if torch is not None else object):
         return tuple(res)
 
 
-def vjp(dlens, seg_dev, px, py, n, seg_len, sched_dev, zparam_dev, n_param, cot, grad,
+def vjp(dlens, seg_dev, px, py, n, seg_len, sched_dev, tables, n_param, cot, grad,
         pupil_per_ray=False):
-    """grad += J^T cot through ort_trace_pupil_vjp. cot: 8 device tensors or None."""
+    """grad += J^T cot through ort_trace_pupil_vjp. tables: device tensors
+    (zern_param, surf_tangent, final_tangent), each possibly None; cot: 8 tensors / None."""
     from .raytrace import _ptr, _stream_handle
 
     lib = _native.load()
@@ -123,19 +190,24 @@ def vjp(dlens, seg_dev, px, py, n, seg_len, sched_dev, zparam_dev, n_param, cot,
     batch = _native.ort_batch(n, seg_len, n, n_seg, int(pupil_per_ray), seg_dev.data_ptr())
     opt = _native.ort_options(_abi.NEWTON_SCHEDULE, 0,
                               None if sched_dev is None else sched_dev.data_ptr())
+    zp, st, ft = tables
+    params = _native.ort_vjp_params(int(n_param), 0, _ptr(zp).value, _ptr(st).value,
+                                    _ptr(ft).value)
     cot_c = _native.ort_rays(*(0 if c is None else c.data_ptr() for c in cot))
     rc = lib.ort_trace_pupil_vjp(C.byref(dlens.c), _ptr(px), _ptr(py), C.byref(batch),
-                                 C.byref(opt), _ptr(zparam_dev), int(n_param),
-                                 C.byref(cot_c), _ptr(grad), _stream_handle())
+                                 C.byref(opt), C.byref(params), C.byref(cot_c), _ptr(grad),
+                                 _stream_handle())
     _native.check(rc, "ort_trace_pupil_vjp")
 
 
 def trace_pupil_grad(optic, dlens, seg_dev, px, py, n, seg_len, wavelength, keys):
     """Differentiable fused trace: returns the 8 output tensors connected to the
-    coefficient tensors of zernike_parameters(optic)."""
-    params = zernike_parameters(optic)
-    zp, n_param = parameter_map(dlens.table, params)
+    parameter tensors of parameters(optic)."""
+    params = parameters(optic)
+    zp, st, ft, n_param, _ = tangent_tables(dlens.table, params)
+    dev = dlens.device
+    tables = tuple(None if a is None else torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+                   for a in (zp, st, ft))
     plan = dict(dlens=dlens, seg_dev=seg_dev, px=px, py=py, n=n, seg_len=seg_len,
-                wavelength=wavelength, keys=keys, n_param=n_param,
-                zparam_dev=torch.from_numpy(zp).to(dlens.device))
-    return _TracePupilFn.apply(plan, *[c for _, c in params])
+                wavelength=wavelength, keys=keys, n_param=n_param, tables=tables)
+    return _TracePupilFn.apply(plan, *[t for _, _, t in params])

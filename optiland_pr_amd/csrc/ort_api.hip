@@ -153,21 +153,24 @@ int ort_trace_pupil(const ort_lens* lens, const double* px, const double* py,
 
 int ort_trace_pupil_vjp(const ort_lens* lens, const double* px, const double* py,
                         const ort_batch* batch, const ort_options* opt,
-                        const int32_t* zern_param, int32_t n_param,
-                        const ort_rays* cotangent, double* grad, void* stream) {
-  if (!batch || !cotangent || n_param < 0) return ORT_ERR_ARG;
+                        const ort_vjp_params* params, const ort_rays* cotangent,
+                        double* grad, void* stream) {
+  if (!batch || !cotangent || !params || params->n_param < 0) return ORT_ERR_ARG;
+  const int32_t n_param = params->n_param;
   if (batch->n_rays == 0 || n_param == 0) return ORT_OK;
-  if (!px || !py || !batch->seg || !zern_param || !grad) return ORT_ERR_ARG;
+  if (!px || !py || !batch->seg || !grad) return ORT_ERR_ARG;
   KArgs a{};
   uint32_t feat = 0;
   int rc = fill_args(a, lens, batch, opt, nullptr, nullptr, nullptr, feat);
   if (rc) return rc;
   if (opt->newton_mode != ORT_NEWTON_SCHEDULE) return ORT_ERR_ARG;
-  if ((feat & ort::KM_ZERN) == 0) return ORT_ERR_ARG;  // no Zernike surface to seed
+  if (params->zern_param && (feat & ort::KM_ZERN) == 0) return ORT_ERR_ARG;
   a.px = px;
   a.py = py;
   JArgs j{};
-  j.zparam = zern_param;
+  j.zparam = params->zern_param;
+  j.tan_surf = params->surf_tangent;
+  j.tan_final = params->final_tangent;
   j.n_param = n_param;
   j.cot = *cotangent;
   j.grad = grad;

@@ -76,8 +76,16 @@ ORT_INLINE double sqrt(double x) {
 }
 
 ORT_INLINE double vv(double x) { return x; }
+ORT_INLINE bool tangent_free(double) { return true; }
 template <int P>
 ORT_INLINE double vv(const Dual<P>& x) { return x.v; }
+template <int P>
+ORT_INLINE bool tangent_free(const Dual<P>& x) {
+  bool z = true;
+#pragma unroll
+  for (int k = 0; k < P; ++k) z = z && x.d[k] == 0.0;
+  return z;
+}
 
 template <int P>
 ORT_INLINE Dual<P> operator+(const Dual<P>& a, const Dual<P>& b) {
@@ -418,8 +426,8 @@ ORT_INLINE T distance_plane(const RayT<T>& r) {
 }
 
 // standard.py:89-140
-template <class T>
-ORT_INLINE T distance_conic(const RayT<T>& r, double R, double k, bool radius_inf) {
+template <class T, class S>
+ORT_INLINE T distance_conic(const RayT<T>& r, const S& R, const S& k, bool radius_inf) {
   if (radius_inf) {
     const T Ns = ::fabs(vv(r.N)) > 1e-14 ? r.N : T(1e-14);
     return -r.z / Ns;
@@ -428,7 +436,7 @@ ORT_INLINE T distance_conic(const RayT<T>& r, double R, double k, bool radius_in
   const T z2 = r.z * r.z;
   T a, b, c;
   // 2*k*N*z + 2*L*x + 2*M*y - 2*N*R + 2*N*z: every "2*" is an exact scaling
-  if (k == 0.0) {
+  if (vv(k) == 0.0 && tangent_free(k)) {
     // sphere: k*N**2 = 0, 2*k*N*z = 0, k*z**2 = 0 and 0 + v == v, so the conic terms
     // drop out without changing a bit (for finite rays)
     a = r.L * r.L + r.M * r.M + N2;
@@ -453,8 +461,9 @@ ORT_INLINE T distance_conic(const RayT<T>& r, double R, double k, bool radius_in
 }
 
 // standard.py:154-167
-template <class T>
-ORT_INLINE void normal_conic(const T& x, const T& y, double R, double k, T& nx, T& ny, T& nz) {
+template <class T, class S>
+ORT_INLINE void normal_conic(const T& x, const T& y, const S& R, const S& k, T& nx, T& ny,
+                             T& nz) {
   const T r2 = x * x + y * y;
   const T denom = R * sqrt(1.0 - (1.0 + k) * r2 / (R * R));
   const auto dd = shared_div(denom);
@@ -468,8 +477,8 @@ ORT_INLINE void normal_conic(const T& x, const T& y, double R, double k, T& nx, 
 }
 
 // base conic sag, standard.py:73-87 (shared by every Newton geometry)
-template <class T>
-ORT_INLINE T sag_conic(const T& r2, double R, double k) {
+template <class T, class S>
+ORT_INLINE T sag_conic(const T& r2, const S& R, const S& k) {
   return r2 / (R * (1.0 + sqrt(1.0 - (1.0 + k) * r2 / (R * R))));
 }
 
@@ -495,8 +504,8 @@ ORT_INLINE T ipow(const T& x, int p) {
 // sag alone (the convergence check after the last update).
 
 // even_asphere.py:82-98 (sag) + :100-129 (normal)
-template <class T, class PD>
-ORT_INLINE T sagnorm_even(const T& x, const T& y, double R, double k, PD C, int nc,
+template <class T, class S, class PD>
+ORT_INLINE T sagnorm_even(const T& x, const T& y, const S& R, const S& k, PD C, int nc,
                           bool want_normal, T& nx, T& ny, T& nz) {
   const T r2 = x * x + y * y;
   const T q = sqrt(1.0 - (1.0 + k) * r2 / (R * R));
@@ -527,8 +536,8 @@ ORT_INLINE T sagnorm_even(const T& x, const T& y, double R, double k, PD C, int 
 
 // odd_asphere.py:73-89 (sag) + :91-130 (normal; non-finite per-term slopes are zeroed,
 // :112-122)
-template <class T, class PD>
-ORT_INLINE T sagnorm_odd(const T& x, const T& y, double R, double k, PD C, int nc,
+template <class T, class S, class PD>
+ORT_INLINE T sagnorm_odd(const T& x, const T& y, const S& R, const S& k, PD C, int nc,
                          bool want_normal, T& nx, T& ny, T& nz) {
   const T r2 = x * x + y * y;
   const T r = sqrt(r2);
@@ -572,8 +581,9 @@ ORT_INLINE T np_sign(const T& v) {  // np.sign: 0 -> 0, NaN -> NaN
 }
 
 // polynomial.py:93-140: conic + sum_ij C_ij x^i y^j
-template <class T, class PD>
-ORT_INLINE T sagnorm_poly(const T& x, const T& y, double R, double k, PD B, bool want_normal,
+template <class T, class S, class PD>
+ORT_INLINE T sagnorm_poly(const T& x, const T& y, const S& R, const S& k, PD B,
+                          bool want_normal,
                           T& nx, T& ny, T& nz) {
   const int ni = (int)B[0], nj = (int)B[1];
   const PD C = B + 2;
@@ -634,8 +644,9 @@ ORT_INLINE T cheb_dt(int n, const T& u) {
   return (double)n * sin((double)n * acos(u)) / sqrt(1.0 - u * u);
 }
 
-template <class T, class PD>
-ORT_INLINE T sagnorm_cheb(const T& x, const T& y, double R, double k, PD B, bool want_normal,
+template <class T, class S, class PD>
+ORT_INLINE T sagnorm_cheb(const T& x, const T& y, const S& R, const S& k, PD B,
+                          bool want_normal,
                           bool& range_error, T& nx, T& ny, T& nz) {
   const int ni = (int)B[0], nj = (int)B[1];
   const double norm_x = B[2], norm_y = B[3];
@@ -829,8 +840,8 @@ ORT_INLINE void polar_unit(const T& xn, const T& yn, const T& rho, T& c1, T& s1)
 // sag (zernike.py:133-161; sets range_error on |x/R_norm| > 1 or |y/R_norm| > 1,
 // :234-246) and, with want_normal, the normal (zernike.py:163-231; the normal omits the
 // normalisation constant: reference quirk)
-template <class T, class PD, class PZ>
-ORT_INLINE T sagnorm_zernike(const T& x, const T& y, double R, double k, double Rn, PZ Tm,
+template <class T, class S, class PD, class PZ>
+ORT_INLINE T sagnorm_zernike(const T& x, const T& y, const S& R, const S& k, double Rn, PZ Tm,
                              int t0, int nt, PD coef, const ZSeed& zs, bool want_normal,
                              bool& range_error, T& nx, T& ny, T& nz) {
   const T xn = x / Rn;
@@ -930,31 +941,32 @@ ORT_INLINE T sagnorm_zernike(const T& x, const T& y, double R, double k, double 
 // runtime switch.
 enum : unsigned { KM_EVEN = 1u, KM_ODD = 2u, KM_ZERN = 4u, KM_FREE = 8u };
 
-template <unsigned KM, class T, class PD, class PZ>
-ORT_INLINE T newton_sagnorm(const ort_surface& s, PD coef, PZ zern, const ZSeed& zs,
-                            const T& x, const T& y, bool want_normal, bool& range_error,
-                            T& nx, T& ny, T& nz) {
+// R, K: the surface's radius and conic (double, or seeded duals in the derivative kernels)
+template <unsigned KM, class T, class S, class PD, class PZ>
+ORT_INLINE T newton_sagnorm(const ort_surface& s, const S& R, const S& K, PD coef, PZ zern,
+                            const ZSeed& zs, const T& x, const T& y, bool want_normal,
+                            bool& range_error, T& nx, T& ny, T& nz) {
   const PD C = coef + s.coef_off;
   if constexpr ((KM & KM_EVEN) != 0) {
     if (KM == KM_EVEN || s.geometry == ORT_GEOM_EVEN_ASPHERE)
-      return sagnorm_even(x, y, s.radius, s.conic, C, s.n_coef, want_normal, nx, ny, nz);
+      return sagnorm_even(x, y, R, K, C, s.n_coef, want_normal, nx, ny, nz);
   }
   if constexpr ((KM & KM_ODD) != 0) {
     if ((KM & ~KM_ODD) == 0 || s.geometry == ORT_GEOM_ODD_ASPHERE)
-      return sagnorm_odd(x, y, s.radius, s.conic, C, s.n_coef, want_normal, nx, ny, nz);
+      return sagnorm_odd(x, y, R, K, C, s.n_coef, want_normal, nx, ny, nz);
   }
   if constexpr ((KM & KM_ZERN) != 0) {
     if ((KM & ~KM_ZERN) == 0 || s.geometry == ORT_GEOM_ZERNIKE)
-      return sagnorm_zernike(x, y, s.radius, s.conic, s.norm_radius, zern, s.coef_off,
-                             s.n_coef, coef, zs, want_normal, range_error, nx, ny, nz);
+      return sagnorm_zernike(x, y, R, K, s.norm_radius, zern, s.coef_off, s.n_coef, coef, zs,
+                             want_normal, range_error, nx, ny, nz);
   }
   if constexpr ((KM & KM_FREE) != 0) {
     switch (s.geometry) {
       case ORT_GEOM_POLYNOMIAL:
-        return sagnorm_poly(x, y, s.radius, s.conic, C, want_normal, nx, ny, nz);
+        return sagnorm_poly(x, y, R, K, C, want_normal, nx, ny, nz);
       case ORT_GEOM_CHEBYSHEV: {
         bool cerr = false;
-        const T z = sagnorm_cheb(x, y, s.radius, s.conic, C, want_normal, cerr, nx, ny, nz);
+        const T z = sagnorm_cheb(x, y, R, K, C, want_normal, cerr, nx, ny, nz);
         if (cerr) range_error = true;
         return z;
       }
@@ -968,24 +980,24 @@ ORT_INLINE T newton_sagnorm(const ort_surface& s, PD coef, PZ zern, const ZSeed&
   return T(NAN);
 }
 
-template <unsigned KM, class T, class PD, class PZ>
-ORT_INLINE void newton_normal(const ort_surface& s, PD coef, PZ zern, const ZSeed& zs,
-                              const T& x, const T& y, T& nx, T& ny, T& nz) {
+template <unsigned KM, class T, class S, class PD, class PZ>
+ORT_INLINE void newton_normal(const ort_surface& s, const S& R, const S& K, PD coef, PZ zern,
+                              const ZSeed& zs, const T& x, const T& y, T& nx, T& ny, T& nz) {
   bool rerr = false;  // the normal never raises (zernike.py:163-231)
-  (void)newton_sagnorm<KM>(s, coef, zern, zs, x, y, true, rerr, nx, ny, nz);
+  (void)newton_sagnorm<KM>(s, R, K, coef, zern, zs, x, y, true, rerr, nx, ny, nz);
 }
 
 // One Newton evaluation at t (newton_raphson.py:140-146): returns f(t) = sag(P(t)) - z(t)
 // and, with want_normal, the normal at P(t) for the update.
-template <unsigned KM, class T, class PD, class PZ>
-ORT_INLINE T newton_eval(const ort_surface& s, PD coef, PZ zern, const ZSeed& zs,
-                         const RayT<T>& r, const T& t, bool want_normal, bool& range_error,
-                         T& nx, T& ny, T& nz) {
+template <unsigned KM, class T, class S, class PD, class PZ>
+ORT_INLINE T newton_eval(const ort_surface& s, const S& R, const S& K, PD coef, PZ zern,
+                         const ZSeed& zs, const RayT<T>& r, const T& t, bool want_normal,
+                         bool& range_error, T& nx, T& ny, T& nz) {
   const T xi = r.x + t * r.L;
   const T yi = r.y + t * r.M;
   const T zi = r.z + t * r.N;
-  return newton_sagnorm<KM>(s, coef, zern, zs, xi, yi, want_normal, range_error, nx, ny, nz) -
-         zi;
+  return newton_sagnorm<KM>(s, R, K, coef, zern, zs, xi, yi, want_normal, range_error, nx, ny,
+                            nz) - zi;
 }
 
 // newton_raphson.py:154-166: t_new = t - f / f'(t) from the normal at P(t)
@@ -1063,32 +1075,32 @@ ORT_INLINE void reflect(RayT<T>& r, T nx, T ny, T nz) {
 }
 
 // surface normal at the current (local) ray position
-template <unsigned KM, class T, class PD, class PZ>
-ORT_INLINE void surface_normal(const ort_surface& s, PD coef, PZ zern, const ZSeed& zs,
-                               const RayT<T>& r, T& nx, T& ny, T& nz) {
+template <unsigned KM, class T, class S, class PD, class PZ>
+ORT_INLINE void surface_normal(const ort_surface& s, const S& R, const S& K, PD coef, PZ zern,
+                               const ZSeed& zs, const RayT<T>& r, T& nx, T& ny, T& nz) {
   switch (s.geometry) {
     case ORT_GEOM_PLANE:  // plane.py:79-98
       nx = T(0.0); ny = T(0.0); nz = T(1.0);
       break;
     case ORT_GEOM_STANDARD:
-      normal_conic(r.x, r.y, s.radius, s.conic, nx, ny, nz);
+      normal_conic(r.x, r.y, R, K, nx, ny, nz);
       break;
     default:
-      newton_normal<KM>(s, coef, zern, zs, r.x, r.y, nx, ny, nz);
+      newton_normal<KM>(s, R, K, coef, zern, zs, r.x, r.y, nx, ny, nz);
   }
 }
 
 // everything in Surface.trace after the distance t is known
 // (standard_surface.py:215-231 minus localize/globalize)
-template <unsigned KM, class T, class PD, class PZ>
-ORT_INLINE void finish_surface(RayT<T>& r, const ort_surface& s, PD coef, PZ zern,
-                               const ZSeed& zs, const T& t, double n_pre, double u,
-                               double alpha_pre) {
+template <unsigned KM, class T, class S, class PD, class PZ>
+ORT_INLINE void finish_surface(RayT<T>& r, const ort_surface& s, const S& R, const S& K,
+                               PD coef, PZ zern, const ZSeed& zs, const T& t, double n_pre,
+                               double u, double alpha_pre) {
   propagate(r, t, alpha_pre);
   add_opd(r, t, n_pre);
   if (s.flags & ORT_SURF_APERTURE) clip_radial(r, s.ap_rmax2, s.ap_rmin2);
   T nx, ny, nz;
-  surface_normal<KM>(s, coef, zern, zs, r, nx, ny, nz);
+  surface_normal<KM>(s, R, K, coef, zern, zs, r, nx, ny, nz);
   if (s.flags & ORT_SURF_REFLECTIVE)
     reflect(r, nx, ny, nz);
   else

@@ -175,7 +175,7 @@ __device__ inline double newton_distance(const KArgs& a, const ort_surface& s, i
     for (; j < max_iter; ++j) {
       bool rerr = false;
       double nx, ny, nz;
-      const double f = ort::newton_eval<(FEAT & F_KM)>(s, cst(a.coef), cst(a.zern), kNoSeed, r,
+      const double f = ort::newton_eval<(FEAT & F_KM)>(s, s.radius, s.conic, cst(a.coef), cst(a.zern), kNoSeed, r,
                                                       t, true, rerr, nx, ny, nz);
       if (active && rerr) range_bits |= range_bit(s);
       const bool conv = !active || !(fabs(f) >= tol);
@@ -197,7 +197,7 @@ __device__ inline double newton_distance(const KArgs& a, const ort_surface& s, i
       bool rerr = false;
       double nx, ny, nz;
       const bool upd = j < U;  // sag + normal at P(t) for an update, the sag alone after
-      const double f = ort::newton_eval<(FEAT & F_KM)>(s, cst(a.coef), cst(a.zern), kNoSeed, r,
+      const double f = ort::newton_eval<(FEAT & F_KM)>(s, s.radius, s.conic, cst(a.coef), cst(a.zern), kNoSeed, r,
                                                       t, upd, rerr, nx, ny, nz);
       // the reference evaluates sag at j = 0..U-1 always, and at j = U only when the
       // loop broke there (U < max_iter)
@@ -283,7 +283,7 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(const KArgs a) {
     }
     const double n_pre = o.n_pre, u = o.u, alpha = o.alpha_pre;
     if constexpr ((FEAT & F_KM) != 0) {
-      ort::finish_surface<(FEAT & F_KM)>(r, s, cst(a.coef), cst(a.zern), kNoSeed, t, n_pre, u,
+      ort::finish_surface<(FEAT & F_KM)>(r, s, s.radius, s.conic, cst(a.coef), cst(a.zern), kNoSeed, t, n_pre, u,
                                          alpha);
     } else {
       // closed-form geometries only: plane / conic normal inline
@@ -418,22 +418,26 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
 }
 
 // ---------------------------------------------------------------------------------
-// Vector-Jacobian product w.r.t. Zernike coefficients (the autograd backward of
-// ort_trace_pupil; reference: torch autograd through the unrolled trace,
-// backend/torch_backend.py + optimization/optimizer/torch/base.py:95-154).
+// Vector-Jacobian product of ort_trace_pupil w.r.t. lens parameters (the autograd
+// backward; reference: torch autograd through the unrolled trace,
+// backend/torch_backend.py + optimization/optimizer/torch/base.py:95-154): Zernike
+// coefficients, surface radius and conic, surface vertex z (thickness variables) and
+// the image-space propagation distance.
 //
-// Forward mode: the ray state carries P tangents (ort::Dual<P>), one per coefficient of
-// this launch's parameter chunk, through exactly the Newton update counts of the primal
-// trace (opt.sched), so the derivative is that of the unrolled iteration the reference
-// differentiates. Each lane contracts its tangents with the ray cotangents; the wave
-// sums them with DPP/shuffles and one lane per wave adds P partial sums to grad.
+// Forward mode: the ray state carries P tangents (ort::Dual<P>), one per parameter of
+// this launch's chunk, through exactly the Newton update counts of the primal trace
+// (opt.sched), so the derivative is that of the unrolled iteration the reference
+// differentiates. Each lane contracts its tangents with the ray cotangents; wave
+// shuffles, then LDS, then one atomic per block and parameter.
 // ---------------------------------------------------------------------------------
 struct JArgs {
-  const int32_t* zparam;  // [n_zern_terms] parameter index per term, < 0: constant
+  const int32_t* zparam;   // [n_zern_terms] parameter index per term, < 0: constant
+  const double* tan_surf;  // [n_param][n_surf][3]: d radius, d conic, d vertex z
+  const double* tan_final; // [n_param]: d final_thickness
   int32_t n_param;
-  int32_t p0;             // first parameter of this launch
-  ort_rays cot;           // cotangents of the outputs (NULL field: zero)
-  double* grad;           // [n_param], accumulated with atomics
+  int32_t p0;              // first parameter of this launch
+  ort_rays cot;            // cotangents of the outputs (NULL field: zero)
+  double* grad;            // [n_param], accumulated with atomics
 };
 
 __device__ inline double wave_sum(double v) {
@@ -450,6 +454,21 @@ __device__ inline void cot_acc(double (&acc)[P], const double* g, int64_t rid,
   for (int k = 0; k < P; ++k) acc[k] += c * v.d[k];
 }
 
+// v with the tangents of this chunk's parameters: tan[p * stride + off] (uniform loads)
+template <int P>
+__device__ inline ort::Dual<P> seeded(double v, const double* tan, int64_t stride, int off,
+                                      const JArgs& j) {
+  ort::Dual<P> r(v);
+  if (tan) {
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+      const int p = j.p0 + k;
+      r.d[k] = p < j.n_param ? cst(tan)[(int64_t)p * stride + off] : 0.0;
+    }
+  }
+  return r;
+}
+
 template <int P, uint32_t KM>
 __global__ __launch_bounds__(kBlock) void vjp_kernel(const KArgs a, const JArgs j) {
   using D = ort::Dual<P>;
@@ -463,33 +482,47 @@ __global__ __launch_bounds__(kBlock) void vjp_kernel(const KArgs a, const JArgs 
   ort::RayT<D> r = ort::promote<D>(ort::generate_ray(sg, a.px[p], a.py[p]));
   const int64_t group = r_ld / a.group_len;
   const ort::ZSeed zs{j.zparam, j.p0};
+  const int64_t ts = (int64_t)a.n_surf * 3;
 
   for (int si = a.start_surface; si < a.n_surf; ++si) {
     const ort_surface s = cst(a.surf)[si];
     const ort_surface_optics o = optics_at(a, lam, si);
-    localize(a, s, r);
+    const D R = seeded<P>(s.radius, j.tan_surf, ts, si * 3 + 0, j);
+    const D K = seeded<P>(s.conic, j.tan_surf, ts, si * 3 + 1, j);
+    const D CZ = seeded<P>(s.cs_t[2], j.tan_surf, ts, si * 3 + 2, j);
+    // localize (coordinate_system.py:73-107) with the vertex z as a parameter
+    r.x = r.x + -s.cs_t[0];
+    r.y = r.y + -s.cs_t[1];
+    r.z = r.z + -CZ;
+    for (int c = 0; c < s.n_cs_loc; ++c) ort::apply_cs_op(r, cst(a.cs)[s.cs_loc_off + c]);
     D t;
     if (s.geometry == ORT_GEOM_PLANE) {
       t = ort::distance_plane(r);
     } else {
-      t = ort::distance_conic(r, s.radius, s.conic, (s.flags & ORT_SURF_RADIUS_INF) != 0);
+      t = ort::distance_conic(r, R, K, (s.flags & ORT_SURF_RADIUS_INF) != 0);
       if (s.geometry != ORT_GEOM_STANDARD) {
-        // replay the primal's update count (newton_raphson.py:137-166)
-        const int U = a.sched ? a.sched[group * a.n_surf + si] : s.max_iter;
-        bool rerr = false;
-        for (int it = 0; it < U; ++it) {
-          D nx, ny, nz;
-          const D f = ort::newton_eval<KM>(s, cst(a.coef), cst(a.zern), zs, r, t, true, rerr,
-                                           nx, ny, nz);
-          t = ort::newton_step(r, t, f, nx, ny, nz);
+        if constexpr (KM != 0) {
+          // replay the primal's update count (newton_raphson.py:137-166)
+          const int U = a.sched ? a.sched[group * a.n_surf + si] : s.max_iter;
+          bool rerr = false;
+          for (int it = 0; it < U; ++it) {
+            D nx, ny, nz;
+            const D f = ort::newton_eval<KM>(s, R, K, cst(a.coef), cst(a.zern), zs, r, t,
+                                             true, rerr, nx, ny, nz);
+            t = ort::newton_step(r, t, f, nx, ny, nz);
+          }
         }
       }
     }
-    ort::finish_surface<KM>(r, s, cst(a.coef), cst(a.zern), zs, t, o.n_pre, o.u, o.alpha_pre);
-    globalize(a, s, r);
+    ort::finish_surface<KM>(r, s, R, K, cst(a.coef), cst(a.zern), zs, t, o.n_pre, o.u,
+                            o.alpha_pre);
+    for (int c = 0; c < s.n_cs_glob; ++c) ort::apply_cs_op(r, cst(a.cs)[s.cs_glob_off + c]);
+    r.x = r.x + s.cs_t[0];
+    r.y = r.y + s.cs_t[1];
+    r.z = r.z + CZ;
   }
   if (a.final_mat >= 0)
-    ort::propagate(r, D(a.final_thickness),
+    ort::propagate(r, seeded<P>(a.final_thickness, j.tan_final, 1, 0, j),
                    tab(a.alpha_tab, a.n_lambda, a.n_mat, lam, a.final_mat));
 
   double acc[P];
@@ -557,7 +590,7 @@ __global__ __launch_bounds__(kBlock) void geom_kernel(const KArgs a, const GArgs
       ort::normal_conic(x, y, s.radius, s.conic, nx, ny, nz);
     } else {
       if constexpr (KM != 0) {
-        z = ort::newton_sagnorm<KM>(s, cst(a.coef), cst(a.zern), kNoSeed, x, y, true,
+        z = ort::newton_sagnorm<KM>(s, s.radius, s.conic, cst(a.coef), cst(a.zern), kNoSeed, x, y, true,
                                     range_error, nx, ny, nz);
       } else {
         z = nx = ny = nz = __builtin_nan("");

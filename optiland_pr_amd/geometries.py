@@ -17,6 +17,14 @@ from . import _abi
 from .coordinate_system import CoordinateSystem
 
 
+def scalar(v):
+    """A plain float from a Python / NumPy number or a (possibly grad-requiring) torch
+    scalar tensor -- geometry parameters may be autograd leaves (autodiff.py)."""
+    if hasattr(v, "detach"):
+        v = v.detach().cpu()
+    return float(np.ravel(np.asarray(v, dtype=np.float64))[0])
+
+
 class BaseGeometry:
     """geometries/base.py:14-110."""
 
@@ -90,7 +98,7 @@ class StandardGeometry(BaseGeometry):
         self.radius = -self.radius
 
     def lower_params(self):
-        return self.radius, self.k, 0.0, 0, 1.0, []
+        return scalar(self.radius), scalar(self.k), 0.0, 0, 1.0, []
 
 
 class NewtonRaphsonGeometry(StandardGeometry):
@@ -114,7 +122,7 @@ class EvenAsphere(NewtonRaphsonGeometry):
         self.is_symmetric = True
 
     def lower_params(self):
-        return (self.radius, self.k, self.tol, self.max_iter, 1.0,
+        return (scalar(self.radius), scalar(self.k), self.tol, self.max_iter, 1.0,
                 [float(c) for c in self.coefficients])
 
 
@@ -233,7 +241,8 @@ class ZernikePolynomialGeometry(NewtonRaphsonGeometry):
         self.is_symmetric = False
 
     def lower_params(self):
-        return self.radius, self.k, self.tol, self.max_iter, self.norm_radius, []
+        return (scalar(self.radius), scalar(self.k), self.tol, self.max_iter,
+                self.norm_radius, [])
 
     def zernike_terms(self):
         """-> list of (c, norm, n, m, a_k list, d_k list) in coefficient order."""
@@ -266,7 +275,7 @@ class PolynomialGeometry(NewtonRaphsonGeometry):
     def lower_params(self):
         c = np.atleast_2d(np.asarray(self.coefficients, dtype=np.float64))
         block = [float(c.shape[0]), float(c.shape[1])] + [float(v) for v in c.ravel()]
-        return self.radius, self.k, self.tol, self.max_iter, 1.0, block
+        return scalar(self.radius), scalar(self.k), self.tol, self.max_iter, 1.0, block
 
 
 class ChebyshevPolynomialGeometry(NewtonRaphsonGeometry):
@@ -289,7 +298,7 @@ class ChebyshevPolynomialGeometry(NewtonRaphsonGeometry):
             c = np.zeros((1, 0))
         block = [float(c.shape[0]), float(c.shape[1]), float(self.norm_x),
                  float(self.norm_y)] + [float(v) for v in c.ravel()]
-        return self.radius, self.k, self.tol, self.max_iter, 1.0, block
+        return scalar(self.radius), scalar(self.k), self.tol, self.max_iter, 1.0, block
 
 
 class BiconicGeometry(NewtonRaphsonGeometry):
@@ -313,7 +322,7 @@ class BiconicGeometry(NewtonRaphsonGeometry):
 
     def lower_params(self):
         block = [self._curv(self.Rx), self._curv(self.Ry), self.kx, self.ky]
-        return self.radius, self.k, self.tol, self.max_iter, 1.0, block
+        return scalar(self.radius), scalar(self.k), self.tol, self.max_iter, 1.0, block
 
 
 class ToroidalGeometry(NewtonRaphsonGeometry):
@@ -336,4 +345,4 @@ class ToroidalGeometry(NewtonRaphsonGeometry):
         c_yz = 1.0 / self.R_yz if has_yz else 0.0
         block = [self.R_rot, c_yz, self.k_yz, 1.0 if has_yz else 0.0,
                  float(len(self.coeffs_poly_y))] + self.coeffs_poly_y
-        return self.radius, self.k, self.tol, self.max_iter, 1.0, block
+        return scalar(self.radius), scalar(self.k), self.tol, self.max_iter, 1.0, block

@@ -23,7 +23,7 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from . import _abi
-from .geometries import NewtonRaphsonGeometry, ZernikePolynomialGeometry
+from .geometries import NewtonRaphsonGeometry, ZernikePolynomialGeometry, scalar
 from .surfaces import ObjectSurface
 
 
@@ -203,7 +203,7 @@ def lower_surface_group(surface_group, wavelengths, record=False, skip_object=Tr
         alpha_tab=alpha_tab,
         wavelengths=wavelengths,
         final_mat=final_mat,
-        final_thickness=float(final.thickness),
+        final_thickness=scalar(final.thickness),
         materials=mats,
         n_rec=len(rec_set),
         rec_surfaces=rec_set,

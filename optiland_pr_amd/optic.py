@@ -57,6 +57,29 @@ class Optic:
             raise ValueError(f"field type {field_type!r} is not supported by the trace core")
         self.field_type = field_type
 
+    # -- parameter setters (optic_updater.py:37-86: what the optimisation variables call;
+    #    torch tensors are kept as given so they can be autograd leaves, autodiff.py) ----
+    def set_radius(self, value, surface_number):
+        self.surface_group.surfaces[surface_number].geometry.radius = value
+
+    def set_conic(self, value, surface_number):
+        self.surface_group.surfaces[surface_number].geometry.k = value
+
+    def set_thickness(self, value, surface_number):
+        """optic_updater.py:67-85: move every later vertex by the change, keep surface 1
+        at z = 0, store the thickness."""
+        from .geometries import scalar
+
+        surfs = self.surface_group.surfaces
+        pos = [float(s.geometry.cs.z) for s in surfs]
+        delta = scalar(value) - pos[surface_number + 1] + pos[surface_number]
+        pos = [p + delta if k > surface_number else p for k, p in enumerate(pos)]
+        z1 = pos[1]
+        for k, s in enumerate(surfs):
+            s.geometry.cs.z = pos[k] - z1
+        if surface_number < len(surfs):
+            surfs[surface_number].thickness = value
+
     def invalidate(self):
         """Drop cached device tables after editing surfaces in place."""
         self._lowered = None

@@ -25,6 +25,7 @@ from .geometries import (
     StandardGeometry,
     ToroidalGeometry,
     ZernikePolynomialGeometry,
+    scalar,
 )
 from .materials import BaseMaterial, IdealMaterial, configure_material
 
@@ -181,7 +182,7 @@ class SurfaceGroup:
 
     @property
     def radii(self):
-        return np.array([s.geometry.radius for s in self.surfaces], dtype=np.float64)
+        return np.array([scalar(s.geometry.radius) for s in self.surfaces], dtype=np.float64)
 
     @property
     def stop_index(self):
@@ -276,7 +277,7 @@ class SurfaceGroup:
                 z = 0.0
             else:
                 prev = self.surfaces[i - 1]
-                z = prev.geometry.cs.z + prev.thickness
+                z = prev.geometry.cs.z + scalar(prev.thickness)
             self.surfaces[i].geometry.cs.z = z
 
     def _create(self, surface_type, comment, index, is_stop, material, kw):
@@ -300,7 +301,7 @@ class SurfaceGroup:
                 z = 0
             else:
                 prev = self.surfaces[index - 1]
-                z = prev.geometry.cs.z + prev.thickness
+                z = prev.geometry.cs.z + scalar(prev.thickness)
         cs = CoordinateSystem(x=x, y=y, z=z, rx=kw.get("rx", 0), ry=kw.get("ry", 0),
                               rz=kw.get("rz", 0))
         # material_factory.py:22-62

@@ -90,6 +90,48 @@ def main():
     np.savez_compressed(os.path.join(HERE, "autograd_tma.npz"), **out)
     print("rms", out["rms_value"], "wsum", out["wsum_value"])
     print(out["rms_grad"])
+    shape_params()
+
+
+def _cooke_leaves(thickness_surface):
+    """Cooke triplet with radius (surfaces 1, 3, 6), conic (5) and one thickness variable
+    as torch leaves, written the way the reference's variables write them
+    (optic_updater.py:37-86). Only one thickness variable: every set_thickness rebuilds
+    the positions from detached values (surface_group.py:143-148), so in the reference
+    only the last one written keeps its graph."""
+    from optiland.samples.objectives import CookeTriplet
+
+    lens = CookeTriplet()
+    leaves = {}
+    for si in (1, 3, 6):
+        t = torch.tensor(float(lens.surface_group.surfaces[si].geometry.radius),
+                         dtype=torch.float64, requires_grad=True)
+        lens.set_radius(t, si)
+        leaves[f"radius{si}"] = t
+    t = torch.tensor(0.0, dtype=torch.float64, requires_grad=True)
+    lens.set_conic(t, 5)
+    leaves["conic5"] = t
+    th = float(lens.surface_group.surfaces[thickness_surface].thickness)
+    t = torch.tensor(th, dtype=torch.float64, requires_grad=True)
+    lens.set_thickness(t, thickness_surface)
+    leaves[f"thickness{thickness_surface}"] = t
+    return lens, leaves
+
+
+def shape_params():
+    """d rms / d (radius, conic, thickness) for the Cooke triplet at field (0, 1),
+    uniform 24, lambda 0.55 (autograd_cooke.npz), with the thickness variable after
+    surface 2 (moves surfaces 3-7) or after surface 6 (moves the image plane)."""
+    out = {}
+    for th in (2, 6):
+        lens, leaves = _cooke_leaves(th)
+        rms = RayOperand.rms_spot_size(lens, -1, 0.0, 1.0, 24, 0.55, "uniform")
+        rms.backward()
+        out[f"t{th}_value"] = np.array(float(rms))
+        out[f"t{th}_names"] = np.array(list(leaves))
+        out[f"t{th}_grad"] = np.array([float(v.grad) for v in leaves.values()])
+        print(th, float(rms), dict(zip(leaves, out[f"t{th}_grad"])))
+    np.savez_compressed(os.path.join(HERE, "autograd_cooke.npz"), **out)
 
 
 if __name__ == "__main__":

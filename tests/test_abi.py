@@ -24,6 +24,7 @@ STRUCTS = {
     "ort_rays": (None, _native.ort_rays),
     "ort_batch": (None, _native.ort_batch),
     "ort_options": (None, _native.ort_options),
+    "ort_vjp_params": (None, _native.ort_vjp_params),
 }
 
 

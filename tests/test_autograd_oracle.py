@@ -106,3 +106,51 @@ def test_parameter_map():
     np.testing.assert_array_equal(zp[20:], np.arange(10, 20))
     with pytest.raises(ValueError):
         parameter_map(table, [(1, _C(9))])
+
+
+def _cooke_rms(radius, conic5, thick, thick_surface, g=None):
+    """Oracle rms spot of the Cooke triplet at (0, 1), uniform 24, lambda 0.55 with the
+    given radii of surfaces 1, 3, 6, conic of surface 5 and thickness after
+    `thick_surface`; the rays are generated from the UNPERTURBED lens (the reference
+    builds ray-generation inputs from detached copies, surface_group.py:143-153)."""
+    from optiland_pr_amd.distribution import create_distribution
+    from optiland_pr_amd.samples import CookeTriplet
+
+    base = CookeTriplet()
+    seg = segment_params(base, 0.0, 1.0, 0)
+    lens = CookeTriplet()
+    for si, r in zip((1, 3, 6), radius, strict=True):
+        lens.set_radius(r, si)
+    lens.set_conic(conic5, 5)
+    lens.set_thickness(thick, thick_surface)
+    table = lower_surface_group(lens.surface_group, [0.55])
+    d = create_distribution("uniform")
+    d.generate_points(24)
+    r = trace_np.trace_segment(table, trace_np.generate_rays(seg, d.x, d.y), 0).rays
+    return np.sqrt(np.mean((r.x - np.mean(r.x)) ** 2 + (r.y - np.mean(r.y)) ** 2))
+
+
+@pytest.mark.parametrize("th", [2, 6])
+def test_oracle_fd_matches_reference_shape_gradients(th):
+    """Radius / conic / thickness gradients of the reference (autograd_cooke.npz) against
+    central differences of the oracle with fixed ray generation."""
+    from optiland_pr_amd.samples import CookeTriplet
+
+    g = load_golden("autograd_cooke")
+    base = CookeTriplet()
+    R0 = [base.surface_group.surfaces[si].geometry.radius for si in (1, 3, 6)]
+    t0 = base.surface_group.surfaces[th].thickness
+    x0 = np.array(R0 + [0.0, t0])
+
+    def f(x):
+        return _cooke_rms(list(x[:3]), x[3], x[4], th)
+
+    assert f(x0) == pytest.approx(float(g[f"t{th}_value"]), rel=1e-12)
+    fd = np.zeros(5)
+    for i in range(5):
+        h = 1e-6 * max(1.0, abs(x0[i]))
+        xp, xm = x0.copy(), x0.copy()
+        xp[i] += h
+        xm[i] -= h
+        fd[i] = (f(xp) - f(xm)) / (2 * h)
+    np.testing.assert_allclose(fd, g[f"t{th}_grad"], rtol=1e-5, atol=1e-9)

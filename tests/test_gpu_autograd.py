@@ -179,3 +179,58 @@ def test_vjp_linear_in_cotangent(torch):
         np.testing.assert_allclose((u + v).numpy(), w.numpy(), rtol=1e-10,
                                    atol=1e-12 * float(w.abs().max()))
     assert autodiff.wants_grad(lens)
+
+
+@pytest.mark.parametrize("th", [2, 6])
+def test_shape_parameter_gradients_match_reference(torch, th):
+    """d rms / d (radius 1, 3, 6; conic 5; thickness after surface `th`) of the Cooke
+    triplet vs the reference's torch autograd (autograd_cooke.npz; pinned against the
+    oracle by finite differences in test_autograd_oracle.py)."""
+    from optiland_pr_amd.operands import RayOperand
+    from optiland_pr_amd.samples import CookeTriplet
+    from tests.conftest import load_golden
+
+    g = load_golden("autograd_cooke")
+    lens = CookeTriplet()
+    leaves = []
+    for si in (1, 3, 6):
+        t = torch.tensor(float(lens.surface_group.surfaces[si].geometry.radius),
+                         dtype=torch.float64, requires_grad=True)
+        lens.set_radius(t, si)
+        leaves.append(t)
+    t = torch.tensor(0.0, dtype=torch.float64, requires_grad=True)
+    lens.set_conic(t, 5)
+    leaves.append(t)
+    t = torch.tensor(float(lens.surface_group.surfaces[th].thickness), dtype=torch.float64,
+                     requires_grad=True)
+    lens.set_thickness(t, th)
+    leaves.append(t)
+    loss = RayOperand.rms_spot_size(lens, -1, 0.0, 1.0, 24, 0.55, "uniform")
+    np.testing.assert_allclose(float(loss), float(g[f"t{th}_value"]), rtol=1e-13)
+    loss.backward()
+    got = np.array([float(v.grad) for v in leaves])
+    np.testing.assert_allclose(got, g[f"t{th}_grad"], rtol=1e-9, atol=1e-12)
+
+
+def test_gradcheck_radius_conic_zernike_mixed(torch):
+    """gradcheck over a mixed parameter set on the TMA: a mirror radius, a conic and
+    non-zero Zernike coefficients (all entering the Newton iteration)."""
+    base = np.array([2e-5, -1e-5, 3e-5, 1e-4, 2e-4, -1e-4, 5e-5, 1e-5, -2e-5, 3e-5])
+    lens, _ = _tma_with_leaves(torch, [base, base, base])
+    g1 = lens.surface_group.surfaces[1].geometry
+    g2 = lens.surface_group.surfaces[2].geometry
+    for g in (lens.surface_group.surfaces[si].geometry for si in (1, 2, 3)):
+        g.coefficients = g.coefficients.detach()
+    R = torch.tensor(-100.0, dtype=torch.float64, requires_grad=True)
+    k = torch.tensor(0.05, dtype=torch.float64, requires_grad=True)
+    c = torch.tensor(base, dtype=torch.float64, requires_grad=True)
+
+    def f(R_, k_, c_):
+        g1.radius = R_
+        g2.k = k_
+        lens.surface_group.surfaces[3].geometry.coefficients = c_
+        r = lens.trace(0.0, 1.0, 0.587, num_rays=3, distribution="hexapolar")
+        return r.x, r.y, r.L
+
+    assert torch.autograd.gradcheck(f, (R, k, c), eps=1e-7, atol=1e-6, rtol=1e-4,
+                                    nondet_tol=1e-12)
