@@ -101,9 +101,6 @@ def config2(args, dev, rank, world, torch):
     def step():
         trace_pupil(dl, seg_dev, px, py, out, R, R, R)
 
-    def cpu():
-        return _cpu_trace(lens, dl, seg, args.cpu_rays, 1)
-
     flops = _flops_per_ray(dl.table)
     return Workload(
         metric="ray-surface intersections/sec at 1M pupil rays, 10-surf double-Gauss",
@@ -115,7 +112,7 @@ def config2(args, dev, rank, world, torch):
             "parallelism": f"dp{world} (ray shards, no collective)"},
         kernel="trace_closed_kernel<F_GEN> (ort_trace_pupil)", launches=1,
         bytes_per_launch=R * (16 + 64), flops_per_ray=flops, pmc_file="hbm_traffic.json",
-        cpu=cpu, rays=R)
+        rays=R)
 
 
 def config3(args, dev, rank, world, torch):
@@ -141,9 +138,6 @@ def config3(args, dev, rank, world, torch):
     def step():
         trace_pupil(dl, seg_dev, px, py, out, n, n_p, n_p, keys=keys)
 
-    def cpu():
-        return _cpu_trace(lens, dl, seg, max(1, args.cpu_rays // 10), len(seg))
-
     return Workload(
         metric="ray-surface intersections/sec, RT-asph even-asphere (Newton sag), 5 fields x "
                "3 lambda x 4M pupil rays",
@@ -154,7 +148,7 @@ def config3(args, dev, rank, world, torch):
                 "parallelism": f"dp{world} (ray shards, no collective)"},
         kernel="trace_kernel<F_GEN|KM_EVEN> (ort_trace_pupil)", launches=1,
         bytes_per_launch=n_p * 16 + n * 64, flops_per_ray=None, pmc_file="hbm_traffic_c3.json",
-        cpu=cpu, rays=n)
+        rays=n)
 
 
 def config4(args, dev, rank, world, torch):
@@ -193,9 +187,6 @@ def config4(args, dev, rank, world, torch):
         if world > 1:
             distributed.gather_image_plane(out.x, out.y, n_loc, len(pairs), n_p)
 
-    def cpu():
-        return _cpu_trace(lens, dl, seg, max(1, args.cpu_rays // 10), len(seg))
-
     return Workload(
         metric="ray-surface intersections/sec, ReverseTelephoto 7 fields x 7 lambda x 2M rays, "
                "sharded + RCCL gather of image-plane hits",
@@ -206,7 +197,7 @@ def config4(args, dev, rank, world, torch):
                 "parallelism": f"dp{world} (pupil shards of every pair) + all_gather"},
         kernel="trace_closed_kernel<F_GEN> (ort_trace_pupil)", launches=1,
         bytes_per_launch=n * (16 + 64), flops_per_ray=None, pmc_file="hbm_traffic_c4.json",
-        cpu=cpu, rays=n)
+        rays=n)
 
 
 def config5(args, dev, rank, world, torch):
@@ -233,21 +224,6 @@ def config5(args, dev, rank, world, torch):
         opt.step()
         state["loss"] = float(loss.detach())
 
-    def cpu():
-        from optiland_pr_amd.lowering import lower_surface_group, segment_params
-
-        table = lower_surface_group(lens.surface_group, [0.587])
-        seg = np.stack([segment_params(lens, 0.0, 1.0, 0)])
-
-        class _DL:
-            pass
-
-        dl = _DL()
-        dl.table = table
-        res = _cpu_trace(lens, dl, seg, max(1, args.cpu_rays // 10), 1)
-        res["sample"] += " (forward trace only: the oracle has no derivative path)"
-        return res
-
     return Workload(
         metric="TMA Zernike optimisation steps: ray-surface intersections/sec of forward + "
                "backward (d rms_spot / d coeff) at 1M rays",
@@ -258,7 +234,7 @@ def config5(args, dev, rank, world, torch):
                 "rays_per_gpu": R, "surfaces": S, "parameters": 30,
                 "parallelism": f"dp{world} (independent replicas)"},
         kernel="vjp_kernel<4, KM_ZERN> (ort_trace_pupil_vjp)", launches=None,
-        bytes_per_launch=None, flops_per_ray=None, pmc_file=None, cpu=cpu, rays=R, state=state)
+        bytes_per_launch=None, flops_per_ray=None, pmc_file=None, rays=R, state=state)
 
 
 CONFIGS = {2: config2, 3: config3, 4: config4, 5: config5}
@@ -273,14 +249,22 @@ def main():
     ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-rays", type=int, default=1_000_000)
+    ap.add_argument("--cpu-seconds", type=float, default=1.5,
+                    help="wall time of the multi-process CPU baseline leg")
     args = ap.parse_args()
-
-    import torch
-    import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # the CPU baseline runs first, before anything touches the GPU (its worker processes
+    # are forked from this one)
+    cpu_line = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu_line = _cpu_baseline(args)
+
+    import torch
+    import torch.distributed as dist
+
     if world > 1:
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
@@ -342,7 +326,7 @@ def main():
             line["roofline_fp64"] = _roofline_fp64(w, kern_ms)
         if getattr(w, "state", None):
             line["config"]["final_loss"] = w.state.get("loss")
-        line["cpu_baseline"] = None if args.no_cpu or world > 1 else w.cpu()
+        line["cpu_baseline"] = cpu_line
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
@@ -407,33 +391,98 @@ def _pmc_summary(name):
         return {}
 
 
-def _cpu_trace(lens, dl, seg, n_rays, n_pairs):
-    """The oracle (NumPy restatement of the reference, oracle/trace_np.py) timed on this
-    host on a bounded sample of the same workload: n_rays pupil rays per pair for up to
-    3 of the workload's pairs, one process; reported per intersection."""
+def _cpu_workload(args):
+    """(lens table, segments, rays per pair, pairs used, label) of the bench config, host
+    only: the same lowered table and ray-generation scalars the GPU gets."""
+    from optiland_pr_amd.lowering import lower_surface_group, segment_params
+    from optiland_pr_amd import samples
+
+    if args.config == 2:
+        lens = samples.DoubleGauss()
+        table = lower_surface_group(lens.surface_group, [0.5876])
+        segs = np.stack([segment_params(lens, 0.0, 1.0, 0)])
+        return table, segs, args.cpu_rays, "DoubleGauss"
+    if args.config == 3:
+        lens = samples.ReverseTelephotoAsphere()
+        wls = [0.4861, 0.5876, 0.6563]
+        table = lower_surface_group(lens.surface_group, wls)
+        segs = np.stack([segment_params(lens, 0.0, float(h), wi)
+                         for h in np.linspace(0, 1, 5) for wi in range(3)])[:3]
+        return table, segs, max(1, args.cpu_rays // 10), "RT-asph"
+    if args.config == 4:
+        lens = samples.ReverseTelephoto()
+        wls = [float(w) for w in np.linspace(0.4861, 0.6563, 7)]
+        table = lower_surface_group(lens.surface_group, wls)
+        segs = np.stack([segment_params(lens, 0.0, float(h), wi)
+                         for h in np.linspace(0, 1, 7) for wi in range(7)])[:3]
+        return table, segs, max(1, args.cpu_rays // 10), "ReverseTelephoto"
+    lens = samples.ThreeMirrorAnastigmat()
+    table = lower_surface_group(lens.surface_group, [0.587])
+    segs = np.stack([segment_params(lens, 0.0, 1.0, 0)])
+    return table, segs, max(1, args.cpu_rays // 10), "TMA (forward trace only: the oracle " \
+        "has no derivative path)"
+
+
+_CPU = {}
+
+
+def _cpu_task(k_lo_hi):
+    """One worker's share: generate + trace rays [lo, hi) of pair k with the oracle."""
     from oracle import trace_np
+
+    k, lo, hi = k_lo_hi
+    table, segs, px, py = _CPU["w"]
+    r = trace_np.generate_rays(segs[k], px[lo:hi], py[lo:hi])
+    trace_np.trace_segment(table, r, int(segs[k]["lambda_idx"]))
+    return hi - lo
+
+
+def _cpu_baseline(args):
+    """The oracle (NumPy restatement of the reference, oracle/trace_np.py) on this host's
+    cores: a bounded sample of the bench workload (up to 3 (field, lambda) pairs) split
+    into contiguous ray chunks over a pool of min(16, cpu_count) forked worker processes
+    (each chunk is its own trace call: for Newton lenses the global stop rule then spans
+    a chunk), repeated for ~--cpu-seconds of wall time (pool start-up excluded); the
+    single-process rate of one repetition is reported alongside."""
+    import multiprocessing as mp
+
     from optiland_pr_amd.distribution import RandomDistribution
 
+    table, segs, n_rays, label = _cpu_workload(args)
     d = RandomDistribution(seed=0)
     d.generate_points(n_rays)
     px, py = np.asarray(d.x), np.asarray(d.y)
-    use = list(range(min(n_pairs, 3)))
-    times = []
-    for _ in range(2):
+    _CPU["w"] = (table, segs, px, py)
+    S = table.n_surfaces
+    units = n_rays * len(segs) * S
+    t0 = time.perf_counter()
+    for k in range(len(segs)):
+        _cpu_task((k, 0, n_rays))
+    t_single = time.perf_counter() - t0
+    workers = max(1, min(16, os.cpu_count() or 1))
+    chunk = -(-n_rays // workers)
+    tasks = [(k, lo, min(n_rays, lo + chunk)) for k in range(len(segs))
+             for lo in range(0, n_rays, chunk)]
+    with mp.get_context("fork").Pool(workers) as pool:
+        pool.map(_cpu_task, [(0, 0, min(n_rays, 64))] * workers)  # warm the workers
+        # repeat the sample until ~args.cpu_seconds of wall time (x workers of CPU work)
+        reps = 0
         t0 = time.perf_counter()
-        for k in use:
-            r = trace_np.generate_rays(seg[k], px, py)
-            trace_np.trace_segment(dl.table, r, int(seg[k]["lambda_idx"]))
-        times.append(time.perf_counter() - t0)
-    t = min(times)
-    S = dl.table.n_surfaces
+        while True:
+            pool.map(_cpu_task, tasks, chunksize=1)
+            reps += 1
+            t = time.perf_counter() - t0
+            if t >= args.cpu_seconds and reps >= 2:
+                break
     return {
-        "value": n_rays * len(use) * S / t,
+        "value": units * reps / t,
         "unit": "intersections/s",
-        "cores": 1,
+        "cores": workers,
         "kind": "port",
-        "sample": f"{n_rays} rays x {len(use)} (field, lambda) pair(s) x {S} surfaces "
-                  f"(generation + trace), NumPy oracle, 1 process, best of 2: {t:.2f} s on "
+        "single_process_value": units / t_single,
+        "sample": f"{label}: {n_rays} rays x {len(segs)} (field, lambda) pair(s) x {S} "
+                  f"surfaces (generation + trace), NumPy oracle, {workers} processes x {reps} "
+                  f"repetitions: {t:.2f} s wall (1 process, 1 repetition: {t_single:.2f} s) on "
                   f"{platform.processor() or platform.machine()}",
     }
 
