@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define ORT_ABI_VERSION 4
+#define ORT_ABI_VERSION 5
 #define ORT_MAX_SURFACES 64
 
 /* ---- geometry kinds ----------------------------------- */
@@ -253,22 +253,40 @@ int ort_trace_pupil(const ort_lens* lens, const double* px, const double* py,
  * through any of: the coefficient of Zernike term j of lens->zern (zern_param[j] == p),
  * the radius / conic / vertex z of traced surface s (surf_tangent[(p*S + s)*3 + 0/1/2]
  * = d value / d p; a thickness variable moves the vertices after it), the image-space
- * propagation distance (final_tangent[p]). NULL tables contribute nothing. */
+ * propagation distance (final_tangent[p]). NULL tables contribute nothing.
+ *
+ * mode ORT_VJP_UNROLLED: forward-mode tangents through the primal's exact Newton
+ *   update counts (the derivative of the unrolled iteration, as torch autograd computes
+ *   it); one re-trace per 4 parameters, no workspace.
+ * mode ORT_VJP_ADJOINT: one reverse-mode pass whatever n_param (the intersection
+ *   distance differentiated through its implicit equation; equals the unrolled
+ *   derivative to the Newton residual when the Newton slope is the sag's derivative --
+ *   not for standard / noll Zernike normals, which omit the normalisation constant).
+ *   Needs n_zern and a device workspace of ort_vjp_workspace_size() bytes. */
+enum ort_vjp_mode { ORT_VJP_UNROLLED = 0, ORT_VJP_ADJOINT = 1 };
 typedef struct ort_vjp_params {
   int32_t n_param;
-  int32_t reserved;
-  const int32_t* zern_param;   /* [n_zern_terms] parameter index per term, < 0: constant */
+  int32_t mode;                /* ort_vjp_mode                                          */
+  const int32_t* zern_param;   /* [n_zern] parameter index per term, < 0: constant      */
   const double* surf_tangent;  /* [n_param][n_surfaces][3]                              */
   const double* final_tangent; /* [n_param]                                             */
+  int32_t n_zern;              /* entries of zern_param (terms of lens->zern)           */
+  int32_t reserved;
+  void* workspace;             /* ADJOINT: device scratch (tape + wave partials)        */
+  int64_t workspace_size;      /* bytes available at workspace                          */
 } ort_vjp_params;
+
+/* Workspace bytes ORT_VJP_ADJOINT needs for this lens, batch and parameter set. */
+int64_t ort_vjp_workspace_size(const ort_lens* lens, const ort_batch* batch,
+                               const ort_vjp_params* params);
 
 /* Backward of ort_trace_pupil: the vector-Jacobian product
  *   grad[p] += sum_rays sum_f cotangent.f[ray] * d out.f[ray] / d param_p
  * for the output fields f of rays_out (x, y, z, L, M, N, i, opd; a NULL cotangent field
  * counts as zero). opt must be ORT_NEWTON_SCHEDULE with the schedule the verified primal
- * trace ran (the derivative is that of the unrolled Newton iteration, as torch autograd
- * computes it through newton_raphson.py:137-166). grad is accumulated with device
- * atomics: zero it first. Ray generation is not differentiated (the reference builds
+ * trace ran (see ort_vjp_mode for how Newton surfaces are differentiated). grad is
+ * accumulated (atomics for UNROLLED, a deterministic reduction for ADJOINT): zero it
+ * first. Ray generation is not differentiated (the reference builds
  * its paraxial quantities from detached copies, surface_group.py:143-153). Replaces
  * reverse-mode torch autograd through the trace (SurfaceGroup.trace under the torch
  * backend, driven by optimization/optimizer/torch/base.py:95-154; variables written by

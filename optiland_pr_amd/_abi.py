@@ -9,7 +9,9 @@ from __future__ import annotations
 
 import numpy as np
 
-ABI_VERSION = 4
+ABI_VERSION = 5
+VJP_UNROLLED = 0
+VJP_ADJOINT = 1
 MAX_SURFACES = 64
 
 # enum ort_geometry

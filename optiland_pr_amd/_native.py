@@ -50,10 +50,14 @@ class ort_batch(C.Structure):
 class ort_vjp_params(C.Structure):
     _fields_ = [
         ("n_param", C.c_int32),
-        ("reserved", C.c_int32),
+        ("mode", C.c_int32),
         ("zern_param", C.c_void_p),
         ("surf_tangent", C.c_void_p),
         ("final_tangent", C.c_void_p),
+        ("n_zern", C.c_int32),
+        ("reserved", C.c_int32),
+        ("workspace", C.c_void_p),
+        ("workspace_size", C.c_int64),
     ]
 
 
@@ -66,6 +70,7 @@ class ort_options(C.Structure):
 
 
 EXPORTS = ("ort_abi_version", "ort_trace_sequential", "ort_trace_pupil", "ort_trace_pupil_vjp",
+           "ort_vjp_workspace_size",
            "ort_surface_sag_normal", "ort_surface_distance", "ort_generate_rays")
 
 _lib = None
@@ -102,6 +107,8 @@ def load(path: str | None = None):
     lib.ort_trace_pupil_vjp.argtypes = [P(ort_lens), C.c_void_p, C.c_void_p, P(ort_batch),
                                         P(ort_options), P(ort_vjp_params), P(ort_rays),
                                         C.c_void_p, C.c_void_p]
+    lib.ort_vjp_workspace_size.restype = C.c_int64
+    lib.ort_vjp_workspace_size.argtypes = [P(ort_lens), P(ort_batch), P(ort_vjp_params)]
     lib.ort_surface_sag_normal.restype = C.c_int
     lib.ort_surface_sag_normal.argtypes = [P(ort_lens), C.c_int32, C.c_void_p, C.c_void_p,
                                            C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p,

@@ -8,11 +8,19 @@ including the unrolled Newton iterations (geometries/newton_raphson.py:137-166),
 TorchOptimizer.optimize (optimization/optimizer/torch/base.py:95-154) calls
 loss.backward() on an operand such as RayOperand.rms_spot_size (operand/ray.py:300-340).
 
-Here the forward is the fused HIP trace (ort_trace_pupil) and the backward is one
-forward-mode derivative launch per chunk of coefficients (ort_trace_pupil_vjp): the rays
-carry dual numbers through exactly the Newton update counts the primal ran, and the
-kernel contracts them with the incoming cotangents on the device. No torch graph is
-built over the per-ray arithmetic; torch only sees one autograd node per trace.
+Here the forward is the fused HIP trace (ort_trace_pupil) and the backward is
+ort_trace_pupil_vjp, in one of two modes (vjp_mode):
+  adjoint   one reverse-mode launch whatever the number of parameters: the primal
+            re-traced with a tape of per-surface states, then the adjoint of each
+            surface step from the image back (ort_adjoint.h); intersection distances are
+            differentiated through their implicit equation;
+  unrolled  one forward-mode launch per chunk of 4 parameters: dual numbers through
+            exactly the Newton update counts the primal ran (the derivative of the
+            unrolled iteration, bit-for-bit the reference's semantics); used for
+            standard / noll Zernike surfaces, whose Newton slope is not the sag's
+            derivative (see vjp_mode).
+No torch graph is built over the per-ray arithmetic; torch only sees one autograd node
+per trace.
 
 Parameters: Zernike coefficients, surface radius and conic (geometry.radius / .k) and
 thickness (Optic.set_thickness moves the later vertices), i.e. what the reference's
@@ -26,6 +34,7 @@ rays are differentiable; records of other surfaces are not.
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import numpy as np
 
@@ -179,8 +188,36 @@ class _TracePupilFn(torch.autograd.Function if torch is not None else object):
         return tuple(res)
 
 
+def vjp_mode(table):
+    """ORT_VJP_ADJOINT (one reverse-mode pass) unless a Zernike surface's Newton slope is
+    not its sag's derivative -- the standard / noll normal omits the normalisation
+    constant (zernike.py:163-231), so the unrolled iteration's derivative only converges
+    linearly to the implicit one there and the forward-mode ORT_VJP_UNROLLED keeps the
+    reference's semantics. ORT_VJP_MODE=unrolled|adjoint overrides (A/B checks)."""
+    env = os.environ.get("ORT_VJP_MODE", "").lower()
+    if env in ("unrolled", "adjoint"):
+        return _abi.VJP_UNROLLED if env == "unrolled" else _abi.VJP_ADJOINT
+    z = table.zern
+    if len(z) and np.any((z["c"] != 0.0) & (z["norm"] != 1.0)):
+        return _abi.VJP_UNROLLED
+    return _abi.VJP_ADJOINT
+
+
+_WORKSPACE = {}
+
+
+def _workspace(device, nbytes):
+    """Device scratch for the adjoint VJP, grown on demand and reused (per device)."""
+    ws = _WORKSPACE.get(device)
+    if ws is None or ws.numel() < nbytes:
+        _WORKSPACE.pop(device, None)
+        ws = torch.empty(int(nbytes), dtype=torch.uint8, device=device)
+        _WORKSPACE[device] = ws
+    return ws
+
+
 def vjp(dlens, seg_dev, px, py, n, seg_len, sched_dev, tables, n_param, cot, grad,
-        pupil_per_ray=False):
+        pupil_per_ray=False, mode=None):
     """grad += J^T cot through ort_trace_pupil_vjp. tables: device tensors
     (zern_param, surf_tangent, final_tangent), each possibly None; cot: 8 tensors / None."""
     from .raytrace import _ptr, _stream_handle
@@ -191,8 +228,16 @@ def vjp(dlens, seg_dev, px, py, n, seg_len, sched_dev, tables, n_param, cot, gra
     opt = _native.ort_options(_abi.NEWTON_SCHEDULE, 0,
                               None if sched_dev is None else sched_dev.data_ptr())
     zp, st, ft = tables
-    params = _native.ort_vjp_params(int(n_param), 0, _ptr(zp).value, _ptr(st).value,
-                                    _ptr(ft).value)
+    mode = vjp_mode(dlens.table) if mode is None else mode
+    params = _native.ort_vjp_params(int(n_param), int(mode), _ptr(zp).value, _ptr(st).value,
+                                    _ptr(ft).value, 0 if zp is None else int(zp.numel()), 0,
+                                    None, 0)
+    if mode == _abi.VJP_ADJOINT:
+        size = lib.ort_vjp_workspace_size(C.byref(dlens.c), C.byref(batch), C.byref(params))
+        _native.check(int(size) if size < 0 else 0, "ort_vjp_workspace_size")
+        ws = _workspace(grad.device, size)
+        params.workspace = ws.data_ptr()
+        params.workspace_size = ws.numel()
     cot_c = _native.ort_rays(*(0 if c is None else c.data_ptr() for c in cot))
     rc = lib.ort_trace_pupil_vjp(C.byref(dlens.c), _ptr(px), _ptr(py), C.byref(batch),
                                  C.byref(opt), C.byref(params), C.byref(cot_c), _ptr(grad),

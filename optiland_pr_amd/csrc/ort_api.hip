@@ -2,7 +2,7 @@
 // unpacking and kernel launches. Kernels are reached through the select_* functions of
 // ort_kernels.h (their templates are instantiated in the ort_k_*.hip units).
 
-#include "ort_kernels.h"
+#include "ort_adjoint.h"
 
 namespace ortk {
 
@@ -151,6 +151,36 @@ int ort_trace_pupil(const ort_lens* lens, const double* px, const double* py,
   return launch(a, feat, s);
 }
 
+// ORT_VJP_ADJOINT workspace: tape [S][kTapeRows][n_rays], partial [n_slot][n_wave],
+// slot_sum [n_slot], need [n_slot] (each 256-byte aligned)
+struct AdjLayout {
+  int32_t n_slot;
+  int64_t n_wave, tape, partial, slot_sum, need, total;
+};
+
+static bool adj_layout(const ort_lens* lens, const ort_batch* batch,
+                       const ort_vjp_params* params, AdjLayout& L) {
+  if (!lens || !batch || !params || params->n_zern < 0 || batch->n_rays < 0) return false;
+  if (params->zern_param && params->n_zern == 0) return false;
+  auto al = [](int64_t v) { return (v + 255) & ~(int64_t)255; };
+  const int64_t S = lens->n_surfaces, n = batch->n_rays;
+  L.n_slot = (int32_t)(3 * S + params->n_zern + 1);
+  L.n_wave = (n + kBlock - 1) / kBlock * (kBlock / 64);
+  L.tape = 0;
+  L.partial = al(L.tape + S * kTapeRows * n * (int64_t)sizeof(double));
+  L.slot_sum = al(L.partial + (int64_t)L.n_slot * L.n_wave * (int64_t)sizeof(double));
+  L.need = al(L.slot_sum + (int64_t)L.n_slot * (int64_t)sizeof(double));
+  L.total = al(L.need + (int64_t)L.n_slot * (int64_t)sizeof(int32_t));
+  return true;
+}
+
+int64_t ort_vjp_workspace_size(const ort_lens* lens, const ort_batch* batch,
+                               const ort_vjp_params* params) {
+  AdjLayout L;
+  if (!adj_layout(lens, batch, params, L)) return ORT_ERR_ARG;
+  return L.total;
+}
+
 int ort_trace_pupil_vjp(const ort_lens* lens, const double* px, const double* py,
                         const ort_batch* batch, const ort_options* opt,
                         const ort_vjp_params* params, const ort_rays* cotangent,
@@ -178,6 +208,30 @@ int ort_trace_pupil_vjp(const ort_lens* lens, const double* px, const double* py
   if (blocks > 0x7fffffff) return ORT_ERR_ARG;
   const uint32_t km = feat & F_KM;
   hipStream_t s = (hipStream_t)stream;
+  if (params->mode == ORT_VJP_ADJOINT) {
+    AdjLayout L;
+    if (!adj_layout(lens, batch, params, L)) return ORT_ERR_ARG;
+    if (!params->workspace || params->workspace_size < L.total) return ORT_ERR_ARG;
+    char* w = (char*)params->workspace;
+    AArgs aj{};
+    aj.zparam = params->zern_param;
+    aj.tan_surf = params->surf_tangent;
+    aj.tan_final = params->final_tangent;
+    aj.n_param = n_param;
+    aj.n_zern = params->n_zern;
+    aj.n_slot = L.n_slot;
+    aj.n_surf = lens->n_surfaces;
+    aj.n_wave = L.n_wave;
+    aj.cot = *cotangent;
+    aj.tape = (double*)(w + L.tape);
+    aj.partial = (double*)(w + L.partial);
+    aj.slot_sum = (double*)(w + L.slot_sum);
+    aj.need = (int32_t*)(w + L.need);
+    aj.grad = grad;
+    // radius / conic tangents need duals seeded on them too
+    return adj_run(a, aj, params->surf_tangent ? 4 : 2, km, blocks, s);
+  }
+  if (params->mode != ORT_VJP_UNROLLED) return ORT_ERR_ARG;
   for (int p0 = 0; p0 < n_param;) {
     const int left = n_param - p0;
     // tangents per launch: ORT_VJP_TANGENTS overrides (A/B timing)

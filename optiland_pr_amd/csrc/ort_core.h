@@ -934,6 +934,86 @@ ORT_INLINE T sagnorm_zernike(const T& x, const T& y, const S& R, const S& k, dou
   return z + total;
 }
 
+// Reverse-mode companion of sagnorm_zernike for the coefficients (adjoint VJP): the sag
+// and the normal's slopes are linear in c_j, so for every term j of the surface
+//   g_j = w_sag * d sag / d c_j + w_dx * d dzdx / d c_j + w_dy * d dzdy / d c_j
+// is handed to emit(j, g_j) -- one pass over the terms, whatever the number of
+// coefficients. The slope part follows the reference's normal, which only sums terms
+// with c_j != 0 (zernike.py:213-214) and omits the normalisation constant.
+template <class PD, class PZ, class F>
+ORT_INLINE void zernike_coef_adjoint(double x, double y, double Rn, PZ Tm, int t0, int nt,
+                                     PD coef, double w_sag, double w_dx, double w_dy,
+                                     F&& emit) {
+  const double xn = x / Rn;
+  const double yn = y / Rn;
+  const double rho = sqrt(xn * xn + yn * yn);
+  double c1, s1;
+  if (rho > 0.0) {
+    c1 = xn / rho;
+    s1 = yn / rho;
+  } else {
+    c1 = 1.0;
+    s1 = 0.0;
+  }
+  const double rho2 = rho * rho;
+  const double eps = 1e-14;
+  const double Rn2 = Rn * Rn;
+  const double drho_dx = (x / Rn2) / (rho + eps);
+  const double drho_dy = (y / Rn2) / (rho + eps);
+  const double rho2e = rho2 + eps;
+  const double inv_rn = 1.0 / Rn;
+  const double dphi_dx = -(yn) / rho2e * inv_rn;
+  const double dphi_dy = (xn) / rho2e * inv_rn;
+  for (int j = 0; j < nt; ++j) {
+    const ort_zernike_term t = Tm[t0 + j];
+    const int am = t.m >= 0 ? t.m : -t.m;
+    double cm = 1.0, sm = 0.0, pm = 1.0, pm1 = 1.0;
+#pragma unroll 1
+    for (int qq = 0; qq < am; ++qq) {
+      const double cn = cm * c1 - sm * s1;
+      sm = sm * c1 + cm * s1;
+      cm = cn;
+      pm1 = pm;
+      pm = pm * rho;
+    }
+    const PD a = coef + t.rad_off;
+    double P = a[0];
+#pragma unroll 1
+    for (int kk = 1; kk < t.n_rad; ++kk) P = P * rho2 + a[kk];
+    const double rt = P * pm;
+    const double az = t.m >= 0 ? cm : sm;
+    double g = w_sag * (t.norm * rt * az);
+    if (t.c != 0.0) {
+      const PD d = a + t.n_rad;
+      double rd = 0.0;
+      if (am > 0) {
+        double Q = d[0];
+#pragma unroll 1
+        for (int kk = 1; kk < t.n_rad; ++kk) Q = Q * rho2 + d[kk];
+        rd = Q * pm1;
+      } else if (t.n_rad > 1) {
+        double Q = d[0];
+#pragma unroll 1
+        for (int kk = 1; kk < t.n_rad - 1; ++kk) Q = Q * rho2 + d[kk];
+        rd = Q * rho;
+      }
+      double dr, dp;
+      if (t.m == 0) {
+        dr = rd;
+        dp = 0.0;
+      } else if (t.m > 0) {
+        dr = rd * cm;
+        dp = (double)(-t.m) * rt * sm;
+      } else {
+        dr = rd * sm;
+        dp = (double)am * rt * cm;
+      }
+      g += w_dx * (dr * drho_dx + dp * dphi_dx) + w_dy * (dr * drho_dy + dp * dphi_dy);
+    }
+    emit(t0 + j, g);
+  }
+}
+
 // Sag and normal of a Newton-iterated geometry (EvenAsphere / OddAsphere / Zernike).
 // KM is a bitmask of the Newton kinds compiled in (KM_EVEN | KM_ODD | KM_ZERN): a lens
 // only pays registers for the kinds it contains.

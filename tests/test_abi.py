@@ -71,7 +71,9 @@ def test_enums_match_header():
                          ("ORT_CS_ROT_Y", _abi.CS_ROT_Y), ("ORT_CS_ROT_Z", _abi.CS_ROT_Z),
                          ("ORT_GEN_INFINITE", _abi.GEN_INFINITE), ("ORT_GEN_FINITE", _abi.GEN_FINITE),
                          ("ORT_NEWTON_SCHEDULE", _abi.NEWTON_SCHEDULE),
-                         ("ORT_NEWTON_WAVE", _abi.NEWTON_WAVE)]:
+                         ("ORT_NEWTON_WAVE", _abi.NEWTON_WAVE),
+                         ("ORT_VJP_UNROLLED", _abi.VJP_UNROLLED),
+                         ("ORT_VJP_ADJOINT", _abi.VJP_ADJOINT)]:
         m = re.search(rf"{cname}\s*=\s*(\d+)", text)
         assert m and int(m.group(1)) == pyval, cname
     for cname, pyval in [("ORT_SURF_REFLECTIVE", _abi.SURF_REFLECTIVE),
@@ -89,7 +91,7 @@ def test_library_exports_every_declared_symbol():
     if not os.path.exists(_native.LIB_PATH):
         pytest.skip("HIP extension not built (run __graft_entry__.build())")
     lib = _native.load()
-    declared = set(re.findall(r"^int (ort_\w+)\(", open(HEADER).read(), re.M))
+    declared = set(re.findall(r"^int(?:64_t)? (ort_\w+)\(", open(HEADER).read(), re.M))
     assert declared == set(_native.EXPORTS)
     for sym in declared:
         assert hasattr(lib, sym), sym
