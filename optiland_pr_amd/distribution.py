@@ -105,6 +105,49 @@ class RingDistribution(BaseDistribution):
         self.y = np.sin(theta)
 
 
+class GaussianQuadrature(BaseDistribution):
+    """distribution.py:268-355: Gaussian-quadrature rings (G. W. Forbes, JOSA A 5, 1988),
+    3 azimuths (-60, 0, 60 deg) per ring, or 1 with is_symmetric; weights per ring."""
+
+    _RADIUS = {
+        1: [0.70711],
+        2: [0.45970, 0.88807],
+        3: [0.33571, 0.70711, 0.94196],
+        4: [0.26350, 0.57446, 0.81853, 0.96466],
+        5: [0.21659, 0.48038, 0.70711, 0.87706, 0.97626],
+        6: [0.18375, 0.41158, 0.61700, 0.78696, 0.91138, 0.98300],
+    }
+    _WEIGHTS = {
+        1: [0.5],
+        2: [0.25, 0.25],
+        3: [0.13889, 0.22222, 0.13889],
+        4: [0.08696, 0.16304, 0.16304, 0.08696],
+        5: [0.059231, 0.11966, 0.14222, 0.11966, 0.059231],
+        6: [0.04283, 0.09019, 0.11698, 0.11698, 0.09019, 0.04283],
+    }
+
+    def __init__(self, is_symmetric=False):
+        self.is_symmetric = is_symmetric
+
+    def _get_radius(self, num_rings: int):
+        if num_rings not in self._RADIUS:
+            raise ValueError("Gaussian quadrature must have between 1 and 6 rings.")
+        return np.array(self._RADIUS[num_rings])
+
+    def generate_points(self, num_rings: int):
+        radius = self._get_radius(num_rings)
+        theta = np.array([0.0]) if self.is_symmetric else np.array(
+            [-1.04719755, 0.0, 1.04719755])
+        self.x = np.outer(radius, np.cos(theta)).flatten()
+        self.y = np.outer(radius, np.sin(theta)).flatten()
+
+    def get_weights(self, num_rings: int):
+        if num_rings not in self._WEIGHTS:
+            raise ValueError("Gaussian quadrature must have between 1 and 6 rings.")
+        w = np.array(self._WEIGHTS[num_rings])
+        return w * 6.0 if self.is_symmetric else w * 2.0
+
+
 def create_distribution(distribution_type) -> BaseDistribution:
     """distribution.py:378-408."""
     classes = {

@@ -469,8 +469,39 @@ def full_size_summaries():
     return res
 
 
+DIST_CASES = [("random", 1000, {"seed": 7}), ("uniform", 33, {}), ("uniform", 128, {}),
+              ("hexapolar", 6, {}), ("hexapolar", 17, {}), ("ring", 13, {}),
+              ("line_x", 21, {}), ("line_y", 20, {}), ("positive_line_x", 9, {}),
+              ("positive_line_y", 10, {}), ("cross", 21, {}), ("cross", 20, {})]
+
+
+def distribution_goldens():
+    """Pupil samples of every reference distribution (distribution.py:72-408), incl.
+    GaussianQuadrature (not in create_distribution) -> tests/golden/distributions.npz."""
+    from optiland.distribution import GaussianQuadrature
+
+    out = {}
+    for kind, n, kw in DIST_CASES:
+        d = RandomDistribution(**kw) if kind == "random" else create_distribution(kind)
+        d.generate_points(n)
+        out[f"{kind}_{n}_x"] = np.asarray(d.x, dtype=np.float64)
+        out[f"{kind}_{n}_y"] = np.asarray(d.y, dtype=np.float64)
+    for sym in (False, True):
+        for rings in range(1, 7):
+            g = GaussianQuadrature(is_symmetric=sym)
+            g.generate_points(rings)
+            key = f"gq_{int(sym)}_{rings}"
+            out[key + "_x"] = np.asarray(g.x, dtype=np.float64)
+            out[key + "_y"] = np.asarray(g.y, dtype=np.float64)
+            out[key + "_w"] = np.asarray(g.get_weights(rings), dtype=np.float64)
+    np.savez_compressed(os.path.join(HERE, "distributions.npz"), **out)
+
+
 def main():
     # --only NAME [NAME ...]: regenerate just those cases, keep the rest of index.json
+    if "--distributions" in sys.argv:
+        distribution_goldens()
+        return
     if "--glasses" in sys.argv:  # re-bake optiland_pr_amd/data/glasses.json only
         glass_table()
         return
@@ -491,6 +522,7 @@ def main():
         index[name] = generate_case(name, builder, fields, wls, dist, num)
         print(f"{name}: {index[name]['n_pupil']} pupil pts, {time.perf_counter() - t0:.2f}s",
               file=sys.stderr)
+    distribution_goldens()
     index["_analysis"] = analysis_goldens()
     index["_full"] = full_size_summaries()
     with open(os.path.join(HERE, "index.json"), "w") as f:
