@@ -225,6 +225,33 @@ enum ort_status {
   ORT_STATUS_CHEBYSHEV_RANGE = 1u << 1 /* chebyshev.py:203-215 ValueError          */
 };
 
+/* Pupil distribution generated on the device (distribution.py:72-408), see
+ * ort_generate_pupil. Tables are device memory prepared by the host (a few KB). */
+enum ort_pupil_kind {
+  ORT_PUPIL_UNIFORM = 0,   /* linspace grid masked to the unit disk        */
+  ORT_PUPIL_HEXAPOLAR = 1, /* 1 + 3 n (n + 1) points on n rings            */
+  ORT_PUPIL_RANDOM = 2,    /* numpy default_rng (PCG64) uniform r, theta   */
+  ORT_PUPIL_RING = 3,
+  ORT_PUPIL_LINE_X = 4,
+  ORT_PUPIL_LINE_Y = 5,
+  ORT_PUPIL_CROSS = 6
+};
+typedef struct ort_pupil {
+  int32_t kind;              /* ort_pupil_kind                                        */
+  int32_t positive_only;     /* LINE_X / LINE_Y: linspace(0, 1, n) instead of (-1, 1)  */
+  int64_t n;                 /* the distribution's num_points / num_rings argument    */
+  int64_t n_points;          /* points generated                                      */
+  int32_t n_rows;            /* UNIFORM: grid rows holding points                     */
+  int32_t reserved;
+  const int64_t* row_start;  /* UNIFORM [n_rows]: index of the row's first point      */
+  const int64_t* row_col;    /* UNIFORM [n_rows][2]: grid row, its first column       */
+  const uint64_t* rng_chunk; /* RANDOM [ceil(n_points / 256)][4]: PCG64 state (lo, hi) *
+                              * before draw 256 c (radii) and before draw n_points +   *
+                              * 256 c (angles)                                        */
+  const uint64_t* rng_lane;  /* RANDOM [256][4]: the LCG map advanced l + 1 steps:     *
+                              * multiplier (lo, hi), increment (lo, hi)               */
+} ort_pupil;
+
 /* ---- entry points ------------------------------------------------------------- */
 
 int ort_abi_version(void);
@@ -312,6 +339,11 @@ int ort_surface_sag_normal(const ort_lens* lens, int32_t surface, const double* 
 int ort_surface_distance(const ort_lens* lens, int32_t surface, const ort_rays* rays,
                          int64_t n, const ort_options* opt, double* t,
                          ort_newton_stat* newton_stat, int32_t* status, void* stream);
+
+/* Pupil coordinates of a distribution on the device: px[k], py[k] for k < n_points
+ * (distribution.py:72-408; the grid kinds bit-identical to NumPy, cos / sin correctly
+ * rounded). Feeds ort_trace_pupil without host-side sampling or a host-to-device copy. */
+int ort_generate_pupil(const ort_pupil* pupil, double* px, double* py, void* stream);
 
 /* Ray generation only (ray_generator.py:28-106): fills rays_out from pupil points. */
 int ort_generate_rays(const double* px, const double* py, ort_rays* rays_out,

@@ -12,6 +12,13 @@ import numpy as np
 ABI_VERSION = 5
 VJP_UNROLLED = 0
 VJP_ADJOINT = 1
+PUPIL_UNIFORM = 0
+PUPIL_HEXAPOLAR = 1
+PUPIL_RANDOM = 2
+PUPIL_RING = 3
+PUPIL_LINE_X = 4
+PUPIL_LINE_Y = 5
+PUPIL_CROSS = 6
 MAX_SURFACES = 64
 
 # enum ort_geometry

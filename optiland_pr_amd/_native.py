@@ -61,6 +61,21 @@ class ort_vjp_params(C.Structure):
     ]
 
 
+class ort_pupil(C.Structure):
+    _fields_ = [
+        ("kind", C.c_int32),
+        ("positive_only", C.c_int32),
+        ("n", C.c_int64),
+        ("n_points", C.c_int64),
+        ("n_rows", C.c_int32),
+        ("reserved", C.c_int32),
+        ("row_start", C.c_void_p),
+        ("row_col", C.c_void_p),
+        ("rng_chunk", C.c_void_p),
+        ("rng_lane", C.c_void_p),
+    ]
+
+
 class ort_options(C.Structure):
     _fields_ = [
         ("newton_mode", C.c_int32),
@@ -70,7 +85,7 @@ class ort_options(C.Structure):
 
 
 EXPORTS = ("ort_abi_version", "ort_trace_sequential", "ort_trace_pupil", "ort_trace_pupil_vjp",
-           "ort_vjp_workspace_size",
+           "ort_vjp_workspace_size", "ort_generate_pupil",
            "ort_surface_sag_normal", "ort_surface_distance", "ort_generate_rays")
 
 _lib = None
@@ -117,6 +132,8 @@ def load(path: str | None = None):
     lib.ort_surface_distance.argtypes = [P(ort_lens), C.c_int32, P(ort_rays), C.c_int64,
                                          P(ort_options), C.c_void_p, C.c_void_p, C.c_void_p,
                                          C.c_void_p]
+    lib.ort_generate_pupil.restype = C.c_int
+    lib.ort_generate_pupil.argtypes = [P(ort_pupil), C.c_void_p, C.c_void_p, C.c_void_p]
     lib.ort_generate_rays.restype = C.c_int
     lib.ort_generate_rays.argtypes = [C.c_void_p, C.c_void_p, P(ort_rays), P(ort_batch),
                                       C.c_void_p]

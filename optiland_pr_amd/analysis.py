@@ -17,6 +17,7 @@ import numpy as np
 
 from . import _abi
 from .distribution import BaseDistribution, create_distribution
+from .pupil import pupil_arrays
 from .lowering import segment_params
 from .raytrace import RealRays, lens_for, trace_pupil
 
@@ -97,11 +98,6 @@ class SpotDiagram:
 
     def _generate_data(self):
         optic = self.optic
-        d = self.distribution
-        if isinstance(d, str):
-            d = create_distribution(d)
-            d.generate_points(self.num_rings)
-        Px, Py = np.asarray(d.x, dtype=np.float64), np.asarray(d.y, dtype=np.float64)
         for hx, hy in self.fields:  # real_ray_tracer.py:59 validation
             if not (-1 <= hx <= 1 and -1 <= hy <= 1):
                 raise ValueError("Normalized field coordinates must be within (-1, 1)")
@@ -109,14 +105,14 @@ class SpotDiagram:
         EPL, EPD = optic.paraxial.EPL(), optic.paraxial.EPD()
         segs = np.stack([segment_params(optic, float(hx), float(hy), wi, EPL, EPD)
                          for hx, hy in self.fields for wi in range(len(self.wavelengths))])
-        n_p = Px.size
-        n = n_p * len(segs)
         dev = dl.device
+        px, py = pupil_arrays(self.distribution, self.num_rings, dev)
+        n_p = px.numel()
+        n = n_p * len(segs)
         out = RealRays.empty(n, 0.0, device=dev)
         keys = [("trace", (float(hx),), (float(hy),), float(w), n_p)
                 for hx, hy in self.fields for w in self.wavelengths]
-        trace_pupil(dl, segs, torch.as_tensor(Px, device=dev), torch.as_tensor(Py, device=dev),
-                    out, n, n_p, n_p, keys=keys, newton_mode=self.newton_mode)
+        trace_pupil(dl, segs, px, py, out, n, n_p, n_p, keys=keys, newton_mode=self.newton_mode)
         self.rays = out
         data = []
         k = 0

@@ -248,6 +248,19 @@ int ort_trace_pupil_vjp(const ort_lens* lens, const double* px, const double* py
   return ORT_OK;
 }
 
+int ort_generate_pupil(const ort_pupil* pupil, double* px, double* py, void* stream) {
+  if (!pupil || pupil->n_points < 0) return ORT_ERR_ARG;
+  if (pupil->n_points == 0) return ORT_OK;
+  if (!px || !py || pupil->kind < ORT_PUPIL_UNIFORM || pupil->kind > ORT_PUPIL_CROSS)
+    return ORT_ERR_ARG;
+  if (pupil->kind == ORT_PUPIL_UNIFORM && (pupil->n_rows <= 0 || !pupil->row_start ||
+                                           !pupil->row_col))
+    return ORT_ERR_ARG;
+  if (pupil->kind == ORT_PUPIL_RANDOM && (!pupil->rng_chunk || !pupil->rng_lane))
+    return ORT_ERR_ARG;
+  return launch_pupil(*pupil, px, py, (hipStream_t)stream);
+}
+
 int ort_surface_sag_normal(const ort_lens* lens, int32_t surface, const double* x,
                            const double* y, int64_t n, double* sag, double* nx, double* ny,
                            double* nz, int32_t* status, void* stream) {

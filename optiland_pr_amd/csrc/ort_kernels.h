@@ -641,5 +641,6 @@ KernelFn select_closed(uint32_t feat);     // closed-form lenses                
 KernelFn select_generate();                // ray generation only               (ort_k_closed.hip)
 VjpFn select_vjp(int tangents, uint32_t km);  // tangents 1, 2 or 4             (ort_k_vjp*.hip)
 GeomFn select_geom(uint32_t km);           // per-geometry primitives           (ort_k_geom.hip)
+int launch_pupil(const ort_pupil& d, double* px, double* py, hipStream_t stream);  // ort_k_pupil.hip
 
 }  // namespace ortk

@@ -22,7 +22,7 @@ import ctypes as C
 import numpy as np
 
 from . import _abi, _native, autodiff
-from .distribution import BaseDistribution, create_distribution
+from .pupil import pupil_arrays
 from .lowering import LensTable, lower_surface_group, segment_params
 
 try:
@@ -382,13 +382,6 @@ class RealRayTracer:
               newton_mode="reference"):
         optic = self.optic
         _validate_normalized(Hx, Hy, "field")
-        if isinstance(distribution, str):
-            distribution = create_distribution(distribution)
-            distribution.generate_points(num_rays)
-        if not isinstance(distribution, BaseDistribution) and not hasattr(distribution, "x"):
-            raise ValueError("Invalid distribution type.")
-        Px = np.asarray(distribution.x, dtype=np.float64)
-        Py = np.asarray(distribution.y, dtype=np.float64)
         Hx = np.atleast_1d(np.asarray(Hx, dtype=np.float64))
         Hy = np.atleast_1d(np.asarray(Hy, dtype=np.float64))
         Hx, Hy = np.broadcast_arrays(Hx, Hy)
@@ -397,11 +390,10 @@ class RealRayTracer:
         EPL, EPD = optic.paraxial.EPL(), optic.paraxial.EPD()
         segs = np.stack([segment_params(optic, float(hx), float(hy), 0, EPL, EPD)
                          for hx, hy in zip(Hx, Hy, strict=True)])
-        n_p = Px.size
-        n = n_p * len(segs)
         dev = dlens.device
-        px = torch.as_tensor(Px, device=dev)
-        py = torch.as_tensor(Py, device=dev)
+        px, py = pupil_arrays(distribution, num_rays, dev)
+        n_p = px.numel()
+        n = n_p * len(segs)
         keys = [("trace", tuple(np.round(Hx, 15)), tuple(np.round(Hy, 15)), float(wavelength), n_p)]
         if autodiff.wants_grad(optic):
             return self._trace_grad(dlens, segs, px, py, n, n_p, wavelength, keys,

@@ -25,6 +25,7 @@ STRUCTS = {
     "ort_batch": (None, _native.ort_batch),
     "ort_options": (None, _native.ort_options),
     "ort_vjp_params": (None, _native.ort_vjp_params),
+    "ort_pupil": (None, _native.ort_pupil),
 }
 
 
@@ -73,7 +74,14 @@ def test_enums_match_header():
                          ("ORT_NEWTON_SCHEDULE", _abi.NEWTON_SCHEDULE),
                          ("ORT_NEWTON_WAVE", _abi.NEWTON_WAVE),
                          ("ORT_VJP_UNROLLED", _abi.VJP_UNROLLED),
-                         ("ORT_VJP_ADJOINT", _abi.VJP_ADJOINT)]:
+                         ("ORT_VJP_ADJOINT", _abi.VJP_ADJOINT),
+                         ("ORT_PUPIL_UNIFORM", _abi.PUPIL_UNIFORM),
+                         ("ORT_PUPIL_HEXAPOLAR", _abi.PUPIL_HEXAPOLAR),
+                         ("ORT_PUPIL_RANDOM", _abi.PUPIL_RANDOM),
+                         ("ORT_PUPIL_RING", _abi.PUPIL_RING),
+                         ("ORT_PUPIL_LINE_X", _abi.PUPIL_LINE_X),
+                         ("ORT_PUPIL_LINE_Y", _abi.PUPIL_LINE_Y),
+                         ("ORT_PUPIL_CROSS", _abi.PUPIL_CROSS)]:
         m = re.search(rf"{cname}\s*=\s*(\d+)", text)
         assert m and int(m.group(1)) == pyval, cname
     for cname, pyval in [("ORT_SURF_REFLECTIVE", _abi.SURF_REFLECTIVE),
