@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define ORT_ABI_VERSION 5
+#define ORT_ABI_VERSION 6
 #define ORT_MAX_SURFACES 64
 
 /* ---- geometry kinds ----------------------------------- */
@@ -59,7 +59,8 @@ enum ort_surface_flags {
   ORT_SURF_RADIUS_INF = 1u << 1, /* standard.py:100-103 plane branch of a conic guess   */
   ORT_SURF_APERTURE = 1u << 2,   /* radial physical aperture: physical_apertures/radial.py */
   ORT_SURF_RECORD = 1u << 3,     /* snapshot the ray state after this surface (_record)  */
-  ORT_SURF_TRANSLATE = 1u << 4   /* informational: the frame is the translation cs_t only  */
+  ORT_SURF_TRANSLATE = 1u << 4,  /* informational: the frame is the translation cs_t only  */
+  ORT_SURF_APERTURE_PROG = 1u << 5 /* general aperture: a program in lens.coef (ap_off)  */
                                  /* (both op lists empty)                                  */
 };
 
@@ -102,8 +103,33 @@ typedef struct ort_surface {
   int32_t rec_slot;   /* slot in the record buffer when ORT_SURF_RECORD              */
   double cs_t[3];     /* root-frame translation: localize = x + -cs_t, then the loc    */
                       /* ops; globalize = the glob ops, then x + cs_t                  */
-  double reserved;
+  int32_t ap_off;     /* ORT_SURF_APERTURE_PROG: aperture program at lens.coef[ap_off] */
+  int32_t ap_len;     /* its length in doubles                                       */
 } ort_surface; /* 128 bytes */
+
+/* Aperture programs (physical_apertures/*.py): postfix, each op a double opcode followed
+ * by its operands; primitives push contains(x, y) of the ray's local (x, y), the boolean
+ * ops pop two and push one; a ray is clipped (i = 0, real_rays.py:132-139) when the
+ * final value is false.
+ *   ORT_AP_RADIAL    r_min^2 r_max^2 ox oy  r_min^2 <= (x-ox)^2 + (y-oy)^2 <= r_max^2
+ *                                           (radial.py:54-63, offset_radial.py:46-58)
+ *   ORT_AP_ELLIPSE   ox oy a^2 b^2          (x-ox)^2 / a^2 + (y-oy)^2 / b^2 <= 1
+ *                                           (elliptical.py:40-55)
+ *   ORT_AP_RECT      x_min x_max y_min y_max (rectangular.py:40-60)
+ *   ORT_AP_POLYGON   n x0 y0 ... x(n-1) y(n-1): even-odd crossing test of the implicitly
+ *                    closed polygon, matplotlib Path.contains_points semantics
+ *                    (polygon.py:50-66 via backend path_contains_points)
+ *   ORT_AP_UNION / ORT_AP_INTERSECT / ORT_AP_DIFFERENCE: a | b, a & b, a & ~b
+ *                    (base.py:255-340) */
+enum ort_aperture_op {
+  ORT_AP_RADIAL = 1,
+  ORT_AP_ELLIPSE = 2,
+  ORT_AP_RECT = 3,
+  ORT_AP_POLYGON = 4,
+  ORT_AP_UNION = 5,
+  ORT_AP_INTERSECT = 6,
+  ORT_AP_DIFFERENCE = 7
+};
 
 /* Per (wavelength, surface) optical constants, read in the same scalar-load batch as
  * the surface record (one round trip per surface instead of three dependent ones). */

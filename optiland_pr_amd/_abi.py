@@ -9,9 +9,16 @@ from __future__ import annotations
 
 import numpy as np
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 VJP_UNROLLED = 0
 VJP_ADJOINT = 1
+AP_RADIAL = 1
+AP_ELLIPSE = 2
+AP_RECT = 3
+AP_POLYGON = 4
+AP_UNION = 5
+AP_INTERSECT = 6
+AP_DIFFERENCE = 7
 PUPIL_UNIFORM = 0
 PUPIL_HEXAPOLAR = 1
 PUPIL_RANDOM = 2
@@ -40,6 +47,7 @@ SURF_RADIUS_INF = 1 << 1
 SURF_APERTURE = 1 << 2
 SURF_RECORD = 1 << 3
 SURF_TRANSLATE = 1 << 4
+SURF_APERTURE_PROG = 1 << 5
 
 # enum ort_cs_kind
 CS_TRANSLATE = 0
@@ -85,7 +93,8 @@ SURFACE = np.dtype(
         ("n_cs_glob", "<i4"),
         ("rec_slot", "<i4"),
         ("cs_t", "<f8", (3,)),
-        ("reserved", "<f8"),
+        ("ap_off", "<i4"),
+        ("ap_len", "<i4"),
     ],
     align=True,
 )

@@ -138,10 +138,21 @@ class _Group:
         self.surfaces = surfaces
 
 
+def _plain(d):
+    """reference to_dict() output with backend arrays / tensors as lists and floats"""
+    if isinstance(d, dict):
+        return {k: _plain(v) for k, v in d.items()}
+    if hasattr(d, "detach"):
+        d = d.detach().cpu().numpy()
+    if isinstance(d, np.ndarray):
+        return d.tolist()
+    return d
+
+
 def lower_reference_group(ref_group, wavelengths, record=False):
     """Reference SurfaceGroup -> LensTable (raises Unsupported when not lowerable)."""
+    from .apertures import BaseAperture
     from .lowering import lower_surface_group
-    from .surfaces import RadialAperture
 
     mats = {}
 
@@ -161,10 +172,11 @@ def lower_reference_group(ref_group, wavelengths, record=False):
             if type(m.propagation_model).__name__ != "HomogeneousPropagation":
                 raise Unsupported("propagation model")
         ap = None
-        if s.aperture is not None:
-            if type(s.aperture).__name__ != "RadialAperture":
-                raise Unsupported(type(s.aperture).__name__)
-            ap = RadialAperture(_f(s.aperture.r_max), _f(s.aperture.r_min))
+        if s.aperture is not None:  # the reference's to_dict schema (physical_apertures)
+            try:
+                ap = BaseAperture.from_dict(_plain(s.aperture.to_dict()))
+            except (ValueError, KeyError, AttributeError) as e:
+                raise Unsupported(type(s.aperture).__name__) from e
         surfs.append(_Surf(_geometry(s.geometry), mat(s.material_pre), mat(s.material_post),
                            bool(im.is_reflective), ap, _f(s.thickness)))
     # lower_surface_group skips ObjectSurface instances; pass the traced surfaces only

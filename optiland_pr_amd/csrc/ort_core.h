@@ -1121,6 +1121,76 @@ ORT_INLINE void clip_radial(RayT<T>& r, double rmax2, double rmin2) {
   }
 }
 
+// General physical apertures (physical_apertures/*.py): the postfix program described
+// at ort_aperture_op, evaluated on the local (x, y); clips like clip_radial. The stack of
+// booleans is a bit mask (at most 32 deep).
+template <class PD>
+ORT_INLINE bool aperture_contains(PD p, int len, double x, double y) {
+  uint32_t st = 0;
+  int sp = 0;
+  for (int q = 0; q < len;) {
+    const int op = (int)p[q];
+    bool v = false;
+    switch (op) {
+      case ORT_AP_RADIAL: {  // radial.py:62, offset_radial.py:57-58
+        const double dx = x - p[q + 3], dy = y - p[q + 4];
+        const double r2 = dx * dx + dy * dy;
+        v = (r2 <= p[q + 2]) && (r2 >= p[q + 1]);
+        q += 5;
+      } break;
+      case ORT_AP_ELLIPSE: {  // elliptical.py:53-55
+        const double dx = x - p[q + 1], dy = y - p[q + 2];
+        v = (dx * dx / p[q + 3] + dy * dy / p[q + 4]) <= 1.0;
+        q += 5;
+      } break;
+      case ORT_AP_RECT:  // rectangular.py:54-59
+        v = (p[q + 1] <= x) && (x <= p[q + 2]) && (p[q + 3] <= y) && (y <= p[q + 4]);
+        q += 5;
+        break;
+      case ORT_AP_POLYGON: {  // matplotlib point_in_path: even-odd crossings, closed
+        const int n = (int)p[q + 1];
+        const PD v0 = p + q + 2;
+        if (isfinite(x) && isfinite(y) && n > 0) {
+          double vx0 = v0[2 * (n - 1)], vy0 = v0[2 * (n - 1) + 1];
+          // edges (v_{k-1} -> v_k) for k = 0..n-1 with v_{-1} = v_{n-1}: the same edge set
+          // as matplotlib's v_0 -> v_1 -> ... -> v_{n-1} -> v_0, the same test per edge
+          bool yflag0 = vy0 >= y;
+          bool in = false;
+          for (int k = 0; k < n; ++k) {
+            const double vx1 = v0[2 * k], vy1 = v0[2 * k + 1];
+            const bool yflag1 = vy1 >= y;
+            if (yflag0 != yflag1 &&
+                (((vy1 - y) * (vx0 - vx1) >= (vx1 - x) * (vy0 - vy1)) == yflag1))
+              in = !in;
+            yflag0 = yflag1;
+            vx0 = vx1;
+            vy0 = vy1;
+          }
+          v = in;
+        }
+        q += 2 + 2 * n;
+      } break;
+      default: {  // boolean ops (base.py:255-340)
+        const bool b = (st >> (sp - 1)) & 1u, a = (st >> (sp - 2)) & 1u;
+        sp -= 2;
+        v = op == ORT_AP_UNION ? (a || b) : (op == ORT_AP_INTERSECT ? (a && b) : (a && !b));
+        q += 1;
+      } break;
+    }
+    st = (st & ~(1u << sp)) | ((uint32_t)v << sp);
+    ++sp;
+  }
+  return sp > 0 && ((st >> (sp - 1)) & 1u);
+}
+
+template <class T, class PD>
+ORT_INLINE void clip_program(RayT<T>& r, PD prog, int len) {
+  if (!aperture_contains(prog, len, vv(r.x), vv(r.y))) {
+    r.i = T(0.0);
+    r.att = T(0.0);
+  }
+}
+
 // rays/real_rays.py:511-547: sign(dot) flip (np.sign: 0 -> 0, NaN -> NaN), |dot|
 template <class T>
 ORT_INLINE T align_normal(const RayT<T>& r, T& nx, T& ny, T& nz) {
@@ -1179,6 +1249,7 @@ ORT_INLINE void finish_surface(RayT<T>& r, const ort_surface& s, const S& R, con
   propagate(r, t, alpha_pre);
   add_opd(r, t, n_pre);
   if (s.flags & ORT_SURF_APERTURE) clip_radial(r, s.ap_rmax2, s.ap_rmin2);
+  if (s.flags & ORT_SURF_APERTURE_PROG) clip_program(r, coef + s.ap_off, s.ap_len);
   T nx, ny, nz;
   surface_normal<KM>(s, R, K, coef, zern, zs, r, nx, ny, nz);
   if (s.flags & ORT_SURF_REFLECTIVE)

@@ -8,7 +8,9 @@ stop flag, radial aperture and mirror flag. This module reads and writes that sc
 with the native host classes, so a lens saved by the reference (e.g. its
 docs/samples/*.json) traces on the MI355X without the reference installed. Catalog
 glasses resolve through the baked table (data/glasses.json); unknown glasses and
-unsupported surface / interaction types raise ValueError.
+unsupported surface / interaction types raise ValueError. Physical apertures of every
+kind (radial, offset radial, elliptical, rectangular, polygon, boolean combinations)
+round-trip in the reference's aperture schema.
 """
 
 from __future__ import annotations
@@ -30,7 +32,8 @@ from .geometries import (
     ZernikePolynomialGeometry,
 )
 from .materials import IdealMaterial, Material
-from .surfaces import ObjectSurface, RadialAperture, Surface
+from .apertures import BaseAperture
+from .surfaces import ObjectSurface, Surface
 
 _FIELD_TYPES = {"AngleField": "angle", "ObjectHeightField": "object_height",
                 "ParaxialImageHeightField": "paraxial_image_height",
@@ -163,10 +166,10 @@ def optic_from_dict(data):
         else:
             apd = sd.get("aperture")
             aperture = None
-            if apd:
-                if apd.get("type", "RadialAperture") != "RadialAperture":
-                    raise ValueError(f"surface {k}: aperture {apd.get('type')} is out of scope")
-                aperture = RadialAperture(r_max=apd["r_max"], r_min=apd.get("r_min", 0.0))
+            if apd:  # physical_apertures/*.py from_dict
+                if "type" not in apd:
+                    apd = dict(apd, type="RadialAperture")
+                aperture = BaseAperture.from_dict(apd)
             s = Surface(prev, post, geometry, is_stop=bool(sd.get("is_stop", False)),
                         aperture=aperture, surface_type=sd.get("surface_type"),
                         is_reflective=bool(sd.get("is_reflective", False)))
@@ -208,9 +211,7 @@ def optic_to_dict(optic):
              "thickness": float(s.thickness)}
         if not isinstance(s, ObjectSurface):
             d.update(material_pre=material_to_dict(s.material_pre), is_stop=bool(s.is_stop),
-                     aperture=None if s.aperture is None else
-                     {"type": "RadialAperture", "r_max": s.aperture.r_max,
-                      "r_min": s.aperture.r_min},
+                     aperture=None if s.aperture is None else s.aperture.to_dict(),
                      coating=None, bsdf=None, is_reflective=bool(s.is_reflective))
         surfaces.append(d)
     fields = [{"field_type": optic.field_type, "x": f.x, "y": f.y, "vx": f.vx, "vy": f.vy}

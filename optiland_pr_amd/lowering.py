@@ -23,6 +23,7 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from . import _abi
+from .apertures import RadialAperture, program_depth
 from .geometries import NewtonRaphsonGeometry, ZernikePolynomialGeometry, scalar
 from .surfaces import ObjectSurface
 
@@ -116,6 +117,7 @@ def lower_surface_group(surface_group, wavelengths, record=False, skip_object=Tr
 
     table = np.zeros(len(surfs), dtype=_abi.SURFACE)
     ops, coef, zern = [], [], []
+    ap_progs = []
     for si, s in enumerate(surfs):
         g = s.geometry
         R, k, tol, max_iter, norm_radius, cc = g.lower_params()
@@ -133,9 +135,16 @@ def lower_surface_group(surface_group, wavelengths, record=False, skip_object=Tr
             if np.isinf(R):
                 flags |= _abi.SURF_RADIUS_INF
         if s.aperture is not None:
-            flags |= _abi.SURF_APERTURE
-            row["ap_rmax2"] = s.aperture.r_max**2  # radial.py:62
-            row["ap_rmin2"] = s.aperture.r_min**2
+            if type(s.aperture) is RadialAperture:  # dedicated radial test
+                flags |= _abi.SURF_APERTURE
+                row["ap_rmax2"] = s.aperture.r_max**2  # radial.py:62
+                row["ap_rmin2"] = s.aperture.r_min**2
+            else:  # any other aperture: a postfix program in coef
+                prog = [float(v) for v in s.aperture.program()]
+                if program_depth(prog) > 32:
+                    raise ValueError("aperture expression nests too deeply (32 levels)")
+                flags |= _abi.SURF_APERTURE_PROG
+                ap_progs.append((si, prog))
         if si in rec_set:
             flags |= _abi.SURF_RECORD
             row["rec_slot"] = rec_set.index(si)
@@ -174,6 +183,11 @@ def lower_surface_group(surface_group, wavelengths, record=False, skip_object=Tr
         ops.extend(glob)
         if not loc and not glob:
             row["flags"] = int(row["flags"]) | _abi.SURF_TRANSLATE
+
+    for si, prog in ap_progs:  # after every geometry block (coef offsets fixed above)
+        table[si]["ap_off"] = len(coef)
+        table[si]["ap_len"] = len(prog)
+        coef.extend(prog)
 
     final = surfs[-1]
     final_mat = mat_id(final.material_post)

@@ -166,6 +166,33 @@ class CookeTripletApertures(CookeTriplet):
         self.surface_group.surfaces[5].aperture = RadialAperture(r_max=8.0, r_min=0.4)
 
 
+STAR = (np.array([4.2, 1.3, 1.2, -3.4, -1.9, -3.3, 1.4, 1.1]),
+        np.array([0.1, 1.2, 4.0, 2.6, -0.3, -3.1, -1.5, -4.1]))  # concave polygon
+
+
+class CookeTripletShapes(CookeTriplet):
+    """CookeTriplet with every non-radial aperture kind: rectangular (s1), offset ellipse
+    (s2), offset annulus (s3), a concave polygon on the stop (s4) and (rectangle |
+    ellipse) minus an offset central obscuration (s6)."""
+
+    def __init__(self):
+        from .apertures import (
+            EllipticalAperture,
+            OffsetRadialAperture,
+            PolygonAperture,
+            RectangularAperture,
+        )
+
+        super().__init__()
+        sg = self.surface_group.surfaces
+        sg[1].aperture = RectangularAperture(-5.5, 5.0, -4.8, 5.2)
+        sg[2].aperture = EllipticalAperture(5.5, 4.6, 0.2, -0.1)
+        sg[3].aperture = OffsetRadialAperture(4.6, 0.3, 0.1, -0.2)
+        sg[4].aperture = PolygonAperture(*STAR)
+        sg[6].aperture = ((RectangularAperture(-6, 6, -2.5, 2.5) | EllipticalAperture(3.5, 6.5))
+                          - OffsetRadialAperture(0.6, 0, 0.1, 0.0))
+
+
 class DecenteredTriplet(Optic):
     """Cooke-like triplet with a tilted/decentred element (rotate_x/y/z coverage)."""
 
@@ -273,6 +300,7 @@ GOLDEN_LENSES = {
     "tma_standard": lambda: ThreeMirrorAnastigmat("standard"),
     "tma_noll": lambda: ThreeMirrorAnastigmat("noll"),
     "cooke_aperture": CookeTripletApertures,
+    "cooke_shapes": CookeTripletShapes,
     "decentered": DecenteredTriplet,
     "freeform": FreeformTriplet,
     "cooke_pih": CookeTripletImageHeight,

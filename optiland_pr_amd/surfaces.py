@@ -15,6 +15,7 @@ from __future__ import annotations
 import numpy as np
 
 from .coordinate_system import CoordinateSystem
+from .apertures import BaseAperture, RadialAperture  # noqa: F401 (re-export)
 from .geometries import (
     BiconicGeometry,
     ChebyshevPolynomialGeometry,
@@ -39,29 +40,17 @@ def _torch_or_none():
         return None
 
 
-class RadialAperture:
-    """physical_apertures/radial.py:24-90: clip (i = 0) outside r_min <= r <= r_max."""
-
-    def __init__(self, r_max, r_min=0):
-        self.r_max = float(r_max)
-        self.r_min = float(r_min)
-
-    def scale(self, scale_factor):
-        self.r_max = self.r_max * scale_factor
-        self.r_min = self.r_min * scale_factor
-
-
 def configure_aperture(aperture):
-    """physical_apertures/radial.py:9-22."""
+    """physical_apertures/radial.py:16-28: a number is a diameter (RadialAperture of half
+    of it), an aperture object is used as is."""
     if aperture is None:
         return None
-    if isinstance(aperture, (int, float)):
+    if isinstance(aperture, (int, float)) and not isinstance(aperture, bool):
         return RadialAperture(r_max=aperture / 2)
-    if isinstance(aperture, RadialAperture):
+    if isinstance(aperture, BaseAperture):
         return aperture
     raise ValueError(
-        f"Invalid `aperture` provided: {aperture}. Only radial apertures are lowered "
-        "to the MI355X trace core."
+        f"Invalid `aperture` provided: {aperture}. Must be scalar or of type `BaseAperture`."
     )
 
 

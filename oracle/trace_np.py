@@ -625,6 +625,60 @@ class TraceResult:
         self.newton_updates = newton_updates  # {surface index: updates}
 
 
+def polygon_contains(vx, vy, x, y):
+    """matplotlib Path.contains_points (the reference's numpy-backend
+    path_contains_points, backend/numpy_backend.py:139-142): even-odd crossings of the
+    implicitly closed polygon, per edge v0 -> v1 toggling when the edge straddles the
+    horizontal through the point and
+    ((vy1 - y) * (vx0 - vx1) >= (vx1 - x) * (vy0 - vy1)) == (vy1 >= y)."""
+    inside = np.zeros(np.shape(x), dtype=bool)
+    n = len(vx)
+    for k in range(n):
+        vx0, vy0 = vx[k - 1], vy[k - 1]
+        vx1, vy1 = vx[k], vy[k]
+        yf0, yf1 = vy0 >= y, vy1 >= y
+        hit = (yf0 != yf1) & (((vy1 - y) * (vx0 - vx1) >= (vx1 - x) * (vy0 - vy1)) == yf1)
+        inside ^= hit
+    return inside & np.isfinite(x) & np.isfinite(y)
+
+
+def aperture_contains(prog, x, y):
+    """Evaluate a lowered aperture program (include/optiland_rt.h ort_aperture_op) with
+    the reference's per-class contains() expressions: radial.py:54-63,
+    offset_radial.py:46-58, elliptical.py:40-55, rectangular.py:40-60, polygon.py:50-66,
+    base.py:255-340 (union / intersection / difference)."""
+    stack = []
+    q = 0
+    while q < len(prog):
+        op = int(prog[q])
+        if op == _abi.AP_RADIAL:
+            rmin2, rmax2, ox, oy = (float(v) for v in prog[q + 1:q + 5])
+            radius2 = (x - ox) ** 2 + (y - oy) ** 2
+            stack.append((radius2 <= rmax2) & (radius2 >= rmin2))
+            q += 5
+        elif op == _abi.AP_ELLIPSE:
+            ox, oy, a2, b2 = (float(v) for v in prog[q + 1:q + 5])
+            xx, yy = x - ox, y - oy
+            stack.append((xx**2 / a2 + yy**2 / b2) <= 1)
+            q += 5
+        elif op == _abi.AP_RECT:
+            x0, x1, y0, y1 = (float(v) for v in prog[q + 1:q + 5])
+            stack.append((x0 <= x) & (x <= x1) & (y0 <= y) & (y <= y1))
+            q += 5
+        elif op == _abi.AP_POLYGON:
+            n = int(prog[q + 1])
+            v = np.asarray(prog[q + 2:q + 2 + 2 * n], dtype=np.float64).reshape(n, 2)
+            stack.append(polygon_contains(v[:, 0], v[:, 1], x, y))
+            q += 2 + 2 * n
+        else:
+            b = stack.pop()
+            a = stack.pop()
+            stack.append(a | b if op == _abi.AP_UNION else
+                         (a & b if op == _abi.AP_INTERSECT else a & ~b))
+            q += 1
+    return stack[-1]
+
+
 def trace_segment(table, rays: Rays, lam: int, record=False, sched=None, start=0):
     """One reference trace call: SurfaceGroup.trace (surface_group.py:232-244) over the
     traced surfaces, then the image-space propagate (real_ray_tracer.py:84-89).
@@ -656,6 +710,10 @@ def trace_segment(table, rays: Rays, lam: int, record=False, sched=None, start=0
         if flags & _abi.SURF_APERTURE:  # radial.py:50-63 + real_rays.py:132-139
             radius2 = r.x**2 + r.y**2
             inside = (radius2 <= float(s["ap_rmax2"])) & (radius2 >= float(s["ap_rmin2"]))
+            r.i = np.where(~inside, np.zeros_like(r.i), r.i)
+        if flags & _abi.SURF_APERTURE_PROG:  # physical_apertures/*.py contains + clip
+            off, ln = int(s["ap_off"]), int(s["ap_len"])
+            inside = aperture_contains(table.coef[off:off + ln], r.x, r.y)
             r.i = np.where(~inside, np.zeros_like(r.i), r.i)
         nx, ny, nz = surface_normal(r, table, s)
         if flags & _abi.SURF_REFLECTIVE:

@@ -39,7 +39,7 @@ def native_case(name, meta, record=False):
 
 # golden cases whose every traced surface is closed-form (plane / conic): the oracle and
 # the HIP kernel reproduce the reference bit for bit there
-CLOSED_FORM = ("cooke", "dg", "rt", "cooke_aperture", "decentered", "json_cooke",
+CLOSED_FORM = ("cooke", "dg", "rt", "cooke_aperture", "cooke_shapes", "decentered", "json_cooke",
                "json_heliar", "json_rt", "cooke_pih", "finite_pih")
 NEWTON = ("rt_asph", "rt_odd", "tma_fringe", "tma_standard", "tma_noll", "freeform")
 ALL_CASES = CLOSED_FORM + NEWTON

@@ -148,6 +148,32 @@ def cooke_aperture():
     return lens
 
 
+STAR = (np.array([4.2, 1.3, 1.2, -3.4, -1.9, -3.3, 1.4, 1.1]),
+        np.array([0.1, 1.2, 4.0, 2.6, -0.3, -3.1, -1.5, -4.1]))  # concave polygon
+
+
+def cooke_shapes():
+    """Cooke triplet with every non-radial aperture kind (physical_apertures/*.py):
+    rectangular (s1), elliptical with offset (s2), offset annulus (s3), a concave polygon
+    on the stop (s4) and (rectangle | ellipse) minus an offset central obscuration (s6)."""
+    from optiland.physical_apertures import (
+        EllipticalAperture,
+        OffsetRadialAperture,
+        PolygonAperture,
+        RectangularAperture,
+    )
+
+    lens = CookeTriplet()
+    sg = lens.surface_group.surfaces
+    sg[1].aperture = RectangularAperture(-5.5, 5.0, -4.8, 5.2)
+    sg[2].aperture = EllipticalAperture(5.5, 4.6, 0.2, -0.1)
+    sg[3].aperture = OffsetRadialAperture(4.6, 0.3, 0.1, -0.2)
+    sg[4].aperture = PolygonAperture(*STAR)
+    sg[6].aperture = ((RectangularAperture(-6, 6, -2.5, 2.5) | EllipticalAperture(3.5, 6.5))
+                      - OffsetRadialAperture(0.6, 0, 0.1, 0.0))
+    return lens
+
+
 def decentered():
     """Cooke triplet with a tilted + decentred second element and an ry/rz tilt chain,
     covering coordinate_system.py:73-107 rotate_x/y/z + translate on refracting surfaces."""
@@ -259,6 +285,7 @@ CASES = {
     "tma_standard": (lambda: tma("standard"), [(0, 0), (0, 1)], [0.587], "uniform", 24),
     "tma_noll": (lambda: tma("noll"), [(0, 1)], [0.587], "uniform", 24),
     "cooke_aperture": (cooke_aperture, [(0, 0), (0, 1)], [0.55], "uniform", 32),
+    "cooke_shapes": (cooke_shapes, [(0, 0), (0, 1), (0.4, -0.6)], [0.55], "uniform", 32),
     "decentered": (decentered, [(0, 0), (0, 1), (0.5, -0.5)], [0.55], "hexapolar", 8),
     "freeform": (freeform, [(0, 0), (0, 1), (0.5, 0.7)], [0.48, 0.55, 0.65], "uniform", 24),
     "json_cooke": (json_lens("cooke_triplet"), [(0, 0), (0, 1)], [0.55], "uniform", 24),
@@ -475,6 +502,47 @@ DIST_CASES = [("random", 1000, {"seed": 7}), ("uniform", 33, {}), ("uniform", 12
               ("positive_line_y", 10, {}), ("cross", 21, {}), ("cross", 20, {})]
 
 
+def aperture_goldens():
+    """contains(x, y) of every reference aperture kind on 6000 points (random, a grid
+    through the vertices, the vertices themselves) -> tests/golden/apertures.npz, with
+    the apertures' to_dict() in apertures.json."""
+    from optiland.physical_apertures import (
+        EllipticalAperture,
+        OffsetRadialAperture,
+        PolygonAperture,
+        RadialAperture,
+        RectangularAperture,
+    )
+
+    aps = {
+        "radial": RadialAperture(3.0, 0.5),
+        "offset_radial": OffsetRadialAperture(2.5, 0.4, 0.7, -0.3),
+        "ellipse": EllipticalAperture(3.5, 2.0, -0.4, 0.6),
+        "rect": RectangularAperture(-2.0, 3.0, -1.5, 2.5),
+        "polygon": PolygonAperture(*STAR),
+        "union": RectangularAperture(-2.0, 3.0, -1.5, 2.5) | EllipticalAperture(3.5, 2.0),
+        "intersection": RadialAperture(3.0) & PolygonAperture(*STAR),
+        "difference": RectangularAperture(-2.0, 3.0, -1.5, 2.5) - OffsetRadialAperture(1.0, 0, 0.5, 0.5),
+        "nested": ((RectangularAperture(-4, 4, -1, 1) + EllipticalAperture(1.5, 4.0))
+                   - RadialAperture(0.8)) & PolygonAperture(*STAR),
+    }
+    rng = np.random.default_rng(17)
+    pts = [rng.uniform(-5, 5, size=(5000, 2))]
+    g = np.linspace(-5, 5, 21)
+    gx, gy = np.meshgrid(g, g)
+    pts.append(np.column_stack((gx.ravel(), gy.ravel())))
+    pts.append(np.column_stack(STAR))
+    pts = np.concatenate(pts)
+    out = {"x": pts[:, 0].copy(), "y": pts[:, 1].copy()}
+    dicts = {}
+    for name, ap in aps.items():
+        out[name] = np.asarray(ap.contains(out["x"], out["y"]), dtype=bool)
+        dicts[name] = json.loads(json.dumps(ap.to_dict(), default=lambda o: np.asarray(o).tolist()))
+    np.savez_compressed(os.path.join(HERE, "apertures.npz"), **out)
+    with open(os.path.join(HERE, "apertures.json"), "w") as f:
+        json.dump(dicts, f, indent=1)
+
+
 def distribution_goldens():
     """Pupil samples of every reference distribution (distribution.py:72-408), incl.
     GaussianQuadrature (not in create_distribution) -> tests/golden/distributions.npz."""
@@ -502,6 +570,9 @@ def main():
     if "--distributions" in sys.argv:
         distribution_goldens()
         return
+    if "--apertures" in sys.argv:
+        aperture_goldens()
+        return
     if "--glasses" in sys.argv:  # re-bake optiland_pr_amd/data/glasses.json only
         glass_table()
         return
@@ -523,6 +594,7 @@ def main():
         print(f"{name}: {index[name]['n_pupil']} pupil pts, {time.perf_counter() - t0:.2f}s",
               file=sys.stderr)
     distribution_goldens()
+    aperture_goldens()
     index["_analysis"] = analysis_goldens()
     index["_full"] = full_size_summaries()
     with open(os.path.join(HERE, "index.json"), "w") as f:

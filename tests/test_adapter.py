@@ -47,7 +47,8 @@ def test_reference_lowering_equals_native(ref, name, wls):
     assert a.final_mat == b.final_mat and a.final_thickness == b.final_thickness
 
 
-@pytest.mark.parametrize("name", ["freeform", "tma_fringe", "rt_asph"])
+@pytest.mark.parametrize("name", ["freeform", "tma_fringe", "rt_asph", "cooke_shapes",
+                                  "cooke_aperture"])
 def test_reference_lowering_equals_native_newton(ref, name):
     """Newton geometries (incl. the freeform kinds): the adapter's lowering of the
     reference lens equals the native lens's bytes, coefficient blocks included."""
