@@ -107,7 +107,7 @@ typedef struct ort_surface {
   int32_t ap_len;     /* its length in doubles                                       */
 } ort_surface; /* 128 bytes */
 
-/* Aperture programs (physical_apertures/*.py): postfix, each op a double opcode followed
+/* Aperture programs (the physical_apertures package): postfix, each op a double opcode followed
  * by its operands; primitives push contains(x, y) of the ray's local (x, y), the boolean
  * ops pop two and push one; a ray is clipped (i = 0, real_rays.py:132-139) when the
  * final value is false.

@@ -198,7 +198,10 @@ def vjp_mode(table):
     if env in ("unrolled", "adjoint"):
         return _abi.VJP_UNROLLED if env == "unrolled" else _abi.VJP_ADJOINT
     z = table.zern
-    if len(z) and np.any((z["c"] != 0.0) & (z["norm"] != 1.0)):
+    live = z["c"] != 0.0
+    for off, t in getattr(table, "device_coeffs", ()):  # values not on the host
+        live[off:off + int(t.numel())] = True
+    if len(z) and np.any(live & (z["norm"] != 1.0)):
         return _abi.VJP_UNROLLED
     return _abi.VJP_ADJOINT
 

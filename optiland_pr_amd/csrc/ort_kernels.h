@@ -290,7 +290,9 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(const KArgs a) {
       ort::propagate(r, t, alpha);
       ort::add_opd(r, t, n_pre);
       if (s.flags & ORT_SURF_APERTURE) ort::clip_radial(r, s.ap_rmax2, s.ap_rmin2);
+#ifndef ORT_NO_AP_PROG
       if (s.flags & ORT_SURF_APERTURE_PROG) ort::clip_program(r, cst(a.coef) + s.ap_off, s.ap_len);
+#endif
       double nx, ny, nz;
       if (s.geometry == ORT_GEOM_PLANE) {
         nx = 0.0; ny = 0.0; nz = 1.0;
@@ -378,7 +380,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
     ort::propagate(r, t, o.alpha_pre);
     ort::add_opd(r, t, o.n_pre);
     if (s.flags & ORT_SURF_APERTURE) ort::clip_radial(r, s.ap_rmax2, s.ap_rmin2);
+#ifndef ORT_NO_AP_PROG
     if (s.flags & ORT_SURF_APERTURE_PROG) ort::clip_program(r, cst(a.coef) + s.ap_off, s.ap_len);
+#endif
     double nx, ny, nz;
     if (is_plane) {
       nx = 0.0; ny = 0.0; nz = 1.0;

@@ -244,12 +244,16 @@ class ZernikePolynomialGeometry(NewtonRaphsonGeometry):
         return (scalar(self.radius), scalar(self.k), self.tol, self.max_iter,
                 self.norm_radius, [])
 
-    def zernike_terms(self):
-        """-> list of (c, norm, n, m, a_k list, d_k list) in coefficient order."""
+    def zernike_terms(self, values=True):
+        """-> list of (c, norm, n, m, a_k list, d_k list) in coefficient order; with
+        values=False the coefficients are left as 0 placeholders (not read)."""
         coeffs = self.coefficients
-        if hasattr(coeffs, "detach"):  # torch tensor (autograd leaf, autodiff.py)
+        n_c = int(coeffs.numel()) if hasattr(coeffs, "numel") else len(coeffs)
+        if not values:
+            coeffs = np.zeros(n_c)
+        elif hasattr(coeffs, "detach"):  # torch tensor (autograd leaf, autodiff.py)
             coeffs = coeffs.detach().cpu().numpy()
-        idx = zernike_indices(self.zernike_type, len(coeffs))
+        idx = zernike_indices(self.zernike_type, n_c)
         out = []
         for (n, m), c in zip(idx, coeffs, strict=True):
             a, d = radial_coefficients(n, abs(m))

@@ -42,6 +42,11 @@ class LensTable:
     materials: list = field(default_factory=list)
     n_rec: int = 0
     rec_surfaces: list = field(default_factory=list)  # traced-surface indices recorded
+    # Zernike coefficients held in device tensors: (first zern row, tensor). Their rows
+    # carry c = 0 placeholders here (the table structure does not depend on the values)
+    # and the uploaded table is patched on the device (raytrace.lens_for), so an
+    # optimisation loop over device-resident coefficients never waits on the GPU.
+    device_coeffs: list = field(default_factory=list)
 
     @property
     def n_surfaces(self):
@@ -88,6 +93,10 @@ class LensTable:
         return b"".join(parts)
 
 
+def _device_tensor(v):
+    return hasattr(v, "is_cuda") and bool(v.is_cuda)
+
+
 def lower_surface_group(surface_group, wavelengths, record=False, skip_object=True):
     """Lower every traced surface (index >= 1) of `surface_group`.
 
@@ -118,6 +127,7 @@ def lower_surface_group(surface_group, wavelengths, record=False, skip_object=Tr
     table = np.zeros(len(surfs), dtype=_abi.SURFACE)
     ops, coef, zern = [], [], []
     ap_progs = []
+    device_coeffs = []
     for si, s in enumerate(surfs):
         g = s.geometry
         R, k, tol, max_iter, norm_radius, cc = g.lower_params()
@@ -152,7 +162,10 @@ def lower_surface_group(surface_group, wavelengths, record=False, skip_object=Tr
             row["rec_slot"] = -1
         row["flags"] = flags
         if isinstance(g, ZernikePolynomialGeometry):
-            terms = g.zernike_terms()
+            on_device = _device_tensor(g.coefficients)
+            terms = g.zernike_terms(values=not on_device)
+            if on_device:
+                device_coeffs.append((len(zern), g.coefficients))
             row["coef_off"] = len(zern)
             row["n_coef"] = len(terms)
             for (c, norm, n, m, a, d) in terms:
@@ -221,6 +234,7 @@ def lower_surface_group(surface_group, wavelengths, record=False, skip_object=Tr
         materials=mats,
         n_rec=len(rec_set),
         rec_surfaces=rec_set,
+        device_coeffs=device_coeffs,
     )
 
 

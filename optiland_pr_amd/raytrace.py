@@ -143,6 +143,15 @@ class DeviceLens:
         self.newton = table.newton_surfaces
         self.sched_cache: dict = {}
 
+    def patch_coefficients(self, device_coeffs):
+        """Write device-resident Zernike coefficients into the uploaded term table
+        (ort_zernike_term.c, the first double of each 32-byte row): a device-to-device
+        copy ordered on the current stream, no host round trip."""
+        rows = self.zern.view(torch.float64).view(-1, _abi.ZERNIKE_TERM.itemsize // 8)
+        for off, t in device_coeffs:
+            v = t.detach().reshape(-1).to(device=self.device, dtype=torch.float64)
+            rows[off:off + v.numel(), 0].copy_(v)
+
     # -- Newton schedule speculate / verify ---------------------------------------------
     def initial_schedule(self, keys):
         S = self.table.n_surfaces
@@ -218,6 +227,8 @@ def lens_for(optic_or_group, wavelengths, record=False, image_record=False):
             # an edited lens starts from the previous Newton schedules (verified anyway)
             hit.sched_cache = old.sched_cache
         cache[key] = hit
+    if table.device_coeffs:
+        hit.patch_coefficients(table.device_coeffs)
     return hit
 
 
