@@ -5,8 +5,9 @@
   * the rays are RealRays (not Paraxial/Polarized) held as torch float64 tensors on the
     HIP device (be.set_backend("torch"); be.set_device("cuda"); be.set_precision("float64")),
   * every traced surface is lowerable (plane / standard / even / odd asphere / Zernike /
-    XY-polynomial / Chebyshev / biconic / toroidal geometry, refractive-reflective interaction without coating or BSDF, radial or no
-    aperture, homogeneous propagation),
+    XY-polynomial / Chebyshev / biconic / toroidal geometry, refractive-reflective interaction without coating or BSDF, any physical
+    aperture (radial, offset, elliptical, rectangular, polygon, file, boolean
+    combinations) or none, homogeneous propagation),
   * autograd is not requested on the ray tensors.
 Otherwise the original Python loop runs unchanged. The rays are traced IN PLACE (the
 reference mutates its RealRays) and every surface's record (_record,
