@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define ORT_ABI_VERSION 6
+#define ORT_ABI_VERSION 7
 #define ORT_MAX_SURFACES 64
 
 /* ---- geometry kinds ----------------------------------- */
@@ -41,7 +41,9 @@ enum ort_geometry { /* see optiland/geometries */
   ORT_GEOM_POLYNOMIAL = 5,   /* polynomial.py:93-140 (XY polynomial)               */
   ORT_GEOM_CHEBYSHEV = 6,    /* chebyshev.py:104-215                               */
   ORT_GEOM_BICONIC = 7,      /* biconic.py:69-158                                  */
-  ORT_GEOM_TOROIDAL = 8      /* toroidal.py:75-233                                 */
+  ORT_GEOM_TOROIDAL = 8,     /* toroidal.py:75-233                                 */
+  ORT_GEOM_FORBES_QBFS = 9,  /* forbes/geometry.py:183-330 + forbes/qpoly.py       */
+  ORT_GEOM_FORBES_Q2D = 10   /* forbes/geometry.py:333-640 + forbes/qpoly.py       */
 };
 /* Coefficient blocks in lens.coef at ort_surface.coef_off (n_coef doubles):
  *   EVEN / ODD_ASPHERE  C_0 .. C_{n-1}
@@ -51,6 +53,12 @@ enum ort_geometry { /* see optiland/geometries */
  *                       ort_surface.radius / conic = R_x / k_x (the Newton start guess)
  *   TOROIDAL            R_rot, c_yz, k_yz, has_yz (0/1), n_poly, alpha_1 .. alpha_n;
  *                       ort_surface.radius = R_yz, conic = 0 (the Newton start guess)
+ *   FORBES_QBFS         norm_radius, L, dep_normal (0 when every coefficient is 0),
+ *                       b_0 .. b_{L-1} (orthonormal P_n coefficients)
+ *   FORBES_Q2D          norm_radius, vertex dz/dx, vertex dz/dy, L0, b_0 .. b_{L0-1}
+ *                       (m = 0 part, as FORBES_QBFS), M, then for m = 1 .. M two
+ *                       Clenshaw records (cosine, then sine): L, d_0 .. d_{L-1},
+ *                       A_0 .. A_{L-1}, B_0 .. B_{L-1}, C_0 .. C_{L-1} (L = 0: no terms)
  * ZERNIKE uses lens.zern[coef_off .. coef_off + n_coef) instead. */
 
 /* ---- surface flags ------------------------------------------------------------ */

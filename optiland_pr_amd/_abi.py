@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import numpy as np
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 VJP_UNROLLED = 0
 VJP_ADJOINT = 1
 AP_RADIAL = 1
@@ -38,7 +38,10 @@ GEOM_POLYNOMIAL = 5
 GEOM_CHEBYSHEV = 6
 GEOM_BICONIC = 7
 GEOM_TOROIDAL = 8
-FREEFORM_GEOMETRIES = (GEOM_POLYNOMIAL, GEOM_CHEBYSHEV, GEOM_BICONIC, GEOM_TOROIDAL)
+GEOM_FORBES_QBFS = 9
+GEOM_FORBES_Q2D = 10
+FREEFORM_GEOMETRIES = (GEOM_POLYNOMIAL, GEOM_CHEBYSHEV, GEOM_BICONIC, GEOM_TOROIDAL,
+                       GEOM_FORBES_QBFS, GEOM_FORBES_Q2D)
 NEWTON_GEOMETRIES = (GEOM_EVEN_ASPHERE, GEOM_ODD_ASPHERE, GEOM_ZERNIKE) + FREEFORM_GEOMETRIES
 
 # enum ort_surface_flags

@@ -5,7 +5,7 @@
   * the rays are RealRays (not Paraxial/Polarized) held as torch float64 tensors on the
     HIP device (be.set_backend("torch"); be.set_device("cuda"); be.set_precision("float64")),
   * every traced surface is lowerable (plane / standard / even / odd asphere / Zernike /
-    XY-polynomial / Chebyshev / biconic / toroidal geometry, refractive-reflective interaction without coating or BSDF, any physical
+    XY-polynomial / Chebyshev / biconic / toroidal / Forbes Q-bfs / Q-2D geometry, refractive-reflective interaction without coating or BSDF, any physical
     aperture (radial, offset, elliptical, rectangular, polygon, file, boolean
     combinations) or none, homogeneous propagation),
   * autograd is not requested on the ray tensors.
@@ -26,6 +26,10 @@ from .geometries import (
     BiconicGeometry,
     ChebyshevPolynomialGeometry,
     EvenAsphere,
+    ForbesQ2dGeometry,
+    ForbesQbfsGeometry,
+    ForbesSolverConfig,
+    ForbesSurfaceConfig,
     OddAsphere,
     Plane,
     PolynomialGeometry,
@@ -119,6 +123,13 @@ def _geometry(g):
         return ToroidalGeometry(cs, _f(g.R_rot), _f(g.R_yz), _f(g.k_yz),
                                 [float(v) for v in np.ravel(_np(g.coeffs_poly_y))],
                                 g.tol, g.max_iter)
+    if name in ("ForbesQbfsGeometry", "ForbesQ2dGeometry"):
+        terms = g.radial_terms if name == "ForbesQbfsGeometry" else g.freeform_coeffs
+        cfg = ForbesSurfaceConfig(radius=_f(g.radius), conic=_f(g.k),
+                                  norm_radius=_f(g.norm_radius),
+                                  terms={k: _f(v) for k, v in terms.items()})
+        cls = ForbesQbfsGeometry if name == "ForbesQbfsGeometry" else ForbesQ2dGeometry
+        return cls(cs, cfg, ForbesSolverConfig(tol=g.tol, max_iter=g.max_iter))
     raise Unsupported(name)
 
 

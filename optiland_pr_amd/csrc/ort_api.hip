@@ -74,7 +74,8 @@ int fill_args(KArgs& a, const ort_lens* lens, const ort_batch* batch, const ort_
   if (lens->geometry_mask & (1u << ORT_GEOM_ODD_ASPHERE)) feat |= ort::KM_ODD;
   if (lens->geometry_mask & (1u << ORT_GEOM_ZERNIKE)) feat |= ort::KM_ZERN;
   if (lens->geometry_mask & ((1u << ORT_GEOM_POLYNOMIAL) | (1u << ORT_GEOM_CHEBYSHEV) |
-                             (1u << ORT_GEOM_BICONIC) | (1u << ORT_GEOM_TOROIDAL)))
+                             (1u << ORT_GEOM_BICONIC) | (1u << ORT_GEOM_TOROIDAL) |
+                             (1u << ORT_GEOM_FORBES_QBFS) | (1u << ORT_GEOM_FORBES_Q2D)))
     feat |= ort::KM_FREE;
   if (rec) feat |= F_REC;
   if (lens->n_lambda == 1) feat |= F_MONO;

@@ -1014,10 +1014,286 @@ ORT_INLINE void zernike_coef_adjoint(double x, double y, double Rn, PZ Tm, int t
   }
 }
 
+// ---- Forbes Q-polynomials: forbes/geometry.py:83-640 + forbes/qpoly.py --------------
+// The lens-only constants (orthonormal-basis coefficients, recurrence A/B/C, the Q-2D
+// vertex slope) come precomputed in the coefficient block (optiland_pr_amd/forbes.py);
+// the per-ray work is the Clenshaw recurrences below, in the reference's operation
+// order. Integer powers u^3.. are products (the reference's libm pow: ulp-level).
+
+// forbes/geometry.py:115-131 (_base_sag)
+template <class T, class S>
+ORT_INLINE T forbes_base_sag(const T& r2, const S& R, const S& k, bool rinf) {
+  if (rinf) return T(0.0);
+  const T a = 1.0 - (1.0 + k) * r2 / (R * R);
+  const T sa = vv(a) < 0.0 ? T(0.0) : a;
+  return r2 / (R * (1.0 + sqrt(sa)));
+}
+
+// forbes/geometry.py:133-150 (_base_sag_derivative: d z_base / d rho)
+template <class T, class S>
+ORT_INLINE T forbes_base_dsag(const T& rho, const T& r2, const S& R, const S& k, bool rinf) {
+  if (rinf || vv(R) == 0.0) return T(0.0);
+  const S c = 1.0 / R;
+  const T a = 1.0 - (k + 1.0) * (c * c) * r2;
+  const T sa = sqrt(vv(a) > 0.0 ? a : T(1e-12));
+  return c * rho / sa;
+}
+
+// forbes/geometry.py:152-180 (_conic_correction_factor and its d/d rho)
+template <class T, class S>
+ORT_INLINE void forbes_conic_factor(const T& r2, const S& R, const S& k, bool rinf, T& f,
+                                    T& df) {
+  if (rinf) {
+    f = T(1.0);
+    df = T(0.0);
+    return;
+  }
+  const S c = 1.0 / R;
+  const S c2 = c * c;
+  const T rho = sqrt(r2);
+  const T na = 1.0 - k * c2 * r2;
+  const T da = 1.0 - (k + 1.0) * c2 * r2;
+  const T Nn = sqrt(vv(na) > 0.0 ? na : T(1e-12));
+  const T Dd = sqrt(vv(da) > 0.0 ? da : T(1e-12));
+  f = Nn / Dd;
+  df = (c2 * rho) / (Nn * (Dd * Dd * Dd));
+}
+
+// Q-bfs Clenshaw over b_0..b_{L-1} at x = u^2 (qpoly.py:127-160): the sum
+// S = 2 (alpha_0 + alpha_1); with want_d also dS/dx from the j = 1 recurrence
+// (qpoly.py:163-192), both in one downward pass.
+template <class T, class PD>
+ORT_INLINE void qbfs_clenshaw(PD b, int L, const T& usq, bool want_d, T& s, T& ds) {
+  if (L <= 0) {
+    s = T(0.0);
+    ds = T(0.0);
+    return;
+  }
+  const int M = L - 1;
+  const T p = 2.0 - 4.0 * usq;
+  T a1 = T(0.0), a2 = T(0.0), d1 = T(0.0), d2 = T(0.0);  // alpha_{i+1}, alpha_{i+2}
+#pragma unroll 1
+  for (int i = M; i >= 0; --i) {
+    T ai, di = T(0.0);
+    if (i == M) {
+      ai = T(b[i]);
+    } else if (i == M - 1) {
+      ai = b[i] + p * a1;
+      if (want_d) di = -4.0 * a1;
+    } else {
+      ai = b[i] + p * a1 - a2;
+      if (want_d) di = (i == M - 2) ? p * d1 - 4.0 * a1 : p * d1 - d2 - 4.0 * a1;
+    }
+    a2 = a1;
+    a1 = ai;
+    d2 = d1;
+    d1 = di;
+  }
+  s = M > 0 ? 2.0 * (a1 + a2) : 2.0 * a1;
+  ds = M > 0 ? 2.0 * (d1 + d2) : 2.0 * d1;
+}
+
+// One Q-2D azimuthal order (qpoly.py:389-430 sum, :443-466 d/d(u^2)): record
+// L, d[L], A[L], B[L], C[L]; q2d_sum_from_alphas (qpoly.py:389-398) on both.
+template <class T, class PD>
+ORT_INLINE void q2d_clenshaw(PD rec, int m, const T& usq, bool want_d, T& s, T& ds) {
+  const int L = (int)rec[0];
+  if (L <= 0) {
+    s = T(0.0);
+    ds = T(0.0);
+    return;
+  }
+  const PD D = rec + 1;
+  const PD A = D + L;
+  const PD Bc = A + L;
+  const PD C = Bc + L;
+  const int top = L - 1;
+  T a1 = T(0.0), a2 = T(0.0), d1 = T(0.0), d2 = T(0.0), a3 = T(0.0), d3 = T(0.0);
+#pragma unroll 1
+  for (int n = top; n >= 0; --n) {
+    T an, dn = T(0.0);
+    if (n == top) {
+      an = T(D[n]);
+    } else {
+      const T w = A[n] + Bc[n] * usq;
+      if (n == top - 1) {
+        an = D[n] + w * a1;
+        if (want_d) dn = Bc[n] * a1;
+      } else {
+        an = D[n] + w * a1 - C[n + 1] * a2;
+        if (want_d) dn = Bc[n] * a1 + w * d1 - C[n + 1] * d2;
+      }
+    }
+    if (n == 3) {
+      a3 = an;
+      d3 = dn;
+    }
+    a2 = a1;
+    a1 = an;
+    d2 = d1;
+    d1 = dn;
+  }
+  s = 0.5 * a1;
+  ds = 0.5 * d1;
+  if (m == 1 && top > 2) {
+    s = s - 0.4 * a3;
+    ds = ds - 0.4 * d3;
+  }
+}
+
+template <class PD>
+ORT_INLINE PD q2d_next(PD rec) {
+  const int L = (int)rec[0];
+  return rec + (L > 0 ? 1 + 4 * L : 1);
+}
+
+// forbes/geometry.py:243-266 (sag) and :296-327 (_surface_normal_analytical)
+template <class T, class S, class PD>
+ORT_INLINE T sagnorm_qbfs(const T& x, const T& y, const S& R, const S& k, bool rinf, PD B,
+                          bool want_normal, T& nx, T& ny, T& nz) {
+  const double nr = B[0];
+  const int L = (int)B[1];
+  const bool dep_normal = B[2] != 0.0;
+  const PD b = B + 3;
+  const T r2 = x * x + y * y;
+  const T usq = r2 / (nr * nr);
+  T ps, unused;
+  qbfs_clenshaw(b, L, usq, false, ps, unused);
+  T cf, dcf;
+  forbes_conic_factor(r2, R, k, rinf, cf, dcf);
+  const T dep = usq * (1.0 - usq) * cf * ps;
+  const T z = forbes_base_sag(r2, R, k, rinf) + (vv(usq) > 1.0 ? T(0.0) : dep);
+  if (want_normal) {
+    const T rho = sqrt(r2 + 1e-12);
+    T dfr = forbes_base_dsag(rho, r2, R, k, rinf);
+    if (dep_normal) {
+      const T u = rho / nr;
+      T pv, pd;
+      qbfs_clenshaw(b, L, u * u, true, pv, pd);
+      const T dpdu = pd * 2.0 * u;
+      const T dpre = (2.0 * u - 4.0 * (u * u * u)) / nr;
+      const T dpoly = dpdu / nr;
+      const T uu = u * u;
+      const T q = uu - uu * uu;
+      const T dd = dpre * cf * pv + q * dcf * pv + q * cf * dpoly;
+      dfr = dfr + (vv(u) >= 1.0 ? T(0.0) : dd);
+    }
+    const T dfx = dfr * (x / rho);
+    const T dfy = dfr * (y / rho);
+    const T mag = sqrt(dfx * dfx + dfy * dfy + 1.0);
+    const T sm = vv(mag) < 1e-12 ? T(1.0) : mag;
+    nx = dfx / sm;
+    ny = dfy / sm;
+    nz = -1.0 / sm;
+  }
+  return z;
+}
+
+// qpoly.py:469-520 (compute_z_zprime_q2d): the m = 0 Q-bfs part and the m > 0 orders at
+// (u, theta); c1 / s1 = cos / sin theta, cos / sin (m theta) by recurrence.
+template <class T, class PD>
+ORT_INLINE void q2d_sums(PD B, const T& u, const T& c1, const T& s1, bool want_d, T& p0,
+                         T& dp0, T& pg, T& dr, T& dt) {
+  const int L0 = (int)B[3];
+  const T usq = u * u;
+  T d0;
+  qbfs_clenshaw(B + 4, L0, usq, want_d, p0, d0);
+  dp0 = d0 * 2.0 * u;
+  PD rec = B + 4 + L0;
+  const int M = (int)rec[0];
+  ++rec;
+  pg = T(0.0);
+  dr = T(0.0);
+  dt = T(0.0);
+  T cm = c1, sm = s1;  // cos / sin (m theta)
+  T um = u;            // u ** m
+  T um1 = T(1.0);      // u ** (m - 1)
+#pragma unroll 1
+  for (int m = 1; m <= M; ++m) {
+    T sa, dsa, sb, dsb;
+    q2d_clenshaw(rec, m, usq, want_d, sa, dsa);
+    rec = q2d_next(rec);
+    q2d_clenshaw(rec, m, usq, want_d, sb, dsb);
+    rec = q2d_next(rec);
+    const T term = um * (cm * sa + sm * sb);
+    pg = m == 1 ? term : pg + term;
+    if (want_d) {
+      const T two_usq = 2.0 * usq;
+      const T at = cm * (two_usq * dsa + (double)m * sa);
+      const T bt = sm * (two_usq * dsb + (double)m * sb);
+      const T rt = um1 * (at + bt);
+      const T tt = (double)m * um * (-sa * sm + sb * cm);
+      dr = m == 1 ? rt : dr + rt;
+      dt = m == 1 ? tt : dt + tt;
+    }
+    const T cn = cm * c1 - sm * s1;
+    sm = sm * c1 + cm * s1;
+    cm = cn;
+    um1 = um;
+    um = um * u;
+  }
+}
+
+// forbes/geometry.py:420-450 (sag) and :545-610 (_surface_normal_analytical)
+template <class T, class S, class PD>
+ORT_INLINE T sagnorm_q2d(const T& x, const T& y, const S& R, const S& k, bool rinf, PD B,
+                         bool want_normal, T& nx, T& ny, T& nz) {
+  const double nr = B[0];
+  const T r2 = x * x + y * y;
+  const T rho0 = sqrt(r2);
+  T c1, s1;
+  polar_unit(x, y, rho0, c1, s1);  // theta = atan2(y, x)
+  T cf, dcf;
+  forbes_conic_factor(r2, R, k, rinf, cf, dcf);
+  T z;
+  {
+    const T u = sqrt(r2 + 1e-12) / nr;
+    T p0, dp0, pg, dr, dt;
+    q2d_sums(B, u, c1, s1, false, p0, dp0, pg, dr, dt);
+    const T uu = u * u;
+    const T total = uu * (1.0 - uu) * cf * p0 + cf * pg;
+    z = forbes_base_sag(r2, R, k, rinf) + (vv(u) > 1.0 ? T(0.0) : total);
+  }
+  if (want_normal) {
+    T dfx, dfy;
+    if (vv(rho0) < 1e-12) {  // the vertex: analytical slope of the m = 1 order
+      dfx = T(B[1]);
+      dfy = T(B[2]);
+    } else {
+      const T u = rho0 / nr;
+      T p0, dp0, pg, dr, dt;
+      q2d_sums(B, u, c1, s1, true, p0, dp0, pg, dr, dt);
+      const T dp0r = dp0 / nr;
+      const T drr = dr / nr;
+      const T uu = u * u;
+      const T dpre = (2.0 * u - 4.0 * (u * u * u)) / nr;
+      const T q = uu - uu * uu;
+      const T ds0 = (dpre * p0 + q * dp0r) * cf + q * p0 * dcf;
+      const T dsg = dcf * pg + cf * drr;
+      const bool out = vv(u) > 1.0;
+      const T dsr = out ? T(0.0) : ds0 + dsg;
+      const T dst = out ? T(0.0) : cf * dt;
+      const T ct = x / rho0, st = y / rho0;
+      const T dsx = ct * dsr - (st / rho0) * dst;
+      const T dsy = st * dsr + (ct / rho0) * dst;
+      const T dbr = forbes_base_dsag(rho0, r2, R, k, rinf);
+      dfx = dbr * ct + dsx;
+      dfy = dbr * st + dsy;
+    }
+    const T mag = sqrt(dfx * dfx + dfy * dfy + 1.0);
+    const T smg = vv(mag) < 1e-12 ? T(1.0) : mag;
+    nx = dfx / smg;
+    ny = dfy / smg;
+    nz = -1.0 / smg;
+  }
+  return z;
+}
+
 // Sag and normal of a Newton-iterated geometry (EvenAsphere / OddAsphere / Zernike).
 // KM is a bitmask of the Newton kinds compiled in (KM_EVEN | KM_ODD | KM_ZERN): a lens
 // only pays registers for the kinds it contains.
-// KM_FREE covers the freeform kinds (XY polynomial, Chebyshev, biconic, toroidal) with a
+// KM_FREE covers the freeform kinds (XY polynomial, Chebyshev, biconic, toroidal, Forbes
+// Q-bfs / Q-2D) with a
 // runtime switch.
 enum : unsigned { KM_EVEN = 1u, KM_ODD = 2u, KM_ZERN = 4u, KM_FREE = 8u };
 
@@ -1052,6 +1328,12 @@ ORT_INLINE T newton_sagnorm(const ort_surface& s, const S& R, const S& K, PD coe
       }
       case ORT_GEOM_BICONIC:
         return sagnorm_biconic(x, y, C, want_normal, nx, ny, nz);
+      case ORT_GEOM_FORBES_QBFS:
+        return sagnorm_qbfs(x, y, R, K, (s.flags & ORT_SURF_RADIUS_INF) != 0, C, want_normal,
+                            nx, ny, nz);
+      case ORT_GEOM_FORBES_Q2D:
+        return sagnorm_q2d(x, y, R, K, (s.flags & ORT_SURF_RADIUS_INF) != 0, C, want_normal,
+                           nx, ny, nz);
       default:
         return sagnorm_toroidal(x, y, C, want_normal, nx, ny, nz);
     }

@@ -8,6 +8,7 @@ zernike}.py: same class names, constructor arguments and defaults. The arithmeti
 
 from __future__ import annotations
 
+import dataclasses
 import functools
 import math
 
@@ -349,4 +350,98 @@ class ToroidalGeometry(NewtonRaphsonGeometry):
         c_yz = 1.0 / self.R_yz if has_yz else 0.0
         block = [self.R_rot, c_yz, self.k_yz, 1.0 if has_yz else 0.0,
                  float(len(self.coeffs_poly_y))] + self.coeffs_poly_y
+        return scalar(self.radius), scalar(self.k), self.tol, self.max_iter, 1.0, block
+
+
+@dataclasses.dataclass
+class ForbesSolverConfig:
+    """geometries/forbes/geometry.py:50-60."""
+
+    tol: float = 1e-10
+    max_iter: int = 100
+
+
+@dataclasses.dataclass
+class ForbesSurfaceConfig:
+    """geometries/forbes/geometry.py:63-80 (terms: {n: c} for Q-bfs,
+    {('a'|'b', m, n): c} for Q-2D)."""
+
+    radius: float
+    conic: float = 0.0
+    norm_radius: float = 1.0
+    terms: dict | None = None
+
+
+class _ForbesBase(NewtonRaphsonGeometry):
+    """geometries/forbes/geometry.py:83-180: base conic + Q-polynomial departure scaled by
+    the conic correction factor; Newton-iterated like every NewtonRaphsonGeometry."""
+
+    def __init__(self, coordinate_system, surface_config, solver_config=None):
+        solver_config = solver_config or ForbesSolverConfig()
+        super().__init__(coordinate_system, surface_config.radius, surface_config.conic,
+                         solver_config.tol, solver_config.max_iter)
+        self.surface_config = surface_config
+        self.solver_config = solver_config
+        self.norm_radius = float(surface_config.norm_radius)
+        self.terms = dict(surface_config.terms or {})
+
+
+class ForbesQbfsGeometry(_ForbesBase):
+    """geometries/forbes/geometry.py:183-330: rotationally symmetric Q-bfs surface.
+
+    Coefficient block: norm_radius, L, dep_normal, b_0 .. b_{L-1} (the orthonormal P_n
+    coefficients, forbes.qbfs_to_pn); dep_normal = 0 when every coefficient is zero (the
+    reference's normal then skips the departure, :300)."""
+
+    geometry_id = _abi.GEOM_FORBES_QBFS
+
+    def __init__(self, coordinate_system, surface_config, solver_config=None):
+        super().__init__(coordinate_system, surface_config, solver_config)
+        self.radial_terms = self.terms
+        self.is_symmetric = True
+
+    def lower_params(self):
+        from .forbes import qbfs_to_pn
+
+        t = {int(k): scalar(v) for k, v in self.radial_terms.items()}
+        cs = [t.get(n, 0.0) for n in range(max(t) + 1)] if t and max(t) >= 0 else []
+        b = qbfs_to_pn(cs)
+        dep = 1.0 if any(c != 0.0 for c in cs) else 0.0
+        block = [self.norm_radius, float(len(b)), dep] + b
+        return scalar(self.radius), scalar(self.k), self.tol, self.max_iter, 1.0, block
+
+
+class ForbesQ2dGeometry(_ForbesBase):
+    """geometries/forbes/geometry.py:333-640: Q-2D freeform surface.
+
+    Coefficient block: norm_radius, d/dx and d/dy of the sag at the vertex, the m = 0
+    Q-bfs record (L, b_0 .. b_{L-1}), the highest azimuthal order M, then per order
+    m = 1..M its cosine and sine Clenshaw records (forbes.q2d_order_block)."""
+
+    geometry_id = _abi.GEOM_FORBES_Q2D
+
+    def __init__(self, coordinate_system, surface_config, solver_config=None):
+        super().__init__(coordinate_system, surface_config, solver_config)
+        self.freeform_coeffs = self.terms
+        self.is_symmetric = False
+
+    def split(self):
+        from .forbes import q2d_split
+
+        cm0, ams, bms = q2d_split({k: scalar(v) for k, v in self.freeform_coeffs.items()})
+        return [float(c) for c in cm0], ams, bms
+
+    def lower_params(self):
+        from .forbes import q2d_order_block, q2d_sum_at_zero, qbfs_to_pn
+
+        cm0, ams, bms = self.split()
+        # vertex slope (forbes/geometry.py:530-543): only the m = 1 order contributes
+        vdx = q2d_sum_at_zero(ams[0], 1) / np.float64(self.norm_radius) if ams and ams[0] else 0.0
+        vdy = q2d_sum_at_zero(bms[0], 1) / np.float64(self.norm_radius) if bms and bms[0] else 0.0
+        b0 = qbfs_to_pn(cm0)
+        block = [self.norm_radius, float(vdx), float(vdy), float(len(b0))] + b0
+        block.append(float(len(ams)))
+        for m in range(1, len(ams) + 1):
+            block += q2d_order_block(ams[m - 1], m)
+            block += q2d_order_block(bms[m - 1], m)
         return scalar(self.radius), scalar(self.k), self.tol, self.max_iter, 1.0, block

@@ -24,12 +24,17 @@ from .geometries import (
     BiconicGeometry,
     ChebyshevPolynomialGeometry,
     EvenAsphere,
+    ForbesQ2dGeometry,
+    ForbesQbfsGeometry,
+    ForbesSolverConfig,
+    ForbesSurfaceConfig,
     OddAsphere,
     Plane,
     PolynomialGeometry,
     StandardGeometry,
     ToroidalGeometry,
     ZernikePolynomialGeometry,
+    scalar,
 )
 from .materials import IdealMaterial, Material
 from .apertures import BaseAperture
@@ -95,11 +100,48 @@ def geometry_from_dict(d):
         return ToroidalGeometry(cs, _f(d.get("radius_x"), np.inf), _f(d.get("radius_y"), np.inf),
                                 _f(d.get("conic_yz", d.get("conic"))),
                                 list(d.get("coeffs_poly_y") or []), tol, max_iter)
+    if t in ("ForbesQbfsGeometry", "ForbesQ2dGeometry"):  # forbes/geometry.py:329-370, 612-640
+        sc, so = d.get("surface_config", {}), d.get("solver_config", {})
+        terms = _forbes_terms(sc.get("terms"), t == "ForbesQbfsGeometry")
+        cfg = ForbesSurfaceConfig(radius=_f(sc.get("radius"), np.inf), conic=_f(sc.get("conic")),
+                                  norm_radius=_f(sc.get("norm_radius"), 1.0), terms=terms)
+        sol = ForbesSolverConfig(tol=_f(so.get("tol"), 1e-10), max_iter=int(so.get("max_iter", 100)))
+        cls = ForbesQbfsGeometry if t == "ForbesQbfsGeometry" else ForbesQ2dGeometry
+        return cls(cs, cfg, sol)
     raise ValueError(f"Unknown or unsupported geometry type: {t}")
+
+
+def _forbes_terms(terms, radial):
+    """Forbes terms from a dict: Q-bfs {n: c} (JSON turns n into a string); Q-2D
+    {(kind, m, n): c} in memory, or as JSON a list of [kind, m, n, c] (tuple keys do not
+    survive JSON) or string keys "a,m,n"."""
+    if not terms:
+        return {}
+    if radial:
+        return {int(k): float(v) for k, v in dict(terms).items()}
+    if isinstance(terms, list):
+        return {(str(a), int(m), int(n)): float(c) for a, m, n, c in terms}
+    out = {}
+    for k, v in terms.items():
+        if isinstance(k, str):
+            a, m, n = (p.strip(" '\"()") for p in k.split(","))
+            k = (a, int(m), int(n))
+        out[(str(k[0]), int(k[1]), int(k[2]))] = float(v)
+    return out
 
 
 def geometry_to_dict(g):
     d = {"type": type(g).__name__, "cs": _cs_to(g.cs)}
+    if isinstance(g, (ForbesQbfsGeometry, ForbesQ2dGeometry)):
+        if isinstance(g, ForbesQbfsGeometry):
+            terms = {str(k): scalar(v) for k, v in g.radial_terms.items()}
+        else:
+            terms = [[k[0], int(k[1]), int(k[2]), scalar(v)]
+                     for k, v in g.freeform_coeffs.items()]
+        d["surface_config"] = {"radius": scalar(g.radius), "conic": scalar(g.k),
+                               "norm_radius": g.norm_radius, "terms": terms}
+        d["solver_config"] = {"tol": g.tol, "max_iter": g.max_iter}
+        return d
     if isinstance(g, Plane):
         d["radius"] = float("inf")
         return d

@@ -250,6 +250,54 @@ class FreeformTriplet(Optic):
         self.update_paraxial()
 
 
+def _forbes_prescription(lens, s2_type, s2_terms):
+    """The reference's Forbes test system (tests/test_geometries.py:2103-2143): a
+    plano / Forbes Q-bfs singlet in H-K3 and a plano / Q-bfs element in H-ZLAF68C at
+    1.55 um; surface 3 as Q-bfs or Q-2D, fields added for off-axis coverage."""
+    lens.set_aperture(aperture_type="EPD", value=4.0)
+    lens.set_field_type(field_type="angle")
+    lens.add_field(y=0)
+    lens.add_field(y=3)
+    lens.add_field(x=2, y=2)
+    lens.add_wavelength(value=1.55, is_primary=True)
+    lens.add_surface(index=0, thickness=0.055)
+    lens.add_surface(index=1, thickness=26.5)
+    lens.add_surface(index=2, thickness=4.0, radius=np.inf, material=("H-K3", "cdgm"),
+                     is_stop=True)
+    kw = ({"radial_terms": s2_terms} if s2_type == "forbes_qbfs"
+          else {"freeform_coeffs": s2_terms})
+    lens.add_surface(index=3, thickness=25.0, radius=22, conic=-4.428, norm_radius=6.336,
+                     surface_type=s2_type, **kw)
+    lens.add_surface(index=4, thickness=7.0, radius=np.inf, material=("H-ZLAF68C", "cdgm"))
+    lens.add_surface(index=5, thickness=10.0, radius=-31.0, conic=0.038,
+                     radial_terms={0: -0.270, 1: 0.087, 2: -0.048, 3: 0.026, 4: -0.012},
+                     norm_radius=10.0, surface_type="forbes_qbfs")
+    lens.add_surface(index=6)
+
+
+class ForbesSinglets(Optic):
+    """Two Forbes Q-bfs elements (forbes/geometry.py:183-330)."""
+
+    def __init__(self):
+        super().__init__()
+        _forbes_prescription(self, "forbes_qbfs",
+                             {0: 1.614, 1: 0.348, 2: 0.150, 3: 0.033, 4: 0.030})
+
+
+class ForbesFreeform(Optic):
+    """The same system with a Q-2D freeform first surface (forbes/geometry.py:333-640):
+    rotationally symmetric terms plus m = 1..4 cosine / sine terms."""
+
+    Q2D = {("a", 0, 0): 1.614, ("a", 0, 1): 0.348, ("a", 0, 2): 0.150,
+           ("a", 1, 1): 0.02, ("b", 1, 1): -0.01, ("a", 1, 3): 0.005,
+           ("a", 2, 0): 0.03, ("b", 2, 1): 0.01, ("a", 3, 0): -0.004,
+           ("b", 4, 1): 0.002}
+
+    def __init__(self):
+        super().__init__()
+        _forbes_prescription(self, "forbes_q2d", dict(self.Q2D))
+
+
 def _cooke_prescription(lens, object_thickness):
     lens.add_surface(index=0, radius=np.inf, thickness=object_thickness)
     lens.add_surface(index=1, radius=22.01359, thickness=3.25896, material="SK16")
@@ -305,4 +353,6 @@ GOLDEN_LENSES = {
     "freeform": FreeformTriplet,
     "cooke_pih": CookeTripletImageHeight,
     "finite_pih": FiniteTripletImageHeight,
+    "forbes": ForbesSinglets,
+    "forbes_q2d": ForbesFreeform,
 }

@@ -20,6 +20,10 @@ from .geometries import (
     BiconicGeometry,
     ChebyshevPolynomialGeometry,
     EvenAsphere,
+    ForbesQ2dGeometry,
+    ForbesQbfsGeometry,
+    ForbesSolverConfig,
+    ForbesSurfaceConfig,
     OddAsphere,
     Plane,
     PolynomialGeometry,
@@ -144,10 +148,16 @@ def _make_geometry(surface_type, cs, kw):
         return ToroidalGeometry(cs, kw.get("radius_x", np.inf), kw.get("radius_y", np.inf),
                                 kw.get("conic", 0.0), kw.get("toroidal_coeffs_poly_y", []),
                                 tol, max_iter)
+    if st in ("forbes_qbfs", "forbes_q2d"):  # geometry_factory.py:282-314
+        cfg = ForbesSurfaceConfig(
+            radius=radius, conic=conic, norm_radius=kw.get("norm_radius", 1.0),
+            terms=kw.get("radial_terms" if st == "forbes_qbfs" else "freeform_coeffs", {}))
+        cls = ForbesQbfsGeometry if st == "forbes_qbfs" else ForbesQ2dGeometry
+        return cls(cs, cfg, ForbesSolverConfig(tol=tol, max_iter=max_iter))
     raise ValueError(
         f"Surface type {st!r} is not lowered to the MI355X trace core (supported: "
         "standard, plane, even_asphere, odd_asphere, zernike, polynomial, chebyshev, "
-        "biconic, toroidal).")
+        "biconic, toroidal, forbes_qbfs, forbes_q2d).")
 
 
 class SurfaceGroup:

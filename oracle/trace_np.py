@@ -14,6 +14,8 @@ It restates, formula by formula and in the same evaluation order, the reference
   newton_raphson.py:119-168                            Newton refinement (global stop)
   even_asphere.py:82-129, odd_asphere.py:73-130        asphere sag / normal
   zernike.py:133-246, zernike/base.py:42-299           Zernike sag / normal
+  polynomial.py, chebyshev.py, biconic.py, toroidal.py  freeform sag / normal
+  forbes/geometry.py:83-640, forbes/qpoly.py            Forbes Q-bfs / Q-2D sag / normal
   homogeneous.py:30-57                                 propagate + absorption
   standard_surface.py:218                              OPD accumulation
   physical_apertures/radial.py:50-63, real_rays.py:132-139  radial clip
@@ -478,6 +480,224 @@ def normal_toroidal(x, y, R_rot, R_yz, c, k, poly):
             np.where(term >= 0, nz, -1.0))
 
 
+# ---- Forbes Q-bfs / Q-2D (forbes/geometry.py:83-640, forbes/qpoly.py) -----------------
+# The lens-only tables (orthonormal-basis coefficients, recurrence A/B/C, vertex slope)
+# are read from the lowered coefficient block (layout: include/optiland_rt.h); the
+# per-ray recurrences below follow qpoly.py's NumPy path operation by operation.
+_FEPS = 1e-12
+
+
+def _forbes_base_sag(r2, R, k):
+    """forbes/geometry.py:115-131."""
+    if np.isinf(R):
+        return np.zeros_like(r2)
+    a = 1 - (1 + k) * r2 / R**2
+    return r2 / (R * (1 + np.sqrt(np.where(a < 0, 0, a))))
+
+
+def _forbes_base_dsag(rho, r2, R, k):
+    """forbes/geometry.py:133-150."""
+    if np.isinf(R) or R == 0:
+        return np.zeros_like(rho)
+    c = 1.0 / R
+    a = 1 - (k + 1) * c**2 * r2
+    return c * rho / np.sqrt(np.where(a > 0, a, 1e-12))
+
+
+def _forbes_conic(r2, R, k):
+    """forbes/geometry.py:152-180."""
+    if np.isinf(R):
+        return 1.0, 0.0
+    c2 = (1.0 / R) ** 2
+    rho = np.sqrt(r2)
+    na = 1 - k * c2 * r2
+    da = 1 - (k + 1) * c2 * r2
+    Nn = np.sqrt(np.where(na > 0, na, 1e-12))
+    Dd = np.sqrt(np.where(da > 0, da, 1e-12))
+    return Nn / Dd, (c2 * rho) / (Nn * Dd**3)
+
+
+def _qbfs_alphas(b, usq, j):
+    """qpoly.py:127-192: alphas[0] (sum recurrence) and, for j = 1, alphas[1]."""
+    m = len(b) - 1
+    al = np.zeros((j + 1, m + 1) + np.shape(usq))
+    p = 2 - 4 * usq
+    al[0][m] = b[m]
+    if m > 0:
+        al[0][m - 1] = b[m - 1] + p * al[0][m]
+    for i in range(m - 2, -1, -1):
+        al[0][i] = b[i] + p * al[0][i + 1] - al[0][i + 2]
+    if j and m - 1 >= 0:
+        al[1][m - 1] = -4 * al[0][m]
+        if m - 2 >= 0:
+            al[1][m - 2] = p * al[1][m - 1] - 4 * al[0][m - 1]
+        for n in range(m - 3, -1, -1):
+            al[1][n] = p * al[1][n + 1] - al[1][n + 2] - 4 * al[0][n + 1]
+    return al
+
+
+def _qbfs_sum(b, usq, j=0):
+    """(S, dS/d usq): 2 (alpha_0 + alpha_1), or 2 alpha_0 for one term."""
+    if len(b) == 0:
+        z = np.zeros_like(usq)
+        return z, z
+    al = _qbfs_alphas(b, usq, j)
+    if len(b) > 1:
+        return 2 * (al[0][0] + al[0][1]), (2 * (al[1][0] + al[1][1]) if j else None)
+    return 2 * al[0][0], (2 * al[1][0] if j else None)
+
+
+def _q2d_records(B):
+    """Parse the Q-2D block: (norm, vdx, vdy, b0, [(m, rec_a, rec_b), ...])."""
+    nr, vdx, vdy, L0 = B[0], B[1], B[2], int(B[3])
+    b0 = list(B[4:4 + L0])
+    pos = 4 + L0
+    M = int(B[pos])
+    pos += 1
+    orders = []
+    for m in range(1, M + 1):
+        recs = []
+        for _ in range(2):
+            L = int(B[pos])
+            if L == 0:
+                recs.append(None)
+                pos += 1
+                continue
+            body = np.asarray(B[pos + 1:pos + 1 + 4 * L]).reshape(4, L)
+            recs.append(body)
+            pos += 1 + 4 * L
+        orders.append((m, recs[0], recs[1]))
+    return nr, vdx, vdy, b0, orders
+
+
+def _q2d_order(rec, m, usq):
+    """qpoly.py:415-466 (clenshaw_q2d + its j = 1 derivative) and :389-398
+    (q2d_sum_from_alphas) for one azimuthal order: (S, dS/d usq)."""
+    D, A, Bc, C = rec
+    top = len(D) - 1
+    al = np.zeros((2, top + 1) + np.shape(usq))
+    al[0][top] = D[top]
+    if top > 0:
+        al[0][top - 1] = D[top - 1] + (A[top - 1] + Bc[top - 1] * usq) * al[0][top]
+    for n in range(top - 2, -1, -1):
+        al[0][n] = D[n] + (A[n] + Bc[n] * usq) * al[0][n + 1] - C[n + 1] * al[0][n + 2]
+    if top - 1 >= 0:
+        al[1][top - 1] = Bc[top - 1] * al[0][top]
+        for n in range(top - 2, -1, -1):
+            al[1][n] = (Bc[n] * al[0][n + 1] + (A[n] + Bc[n] * usq) * al[1][n + 1]
+                        - C[n + 1] * al[1][n + 2])
+    out = []
+    for a in al:
+        s = 0.5 * a[0]
+        if m == 1 and top > 2:
+            s -= 2 / 5 * a[3]
+        out.append(s)
+    return out
+
+
+def _q2d_sums(B, u, t):
+    """qpoly.py:469-520 compute_z_zprime_q2d."""
+    nr, vdx, vdy, b0, orders = _q2d_records(B)
+    usq = u * u
+    z = np.zeros_like(u)
+    p0, dp0 = z, z
+    if b0:
+        p0, d = _qbfs_sum(b0, usq, 1)
+        dp0 = d * 2 * u
+    pg, dr, dt = [], [], []
+    for m, ra, rb in orders:
+        sa = sb = dsa = dsb = 0
+        if ra is not None:
+            sa, dsa = _q2d_order(ra, m, usq)
+        if rb is not None:
+            sb, dsb = _q2d_order(rb, m, usq)
+        um = u**m
+        ct, st = np.cos(m * t), np.sin(m * t)
+        pg.append(um * (ct * sa + st * sb))
+        umm1 = u ** (m - 1) if m > 0 else np.ones_like(u)
+        two = 2 * usq
+        dr.append(umm1 * (ct * (two * dsa + m * sa) + st * (two * dsb + m * sb)))
+        dt.append(m * um * (-sa * st + sb * ct))
+    sm = (lambda v: np.sum(np.stack(v), axis=0) if v else z)
+    return p0, dp0, sm(pg), sm(dr), sm(dt)
+
+
+def sag_qbfs(x, y, R, k, B):
+    """forbes/geometry.py:243-266."""
+    nr, L = np.array(B[0]), int(B[1])
+    b = list(B[3:3 + L])
+    r2 = x**2 + y**2
+    usq = r2 / (nr**2)
+    ps = _qbfs_sum(b, usq)[0] if L else np.zeros_like(usq)
+    cf, _ = _forbes_conic(r2, R, k)
+    dep = usq * (1 - usq) * cf * ps
+    return _forbes_base_sag(r2, R, k) + np.where(usq > 1, 0.0, dep)
+
+
+def normal_qbfs(x, y, R, k, B):
+    """forbes/geometry.py:268-327 (NumPy: the analytical branch)."""
+    nr, L, dep = np.array(B[0]), int(B[1]), B[2] != 0.0
+    b = list(B[3:3 + L])
+    r2 = x**2 + y**2
+    rho = np.sqrt(r2 + _FEPS)
+    dfr = _forbes_base_dsag(rho, r2, R, k)
+    if dep:
+        u = rho / nr
+        pv, pd = _qbfs_sum(b, u**2, 1)
+        dpdu = pd * 2 * u
+        dpre = (2 * u - 4 * u**3) / nr
+        cf, dcf = _forbes_conic(r2, R, k)
+        usq = u**2
+        dd = (dpre * cf * pv + (usq - usq**2) * dcf * pv + (usq - usq**2) * cf * (dpdu / nr))
+        dfr = dfr + np.where(u >= 1, 0.0, dd)
+    dfx, dfy = dfr * (x / rho), dfr * (y / rho)
+    mag = np.sqrt(dfx**2 + dfy**2 + 1)
+    sm = np.where(mag < _FEPS, 1.0, mag)
+    return dfx / sm, dfy / sm, -1 / sm
+
+
+def sag_q2d(x, y, R, k, B):
+    """forbes/geometry.py:420-450."""
+    nr = np.array(B[0])
+    r2 = x**2 + y**2
+    rho = np.sqrt(r2 + _FEPS)
+    u = rho / nr
+    t = np.arctan2(y, np.where(rho < _FEPS, x + 1e-12, x))
+    p0, _, pg, _, _ = _q2d_sums(B, u, t)
+    cf, _ = _forbes_conic(r2, R, k)
+    usq = u**2
+    total = usq * (1 - usq) * cf * p0 + cf * pg
+    return _forbes_base_sag(r2, R, k) + np.where(u > 1, 0.0, total)
+
+
+def normal_q2d(x, y, R, k, B):
+    """forbes/geometry.py:545-610 (NumPy: the analytical branch)."""
+    nr, vdx, vdy = np.array(B[0]), B[1], B[2]
+    r2 = x**2 + y**2
+    rho = np.sqrt(r2)
+    isv = rho < _FEPS
+    rs = np.where(isv, _FEPS, rho)
+    u = rho / nr
+    t = np.arctan2(y, x)
+    p0, dp0, pg, dr, dt = _q2d_sums(B, u, t)
+    cf, dcf = _forbes_conic(r2, R, k)
+    usq = u**2
+    dpre = (2 * u - 4 * u**3) / nr
+    ds0 = (dpre * p0 + (usq - usq**2) * (dp0 / nr)) * cf + (usq - usq**2) * p0 * dcf
+    dsg = (dcf * pg) + (cf * (dr / nr))
+    dsr = np.where(u > 1, 0.0, ds0 + dsg)
+    dst = np.where(u > 1, 0.0, cf * dt)
+    ct, st = x / rs, y / rs
+    dsx = ct * dsr - (st / rs) * dst
+    dsy = st * dsr + (ct / rs) * dst
+    dbr = _forbes_base_dsag(rho, r2, R, k)
+    dfx = np.where(isv, vdx, dbr * ct + dsx)
+    dfy = np.where(isv, vdy, dbr * st + dsy)
+    mag = np.sqrt(dfx**2 + dfy**2 + 1)
+    sm = np.where(mag < _FEPS, 1.0, mag)
+    return dfx / sm, dfy / sm, -1.0 / sm
+
+
 def _geometry_fns(table, s):
     g = int(s["geometry"])
     R, k = float(s["radius"]), float(s["conic"])
@@ -518,6 +738,11 @@ def _geometry_fns(table, s):
         k_ = np.array(k_yz)
         return ((lambda x, y: sag_toroidal(x, y, R_rot, R_yz, c, k_, poly)),
                 (lambda x, y: normal_toroidal(x, y, R_rot, R_yz, c, k_, poly)))
+    if g in (_abi.GEOM_FORBES_QBFS, _abi.GEOM_FORBES_Q2D):
+        Rf, kf = np.array(R), np.array(k)
+        sag_f, nrm_f = ((sag_qbfs, normal_qbfs) if g == _abi.GEOM_FORBES_QBFS
+                        else (sag_q2d, normal_q2d))
+        return (lambda x, y: sag_f(x, y, Rf, kf, B)), (lambda x, y: nrm_f(x, y, Rf, kf, B))
     raise ValueError(g)
 
 

@@ -41,7 +41,8 @@ def native_case(name, meta, record=False):
 # the HIP kernel reproduce the reference bit for bit there
 CLOSED_FORM = ("cooke", "dg", "rt", "cooke_aperture", "cooke_shapes", "decentered", "json_cooke",
                "json_heliar", "json_rt", "cooke_pih", "finite_pih")
-NEWTON = ("rt_asph", "rt_odd", "tma_fringe", "tma_standard", "tma_noll", "freeform")
+NEWTON = ("rt_asph", "rt_odd", "tma_fringe", "tma_standard", "tma_noll", "freeform",
+          "forbes", "forbes_q2d")
 ALL_CASES = CLOSED_FORM + NEWTON
 
 FIELDS = _abi.RAY_FIELDS

@@ -11,6 +11,9 @@ from optiland_pr_amd.geometries import (
     BiconicGeometry,
     ChebyshevPolynomialGeometry,
     EvenAsphere,
+    ForbesQ2dGeometry,
+    ForbesQbfsGeometry,
+    ForbesSurfaceConfig,
     OddAsphere,
     Plane,
     PolynomialGeometry,
@@ -63,9 +66,17 @@ def build(spec):
     if k == "toroidal":
         return ToroidalGeometry(cs, radius_x=spec["radius_x"], radius_y=spec["radius_y"],
                                 conic=spec["conic"], coeffs_poly_y=spec["coeffs_poly_y"])
+    if k in ("forbes_qbfs", "forbes_q2d"):
+        if k == "forbes_qbfs":
+            terms = {int(n): c for n, c in spec["radial_terms"]}
+        else:
+            terms = {(a, int(m), int(n)): c for a, m, n, c in spec["freeform_coeffs"]}
+        cfg = ForbesSurfaceConfig(radius=spec["radius"], conic=spec["conic"],
+                                  norm_radius=spec["norm_radius"], terms=terms)
+        return (ForbesQbfsGeometry if k == "forbes_qbfs" else ForbesQ2dGeometry)(cs, cfg)
     raise ValueError(k)
 
 
 CASES = sorted(specs())
 NEWTON_KINDS = ("even_asphere", "odd_asphere", "zernike", "polynomial", "chebyshev",
-                "biconic", "toroidal")
+                "biconic", "toroidal", "forbes_qbfs", "forbes_q2d")

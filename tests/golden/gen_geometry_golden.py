@@ -95,7 +95,42 @@ SPECS = {
                         coeffs_poly_y=[1e-5, -2e-6]),
     "toroid_neg": dict(kind="toroidal", radius_x=-30.0, radius_y=-20.0, conic=0.3,
                        coeffs_poly_y=[2e-5, 1e-7]),
+    # Forbes (tests/test_geometries.py:2103-2720): radial_terms as [n, c] pairs,
+    # freeform_coeffs as [kind, m, n, c] (JSON has no tuple keys)
+    "qbfs_zemax": dict(kind="forbes_qbfs", radius=21.723, conic=-4.428, norm_radius=6.336,
+                       radial_terms=[[0, 1.614], [1, 0.348], [2, 0.150], [3, 0.033],
+                                     [4, 0.030]]),
+    "qbfs_plane_base": dict(kind="forbes_qbfs", radius=float("inf"), conic=0.0,
+                            norm_radius=10.0, radial_terms=[[1, 1e-3]]),
+    "qbfs_small": dict(kind="forbes_qbfs", radius=22.0, conic=-4.428, norm_radius=6.336,
+                       radial_terms=[[0, 1.6e-4], [1, 0.3e-4], [2, 0.15e-4]]),
+    "qbfs_sparse": dict(kind="forbes_qbfs", radius=50.0, conic=-1.0, norm_radius=10.0,
+                        radial_terms=[[2, 1e-4]]),
+    "qbfs_zero": dict(kind="forbes_qbfs", radius=-35.0, conic=0.3, norm_radius=8.0,
+                      radial_terms=[[0, 0.0], [1, 0.0]]),
+    "q2d_mixed": dict(kind="forbes_q2d", radius=50.0, conic=0.0, norm_radius=10.0,
+                      freeform_coeffs=[["a", 0, 0, 1e-3], ["a", 0, 1, -2e-4],
+                                       ["a", 1, 1, 2e-4], ["b", 1, 1, 3e-4],
+                                       ["a", 2, 0, 1e-4], ["b", 3, 2, -5e-5],
+                                       ["a", 1, 4, 1e-5], ["a", 1, 0, 4e-4]]),
+    "q2d_dict": dict(kind="forbes_q2d", radius=123.4, conic=-0.9, norm_radius=45.6,
+                     freeform_coeffs=[["a", 2, 2, 1e-4], ["b", 1, 1, -5e-5]]),
+    "q2d_conic": dict(kind="forbes_q2d", radius=-40.0, conic=0.5, norm_radius=8.0,
+                      freeform_coeffs=[["a", 1, 1, 3e-4], ["a", 1, 3, -1e-4],
+                                       ["b", 1, 0, 2e-4], ["b", 2, 1, 1e-4],
+                                       ["a", 4, 0, 5e-5], ["a", 0, 2, 2e-4]]),
+    "q2d_sine_only": dict(kind="forbes_q2d", radius=100.0, conic=0.0, norm_radius=10.0,
+                          freeform_coeffs=[["b", 1, 1, 1e-3]]),
 }
+
+
+def _forbes(spec):
+    cfg = dict(radius=spec["radius"], conic=spec["conic"], norm_radius=spec["norm_radius"])
+    if spec["kind"] == "forbes_qbfs":
+        cfg["terms"] = {int(n): c for n, c in spec["radial_terms"]}
+    else:
+        cfg["terms"] = {(k, int(m), int(n)): c for k, m, n, c in spec["freeform_coeffs"]}
+    return cfg
 
 
 def build(spec):
@@ -131,6 +166,10 @@ def build(spec):
         return geometries.ToroidalGeometry(cs, radius_x=spec["radius_x"],
                                            radius_y=spec["radius_y"], conic=spec["conic"],
                                            coeffs_poly_y=spec["coeffs_poly_y"])
+    if k in ("forbes_qbfs", "forbes_q2d"):
+        cls = (geometries.ForbesQbfsGeometry if k == "forbes_qbfs"
+               else geometries.ForbesQ2dGeometry)
+        return cls(cs, geometries.ForbesSurfaceConfig(**_forbes(spec)))
     raise ValueError(k)
 
 

@@ -226,6 +226,47 @@ def freeform():
     return lens
 
 
+def _forbes_prescription(lens, s2_type, s2_terms):
+    """tests/test_geometries.py:2103-2143 (forbes_system): a plano-Forbes singlet and a
+    plano-Forbes element at 1.55 um, CDGM glasses; fields added for off-axis coverage."""
+    lens.set_aperture(aperture_type="EPD", value=4.0)
+    lens.set_field_type(field_type="angle")
+    lens.add_field(y=0)
+    lens.add_field(y=3)
+    lens.add_field(x=2, y=2)
+    lens.add_wavelength(value=1.55, is_primary=True)
+    h_k3 = Material("H-K3", reference="cdgm")
+    h_zlaf = Material("H-ZLAF68C", reference="cdgm")
+    lens.add_surface(index=0, thickness=0.055)
+    lens.add_surface(index=1, thickness=26.5)
+    lens.add_surface(index=2, thickness=4.0, radius=np.inf, material=h_k3, is_stop=True)
+    kw = ({"radial_terms": s2_terms} if s2_type == "forbes_qbfs"
+          else {"freeform_coeffs": s2_terms})
+    lens.add_surface(index=3, thickness=25.0, radius=22, conic=-4.428, norm_radius=6.336,
+                     surface_type=s2_type, **kw)
+    lens.add_surface(index=4, thickness=7.0, radius=np.inf, material=h_zlaf)
+    lens.add_surface(index=5, thickness=10.0, radius=-31.0, conic=0.038,
+                     radial_terms={0: -0.270, 1: 0.087, 2: -0.048, 3: 0.026, 4: -0.012},
+                     norm_radius=10.0, surface_type="forbes_qbfs")
+    lens.add_surface(index=6)
+    return lens
+
+
+FORBES_S2_QBFS = {0: 1.614, 1: 0.348, 2: 0.150, 3: 0.033, 4: 0.030}
+FORBES_S2_Q2D = {("a", 0, 0): 1.614, ("a", 0, 1): 0.348, ("a", 0, 2): 0.150,
+                 ("a", 1, 1): 0.02, ("b", 1, 1): -0.01, ("a", 1, 3): 0.005,
+                 ("a", 2, 0): 0.03, ("b", 2, 1): 0.01, ("a", 3, 0): -0.004,
+                 ("b", 4, 1): 0.002}
+
+
+def forbes():
+    return _forbes_prescription(ref_optic.Optic(), "forbes_qbfs", FORBES_S2_QBFS)
+
+
+def forbes_q2d():
+    return _forbes_prescription(ref_optic.Optic(), "forbes_q2d", FORBES_S2_Q2D)
+
+
 def _cooke_prescription(lens, object_thickness):
     lens.add_surface(index=0, radius=np.inf, thickness=object_thickness)
     lens.add_surface(index=1, radius=22.01359, thickness=3.25896, material="SK16")
@@ -293,6 +334,8 @@ CASES = {
                     "uniform", 24),
     "json_rt": (json_lens("reverse_telephoto"), [(0, 0), (0, 1)], [0.5876], "uniform", 24),
     "cooke_pih": (cooke_pih, [(0, 0), (0, 0.6), (0.3, 1)], [0.55], "uniform", 24),
+    "forbes": (forbes, [(0, 0), (0, 1), (0.7, 0.7)], [1.55], "uniform", 24),
+    "forbes_q2d": (forbes_q2d, [(0, 0), (0, 1), (0.7, 0.7)], [1.55], "uniform", 24),
     "finite_pih": (finite_pih, [(0, 0), (0, 1), (-0.4, 0.7)], [0.48, 0.55], "uniform", 24),
 }
 
@@ -420,7 +463,7 @@ def glass_table():
     specs = [("SK16", None), ("F2", "schott"), ("N-SSK2", None), ("N-SK2", None),
              ("F5", "schott"), ("N-SK16", None), ("N-SK10", None), ("SK15", None),
              ("BASF2", None), ("FK3", None), ("SF15", "hikari"), ("N-LAK12", None),
-             ("E-LLF6", None)]
+             ("E-LLF6", None), ("H-K3", "cdgm"), ("H-ZLAF68C", "cdgm")]
     out = {}
     for name, ref in specs:
         m = Material(name, ref) if ref else Material(name)

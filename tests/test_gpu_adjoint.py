@@ -91,6 +91,8 @@ CASES = [
     ("tma_fringe", [("zernike", 1), ("zernike", 2), ("zernike", 3), ("radius", 1),
                     ("conic", 2), ("thickness", 1)], 1e-7),
     ("freeform", [("thickness", 1), ("thickness", 3)], 1e-7),
+    ("forbes", [("radius", 3), ("conic", 5), ("thickness", 3)], 1e-7),
+    ("forbes_q2d", [("radius", 3), ("conic", 3), ("radius", 5), ("thickness", 2)], 1e-7),
 ]
 
 
