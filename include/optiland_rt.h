@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define ORT_ABI_VERSION 7
+#define ORT_ABI_VERSION 8
 #define ORT_MAX_SURFACES 64
 
 /* ---- geometry kinds ----------------------------------- */
@@ -162,6 +162,38 @@ typedef struct ort_zernike_term {
   int32_t n_rad;
 } ort_zernike_term; /* 32 bytes */
 
+/* Dispersion of one material for per-ray wavelengths (ort_batch.w): n(lambda) by the
+ * material's formula (materials/material_file.py:250-428) or tabulated n, k(lambda) by
+ * linear interpolation of tabulated data (material_file.py:219-249, numpy.interp
+ * semantics), or constants (materials/ideal.py). Lambda-independent subexpressions of
+ * the formulas are formed on the host, so coef[coef_off ..] holds
+ *   FORMULA_1   1 + C0, then pairs (B_i, C_i ** 2)     n = sqrt(n0 + sum B w^2 / (w^2 - C))
+ *   FORMULA_2   1 + C0, then pairs (B_i, C_i)
+ *   FORMULA_3   C0, then pairs (A_i, e_i)              n = sqrt(C0 + sum A w^e)
+ *   FORMULA_4   C0, C1, C2, C3 ** C4, C5, C6, C7 ** C8, then pairs (A_i, e_i)
+ *   FORMULA_5   C0, then pairs (A_i, e_i)              n = C0 + sum A w^e
+ *   FORMULA_6   1 + C0, then pairs (B_i, C_i)          n = n0 + sum B / (C - w^-2)
+ *   FORMULA_7   C0 .. C(n-1)  (Herzberger)
+ *   FORMULA_8   C0 .. C3      (retro)
+ *   FORMULA_9   C0 .. C5      (exotic)
+ *   TABULATED   lambda_0 .. lambda_(n-1), n_0 .. n_(n-1)  (n_coef = points)
+ * and, when k_len > 0, k wavelengths at coef[k_off], k values at coef[k_off + k_len]. */
+enum ort_material_kind {
+  ORT_MAT_IDEAL = 0,
+  ORT_MAT_FORMULA_1 = 1, /* ... ORT_MAT_FORMULA_9 = 9: refractiveindex.info formulas */
+  ORT_MAT_TABULATED = 10
+};
+typedef struct ort_material {
+  int32_t kind;     /* enum ort_material_kind                                          */
+  int32_t n_coef;   /* doubles at coef[coef_off] (TABULATED: points)                   */
+  int32_t coef_off;
+  int32_t k_len;    /* tabulated k points; 0: k = k_const                              */
+  int32_t k_off;
+  int32_t reserved;
+  double n_const;   /* IDEAL: n                                                        */
+  double k_const;   /* IDEAL: k (glasses without k data: 0)                            */
+} ort_material; /* 40 bytes */
+
 /* The lowered lens (all pointers are device pointers). */
 typedef struct ort_lens {
   const ort_surface* surfaces;
@@ -179,6 +211,8 @@ typedef struct ort_lens {
   uint32_t geometry_mask;  /* OR of (1u << geometry) over the surfaces; selects the  */
   int32_t reserved;        /* kernel specialisation (no Newton code for sphere lenses) */
   double final_thickness;  /* real_ray_tracer.py:84-89 image-space propagate distance */
+  const ort_material* materials; /* [n_mat]: per-ray dispersion (ort_batch.w); may be  *
+                                  * NULL when no batch carries per-ray wavelengths    */
 } ort_lens;
 
 /* Ray state, structure of arrays, one double per ray per attribute (device). */
@@ -222,6 +256,13 @@ typedef struct ort_batch {
   int32_t n_seg;          /* entries in seg (>= ceil(n_rays / seg_len) when seg set) */
   int32_t pupil_per_ray;  /* px/py hold n_rays points (1) or seg_len points tiled (0) */
   const ort_segment* seg; /* device                                                   */
+  /* Per-ray wavelengths in um (device, [n_rays]; NULL: the wavelength of each ray is
+   * its segment's lambda_idx into the n_tab / alpha_tab / optics tables). When set,
+   * n and k are evaluated per ray and surface from lens.materials, as the reference
+   * does for a RealRays with any wavelength array (material.n(rays.w),
+   * standard_surface.py:218, refractive_reflective_model.py:32-55, homogeneous.py:30-57).
+   * ort_trace_sequential only. */
+  const double* w;
 } ort_batch;
 
 /* Newton semantics (newton_raphson.py:137-166). */
@@ -378,6 +419,13 @@ int ort_surface_distance(const ort_lens* lens, int32_t surface, const ort_rays* 
  * (distribution.py:72-408; the grid kinds bit-identical to NumPy, cos / sin correctly
  * rounded). Feeds ort_trace_pupil without host-side sampling or a host-to-device copy. */
 int ort_generate_pupil(const ort_pupil* pupil, double* px, double* py, void* stream);
+
+/* n(lambda) and k(lambda) of material `mat` of the lens (lens.materials) at n device
+ * wavelengths: BaseMaterial.n / .k (materials/base.py:73-119) on the device, the same
+ * evaluation the trace kernels run per ray when ort_batch.w is set. n_out / k_out are
+ * device [n] (either may be NULL). */
+int ort_material_nk(const ort_lens* lens, int32_t mat, const double* w, int64_t n,
+                    double* n_out, double* k_out, void* stream);
 
 /* Ray generation only (ray_generator.py:28-106): fills rays_out from pupil points. */
 int ort_generate_rays(const double* px, const double* py, ort_rays* rays_out,

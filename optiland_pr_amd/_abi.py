@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import numpy as np
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 VJP_UNROLLED = 0
 VJP_ADJOINT = 1
 AP_RADIAL = 1
@@ -136,6 +136,25 @@ SEGMENT = np.dtype(
     align=True,
 )
 assert SEGMENT.itemsize == 64
+
+# enum ort_material_kind
+MAT_IDEAL = 0
+MAT_TABULATED = 10
+
+MATERIAL = np.dtype(
+    [
+        ("kind", "<i4"),
+        ("n_coef", "<i4"),
+        ("coef_off", "<i4"),
+        ("k_len", "<i4"),
+        ("k_off", "<i4"),
+        ("reserved", "<i4"),
+        ("n_const", "<f8"),
+        ("k_const", "<f8"),
+    ],
+    align=True,
+)
+assert MATERIAL.itemsize == 40
 
 NEWTON_STAT = np.dtype(
     [("conv_mask", "<u8"), ("last_bad", "<i4"), ("max_updates", "<i4")], align=True

@@ -29,6 +29,7 @@ class ort_lens(C.Structure):
         ("geometry_mask", C.c_uint32),
         ("reserved", C.c_int32),
         ("final_thickness", C.c_double),
+        ("materials", C.c_void_p),
     ]
 
 
@@ -44,6 +45,7 @@ class ort_batch(C.Structure):
         ("n_seg", C.c_int32),
         ("pupil_per_ray", C.c_int32),
         ("seg", C.c_void_p),
+        ("w", C.c_void_p),
     ]
 
 
@@ -86,7 +88,8 @@ class ort_options(C.Structure):
 
 EXPORTS = ("ort_abi_version", "ort_trace_sequential", "ort_trace_pupil", "ort_trace_pupil_vjp",
            "ort_vjp_workspace_size", "ort_generate_pupil",
-           "ort_surface_sag_normal", "ort_surface_distance", "ort_generate_rays")
+           "ort_surface_sag_normal", "ort_surface_distance", "ort_generate_rays",
+           "ort_material_nk")
 
 _lib = None
 
@@ -134,6 +137,9 @@ def load(path: str | None = None):
                                          C.c_void_p]
     lib.ort_generate_pupil.restype = C.c_int
     lib.ort_generate_pupil.argtypes = [P(ort_pupil), C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.ort_material_nk.restype = C.c_int
+    lib.ort_material_nk.argtypes = [P(ort_lens), C.c_int32, C.c_void_p, C.c_int64, C.c_void_p,
+                                    C.c_void_p, C.c_void_p]
     lib.ort_generate_rays.restype = C.c_int
     lib.ort_generate_rays.argtypes = [C.c_void_p, C.c_void_p, P(ort_rays), P(ort_batch),
                                       C.c_void_p]

@@ -38,7 +38,7 @@ from .geometries import (
     ZernikePolynomialGeometry,
 )
 from .coordinate_system import CoordinateSystem
-from .materials import BaseMaterial
+from .materials import BaseMaterial, lower_dispersion
 
 _ORIGINAL = {}
 
@@ -58,6 +58,13 @@ class _RefMaterial(BaseMaterial):
 
     def _calculate_k(self, w):
         return np.asarray(_np(self.m.k(w)), dtype=np.float64) * np.ones_like(w)
+
+    def lower(self):
+        m = self.m
+        if type(m).__name__ == "IdealMaterial":
+            return 0, [], [], [], _f(m.index), _f(m.absorp)
+        return lower_dispersion(m._n_formula, m.coefficients, m._k_wavelength, m._k,
+                                getattr(m, "_n_wavelength", None), getattr(m, "_n", None))
 
     def key(self):
         # same dedup keys as the native materials (materials.py), so tables match

@@ -78,7 +78,14 @@ int fill_args(KArgs& a, const ort_lens* lens, const ort_batch* batch, const ort_
                              (1u << ORT_GEOM_FORBES_QBFS) | (1u << ORT_GEOM_FORBES_Q2D)))
     feat |= ort::KM_FREE;
   if (rec) feat |= F_REC;
-  if (lens->n_lambda == 1) feat |= F_MONO;
+  if (batch->w) {  // per-ray wavelengths: n, k from the material tables
+    if (!lens->materials) return ORT_ERR_ARG;
+    a.w = batch->w;
+    a.mats = lens->materials;
+    feat |= F_WRAY;
+  } else if (lens->n_lambda == 1) {
+    feat |= F_MONO;
+  }
   if (opt->newton_mode != ORT_NEWTON_SCHEDULE && opt->newton_mode != ORT_NEWTON_WAVE)
     return ORT_ERR_ARG;
   return ORT_OK;
@@ -116,6 +123,17 @@ extern "C" {
 
 int ort_abi_version(void) { return ORT_ABI_VERSION; }
 
+int ort_material_nk(const ort_lens* lens, int32_t mat, const double* w, int64_t n,
+                    double* n_out, double* k_out, void* stream) {
+  if (!lens || !lens->materials || !lens->coef || n < 0) return ORT_ERR_ARG;
+  if (mat < 0 || mat >= lens->n_mat) return ORT_ERR_ARG;
+  if (n == 0) return ORT_OK;
+  if (!w || (n + kBlock - 1) / kBlock > 0x7fffffff) return ORT_ERR_ARG;
+  launch_material_nk(lens->materials, lens->coef, mat, w, n, n_out, k_out,
+                     (hipStream_t)stream);
+  return hipGetLastError() == hipSuccess ? ORT_OK : ORT_ERR_LAUNCH;
+}
+
 int ort_trace_sequential(const ort_lens* lens, const ort_rays* rays_in, ort_rays* rays_out,
                          const ort_batch* batch, const ort_options* opt, double* rec,
                          ort_newton_stat* newton_stat, int32_t* status, void* stream) {
@@ -138,7 +156,7 @@ int ort_trace_pupil(const ort_lens* lens, const double* px, const double* py,
                     void* stream) {
   if (!rays_out || !batch) return ORT_ERR_ARG;
   if (batch->n_rays == 0) return ORT_OK;
-  if (!px || !py || !batch->seg) return ORT_ERR_ARG;
+  if (!px || !py || !batch->seg || batch->w) return ORT_ERR_ARG;
   KArgs a{};
   uint32_t feat = 0;
   int rc = fill_args(a, lens, batch, opt, rec, newton_stat, status, feat);
@@ -189,7 +207,7 @@ int ort_trace_pupil_vjp(const ort_lens* lens, const double* px, const double* py
   if (!batch || !cotangent || !params || params->n_param < 0) return ORT_ERR_ARG;
   const int32_t n_param = params->n_param;
   if (batch->n_rays == 0 || n_param == 0) return ORT_OK;
-  if (!px || !py || !batch->seg || !grad) return ORT_ERR_ARG;
+  if (!px || !py || !batch->seg || !grad || batch->w) return ORT_ERR_ARG;
   KArgs a{};
   uint32_t feat = 0;
   int rc = fill_args(a, lens, batch, opt, nullptr, nullptr, nullptr, feat);

@@ -23,13 +23,34 @@ __global__ __launch_bounds__(kBlock) void generate_kernel(const KArgs a) {
 
 KernelFn select_generate() { return generate_kernel; }
 
+__global__ __launch_bounds__(kBlock) void material_nk_kernel(const ort_material* mats,
+                                                             const double* coef, int32_t mat,
+                                                             const double* w, int64_t n,
+                                                             double* n_out, double* k_out) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const ort_material m = mats[mat];
+  const double wi = w[i];
+  if (n_out) n_out[i] = ort::material_n(m, coef, wi);
+  if (k_out) k_out[i] = ort::material_k(m, coef, wi);
+}
+
+void launch_material_nk(const ort_material* mats, const double* coef, int32_t mat,
+                        const double* w, int64_t n, double* n_out, double* k_out,
+                        hipStream_t stream) {
+  const int64_t blocks = (n + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(material_nk_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream,
+                     mats, coef, mat, w, n, n_out, k_out);
+}
+
 KernelFn select_closed(uint32_t feat) {
-  switch (feat & (F_GEN | F_REC | F_MONO)) {
+  switch (feat & (F_GEN | F_REC | F_MONO | F_WRAY)) {
 #define ORT_C(F) \
   case (F):      \
     return trace_closed_kernel<(F)>;
     ORT_C(0) ORT_C(F_GEN) ORT_C(F_REC) ORT_C(F_GEN | F_REC)
     ORT_C(F_MONO) ORT_C(F_MONO | F_GEN) ORT_C(F_MONO | F_REC) ORT_C(F_MONO | F_GEN | F_REC)
+    ORT_C(F_WRAY) ORT_C(F_WRAY | F_REC)
 #undef ORT_C
     default: return nullptr;
   }

@@ -26,6 +26,7 @@
 #include <stdlib.h>
 
 #include "ort_core.h"
+#include "ort_material.h"
 
 namespace ortk {
 
@@ -56,6 +57,7 @@ enum : uint32_t {
   F_GEN = 1u << 4,
   F_REC = 1u << 5,   // some surfaces are recorded (standard_surface.py:266-286)
   F_MONO = 1u << 6,  // one wavelength in the lens tables (closed-form kernels only)
+  F_WRAY = 1u << 7,  // per-ray wavelengths: n, k from lens.materials (ort_batch.w)
 };
 
 struct KArgs {
@@ -92,6 +94,9 @@ struct KArgs {
   double* rec;
   ort_newton_stat* stats;
   int32_t* status;
+  // per-ray wavelengths (F_WRAY)
+  const double* w;
+  const ort_material* mats;
 };
 
 __device__ inline uint64_t wave_and_u64(uint64_t v) {
@@ -131,6 +136,37 @@ __device__ inline ort_surface_optics optics_at(const KArgs& a, int lam, int si) 
   if constexpr ((FEAT & F_MONO) != 0) return cst(a.optics)[si];
   if (a.n_lambda == 1) return cst(a.optics)[si];
   return a.optics[lam * a.n_surf + si];
+}
+
+// F_WRAY: the surface's optical constants at this ray's own wavelength w, evaluated from
+// the material tables as the reference evaluates material.n(rays.w) / .k(rays.w)
+// (standard_surface.py:218, refractive_reflective_model.py:32-55, homogeneous.py:45-54)
+__device__ inline ort_surface_optics optics_ray(const KArgs& a, const ort_surface& s,
+                                                double w) {
+  const ort_material mp = cst(a.mats)[s.mat_pre];
+  const ort_material mq = cst(a.mats)[s.mat_post];
+  ort_surface_optics o;
+  o.n_pre = ort::material_n(mp, a.coef, w);
+  o.u = o.n_pre / ort::material_n(mq, a.coef, w);
+  o.alpha_pre = ort::absorption_alpha(ort::material_k(mp, a.coef, w), w);
+  o.reserved = 0.0;
+  return o;
+}
+
+template <uint32_t FEAT>
+__device__ inline ort_surface_optics surface_optics(const KArgs& a, const ort_surface& s,
+                                                    int lam, int si, double w) {
+  if constexpr ((FEAT & F_WRAY) != 0) return optics_ray(a, s, w);
+  return optics_at<FEAT>(a, lam, si);
+}
+
+// absorption of the image-space medium (final propagate)
+template <uint32_t FEAT>
+__device__ inline double final_alpha(const KArgs& a, int lam, double w) {
+  if constexpr ((FEAT & F_WRAY) != 0)
+    return ort::absorption_alpha(ort::material_k(cst(a.mats)[a.final_mat], a.coef, w), w);
+  if constexpr ((FEAT & F_MONO) != 0) return cst(a.alpha_tab)[a.final_mat];
+  return tab(a.alpha_tab, a.n_lambda, a.n_mat, lam, a.final_mat);
 }
 
 // localize / globalize (coordinate_system.py:73-107): the root frame's translation
@@ -238,6 +274,7 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(const KArgs a) {
   // segment / wavelength / Newton group of this ray
   const int64_t sidx = a.seg ? r_ld / a.seg_len : 0;
   int lam = 0;
+  double wl = 0.0;  // F_WRAY: this ray's wavelength
   ort::Ray r;
   if constexpr (FEAT & F_GEN) {
     const ort_segment sg = a.seg[sidx];
@@ -246,6 +283,7 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(const KArgs a) {
     r = ort::generate_ray(sg, a.px[p], a.py[p]);
   } else {
     if (a.seg) lam = a.seg[sidx].lambda_idx;
+    if constexpr ((FEAT & F_WRAY) != 0) wl = a.w[r_ld];
     r.x = a.in.x[r_ld];
     r.y = a.in.y[r_ld];
     r.z = a.in.z[r_ld];
@@ -267,7 +305,7 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(const KArgs a) {
 
   for (int si = a.start_surface; si < a.n_surf; ++si) {
     const ort_surface s = cst(a.surf)[si];
-    const ort_surface_optics o = optics_at(a, lam, si);
+    const ort_surface_optics o = surface_optics<FEAT>(a, s, lam, si, wl);
     localize(a, s, r);
     double t;
     if (s.geometry == ORT_GEOM_PLANE) {
@@ -321,9 +359,7 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(const KArgs a) {
   }
   // real_ray_tracer.py:84-89: image-space propagate by the last surface's thickness
   // (final_mat < 0: plain SurfaceGroup.trace, no propagate)
-  if (a.final_mat >= 0)
-    ort::propagate(r, a.final_thickness,
-                   tab(a.alpha_tab, a.n_lambda, a.n_mat, lam, a.final_mat));
+  if (a.final_mat >= 0) ort::propagate(r, a.final_thickness, final_alpha<FEAT>(a, lam, wl));
 
   if constexpr ((FEAT & (ort::KM_ZERN | ort::KM_FREE)) != 0) {
     if (range_bits && active && a.status) atomicOr(a.status, range_bits);
@@ -350,6 +386,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
   const bool active = rid < a.n_rays;
   const int64_t r_ld = active ? rid : 0;
   int lam = 0;
+  double wl = 0.0;  // F_WRAY: this ray's wavelength
   ort::Ray r;
   if constexpr ((FEAT & F_GEN) != 0) {
     const int64_t sidx = a.n_seg == 1 ? 0 : r_ld / a.seg_len;
@@ -359,6 +396,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
     r = ort::generate_ray(sg, a.px[p], a.py[p]);
   } else {
     if (a.seg) lam = a.seg[a.n_seg == 1 ? 0 : r_ld / a.seg_len].lambda_idx;
+    if constexpr ((FEAT & F_WRAY) != 0) wl = a.w[r_ld];
     r.x = a.in.x[r_ld];
     r.y = a.in.y[r_ld];
     r.z = a.in.z[r_ld];
@@ -371,7 +409,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
   }
   for (int si = a.start_surface; si < a.n_surf; ++si) {
     const ort_surface s = cst(a.surf)[si];
-    const ort_surface_optics o = optics_at<FEAT>(a, lam, si);
+    const ort_surface_optics o = surface_optics<FEAT>(a, s, lam, si, wl);
     localize(a, s, r);
     const bool is_plane = s.geometry == ORT_GEOM_PLANE;
     const double t = is_plane ? ort::distance_plane(r)
@@ -408,10 +446,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
       }
     }
   }
-  if (a.final_mat >= 0)
-    ort::propagate(r, a.final_thickness,
-                   (FEAT & F_MONO) ? cst(a.alpha_tab)[a.final_mat]
-                                   : tab(a.alpha_tab, a.n_lambda, a.n_mat, lam, a.final_mat));
+  if (a.final_mat >= 0) ort::propagate(r, a.final_thickness, final_alpha<FEAT>(a, lam, wl));
   if (!active) return;
   a.out.x[rid] = r.x;
   a.out.y[rid] = r.y;
@@ -645,6 +680,11 @@ typedef void (*GeomFn)(const KArgs, const GArgs);
 KernelFn select_trace(uint32_t feat);      // Newton lenses, any F_GEN / F_REC  (ort_k_trace*.hip)
 KernelFn select_closed(uint32_t feat);     // closed-form lenses                (ort_k_closed.hip)
 KernelFn select_generate();                // ray generation only               (ort_k_closed.hip)
+KernelFn select_trace_w(uint32_t feat);    // Newton lenses, per-ray wavelengths (ort_k_trace_w.hip)
+// n(w), k(w) of one material (ort_material_nk)                            (ort_k_closed.hip)
+void launch_material_nk(const ort_material* mats, const double* coef, int32_t mat,
+                        const double* w, int64_t n, double* n_out, double* k_out,
+                        hipStream_t stream);
 VjpFn select_vjp(int tangents, uint32_t km);  // tangents 1, 2 or 4             (ort_k_vjp*.hip)
 GeomFn select_geom(uint32_t km);           // per-geometry primitives           (ort_k_geom.hip)
 int launch_pupil(const ort_pupil& d, double* px, double* py, hipStream_t stream);  // ort_k_pupil.hip

@@ -40,6 +40,7 @@ class LensTable:
     final_mat: int
     final_thickness: float
     materials: list = field(default_factory=list)
+    mat_table: np.ndarray = None  # _abi.MATERIAL [n_mat] (per-ray wavelengths)
     n_rec: int = 0
     rec_surfaces: list = field(default_factory=list)  # traced-surface indices recorded
     # Zernike coefficients held in device tensors: (first zern row, tensor). Their rows
@@ -87,7 +88,8 @@ class LensTable:
     def fingerprint(self):
         """Bytes of everything the device reads: equal fingerprints trace identically."""
         parts = [np.ascontiguousarray(a).tobytes() for a in
-                 (self.surfaces, self.cs_ops, self.coef, self.zern, self.n_tab, self.alpha_tab)]
+                 (self.surfaces, self.cs_ops, self.coef, self.zern, self.n_tab, self.alpha_tab,
+                  self.mat_table)]
         parts.append(np.array([self.final_mat], dtype=np.int64).tobytes())
         parts.append(np.array([self.final_thickness], dtype=np.float64).tobytes())
         return b"".join(parts)
@@ -205,6 +207,23 @@ def lower_surface_group(surface_group, wavelengths, record=False, skip_object=Tr
     final = surfs[-1]
     final_mat = mat_id(final.material_post)
 
+    # per-ray dispersion records (used only when a batch carries per-ray wavelengths),
+    # their coefficient / tabulated-k blocks after everything else in coef
+    mat_table = np.zeros(len(mats), dtype=_abi.MATERIAL)
+    for mi, m in enumerate(mats):
+        kind, cc, kw, kv, n_const, k_const = m.lower()
+        row = mat_table[mi]
+        row["kind"] = kind
+        row["n_coef"] = len(cc) // 2 if kind == _abi.MAT_TABULATED else len(cc)
+        row["coef_off"] = len(coef)
+        coef.extend(cc)
+        row["k_len"] = len(kw)
+        row["k_off"] = len(coef)
+        coef.extend(kw)
+        coef.extend(kv)
+        row["n_const"] = n_const
+        row["k_const"] = k_const
+
     cs = np.zeros(max(1, len(ops)), dtype=_abi.CS_OP)
     for i, (kind, p) in enumerate(ops):
         cs[i]["kind"] = kind
@@ -232,6 +251,7 @@ def lower_surface_group(surface_group, wavelengths, record=False, skip_object=Tr
         final_mat=final_mat,
         final_thickness=scalar(final.thickness),
         materials=mats,
+        mat_table=mat_table,
         n_rec=len(rec_set),
         rec_surfaces=rec_set,
         device_coeffs=device_coeffs,

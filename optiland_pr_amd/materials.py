@@ -68,6 +68,10 @@ class IdealMaterial(BaseMaterial):
     def key(self):
         return ("ideal", float(self.index[0]), float(self.absorp[0]))
 
+    def lower(self):
+        """-> (kind, coefficients, k wavelengths, k values, n_const, k_const)."""
+        return 0, [], [], [], float(self.index[0]), float(self.absorp[0])
+
     def __repr__(self):
         return f"IdealMaterial(n={self.index[0]}, k={self.absorp[0]})"
 
@@ -101,6 +105,10 @@ class Material(BaseMaterial):
 
     def key(self):
         return ("glass", self.source)
+
+    def lower(self):
+        return lower_dispersion(self._n_formula, self.coefficients, self._k_wavelength,
+                                self._k, self._n_wavelength, self._n)
 
     def __repr__(self):
         return f"Material({self.name!r}, {self.reference!r})"
@@ -189,6 +197,39 @@ class Material(BaseMaterial):
 
     def _tabulated_n(self, w):  # :422-428
         return np.interp(w, self._n_wavelength, self._n)
+
+
+def lower_dispersion(formula, coefficients, k_wavelength, k, n_wavelength, n):
+    """Per-ray dispersion record of a catalog material (include/optiland_rt.h
+    ort_material) -> (kind, coefficients, k wavelengths, k values, n_const, k_const):
+    the formula id and its coefficients with the wavelength-independent subexpressions
+    formed here in NumPy exactly as the reference forms them on every call
+    (material_file.py:250-428: 1 + C0, C ** 2, C3 ** C4, C7 ** C8), and the tabulated k
+    data (:219-249)."""
+    kw = [] if k is None or k_wavelength is None else [float(v) for v in np.ravel(k_wavelength)]
+    kv = [] if not kw else [float(v) for v in np.ravel(k)]
+    if formula in ("tabulated n", "tabulated nk"):
+        return (10, [float(v) for v in np.ravel(n_wavelength)] + [float(v) for v in np.ravel(n)],
+                kw, kv, 0.0, 0.0)
+    fid = int(str(formula).split()[-1])
+    c = [np.atleast_1d(np.asarray(v, dtype=np.float64)) for v in np.ravel(coefficients)]
+    f1 = lambda v: float(np.ravel(v)[0])  # noqa: E731
+    if fid in (1, 2, 3, 5, 6) and len(c) % 2 == 0:
+        raise ValueError(f"Invalid coefficients for dispersion formula {fid}.")
+    if fid in (1, 2, 6):  # n0 = 1 + C0, pairs (B, C); C ** 2 for the Sellmeier form
+        out = [f1(1 + c[0])]
+        for i in range(1, len(c), 2):
+            out += [f1(c[i]), f1(c[i + 1] ** 2 if fid == 1 else c[i + 1])]
+    elif fid == 4:
+        if len(c) < 9 or len(c) % 2 == 0:
+            raise ValueError("Invalid coefficients for dispersion formula 4.")
+        out = [f1(c[0]), f1(c[1]), f1(c[2]), f1(c[3] ** c[4]), f1(c[5]), f1(c[6]),
+               f1(c[7] ** c[8])] + [f1(v) for v in c[9:]]
+    elif fid == 8 and len(c) != 4:
+        raise ValueError("Invalid coefficients for dispersion formula 8.")
+    else:  # 3, 5, 7, 8, 9: the coefficients as they are
+        out = [f1(v) for v in c]
+    return fid, out, kw, kv, 0.0, 0.0
 
 
 def configure_material(spec):

@@ -130,6 +130,8 @@ class DeviceLens:
         self.alpha_tab = torch.as_tensor(np.ascontiguousarray(table.alpha_tab),
                                          dtype=torch.float64, device=d)
         self.optics = _to_device_bytes(table.optics, d)
+        mt = table.mat_table if table.mat_table is not None else np.zeros(1, _abi.MATERIAL)
+        self.mats = _to_device_bytes(mt, d)
         mask = 0
         for g in np.unique(table.surfaces["geometry"]):
             mask |= 1 << int(g)
@@ -139,7 +141,7 @@ class DeviceLens:
             self.zern.data_ptr(), self.n_tab.data_ptr(), self.alpha_tab.data_ptr(),
             self.optics.data_ptr(),
             table.n_surfaces, len(table.wavelengths), table.n_tab.shape[1], table.final_mat,
-            mask, 0, table.final_thickness)
+            mask, 0, table.final_thickness, self.mats.data_ptr())
         self.newton = table.newton_surfaces
         self.sched_cache: dict = {}
 
@@ -314,8 +316,10 @@ def trace_pupil(dlens: DeviceLens, segments, px, py, out: RealRays, n_rays,
 
 def trace_rays(dlens: DeviceLens, rays_in: RealRays, rays_out: RealRays, group_len=None,
                keys=(), rec=None, newton_mode="reference", start_surface=0, segments=None,
-               seg_len=None):
-    """Trace resident rays (ort_trace_sequential); rays_out may be rays_in (in place)."""
+               seg_len=None, per_ray_w=False):
+    """Trace resident rays (ort_trace_sequential); rays_out may be rays_in (in place).
+    per_ray_w: n and k per ray from rays_in.w (the lens's material tables) instead of
+    the per-wavelength tables."""
     lib = _native.load()
     n = len(rays_in)
     group_len = group_len or max(n, 1)
@@ -325,6 +329,13 @@ def trace_rays(dlens: DeviceLens, rays_in: RealRays, rays_out: RealRays, group_l
         batch = _native.ort_batch(n, seg_len, group_len, len(segments), 0, seg_dev.data_ptr())
     else:
         batch = _native.ort_batch(n, max(n, 1), group_len, 0, 0, None)
+    w_keep = None
+    if per_ray_w:
+        w_keep = rays_in.w.to(device=dlens.device, dtype=torch.float64).reshape(-1)
+        w_keep = w_keep.expand(n).contiguous() if w_keep.numel() == 1 else w_keep.contiguous()
+        if w_keep.numel() != n:
+            raise ValueError("rays.w must hold one wavelength per ray")
+        batch.w = w_keep.data_ptr()
     in_c, out_c = rays_in.c_struct(), rays_out.c_struct()
 
     def launch(opt, stats, status):
@@ -341,6 +352,7 @@ def trace_rays(dlens: DeviceLens, rays_in: RealRays, rays_out: RealRays, group_l
             setattr(src, a, getattr(rays_in, a).clone())
         in_c = src.c_struct()
     _run(dlens, launch, n, group_len, list(keys), newton_mode)
+    del w_keep  # (the launches above are ordered on the stream before any reuse)
     return seg_dev
 
 
@@ -502,10 +514,10 @@ def trace_surface_group(sg, rays: RealRays, skip=0, newton_mode="reference"):
     """SurfaceGroup.trace(rays, skip) (surface_group.py:232-244): in-place trace of
     resident RealRays through the traced surfaces (no image-space propagate)."""
     w = torch.unique(rays.w)
-    if w.numel() != 1:
-        raise ValueError("SurfaceGroup.trace on the MI355X core expects one wavelength per "
-                         "call (the reference traces one wavelength per Optic.trace)")
-    wl = float(w.item())
+    # one wavelength: n / k from the per-wavelength tables (the common Optic.trace case);
+    # several: every ray's own n(w), k(w) from the material tables in the kernel
+    per_ray = w.numel() != 1
+    wl = float(w[0].item())
     table = lower_surface_group(sg, [wl], record=(sg.record == "all"))
     # SurfaceGroup.trace does not include the image-space propagate of RealRayTracer
     table.final_mat = -1
@@ -520,7 +532,7 @@ def trace_surface_group(sg, rays: RealRays, skip=0, newton_mode="reference"):
         for a in (*_abi.RAY_FIELDS, "w"):
             setattr(rays0, a, getattr(rays, a).clone())
     trace_rays(dlens, rays, rays, rec=rec, newton_mode=newton_mode,
-               start_surface=max(int(skip) - 1, 0))
+               start_surface=max(int(skip) - 1, 0), per_ray_w=per_ray)
     if rec is not None:
         _record_into(sg, rec, n, table.rec_surfaces, rays0)
     return rays
@@ -586,3 +598,16 @@ def geometry_distance(geometry, rays):
 
     _run(dl, launch, n, max(n, 1), [("distance", n)])
     return t
+
+
+def material_nk(dlens: DeviceLens, mat: int, w):
+    """(n, k) of lens material `mat` at device wavelengths w (ort_material_nk): the per-ray
+    dispersion the kernels evaluate when rays carry their own wavelengths."""
+    lib = _native.load()
+    w = _as_device(w, dlens.device)
+    n_out = torch.empty_like(w)
+    k_out = torch.empty_like(w)
+    rc = lib.ort_material_nk(C.byref(dlens.c), int(mat), _ptr(w), w.numel(), _ptr(n_out),
+                             _ptr(k_out), _stream_handle())
+    _native.check(rc, "ort_material_nk")
+    return n_out, k_out

@@ -813,6 +813,68 @@ def propagate(r: Rays, t, alpha):
         r.i = r.i * np.exp(-alpha * t * 1e3)
 
 
+def propagate_w(r: Rays, t, k, w):
+    """homogeneous.py:30-57 with per-ray k(w) and w: absorption when any k > 0."""
+    r.x = r.x + t * r.L
+    r.y = r.y + t * r.M
+    r.z = r.z + t * r.N
+    if np.any(k > 0):
+        alpha = 4 * np.pi * k / w
+        r.i = r.i * np.exp(-alpha * t * 1e3)
+
+
+# -- per-ray dispersion (materials/material_file.py:219-428 on the lowered ort_material
+#    records: wavelength-independent subexpressions were formed by the host lowering) --
+def material_n(table, mi, w):
+    m = table.mat_table[mi]
+    kind, nc, off = int(m["kind"]), int(m["n_coef"]), int(m["coef_off"])
+    c = table.coef[off:off + (2 * nc if kind == _abi.MAT_TABULATED else nc)]
+    if kind == _abi.MAT_IDEAL:  # ideal.py: constant n
+        return np.full_like(w, float(m["n_const"]))
+    if kind == _abi.MAT_TABULATED:  # :422-428
+        return np.interp(w, c[:nc], c[nc:])
+    if kind in (1, 2):  # Sellmeier (C ** 2 pre-formed) / Sellmeier-2
+        n = c[0]
+        for k in range(1, len(c), 2):
+            n = n + c[k] * w**2 / (w**2 - c[k + 1])
+        return np.sqrt(n)
+    if kind in (3, 5):  # polynomial / Cauchy
+        n = c[0]
+        for k in range(1, len(c), 2):
+            n = n + c[k] * w ** c[k + 1]
+        return np.sqrt(n) if kind == 3 else n
+    if kind == 4:
+        n = c[0] + c[1] * w ** c[2] / (w**2 - c[3]) + c[4] * w ** c[5] / (w**2 - c[6])
+        for k in range(7, len(c), 2):
+            n = n + c[k] * w ** c[k + 1]
+        return np.sqrt(n)
+    if kind == 6:
+        n = c[0]
+        for k in range(1, len(c), 2):
+            n = n + c[k] / (c[k + 1] - w**-2)
+        return n
+    if kind == 7:
+        n = c[0] + c[1] / (w**2 - 0.028) + c[2] * (1 / (w**2 - 0.028)) ** 2
+        for k in range(3, len(c)):
+            n = n + c[k] * w ** (2 * (k - 2))
+        return n
+    if kind == 8:
+        b = c[0] + c[1] * w**2 / (w**2 - c[2]) + c[3] * w**2
+        return np.sqrt((1 + 2 * b) / (1 - b))
+    if kind == 9:
+        n = c[0] + c[1] / (w**2 - c[2]) + c[3] * (w - c[4]) / ((w - c[4]) ** 2 + c[5])
+        return np.sqrt(n)
+    raise ValueError(kind)
+
+
+def material_k(table, mi, w):
+    m = table.mat_table[mi]
+    kl, ko = int(m["k_len"]), int(m["k_off"])
+    if kl == 0:
+        return np.full_like(w, float(m["k_const"]))
+    return np.interp(w, table.coef[ko:ko + kl], table.coef[ko + kl:ko + 2 * kl])
+
+
 def _align(r: Rays, nx, ny, nz):
     """real_rays.py:511-547."""
     dot = r.L * nx + r.M * ny + r.N * nz
@@ -904,10 +966,14 @@ def aperture_contains(prog, x, y):
     return stack[-1]
 
 
-def trace_segment(table, rays: Rays, lam: int, record=False, sched=None, start=0):
+def trace_segment(table, rays: Rays, lam: int, record=False, sched=None, start=0, w=None):
     """One reference trace call: SurfaceGroup.trace (surface_group.py:232-244) over the
     traced surfaces, then the image-space propagate (real_ray_tracer.py:84-89).
-    `rays` is modified in place (the reference mutates RealRays)."""
+    `rays` is modified in place (the reference mutates RealRays). w: per-ray
+    wavelengths -- n and k then come from the material records per ray (as the reference
+    evaluates material.n(rays.w)) instead of the lambda-th table row."""
+    if w is not None:
+        return _trace_segment_w(table, rays, w, record, sched, start)
     r = rays
     records = {}
     updates = {}
@@ -953,6 +1019,50 @@ def trace_segment(table, rays: Rays, lam: int, record=False, sched=None, start=0
         # real_ray_tracer.py:84-89 always propagates (by 0 for the samples), and applies
         # absorption only when k>0 of the image-space material.
         propagate(r, table.final_thickness, float(a_tab[table.final_mat]))
+    return TraceResult(r, records, updates)
+
+
+def _trace_segment_w(table, r: Rays, w, record, sched, start):
+    records, updates = {}, {}
+    w = np.asarray(w, dtype=np.float64)
+    for si in range(start, len(table.surfaces)):
+        s = table.surfaces[si]
+        g = int(s["geometry"])
+        flags = int(s["flags"])
+        ct = s["cs_t"]
+        r.x, r.y, r.z = r.x + -float(ct[0]), r.y + -float(ct[1]), r.z + -float(ct[2])
+        apply_cs(r, table.cs_ops[int(s["cs_loc_off"]):int(s["cs_loc_off"]) + int(s["n_cs_loc"])])
+        if g == _abi.GEOM_PLANE:
+            t = distance_plane(r)
+        elif g == _abi.GEOM_STANDARD:
+            t = distance_conic(r, float(s["radius"]), float(s["conic"]),
+                               bool(flags & _abi.SURF_RADIUS_INF))
+        else:
+            t, updates[si] = distance_newton(
+                r, table, s, None if sched is None else sched.get(si))
+        mp, mq = int(s["mat_pre"]), int(s["mat_post"])
+        n_pre = material_n(table, mp, w)
+        propagate_w(r, t, material_k(table, mp, w), w)
+        r.opd = r.opd + np.abs(t * n_pre)  # standard_surface.py:218
+        if flags & _abi.SURF_APERTURE:
+            radius2 = r.x**2 + r.y**2
+            inside = (radius2 <= float(s["ap_rmax2"])) & (radius2 >= float(s["ap_rmin2"]))
+            r.i = np.where(~inside, np.zeros_like(r.i), r.i)
+        if flags & _abi.SURF_APERTURE_PROG:
+            off, ln = int(s["ap_off"]), int(s["ap_len"])
+            inside = aperture_contains(table.coef[off:off + ln], r.x, r.y)
+            r.i = np.where(~inside, np.zeros_like(r.i), r.i)
+        nx, ny, nz = surface_normal(r, table, s)
+        if flags & _abi.SURF_REFLECTIVE:
+            reflect(r, nx, ny, nz)
+        else:
+            refract(r, nx, ny, nz, n_pre, material_n(table, mq, w))
+        apply_cs(r, table.cs_ops[int(s["cs_glob_off"]):int(s["cs_glob_off"]) + int(s["n_cs_glob"])])
+        r.x, r.y, r.z = r.x + float(ct[0]), r.y + float(ct[1]), r.z + float(ct[2])
+        if record:
+            records[si] = r.copy()
+    if table.final_mat >= 0:
+        propagate_w(r, table.final_thickness, material_k(table, table.final_mat, w), w)
     return TraceResult(r, records, updates)
 
 

@@ -539,6 +539,50 @@ def full_size_summaries():
     return res
 
 
+MIXED_W_CASES = {  # name -> (builder, field (Hx, Hy), pupil n, wavelength range)
+    "cooke": (CookeTriplet, (0.0, 0.7), 24, (0.42, 0.75)),
+    "dg": (DoubleGauss, (0.0, 1.0), 24, (0.45, 0.70)),
+    "freeform": (None, (0.3, 0.6), 20, (0.45, 0.70)),
+}
+
+
+def mixed_wavelength_goldens():
+    """SurfaceGroup.trace (surface_group.py:232-244) of RealRays whose every ray has its
+    own wavelength: the materials evaluate n(rays.w) and k(rays.w) per ray. Rays are
+    generated at the primary wavelength, then given seeded random wavelengths. Also
+    n(w), k(w) of every baked catalog glass on a wavelength sweep."""
+    from optiland.rays import RealRays
+
+    out = {}
+    rng = np.random.default_rng(123)
+    for name, (builder, (hx, hy), num, (w0, w1)) in MIXED_W_CASES.items():
+        lens = freeform() if builder is None else builder()
+        wl = float(lens.primary_wavelength)
+        d = create_distribution("uniform")
+        d.generate_points(num)
+        rays = RayGenerator(lens).generate_rays(hx, hy, d.x, d.y, wl)
+        n = np.asarray(rays.x).size
+        w = rng.uniform(w0, w1, n)
+        r = RealRays(np.asarray(rays.x), np.asarray(rays.y), np.asarray(rays.z),
+                     np.asarray(rays.L), np.asarray(rays.M), np.asarray(rays.N),
+                     np.asarray(rays.i), w)
+        for a in ("x", "y", "z", "L", "M", "N", "i"):
+            out[f"{name}/in_{a}"] = np.array(getattr(r, a), dtype=np.float64)
+        out[f"{name}/w"] = w
+        lens.surface_group.trace(r)
+        for a in ("x", "y", "z", "L", "M", "N", "i", "opd"):
+            out[f"{name}/{a}"] = np.array(getattr(r, a), dtype=np.float64)
+    sweep = np.linspace(0.36, 1.6, 157)
+    with open(os.path.join(REPO, "optiland_pr_amd", "data", "glasses.json")) as f:
+        glasses = json.load(f)
+    for key, e in glasses.items():
+        m = Material(e["name"], e["reference"]) if e["reference"] else Material(e["name"])
+        out[f"glass/{key}/n"] = np.asarray(m.n(sweep), dtype=np.float64) * np.ones_like(sweep)
+        out[f"glass/{key}/k"] = np.asarray(m.k(sweep), dtype=np.float64) * np.ones_like(sweep)
+    out["glass/w"] = sweep
+    np.savez_compressed(os.path.join(HERE, "mixed_w.npz"), **out)
+
+
 DIST_CASES = [("random", 1000, {"seed": 7}), ("uniform", 33, {}), ("uniform", 128, {}),
               ("hexapolar", 6, {}), ("hexapolar", 17, {}), ("ring", 13, {}),
               ("line_x", 21, {}), ("line_y", 20, {}), ("positive_line_x", 9, {}),
@@ -613,6 +657,9 @@ def main():
     if "--distributions" in sys.argv:
         distribution_goldens()
         return
+    if "--mixed-w" in sys.argv:
+        mixed_wavelength_goldens()
+        return
     if "--apertures" in sys.argv:
         aperture_goldens()
         return
@@ -638,6 +685,7 @@ def main():
               file=sys.stderr)
     distribution_goldens()
     aperture_goldens()
+    mixed_wavelength_goldens()
     index["_analysis"] = analysis_goldens()
     index["_full"] = full_size_summaries()
     with open(os.path.join(HERE, "index.json"), "w") as f:

@@ -1,0 +1,67 @@
+"""Per-ray wavelengths: the oracle's per-ray dispersion restatement
+(oracle/trace_np.py material_n / material_k / _trace_segment_w, from the lowered
+ort_material records) against the reference's own outputs (tests/golden/mixed_w.npz,
+gen_golden.py mixed_wavelength_goldens): every baked glass's n(w), k(w) on a 157-point
+sweep, and SurfaceGroup.trace of RealRays with a different wavelength on every ray
+(Cooke triplet, DoubleGauss, the freeform Newton lens). Bit-exact: same NumPy
+operations on the same doubles.
+"""
+
+import os
+
+import numpy as np
+import pytest
+
+from oracle import trace_np
+from optiland_pr_amd.lowering import lower_surface_group
+from optiland_pr_amd.materials import Material
+from tests._cases import build_lens
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "mixed_w.npz")
+CASES = ("cooke", "dg", "freeform")
+
+
+def _golden():
+    d = np.load(GOLDEN, allow_pickle=False)
+    return {k: d[k] for k in d.files}
+
+
+def _glass_keys(g):
+    return sorted({k.split("/")[1] for k in g if k.startswith("glass/") and k != "glass/w"})
+
+
+def test_glass_dispersion_bit_exact():
+    from types import SimpleNamespace
+
+    from optiland_pr_amd import _abi
+
+    g = _golden()
+    w = g["glass/w"]
+    keys = _glass_keys(g)
+    assert len(keys) >= 15
+    for key in keys:
+        name, _, ref = key.partition("|")
+        m = Material(name, ref or None)
+        kind, cc, kw, kv, n_const, k_const = m.lower()
+        rec = np.zeros(1, dtype=_abi.MATERIAL)
+        rec[0] = (kind, len(cc) // 2 if kind == _abi.MAT_TABULATED else len(cc), 0, len(kw),
+                  len(cc), 0, n_const, k_const)
+        table = SimpleNamespace(mat_table=rec, coef=np.array(cc + kw + kv, dtype=np.float64))
+        np.testing.assert_array_equal(trace_np.material_n(table, 0, w), g[f"glass/{key}/n"],
+                                      err_msg=key)
+        np.testing.assert_array_equal(trace_np.material_k(table, 0, w), g[f"glass/{key}/k"],
+                                      err_msg=key)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_mixed_wavelength_trace_bit_exact(name):
+    g = _golden()
+    lens = build_lens(name)
+    table = lower_surface_group(lens.surface_group, [lens.primary_wavelength])
+    table.final_mat = -1  # SurfaceGroup.trace: no image-space propagate
+    rays = trace_np.Rays(*(g[f"{name}/in_{a}"].copy() for a in ("x", "y", "z", "L", "M", "N", "i")))
+    with np.errstate(all="ignore"):
+        res = trace_np.trace_segment(table, rays, 0, w=g[f"{name}/w"])
+    for a in ("x", "y", "z", "L", "M", "N", "i", "opd"):
+        np.testing.assert_array_equal(getattr(res.rays, a), g[f"{name}/{a}"], err_msg=a)
+    assert np.unique(g[f"{name}/w"]).size == g[f"{name}/w"].size  # truly per-ray
