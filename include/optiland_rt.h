@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define ORT_ABI_VERSION 8
+#define ORT_ABI_VERSION 9
 #define ORT_MAX_SURFACES 64
 
 /* ---- geometry kinds ----------------------------------- */
@@ -72,6 +72,34 @@ enum ort_surface_flags {
                                  /* (both op lists empty)                                  */
 };
 
+/* ---- interaction models (optiland/interactions) ----------------------------------
+ * What happens at the surface after the ray reaches it (standard_surface.py:225). The
+ * parameters live in lens.coef at ort_surface.ia_off:
+ *   REFRACT_REFLECT  (none)    refractive_reflective_model.py:32-55 + real_rays.py:141-181
+ *   THIN_LENS        f         thin_lens_interaction_model.py:55-113: paraxial phase
+ *                              transformation; leaves the direction unnormalised (N = 1),
+ *                              the next propagation normalises it (homogeneous.py:55-57)
+ *   PHASE            kind, efficiency, then the profile's parameters (ort_phase_kind):
+ *                              phase_interaction_model.py:45-132 (generalised Snell's law)
+ *                    CONSTANT  phase                          phase/constant.py
+ *                    LINEAR    K_x, K_y (order 2 pi / period times cos / sin of the angle,
+ *                              phase/linear_grating.py:51-54)
+ *                    RADIAL    n, a_1 .. a_n (phi = sum a_i r^(2i), phase/radial.py)
+ *   DIFFRACTIVE      order m, period, then
+ *                    0, -sin(angle), cos(angle)   PlaneGrating: constant grating vector
+ *                                                 (plane_grating.py:105-124)
+ *                    1, tan(angle), R**2, R**3, k + 1   StandardGratingGeometry: grating
+ *                                                 vector from the groove tangent
+ *                                                 (standard_grating.py:93-146, 224-247)
+ *                              diffractive_model.py:28-61 + real_rays.py:183-498 */
+enum ort_interaction {
+  ORT_IA_REFRACT_REFLECT = 0,
+  ORT_IA_THIN_LENS = 1,
+  ORT_IA_PHASE = 2,
+  ORT_IA_DIFFRACTIVE = 3
+};
+enum ort_phase_kind { ORT_PHASE_CONSTANT = 0, ORT_PHASE_LINEAR = 1, ORT_PHASE_RADIAL = 2 };
+
 /* ---- coordinate-system op (coordinate_system.py:73-107, real_rays.py:90-130) ---- */
 enum ort_cs_kind {
   ORT_CS_TRANSLATE = 0, /* p = (dx, dy, dz)                         rays/base.py:28-42 */
@@ -113,7 +141,10 @@ typedef struct ort_surface {
                       /* ops; globalize = the glob ops, then x + cs_t                  */
   int32_t ap_off;     /* ORT_SURF_APERTURE_PROG: aperture program at lens.coef[ap_off] */
   int32_t ap_len;     /* its length in doubles                                       */
-} ort_surface; /* 128 bytes */
+  int32_t interaction; /* enum ort_interaction                                        */
+  int32_t ia_off;      /* its parameter block at lens.coef[ia_off]                    */
+  double reserved;
+} ort_surface; /* 144 bytes */
 
 /* Aperture programs (the physical_apertures package): postfix, each op a double opcode followed
  * by its operands; primitives push contains(x, y) of the ray's local (x, y), the boolean
@@ -146,7 +177,7 @@ typedef struct ort_surface_optics {
   double u;         /* n_pre / n_post (real_rays.py:152); the same IEEE quotient the  */
                     /* reference forms per ray                                        */
   double alpha_pre; /* 4 pi k / lambda of material_pre, 0 when k == 0 (homogeneous.py) */
-  double reserved;
+  double n_post;    /* n of material_post (thin-lens / phase / grating interactions)  */
 } ort_surface_optics; /* 32 bytes */
 
 /* One Zernike term: c * norm * R_n^|m|(rho) * {cos m phi | sin |m| phi}
@@ -209,10 +240,15 @@ typedef struct ort_lens {
   int32_t final_mat;       /* material_post of the last surface (image space); < 0:  *
                             * no image-space propagate (bare SurfaceGroup.trace)     */
   uint32_t geometry_mask;  /* OR of (1u << geometry) over the surfaces; selects the  */
-  int32_t reserved;        /* kernel specialisation (no Newton code for sphere lenses) */
+                           /* kernel specialisation (no Newton code for sphere lenses) */
+  uint32_t interaction_mask; /* OR of (1u << interaction) over the surfaces: anything   */
+                             /* beyond REFRACT_REFLECT selects the interaction kernels  */
   double final_thickness;  /* real_ray_tracer.py:84-89 image-space propagate distance */
   const ort_material* materials; /* [n_mat]: per-ray dispersion (ort_batch.w); may be  *
                                   * NULL when no batch carries per-ray wavelengths    */
+  const double* wavelengths; /* [n_lambda] um, the wavelength of each table row (phase  *
+                              * and grating interactions use it); may be NULL when      *
+                              * interaction_mask has no PHASE / DIFFRACTIVE bit         */
 } ort_lens;
 
 /* Ray state, structure of arrays, one double per ray per attribute (device). */

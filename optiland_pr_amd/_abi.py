@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import numpy as np
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 VJP_UNROLLED = 0
 VJP_ADJOINT = 1
 AP_RADIAL = 1
@@ -51,6 +51,15 @@ SURF_APERTURE = 1 << 2
 SURF_RECORD = 1 << 3
 SURF_TRANSLATE = 1 << 4
 SURF_APERTURE_PROG = 1 << 5
+
+# enum ort_interaction / ort_phase_kind
+IA_REFRACT_REFLECT = 0
+IA_THIN_LENS = 1
+IA_PHASE = 2
+IA_DIFFRACTIVE = 3
+PHASE_CONSTANT = 0
+PHASE_LINEAR = 1
+PHASE_RADIAL = 2
 
 # enum ort_cs_kind
 CS_TRANSLATE = 0
@@ -98,13 +107,16 @@ SURFACE = np.dtype(
         ("cs_t", "<f8", (3,)),
         ("ap_off", "<i4"),
         ("ap_len", "<i4"),
+        ("interaction", "<i4"),
+        ("ia_off", "<i4"),
+        ("reserved", "<f8"),
     ],
     align=True,
 )
-assert SURFACE.itemsize == 128
+assert SURFACE.itemsize == 144
 
 SURFACE_OPTICS = np.dtype(
-    [("n_pre", "<f8"), ("u", "<f8"), ("alpha_pre", "<f8"), ("reserved", "<f8")], align=True
+    [("n_pre", "<f8"), ("u", "<f8"), ("alpha_pre", "<f8"), ("n_post", "<f8")], align=True
 )
 assert SURFACE_OPTICS.itemsize == 32
 

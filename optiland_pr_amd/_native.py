@@ -27,9 +27,10 @@ class ort_lens(C.Structure):
         ("n_mat", C.c_int32),
         ("final_mat", C.c_int32),
         ("geometry_mask", C.c_uint32),
-        ("reserved", C.c_int32),
+        ("interaction_mask", C.c_uint32),
         ("final_thickness", C.c_double),
         ("materials", C.c_void_p),
+        ("wavelengths", C.c_void_p),
     ]
 
 

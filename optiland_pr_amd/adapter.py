@@ -32,12 +32,15 @@ from .geometries import (
     ForbesSurfaceConfig,
     OddAsphere,
     Plane,
+    PlaneGrating,
     PolynomialGeometry,
     StandardGeometry,
+    StandardGratingGeometry,
     ToroidalGeometry,
     ZernikePolynomialGeometry,
 )
 from .coordinate_system import CoordinateSystem
+from .interactions import BaseInteractionModel
 from .materials import BaseMaterial, lower_dispersion
 
 _ORIGINAL = {}
@@ -105,6 +108,13 @@ def _geometry(g):
     cs = _cs(g.cs)
     if name == "Plane":
         return Plane(cs)
+    if name == "PlaneGrating":
+        return PlaneGrating(cs, _f(g.grating_order), _f(g.grating_period),
+                            _f(g.groove_orientation_angle))
+    if name == "StandardGratingGeometry":
+        return StandardGratingGeometry(cs, _f(g.radius), _f(g.grating_order),
+                                       _f(g.grating_period), _f(g.groove_orientation_angle),
+                                       _f(g.k))
     if name == "StandardGeometry":
         return StandardGeometry(cs, _f(g.radius), _f(g.k))
     if name == "EvenAsphere":
@@ -143,8 +153,10 @@ def _geometry(g):
 class _Surf:
     """Duck-typed stand-in for optiland_pr_amd.surfaces.Surface during lowering."""
 
-    def __init__(self, geometry, pre, post, is_reflective, aperture, thickness):
+    def __init__(self, geometry, pre, post, is_reflective, aperture, thickness,
+                 interaction_model=None):
         self.geometry = geometry
+        self.interaction_model = interaction_model
         self.material_pre = pre
         self.material_post = post
         self.is_reflective = is_reflective
@@ -183,10 +195,15 @@ def lower_reference_group(ref_group, wavelengths, record=False):
     surfs = []
     for s in ref_group.surfaces[1:]:
         im = s.interaction_model
-        if type(im).__name__ != "RefractiveReflectiveModel":
-            raise Unsupported(type(im).__name__)
         if getattr(im, "coating", None) is not None or getattr(im, "bsdf", None) is not None:
             raise Unsupported("coating/bsdf")
+        if type(im).__name__ not in ("RefractiveReflectiveModel", "ThinLensInteractionModel",
+                                     "PhaseInteractionModel", "DiffractiveInteractionModel"):
+            raise Unsupported(type(im).__name__)
+        try:  # the reference's to_dict schema (interactions/*.py, phase/*.py)
+            native_im = BaseInteractionModel.from_dict(_plain(im.to_dict()))
+        except (ValueError, KeyError, TypeError) as e:
+            raise Unsupported(type(im).__name__) from e
         for m in (s.material_pre, s.material_post):
             if type(m.propagation_model).__name__ != "HomogeneousPropagation":
                 raise Unsupported("propagation model")
@@ -197,7 +214,7 @@ def lower_reference_group(ref_group, wavelengths, record=False):
             except (ValueError, KeyError, AttributeError) as e:
                 raise Unsupported(type(s.aperture).__name__) from e
         surfs.append(_Surf(_geometry(s.geometry), mat(s.material_pre), mat(s.material_post),
-                           bool(im.is_reflective), ap, _f(s.thickness)))
+                           bool(im.is_reflective), ap, _f(s.thickness), native_im))
     # lower_surface_group skips ObjectSurface instances; pass the traced surfaces only
     return lower_surface_group(_Group(surfs), wavelengths, record=record)
 

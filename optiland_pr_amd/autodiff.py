@@ -225,6 +225,9 @@ def vjp(dlens, seg_dev, px, py, n, seg_len, sched_dev, tables, n_param, cot, gra
     (zern_param, surf_tangent, final_tangent), each possibly None; cot: 8 tensors / None."""
     from .raytrace import _ptr, _stream_handle
 
+    if dlens.table.interaction_mask & ~(1 << _abi.IA_REFRACT_REFLECT):
+        raise NotImplementedError("autograd through thin-lens, phase or grating surfaces is "
+                                  "not implemented by the trace core (no derivative kernels)")
     lib = _native.load()
     n_seg = seg_dev.numel() // _abi.SEGMENT.itemsize
     batch = _native.ort_batch(n, seg_len, n, n_seg, int(pupil_per_ray), seg_dev.data_ptr())

@@ -86,6 +86,12 @@ int fill_args(KArgs& a, const ort_lens* lens, const ort_batch* batch, const ort_
   } else if (lens->n_lambda == 1) {
     feat |= F_MONO;
   }
+  if (lens->interaction_mask & ~(1u << ORT_IA_REFRACT_REFLECT)) {
+    feat |= F_IA;
+    a.lambdas = lens->wavelengths;
+    const uint32_t need_w = (1u << ORT_IA_PHASE) | (1u << ORT_IA_DIFFRACTIVE);
+    if ((lens->interaction_mask & need_w) && !batch->w && !lens->wavelengths) return ORT_ERR_ARG;
+  }
   if (opt->newton_mode != ORT_NEWTON_SCHEDULE && opt->newton_mode != ORT_NEWTON_WAVE)
     return ORT_ERR_ARG;
   return ORT_OK;
@@ -93,7 +99,9 @@ int fill_args(KArgs& a, const ort_lens* lens, const ort_batch* batch, const ort_
 
 int launch(const KArgs& a, uint32_t feat, hipStream_t stream) {
   if (a.n_rays == 0) return ORT_OK;
-  KernelFn fn = (feat & F_KM) == 0 ? select_closed(feat) : select_trace(feat & ~F_MONO);
+  KernelFn fn = (feat & F_IA) != 0    ? select_trace_ia(feat)
+                : (feat & F_KM) == 0 ? select_closed(feat)
+                                     : select_trace(feat & ~F_MONO);
   if (!fn) return ORT_ERR_ARG;
   const int64_t blocks = (a.n_rays + kBlock - 1) / kBlock;
   if (blocks > 0x7fffffff) return ORT_ERR_ARG;
@@ -214,6 +222,7 @@ int ort_trace_pupil_vjp(const ort_lens* lens, const double* px, const double* py
   if (rc) return rc;
   if (opt->newton_mode != ORT_NEWTON_SCHEDULE) return ORT_ERR_ARG;
   if (params->zern_param && (feat & ort::KM_ZERN) == 0) return ORT_ERR_ARG;
+  if (feat & F_IA) return ORT_ERR_ARG;  // no derivative kernels for thin-lens / phase / grating
   a.px = px;
   a.py = py;
   JArgs j{};

@@ -26,6 +26,7 @@
 #include <stdlib.h>
 
 #include "ort_core.h"
+#include "ort_interact.h"
 #include "ort_material.h"
 
 namespace ortk {
@@ -58,6 +59,7 @@ enum : uint32_t {
   F_REC = 1u << 5,   // some surfaces are recorded (standard_surface.py:266-286)
   F_MONO = 1u << 6,  // one wavelength in the lens tables (closed-form kernels only)
   F_WRAY = 1u << 7,  // per-ray wavelengths: n, k from lens.materials (ort_batch.w)
+  F_IA = 1u << 8,    // thin-lens / phase / grating interactions (ort_interaction)
 };
 
 struct KArgs {
@@ -97,6 +99,8 @@ struct KArgs {
   // per-ray wavelengths (F_WRAY)
   const double* w;
   const ort_material* mats;
+  // wavelength of each table row (F_IA: phase / grating interactions)
+  const double* lambdas;
 };
 
 __device__ inline uint64_t wave_and_u64(uint64_t v) {
@@ -147,9 +151,9 @@ __device__ inline ort_surface_optics optics_ray(const KArgs& a, const ort_surfac
   const ort_material mq = cst(a.mats)[s.mat_post];
   ort_surface_optics o;
   o.n_pre = ort::material_n(mp, a.coef, w);
-  o.u = o.n_pre / ort::material_n(mq, a.coef, w);
+  o.n_post = ort::material_n(mq, a.coef, w);
+  o.u = o.n_pre / o.n_post;
   o.alpha_pre = ort::absorption_alpha(ort::material_k(mp, a.coef, w), w);
-  o.reserved = 0.0;
   return o;
 }
 
@@ -265,6 +269,38 @@ __device__ inline double newton_distance(const KArgs& a, const ort_surface& s, i
   return t;
 }
 
+// F_IA: the surface's interaction model after propagation / OPD / clipping
+// (standard_surface.py:225 -> interactions/*.py). unnorm tracks the reference's
+// rays.is_normalized flag, which only a thin lens clears (homogeneous.py:55-57).
+template <uint32_t FEAT>
+__device__ inline void interact(const KArgs& a, const ort_surface& s, ort::Ray& r,
+                                const ort_surface_optics& o, int lam, double wl,
+                                bool& unnorm) {
+  const bool refl = (s.flags & ORT_SURF_REFLECTIVE) != 0;
+  const PD p = cst(a.coef) + s.ia_off;
+  if (s.interaction == ORT_IA_THIN_LENS) {
+    ort::thin_lens(r, p[0], o.n_pre, refl ? -o.n_pre : o.n_post);
+    unnorm = true;
+    return;
+  }
+  double nx, ny, nz;
+  ort::surface_normal<(FEAT & F_KM)>(s, s.radius, s.conic, cst(a.coef), cst(a.zern), kNoSeed,
+                                     r, nx, ny, nz);
+  if (s.interaction == ORT_IA_REFRACT_REFLECT) {
+    if (refl)
+      ort::reflect(r, nx, ny, nz);
+    else
+      ort::refract(r, nx, ny, nz, o.u);
+    return;
+  }
+  double w = wl;
+  if constexpr ((FEAT & F_WRAY) == 0) w = a.n_lambda == 1 ? cst(a.lambdas)[0] : a.lambdas[lam];
+  if (s.interaction == ORT_IA_PHASE)
+    ort::phase_interact(r, p, nx, ny, nz, o.n_pre, refl ? o.n_pre : o.n_post, refl, w);
+  else
+    ort::diffract(r, p, nx, ny, nz, o.n_pre, o.n_post, refl, w);
+}
+
 template <uint32_t FEAT>
 __global__ __launch_bounds__(kBlock) void trace_kernel(const KArgs a) {
   const int64_t rid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -302,6 +338,7 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(const KArgs a) {
     group_uniform = __all(group == g0);
   }
   int range_bits = 0;
+  bool unnorm = false;  // F_IA: rays.is_normalized == False after a thin lens
 
   for (int si = a.start_surface; si < a.n_surf; ++si) {
     const ort_surface s = cst(a.surf)[si];
@@ -320,7 +357,17 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(const KArgs a) {
       }
     }
     const double n_pre = o.n_pre, u = o.u, alpha = o.alpha_pre;
-    if constexpr ((FEAT & F_KM) != 0) {
+    if constexpr ((FEAT & F_IA) != 0) {
+      ort::propagate(r, t, alpha);
+      if (unnorm) {  // homogeneous.py:55-57
+        ort::normalize_dir(r);
+        unnorm = false;
+      }
+      ort::add_opd(r, t, n_pre);
+      if (s.flags & ORT_SURF_APERTURE) ort::clip_radial(r, s.ap_rmax2, s.ap_rmin2);
+      if (s.flags & ORT_SURF_APERTURE_PROG) ort::clip_program(r, cst(a.coef) + s.ap_off, s.ap_len);
+      interact<FEAT>(a, s, r, o, lam, wl, unnorm);
+    } else if constexpr ((FEAT & F_KM) != 0) {
       ort::finish_surface<(FEAT & F_KM)>(r, s, s.radius, s.conic, cst(a.coef), cst(a.zern), kNoSeed, t, n_pre, u,
                                          alpha);
     } else {
@@ -359,7 +406,12 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(const KArgs a) {
   }
   // real_ray_tracer.py:84-89: image-space propagate by the last surface's thickness
   // (final_mat < 0: plain SurfaceGroup.trace, no propagate)
-  if (a.final_mat >= 0) ort::propagate(r, a.final_thickness, final_alpha<FEAT>(a, lam, wl));
+  if (a.final_mat >= 0) {
+    ort::propagate(r, a.final_thickness, final_alpha<FEAT>(a, lam, wl));
+    if constexpr ((FEAT & F_IA) != 0) {
+      if (unnorm) ort::normalize_dir(r);
+    }
+  }
 
   if constexpr ((FEAT & (ort::KM_ZERN | ort::KM_FREE)) != 0) {
     if (range_bits && active && a.status) atomicOr(a.status, range_bits);
@@ -681,6 +733,7 @@ KernelFn select_trace(uint32_t feat);      // Newton lenses, any F_GEN / F_REC  
 KernelFn select_closed(uint32_t feat);     // closed-form lenses                (ort_k_closed.hip)
 KernelFn select_generate();                // ray generation only               (ort_k_closed.hip)
 KernelFn select_trace_w(uint32_t feat);    // Newton lenses, per-ray wavelengths (ort_k_trace_w.hip)
+KernelFn select_trace_ia(uint32_t feat);   // thin-lens / phase / grating lenses (ort_k_trace_ia.hip)
 // n(w), k(w) of one material (ort_material_nk)                            (ort_k_closed.hip)
 void launch_material_nk(const ort_material* mats, const double* coef, int32_t mat,
                         const double* w, int64_t n, double* n_out, double* k_out,

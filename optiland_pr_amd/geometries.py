@@ -102,6 +102,30 @@ class StandardGeometry(BaseGeometry):
         return scalar(self.radius), scalar(self.k), 0.0, 0, 1.0, []
 
 
+class PlaneGrating(Plane):
+    """geometries/plane_grating.py:19-153: a plane carrying a grating (order, period,
+    groove orientation angle) for the diffractive interaction."""
+
+    def __init__(self, coordinate_system, grating_order, grating_period,
+                 groove_orientation_angle):
+        super().__init__(coordinate_system)
+        self.grating_order = grating_order
+        self.grating_period = grating_period
+        self.groove_orientation_angle = groove_orientation_angle
+
+
+class StandardGratingGeometry(StandardGeometry):
+    """geometries/standard_grating.py:25-294: a sphere / conic carrying a grating (its
+    distance and normal are the standard ones, standard_grating.py:148-222)."""
+
+    def __init__(self, coordinate_system, radius, grating_order, grating_period,
+                 groove_orientation_angle, conic=0.0):
+        super().__init__(coordinate_system, radius, conic)
+        self.grating_order = grating_order
+        self.grating_period = grating_period
+        self.groove_orientation_angle = groove_orientation_angle
+
+
 class NewtonRaphsonGeometry(StandardGeometry):
     """geometries/newton_raphson.py:43-168 (conic initial guess + Newton refinement)."""
 

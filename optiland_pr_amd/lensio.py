@@ -30,12 +30,15 @@ from .geometries import (
     ForbesSurfaceConfig,
     OddAsphere,
     Plane,
+    PlaneGrating,
     PolynomialGeometry,
+    StandardGratingGeometry,
     StandardGeometry,
     ToroidalGeometry,
     ZernikePolynomialGeometry,
     scalar,
 )
+from .interactions import BaseInteractionModel, RefractiveReflectiveModel
 from .materials import IdealMaterial, Material
 from .apertures import BaseAperture
 from .surfaces import ObjectSurface, Surface
@@ -72,6 +75,16 @@ def geometry_from_dict(d):
     tol, max_iter = _f(d.get("tol"), 1e-10), int(d.get("max_iter", 100))
     if t == "Plane":
         return Plane(cs)
+    if t in ("PlaneGrating", "StandardGratingGeometry"):
+        # plane_grating.py / standard_grating.py to_dict write "order" / "period" /
+        # "angle" (the reference's own from_dict cannot read them back)
+        order = d.get("grating_order", d.get("order", 0))
+        period = _f(d.get("grating_period", d.get("period")), np.inf)
+        angle = _f(d.get("groove_orientation_angle", d.get("angle")))
+        if t == "PlaneGrating":
+            return PlaneGrating(cs, order, period, angle)
+        return StandardGratingGeometry(cs, _f(d.get("radius"), np.inf), order, period, angle,
+                                       _f(d.get("conic")))
     if t == "StandardGeometry":
         return StandardGeometry(cs, _f(d.get("radius"), np.inf), _f(d.get("conic")))
     if t == "EvenAsphere":
@@ -142,6 +155,9 @@ def geometry_to_dict(g):
                                "norm_radius": g.norm_radius, "terms": terms}
         d["solver_config"] = {"tol": g.tol, "max_iter": g.max_iter}
         return d
+    if isinstance(g, (PlaneGrating, StandardGratingGeometry)):
+        d.update(order=g.grating_order, period=g.grating_period,
+                 angle=g.groove_orientation_angle)
     if isinstance(g, Plane):
         d["radius"] = float("inf")
         return d
@@ -212,9 +228,12 @@ def optic_from_dict(data):
                 if "type" not in apd:
                     apd = dict(apd, type="RadialAperture")
                 aperture = BaseAperture.from_dict(apd)
+            imd = sd.get("interaction_model")  # standard_surface.py:352-365
+            model = (BaseInteractionModel.from_dict(imd) if imd else
+                     RefractiveReflectiveModel(is_reflective=bool(sd.get("is_reflective", False))))
             s = Surface(prev, post, geometry, is_stop=bool(sd.get("is_stop", False)),
                         aperture=aperture, surface_type=sd.get("surface_type"),
-                        is_reflective=bool(sd.get("is_reflective", False)))
+                        interaction_model=model)
             if isinstance(geometry, ZernikePolynomialGeometry):
                 s.surface_type = "zernike"
             elif isinstance(geometry, ChebyshevPolynomialGeometry):
@@ -254,7 +273,9 @@ def optic_to_dict(optic):
         if not isinstance(s, ObjectSurface):
             d.update(material_pre=material_to_dict(s.material_pre), is_stop=bool(s.is_stop),
                      aperture=None if s.aperture is None else s.aperture.to_dict(),
-                     coating=None, bsdf=None, is_reflective=bool(s.is_reflective))
+                     coating=None, bsdf=None, is_reflective=bool(s.is_reflective),
+                     surface_type=s.surface_type,
+                     interaction_model=s.interaction_model.to_dict())
         surfaces.append(d)
     fields = [{"field_type": optic.field_type, "x": f.x, "y": f.y, "vx": f.vx, "vy": f.vy}
               for f in optic.fields.fields]

@@ -68,7 +68,15 @@ class LensTable:
         o["n_pre"] = self.n_tab[:, self.surfaces["mat_pre"]]
         o["u"] = self.u_tab
         o["alpha_pre"] = self.alpha_tab[:, self.surfaces["mat_pre"]]
+        o["n_post"] = self.n_tab[:, self.surfaces["mat_post"]]
         return o
+
+    @property
+    def interaction_mask(self):
+        m = 0
+        for v in np.unique(self.surfaces["interaction"]):
+            m |= 1 << int(v)
+        return m
 
     @property
     def newton_surfaces(self):
@@ -129,6 +137,7 @@ def lower_surface_group(surface_group, wavelengths, record=False, skip_object=Tr
     table = np.zeros(len(surfs), dtype=_abi.SURFACE)
     ops, coef, zern = [], [], []
     ap_progs = []
+    ia_blocks = []
     device_coeffs = []
     for si, s in enumerate(surfs):
         g = s.geometry
@@ -178,6 +187,11 @@ def lower_surface_group(surface_group, wavelengths, record=False, skip_object=Tr
             row["coef_off"] = len(coef)
             row["n_coef"] = len(cc)
             coef.extend(cc)
+        im = getattr(s, "interaction_model", None)
+        if im is not None:
+            row["interaction"] = im.interaction_id
+            if im.interaction_id != _abi.IA_REFRACT_REFLECT:
+                ia_blocks.append((si, [float(v) for v in im.lower(g)]))
         row["mat_pre"] = mat_id(s.material_pre)
         row["mat_post"] = mat_id(s.material_post)
         loc = g.cs.localize_ops()
@@ -203,6 +217,9 @@ def lower_surface_group(surface_group, wavelengths, record=False, skip_object=Tr
         table[si]["ap_off"] = len(coef)
         table[si]["ap_len"] = len(prog)
         coef.extend(prog)
+    for si, blk in ia_blocks:  # interaction parameter blocks (ort_interaction)
+        table[si]["ia_off"] = len(coef)
+        coef.extend(blk)
 
     final = surfs[-1]
     final_mat = mat_id(final.material_post)

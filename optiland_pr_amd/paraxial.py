@@ -51,8 +51,14 @@ class Paraxial:
             t = pos[k] - z_
             z_ = pos[k]
             y_ = y_ + t * u_
+            thin = getattr(surfs[k], "surface_type", None) == "paraxial"
             if surfs[k].is_reflective:
-                u_ = -u_ - 2 * y_ / R[k]
+                if thin:  # paraxial_ray_tracer.py:118-120
+                    u_ = -u_ - y_ / surfs[k].interaction_model.f
+                else:
+                    u_ = -u_ - 2 * y_ / R[k]
+            elif thin:  # :124-126
+                u_ = (n[k - 1] * u_ - y_ / surfs[k].interaction_model.f) / n[k]
             else:
                 u_ = (n[k - 1] * u_ - y_ * power[k]) / n[k]
             heights.append(np.copy(y_))

@@ -136,12 +136,15 @@ class DeviceLens:
         for g in np.unique(table.surfaces["geometry"]):
             mask |= 1 << int(g)
         self.geometry_mask = mask
+        self.lambdas = torch.as_tensor(np.asarray(table.wavelengths, dtype=np.float64),
+                                       dtype=torch.float64, device=d)
         self.c = _native.ort_lens(
             self.surfaces.data_ptr(), self.cs_ops.data_ptr(), self.coef.data_ptr(),
             self.zern.data_ptr(), self.n_tab.data_ptr(), self.alpha_tab.data_ptr(),
             self.optics.data_ptr(),
             table.n_surfaces, len(table.wavelengths), table.n_tab.shape[1], table.final_mat,
-            mask, 0, table.final_thickness, self.mats.data_ptr())
+            mask, table.interaction_mask, table.final_thickness, self.mats.data_ptr(),
+            self.lambdas.data_ptr())
         self.newton = table.newton_surfaces
         self.sched_cache: dict = {}
 

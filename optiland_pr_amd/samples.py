@@ -338,6 +338,104 @@ class FiniteTripletImageHeight(Optic):
         self.add_wavelength(value=0.55, is_primary=True)
 
 
+class ParaxialLens(Optic):
+    """Two thin lenses (surface_type "paraxial") around a glass singlet, the second in a
+    medium of index 1.2 (thin_lens_interaction_model.py)."""
+
+    def __init__(self):
+        from .materials import IdealMaterial
+
+        super().__init__()
+        self.add_surface(index=0, thickness=np.inf)
+        self.add_surface(index=1, surface_type="paraxial", f=80, thickness=10, is_stop=True)
+        self.add_surface(index=2, radius=60.0, thickness=4.0, material="SK16")
+        self.add_surface(index=3, radius=-200.0, thickness=10.0)
+        self.add_surface(index=4, surface_type="paraxial", f=-150, thickness=40,
+                         material=IdealMaterial(1.2, 0))
+        self.add_surface(index=5)
+        self.set_aperture(aperture_type="EPD", value=10)
+        self.set_field_type(field_type="angle")
+        self.add_field(y=0)
+        self.add_field(y=5)
+        self.add_field(x=2, y=3)
+        self.add_wavelength(value=0.55, is_primary=True)
+
+
+class ParaxialMirror(Optic):
+    """A reflective thin lens (n2 = -n1)."""
+
+    def __init__(self):
+        super().__init__()
+        self.add_surface(index=0, thickness=np.inf)
+        self.add_surface(index=1, surface_type="paraxial", f=-60, thickness=-50,
+                         material="mirror", is_stop=True)
+        self.add_surface(index=2)
+        self.set_aperture(aperture_type="EPD", value=12)
+        self.set_field_type(field_type="angle")
+        self.add_field(y=0)
+        self.add_field(y=4)
+        self.add_wavelength(value=0.6, is_primary=True)
+
+
+class PhasePlate(Optic):
+    """Phase surfaces (phase_interaction_model.py): a linear grating on a plane, a radial
+    profile on a sphere, a constant phase, a metalens-like radial profile on a plane."""
+
+    def __init__(self):
+        from .interactions import (ConstantPhaseProfile, LinearGratingPhaseProfile,
+                                   RadialPhaseProfile)
+
+        super().__init__()
+        self.add_surface(index=0, thickness=np.inf)
+        self.add_surface(index=1, thickness=5, is_stop=True,
+                         phase_profile=LinearGratingPhaseProfile(period=5.0, angle=0.4, order=1,
+                                                                 efficiency=0.8))
+        self.add_surface(index=2, radius=60.0, thickness=4.0, material="SK16",
+                         phase_profile=RadialPhaseProfile([-0.02, 1e-5, -2e-8]))
+        self.add_surface(index=3, radius=-200.0, thickness=3.0,
+                         phase_profile=ConstantPhaseProfile(0.7))
+        self.add_surface(index=4, thickness=60.0, phase_profile=RadialPhaseProfile([-0.15]))
+        self.add_surface(index=5)
+        self.set_aperture(aperture_type="EPD", value=10)
+        self.set_field_type(field_type="angle")
+        self.add_field(y=0)
+        self.add_field(y=5)
+        self.add_field(x=1.5, y=-3)
+        self.add_wavelength(value=0.48)
+        self.add_wavelength(value=0.55, is_primary=True)
+        self.add_wavelength(value=0.65)
+
+
+class Grating(Optic):
+    """The reference's grating test systems (tests/test_grating.py:7-117): "flat" / "curved"
+    transmission gratings behind an N-BK7 plate or a "reflective" curved grating; `angle`
+    rotates the grooves."""
+
+    def __init__(self, kind="flat", angle=0.0):
+        super().__init__()
+        self.add_surface(index=0, radius=np.inf, thickness=np.inf)
+        if kind == "reflective":
+            self.add_surface(index=1, radius=70, thickness=-30, material="mirror",
+                             surface_type="grating", is_stop=True, grating_period=5.0,
+                             grating_order=1, groove_orientation_angle=angle)
+            self.add_surface(index=2)
+        else:
+            self.add_surface(index=1, radius=np.inf, thickness=10)
+            self.add_surface(index=2, radius=np.inf, thickness=5, material="N-BK7")
+            kw = dict(radius=np.inf) if kind == "flat" else dict(radius=50.0, conic=1.0)
+            self.add_surface(index=3, thickness=30, surface_type="grating", grating_order=-1,
+                             grating_period=5.0, groove_orientation_angle=angle, is_stop=True,
+                             **kw)
+            self.add_surface(index=4)
+        self.set_aperture(aperture_type="EPD", value=15)
+        self.set_field_type(field_type="angle")
+        self.add_field(y=0)
+        self.add_field(y=10)
+        self.add_field(y=0, x=10)
+        self.add_wavelength(value=0.587, is_primary=True)
+        self.update_paraxial()
+
+
 GOLDEN_LENSES = {
     "cooke": CookeTriplet,
     "dg": DoubleGauss,
@@ -355,4 +453,11 @@ GOLDEN_LENSES = {
     "finite_pih": FiniteTripletImageHeight,
     "forbes": ForbesSinglets,
     "forbes_q2d": ForbesFreeform,
+    "paraxial_lens": ParaxialLens,
+    "paraxial_mirror": ParaxialMirror,
+    "phase_plate": PhasePlate,
+    "grating_flat": lambda: Grating("flat"),
+    "grating_curved": lambda: Grating("curved"),
+    "grating_reflective": lambda: Grating("reflective"),
+    "grating_tilted": lambda: Grating("curved", angle=0.35),
 }

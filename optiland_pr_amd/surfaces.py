@@ -26,12 +26,15 @@ from .geometries import (
     ForbesSurfaceConfig,
     OddAsphere,
     Plane,
+    PlaneGrating,
     PolynomialGeometry,
+    StandardGratingGeometry,
     StandardGeometry,
     ToroidalGeometry,
     ZernikePolynomialGeometry,
     scalar,
 )
+from .interactions import RefractiveReflectiveModel, make_interaction
 from .materials import BaseMaterial, IdealMaterial, configure_material
 
 
@@ -62,8 +65,14 @@ class Surface:
     """standard_surface.py:32-233 (the real-ray branch of Surface.trace runs in HIP)."""
 
     def __init__(self, previous_surface, material_post, geometry, is_stop=False,
-                 aperture=None, surface_type=None, comment="", is_reflective=False):
+                 aperture=None, surface_type=None, comment="", is_reflective=False,
+                 interaction_model=None):
         self.geometry = geometry
+        # standard_surface.py:74-83 (refractive / reflective unless given)
+        if interaction_model is None:
+            interaction_model = RefractiveReflectiveModel(is_reflective=is_reflective)
+        self.interaction_model = interaction_model
+        interaction_model.parent_surface = self
         self.previous_surface = previous_surface
         self._material_post = material_post
         self.is_stop = is_stop
@@ -71,7 +80,6 @@ class Surface:
         self.semi_aperture = None
         self.surface_type = surface_type
         self.comment = comment
-        self.is_reflective = is_reflective
         self.thickness = 0.0
         self.reset()
 
@@ -89,6 +97,14 @@ class Surface:
     @material_post.setter
     def material_post(self, m):
         self._material_post = m
+
+    @property
+    def is_reflective(self):
+        return self.interaction_model.is_reflective
+
+    @is_reflective.setter
+    def is_reflective(self, value):
+        self.interaction_model.is_reflective = bool(value)
 
     def set_semi_aperture(self, r_max):
         self.semi_aperture = r_max
@@ -118,8 +134,15 @@ def _make_geometry(surface_type, cs, kw):
         if np.isinf(radius):
             return Plane(cs)
         return StandardGeometry(cs, radius, conic)
-    if st == "plane":
+    if st in ("plane", "paraxial"):  # geometry_factory.py:352-367: a paraxial surface is a plane
         return Plane(cs)
+    if st == "grating":  # geometry_factory.py:154-180 with GratingConfig defaults
+        order = kw.get("grating_order", 0)
+        period = kw.get("grating_period", np.inf)
+        angle = kw.get("groove_orientation_angle", 0.0)
+        if np.isinf(radius):
+            return PlaneGrating(cs, order, period, angle)
+        return StandardGratingGeometry(cs, radius, order, period, angle, conic)
     if st == "even_asphere":
         return EvenAsphere(cs, radius, conic, kw.get("tol", 1e-6), kw.get("max_iter", 100),
                            kw.get("coefficients", []))
@@ -156,8 +179,8 @@ def _make_geometry(surface_type, cs, kw):
         return cls(cs, cfg, ForbesSolverConfig(tol=tol, max_iter=max_iter))
     raise ValueError(
         f"Surface type {st!r} is not lowered to the MI355X trace core (supported: "
-        "standard, plane, even_asphere, odd_asphere, zernike, polynomial, chebyshev, "
-        "biconic, toroidal, forbes_qbfs, forbes_q2d).")
+        "standard, plane, paraxial, grating, even_asphere, odd_asphere, zernike, "
+        "polynomial, chebyshev, biconic, toroidal, forbes_qbfs, forbes_q2d).")
 
 
 class SurfaceGroup:
@@ -311,11 +334,24 @@ class SurfaceGroup:
             s = ObjectSurface(geometry, material_post, comment)
             s.thickness = kw.get("thickness", 0.0)
             return s
-        if kw.get("phase_profile") is not None or surface_type in ("paraxial", "grating"):
-            raise ValueError(f"interaction for surface_type={surface_type!r} is out of scope")
+        if surface_type == "paraxial" and index == 0:
+            raise ValueError("Paraxial surface cannot be the object surface.")
+        # surface_factory.py:117-140: the interaction model follows the surface type
+        interaction_type = kw.get("interaction_type", "refractive_reflective")
+        if surface_type == "paraxial":
+            interaction_type = "thin_lens"
+        elif surface_type == "grating":
+            interaction_type = "diffractive"
+        elif kw.get("phase_profile") is not None:
+            interaction_type = "phase"
+        for key in ("coating", "bsdf"):
+            if kw.get(key) is not None:
+                raise ValueError(f"{key} is out of scope for the trace core")
+        model = make_interaction(interaction_type, is_reflective, focal_length=kw.get("f"),
+                                 phase_profile=kw.get("phase_profile"))
         return Surface(None, material_post, geometry, is_stop=is_stop,
                        aperture=kw.get("aperture"), surface_type=surface_type,
-                       comment=comment, is_reflective=is_reflective)
+                       comment=comment, interaction_model=model)
 
     def trace(self, rays, skip=0):
         """surface_group.py:232-244: trace `rays` (RealRays, device) in place."""

@@ -20,6 +20,13 @@ It restates, formula by formula and in the same evaluation order, the reference
   standard_surface.py:218                              OPD accumulation
   physical_apertures/radial.py:50-63, real_rays.py:132-139  radial clip
   real_rays.py:141-181, 511-547                        refract / reflect
+  interactions/thin_lens_interaction_model.py:55-113   thin lens (+ normalize on the
+                                                       next propagate, homogeneous.py:55-57)
+  interactions/phase_interaction_model.py:45-132,      phase surfaces
+    phase/{constant,linear_grating,radial}.py
+  interactions/diffractive_model.py:28-61,             gratings
+    real_rays.py:183-509, plane_grating.py:105-124,
+    standard_grating.py:93-146, 224-247
   real_ray_tracer.py:84-89                             image-space propagate
 
 Input is the lowered lens (optiland_pr_amd._abi structured arrays: the same bytes the
@@ -902,6 +909,162 @@ def reflect(r: Rays, nx, ny, nz):
     r.N = r.N - 2 * dot * nz
 
 
+def normalize(r: Rays):
+    """real_rays.py:503-509."""
+    mag = np.sqrt(r.L**2 + r.M**2 + r.N**2)
+    r.L, r.M, r.N = r.L / mag, r.M / mag, r.N / mag
+
+
+def thin_lens(r: Rays, f, n1, n2):
+    """thin_lens_interaction_model.py:69-111 (f: 0-d array as in the reference)."""
+    f = np.asarray(f)
+    r.opd = r.opd - (r.x**2 + r.y**2) / (2 * f)
+    ux1 = r.L / r.N
+    uy1 = r.M / r.N
+    ux2 = 1 / n2 * (n1 * ux1 - r.x / f)
+    uy2 = 1 / n2 * (n1 * uy1 - r.y / f)
+    r.L, r.M, r.N = ux2, uy2, np.ones_like(ux2)
+
+
+def _phase_profile(blk, x, y):
+    """phase/constant.py, linear_grating.py:60-92, radial.py:26-75 -> phase, grad x, y."""
+    kind = int(blk[0])
+    if kind == _abi.PHASE_CONSTANT:
+        return np.full_like(x, blk[2]), np.zeros_like(x), np.zeros_like(y)
+    if kind == _abi.PHASE_LINEAR:
+        kx, ky = float(blk[2]), float(blk[3])
+        return kx * x + ky * y, np.full_like(x, kx), np.full_like(y, ky)
+    coeffs = [float(c) for c in blk[3:3 + int(blk[2])]]
+    r_squared = x**2 + y**2
+    phase = np.zeros_like(x)
+    for i, coeff in enumerate(coeffs):
+        power = i + 1
+        phase = phase + coeff * (r_squared**power)
+    r = np.sqrt(r_squared)
+    d_phi_dr = np.zeros_like(r)
+    for i, coeff in enumerate(coeffs):
+        power = i + 1
+        d_phi_dr = d_phi_dr + coeff * 2 * power * (r ** (2 * power - 1))
+    safe_r = np.where(r == 0, 1.0, r)
+    dx = np.where(r == 0, 0.0, (d_phi_dr / safe_r) * x)
+    dy = np.where(r == 0, 0.0, (d_phi_dr / safe_r) * y)
+    return phase, dx, dy
+
+
+def phase_interact(r: Rays, blk, nx, ny, nz, n1, n2, reflective, w):
+    """phase_interaction_model.py:45-132."""
+    if reflective:
+        n2 = n1
+    k0 = 2 * np.pi / w
+    k_ix, k_iy, k_iz = n1 * k0 * r.L, n1 * k0 * r.M, n1 * k0 * r.N
+    phase_val, gx, gy = _phase_profile(blk, r.x, r.y)
+    gz = np.zeros_like(r.x)
+    gdn = gx * nx + gy * ny + gz * nz
+    Gx, Gy, Gz = gx - gdn * nx, gy - gdn * ny, gz - gdn * nz
+    kdn = k_ix * nx + k_iy * ny + k_iz * nz
+    kpx, kpy, kpz = k_ix - kdn * nx, k_iy - kdn * ny, k_iz - kdn * nz
+    kox, koy, koz = kpx + Gx, kpy + Gy, kpz + Gz
+    par2 = kox**2 + koy**2 + koz**2
+    R_sq = (n2 * k0) ** 2 - par2
+    r.i = np.where(R_sq < 0.0, np.zeros_like(r.i), r.i)
+    R_sq = np.maximum(0.0, R_sq)
+    alpha = (-1.0 if reflective else 1.0) * np.sqrt(R_sq)
+    kx, ky, kz = kox + alpha * nx, koy + alpha * ny, koz + alpha * nz
+    mag = np.sqrt(kx**2 + ky**2 + kz**2)
+    r.L, r.M, r.N = kx / mag, ky / mag, kz / mag
+    r.opd = r.opd + -phase_val / k0
+    r.i = r.i * float(blk[1])
+
+
+def grating_vector(blk, x, y, nx, ny, nz):
+    """plane_grating.py:105-124 / standard_grating.py:93-146, 224-247 (the scalars tan,
+    R**2, R**3, k + 1 formed by the lowering as the reference forms them)."""
+    if float(blk[2]) == 0.0:
+        ones = np.ones_like(x)
+        return float(blk[3]) * ones, float(blk[4]) * ones, np.zeros_like(x)
+    ta, R2, R3, kp1 = (float(v) for v in blk[3:7])
+    s = np.sqrt((R2 - kp1 * (x**2 + y**2)) / R2)
+    dzdx = (x + y * ta) * (2 * R2 * s * (s + 1) + kp1 * (x**2 + y**2)) / (R3 * s * (s + 1) ** 2)
+    tx, ty, tz = np.ones_like(dzdx), np.ones_like(dzdx) * ta, dzdx
+    nt = np.sqrt(tx**2 + ty**2 + tz**2)
+    tx, ty, tz = tx / nt, ty / nt, tz / nt
+    fx = ny * tz - nz * ty
+    fy = -nx * tz + nz * tx
+    fz = nx * ty - ny * tx
+    mag = np.sqrt(fx**2 + fy**2 + fz**2)
+    return -(fx / mag), -(fy / mag), -(fz / mag)
+
+
+def diffract(r: Rays, blk, nx, ny, nz, n1, n2, reflective, w):
+    """diffractive_model.py:37-56 + real_rays.py:183-498 (gratingdiffract)."""
+    fx, fy, fz = grating_vector(blk, r.x, r.y, nx, ny, nz)
+    m = float(blk[0])
+    d = float(blk[1]) / np.sqrt(fx**2 + fy**2)
+    L0, M0, N0 = r.L, r.M, r.N
+    nx, ny, nz, _ = _align(r, nx, ny, nz)
+    n2c = n2 * (-1 if reflective else 1)
+    D = (-(L0**2) * d**2 * n1**2 * ny**2 - L0**2 * d**2 * n1**2 * nz**2
+         + 2 * L0 * M0 * d**2 * n1**2 * nx * ny + 2 * L0 * N0 * d**2 * n1**2 * nx * nz
+         - 2 * L0 * d * fx * m * n1 * ny**2 * w - 2 * L0 * d * fx * m * n1 * nz**2 * w
+         + 2 * L0 * d * fy * m * n1 * nx * ny * w + 2 * L0 * d * fz * m * n1 * nx * nz * w
+         - M0**2 * d**2 * n1**2 * nx**2 - M0**2 * d**2 * n1**2 * nz**2
+         + 2 * M0 * N0 * d**2 * n1**2 * ny * nz + 2 * M0 * d * fx * m * n1 * nx * ny * w
+         - 2 * M0 * d * fy * m * n1 * nx**2 * w - 2 * M0 * d * fy * m * n1 * nz**2 * w
+         + 2 * M0 * d * fz * m * n1 * ny * nz * w
+         - N0**2 * d**2 * n1**2 * nx**2 - N0**2 * d**2 * n1**2 * ny**2
+         + 2 * N0 * d * fx * m * n1 * nx * nz * w + 2 * N0 * d * fy * m * n1 * ny * nz * w
+         - 2 * N0 * d * fz * m * n1 * nx**2 * w - 2 * N0 * d * fz * m * n1 * ny**2 * w
+         + d**2 * n2c**2 * nx**2 + d**2 * n2c**2 * ny**2 + d**2 * n2c**2 * nz**2
+         - fx**2 * m**2 * ny**2 * w**2 - fx**2 * m**2 * nz**2 * w**2
+         + 2 * fx * fy * m**2 * nx * ny * w**2 + 2 * fx * fz * m**2 * nx * nz * w**2
+         - fy**2 * m**2 * nx**2 * w**2 - fy**2 * m**2 * nz**2 * w**2
+         + 2 * fy * fz * m**2 * ny * nz * w**2
+         - fz**2 * m**2 * nx**2 * w**2 - fz**2 * m**2 * ny**2 * w**2)
+    with np.errstate(invalid="ignore"):
+        sD = np.sqrt(D)
+    AL = (L0 * d * n1 * ny**2 + L0 * d * n1 * nz**2 - M0 * d * n1 * nx * ny
+          - N0 * d * n1 * nx * nz + fx * m * ny**2 * w + fx * m * nz**2 * w
+          - fy * m * nx * ny * w - fz * m * nx * nz * w)
+    AM = (-L0 * d * n1 * nx * ny + M0 * d * n1 * nx**2 + M0 * d * n1 * nz**2
+          - N0 * d * n1 * ny * nz - fx * m * nx * ny * w + fy * m * nx**2 * w
+          + fy * m * nz**2 * w - fz * m * ny * nz * w)
+    PN = (L0 * d * n1 * nx * nz + M0 * d * n1 * ny * nz - N0 * d * n1 * nx**2
+          - N0 * d * n1 * ny**2 + fx * m * nx * nz * w + fy * m * ny * nz * w
+          - fz * m * nx**2 * w - fz * m * ny**2 * w)
+    if reflective:
+        r.L = (AL - nx * sD) / (d * n2c)
+        r.M = (AM - ny * sD) / (d * n2c)
+        r.N = -nz * sD / (d * n2c) - PN / (d * n2c)
+    else:
+        r.L = (AL + nx * sD) / (d * n2c)
+        r.M = (AM + ny * sD) / (d * n2c)
+        r.N = nz * sD / (d * n2c) - PN / (d * n2c)
+    normalize(r)
+
+
+def interact(r: Rays, table, s, n1, n2, w):
+    """The surface's interaction model (standard_surface.py:225). Returns True when the
+    rays are left unnormalised (thin lens)."""
+    ia = int(s["interaction"])
+    flags = int(s["flags"])
+    refl = bool(flags & _abi.SURF_REFLECTIVE)
+    blk = table.coef[int(s["ia_off"]):]
+    if ia == _abi.IA_THIN_LENS:
+        thin_lens(r, blk[0], n1, -n1 if refl else n2)
+        return True
+    nx, ny, nz = surface_normal(r, table, s)
+    if ia == _abi.IA_REFRACT_REFLECT:
+        if refl:
+            reflect(r, nx, ny, nz)
+        else:
+            refract(r, nx, ny, nz, n1, n2)
+    elif ia == _abi.IA_PHASE:
+        phase_interact(r, blk, nx, ny, nz, n1, n2, refl, w)
+    else:
+        diffract(r, blk, nx, ny, nz, n1, n2, refl, w)
+    return False
+
+
 # --------------------------------------------------------------------------------------
 # the trace
 # --------------------------------------------------------------------------------------
@@ -977,8 +1140,10 @@ def trace_segment(table, rays: Rays, lam: int, record=False, sched=None, start=0
     r = rays
     records = {}
     updates = {}
+    unnorm = False
     n_tab = table.n_tab[lam]
     a_tab = table.alpha_tab[lam]
+    w_lam = float(table.wavelengths[lam])
     for si in range(start, len(table.surfaces)):
         s = table.surfaces[si]
         g = int(s["geometry"])
@@ -997,6 +1162,8 @@ def trace_segment(table, rays: Rays, lam: int, record=False, sched=None, start=0
                 r, table, s, None if sched is None else sched.get(si))
         mp, mq = int(s["mat_pre"]), int(s["mat_post"])
         propagate(r, t, float(a_tab[mp]))
+        if unnorm:  # homogeneous.py:55-57
+            normalize(r)
         r.opd = r.opd + np.abs(t * n_tab[mp])  # standard_surface.py:218
         if flags & _abi.SURF_APERTURE:  # radial.py:50-63 + real_rays.py:132-139
             radius2 = r.x**2 + r.y**2
@@ -1006,11 +1173,7 @@ def trace_segment(table, rays: Rays, lam: int, record=False, sched=None, start=0
             off, ln = int(s["ap_off"]), int(s["ap_len"])
             inside = aperture_contains(table.coef[off:off + ln], r.x, r.y)
             r.i = np.where(~inside, np.zeros_like(r.i), r.i)
-        nx, ny, nz = surface_normal(r, table, s)
-        if flags & _abi.SURF_REFLECTIVE:
-            reflect(r, nx, ny, nz)
-        else:
-            refract(r, nx, ny, nz, n_tab[mp], n_tab[mq])
+        unnorm = interact(r, table, s, n_tab[mp], n_tab[mq], w_lam)
         apply_cs(r, table.cs_ops[int(s["cs_glob_off"]):int(s["cs_glob_off"]) + int(s["n_cs_glob"])])
         r.x, r.y, r.z = r.x + float(ct[0]), r.y + float(ct[1]), r.z + float(ct[2])
         if record:
@@ -1019,11 +1182,14 @@ def trace_segment(table, rays: Rays, lam: int, record=False, sched=None, start=0
         # real_ray_tracer.py:84-89 always propagates (by 0 for the samples), and applies
         # absorption only when k>0 of the image-space material.
         propagate(r, table.final_thickness, float(a_tab[table.final_mat]))
+        if unnorm:
+            normalize(r)
     return TraceResult(r, records, updates)
 
 
 def _trace_segment_w(table, r: Rays, w, record, sched, start):
     records, updates = {}, {}
+    unnorm = False
     w = np.asarray(w, dtype=np.float64)
     for si in range(start, len(table.surfaces)):
         s = table.surfaces[si]
@@ -1043,6 +1209,8 @@ def _trace_segment_w(table, r: Rays, w, record, sched, start):
         mp, mq = int(s["mat_pre"]), int(s["mat_post"])
         n_pre = material_n(table, mp, w)
         propagate_w(r, t, material_k(table, mp, w), w)
+        if unnorm:
+            normalize(r)
         r.opd = r.opd + np.abs(t * n_pre)  # standard_surface.py:218
         if flags & _abi.SURF_APERTURE:
             radius2 = r.x**2 + r.y**2
@@ -1052,17 +1220,15 @@ def _trace_segment_w(table, r: Rays, w, record, sched, start):
             off, ln = int(s["ap_off"]), int(s["ap_len"])
             inside = aperture_contains(table.coef[off:off + ln], r.x, r.y)
             r.i = np.where(~inside, np.zeros_like(r.i), r.i)
-        nx, ny, nz = surface_normal(r, table, s)
-        if flags & _abi.SURF_REFLECTIVE:
-            reflect(r, nx, ny, nz)
-        else:
-            refract(r, nx, ny, nz, n_pre, material_n(table, mq, w))
+        unnorm = interact(r, table, s, n_pre, material_n(table, mq, w), w)
         apply_cs(r, table.cs_ops[int(s["cs_glob_off"]):int(s["cs_glob_off"]) + int(s["n_cs_glob"])])
         r.x, r.y, r.z = r.x + float(ct[0]), r.y + float(ct[1]), r.z + float(ct[2])
         if record:
             records[si] = r.copy()
     if table.final_mat >= 0:
         propagate_w(r, table.final_thickness, material_k(table, table.final_mat, w), w)
+        if unnorm:
+            normalize(r)
     return TraceResult(r, records, updates)
 
 

@@ -40,9 +40,11 @@ def native_case(name, meta, record=False):
 # golden cases whose every traced surface is closed-form (plane / conic): the oracle and
 # the HIP kernel reproduce the reference bit for bit there
 CLOSED_FORM = ("cooke", "dg", "rt", "cooke_aperture", "cooke_shapes", "decentered", "json_cooke",
-               "json_heliar", "json_rt", "cooke_pih", "finite_pih")
+               "json_heliar", "json_rt", "cooke_pih", "finite_pih", "paraxial_lens",
+               "paraxial_mirror", "grating_flat", "grating_curved", "grating_reflective",
+               "grating_tilted")
 NEWTON = ("rt_asph", "rt_odd", "tma_fringe", "tma_standard", "tma_noll", "freeform",
-          "forbes", "forbes_q2d")
+          "forbes", "forbes_q2d", "phase_plate")
 ALL_CASES = CLOSED_FORM + NEWTON
 
 FIELDS = _abi.RAY_FIELDS

@@ -304,6 +304,101 @@ def finite_pih():
     return lens
 
 
+def paraxial_lens():
+    """Two thin lenses (surface_type "paraxial", thin_lens_interaction_model.py) around a
+    glass singlet, the second thin lens in a medium of index 1.2: covers the paraxial
+    phase transformation and the normalisation at the next propagation."""
+    lens = ref_optic.Optic()
+    lens.add_surface(index=0, thickness=np.inf)
+    lens.add_surface(index=1, surface_type="paraxial", f=80, thickness=10, is_stop=True)
+    lens.add_surface(index=2, radius=60.0, thickness=4.0, material="SK16")
+    lens.add_surface(index=3, radius=-200.0, thickness=10.0)
+    lens.add_surface(index=4, surface_type="paraxial", f=-150, thickness=40,
+                     material=IdealMaterial(1.2, 0))
+    lens.add_surface(index=5)
+    lens.set_aperture(aperture_type="EPD", value=10)
+    lens.set_field_type(field_type="angle")
+    lens.add_field(y=0)
+    lens.add_field(y=5)
+    lens.add_field(x=2, y=3)
+    lens.add_wavelength(value=0.55, is_primary=True)
+    return lens
+
+
+def paraxial_mirror():
+    """A reflective thin lens (n2 = -n1; paraxial_ray_tracer.py:118-120)."""
+    lens = ref_optic.Optic()
+    lens.add_surface(index=0, thickness=np.inf)
+    lens.add_surface(index=1, surface_type="paraxial", f=-60, thickness=-50, material="mirror",
+                     is_stop=True)
+    lens.add_surface(index=2)
+    lens.set_aperture(aperture_type="EPD", value=12)
+    lens.set_field_type(field_type="angle")
+    lens.add_field(y=0)
+    lens.add_field(y=4)
+    lens.add_wavelength(value=0.6, is_primary=True)
+    return lens
+
+
+def phase_plate():
+    """Phase surfaces (phase_interaction_model.py): a linear grating on a plane, a radial
+    profile on a sphere, a constant phase, a metalens-like radial profile on a plane."""
+    from optiland.phase import ConstantPhaseProfile, LinearGratingPhaseProfile, RadialPhaseProfile
+
+    lens = ref_optic.Optic()
+    lens.add_surface(index=0, thickness=np.inf)
+    lens.add_surface(index=1, thickness=5, is_stop=True,
+                     phase_profile=LinearGratingPhaseProfile(period=5.0, angle=0.4, order=1,
+                                                             efficiency=0.8))
+    lens.add_surface(index=2, radius=60.0, thickness=4.0, material="SK16",
+                     phase_profile=RadialPhaseProfile([-0.02, 1e-5, -2e-8]))
+    lens.add_surface(index=3, radius=-200.0, thickness=3.0,
+                     phase_profile=ConstantPhaseProfile(0.7))
+    lens.add_surface(index=4, thickness=60.0, phase_profile=RadialPhaseProfile([-0.15]))
+    lens.add_surface(index=5)
+    lens.set_aperture(aperture_type="EPD", value=10)
+    lens.set_field_type(field_type="angle")
+    lens.add_field(y=0)
+    lens.add_field(y=5)
+    lens.add_field(x=1.5, y=-3)
+    lens.add_wavelength(value=0.48)
+    lens.add_wavelength(value=0.55, is_primary=True)
+    lens.add_wavelength(value=0.65)
+    return lens
+
+
+def _grating_common(lens):
+    lens.set_aperture(aperture_type="EPD", value=15)
+    lens.set_field_type(field_type="angle")
+    lens.add_field(y=0)
+    lens.add_field(y=10)
+    lens.add_field(y=0, x=10)
+    lens.add_wavelength(value=0.587, is_primary=True)
+    lens.update_paraxial()
+    return lens
+
+
+def grating(kind, angle=0.0):
+    """The reference's grating test systems (tests/test_grating.py:7-117): flat and
+    curved transmission gratings behind an N-BK7 plate, a curved reflective grating;
+    `angle` rotates the grooves (groove_orientation_angle)."""
+    lens = ref_optic.Optic()
+    lens.add_surface(index=0, radius=np.inf, thickness=np.inf)
+    if kind == "reflective":
+        lens.add_surface(index=1, radius=70, thickness=-30, material="mirror",
+                         surface_type="grating", is_stop=True, grating_period=5.0,
+                         grating_order=1, groove_orientation_angle=angle)
+        lens.add_surface(index=2)
+        return _grating_common(lens)
+    lens.add_surface(index=1, radius=np.inf, thickness=10)
+    lens.add_surface(index=2, radius=np.inf, thickness=5, material="N-BK7")
+    kw = dict(radius=np.inf) if kind == "flat" else dict(radius=50.0, conic=1.0)
+    lens.add_surface(index=3, thickness=30, surface_type="grating", grating_order=-1,
+                     grating_period=5.0, groove_orientation_angle=angle, is_stop=True, **kw)
+    lens.add_surface(index=4)
+    return _grating_common(lens)
+
+
 def json_lens(name):
     """A lens file from the reference's docs/samples (copied as data to tests/golden/lenses),
     loaded with the reference's own Optic.from_dict (optic.py:674-713)."""
@@ -337,6 +432,18 @@ CASES = {
     "forbes": (forbes, [(0, 0), (0, 1), (0.7, 0.7)], [1.55], "uniform", 24),
     "forbes_q2d": (forbes_q2d, [(0, 0), (0, 1), (0.7, 0.7)], [1.55], "uniform", 24),
     "finite_pih": (finite_pih, [(0, 0), (0, 1), (-0.4, 0.7)], [0.48, 0.55], "uniform", 24),
+    "paraxial_lens": (paraxial_lens, [(0, 0), (0, 1), (0.4, 0.6)], [0.48, 0.55], "uniform", 24),
+    "paraxial_mirror": (paraxial_mirror, [(0, 0), (0, 1)], [0.6], "uniform", 24),
+    "phase_plate": (phase_plate, [(0, 0), (0, 1), (0.3, -0.6)], [0.48, 0.55, 0.65],
+                    "uniform", 24),
+    "grating_flat": (lambda: grating("flat"), [(0, 0), (0, 1), (1, 0), (0.2, 0.8)], [0.587],
+                     "uniform", 24),
+    "grating_curved": (lambda: grating("curved"), [(0, 0), (0, 1), (1, 0), (0.2, 0.8)],
+                       [0.55, 0.587], "uniform", 24),
+    "grating_reflective": (lambda: grating("reflective"), [(0, 0), (0, 1), (0.2, 0.8)],
+                           [0.587], "uniform", 24),
+    "grating_tilted": (lambda: grating("curved", angle=0.35), [(0, 0), (0.2, 0.8)], [0.587],
+                       "uniform", 24),
 }
 
 
@@ -463,7 +570,7 @@ def glass_table():
     specs = [("SK16", None), ("F2", "schott"), ("N-SSK2", None), ("N-SK2", None),
              ("F5", "schott"), ("N-SK16", None), ("N-SK10", None), ("SK15", None),
              ("BASF2", None), ("FK3", None), ("SF15", "hikari"), ("N-LAK12", None),
-             ("E-LLF6", None), ("H-K3", "cdgm"), ("H-ZLAF68C", "cdgm")]
+             ("E-LLF6", None), ("H-K3", "cdgm"), ("H-ZLAF68C", "cdgm"), ("N-BK7", None)]
     out = {}
     for name, ref in specs:
         m = Material(name, ref) if ref else Material(name)
@@ -543,6 +650,10 @@ MIXED_W_CASES = {  # name -> (builder, field (Hx, Hy), pupil n, wavelength range
     "cooke": (CookeTriplet, (0.0, 0.7), 24, (0.42, 0.75)),
     "dg": (DoubleGauss, (0.0, 1.0), 24, (0.45, 0.70)),
     "freeform": (None, (0.3, 0.6), 20, (0.45, 0.70)),
+    "paraxial_lens": (paraxial_lens, (0.3, 0.6), 20, (0.45, 0.70)),
+    "phase_plate": (phase_plate, (0.3, -0.6), 20, (0.45, 0.70)),
+    "grating_curved": (lambda: grating("curved"), (0.2, 0.8), 20, (0.45, 0.70)),
+    "grating_reflective": (lambda: grating("reflective"), (0.2, 0.8), 20, (0.45, 0.70)),
 }
 
 

@@ -18,7 +18,8 @@ from optiland_pr_amd.materials import Material
 from tests._cases import build_lens
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "mixed_w.npz")
-CASES = ("cooke", "dg", "freeform")
+CASES = ("cooke", "dg", "freeform", "paraxial_lens", "phase_plate", "grating_curved",
+         "grating_reflective")
 
 
 def _golden():
