@@ -68,7 +68,8 @@ enum ort_surface_flags {
   ORT_SURF_APERTURE = 1u << 2,   /* radial physical aperture: physical_apertures/radial.py */
   ORT_SURF_RECORD = 1u << 3,     /* snapshot the ray state after this surface (_record)  */
   ORT_SURF_TRANSLATE = 1u << 4,  /* informational: the frame is the translation cs_t only  */
-  ORT_SURF_APERTURE_PROG = 1u << 5 /* general aperture: a program in lens.coef (ap_off)  */
+  ORT_SURF_APERTURE_PROG = 1u << 5, /* general aperture: a program in lens.coef (ap_off) */
+  ORT_SURF_INV_R2 = 1u << 6        /* inv_r2 holds RN(1 / (R * R)) (finite, normal range)  */
                                  /* (both op lists empty)                                  */
 };
 
@@ -143,7 +144,10 @@ typedef struct ort_surface {
   int32_t ap_len;     /* its length in doubles                                       */
   int32_t interaction; /* enum ort_interaction                                        */
   int32_t ia_off;      /* its parameter block at lens.coef[ia_off]                    */
-  double reserved;
+  double inv_r2;       /* ORT_SURF_INV_R2: the correctly rounded 1 / (R * R); the conic */
+                       /* normal's (1 + k) r^2 / (R * R) is then q = a y refined once by  */
+                       /* its residual (Markstein), the same IEEE quotient without a      */
+                       /* per-ray reciprocal                                              */
 } ort_surface; /* 144 bytes */
 
 /* Aperture programs (the physical_apertures package): postfix, each op a double opcode followed

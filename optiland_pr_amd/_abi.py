@@ -51,6 +51,7 @@ SURF_APERTURE = 1 << 2
 SURF_RECORD = 1 << 3
 SURF_TRANSLATE = 1 << 4
 SURF_APERTURE_PROG = 1 << 5
+SURF_INV_R2 = 1 << 6
 
 # enum ort_interaction / ort_phase_kind
 IA_REFRACT_REFLECT = 0
@@ -109,7 +110,7 @@ SURFACE = np.dtype(
         ("ap_len", "<i4"),
         ("interaction", "<i4"),
         ("ia_off", "<i4"),
-        ("reserved", "<f8"),
+        ("inv_r2", "<f8"),
     ],
     align=True,
 )

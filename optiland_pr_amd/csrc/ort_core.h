@@ -19,6 +19,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "../../include/optiland_rt.h"
 
 #ifndef ORT_HD
@@ -436,16 +438,18 @@ ORT_INLINE T distance_conic(const RayT<T>& r, const S& R, const S& k, bool radiu
   const T z2 = r.z * r.z;
   T a, b, c;
   // 2*k*N*z + 2*L*x + 2*M*y - 2*N*R + 2*N*z: every "2*" is an exact scaling
+  // b: every term of the reference's sum carries an exact factor 2 and 2 RN(v) == RN(2 v)
+  // (outside the subnormal range), so the sum of the halves doubled once is the same
+  // double as the reference's sum of doubled terms, with one multiply instead of five
   if (vv(k) == 0.0 && tangent_free(k)) {
     // sphere: k*N**2 = 0, 2*k*N*z = 0, k*z**2 = 0 and 0 + v == v, so the conic terms
     // drop out without changing a bit (for finite rays)
     a = r.L * r.L + r.M * r.M + N2;
-    b = 2.0 * r.L * r.x + 2.0 * r.M * r.y - 2.0 * r.N * R + 2.0 * r.N * r.z;
+    b = 2.0 * (r.L * r.x + r.M * r.y - r.N * R + r.N * r.z);
     c = 0.0 - 2.0 * R * r.z + r.x * r.x + r.y * r.y + z2;
   } else {
     a = k * N2 + r.L * r.L + r.M * r.M + N2;
-    b = 2.0 * k * r.N * r.z + 2.0 * r.L * r.x + 2.0 * r.M * r.y - 2.0 * r.N * R +
-        2.0 * r.N * r.z;
+    b = 2.0 * (k * r.N * r.z + r.L * r.x + r.M * r.y - r.N * R + r.N * r.z);
     c = k * z2 - 2.0 * R * r.z + r.x * r.x + r.y * r.y + z2;
   }
   const T d = b * b - 4.0 * a * c;
@@ -470,6 +474,29 @@ ORT_INLINE void normal_conic(const T& x, const T& y, const S& R, const S& k, T& 
   const T dfdx = sdiv(x, dd);
   const T dfdy = sdiv(y, dd);
   const T mag = sqrt(dfdx * dfdx + dfdy * dfdy + 1.0);  // dfdz**2 = (-1)**2 = 1
+  const auto dm = shared_div(mag);
+  nx = sdiv(dfdx, dm);
+  ny = sdiv(dfdy, dm);
+  nz = sdiv(-1.0, dm);
+}
+
+// normal_conic with the host's correctly rounded inv_r2 = RN(1 / (R * R)): the quotient
+// (1 + k) r^2 / (R * R) is q0 = a inv_r2 corrected once by its exact residual, which is
+// the correctly rounded quotient (Markstein's theorem; checked here on 4e8 random
+// operands incl. all-ones and power-of-two divisors). Operands outside the normal range
+// only occur for r^2 = 0 / inf / NaN, where 1 - q is the same as the reference's.
+ORT_INLINE void normal_conic_rcp(double x, double y, double R, double k, double inv_r2,
+                                 double& nx, double& ny, double& nz) {
+  const double r2 = x * x + y * y;
+  const double a = (1.0 + k) * r2;
+  const double q0 = a * inv_r2;
+  const double rr = R * R;
+  const double q = fma(fma(-rr, q0, a), inv_r2, q0);
+  const double denom = R * sqrt(1.0 - q);
+  const auto dd = shared_div(denom);
+  const double dfdx = sdiv(x, dd);
+  const double dfdy = sdiv(y, dd);
+  const double mag = sqrt(dfdx * dfdx + dfdy * dfdy + 1.0);
   const auto dm = shared_div(mag);
   nx = sdiv(dfdx, dm);
   ny = sdiv(dfdy, dm);
@@ -1515,6 +1542,12 @@ ORT_INLINE void surface_normal(const ort_surface& s, const S& R, const S& K, PD 
       nx = T(0.0); ny = T(0.0); nz = T(1.0);
       break;
     case ORT_GEOM_STANDARD:
+      if constexpr (std::is_same<T, double>::value && std::is_same<S, double>::value) {
+        if (s.flags & ORT_SURF_INV_R2) {
+          normal_conic_rcp(r.x, r.y, R, K, s.inv_r2, nx, ny, nz);
+          break;
+        }
+      }
       normal_conic(r.x, r.y, R, K, nx, ny, nz);
       break;
     default:

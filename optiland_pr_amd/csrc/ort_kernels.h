@@ -381,6 +381,8 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(const KArgs a) {
       double nx, ny, nz;
       if (s.geometry == ORT_GEOM_PLANE) {
         nx = 0.0; ny = 0.0; nz = 1.0;
+      } else if (s.flags & ORT_SURF_INV_R2) {
+        ort::normal_conic_rcp(r.x, r.y, s.radius, s.conic, s.inv_r2, nx, ny, nz);
       } else {
         ort::normal_conic(r.x, r.y, s.radius, s.conic, nx, ny, nz);
       }
@@ -476,6 +478,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
     double nx, ny, nz;
     if (is_plane) {
       nx = 0.0; ny = 0.0; nz = 1.0;
+    } else if (s.flags & ORT_SURF_INV_R2) {
+      ort::normal_conic_rcp(r.x, r.y, s.radius, s.conic, s.inv_r2, nx, ny, nz);
     } else {
       ort::normal_conic(r.x, r.y, s.radius, s.conic, nx, ny, nz);
     }

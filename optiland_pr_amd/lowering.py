@@ -155,6 +155,13 @@ def lower_surface_group(surface_group, wavelengths, record=False, skip_object=Tr
         if isinstance(g, NewtonRaphsonGeometry) or g.geometry_id == _abi.GEOM_STANDARD:
             if np.isinf(R):
                 flags |= _abi.SURF_RADIUS_INF
+        if g.geometry_id == _abi.GEOM_STANDARD:
+            # the conic normal's divisor R * R with its correctly rounded reciprocal
+            # (ort_surface.inv_r2), when both are normal finite numbers
+            rr = np.float64(R) * np.float64(R)
+            if np.isfinite(rr) and 2.0**-300 <= rr <= 2.0**300:
+                row["inv_r2"] = np.float64(1.0) / rr
+                flags |= _abi.SURF_INV_R2
         if s.aperture is not None:
             if type(s.aperture) is RadialAperture:  # dedicated radial test
                 flags |= _abi.SURF_APERTURE
