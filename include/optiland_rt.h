@@ -43,9 +43,14 @@ enum ort_geometry { /* see optiland/geometries */
   ORT_GEOM_BICONIC = 7,      /* biconic.py:69-158                                  */
   ORT_GEOM_TOROIDAL = 8,     /* toroidal.py:75-233                                 */
   ORT_GEOM_FORBES_QBFS = 9,  /* forbes/geometry.py:183-330 + forbes/qpoly.py       */
-  ORT_GEOM_FORBES_Q2D = 10   /* forbes/geometry.py:333-640 + forbes/qpoly.py       */
+  ORT_GEOM_FORBES_Q2D = 10,  /* forbes/geometry.py:333-640 + forbes/qpoly.py       */
+  ORT_GEOM_GRID_SAG = 11     /* grid_sag.py:61-149: bilinear sag grid, own Newton   */
 };
 /* Coefficient blocks in lens.coef at ort_surface.coef_off (n_coef doubles):
+ *   GRID_SAG            nx, ny, x_0 .. x_(nx-1), y_0 .. y_(ny-1), sag[ny][nx] (row = y);
+ *                       the intersection starts at t = 0 and stops when max |dt| < tol
+ *                       over the call (grid_sag.py:108-140): schedule / newton_stat bit j
+ *                       then means "the stop test passed after j updates"
  *   EVEN / ODD_ASPHERE  C_0 .. C_{n-1}
  *   POLYNOMIAL          ni, nj, C[0][0], C[0][1], ..., C[ni-1][nj-1]  (x^i y^j, row-major)
  *   CHEBYSHEV           ni, nj, norm_x, norm_y, C[0][0], ..., C[ni-1][nj-1]

@@ -40,8 +40,9 @@ GEOM_BICONIC = 7
 GEOM_TOROIDAL = 8
 GEOM_FORBES_QBFS = 9
 GEOM_FORBES_Q2D = 10
+GEOM_GRID_SAG = 11
 FREEFORM_GEOMETRIES = (GEOM_POLYNOMIAL, GEOM_CHEBYSHEV, GEOM_BICONIC, GEOM_TOROIDAL,
-                       GEOM_FORBES_QBFS, GEOM_FORBES_Q2D)
+                       GEOM_FORBES_QBFS, GEOM_FORBES_Q2D, GEOM_GRID_SAG)
 NEWTON_GEOMETRIES = (GEOM_EVEN_ASPHERE, GEOM_ODD_ASPHERE, GEOM_ZERNIKE) + FREEFORM_GEOMETRIES
 
 # enum ort_surface_flags

@@ -31,6 +31,7 @@ from .geometries import (
     ForbesSolverConfig,
     ForbesSurfaceConfig,
     OddAsphere,
+    GridSagGeometry,
     Plane,
     PlaneGrating,
     PolynomialGeometry,
@@ -108,6 +109,9 @@ def _geometry(g):
     cs = _cs(g.cs)
     if name == "Plane":
         return Plane(cs)
+    if name == "GridSagGeometry":
+        return GridSagGeometry(cs, _np(g.x_grid), _np(g.y_grid), _np(g.sag_grid), g.tol,
+                               g.max_iter)
     if name == "PlaneGrating":
         return PlaneGrating(cs, _f(g.grating_order), _f(g.grating_period),
                             _f(g.groove_orientation_angle))

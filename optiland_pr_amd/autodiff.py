@@ -225,6 +225,9 @@ def vjp(dlens, seg_dev, px, py, n, seg_len, sched_dev, tables, n_param, cot, gra
     (zern_param, surf_tangent, final_tangent), each possibly None; cot: 8 tensors / None."""
     from .raytrace import _ptr, _stream_handle
 
+    if np.any(dlens.table.surfaces["geometry"] == _abi.GEOM_GRID_SAG):
+        raise NotImplementedError("autograd through grid-sag surfaces is not implemented by "
+                                  "the trace core (no derivative kernels)")
     if dlens.table.interaction_mask & ~(1 << _abi.IA_REFRACT_REFLECT):
         raise NotImplementedError("autograd through thin-lens, phase or grating surfaces is "
                                   "not implemented by the trace core (no derivative kernels)")

@@ -75,7 +75,8 @@ int fill_args(KArgs& a, const ort_lens* lens, const ort_batch* batch, const ort_
   if (lens->geometry_mask & (1u << ORT_GEOM_ZERNIKE)) feat |= ort::KM_ZERN;
   if (lens->geometry_mask & ((1u << ORT_GEOM_POLYNOMIAL) | (1u << ORT_GEOM_CHEBYSHEV) |
                              (1u << ORT_GEOM_BICONIC) | (1u << ORT_GEOM_TOROIDAL) |
-                             (1u << ORT_GEOM_FORBES_QBFS) | (1u << ORT_GEOM_FORBES_Q2D)))
+                             (1u << ORT_GEOM_FORBES_QBFS) | (1u << ORT_GEOM_FORBES_Q2D) |
+                             (1u << ORT_GEOM_GRID_SAG)))
     feat |= ort::KM_FREE;
   if (rec) feat |= F_REC;
   if (batch->w) {  // per-ray wavelengths: n, k from the material tables
@@ -223,6 +224,7 @@ int ort_trace_pupil_vjp(const ort_lens* lens, const double* px, const double* py
   if (opt->newton_mode != ORT_NEWTON_SCHEDULE) return ORT_ERR_ARG;
   if (params->zern_param && (feat & ort::KM_ZERN) == 0) return ORT_ERR_ARG;
   if (feat & F_IA) return ORT_ERR_ARG;  // no derivative kernels for thin-lens / phase / grating
+  if (lens->geometry_mask & (1u << ORT_GEOM_GRID_SAG)) return ORT_ERR_ARG;  // nor grid sags
   a.px = px;
   a.py = py;
   JArgs j{};

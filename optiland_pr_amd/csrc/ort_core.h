@@ -1316,6 +1316,99 @@ ORT_INLINE T sagnorm_q2d(const T& x, const T& y, const S& R, const S& k, bool ri
   return z;
 }
 
+// ---- grid sag: geometries/grid_sag.py:61-149 ------------------------------------------
+// Block (lens.coef at coef_off): nx, ny, x grid, y grid, sag[ny][nx]. Per-lane table reads
+// go through the generic address space (divergent indices).
+struct GridView {
+  const double* x;
+  const double* y;
+  const double* z;
+  int nx, ny;
+};
+
+template <class PD>
+ORT_INLINE GridView grid_view(PD C) {
+  GridView g;
+  g.nx = (int)C[0];
+  g.ny = (int)C[1];
+  g.x = (const double*)(C + 2);
+  g.y = g.x + g.nx;
+  g.z = g.y + g.ny;
+  return g;
+}
+
+// numpy.searchsorted(v, x, side="right") - 1, NaN sorting last
+ORT_INLINE int grid_cell(const double* v, int n, double x) {
+  if (!(x == x)) return n - 1;
+  int lo = 0, hi = n;  // first index with v[k] > x
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (v[mid] <= x)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo - 1;
+}
+
+// grid_sag.py:61-101: bilinear sag (NaN off the grid) and its x / y derivatives
+ORT_INLINE double grid_interp(const GridView& g, double x, double y, double& dsdx,
+                              double& dsdy) {
+  int i = grid_cell(g.x, g.nx, x);
+  int j = grid_cell(g.y, g.ny, y);
+  const bool off = (x < g.x[0]) || (x > g.x[g.nx - 1]) || (y < g.y[0]) || (y > g.y[g.ny - 1]);
+  i = i < 0 ? 0 : i;
+  j = j < 0 ? 0 : j;
+  i = i >= g.nx - 1 ? g.nx - 2 : i;
+  j = j >= g.ny - 1 ? g.ny - 2 : j;
+  const double x1 = g.x[i], x2 = g.x[i + 1], y1 = g.y[j], y2 = g.y[j + 1];
+  const double* r0 = g.z + (int64_t)j * g.nx + i;
+  const double z11 = r0[0], z12 = r0[1], z21 = r0[g.nx], z22 = r0[g.nx + 1];
+  const double tx = (x - x1) / (x2 - x1);
+  const double ty = (y - y1) / (y2 - y1);
+  const double z_y1 = z11 * (1.0 - tx) + z12 * tx;
+  const double z_y2 = z21 * (1.0 - tx) + z22 * tx;
+  const double sag = z_y1 * (1.0 - ty) + z_y2 * ty;
+  dsdx = ((z12 - z11) * (1.0 - ty) + (z22 - z21) * ty) / (x2 - x1);
+  dsdy = ((z21 - z11) * (1.0 - tx) + (z22 - z12) * tx) / (y2 - y1);
+  return off ? __builtin_nan("") : sag;
+}
+
+// grid_sag.py:103-106, 142-149: normal (-ds/dx, -ds/dy, 1) normalised
+ORT_INLINE double sagnorm_grid(const GridView& g, double x, double y, bool want_normal,
+                               double& nx, double& ny, double& nz) {
+  double dsdx, dsdy;
+  const double sag = grid_interp(g, x, y, dsdx, dsdy);
+  if (want_normal) {
+    const double mag = sqrt(dsdx * dsdx + dsdy * dsdy + 1.0);
+    const SharedDiv dm = shared_div(mag);
+    nx = sdiv(-dsdx, dm);
+    ny = sdiv(-dsdy, dm);
+    nz = sdiv(1.0, dm);
+  }
+  return sag;
+}
+
+// grid_sag.py:111-126: one Newton update from t (returns dt = -f / f')
+ORT_INLINE double grid_step(const GridView& g, const Ray& r, double t) {
+  const double xi = r.x + t * r.L;
+  const double yi = r.y + t * r.M;
+  const double zi = r.z + t * r.N;
+  double dsdx, dsdy;
+  const double f = grid_interp(g, xi, yi, dsdx, dsdy) - zi;
+  const double fp = dsdx * r.L + dsdy * r.M - r.N;
+  return -f / fp;
+}
+
+// grid_sag.py:131-140: rays that end off the grid get NaN
+ORT_INLINE double grid_final(const GridView& g, const Ray& r, double t) {
+  const double xf = r.x + t * r.L;
+  const double yf = r.y + t * r.M;
+  const bool off =
+      (xf < g.x[0]) || (xf > g.x[g.nx - 1]) || (yf < g.y[0]) || (yf > g.y[g.ny - 1]);
+  return off ? __builtin_nan("") : t;
+}
+
 // Sag and normal of a Newton-iterated geometry (EvenAsphere / OddAsphere / Zernike).
 // KM is a bitmask of the Newton kinds compiled in (KM_EVEN | KM_ODD | KM_ZERN): a lens
 // only pays registers for the kinds it contains.
@@ -1361,6 +1454,13 @@ ORT_INLINE T newton_sagnorm(const ort_surface& s, const S& R, const S& K, PD coe
       case ORT_GEOM_FORBES_Q2D:
         return sagnorm_q2d(x, y, R, K, (s.flags & ORT_SURF_RADIUS_INF) != 0, C, want_normal,
                            nx, ny, nz);
+      case ORT_GEOM_GRID_SAG:  // primal kernels only (no derivative kernels for grids)
+        if constexpr (std::is_same<T, double>::value) {
+          return sagnorm_grid(grid_view(C), x, y, want_normal, nx, ny, nz);
+        } else {
+          nx = ny = nz = T(NAN);
+          return T(NAN);
+        }
       default:
         return sagnorm_toroidal(x, y, C, want_normal, nx, ny, nz);
     }

@@ -200,11 +200,80 @@ __device__ inline int range_bit(const ort_surface& s) {
                                           : (int)ORT_STATUS_ZERNIKE_RANGE;
 }
 
+// Newton statistics of one (group, surface): AND of the per-update convergence bits and
+// the max non-converged index (see ort_newton_stat), read-before-atomic
+__device__ inline void report_newton(const KArgs& a, int si, bool active, int64_t group,
+                                     bool group_uniform, uint64_t mask, int last_bad) {
+  if (!a.stats) return;
+  if (!active) {
+    mask = ~0ull;
+    last_bad = -1;
+  }
+  ort_newton_stat* st = &a.stats[group * a.n_surf + si];
+  if (group_uniform) {
+    mask = wave_and_u64(mask);
+    last_bad = wave_max_i32(last_bad);
+    if ((threadIdx.x & 63) == 0) {
+      if (mask != ~0ull) and_if_changes(&st->conv_mask, mask);
+      if (last_bad >= 0) max_if_changes(&st->last_bad, last_bad);
+    }
+  } else if (active) {
+    if (mask != ~0ull) and_if_changes(&st->conv_mask, mask);
+    if (last_bad >= 0) max_if_changes(&st->last_bad, last_bad);
+  }
+}
+
+// Grid-sag intersection (grid_sag.py:108-140): Newton from t = 0, the reference stops
+// after the first update whose max |dt| over the call is < tol. Under the schedule every
+// ray makes exactly U updates and reports bit j = "|dt| < tol after update j" (j >= 1),
+// so the host's verify reads the stopping count exactly as for the other Newton kinds.
+template <uint32_t FEAT>
+__device__ inline double grid_distance(const KArgs& a, const ort_surface& s, int si,
+                                       const ort::Ray& r, bool active, int64_t group,
+                                       bool group_uniform) {
+  const ort::GridView g = ort::grid_view(a.coef + s.coef_off);
+  const double tol = s.tol;
+  const int max_iter = s.max_iter;
+  double t = 0.0;
+  if (a.newton_mode == ORT_NEWTON_WAVE) {
+    int j = 0;
+    while (j < max_iter) {
+      const double dt = ort::grid_step(g, r, t);
+      t = t + dt;
+      ++j;
+      if (__all(!active || fabs(dt) < tol)) break;
+    }
+    if (a.stats && (threadIdx.x & 63) == 0)
+      max_if_changes(&a.stats[(group_uniform ? group : 0) * a.n_surf + si].max_updates, j);
+    return ort::grid_final(g, r, t);
+  }
+  const int U = a.sched ? a.sched[group * a.n_surf + si] : max_iter;
+  uint64_t mask = 0;
+  int last_bad = -1;
+  for (int j = 0;; ++j) {
+    const bool lane_on = active && j < U;
+    if (!__any(lane_on)) break;
+    if (lane_on) {
+      const double dt = ort::grid_step(g, r, t);
+      t = t + dt;
+      const bool conv = fabs(dt) < tol;  // NaN never converges
+      if (conv && j + 1 < 64) mask |= 1ull << (j + 1);
+      if (!conv) last_bad = j + 1;
+    }
+  }
+  report_newton(a, si, active, group, group_uniform, mask, last_bad);
+  return ort::grid_final(g, r, t);
+}
+
 // Newton refinement of t at surface s for one lane (newton_raphson.py:119-168).
 template <uint32_t FEAT>
 __device__ inline double newton_distance(const KArgs& a, const ort_surface& s, int si,
                                          const ort::Ray& r, bool active, int64_t group,
                                          bool group_uniform, int& range_bits) {
+  if constexpr ((FEAT & ort::KM_FREE) != 0) {
+    if (s.geometry == ORT_GEOM_GRID_SAG)
+      return grid_distance<FEAT>(a, s, si, r, active, group, group_uniform);
+  }
   double t = ort::distance_conic(r, s.radius, s.conic, (s.flags & ORT_SURF_RADIUS_INF) != 0);
   const double tol = s.tol;
   const int max_iter = s.max_iter;

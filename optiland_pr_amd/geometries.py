@@ -126,6 +126,40 @@ class StandardGratingGeometry(StandardGeometry):
         self.groove_orientation_angle = groove_orientation_angle
 
 
+class GridSagGeometry(BaseGeometry):
+    """geometries/grid_sag.py:15-180: sag bilinearly interpolated on a rectangular grid
+    (NaN outside it), intersected by its own Newton loop from t = 0 with the global stop
+    rule max |dt| < tol."""
+
+    geometry_id = _abi.GEOM_GRID_SAG
+
+    def __init__(self, coordinate_system, x_coordinates, y_coordinates, sag_values,
+                 tol=1e-6, max_iter=100):
+        super().__init__(coordinate_system)
+        self.x_grid = np.asarray(x_coordinates, dtype=np.float64)
+        self.y_grid = np.asarray(y_coordinates, dtype=np.float64)
+        self.sag_grid = np.asarray(sag_values, dtype=np.float64)
+        self.tol = tol
+        self.max_iter = max_iter
+        self.is_symmetric = False
+        self.radius = np.inf
+        if self.sag_grid.shape != (len(self.y_grid), len(self.x_grid)):
+            raise ValueError(
+                f"Shape of sag_values {self.sag_grid.shape} must match "
+                f"(len(y_coordinates), len(x_coordinates)) = "
+                f"({len(self.y_grid)}, {len(self.x_grid)}).")
+        if len(self.x_grid) < 2 or len(self.y_grid) < 2:
+            raise ValueError("the sag grid needs at least 2 x 2 points")
+
+    def flip(self):
+        self.sag_grid = -self.sag_grid
+
+    def lower_params(self):
+        blk = [float(len(self.x_grid)), float(len(self.y_grid)), *self.x_grid.tolist(),
+               *self.y_grid.tolist(), *self.sag_grid.ravel().tolist()]
+        return np.inf, 0.0, float(self.tol), int(self.max_iter), 1.0, blk
+
+
 class NewtonRaphsonGeometry(StandardGeometry):
     """geometries/newton_raphson.py:43-168 (conic initial guess + Newton refinement)."""
 

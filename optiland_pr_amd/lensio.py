@@ -28,6 +28,7 @@ from .geometries import (
     ForbesQbfsGeometry,
     ForbesSolverConfig,
     ForbesSurfaceConfig,
+    GridSagGeometry,
     OddAsphere,
     Plane,
     PlaneGrating,
@@ -75,6 +76,9 @@ def geometry_from_dict(d):
     tol, max_iter = _f(d.get("tol"), 1e-10), int(d.get("max_iter", 100))
     if t == "Plane":
         return Plane(cs)
+    if t == "GridSagGeometry":  # grid_sag.py:155-180
+        return GridSagGeometry(cs, d["x_coordinates"], d["y_coordinates"], d["sag_values"],
+                               _f(d.get("tol"), 1e-6), int(d.get("max_iter", 100)))
     if t in ("PlaneGrating", "StandardGratingGeometry"):
         # plane_grating.py / standard_grating.py to_dict write "order" / "period" /
         # "angle" (the reference's own from_dict cannot read them back)
@@ -154,6 +158,10 @@ def geometry_to_dict(g):
         d["surface_config"] = {"radius": scalar(g.radius), "conic": scalar(g.k),
                                "norm_radius": g.norm_radius, "terms": terms}
         d["solver_config"] = {"tol": g.tol, "max_iter": g.max_iter}
+        return d
+    if isinstance(g, GridSagGeometry):
+        d.update(x_coordinates=g.x_grid.tolist(), y_coordinates=g.y_grid.tolist(),
+                 sag_values=g.sag_grid.tolist(), tol=g.tol, max_iter=g.max_iter)
         return d
     if isinstance(g, (PlaneGrating, StandardGratingGeometry)):
         d.update(order=g.grating_order, period=g.grating_period,

@@ -436,6 +436,29 @@ class Grating(Optic):
         self.update_paraxial()
 
 
+class GridSagLens(Optic):
+    """A singlet whose front surface is a 17 x 13 bilinear sag grid (grid_sag.py)."""
+
+    def __init__(self):
+        super().__init__()
+        gx = np.linspace(-7, 7, 17)
+        gy = np.linspace(-6, 6, 13)
+        X, Y = np.meshgrid(gx, gy)
+        z = (X**2 + Y**2) / 80.0 + 0.003 * X * Y - 0.02 * Y
+        self.add_surface(index=0, thickness=np.inf)
+        self.add_surface(index=1, surface_type="grid_sag", x_coordinates=gx.tolist(),
+                         y_coordinates=gy.tolist(), sag_values=z.tolist(), thickness=4.0,
+                         material="SK16", is_stop=True)
+        self.add_surface(index=2, radius=-60.0, thickness=45.0)
+        self.add_surface(index=3)
+        self.set_aperture(aperture_type="EPD", value=10)
+        self.set_field_type(field_type="angle")
+        self.add_field(y=0)
+        self.add_field(y=5)
+        self.add_field(x=3, y=2)
+        self.add_wavelength(value=0.55, is_primary=True)
+
+
 GOLDEN_LENSES = {
     "cooke": CookeTriplet,
     "dg": DoubleGauss,
@@ -460,4 +483,5 @@ GOLDEN_LENSES = {
     "grating_curved": lambda: Grating("curved"),
     "grating_reflective": lambda: Grating("reflective"),
     "grating_tilted": lambda: Grating("curved", angle=0.35),
+    "grid_lens": GridSagLens,
 }

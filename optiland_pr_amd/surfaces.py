@@ -26,6 +26,7 @@ from .geometries import (
     ForbesSurfaceConfig,
     OddAsphere,
     Plane,
+    GridSagGeometry,
     PlaneGrating,
     PolynomialGeometry,
     StandardGratingGeometry,
@@ -171,6 +172,10 @@ def _make_geometry(surface_type, cs, kw):
         return ToroidalGeometry(cs, kw.get("radius_x", np.inf), kw.get("radius_y", np.inf),
                                 kw.get("conic", 0.0), kw.get("toroidal_coeffs_poly_y", []),
                                 tol, max_iter)
+    if st == "grid_sag":  # geometry_factory.py:340-349, GridSagConfig defaults
+        return GridSagGeometry(cs, kw.get("x_coordinates", []), kw.get("y_coordinates", []),
+                               kw.get("sag_values", []), kw.get("tol", 1e-6),
+                               kw.get("max_iter", 100))
     if st in ("forbes_qbfs", "forbes_q2d"):  # geometry_factory.py:282-314
         cfg = ForbesSurfaceConfig(
             radius=radius, conic=conic, norm_radius=kw.get("norm_radius", 1.0),
@@ -180,7 +185,7 @@ def _make_geometry(surface_type, cs, kw):
     raise ValueError(
         f"Surface type {st!r} is not lowered to the MI355X trace core (supported: "
         "standard, plane, paraxial, grating, even_asphere, odd_asphere, zernike, "
-        "polynomial, chebyshev, biconic, toroidal, forbes_qbfs, forbes_q2d).")
+        "polynomial, chebyshev, biconic, toroidal, forbes_qbfs, forbes_q2d, grid_sag).")
 
 
 class SurfaceGroup:

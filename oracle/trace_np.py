@@ -705,6 +705,72 @@ def normal_q2d(x, y, R, k, B):
     return dfx / sm, dfy / sm, -1.0 / sm
 
 
+def _grid(B):
+    n, m = int(B[0]), int(B[1])
+    xg = np.asarray(B[2:2 + n], dtype=np.float64)
+    yg = np.asarray(B[2 + n:2 + n + m], dtype=np.float64)
+    zg = np.asarray(B[2 + n + m:2 + n + m + n * m], dtype=np.float64).reshape(m, n)
+    return xg, yg, zg
+
+
+def grid_interpolate(B, x, y):
+    """grid_sag.py:61-101 (bilinear sag, its derivatives, NaN outside the grid)."""
+    xg, yg, zg = _grid(B)
+    i = np.searchsorted(xg, x, side="right") - 1
+    j = np.searchsorted(yg, y, side="right") - 1
+    nan_mask = (x < xg[0]) | (x > xg[-1]) | (y < yg[0]) | (y > yg[-1])
+    i = np.where(i < 0, 0, i)
+    j = np.where(j < 0, 0, j)
+    i = np.where(i >= len(xg) - 1, len(xg) - 2, i)
+    j = np.where(j >= len(yg) - 1, len(yg) - 2, j)
+    x1, x2 = xg[i], xg[i + 1]
+    y1, y2 = yg[j], yg[j + 1]
+    z11, z12 = zg[j, i], zg[j, i + 1]
+    z21, z22 = zg[j + 1, i], zg[j + 1, i + 1]
+    tx = (x - x1) / (x2 - x1)
+    ty = (y - y1) / (y2 - y1)
+    z_y1 = z11 * (1 - tx) + z12 * tx
+    z_y2 = z21 * (1 - tx) + z22 * tx
+    sag = z_y1 * (1 - ty) + z_y2 * ty
+    ds_dx = ((z12 - z11) * (1 - ty) + (z22 - z21) * ty) / (x2 - x1)
+    ds_dy = ((z21 - z11) * (1 - tx) + (z22 - z12) * tx) / (y2 - y1)
+    return np.where(nan_mask, np.nan, sag), ds_dx, ds_dy
+
+
+def normal_grid(B, x, y):
+    """grid_sag.py:142-149."""
+    _, ds_dx, ds_dy = grid_interpolate(B, x, y)
+    nx, ny, nz = -ds_dx, -ds_dy, np.ones_like(x)
+    mag = np.sqrt(nx**2 + ny**2 + nz**2)
+    return nx / mag, ny / mag, nz / mag
+
+
+def distance_grid(r: Rays, B, tol, max_iter, sched=None):
+    """grid_sag.py:108-140: Newton from t = 0, global stop max|dt| < tol checked after
+    each update, rays off the grid -> NaN. Returns (t, updates)."""
+    xg, yg, _ = _grid(B)
+    t = np.zeros_like(r.x)
+    updates = 0
+    for _ in range(max_iter):
+        if sched is not None and updates >= sched:
+            break
+        x_i = r.x + t * r.L
+        y_i = r.y + t * r.M
+        z_i = r.z + t * r.N
+        sag, ds_dx, ds_dy = grid_interpolate(B, x_i, y_i)
+        f = sag - z_i
+        f_prime = ds_dx * r.L + ds_dy * r.M - r.N
+        dt = -f / f_prime
+        t = t + dt
+        updates += 1
+        if sched is None and np.max(np.abs(dt)) < tol:
+            break
+    x_f = r.x + t * r.L
+    y_f = r.y + t * r.M
+    oob = (x_f < xg[0]) | (x_f > xg[-1]) | (y_f < yg[0]) | (y_f > yg[-1])
+    return np.where(oob, np.nan, t), updates
+
+
 def _geometry_fns(table, s):
     g = int(s["geometry"])
     R, k = float(s["radius"]), float(s["conic"])
@@ -745,6 +811,9 @@ def _geometry_fns(table, s):
         k_ = np.array(k_yz)
         return ((lambda x, y: sag_toroidal(x, y, R_rot, R_yz, c, k_, poly)),
                 (lambda x, y: normal_toroidal(x, y, R_rot, R_yz, c, k_, poly)))
+    if g == _abi.GEOM_GRID_SAG:
+        return ((lambda x, y: grid_interpolate(B, x, y)[0]),
+                (lambda x, y: normal_grid(B, x, y)))
     if g in (_abi.GEOM_FORBES_QBFS, _abi.GEOM_FORBES_Q2D):
         Rf, kf = np.array(R), np.array(k)
         sag_f, nrm_f = ((sag_qbfs, normal_qbfs) if g == _abi.GEOM_FORBES_QBFS
@@ -757,6 +826,11 @@ def distance_newton(r: Rays, table, s, sched=None):
     """newton_raphson.py:119-168. Returns (t, updates). The stop test is GLOBAL over all
     rays of this trace call: max(|f|) < tol (NaN never passes). If sched is given,
     exactly that many updates are made instead."""
+    if int(s["geometry"]) == _abi.GEOM_GRID_SAG:
+        off, nc = int(s["coef_off"]), int(s["n_coef"])
+        with np.errstate(invalid="ignore", divide="ignore"):
+            return distance_grid(r, table.coef[off:off + nc], float(s["tol"]),
+                                 int(s["max_iter"]), sched)
     sag, normal = _geometry_fns(table, s)
     t = distance_conic(r, float(s["radius"]), float(s["conic"]),
                        bool(int(s["flags"]) & _abi.SURF_RADIUS_INF))

@@ -74,9 +74,13 @@ def build(spec):
         cfg = ForbesSurfaceConfig(radius=spec["radius"], conic=spec["conic"],
                                   norm_radius=spec["norm_radius"], terms=terms)
         return (ForbesQbfsGeometry if k == "forbes_qbfs" else ForbesQ2dGeometry)(cs, cfg)
+    if k == "grid_sag":
+        from optiland_pr_amd.geometries import GridSagGeometry
+
+        return GridSagGeometry(cs, spec["x"], spec["y"], spec["sag"])
     raise ValueError(k)
 
 
 CASES = sorted(specs())
 NEWTON_KINDS = ("even_asphere", "odd_asphere", "zernike", "polynomial", "chebyshev",
-                "biconic", "toroidal", "forbes_qbfs", "forbes_q2d")
+                "biconic", "toroidal", "forbes_qbfs", "forbes_q2d", "grid_sag")

@@ -124,6 +124,11 @@ SPECS = {
 }
 
 
+SPECS["grid_tilt"] = dict(kind="grid_sag", x=[-1.0, 1.0], y=[-1.0, 1.0],  # test_grid_sag_geometry.py:49-76
+                          sag=[[-0.1, 0.1], [-0.1, 0.1]])
+SPECS["grid_bowl"] = dict(kind="grid_sag", x=[-9.0, -7.875, -6.75, -5.625, -4.5, -3.375, -2.25, -1.125, 0.0, 1.125, 2.25, 3.375, 4.5, 5.625, 6.75, 7.875, 9.0], y=[-7.0, -5.833333333333333, -4.666666666666666, -3.5, -2.333333333333333, -1.166666666666666, 0.0, 1.1666666666666679, 2.333333333333334, 3.5, 4.666666666666668, 5.833333333333334, 7.0], sag=[[2.796, 2.4005625, 2.05575, 1.7615625000000001, 1.518, 1.3250625, 1.1827500000000002, 1.0910625, 1.05, 1.0595625, 1.11975, 1.2305625, 1.3920000000000001, 1.6040625, 1.8667500000000001, 2.1800624999999996, 2.544], [2.4638888888888886, 2.071076388888889, 1.728888888888889, 1.4373263888888888, 1.1963888888888887, 1.0060763888888888, 0.8663888888888888, 0.7773263888888888, 0.7388888888888888, 0.7510763888888887, 0.8138888888888888, 0.9273263888888887, 1.0913888888888887, 1.3060763888888887, 1.5713888888888887, 1.887326388888889, 2.2538888888888886], [2.1862222222222223, 1.796034722222222, 1.456472222222222, 1.167534722222222, 0.9292222222222221, 0.741534722222222, 0.6044722222222221, 0.5180347222222221, 0.4822222222222221, 0.4970347222222221, 0.562472222222222, 0.6785347222222221, 0.845222222222222, 1.0625347222222221, 1.330472222222222, 1.6490347222222221, 2.018222222222222], [1.9629999999999999, 1.5754375, 1.2385, 0.9521875000000001, 0.7165, 0.5314375, 0.397, 0.31318750000000006, 0.28, 0.2974375, 0.36550000000000005, 0.4841875, 0.6535000000000001, 0.8734375, 1.144, 1.4651874999999999, 1.837], [1.7942222222222224, 1.4092847222222225, 1.0749722222222224, 0.7912847222222221, 0.5582222222222222, 0.37578472222222215, 0.2439722222222222, 0.16278472222222218, 0.13222222222222219, 0.15228472222222217, 0.22297222222222218, 0.3442847222222222, 0.5162222222222221, 0.7387847222222221, 1.0119722222222223, 1.3357847222222223, 1.7102222222222223], [1.679888888888889, 1.297576388888889, 0.9658888888888889, 0.6848263888888888, 0.4543888888888889, 0.2745763888888889, 0.14538888888888887, 0.06682638888888885, 0.038888888888888855, 0.06157638888888886, 0.13488888888888886, 0.2588263888888889, 0.4333888888888889, 0.6585763888888889, 0.9343888888888888, 1.2608263888888889, 1.6378888888888892], [1.62, 1.2403125, 0.91125, 0.6328125, 0.405, 0.2278125, 0.10125, 0.0253125, 0.0, 0.0253125, 0.10125, 0.2278125, 0.405, 0.6328125, 0.91125, 1.2403125, 1.62], [1.6145555555555555, 1.2374930555555554, 0.9110555555555555, 0.6352430555555555, 0.4100555555555556, 0.23549305555555558, 0.1115555555555556, 0.03824305555555559, 0.015555555555555597, 0.0434930555555556, 0.12205555555555561, 0.25124305555555565, 0.43105555555555564, 0.6614930555555556, 0.9425555555555556, 1.2742430555555555, 1.6565555555555558], [1.6635555555555555, 1.2891180555555555, 0.9653055555555556, 0.6921180555555557, 0.4695555555555556, 0.29761805555555565, 0.17630555555555558, 0.10561805555555559, 0.0855555555555556, 0.1161180555555556, 0.1973055555555556, 0.3291180555555556, 0.5115555555555557, 0.7446180555555557, 1.0283055555555556, 1.3626180555555556, 1.7475555555555555], [1.7670000000000001, 1.3951875, 1.074, 0.8034374999999999, 0.5835, 0.41418750000000004, 0.2955, 0.2274375, 0.21, 0.24318750000000003, 0.32699999999999996, 0.46143750000000006, 0.6465, 0.8821875, 1.1685, 1.5054375000000002, 1.893], [1.924888888888889, 1.5557013888888889, 1.2371388888888892, 0.9692013888888891, 0.751888888888889, 0.5852013888888891, 0.46913888888888905, 0.40370138888888907, 0.3888888888888891, 0.4247013888888891, 0.5111388888888891, 0.648201388888889, 0.8358888888888891, 1.074201388888889, 1.3631388888888891, 1.7027013888888891, 2.092888888888889], [2.137222222222223, 1.7706597222222225, 1.4547222222222222, 1.1894097222222224, 0.9747222222222223, 0.8106597222222223, 0.6972222222222224, 0.6344097222222224, 0.6222222222222223, 0.6606597222222225, 0.7497222222222224, 0.8894097222222224, 1.0797222222222222, 1.3206597222222225, 1.6122222222222224, 1.9544097222222223, 2.3472222222222228], [2.4040000000000004, 2.0400625, 1.72675, 1.4640624999999998, 1.252, 1.0905624999999999, 0.9797499999999999, 0.9195625000000001, 0.9099999999999999, 0.9510624999999999, 1.04275, 1.1850625, 1.378, 1.6215625, 1.91575, 2.2605625000000003, 2.656]])
+
+
 def _forbes(spec):
     cfg = dict(radius=spec["radius"], conic=spec["conic"], norm_radius=spec["norm_radius"])
     if spec["kind"] == "forbes_qbfs":
@@ -170,6 +175,8 @@ def build(spec):
         cls = (geometries.ForbesQbfsGeometry if k == "forbes_qbfs"
                else geometries.ForbesQ2dGeometry)
         return cls(cs, geometries.ForbesSurfaceConfig(**_forbes(spec)))
+    if k == "grid_sag":
+        return geometries.GridSagGeometry(cs, spec["x"], spec["y"], spec["sag"])
     raise ValueError(k)
 
 

@@ -399,6 +399,35 @@ def grating(kind, angle=0.0):
     return _grating_common(lens)
 
 
+def grid_sag_values():
+    """A 17 x 13 sag grid over [-7, 7] x [-6, 6] mm: a weak sphere-like bowl, an xy term
+    and a y tilt (shared with optiland_pr_amd.samples.GridSagLens)."""
+    gx = np.linspace(-7, 7, 17)
+    gy = np.linspace(-6, 6, 13)
+    X, Y = np.meshgrid(gx, gy)
+    return gx, gy, (X**2 + Y**2) / 80.0 + 0.003 * X * Y - 0.02 * Y
+
+
+def grid_lens():
+    """A singlet whose front surface is a bilinear sag grid (grid_sag.py), behind it a
+    sphere: covers the grid Newton loop (t from 0, global max|dt| < tol)."""
+    gx, gy, z = grid_sag_values()
+    lens = ref_optic.Optic()
+    lens.add_surface(index=0, thickness=np.inf)
+    lens.add_surface(index=1, surface_type="grid_sag", x_coordinates=gx.tolist(),
+                     y_coordinates=gy.tolist(), sag_values=z.tolist(), thickness=4.0,
+                     material="SK16", is_stop=True)
+    lens.add_surface(index=2, radius=-60.0, thickness=45.0)
+    lens.add_surface(index=3)
+    lens.set_aperture(aperture_type="EPD", value=10)
+    lens.set_field_type(field_type="angle")
+    lens.add_field(y=0)
+    lens.add_field(y=5)
+    lens.add_field(x=3, y=2)
+    lens.add_wavelength(value=0.55, is_primary=True)
+    return lens
+
+
 def json_lens(name):
     """A lens file from the reference's docs/samples (copied as data to tests/golden/lenses),
     loaded with the reference's own Optic.from_dict (optic.py:674-713)."""
@@ -444,6 +473,7 @@ CASES = {
                            [0.587], "uniform", 24),
     "grating_tilted": (lambda: grating("curved", angle=0.35), [(0, 0), (0.2, 0.8)], [0.587],
                        "uniform", 24),
+    "grid_lens": (grid_lens, [(0, 0), (0, 1), (0.6, 0.6)], [0.48, 0.55], "uniform", 24),
 }
 
 
