@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define ORT_ABI_VERSION 9
+#define ORT_ABI_VERSION 10
 #define ORT_MAX_SURFACES 64
 
 /* ---- geometry kinds ----------------------------------- */
@@ -74,8 +74,19 @@ enum ort_surface_flags {
   ORT_SURF_RECORD = 1u << 3,     /* snapshot the ray state after this surface (_record)  */
   ORT_SURF_TRANSLATE = 1u << 4,  /* informational: the frame is the translation cs_t only  */
   ORT_SURF_APERTURE_PROG = 1u << 5, /* general aperture: a program in lens.coef (ap_off) */
-  ORT_SURF_INV_R2 = 1u << 6        /* inv_r2 holds RN(1 / (R * R)) (finite, normal range)  */
-                                 /* (both op lists empty)                                  */
+  ORT_SURF_INV_R2 = 1u << 6,       /* inv_r2 holds RN(1 / (R * R)) (finite, normal range)  */
+  ORT_SURF_ALPHA_ALL = 1u << 7,    /* optics.alpha_pre > 0 at every wavelength row: the     */
+                                   /* absorption step runs unconditionally (homogeneous.py) */
+  ORT_SURF_ALPHA_NONE = 1u << 8    /* optics.alpha_pre == 0 at every row: no absorption     */
+                                   /* (neither bit: decided per ray / row)                  */
+};
+
+/* ---- lens-wide frame facts (ort_lens.frame_flags) --------------------------------- */
+enum ort_lens_flags {
+  /* every surface's frame is a translation along z only: both op lists empty and
+   * cs_t[0], cs_t[1] == +0 (a centred axial lens such as every sample objective). The
+   * kernels then skip localize's x + -0, y + -0 (identities) and the op-list loops. */
+  ORT_LENS_AXIAL = 1u << 0
 };
 
 /* ---- interaction models (optiland/interactions) ----------------------------------
@@ -153,7 +164,12 @@ typedef struct ort_surface {
                        /* normal's (1 + k) r^2 / (R * R) is then q = a y refined once by  */
                        /* its residual (Markstein), the same IEEE quotient without a      */
                        /* per-ray reciprocal                                              */
-} ort_surface; /* 144 bytes */
+  /* lens-constant subexpressions of the conic formulas, formed on the host with the same
+   * IEEE operations (standard.py:104-118, 154-167): 2 R, RN(1 + k), RN(R * R) */
+  double two_r;
+  double one_plus_k;
+  double r_sq;
+} ort_surface; /* 168 bytes */
 
 /* Aperture programs (the physical_apertures package): postfix, each op a double opcode followed
  * by its operands; primitives push contains(x, y) of the ray's local (x, y), the boolean
@@ -187,7 +203,8 @@ typedef struct ort_surface_optics {
                     /* reference forms per ray                                        */
   double alpha_pre; /* 4 pi k / lambda of material_pre, 0 when k == 0 (homogeneous.py) */
   double n_post;    /* n of material_post (thin-lens / phase / grating interactions)  */
-} ort_surface_optics; /* 32 bytes */
+  double u_sq;      /* RN(u * u), the u ** 2 of real_rays.py:156                       */
+} ort_surface_optics; /* 40 bytes */
 
 /* One Zernike term: c * norm * R_n^|m|(rho) * {cos m phi | sin |m| phi}
  * (zernike/base.py:42-68, 228-299). Radial coefficients a_k (for rho^(n-2k)) and
@@ -258,6 +275,8 @@ typedef struct ort_lens {
   const double* wavelengths; /* [n_lambda] um, the wavelength of each table row (phase  *
                               * and grating interactions use it); may be NULL when      *
                               * interaction_mask has no PHASE / DIFFRACTIVE bit         */
+  uint32_t frame_flags;      /* enum ort_lens_flags (0: make no assumption)              */
+  uint32_t reserved;
 } ort_lens;
 
 /* Ray state, structure of arrays, one double per ray per attribute (device). */
@@ -323,12 +342,18 @@ enum ort_newton_mode {
   ORT_NEWTON_WAVE = 1
 };
 
+/* Newton statistics of one (group, surface). The "stop index" k of an update sequence is
+ * the number of updates after which the reference's global test would pass: for the
+ * Newton-Raphson kinds the test |f(t_k)| < tol evaluated before update k (k = 0 .. U,
+ * newton_raphson.py:140-149), for GRID_SAG the test |dt| < tol after update k - 1
+ * (k = 1 .. U, grid_sag.py:125-129; bit 0 is never set). */
 typedef struct ort_newton_stat {
-  uint64_t conv_mask;  /* AND over rays: bit j set when |f(t_j)| < tol (j < 64)      */
-  int32_t last_bad;    /* max over rays of the largest j <= sched with |f(t_j)| >= tol
-                          or NaN; -1 when every ray converged at every j              */
-  int32_t max_updates; /* ORT_NEWTON_WAVE: max updates any wave performed            */
-} ort_newton_stat; /* 16 bytes */
+  uint64_t conv_mask[2]; /* AND over rays: bit b of word w set when the test passed at
+                            stop index k = opt.conv_base + 64 w + b (a 128-index window) */
+  int32_t last_bad;      /* max over rays of the largest k <= sched that failed the test
+                            (or was NaN); -1 when every ray passed at every k            */
+  int32_t max_updates;   /* ORT_NEWTON_WAVE: max updates any wave performed              */
+} ort_newton_stat; /* 24 bytes */
 
 typedef struct ort_options {
   int32_t newton_mode;   /* enum ort_newton_mode                                     */
@@ -337,12 +362,18 @@ typedef struct ort_options {
    * and surface (entries of non-Newton surfaces are ignored). NULL means "max_iter"
    * everywhere. */
   const int32_t* sched;
+  /* first stop index of the ort_newton_stat.conv_mask window (>= 0; 0 covers every
+   * schedule up to 127 updates -- the default max_iter is 100) */
+  int32_t conv_base;
+  int32_t reserved;
 } ort_options;
 
 /* status bits written with atomicOr into *status (device int32) */
 enum ort_status {
-  ORT_STATUS_ZERNIKE_RANGE = 1u << 0,  /* zernike.py:234-246 ValueError            */
-  ORT_STATUS_CHEBYSHEV_RANGE = 1u << 1 /* chebyshev.py:203-215 ValueError          */
+  ORT_STATUS_ZERNIKE_RANGE = 1u << 0,   /* zernike.py:234-246 ValueError            */
+  ORT_STATUS_CHEBYSHEV_RANGE = 1u << 1, /* chebyshev.py:203-215 ValueError          */
+  ORT_STATUS_BAD_GEOMETRY = 1u << 2     /* a surface with an unknown geometry id: its
+                                           rays are NaN (never a silent substitute)  */
 };
 
 /* Pupil distribution generated on the device (distribution.py:72-408), see
@@ -479,7 +510,7 @@ int ort_generate_rays(const double* px, const double* py, ort_rays* rays_out,
 /* Error codes */
 enum ort_error {
   ORT_OK = 0,
-  ORT_ERR_ARG = -1,      /* null pointer / bad size                                   */
+  ORT_ERR_ARG = -1,      /* null pointer / bad size / unknown geometry_mask bits       */
   ORT_ERR_SURFACES = -2, /* n_surfaces outside [0, ORT_MAX_SURFACES]                  */
   ORT_ERR_LAUNCH = -3    /* hipGetLastError() after launch                            */
 };

@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import numpy as np
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 VJP_UNROLLED = 0
 VJP_ADJOINT = 1
 AP_RADIAL = 1
@@ -53,6 +53,9 @@ SURF_RECORD = 1 << 3
 SURF_TRANSLATE = 1 << 4
 SURF_APERTURE_PROG = 1 << 5
 SURF_INV_R2 = 1 << 6
+SURF_ALPHA_ALL = 1 << 7
+SURF_ALPHA_NONE = 1 << 8
+LENS_AXIAL = 1 << 0  # ort_lens.frame_flags
 
 # enum ort_interaction / ort_phase_kind
 IA_REFRACT_REFLECT = 0
@@ -80,6 +83,7 @@ NEWTON_WAVE = 1
 # enum ort_status
 STATUS_ZERNIKE_RANGE = 1 << 0
 STATUS_CHEBYSHEV_RANGE = 1 << 1
+STATUS_BAD_GEOMETRY = 1 << 2
 
 CS_OP = np.dtype(
     [("kind", "<i4"), ("reserved", "<i4"), ("p", "<f8", (3,))], align=True
@@ -112,15 +116,19 @@ SURFACE = np.dtype(
         ("interaction", "<i4"),
         ("ia_off", "<i4"),
         ("inv_r2", "<f8"),
+        ("two_r", "<f8"),
+        ("one_plus_k", "<f8"),
+        ("r_sq", "<f8"),
     ],
     align=True,
 )
-assert SURFACE.itemsize == 144
+assert SURFACE.itemsize == 168
 
 SURFACE_OPTICS = np.dtype(
-    [("n_pre", "<f8"), ("u", "<f8"), ("alpha_pre", "<f8"), ("n_post", "<f8")], align=True
+    [("n_pre", "<f8"), ("u", "<f8"), ("alpha_pre", "<f8"), ("n_post", "<f8"), ("u_sq", "<f8")],
+    align=True,
 )
-assert SURFACE_OPTICS.itemsize == 32
+assert SURFACE_OPTICS.itemsize == 40
 
 ZERNIKE_TERM = np.dtype(
     [
@@ -171,8 +179,9 @@ MATERIAL = np.dtype(
 assert MATERIAL.itemsize == 40
 
 NEWTON_STAT = np.dtype(
-    [("conv_mask", "<u8"), ("last_bad", "<i4"), ("max_updates", "<i4")], align=True
+    [("conv_mask", "<u8", (2,)), ("last_bad", "<i4"), ("max_updates", "<i4")], align=True
 )
-assert NEWTON_STAT.itemsize == 16
+assert NEWTON_STAT.itemsize == 24
+CONV_WINDOW = 128  # stop indices per conv_mask window (ort_options.conv_base)
 
 RAY_FIELDS = ("x", "y", "z", "L", "M", "N", "i", "opd")

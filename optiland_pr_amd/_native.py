@@ -31,6 +31,8 @@ class ort_lens(C.Structure):
         ("final_thickness", C.c_double),
         ("materials", C.c_void_p),
         ("wavelengths", C.c_void_p),
+        ("frame_flags", C.c_uint32),
+        ("reserved", C.c_uint32),
     ]
 
 
@@ -84,6 +86,8 @@ class ort_options(C.Structure):
         ("newton_mode", C.c_int32),
         ("start_surface", C.c_int32),
         ("sched", C.c_void_p),
+        ("conv_base", C.c_int32),
+        ("reserved", C.c_int32),
     ]
 
 

@@ -16,7 +16,7 @@ int launch_geom(const ort_lens* lens, int32_t surface, int64_t n, const ort_rays
   if (!lens || n < 0) return ORT_ERR_ARG;
   if (n == 0) return ORT_OK;
   if (surface < 0 || surface >= lens->n_surfaces) return ORT_ERR_ARG;
-  const ort_options dflt{ORT_NEWTON_SCHEDULE, 0, nullptr};
+  const ort_options dflt{ORT_NEWTON_SCHEDULE, 0, nullptr, 0, 0};
   ort_batch b{};
   b.n_rays = n;
   b.seg_len = n;
@@ -66,6 +66,11 @@ int fill_args(KArgs& a, const ort_lens* lens, const ort_batch* batch, const ort_
   a.newton_mode = opt->newton_mode;
   a.start_surface = opt->start_surface;
   a.sched = opt->sched;
+  a.conv_base = opt->conv_base;
+  if (opt->conv_base < 0) return ORT_ERR_ARG;
+  // geometry ids this library knows (enum ort_geometry): anything else is refused here
+  // rather than traced as some other kind
+  if (lens->geometry_mask & ~((2u << ORT_GEOM_GRID_SAG) - 1u)) return ORT_ERR_ARG;
   a.rec = rec;
   a.stats = stats;
   a.status = status;
@@ -93,6 +98,7 @@ int fill_args(KArgs& a, const ort_lens* lens, const ort_batch* batch, const ort_
     const uint32_t need_w = (1u << ORT_IA_PHASE) | (1u << ORT_IA_DIFFRACTIVE);
     if ((lens->interaction_mask & need_w) && !batch->w && !lens->wavelengths) return ORT_ERR_ARG;
   }
+  if (lens->frame_flags & ORT_LENS_AXIAL) feat |= F_AXIAL;
   if (opt->newton_mode != ORT_NEWTON_SCHEDULE && opt->newton_mode != ORT_NEWTON_WAVE)
     return ORT_ERR_ARG;
   return ORT_OK;
@@ -100,9 +106,9 @@ int fill_args(KArgs& a, const ort_lens* lens, const ort_batch* batch, const ort_
 
 int launch(const KArgs& a, uint32_t feat, hipStream_t stream) {
   if (a.n_rays == 0) return ORT_OK;
-  KernelFn fn = (feat & F_IA) != 0    ? select_trace_ia(feat)
+  KernelFn fn = (feat & F_IA) != 0    ? select_trace_ia(feat & ~F_AXIAL)
                 : (feat & F_KM) == 0 ? select_closed(feat)
-                                     : select_trace(feat & ~F_MONO);
+                                     : select_trace(feat & ~(F_MONO | F_AXIAL));
   if (!fn) return ORT_ERR_ARG;
   const int64_t blocks = (a.n_rays + kBlock - 1) / kBlock;
   if (blocks > 0x7fffffff) return ORT_ERR_ARG;
@@ -113,7 +119,7 @@ int launch(const KArgs& a, uint32_t feat, hipStream_t stream) {
 int init_outputs(const KArgs& a, hipStream_t stream) {
   if (a.stats) {
     const int64_t groups = (a.n_rays + a.group_len - 1) / a.group_len;
-    // conv_mask = ~0, last_bad = -1, max_updates = -1 (all 0xFF bytes)
+    // conv_mask = {~0, ~0}, last_bad = -1, max_updates = -1 (all 0xFF bytes)
     if (hipMemsetAsync(a.stats, 0xFF, (size_t)(groups > 0 ? groups : 1) * a.n_surf *
                                           sizeof(ort_newton_stat),
                        stream) != hipSuccess)

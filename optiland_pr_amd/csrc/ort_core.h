@@ -1461,8 +1461,10 @@ ORT_INLINE T newton_sagnorm(const ort_surface& s, const S& R, const S& K, PD coe
           nx = ny = nz = T(NAN);
           return T(NAN);
         }
-      default:
+      case ORT_GEOM_TOROIDAL:
         return sagnorm_toroidal(x, y, C, want_normal, nx, ny, nz);
+      default:  // an id this library does not know: NaN, never another kind's sag
+        break;
     }
   }
   nx = ny = nz = T(NAN);
@@ -1511,6 +1513,17 @@ ORT_INLINE void propagate(RayT<T>& r, const T& t, double alpha) {
   r.y = r.y + t * r.M;
   r.z = r.z + t * r.N;
   if (alpha > 0.0) r.att = r.att + -alpha * t * 1e3;
+}
+
+// propagate with the surface's absorption decided by its ORT_SURF_ALPHA_* flags when
+// every wavelength row agrees (a scalar branch instead of a per-lane select); same values
+template <class T>
+ORT_INLINE void propagate_flagged(RayT<T>& r, const T& t, double alpha, int32_t flags) {
+  r.x = r.x + t * r.L;
+  r.y = r.y + t * r.M;
+  r.z = r.z + t * r.N;
+  if (flags & ORT_SURF_ALPHA_NONE) return;
+  if ((flags & ORT_SURF_ALPHA_ALL) || alpha > 0.0) r.att = r.att + -alpha * t * 1e3;
 }
 
 // surfaces/standard_surface.py:218

@@ -1,0 +1,328 @@
+// ort_fastpath.h -- the closed-form surface math (plane / conic, ray generation) with
+// DEFERRED range checks, for trace_closed_kernel (ort_kernels.h).
+//
+// ort_core.h's sqrt / shared_div / sdiv run the correctly rounded gfx950 sequences
+// without their range wrappers and fall back per operation (a divergent branch around
+// every op) when an operand leaves the range where the wrappers are identities. Here the
+// same instruction sequences run unconditionally and each operation only ORs "an operand
+// was outside that range" into a per-lane flag; a lane that ends its ray with the flag
+// set re-traces the whole ray on the per-operation path. Every value a lane keeps is
+// therefore bit-identical to ort_core.h's (and so to the reference's IEEE operations):
+// inside the ranges the fast sequences ARE the IEEE results, outside them the ray is
+// recomputed. What goes away is the exec-mask bookkeeping and the taken branch per op.
+//
+// Ranges (the same as ort_core.h):
+//   sqrt(x):   2^-767 <= x < inf
+//   a / b:     2^-300 <= |b| <= 2^300 and 2^-300 <= |a| <= 2^300, or a == +0: the
+//              quotient sequence q0 = a y, r = fma(-b, q0, a), q = fma(r, y, q0) then
+//              yields +0 * sign(b) exactly (q0 carries the sign, r = +0); -0 and every
+//              other value outside the range takes the exact path.
+//
+// Formulas and their order follow ort_core.h (and through it the reference files cited
+// there); only the check placement differs. Host compilation: plain IEEE operations.
+#pragma once
+
+#include "ort_core.h"
+
+namespace ort {
+namespace fast {
+
+// Lens constants: from the host table (ort_surface.two_r / one_plus_k / r_sq,
+// ort_surface_optics.u_sq) or recomputed per wave (ORT_NO_HOSTCONST; same values)
+#ifdef ORT_NO_HOSTCONST
+#define ORT_TWO_R(s) (2.0 * (s).radius)
+#define ORT_ONE_PLUS_K(s) (1.0 + (s).conic)
+#define ORT_R_SQ(s) ((s).radius * (s).radius)
+#define ORT_U_SQ(u, u_sq) ((u) * (u))
+#else
+#define ORT_TWO_R(s) ((s).two_r)
+#define ORT_ONE_PLUS_K(s) ((s).one_plus_k)
+#define ORT_R_SQ(s) ((s).r_sq)
+#define ORT_U_SQ(u, u_sq) (u_sq)
+#endif
+
+// ORT_FAST_NOCHECK (timing experiments only, never a shipped build): drop the range
+// checks to measure what they cost
+#ifdef ORT_FAST_NOCHECK
+#define ORT_CHK(bad, cond) ((void)0)
+#else
+#define ORT_CHK(bad, cond) ((bad) = (bad) | (cond))
+#endif
+
+ORT_INLINE bool in_div_range(double v) {
+  const double av = ::fabs(v);
+  return av >= 0x1p-300 && av <= 0x1p300;  // false for 0, inf, NaN
+}
+ORT_INLINE bool is_pos_zero(double v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_class(v, 1 << 6);  // v_cmp_class_f64: +0 only
+#else
+  return v == 0.0 && !signbit(v);
+#endif
+}
+
+// sqrt(x) for 2^-767 <= x < inf (ort_core.h sqrt)
+ORT_INLINE double sqrt(double x, bool& bad) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y;
+  double h = y * 0.5;
+  const double r = fma(-h, g, 0.5);
+  g = fma(g, r, g);
+  h = fma(h, r, h);
+  double d = fma(-g, g, x);
+  g = fma(d, h, g);
+  d = fma(-g, g, x);
+  g = fma(d, h, g);
+  ORT_CHK(bad, !(x >= 0x1p-767 && x < __builtin_inf()));
+  return g;
+#else
+  (void)bad;
+  return ::sqrt(x);
+#endif
+}
+
+// sqrt(x) where x >= 1 unless NaN (sums of squares plus 1): only the upper bound is live
+ORT_INLINE double sqrt_ge1(double x, bool& bad) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y;
+  double h = y * 0.5;
+  const double r = fma(-h, g, 0.5);
+  g = fma(g, r, g);
+  h = fma(h, r, h);
+  double d = fma(-g, g, x);
+  g = fma(d, h, g);
+  d = fma(-g, g, x);
+  g = fma(d, h, g);
+  ORT_CHK(bad, !(x < __builtin_inf()));
+  return g;
+#else
+  (void)bad;
+  return ::sqrt(x);
+#endif
+}
+
+ORT_INLINE SharedDiv shared_div(double b, bool& bad) {
+  SharedDiv d;
+  d.b = b;
+  d.ok = true;
+#if defined(__HIP_DEVICE_COMPILE__)
+  double y = __builtin_amdgcn_rcp(b);
+  double e = fma(-b, y, 1.0);
+  y = fma(y, e, y);
+  e = fma(-b, y, 1.0);
+  y = fma(y, e, y);
+  d.y = y;
+  ORT_CHK(bad, !in_div_range(b));
+#else
+  (void)bad;
+  d.y = 0.0;
+#endif
+  return d;
+}
+
+// the divisor is known to lie in [1, inf) unless NaN (a norm of (., ., 1))
+ORT_INLINE SharedDiv shared_div_ge1(double b, bool& bad) {
+  SharedDiv d;
+  d.b = b;
+  d.ok = true;
+#if defined(__HIP_DEVICE_COMPILE__)
+  double y = __builtin_amdgcn_rcp(b);
+  double e = fma(-b, y, 1.0);
+  y = fma(y, e, y);
+  e = fma(-b, y, 1.0);
+  y = fma(y, e, y);
+  d.y = y;
+  ORT_CHK(bad, !(b <= 0x1p300));
+#else
+  (void)bad;
+  d.y = 0.0;
+#endif
+  return d;
+}
+
+ORT_INLINE double quot(double a, const SharedDiv& d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const double q0 = a * d.y;
+  const double r = fma(-d.b, q0, a);
+  return fma(r, d.y, q0);
+#else
+  return a / d.b;
+#endif
+}
+
+// The same quotient for a divisor known to be > 0: -fma(-r, y, -q0) rounds q0 + r y
+// exactly as fma(r, y, q0) does (round-to-nearest is symmetric), but an exact-zero
+// numerator now keeps its sign (+-0 / b = +-0): fma(r, y, q0) turns -0 / b into +0
+// because r = +0 (an exact sum of opposite zeros), the negated form does not. (For
+// b < 0 the plain form is the one that is right for both zeros.)
+ORT_INLINE double quot_pos(double a, const SharedDiv& d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const double q0 = a * d.y;
+  const double r = fma(-d.b, q0, a);
+  return -fma(-r, d.y, -q0);
+#else
+  return a / d.b;
+#endif
+}
+
+// a / b, |a| in range
+ORT_INLINE double sdiv(double a, const SharedDiv& d, bool& bad) {
+  ORT_CHK(bad, !in_div_range(a));
+  return quot(a, d);
+}
+// a / b, |a| in range or a == +0 (coordinates on a symmetry plane)
+ORT_INLINE double sdiv0(double a, const SharedDiv& d, bool& bad) {
+  ORT_CHK(bad, !(in_div_range(a) || is_pos_zero(a)));
+  return quot(a, d);
+}
+
+// a / b as one IEEE division
+ORT_INLINE double div(double a, double b, bool& bad) {
+  const SharedDiv d = shared_div(b, bad);
+  return sdiv0(a, d, bad);
+}
+
+// rays/ray_generator.py:71-106 + fields/field_types.py:160-181 (ort_core.h generate_ray)
+ORT_INLINE Ray generate_ray(const ort_segment& s, double px, double py, bool& bad) {
+  Ray r;
+  double x0, y0;
+  if (s.mode == ORT_GEN_INFINITE) {
+    x0 = px * s.epd / 2.0 * s.vx + s.x_off;
+    y0 = py * s.epd / 2.0 * s.vy + s.y_off;
+  } else {
+    x0 = s.x_off;
+    y0 = s.y_off;
+  }
+  const double z0 = s.z0;
+  const double x1 = px * s.epd * s.vx / 2.0;
+  const double y1 = py * s.epd * s.vy / 2.0;
+  const double z1 = s.epl;
+  const double dx = x1 - x0, dy = y1 - y0, dz = z1 - z0;
+  const double mag = sqrt(dx * dx + dy * dy + dz * dz, bad);
+  ORT_CHK(bad, (mag < 1e-9));  // the (0, 0, 1) branch of ray_generator.py:82-89
+  const SharedDiv dm = shared_div(mag, bad);
+  // mag > 0: quot_pos is exact for zero numerators of either sign
+  ORT_CHK(bad, !((in_div_range(dx) || dx == 0.0) && (in_div_range(dy) || dy == 0.0) &&
+                 (in_div_range(dz) || dz == 0.0)));
+  r.L = quot_pos(dx, dm);
+  r.M = quot_pos(dy, dm);
+  r.N = quot_pos(dz, dm);
+  r.x = x0;
+  r.y = y0;
+  r.z = z0;
+  r.i = 1.0;
+  r.opd = 0.0;
+  r.att = 0.0;
+  return r;
+}
+
+// plane.py:61-77 (-z / N) and the plane branch of standard.py:100-103
+ORT_INLINE double distance_plane(const Ray& r, bool& bad) { return div(-r.z, r.N, bad); }
+
+// standard.py:89-140 (ort_core.h distance_conic); s.two_r = 2 R formed on the host
+ORT_INLINE double distance_conic(const Ray& r, const ort_surface& s, bool radius_inf,
+                                 bool& bad) {
+  if (radius_inf) {
+    const double Ns = ::fabs(r.N) > 1e-14 ? r.N : 1e-14;
+    return div(-r.z, Ns, bad);
+  }
+  const double R = s.radius, k = s.conic;
+  const double N2 = r.N * r.N;
+  const double z2 = r.z * r.z;
+  double a, b, c;
+  if (k == 0.0) {
+    a = r.L * r.L + r.M * r.M + N2;
+    b = 2.0 * (r.L * r.x + r.M * r.y - r.N * R + r.N * r.z);
+    c = 0.0 - ORT_TWO_R(s) * r.z + r.x * r.x + r.y * r.y + z2;
+  } else {
+    a = k * N2 + r.L * r.L + r.M * r.M + N2;
+    b = 2.0 * (k * r.N * r.z + r.L * r.x + r.M * r.y - r.N * R + r.N * r.z);
+    c = k * z2 - ORT_TWO_R(s) * r.z + r.x * r.x + r.y * r.y + z2;
+  }
+  const double d = b * b - 4.0 * a * c;
+  const double sd = sqrt(d, bad);
+  const SharedDiv a2 = shared_div(2.0 * a, bad);
+  // nonzero numerators (checked): quot_pos and quot agree for either sign of a
+  const double n1 = -b + sd, n2 = -b - sd;
+  ORT_CHK(bad, !(in_div_range(n1) && in_div_range(n2)));
+  const double t1 = quot_pos(n1, a2);
+  const double t2 = quot_pos(n2, a2);
+  const double z1 = r.z + t1 * r.N;
+  const double zz2 = r.z + t2 * r.N;
+  ORT_CHK(bad, (a == 0.0));  // the -c / b branch (standard.py:138)
+  return ::fabs(z1) <= ::fabs(zz2) ? t1 : t2;
+}
+
+// standard.py:154-167 with the host's inv_r2 = RN(1 / (R * R)) (ort_core.h
+// normal_conic_rcp: the Markstein-corrected quotient needs no range check of its own --
+// r^2 = 0 / inf / NaN give the reference's 1 - q)
+ORT_INLINE void normal_conic_rcp(double x, double y, const ort_surface& s, double& nx,
+                                 double& ny, double& nz, bool& bad) {
+  const double r2 = x * x + y * y;
+  const double a = ORT_ONE_PLUS_K(s) * r2;
+  const double q0 = a * s.inv_r2;
+  const double q = fma(fma(-ORT_R_SQ(s), q0, a), s.inv_r2, q0);
+  const double denom = s.radius * sqrt(1.0 - q, bad);
+  const SharedDiv dd = shared_div(denom, bad);
+  const double dfdx = sdiv0(x, dd, bad);
+  const double dfdy = sdiv0(y, dd, bad);
+  const double mag = sqrt_ge1(dfdx * dfdx + dfdy * dfdy + 1.0, bad);
+  const SharedDiv dm = shared_div_ge1(mag, bad);
+  // dfdx = x / denom with x checked (|x| in [2^-300, 2^300] or +0) and |denom| <= 2^300:
+  // |dfdx| >= 2^-600 or +-0, and |dfdx| <= mag -- in range for the positive divisor
+  // mag, zeros of either sign included (quot_pos): no check left to make
+  nx = quot_pos(dfdx, dm);
+  ny = quot_pos(dfdy, dm);
+  nz = quot(-1.0, dm);  // constant numerator: always in range
+}
+
+// rays/real_rays.py:511-547 (ort_core.h align_normal) for dot != 0: sign(dot) is +-1 and
+// n * sign(dot) is n with its sign bit flipped when dot < 0 -- the same bits as the
+// product; dot == 0 (sign 0) and NaN take the exact path
+ORT_INLINE double align_normal(const Ray& r, double& nx, double& ny, double& nz, bool& bad) {
+#ifdef ORT_NO_SIGN_XOR
+  return ::ort::align_normal(r, nx, ny, nz);
+#endif
+  const double dot = r.L * nx + r.M * ny + r.N * nz;
+  ORT_CHK(bad, !(::fabs(dot) > 0.0));
+  const uint64_t sb = (uint64_t)__double_as_longlong(dot) & 0x8000000000000000ull;
+  nx = __longlong_as_double((long long)((uint64_t)__double_as_longlong(nx) ^ sb));
+  ny = __longlong_as_double((long long)((uint64_t)__double_as_longlong(ny) ^ sb));
+  nz = __longlong_as_double((long long)((uint64_t)__double_as_longlong(nz) ^ sb));
+  return ::fabs(dot);
+}
+
+// rays/real_rays.py:141-163 (ort_core.h refract); u_sq = RN(u * u) from the host table
+ORT_INLINE void refract(Ray& r, double nx, double ny, double nz, double u, double u_sq,
+                        bool& bad) {
+  const double dot = align_normal(r, nx, ny, nz, bad);
+  const double root = sqrt(1.0 - ORT_U_SQ(u, u_sq) * (1.0 - dot * dot), bad);
+  const double L0 = r.L, M0 = r.M, N0 = r.N;
+  r.L = u * L0 + nx * root - u * nx * dot;
+  r.M = u * M0 + ny * root - u * ny * dot;
+  r.N = u * N0 + nz * root - u * nz * dot;
+}
+
+// Refraction at a flat surface: the plane normal (0, 0, 1) (plane.py:79-98) or the
+// infinite-radius conic's (+-0, +-0, -1) (standard.py:154-167). For finite L, M and
+// N != 0 the reference's expressions reduce exactly:
+//   dot = L*0 + M*0 + N*1 = N, sign(dot) = sign(N), |dot| = |N|;
+//   L' = u L + (+-0) root - u (+-0) |N| = u L + 0.0 (the zero terms only turn a -0
+//   product into +0, as adding +0 does), M' likewise;
+//   N' = (u N + sign(N) root) - (u sign(N)) |N| = (u N + sign(N) root) - u N.
+// N == 0 / NaN takes the exact path; a non-finite L or M only reaches here on a ray that
+// already failed a check (or came in non-finite, which closed_ray_in flags).
+ORT_INLINE void refract_flat(Ray& r, double u, double u_sq, bool& bad) {
+  ORT_CHK(bad, !(::fabs(r.N) > 0.0));
+  const double root = sqrt(1.0 - ORT_U_SQ(u, u_sq) * (1.0 - r.N * r.N), bad);
+  const double uN = u * r.N;
+  const double sroot = ::copysign(root, r.N);
+  r.L = u * r.L + 0.0;
+  r.M = u * r.M + 0.0;
+  r.N = (uN + sroot) - uN;
+}
+
+}  // namespace fast
+}  // namespace ort

@@ -44,10 +44,15 @@ void launch_material_nk(const ort_material* mats, const double* coef, int32_t ma
 }
 
 KernelFn select_closed(uint32_t feat) {
-  switch (feat & (F_GEN | F_REC | F_MONO | F_WRAY)) {
+#ifdef ORT_NO_AXIAL  // A/B timing only
+  feat &= ~F_AXIAL;
+#endif
+  switch (feat & (F_GEN | F_REC | F_MONO | F_WRAY | F_AXIAL)) {
 #define ORT_C(F) \
   case (F):      \
-    return trace_closed_kernel<(F)>;
+    return trace_closed_kernel<(F)>;        \
+  case (F) | F_AXIAL:                       \
+    return trace_closed_kernel<(F) | F_AXIAL>;
     ORT_C(0) ORT_C(F_GEN) ORT_C(F_REC) ORT_C(F_GEN | F_REC)
     ORT_C(F_MONO) ORT_C(F_MONO | F_GEN) ORT_C(F_MONO | F_REC) ORT_C(F_MONO | F_GEN | F_REC)
     ORT_C(F_WRAY) ORT_C(F_WRAY | F_REC)

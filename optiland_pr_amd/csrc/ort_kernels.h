@@ -26,6 +26,7 @@
 #include <stdlib.h>
 
 #include "ort_core.h"
+#include "ort_fastpath.h"
 #include "ort_interact.h"
 #include "ort_material.h"
 
@@ -60,6 +61,7 @@ enum : uint32_t {
   F_MONO = 1u << 6,  // one wavelength in the lens tables (closed-form kernels only)
   F_WRAY = 1u << 7,  // per-ray wavelengths: n, k from lens.materials (ort_batch.w)
   F_IA = 1u << 8,    // thin-lens / phase / grating interactions (ort_interaction)
+  F_AXIAL = 1u << 9, // ORT_LENS_AXIAL: every frame a +z translation (closed-form kernels)
 };
 
 struct KArgs {
@@ -92,6 +94,7 @@ struct KArgs {
   int32_t newton_mode;
   int32_t start_surface;
   const int32_t* sched;
+  int32_t conv_base;  // first stop index of the ort_newton_stat.conv_mask window
   // outputs
   double* rec;
   ort_newton_stat* stats;
@@ -153,6 +156,7 @@ __device__ inline ort_surface_optics optics_ray(const KArgs& a, const ort_surfac
   o.n_pre = ort::material_n(mp, a.coef, w);
   o.n_post = ort::material_n(mq, a.coef, w);
   o.u = o.n_pre / o.n_post;
+  o.u_sq = o.u * o.u;
   o.alpha_pre = ort::absorption_alpha(ort::material_k(mp, a.coef, w), w);
   return o;
 }
@@ -179,8 +183,10 @@ __device__ inline double final_alpha(const KArgs& a, int lam, double w) {
 // shuffling around one)
 template <class T>
 __device__ inline void localize(const KArgs& a, const ort_surface& s, ort::RayT<T>& r) {
-  r.x = r.x + -s.cs_t[0];
-  r.y = r.y + -s.cs_t[1];
+  {
+    r.x = r.x + -s.cs_t[0];
+    r.y = r.y + -s.cs_t[1];
+  }
   r.z = r.z + -s.cs_t[2];
   for (int c = 0; c < s.n_cs_loc; ++c) ort::apply_cs_op(r, cst(a.cs)[s.cs_loc_off + c]);
 }
@@ -193,6 +199,10 @@ __device__ inline void globalize(const KArgs& a, const ort_surface& s, ort::RayT
   r.z = r.z + s.cs_t[2];
 }
 
+// geometry ids this library implements (enum ort_geometry); the kernels turn any other
+// id into NaN rays plus ORT_STATUS_BAD_GEOMETRY
+__device__ inline bool known_geometry(int g) { return g >= ORT_GEOM_PLANE && g <= ORT_GEOM_GRID_SAG; }
+
 // status bit of a normalisation-range error at surface s (zernike.py:234-246,
 // chebyshev.py:203-215: both raise ValueError in the reference)
 __device__ inline int range_bit(const ort_surface& s) {
@@ -200,27 +210,38 @@ __device__ inline int range_bit(const ort_surface& s) {
                                           : (int)ORT_STATUS_ZERNIKE_RANGE;
 }
 
+// Per-lane "the stop test passed at stop index k" bits over the 128-index window
+// [conv_base, conv_base + 128) of ort_newton_stat.conv_mask
+struct ConvBits {
+  uint64_t w0 = 0, w1 = 0;
+  __device__ inline void set(int k, int base) {
+    const int b = k - base;
+    if (b >= 0 && b < 64) w0 |= 1ull << b;
+    else if (b >= 64 && b < 128) w1 |= 1ull << (b - 64);
+  }
+};
+
 // Newton statistics of one (group, surface): AND of the per-update convergence bits and
 // the max non-converged index (see ort_newton_stat), read-before-atomic
 __device__ inline void report_newton(const KArgs& a, int si, bool active, int64_t group,
-                                     bool group_uniform, uint64_t mask, int last_bad) {
+                                     bool group_uniform, ConvBits m, int last_bad) {
   if (!a.stats) return;
   if (!active) {
-    mask = ~0ull;
+    m.w0 = m.w1 = ~0ull;
     last_bad = -1;
   }
   ort_newton_stat* st = &a.stats[group * a.n_surf + si];
   if (group_uniform) {
-    mask = wave_and_u64(mask);
+    m.w0 = wave_and_u64(m.w0);
+    m.w1 = wave_and_u64(m.w1);
     last_bad = wave_max_i32(last_bad);
-    if ((threadIdx.x & 63) == 0) {
-      if (mask != ~0ull) and_if_changes(&st->conv_mask, mask);
-      if (last_bad >= 0) max_if_changes(&st->last_bad, last_bad);
-    }
-  } else if (active) {
-    if (mask != ~0ull) and_if_changes(&st->conv_mask, mask);
-    if (last_bad >= 0) max_if_changes(&st->last_bad, last_bad);
+    if ((threadIdx.x & 63) != 0) return;
+  } else if (!active) {
+    return;
   }
+  if (m.w0 != ~0ull) and_if_changes(&st->conv_mask[0], m.w0);
+  if (m.w1 != ~0ull) and_if_changes(&st->conv_mask[1], m.w1);
+  if (last_bad >= 0) max_if_changes(&st->last_bad, last_bad);
 }
 
 // Grid-sag intersection (grid_sag.py:108-140): Newton from t = 0, the reference stops
@@ -248,7 +269,7 @@ __device__ inline double grid_distance(const KArgs& a, const ort_surface& s, int
     return ort::grid_final(g, r, t);
   }
   const int U = a.sched ? a.sched[group * a.n_surf + si] : max_iter;
-  uint64_t mask = 0;
+  ConvBits mask;
   int last_bad = -1;
   for (int j = 0;; ++j) {
     const bool lane_on = active && j < U;
@@ -257,7 +278,7 @@ __device__ inline double grid_distance(const KArgs& a, const ort_surface& s, int
       const double dt = ort::grid_step(g, r, t);
       t = t + dt;
       const bool conv = fabs(dt) < tol;  // NaN never converges
-      if (conv && j + 1 < 64) mask |= 1ull << (j + 1);
+      if (conv) mask.set(j + 1, a.conv_base);  // stop index j + 1: the test after update j
       if (!conv) last_bad = j + 1;
     }
   }
@@ -297,7 +318,7 @@ __device__ inline double newton_distance(const KArgs& a, const ort_surface& s, i
   }
   // ORT_NEWTON_SCHEDULE: exactly U updates, plus the check evaluation at j = U.
   const int U = a.sched ? a.sched[group * a.n_surf + si] : max_iter;
-  uint64_t mask = 0;
+  ConvBits mask;
   int last_bad = -1;
   for (int j = 0;; ++j) {
     const bool lane_on = active && j <= U;
@@ -312,29 +333,12 @@ __device__ inline double newton_distance(const KArgs& a, const ort_surface& s, i
       // loop broke there (U < max_iter)
       if (rerr && (j < U || U < max_iter)) range_bits |= range_bit(s);
       const bool conv = fabs(f) < tol;  // NaN never converges (np.max propagates NaN)
-      if (conv && j < 64) mask |= 1ull << j;
+      if (conv) mask.set(j, a.conv_base);
       if (!conv) last_bad = j;
       if (upd) t = ort::newton_step(r, t, f, nx, ny, nz);
     }
   }
-  if (a.stats) {
-    if (!active) {
-      mask = ~0ull;
-      last_bad = -1;
-    }
-    ort_newton_stat* st = &a.stats[group * a.n_surf + si];
-    if (group_uniform) {
-      mask = wave_and_u64(mask);
-      last_bad = wave_max_i32(last_bad);
-      if ((threadIdx.x & 63) == 0) {
-        if (mask != ~0ull) and_if_changes(&st->conv_mask, mask);
-        if (last_bad >= 0) max_if_changes(&st->last_bad, last_bad);
-      }
-    } else if (active) {
-      if (mask != ~0ull) and_if_changes(&st->conv_mask, mask);
-      if (last_bad >= 0) max_if_changes(&st->last_bad, last_bad);
-    }
-  }
+  report_newton(a, si, active, group, group_uniform, mask, last_bad);
   return t;
 }
 
@@ -414,6 +418,7 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(const KArgs a) {
     const ort_surface_optics o = surface_optics<FEAT>(a, s, lam, si, wl);
     localize(a, s, r);
     double t;
+    if (!known_geometry(s.geometry)) range_bits |= ORT_STATUS_BAD_GEOMETRY;
     if (s.geometry == ORT_GEOM_PLANE) {
       t = ort::distance_plane(r);
     } else if (s.geometry == ORT_GEOM_STANDARD) {
@@ -484,9 +489,7 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(const KArgs a) {
     }
   }
 
-  if constexpr ((FEAT & (ort::KM_ZERN | ort::KM_FREE)) != 0) {
-    if (range_bits && active && a.status) atomicOr(a.status, range_bits);
-  }
+  if (range_bits && active && a.status) atomicOr(a.status, range_bits);
   if (!active) return;
   a.out.x[rid] = r.x;
   a.out.y[rid] = r.y;
@@ -499,24 +502,29 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(const KArgs a) {
 }
 
 // Closed-form lenses (planes, spheres, conics: no Newton surface) -- the DoubleGauss /
-// Cooke / ReverseTelephoto path. One ray per lane: at 52 VGPRs the kernel runs 8 waves
+// Cooke / ReverseTelephoto path. One ray per lane: at <= 64 VGPRs the kernel runs 8 waves
 // per SIMD, which hides the fp64 div/sqrt latency better than 2 or 4 rays per lane
 // (measured: 2 rays/lane 7% slower at 5 waves/SIMD, 4 rays/lane 28% slower).
 // Per surface: one batch of scalar loads (surface record + optics of this wavelength).
-template <uint32_t FEAT>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) void trace_closed_kernel(const KArgs a) {
-  const int64_t rid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  const bool active = rid < a.n_rays;
-  const int64_t r_ld = active ? rid : 0;
-  int lam = 0;
-  double wl = 0.0;  // F_WRAY: this ray's wavelength
+//
+// FAST = true: the surface math of ort_fastpath.h (range checks deferred into `bad`);
+// FAST = false: ort_core.h's per-operation exact path. The kernel runs the fast trace and
+// re-traces on the exact path only the lanes whose `bad` is set (operands outside the
+// ranges where the short sequences are the IEEE results: NaN / missed rays, zeros, ...),
+// so every output is the exact path's.
+template <uint32_t FEAT, bool FAST>
+__device__ inline ort::Ray closed_ray_in(const KArgs& a, int64_t r_ld, int& lam, double& wl,
+                                         bool& bad) {
   ort::Ray r;
   if constexpr ((FEAT & F_GEN) != 0) {
     const int64_t sidx = a.n_seg == 1 ? 0 : r_ld / a.seg_len;
     const ort_segment sg = a.n_seg == 1 ? cst(a.seg)[0] : a.seg[sidx];
     lam = sg.lambda_idx;
     const int64_t p = a.pupil_per_ray ? r_ld : (r_ld - sidx * a.seg_len);
-    r = ort::generate_ray(sg, a.px[p], a.py[p]);
+    if constexpr (FAST)
+      r = ort::fast::generate_ray(sg, a.px[p], a.py[p], bad);
+    else
+      r = ort::generate_ray(sg, a.px[p], a.py[p]);
   } else {
     if (a.seg) lam = a.seg[a.n_seg == 1 ? 0 : r_ld / a.seg_len].lambda_idx;
     if constexpr ((FEAT & F_WRAY) != 0) wl = a.w[r_ld];
@@ -529,34 +537,84 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
     r.i = a.in.i[r_ld];
     r.opd = a.in.opd[r_ld];
     r.att = 0.0;
+    // the fast flat-surface refraction assumes finite directions (ort_fastpath.h)
+    if constexpr (FAST) bad = bad | !(::fabs(r.L) < __builtin_inf() && ::fabs(r.M) < __builtin_inf());
   }
+  return r;
+}
+
+template <uint32_t FEAT, bool FAST>
+__device__ inline void closed_surfaces(const KArgs& a, ort::Ray& r, int lam, double wl,
+                                       int64_t rid, bool active, bool& bad, bool& geom_bad) {
   for (int si = a.start_surface; si < a.n_surf; ++si) {
     const ort_surface s = cst(a.surf)[si];
     const ort_surface_optics o = surface_optics<FEAT>(a, s, lam, si, wl);
-    localize(a, s, r);
+    if constexpr ((FEAT & F_AXIAL) != 0)
+      r.z = r.z + -s.cs_t[2];  // x + -0 and y + -0 are identities
+    else
+      localize(a, s, r);
     const bool is_plane = s.geometry == ORT_GEOM_PLANE;
-    const double t = is_plane ? ort::distance_plane(r)
-                              : ort::distance_conic(r, s.radius, s.conic,
-                                                    (s.flags & ORT_SURF_RADIUS_INF) != 0);
+    const bool radius_inf = (s.flags & ORT_SURF_RADIUS_INF) != 0;
+    double t;
+    if constexpr (FAST) {
+      t = is_plane ? ort::fast::distance_plane(r, bad)
+                   : ort::fast::distance_conic(r, s, radius_inf, bad);
+    } else {
+      t = is_plane ? ort::distance_plane(r) : ort::distance_conic(r, s.radius, s.conic, radius_inf);
+    }
+    if (!is_plane && s.geometry != ORT_GEOM_STANDARD) {  // not a closed-form id: NaN rays
+      t = __builtin_nan("");
+      geom_bad = true;
+    }
+#ifndef ORT_NO_ALPHA_FLAGS
+    if constexpr ((FEAT & F_WRAY) != 0)
+      ort::propagate(r, t, o.alpha_pre);
+    else
+      ort::propagate_flagged(r, t, o.alpha_pre, s.flags);
+#else
     ort::propagate(r, t, o.alpha_pre);
+#endif
     ort::add_opd(r, t, o.n_pre);
     if (s.flags & ORT_SURF_APERTURE) ort::clip_radial(r, s.ap_rmax2, s.ap_rmin2);
 #ifndef ORT_NO_AP_PROG
     if (s.flags & ORT_SURF_APERTURE_PROG) ort::clip_program(r, cst(a.coef) + s.ap_off, s.ap_len);
 #endif
-    double nx, ny, nz;
-    if (is_plane) {
-      nx = 0.0; ny = 0.0; nz = 1.0;
-    } else if (s.flags & ORT_SURF_INV_R2) {
-      ort::normal_conic_rcp(r.x, r.y, s.radius, s.conic, s.inv_r2, nx, ny, nz);
+    const bool refl = (s.flags & ORT_SURF_REFLECTIVE) != 0;
+#ifndef ORT_NO_FLAT_FAST
+    constexpr bool kFlat = FAST;
+#else
+    constexpr bool kFlat = false;
+#endif
+    if (kFlat && !refl && (is_plane || radius_inf)) {
+      ort::fast::refract_flat(r, o.u, o.u_sq, bad);  // normal (0, 0, +-1): reduced exactly
     } else {
-      ort::normal_conic(r.x, r.y, s.radius, s.conic, nx, ny, nz);
+      double nx, ny, nz;
+      if (is_plane) {
+        nx = 0.0; ny = 0.0; nz = 1.0;
+      } else if (s.flags & ORT_SURF_INV_R2) {
+        if constexpr (FAST)
+          ort::fast::normal_conic_rcp(r.x, r.y, s, nx, ny, nz, bad);
+        else
+          ort::normal_conic_rcp(r.x, r.y, s.radius, s.conic, s.inv_r2, nx, ny, nz);
+      } else {
+        ort::normal_conic(r.x, r.y, s.radius, s.conic, nx, ny, nz);
+      }
+      if (refl) {
+        ort::reflect(r, nx, ny, nz);
+      } else {
+        if constexpr (FAST)
+          ort::fast::refract(r, nx, ny, nz, o.u, o.u_sq, bad);
+        else
+          ort::refract(r, nx, ny, nz, o.u);
+      }
     }
-    if (s.flags & ORT_SURF_REFLECTIVE)
-      ort::reflect(r, nx, ny, nz);
-    else
-      ort::refract(r, nx, ny, nz, o.u);
-    globalize(a, s, r);
+    if constexpr ((FEAT & F_AXIAL) != 0) {
+      r.x = r.x + 0.0;  // the reference's translate by +cs_t (= +0): -0 becomes +0
+      r.y = r.y + 0.0;
+      r.z = r.z + s.cs_t[2];
+    } else {
+      globalize(a, s, r);
+    }
     if constexpr ((FEAT & F_REC) != 0) {
       if ((s.flags & ORT_SURF_RECORD) && active) {
         double* b = a.rec + (int64_t)s.rec_slot * 8 * a.n_rays + rid;
@@ -571,7 +629,29 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
       }
     }
   }
+}
+
+template <uint32_t FEAT>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) void trace_closed_kernel(const KArgs a) {
+  const int64_t rid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const bool active = rid < a.n_rays;
+  const int64_t r_ld = active ? rid : 0;
+  int lam = 0;
+  double wl = 0.0;  // F_WRAY: this ray's wavelength
+  bool bad = false, geom_bad = false;
+#ifndef ORT_NO_DEFERRED_CHECKS
+  ort::Ray r = closed_ray_in<FEAT, true>(a, r_ld, lam, wl, bad);
+  closed_surfaces<FEAT, true>(a, r, lam, wl, rid, active, bad, geom_bad);
+  if (__builtin_expect(bad, 0)) {  // this lane left the fast path's ranges: exact re-trace
+    r = closed_ray_in<FEAT, false>(a, r_ld, lam, wl, bad);
+    closed_surfaces<FEAT, false>(a, r, lam, wl, rid, active, bad, geom_bad);
+  }
+#else
+  ort::Ray r = closed_ray_in<FEAT, false>(a, r_ld, lam, wl, bad);
+  closed_surfaces<FEAT, false>(a, r, lam, wl, rid, active, bad, geom_bad);
+#endif
   if (a.final_mat >= 0) ort::propagate(r, a.final_thickness, final_alpha<FEAT>(a, lam, wl));
+  if (geom_bad && a.status && threadIdx.x == 0) atomicOr(a.status, (int)ORT_STATUS_BAD_GEOMETRY);
   if (!active) return;
   a.out.x[rid] = r.x;
   a.out.y[rid] = r.y;

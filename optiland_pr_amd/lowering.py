@@ -69,7 +69,18 @@ class LensTable:
         o["u"] = self.u_tab
         o["alpha_pre"] = self.alpha_tab[:, self.surfaces["mat_pre"]]
         o["n_post"] = self.n_tab[:, self.surfaces["mat_post"]]
+        o["u_sq"] = o["u"] * o["u"]
         return o
+
+    @property
+    def frame_flags(self):
+        """ort_lens.frame_flags: ORT_LENS_AXIAL when every surface frame is a +z
+        translation (no rotation / reference-cs ops, cs_t[0] = cs_t[1] = +0)."""
+        s = self.surfaces
+        t = s["cs_t"][:, :2]
+        axial = (np.all(s["n_cs_loc"] == 0) and np.all(s["n_cs_glob"] == 0)
+                 and np.all(t == 0.0) and not np.any(np.signbit(t)))
+        return _abi.LENS_AXIAL if axial else 0
 
     @property
     def interaction_mask(self):
@@ -149,6 +160,11 @@ def lower_surface_group(surface_group, wavelengths, record=False, skip_object=Tr
         row["tol"] = tol
         row["max_iter"] = max_iter
         row["norm_radius"] = norm_radius
+        # lens-constant subexpressions of the conic formulas (the same IEEE operations the
+        # kernels would repeat per ray): 2 R, 1 + k, R * R
+        row["two_r"] = np.float64(2.0) * np.float64(R)
+        row["one_plus_k"] = np.float64(1.0) + np.float64(k)
+        row["r_sq"] = np.float64(R) * np.float64(R)
         flags = 0
         if s.is_reflective:
             flags |= _abi.SURF_REFLECTIVE
@@ -264,6 +280,12 @@ def lower_surface_group(surface_group, wavelengths, record=False, skip_object=Tr
             kv = m.k_scalar(w)
             # homogeneous.py:49-54: applied only when k > 0; alpha = 4*pi*k/w
             alpha_tab[j, mi] = (4 * np.pi * np.float64(kv) / np.float64(w)) if kv > 0 else 0.0
+    for row in table:  # absorption decided per surface when every wavelength row agrees
+        a = alpha_tab[:, int(row["mat_pre"])]
+        if np.all(a > 0):
+            row["flags"] = int(row["flags"]) | _abi.SURF_ALPHA_ALL
+        elif np.all(a == 0):
+            row["flags"] = int(row["flags"]) | _abi.SURF_ALPHA_NONE
     return LensTable(
         surfaces=table,
         cs_ops=cs,

@@ -144,7 +144,7 @@ class DeviceLens:
             self.optics.data_ptr(),
             table.n_surfaces, len(table.wavelengths), table.n_tab.shape[1], table.final_mat,
             mask, table.interaction_mask, table.final_thickness, self.mats.data_ptr(),
-            self.lambdas.data_ptr())
+            self.lambdas.data_ptr(), table.frame_flags)
         self.newton = table.newton_surfaces
         self.sched_cache: dict = {}
 
@@ -171,28 +171,68 @@ class DeviceLens:
             else:
                 for s in self.newton:
                     sched[g, s] = min(3, int(self.table.surfaces[s]["max_iter"]))
+        # a schedule cached for another lens (lens_for keeps it across edits) must still
+        # be a legal update count for this surface: 1 .. max_iter for a grid sag
+        for s in self.newton:
+            surf = self.table.surfaces[s]
+            lo = 1 if int(surf["geometry"]) == _abi.GEOM_GRID_SAG else 0
+            sched[:, s] = np.clip(sched[:, s], lo, max(lo, int(surf["max_iter"])))
         return sched
 
-    def verify(self, sched, stats):
-        """-> (ok, new_sched). stats: NEWTON_STAT [n_groups][S]."""
+    def verify(self, sched, windows):
+        """-> (ok, new_sched, need_base). windows: {conv_base: NEWTON_STAT [n_groups][S]}
+        from launches of this same schedule. The reference stops at the first stop index
+        k (updates made, >= 1 for a grid sag) whose global test passes, else after
+        max_iter updates; sched[g][s] == U is right when no k < U passed and either
+        U == max_iter or every ray passed at U. need_base: another conv_mask window is
+        needed to decide (schedules beyond 128 updates), launch with that conv_base."""
         ok = True
         new = sched.copy()
+        W = _abi.CONV_WINDOW
+        base0 = windows[min(windows)]
         for g in range(sched.shape[0]):
             for s in self.newton:
                 U = int(sched[g, s])
-                max_iter = int(self.table.surfaces[s]["max_iter"])
-                mask = int(stats[g, s]["conv_mask"])
-                last_bad = int(stats[g, s]["last_bad"])
-                below = mask & ((1 << min(U, 64)) - 1)
-                if below:  # every ray had |f| < tol before update U: the reference stops there
-                    new[g, s] = (below & -below).bit_length() - 1
+                surf = self.table.surfaces[s]
+                max_iter = int(surf["max_iter"])
+                k_min = 1 if int(surf["geometry"]) == _abi.GEOM_GRID_SAG else 0
+                if U < k_min:  # grid_sag.py:111-129 always makes the first update
+                    new[g, s] = k_min
                     ok = False
                     break
-                if U < max_iter and last_bad >= U:  # not all converged at U: it goes on
+                last_bad = int(base0[g, s]["last_bad"])
+                k, need = self._first_passed(windows, g, s, k_min, U, W)
+                if need is not None:
+                    return False, sched, need
+                if k is not None:  # every ray passed before update U: the reference stops there
+                    new[g, s] = k
+                    ok = False
+                    break
+                if U < max_iter and last_bad >= U:  # not all passed at U: it goes on
                     new[g, s] = max_iter if U >= 8 else min(max_iter, max(2 * U + 2, 8))
                     ok = False
                     break
-        return ok, new
+        return ok, new, None
+
+    @staticmethod
+    def _first_passed(windows, g, s, k_lo, k_hi, W):
+        """Smallest stop index k in [k_lo, k_hi) whose test passed for every ray, from
+        the conv_mask windows -> (k or None, None), or (None, base) when an index below
+        the answer is not covered by any window yet."""
+        k = k_lo
+        while k < k_hi:
+            base = (k // W) * W
+            st = windows.get(base)
+            if st is None:
+                return None, base
+            m = int(st[g, s]["conv_mask"][0]) | (int(st[g, s]["conv_mask"][1]) << 64)
+            m >>= k - base  # bits for k .. base + W - 1
+            top = min(k_hi, base + W) - k
+            m &= (1 << top) - 1
+            if m:
+                return k + ((m & -m).bit_length() - 1), None
+            k = base + W
+        return None, None
 
     def remember(self, keys, sched):
         for g, k in enumerate(keys):
@@ -266,10 +306,15 @@ def _run(dlens: DeviceLens, launch, n_rays, group_len, keys, newton_mode="refere
     stats = torch.empty(n_groups * S * _abi.NEWTON_STAT.itemsize, dtype=torch.uint8, device=dev)
     for _ in range(64):
         sched_dev = torch.from_numpy(sched.reshape(-1).copy()).to(dev)
-        opt = _native.ort_options(_abi.NEWTON_SCHEDULE, 0, sched_dev.data_ptr())
-        launch(opt, stats, status)
-        st = stats.cpu().numpy().view(_abi.NEWTON_STAT).reshape(n_groups, S)
-        ok, new = dlens.verify(sched, st)
+        windows = {}
+        base = 0
+        while True:  # conv_mask windows of this schedule until verify can decide
+            opt = _native.ort_options(_abi.NEWTON_SCHEDULE, 0, sched_dev.data_ptr(), base)
+            launch(opt, stats, status)
+            windows[base] = stats.cpu().numpy().view(_abi.NEWTON_STAT).reshape(n_groups, S)
+            ok, new, base = dlens.verify(sched, windows)
+            if base is None:
+                break
         if ok:
             dlens.remember(keys, sched)
             dlens.last_schedule = sched
@@ -283,6 +328,9 @@ def _raise_status(status):
     if status is None:
         return
     v = int(status.item())
+    if v & _abi.STATUS_BAD_GEOMETRY:
+        raise ValueError("the lens table holds a geometry id the trace core does not know "
+                         "(library / host ABI mismatch?)")
     if v & _abi.STATUS_ZERNIKE_RANGE:
         raise ZernikeRangeError(_ZERNIKE_MSG)
     if v & _abi.STATUS_CHEBYSHEV_RANGE:

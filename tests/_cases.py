@@ -44,7 +44,7 @@ CLOSED_FORM = ("cooke", "dg", "rt", "cooke_aperture", "cooke_shapes", "decentere
                "paraxial_mirror", "grating_flat", "grating_curved", "grating_reflective",
                "grating_tilted")
 NEWTON = ("rt_asph", "rt_odd", "tma_fringe", "tma_standard", "tma_noll", "freeform",
-          "forbes", "forbes_q2d", "phase_plate")  # grid_lens: golden not generated yet (gen_golden.py --only grid_lens)
+          "forbes", "forbes_q2d", "phase_plate", "grid_lens")
 ALL_CASES = CLOSED_FORM + NEWTON
 
 FIELDS = _abi.RAY_FIELDS

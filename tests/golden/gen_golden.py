@@ -40,6 +40,7 @@ import optiland.backend as be  # noqa: E402
 from optiland import optic as ref_optic  # noqa: E402
 from optiland.analysis import SpotDiagram  # noqa: E402
 from optiland.distribution import RandomDistribution, create_distribution  # noqa: E402
+from optiland.geometries.grid_sag import GridSagGeometry  # noqa: E402
 from optiland.geometries.newton_raphson import NewtonRaphsonGeometry  # noqa: E402
 from optiland.materials.ideal import IdealMaterial  # noqa: E402
 from optiland.materials.material import Material  # noqa: E402
@@ -483,9 +484,36 @@ CASES = {
 _newton_counts: dict[int, int] = {}
 
 
+def _instrument_grid(si, g):
+    """GridSagGeometry.distance (grid_sag.py:108-140) calls _interpolate once per update:
+    the number of those calls inside one distance() is its update count."""
+    orig_distance = g.distance
+    orig_interp = g._interpolate
+
+    def distance(rays, _g=g, _si=si, _od=orig_distance, _oi=orig_interp):
+        count = [0]
+
+        def counting_interp(x, y):
+            count[0] += 1
+            return _oi(x, y)
+
+        _g._interpolate = counting_interp
+        try:
+            t = _od(rays)
+        finally:
+            _g._interpolate = _oi
+        _newton_counts[_si] = count[0]
+        return t
+
+    g.distance = distance
+
+
 def _instrument_newton(lens):
     for si, s in enumerate(lens.surface_group.surfaces):
         g = s.geometry
+        if isinstance(g, GridSagGeometry):
+            _instrument_grid(si, g)
+            continue
         if not isinstance(g, NewtonRaphsonGeometry):
             continue
         orig_distance = g.distance
@@ -523,6 +551,15 @@ def material_table(lens, wavelengths):
             n[j, si] = float(np.ravel(m.n(np.array([w])))[0])
             k[j, si] = float(np.ravel(m.k(np.array([w])))[0])
     return n, k
+
+
+def _paraxial_or_nan(fn):
+    """A paraxial scalar for the metadata, or NaN where the reference's paraxial tracer
+    cannot run (a grid sag surface has no radius: surface_group.py:153)."""
+    try:
+        return float(fn())
+    except AttributeError:
+        return float("nan")
 
 
 def generate_case(name, builder, fields, wavelengths, dist, num):
@@ -584,8 +621,8 @@ def generate_case(name, builder, fields, wavelengths, dist, num):
         num_surfaces=S,
         EPL=float(lens.paraxial.EPL()),
         EPD=float(lens.paraxial.EPD()),
-        f2=float(lens.paraxial.f2()),
-        XPL=float(lens.paraxial.XPL()),
+        f2=_paraxial_or_nan(lens.paraxial.f2),
+        XPL=_paraxial_or_nan(lens.paraxial.XPL),
         primary_wavelength=float(lens.primary_wavelength),
         norm_radius=[float(getattr(s.geometry, "norm_radius", np.nan)) for s in sg.surfaces],
         semi_aperture=[None if s.semi_aperture is None else float(np.ravel(s.semi_aperture)[0])

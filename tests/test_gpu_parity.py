@@ -100,7 +100,8 @@ def test_trace_resident_rays_vs_reference(torch, name, golden_index):
     assert _abi.RAY_FIELDS
 
 
-@pytest.mark.parametrize("name", ["rt_asph", "rt_odd", "tma_fringe", "tma_standard"])
+@pytest.mark.parametrize("name", ["rt_asph", "rt_odd", "tma_fringe", "tma_standard",
+                                  "grid_lens"])
 def test_newton_schedule_matches_reference_global_rule(torch, name, golden_index):
     dl, g, _, _, keys = gpu_trace_case(torch, name, golden_index[name])
     ref = g["newton_updates"]
@@ -261,3 +262,82 @@ def test_doublegauss_1m_full_size_properties(torch, golden_index):
     assert float(np.sum(x * x)) == ref["sum_x2"]
     assert [float(x[0]), float(y[0]), float(opd[0])] == ref["first"]
     assert [float(x[-1]), float(y[-1]), float(opd[-1])] == ref["last"]
+
+
+def test_unknown_geometry_id_fails_loudly(torch):
+    """A geometry id outside enum ort_geometry is never traced as another kind: refused
+    at the boundary when the lens's geometry_mask names it (ORT_ERR_ARG), NaN rays plus
+    ORT_STATUS_BAD_GEOMETRY (-> ValueError) when only the surface record holds it."""
+    from optiland_pr_amd import _native
+    from optiland_pr_amd.lowering import segment_params
+    from optiland_pr_amd.raytrace import DeviceLens, RealRays, lens_for, trace_pupil
+    from optiland_pr_amd.samples import CookeTriplet
+
+    lens = CookeTriplet()
+    table = lens_for(lens, [0.55]).table
+    table.surfaces = table.surfaces.copy()
+    table.surfaces[2]["geometry"] = 12
+    seg = np.stack([segment_params(lens, 0.0, 1.0, 0)])
+    n = 256
+    px = torch.linspace(-0.5, 0.5, n, dtype=torch.float64, device="cuda")
+    py = torch.zeros(n, dtype=torch.float64, device="cuda")
+    out = RealRays.empty(n, 0.55)
+    dl = DeviceLens(table)
+    with pytest.raises(RuntimeError, match="ORT_ERR_ARG"):
+        trace_pupil(dl, seg, px, py, out, n, n, n)
+    dl.c.geometry_mask = dl.geometry_mask & ~(1 << 12)  # a stale / inconsistent mask
+    trace_pupil(dl, seg, px, py, out, n, n, n)
+    torch.cuda.synchronize()
+    assert np.isnan(out.numpy()["x"]).all()  # the closed-form kernel: NaN rays
+    st = torch.zeros(1, dtype=torch.int32, device="cuda")
+    import ctypes as C
+
+    from optiland_pr_amd import _abi
+    from optiland_pr_amd.raytrace import _ptr, _stream_handle, upload_segments
+
+    seg_dev = upload_segments(seg, "cuda")
+    batch = _native.ort_batch(n, n, n, 1, 0, seg_dev.data_ptr())
+    opt = _native.ort_options(_abi.NEWTON_SCHEDULE, 0, None)
+    out_c = out.c_struct()
+    rc = _native.load().ort_trace_pupil(C.byref(dl.c), _ptr(px), _ptr(py), C.byref(out_c),
+                                        C.byref(batch), C.byref(opt), None, None, _ptr(st),
+                                        _stream_handle())
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert int(st.item()) & _abi.STATUS_BAD_GEOMETRY  # ... and the status bit when asked
+
+
+@pytest.mark.parametrize("lens_name", ["cooke", "dg"])
+def test_signed_zeros_bit_exact(torch, lens_name):
+    """Rays on the symmetry planes (px = +-0, py = +-0, the on-axis chief ray) through
+    convex and concave surfaces: every output equal to the oracle's INCLUDING the sign of
+    zero results (the closed-form fast path's quotients keep signed zeros; a -0 input
+    takes the exact path)."""
+    from oracle import trace_np
+    from optiland_pr_amd.lowering import segment_params
+    from optiland_pr_amd.raytrace import RealRays, lens_for, trace_pupil
+    from optiland_pr_amd.samples import CookeTriplet, DoubleGauss
+
+    lens = CookeTriplet() if lens_name == "cooke" else DoubleGauss()
+    v = np.linspace(-1.0, 1.0, 41)
+    px = np.concatenate([np.zeros(41), v, -np.zeros(41), v, [0.0, -0.0, 0.0, -0.0]])
+    py = np.concatenate([v, np.zeros(41), v, -np.zeros(41), [0.0, 0.0, -0.0, -0.0]])
+    n = px.size
+    wl = 0.55 if lens_name == "cooke" else 0.5876
+    dl = lens_for(lens, [wl])
+    for hx, hy in ((0.0, 0.0), (0.0, 1.0), (0.5, 0.0)):
+        seg = np.stack([segment_params(lens, hx, hy, 0)])
+        out = RealRays.empty(n, wl)
+        trace_pupil(dl, seg, torch.as_tensor(px, device="cuda"),
+                    torch.as_tensor(py, device="cuda"), out, n, n, n)
+        torch.cuda.synchronize()
+        ref = trace_np.trace_segment(dl.table, trace_np.generate_rays(seg[0], px, py), 0).rays
+        got = out.numpy()
+        for a in FIELDS:
+            g, r = got[a], getattr(ref, a)
+            if a == "i":
+                np.testing.assert_allclose(g, r, rtol=1e-12, atol=0)
+                continue
+            np.testing.assert_array_equal(g, r, err_msg=f"{lens_name} ({hx},{hy}) {a}")
+            np.testing.assert_array_equal(np.signbit(g), np.signbit(r),
+                                          err_msg=f"{lens_name} ({hx},{hy}) sign of {a}")

@@ -36,8 +36,12 @@ def test_paraxial_and_positions(name, golden_index):
     g = load_golden(name)
     assert lens.paraxial.EPL() == meta["EPL"]
     assert lens.paraxial.EPD() == meta["EPD"]
-    assert lens.paraxial.f2() == meta["f2"]
-    assert lens.paraxial.XPL() == meta["XPL"]
+    # NaN in the golden: the reference's paraxial tracer cannot run on the lens (a grid
+    # sag has no radius, surface_group.py:153)
+    if not np.isnan(meta["f2"]):
+        assert lens.paraxial.f2() == meta["f2"]
+    if not np.isnan(meta["XPL"]):
+        assert lens.paraxial.XPL() == meta["XPL"]
     np.testing.assert_array_equal(np.ravel(lens.surface_group.positions), g["positions"])
     nr = [getattr(s.geometry, "norm_radius", np.nan) for s in lens.surface_group.surfaces]
     np.testing.assert_array_equal(nr, meta["norm_radius"])

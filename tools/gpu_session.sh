@@ -34,7 +34,9 @@ for step in "$@"; do
     pmcstall) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
          run pmc_stall 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d gpurun_out/pmc_stall -o run -- python3 bench.py --no-cpu --steps 10 --warmup 2 ;;
     counters) run counters 120 rocprofv3 -L ;;
-    ab) run ab 900 bash tools/ab.sh $(ls optiland_pr_amd/lib/variants) ;;
+    pmcissue) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
+         run pmc_issue 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_INSTS_VALU_TRANS_F64 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES --kernel-trace --output-format csv -d gpurun_out/pmc_issue -o run -- python3 bench.py --no-cpu --steps 10 --warmup 2 ;;
+    ab) run ab 900 bash tools/ab.sh $(cd optiland_pr_amd/lib/variants && ls *.so) ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
