@@ -254,6 +254,10 @@ def main():
     ap.add_argument("--cpu-rays", type=int, default=1_000_000)
     ap.add_argument("--cpu-seconds", type=float, default=1.5,
                     help="wall time of the multi-process CPU baseline leg")
+    ap.add_argument("--ramp-seconds", type=float, default=0.5,
+                    help="untimed steps before the warmup until the GPU clock has ramped "
+                         "(MI355X power management raises the engine clock only under "
+                         "sustained load: the first ~50 ms of launches run up to 15%% slower)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -278,28 +282,36 @@ def main():
     _native.load()
     w = CONFIGS[args.config](args, dev, rank, world, torch)
 
+    # clock ramp (untimed): keep the GPU busy until its engine clock has risen, then the
+    # W warmup steps
+    t_ramp = time.perf_counter()
+    while time.perf_counter() - t_ramp < args.ramp_seconds:
+        for _ in range(8):
+            w.step()
+        torch.cuda.synchronize()
     for _ in range(args.warmup):
         w.step()
     torch.cuda.synchronize()
 
-    # per-step device time with HIP events on the stream the kernels are launched on
-    # (torch's current stream: raytrace._stream_handle)
+    # device time of the step's kernel(s): HIP events on the stream they are launched on
+    # (torch's current stream: raytrace._stream_handle) at both ends of the timed region;
+    # per step = that span / K (kernel + the ~1 us launch gap between back-to-back
+    # kernels; an event pair around every step would itself add ~6 us to each step)
     stream = torch.cuda.current_stream()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        ev[k][0].record(stream)
+    ev0.record(stream)
+    for _ in range(args.steps):
         w.step()
-        ev[k][1].record(stream)
+    ev1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    kern_ms = ev0.elapsed_time(ev1) / args.steps
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -324,6 +336,9 @@ def main():
             "data": "synthetic (random pupil rays, numpy default_rng seed = rank)",
             "config": w.config,
             "roofline": _roofline(w, kern_ms),
+            "timing": {"clock_ramp_s": args.ramp_seconds,
+                       "device_ms_per_step": kern_ms,
+                       "kernel_time": "HIP events at both ends of the timed region / steps"},
         }
         if w.flops_per_ray is not None:
             line["roofline_fp64"] = _roofline_fp64(w, kern_ms)

@@ -5,7 +5,7 @@
 set -u
 cd "$(dirname "$0")/.."
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
-B="python3 bench.py --no-cpu --steps 20 --warmup 3"
+B="python3 bench.py --no-cpu --steps 200 --warmup 5"
 run() { local n=$1; shift; echo "== $n"; timeout -k 10 300 "$@" > gpurun_out/$n.log 2>&1; local rc=$?; echo "rc=$rc"; [ $rc -eq 0 ] || exit $rc; }
 mkdir -p gpurun_out
 run rocprof rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- $B
