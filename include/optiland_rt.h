@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define ORT_ABI_VERSION 10
+#define ORT_ABI_VERSION 11
 #define ORT_MAX_SURFACES 64
 
 /* ---- geometry kinds ----------------------------------- */
@@ -294,10 +294,17 @@ typedef struct ort_rays {
 /* Per (field, wavelength) segment parameters for in-kernel ray generation
  * (ray_generator.py:71-89 + field_types.py:160-172, infinite object, AngleField,
  * or field_types.py:173-181 finite object). Host scalars are computed in NumPy. */
-enum ort_gen_mode { ORT_GEN_INFINITE = 0, ORT_GEN_FINITE = 1 };
+enum ort_gen_mode {
+  ORT_GEN_INFINITE = 0,
+  ORT_GEN_FINITE = 1,
+  /* object-space telecentric (ray_generator.py:56-73): the pupil target is
+   * (Px vx + x0, Py vy + y0, epl) with epl = sqrt(1 - NA^2) / NA + z0 formed on the
+   * host; epd is unused */
+  ORT_GEN_TELECENTRIC = 2
+};
 typedef struct ort_segment {
   double epd;      /* EPD (paraxial.py:232-297)                                     */
-  double epl;      /* EPL (paraxial.py:207-230)                                     */
+  double epl;      /* EPL (paraxial.py:207-230); TELECENTRIC: the target plane z    */
   double vx, vy;   /* 1 - vignetting factor                                         */
   double x_off;    /* infinite: -tan(radians(field_x)) * (offset + EPL); finite: x0 */
   double y_off;
@@ -305,6 +312,32 @@ typedef struct ort_segment {
   int32_t lambda_idx;
   int32_t mode;    /* enum ort_gen_mode                                             */
 } ort_segment; /* 64 bytes */
+
+/* Pupil apodization (the optiland/apodization package): the generated ray's intensity as a
+ * function of its normalised pupil coordinates, apodization.get_intensity(Px, Py)
+ * (ray_generator.py:91-95; no apodization: 1). r = sqrt(Px^2 + Py^2). Lens-constant
+ * subexpressions are formed on the host with the reference's own operations:
+ *   GAUSSIAN        p0 = 2 sigma^2        exp(-(Px^2 + Py^2) / p0)          gaussian.py
+ *   COSINE_SQUARED  p0 = R, p1 = 2 R      r < R ? cos(pi r / p1)^2 : 0      cosine_squared.py
+ *   HANN            p0 = D / 2, p1 = D    r < p0 ? 0.5 (1 - cos(2 pi r / D)) : 0   hann.py
+ *   POLYNOMIAL      p0 = R, p1 = p        r < R ? (1 - (r / R)^2)^p : 0     polynomial.py
+ *   SUPER_GAUSSIAN  p0 = w, p1 = n        exp(-((r / w)^n))                 super_gaussian.py
+ *   TUKEY           p0 = R, p1 = R (1 - alpha / 2), p2 = R alpha / 2:
+ *                   r <= p1 ? 1 : r < R ? 0.5 (1 + cos(pi (r - p1) / p2)) : 0   tukey.py */
+enum ort_apod_kind {
+  ORT_APOD_UNIFORM = 0,
+  ORT_APOD_GAUSSIAN = 1,
+  ORT_APOD_COSINE_SQUARED = 2,
+  ORT_APOD_HANN = 3,
+  ORT_APOD_POLYNOMIAL = 4,
+  ORT_APOD_SUPER_GAUSSIAN = 5,
+  ORT_APOD_TUKEY = 6
+};
+typedef struct ort_apodization {
+  int32_t kind;  /* enum ort_apod_kind */
+  int32_t reserved;
+  double p[4];
+} ort_apodization; /* 40 bytes */
 
 /* A batch of rays: n_rays rays split into consecutive segments of seg_len rays (the
  * reference's field-major layout real_ray_tracer.py:74-77, generalised to (field,
@@ -327,6 +360,10 @@ typedef struct ort_batch {
    * standard_surface.py:218, refractive_reflective_model.py:32-55, homogeneous.py:30-57).
    * ort_trace_sequential only. */
   const double* w;
+  /* Pupil apodization of the generated rays (device, one record; NULL: intensity 1).
+   * Read by the entry points that generate rays (ort_trace_pupil, its VJP,
+   * ort_generate_rays). */
+  const ort_apodization* apod;
 } ort_batch;
 
 /* Newton semantics (newton_raphson.py:137-166). */

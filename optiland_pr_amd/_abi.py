@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import numpy as np
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 VJP_UNROLLED = 0
 VJP_ADJOINT = 1
 AP_RADIAL = 1
@@ -75,6 +75,16 @@ CS_ROT_Z = 3
 # enum ort_gen_mode
 GEN_INFINITE = 0
 GEN_FINITE = 1
+GEN_TELECENTRIC = 2
+
+# enum ort_apod_kind
+APOD_UNIFORM = 0
+APOD_GAUSSIAN = 1
+APOD_COSINE_SQUARED = 2
+APOD_HANN = 3
+APOD_POLYNOMIAL = 4
+APOD_SUPER_GAUSSIAN = 5
+APOD_TUKEY = 6
 
 # enum ort_newton_mode
 NEWTON_SCHEDULE = 0
@@ -158,6 +168,16 @@ SEGMENT = np.dtype(
     align=True,
 )
 assert SEGMENT.itemsize == 64
+
+APODIZATION = np.dtype(
+    [
+        ("kind", "<i4"),
+        ("reserved", "<i4"),
+        ("p", "<f8", (4,)),
+    ],
+    align=True,
+)
+assert APODIZATION.itemsize == 40
 
 # enum ort_material_kind
 MAT_IDEAL = 0

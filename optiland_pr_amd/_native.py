@@ -49,6 +49,7 @@ class ort_batch(C.Structure):
         ("pupil_per_ray", C.c_int32),
         ("seg", C.c_void_p),
         ("w", C.c_void_p),
+        ("apod", C.c_void_p),
     ]
 
 

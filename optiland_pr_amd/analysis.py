@@ -18,7 +18,7 @@ import numpy as np
 from . import _abi
 from .distribution import BaseDistribution, create_distribution
 from .pupil import pupil_arrays
-from .lowering import segment_params
+from .lowering import pupil_scalars, segment_params
 from .raytrace import RealRays, lens_for, trace_pupil
 
 try:
@@ -102,7 +102,7 @@ class SpotDiagram:
             if not (-1 <= hx <= 1 and -1 <= hy <= 1):
                 raise ValueError("Normalized field coordinates must be within (-1, 1)")
         dl = lens_for(optic, self.wavelengths)
-        EPL, EPD = optic.paraxial.EPL(), optic.paraxial.EPD()
+        EPL, EPD = pupil_scalars(optic)
         segs = np.stack([segment_params(optic, float(hx), float(hy), wi, EPL, EPD)
                          for hx, hy in self.fields for wi in range(len(self.wavelengths))])
         dev = dl.device

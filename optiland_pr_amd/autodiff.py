@@ -234,6 +234,7 @@ def vjp(dlens, seg_dev, px, py, n, seg_len, sched_dev, tables, n_param, cot, gra
     lib = _native.load()
     n_seg = seg_dev.numel() // _abi.SEGMENT.itemsize
     batch = _native.ort_batch(n, seg_len, n, n_seg, int(pupil_per_ray), seg_dev.data_ptr())
+    batch.apod = None if dlens.apod is None else dlens.apod.data_ptr()
     opt = _native.ort_options(_abi.NEWTON_SCHEDULE, 0,
                               None if sched_dev is None else sched_dev.data_ptr())
     zp, st, ft = tables

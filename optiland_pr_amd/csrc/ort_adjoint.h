@@ -211,7 +211,7 @@ __global__ __launch_bounds__(kBlock) void adj_kernel(const KArgs a, const AArgs 
   };
 
   // ---- forward: the primal trace, taping (incoming ray, t, Newton iterates) per surface
-  ort::Ray r = ort::generate_ray(sg, a.px[p], a.py[p]);
+  ort::Ray r = ort::generate_ray(sg, a.px[p], a.py[p], a.apod);
   for (int si = a.start_surface; si < a.n_surf; ++si) {
     const ort_surface s = cst(a.surf)[si];
     const ort_surface_optics o = optics_at(a, lam, si);

@@ -63,6 +63,7 @@ int fill_args(KArgs& a, const ort_lens* lens, const ort_batch* batch, const ort_
   a.seg = batch->seg;
   a.n_seg = batch->n_seg;
   a.pupil_per_ray = batch->pupil_per_ray;
+  a.apod = batch->apod;
   a.newton_mode = opt->newton_mode;
   a.start_surface = opt->start_surface;
   a.sched = opt->sched;
@@ -337,6 +338,7 @@ int ort_generate_rays(const double* px, const double* py, ort_rays* rays_out,
   a.seg_len = batch->seg_len;
   a.seg = batch->seg;
   a.pupil_per_ray = batch->pupil_per_ray;
+  a.apod = batch->apod;
   if (a.n_rays == 0) return ORT_OK;
   const int64_t blocks = (a.n_rays + kBlock - 1) / kBlock;
   hipLaunchKernelGGL(select_generate(), dim3((unsigned)blocks), dim3(kBlock), 0,

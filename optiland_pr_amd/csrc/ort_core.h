@@ -345,9 +345,63 @@ ORT_INLINE Dual<P> zcoef(double c, int j, const ZSeed& zs, Dual<P>*) {
 }
 
 // ---------------------------------------------------------------------------------
-// ray generation: rays/ray_generator.py:71-106 + fields/field_types.py:160-181
+// pupil apodization: apodization/*.py get_intensity(Px, Py), called from
+// rays/ray_generator.py:91-95. The same operations in the same order as the NumPy
+// expressions (x**2 is x * x, x**0.5 is sqrt, NumPy's fast scalar powers); exp / cos /
+// pow are the device's libm (within an ulp or so of NumPy's: intensity parity is
+// relative). Constants p[] come from the host (include/optiland_rt.h).
 // ---------------------------------------------------------------------------------
-ORT_INLINE Ray generate_ray(const ort_segment& s, double px, double py) {
+ORT_INLINE double apod_pow(double x, double e) {
+  // numpy fast_scalar_power: x**0 = 1, x**0.5 = sqrt, x**1 = x, x**2 = square
+  if (e == 1.0) return x;
+  if (e == 2.0) return x * x;
+  if (e == 0.5) return sqrt(x);
+  if (e == 0.0) return 1.0;
+  return ::pow(x, e);
+}
+
+ORT_INLINE double apodize(const ort_apodization& a, double px, double py) {
+  constexpr double kPi = 3.141592653589793;  // be.pi
+  const double r2 = px * px + py * py;
+  switch (a.kind) {
+    case ORT_APOD_GAUSSIAN:  // gaussian.py: exp(-(Px**2 + Py**2) / (2 * sigma**2))
+      return ::exp(-r2 / a.p[0]);
+    case ORT_APOD_COSINE_SQUARED: {  // cosine_squared.py
+      const double r = sqrt(r2);
+      const double c = ::cos((kPi * r) / a.p[1]);
+      return r < a.p[0] ? c * c : 0.0;
+    }
+    case ORT_APOD_HANN: {  // hann.py: R = D / 2, 0.5 * (1 - cos((2 * pi * r) / D))
+      const double r = sqrt(r2);
+      const double v = 0.5 * (1.0 - ::cos((2.0 * kPi * r) / a.p[1]));
+      return r < a.p[0] ? v : 0.0;
+    }
+    case ORT_APOD_POLYNOMIAL: {  // polynomial.py: (1 - (r / R)**2)**p
+      const double r = sqrt(r2);
+      const double q = r / a.p[0];
+      const double v = apod_pow(1.0 - q * q, a.p[1]);
+      return r < a.p[0] ? v : 0.0;
+    }
+    case ORT_APOD_SUPER_GAUSSIAN:  // super_gaussian.py: exp(-((r2**0.5 / w)**n))
+      return ::exp(-apod_pow(sqrt(r2) / a.p[0], a.p[1]));
+    case ORT_APOD_TUKEY: {  // tukey.py
+      const double r = sqrt(r2);
+      if (r <= a.p[1]) return 1.0;
+      if (r < a.p[0]) return 0.5 * (1.0 + ::cos(kPi * (r - a.p[1]) / a.p[2]));
+      return 0.0;
+    }
+    case ORT_APOD_UNIFORM:  // uniform.py: ones
+      return 1.0;
+    default:  // not a kind this library knows: NaN rather than a silent 1
+      return __builtin_nan("");
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// ray generation: rays/ray_generator.py:49-106 + fields/field_types.py:160-181
+// ---------------------------------------------------------------------------------
+ORT_INLINE Ray generate_ray(const ort_segment& s, double px, double py,
+                            const ort_apodization* apod = nullptr) {
   Ray r;
   double x0, y0;
   if (s.mode == ORT_GEN_INFINITE) {
@@ -358,8 +412,14 @@ ORT_INLINE Ray generate_ray(const ort_segment& s, double px, double py) {
     y0 = s.y_off;
   }
   const double z0 = s.z0;
-  const double x1 = px * s.epd * s.vx / 2.0;  // ray_generator.py:76
-  const double y1 = py * s.epd * s.vy / 2.0;  // ray_generator.py:77
+  double x1, y1;
+  if (s.mode == ORT_GEN_TELECENTRIC) {  // ray_generator.py:70-73
+    x1 = px * s.vx + x0;
+    y1 = py * s.vy + y0;
+  } else {
+    x1 = px * s.epd * s.vx / 2.0;  // ray_generator.py:76
+    y1 = py * s.epd * s.vy / 2.0;  // ray_generator.py:77
+  }
   const double z1 = s.epl;
   const double dx = x1 - x0, dy = y1 - y0, dz = z1 - z0;
   double mag = sqrt(dx * dx + dy * dy + dz * dz);  // :80
@@ -372,7 +432,7 @@ ORT_INLINE Ray generate_ray(const ort_segment& s, double px, double py) {
   r.x = x0;
   r.y = y0;
   r.z = z0;
-  r.i = 1.0;  // no apodization: be.ones_like(Px)
+  r.i = apod ? apodize(*apod, px, py) : 1.0;  // ray_generator.py:91-95
   r.opd = 0.0;
   r.att = 0.0;
   return r;

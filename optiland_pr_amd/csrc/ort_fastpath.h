@@ -185,7 +185,8 @@ ORT_INLINE double div(double a, double b, bool& bad) {
 }
 
 // rays/ray_generator.py:71-106 + fields/field_types.py:160-181 (ort_core.h generate_ray)
-ORT_INLINE Ray generate_ray(const ort_segment& s, double px, double py, bool& bad) {
+ORT_INLINE Ray generate_ray(const ort_segment& s, double px, double py,
+                            const ort_apodization* apod, bool& bad) {
   Ray r;
   double x0, y0;
   if (s.mode == ORT_GEN_INFINITE) {
@@ -196,8 +197,14 @@ ORT_INLINE Ray generate_ray(const ort_segment& s, double px, double py, bool& ba
     y0 = s.y_off;
   }
   const double z0 = s.z0;
-  const double x1 = px * s.epd * s.vx / 2.0;
-  const double y1 = py * s.epd * s.vy / 2.0;
+  double x1, y1;
+  if (s.mode == ORT_GEN_TELECENTRIC) {
+    x1 = px * s.vx + x0;
+    y1 = py * s.vy + y0;
+  } else {
+    x1 = px * s.epd * s.vx / 2.0;
+    y1 = py * s.epd * s.vy / 2.0;
+  }
   const double z1 = s.epl;
   const double dx = x1 - x0, dy = y1 - y0, dz = z1 - z0;
   const double mag = sqrt(dx * dx + dy * dy + dz * dz, bad);
@@ -212,7 +219,7 @@ ORT_INLINE Ray generate_ray(const ort_segment& s, double px, double py, bool& ba
   r.x = x0;
   r.y = y0;
   r.z = z0;
-  r.i = 1.0;
+  r.i = apod ? apodize(*apod, px, py) : 1.0;  // no range-sensitive operations
   r.opd = 0.0;
   r.att = 0.0;
   return r;

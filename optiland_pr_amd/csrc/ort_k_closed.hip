@@ -10,7 +10,7 @@ __global__ __launch_bounds__(kBlock) void generate_kernel(const KArgs a) {
   const int64_t sidx = rid / a.seg_len;
   const ort_segment sg = a.seg[sidx];
   const int64_t p = a.pupil_per_ray ? rid : (rid - sidx * a.seg_len);
-  const ort::Ray r = ort::generate_ray(sg, a.px[p], a.py[p]);
+  const ort::Ray r = ort::generate_ray(sg, a.px[p], a.py[p], a.apod);
   a.out.x[rid] = r.x;
   a.out.y[rid] = r.y;
   a.out.z[rid] = r.z;

@@ -104,6 +104,8 @@ struct KArgs {
   const ort_material* mats;
   // wavelength of each table row (F_IA: phase / grating interactions)
   const double* lambdas;
+  // pupil apodization of generated rays (NULL: intensity 1)
+  const ort_apodization* apod;
 };
 
 __device__ inline uint64_t wave_and_u64(uint64_t v) {
@@ -389,7 +391,7 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(const KArgs a) {
     const ort_segment sg = a.seg[sidx];
     lam = sg.lambda_idx;
     const int64_t p = a.pupil_per_ray ? r_ld : (r_ld - sidx * a.seg_len);
-    r = ort::generate_ray(sg, a.px[p], a.py[p]);
+    r = ort::generate_ray(sg, a.px[p], a.py[p], a.apod);
   } else {
     if (a.seg) lam = a.seg[sidx].lambda_idx;
     if constexpr ((FEAT & F_WRAY) != 0) wl = a.w[r_ld];
@@ -521,10 +523,11 @@ __device__ inline ort::Ray closed_ray_in(const KArgs& a, int64_t r_ld, int& lam,
     const ort_segment sg = a.n_seg == 1 ? cst(a.seg)[0] : a.seg[sidx];
     lam = sg.lambda_idx;
     const int64_t p = a.pupil_per_ray ? r_ld : (r_ld - sidx * a.seg_len);
+    // no apodization here: trace_closed_kernel applies it to the stored intensity
     if constexpr (FAST)
-      r = ort::fast::generate_ray(sg, a.px[p], a.py[p], bad);
+      r = ort::fast::generate_ray(sg, a.px[p], a.py[p], nullptr, bad);
     else
-      r = ort::generate_ray(sg, a.px[p], a.py[p]);
+      r = ort::generate_ray(sg, a.px[p], a.py[p], nullptr);
   } else {
     if (a.seg) lam = a.seg[a.n_seg == 1 ? 0 : r_ld / a.seg_len].lambda_idx;
     if constexpr ((FEAT & F_WRAY) != 0) wl = a.w[r_ld];
@@ -659,7 +662,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
   a.out.L[rid] = r.L;
   a.out.M[rid] = r.M;
   a.out.N[rid] = r.N;
-  a.out.i[rid] = ort::intensity(r);
+  double inten = ort::intensity(r);
+#ifndef ORT_NO_APOD
+  if constexpr ((FEAT & F_GEN) != 0) {
+    // Pupil apodization (ray_generator.py:91-95), applied to the stored intensity: the
+    // trace only ever multiplies the intensity (absorption) or zeroes it (clipping), so
+    // apod * (1 * e^att or 0) is the value the ray would carry from an apodized start,
+    // with the apodization code outside the traced loop.
+    if (a.apod) {
+      const int64_t sidx = a.n_seg == 1 ? 0 : rid / a.seg_len;
+      const int64_t p = a.pupil_per_ray ? rid : (rid - sidx * a.seg_len);
+      inten = ort::apodize(*cst(a.apod), a.px[p], a.py[p]) * inten;
+    }
+  }
+#endif
+  a.out.i[rid] = inten;
   a.out.opd[rid] = r.opd;
 }
 
@@ -725,7 +742,7 @@ __global__ __launch_bounds__(kBlock) void vjp_kernel(const KArgs a, const JArgs 
   const ort_segment sg = a.seg[sidx];
   const int lam = sg.lambda_idx;
   const int64_t p = a.pupil_per_ray ? r_ld : (r_ld - sidx * a.seg_len);
-  ort::RayT<D> r = ort::promote<D>(ort::generate_ray(sg, a.px[p], a.py[p]));
+  ort::RayT<D> r = ort::promote<D>(ort::generate_ray(sg, a.px[p], a.py[p], a.apod));
   const int64_t group = r_ld / a.group_len;
   const ort::ZSeed zs{j.zparam, j.p0};
   const int64_t ts = (int64_t)a.n_surf * 3;

@@ -43,7 +43,7 @@ def trace_sharded(optic, fields, wavelengths, px, py, group=None, newton_mode="r
     Newton semantics: each rank verifies its own schedule; the reference's global rule
     spans all ranks of a pair, so the schedule is agreed with one all_reduce(MAX) of the
     per-pair update counts when ranks disagree (rare)."""
-    from .lowering import segment_params
+    from .lowering import pupil_scalars, segment_params
     from .raytrace import RealRays, lens_for, trace_pupil
 
     rank, world = world_info(group)
@@ -51,7 +51,7 @@ def trace_sharded(optic, fields, wavelengths, px, py, group=None, newton_mode="r
     a, b = shard_range(n_p, rank, world)
     dl = lens_for(optic, list(wavelengths))
     dev = dl.device
-    EPL, EPD = optic.paraxial.EPL(), optic.paraxial.EPD()
+    EPL, EPD = pupil_scalars(optic)
     segs = np.stack([segment_params(optic, float(hx), float(hy), wi, EPL, EPD)
                      for hx, hy in fields for wi in range(len(wavelengths))])
     n_loc = b - a
@@ -89,6 +89,7 @@ def _agree_newton_schedule(dl, keys, segs, px, py, out, n, n_loc, group):
         lib = _native.load()
         seg_dev = upload_segments(segs, dl.device)
         batch = _native.ort_batch(n, n_loc, n_loc, len(segs), 0, seg_dev.data_ptr())
+        batch.apod = None if dl.apod is None else dl.apod.data_ptr()
         sched_dev = torch.as_tensor(agreed.reshape(-1), device=dl.device)
         opt = _native.ort_options(_abi.NEWTON_SCHEDULE, 0, sched_dev.data_ptr())
         out_c = out.c_struct()

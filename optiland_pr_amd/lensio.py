@@ -267,6 +267,11 @@ def optic_from_dict(data):
         optic.add_wavelength(wd["value"], bool(wd.get("is_primary", False)),
                              wd.get("unit", "um"))
     optic.polarization = data.get("wavelengths", {}).get("polarization", "ignore")
+    apod = data.get("apodization")  # optic.py:691-693
+    if apod:
+        from .apodization import BaseApodization
+
+        optic.apodization = BaseApodization.from_dict(apod)
     return optic
 
 
@@ -298,6 +303,7 @@ def optic_to_dict(optic):
                                          "unit": "um"}
                                         for w in optic.wavelengths.wavelengths],
                         "polarization": optic.polarization},
+        "apodization": optic.apodization.to_dict() if optic.apodization else None,
         "pickups": [],
         "solves": {"solves": []},
         "surface_group": {"surfaces": surfaces},

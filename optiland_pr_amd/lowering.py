@@ -48,6 +48,9 @@ class LensTable:
     # and the uploaded table is patched on the device (raytrace.lens_for), so an
     # optimisation loop over device-resident coefficients never waits on the GPU.
     device_coeffs: list = field(default_factory=list)
+    # pupil apodization of generated rays (_abi.APODIZATION record; None: intensity 1).
+    # An Optic-level property (optic.py:137): set by raytrace.lens_for from the Optic.
+    apod: np.ndarray = None
 
     @property
     def n_surfaces(self):
@@ -111,7 +114,16 @@ class LensTable:
                   self.mat_table)]
         parts.append(np.array([self.final_mat], dtype=np.int64).tobytes())
         parts.append(np.array([self.final_thickness], dtype=np.float64).tobytes())
+        if self.apod is not None:
+            parts.append(np.ascontiguousarray(self.apod).tobytes())
         return b"".join(parts)
+
+
+def lower_apodization(optic):
+    """optic.apodization (optiland/apodization) -> one _abi.APODIZATION record, or None
+    (no apodization, or an Optic-less surface group)."""
+    apod = getattr(optic, "apodization", None)
+    return None if apod is None else apod.lower()
 
 
 def _device_tensor(v):
@@ -341,17 +353,41 @@ def _starting_z_offset(optic):
     return offset - np.min(z)
 
 
+def pupil_scalars(optic):
+    """(EPL, EPD) for ray generation (paraxial.py:207-297), computed once per trace call.
+    Object-space telecentric systems aim at the object-space NA instead and the reference
+    computes neither (ray_generator.py:56-73): (None, None)."""
+    if optic.obj_space_telecentric:
+        return None, None
+    return optic.paraxial.EPL(), optic.paraxial.EPD()
+
+
+def _telecentric_checks(optic):
+    """ray_generator.py:56-68."""
+    if optic.field_type == "angle":
+        raise ValueError('Field type cannot be "angle" for telecentric object space.')
+    if optic.aperture.ap_type == "EPD":
+        raise ValueError('Aperture type cannot be "EPD" for telecentric object space.')
+    if optic.aperture.ap_type == "imageFNO":
+        raise ValueError('Aperture type cannot be "imageFNO" for telecentric object space.')
+
+
 def segment_params(optic, Hx, Hy, lambda_idx, EPL=None, EPD=None):
     """One ort_segment for field (Hx, Hy): ray_generator.py:49-89 + AngleField /
-    ObjectHeightField.get_ray_origins (field_types.py:139-181, 255-275)."""
+    ObjectHeightField / ParaxialImageHeightField.get_ray_origins (field_types.py:139-181,
+    255-275, 336-390); object-space telecentric aiming ray_generator.py:56-73."""
     seg = np.zeros((), dtype=_abi.SEGMENT)
-    if optic.obj_space_telecentric:
-        raise ValueError("telecentric object space is out of scope for the trace core")
     vxf, vyf = optic.fields.get_vig_factor(Hx, Hy)
     vx = 1 - np.array(vxf)
     vy = 1 - np.array(vyf)
-    EPL = optic.paraxial.EPL() if EPL is None else EPL
-    EPD = optic.paraxial.EPD() if EPD is None else EPD
+    telecentric = bool(optic.obj_space_telecentric)
+    if telecentric:
+        if optic.field_type == "angle":
+            _telecentric_checks(optic)  # raises (the angle origins would need EPL first)
+        EPL = EPD = 0.0
+    else:
+        EPL = optic.paraxial.EPL() if EPL is None else EPL
+        EPD = optic.paraxial.EPD() if EPD is None else EPD
     max_field = optic.fields.max_field
     field_x = max_field * Hx
     field_y = max_field * Hy
@@ -377,7 +413,7 @@ def segment_params(optic, Hx, Hy, lambda_idx, EPL=None, EPD=None):
         seg["mode"] = _abi.GEN_FINITE
         seg["x_off"] = float(np.array(field_x))
         seg["y_off"] = float(np.array(field_y))
-        seg["z0"] = float(obj.geometry.cs.z)  # plane object: sag 0 (field_types.py:273)
+        seg["z0"] = float(0.0 + obj.geometry.cs.z)  # plane object: sag 0 (field_types.py:273)
     elif optic.field_type == "paraxial_image_height":
         # ParaxialImageHeightField.get_ray_origins (field_types.py:336-390): the object-side
         # chief-ray slope / height that lands the paraxial chief ray at the target image
@@ -402,8 +438,15 @@ def segment_params(optic, Hx, Hy, lambda_idx, EPL=None, EPD=None):
             seg["z0"] = float(0.0 + obj.geometry.cs.z)  # plane object: sag 0
     else:
         raise ValueError(f"field type {optic.field_type!r} not supported")
-    seg["epd"] = float(EPD)
-    seg["epl"] = float(EPL)
+    if telecentric:  # ray_generator.py:56-73: aim at z = sqrt(1 - NA^2) / NA + z0
+        _telecentric_checks(optic)
+        sin = optic.aperture.value
+        seg["mode"] = _abi.GEN_TELECENTRIC
+        seg["epd"] = 0.0
+        seg["epl"] = float(np.sqrt(1 - sin**2) / sin + seg["z0"])
+    else:
+        seg["epd"] = float(EPD)
+        seg["epl"] = float(EPL)
     seg["vx"] = float(vx)
     seg["vy"] = float(vy)
     seg["lambda_idx"] = int(lambda_idx)

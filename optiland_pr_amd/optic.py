@@ -51,6 +51,23 @@ class Optic:
         self._lowered = None
         self.aperture = Aperture(aperture_type, value)
 
+    def set_apodization(self, apodization=None, **kwargs):
+        """optic.py:401-419 -> optic_updater.py:312-350: an apodization instance, a
+        class name plus its keyword arguments, a to_dict() dict, or None."""
+        from .apodization import resolve
+
+        self.apodization = resolve(apodization, **kwargs)
+
+    def image_solve(self):
+        """optic_updater.py:258-270: move the image surface to the paraxial focus of the
+        marginal ray."""
+        ya, ua = self.paraxial.marginal_ray()
+        offset = float(ya[-1, 0] / ua[-1, 0])
+        surfs = self.surface_group.surfaces
+        surfs[-1].geometry.cs.z -= offset
+        surfs[-2].thickness = surfs[-1].geometry.cs.z - surfs[-2].geometry.cs.z
+        self._lowered = None
+
     def set_field_type(self, field_type):
         """optic.py:298-318: 'angle' | 'object_height' | 'paraxial_image_height'."""
         if field_type not in ("angle", "object_height", "paraxial_image_height"):

@@ -23,7 +23,8 @@ import numpy as np
 
 from . import _abi, _native, autodiff
 from .pupil import pupil_arrays
-from .lowering import LensTable, lower_surface_group, segment_params
+from .lowering import (LensTable, lower_apodization, lower_surface_group, pupil_scalars,
+                       segment_params)
 
 try:
     import torch
@@ -56,6 +57,11 @@ def get_device():
 
 def _ptr(t):
     return C.c_void_p(t.data_ptr()) if t is not None else C.c_void_p(0)
+
+
+def _addr(t):
+    """A device tensor's address for a c_void_p struct field (None: NULL)."""
+    return t.data_ptr() if t is not None else None
 
 
 def _stream_handle():
@@ -145,6 +151,8 @@ class DeviceLens:
             table.n_surfaces, len(table.wavelengths), table.n_tab.shape[1], table.final_mat,
             mask, table.interaction_mask, table.final_thickness, self.mats.data_ptr(),
             self.lambdas.data_ptr(), table.frame_flags)
+        # the pupil apodization record (ort_batch.apod of generating launches)
+        self.apod = None if table.apod is None else _to_device_bytes(table.apod, d)
         self.newton = table.newton_surfaces
         self.sched_cache: dict = {}
 
@@ -260,6 +268,7 @@ def lens_for(optic_or_group, wavelengths, record=False, image_record=False):
         except AttributeError:
             pass
     table = lower_surface_group(sg, wavelengths, record=record)
+    table.apod = lower_apodization(host)
     if image_record:
         table.final_mat = -1
     fp = table.fingerprint()
@@ -352,6 +361,7 @@ def trace_pupil(dlens: DeviceLens, segments, px, py, out: RealRays, n_rays,
     n_seg = seg_dev.numel() // _abi.SEGMENT.itemsize
     batch = _native.ort_batch(n_rays, seg_len, group_len, n_seg, int(pupil_per_ray),
                               seg_dev.data_ptr())
+    batch.apod = _addr(dlens.apod)
     out_c = out.c_struct()
 
     def launch(opt, stats, status):
@@ -407,11 +417,15 @@ def trace_rays(dlens: DeviceLens, rays_in: RealRays, rays_out: RealRays, group_l
     return seg_dev
 
 
-def generate_rays(segments, px, py, out: RealRays, n_rays, seg_len, pupil_per_ray=False):
+def generate_rays(segments, px, py, out: RealRays, n_rays, seg_len, pupil_per_ray=False,
+                  apod=None):
+    """Ray generation only (ort_generate_rays). apod: a device APODIZATION record
+    (DeviceLens.apod) or None."""
     lib = _native.load()
     seg_dev = _to_device_bytes(segments, out.x.device)
     batch = _native.ort_batch(n_rays, seg_len, n_rays, len(segments), int(pupil_per_ray),
                               seg_dev.data_ptr())
+    batch.apod = _addr(apod)
     out_c = out.c_struct()
     rc = lib.ort_generate_rays(_ptr(px), _ptr(py), C.byref(out_c), C.byref(batch),
                                _stream_handle())
@@ -461,7 +475,7 @@ class RealRayTracer:
         Hx, Hy = np.broadcast_arrays(Hx, Hy)
         record = optic.surface_group.record
         dlens = lens_for(optic, [wavelength], record=True if record == "all" else False)
-        EPL, EPD = optic.paraxial.EPL(), optic.paraxial.EPD()
+        EPL, EPD = pupil_scalars(optic)
         segs = np.stack([segment_params(optic, float(hx), float(hy), 0, EPL, EPD)
                          for hx, hy in zip(Hx, Hy, strict=True)])
         dev = dlens.device
@@ -497,7 +511,7 @@ class RealRayTracer:
         Py = Py * (1 - vys)
         record = optic.surface_group.record
         dlens = lens_for(optic, [wavelength], record=True if record == "all" else False)
-        EPL, EPD = optic.paraxial.EPL(), optic.paraxial.EPD()
+        EPL, EPD = pupil_scalars(optic)
         uniq = {}
         segs = np.empty(n, dtype=_abi.SEGMENT)
         for r in range(n):
@@ -550,7 +564,7 @@ class RealRayTracer:
         sg = self.optic.surface_group
         if rec is not None:
             rays0 = RealRays.empty(n, 0.0, device=dlens.device)
-            generate_rays(segs, px, py, rays0, n, seg_len, pupil_per_ray)
+            generate_rays(segs, px, py, rays0, n, seg_len, pupil_per_ray, apod=dlens.apod)
             _record_into(sg, rec, n, dlens.table.rec_surfaces, rays0)
         else:
             sg.reset()

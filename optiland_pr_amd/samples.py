@@ -459,6 +459,59 @@ class GridSagLens(Optic):
         self.add_wavelength(value=0.55, is_primary=True)
 
 
+
+
+_UV_PRESCRIPTION = (  # (radius, thickness, glass) of surfaces 1-42, lithography.py:23-64
+    (-737.7847, 27.484, True), (-235.2891, 0.916, False), (211.1786, 36.646, True),
+    (-461.3986, 0.916, False), (412.6778, 21.071, True), (160.5391, 16.197, False),
+    (-604.1283, 7.215, True), (218.1877, 23.941, False), (-3586.063, 11.978, True),
+    (251.8168, 47.506, False), (-85.2817, 11.961, True), (584.8597, 9.968, False),
+    (4074.801, 35.291, True), (-162.0185, 0.923, False), (629.544, 41.227, True),
+    (-226.7397, 0.916, False), (522.2739, 27.842, True), (-582.424, 0.916, False),
+    (423.729, 22.904, True), (-1385.36, 0.916, False), (212.039, 33.646, True),
+    (802.3695, 55.304, False), (-776.5697, 8.703, True), (106.1728, 24.09, False),
+    (-200.683, 11.452, True), (311.8264, 59.54, False), (-77.2276, 11.772, True),
+    (2317.8032, 11.862, False), (-290.8859, 22.904, True), (-148.3577, 1.373, False),
+    (-5658.5043, 41.227, True), (-151.9858, 0.916, False), (678.1005, 32.981, True),
+    (-358.554, 0.916, False), (264.2734, 32.814, True), (2309.6884, 0.916, False),
+    (171.2681, 29.015, True), (364.7765, 0.918, False), (113.37, 76.259, True),
+    (78.6982, 54.304, False), (49.5443, 18.65, True), (109.8136, 13.07647896, False),
+)
+
+
+class UVProjectionLens(Optic):
+    """samples/lithography.py:8-84: 248 nm projection lens, 42 spheres (S = 43),
+    object-space telecentric (objectNA 0.133, object-height fields), image_solve."""
+
+    def __init__(self):
+        from .materials import IdealMaterial
+
+        super().__init__()
+        sio2 = IdealMaterial(n=1.5084, k=0)
+        self.add_surface(index=0, radius=np.inf, thickness=110.85883544)
+        for k, (r, t, glass) in enumerate(_UV_PRESCRIPTION, start=1):
+            self.add_surface(index=k, radius=r, thickness=t, is_stop=(k == 20),
+                             **({"material": sio2} if glass else {}))
+        self.add_surface(index=43, radius=np.inf)
+        self.set_aperture(aperture_type="objectNA", value=0.133)
+        self.set_field_type(field_type="object_height")
+        self.add_field(y=0)
+        self.add_field(y=32)
+        self.add_field(y=48)
+        self.add_wavelength(value=0.248, is_primary=True)
+        self.obj_space_telecentric = True
+        self.image_solve()
+
+
+class CookeTripletApodized(CookeTriplet):
+    """CookeTriplet with a pupil apodization (optic.set_apodization): every apodization
+    kind of optiland/apodization is exercised by the parity fixtures through this lens."""
+
+    def __init__(self, apodization="GaussianApodization", **kwargs):
+        super().__init__()
+        self.set_apodization(apodization, **kwargs)
+
+
 GOLDEN_LENSES = {
     "cooke": CookeTriplet,
     "dg": DoubleGauss,
@@ -484,4 +537,12 @@ GOLDEN_LENSES = {
     "grating_reflective": lambda: Grating("reflective"),
     "grating_tilted": lambda: Grating("curved", angle=0.35),
     "grid_lens": GridSagLens,
+    "uv_projection": UVProjectionLens,
+    "apod_gaussian": lambda: CookeTripletApodized("GaussianApodization", sigma=0.6),
+    "apod_cos2": lambda: CookeTripletApodized("CosineSquaredApodization", R=0.9),
+    "apod_hann": lambda: CookeTripletApodized("HannApodization", D=1.8),
+    "apod_poly": lambda: CookeTripletApodized("PolynomialApodization", R=0.95, p=1.5),
+    "apod_supergauss": lambda: CookeTripletApodized("SuperGaussianApodization", w=0.7, n=3.5),
+    "apod_tukey": lambda: CookeTripletApodized("TukeyApodization", R=0.9, alpha=0.6),
+    "apod_uniform": lambda: CookeTripletApodized("UniformApodization"),
 }

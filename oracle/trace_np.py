@@ -72,21 +72,55 @@ class Rays:
         return {a: getattr(self, a) for a in _abi.RAY_FIELDS}
 
 
-def generate_rays(seg, px, py):
-    """ray_generator.py:49-106 with AngleField.get_ray_origins field_types.py:139-181.
+def apodize(apod, px, py):
+    """apodization/*.py get_intensity(Px, Py) (ray_generator.py:91-95) from the lowered
+    record (_abi.APODIZATION: kind + the host-formed constants p, include/optiland_rt.h),
+    the reference's NumPy expressions in the reference's order."""
+    k, p = int(apod["kind"]), [float(v) for v in apod["p"]]
+    with np.errstate(invalid="ignore", divide="ignore"):
+        if k == _abi.APOD_UNIFORM:  # uniform.py
+            return np.ones_like(px)
+        if k == _abi.APOD_GAUSSIAN:  # gaussian.py:65-76
+            return np.exp(-(px**2 + py**2) / p[0])
+        r = (px**2 + py**2) ** 0.5
+        if k == _abi.APOD_COSINE_SQUARED:  # cosine_squared.py:43-48
+            return np.where(r < p[0], np.cos((np.pi * r) / p[1]) ** 2, 0.0)
+        if k == _abi.APOD_HANN:  # hann.py
+            return np.where(r < p[0], 0.5 * (1 - np.cos((2 * np.pi * r) / p[1])), 0.0)
+        if k == _abi.APOD_POLYNOMIAL:  # polynomial.py
+            return np.where(r < p[0], (1 - (r / p[0]) ** 2) ** p[1], 0.0)
+        if k == _abi.APOD_SUPER_GAUSSIAN:  # super_gaussian.py
+            return np.exp(-((r / p[0]) ** p[1]))
+        if k == _abi.APOD_TUKEY:  # tukey.py
+            taper = 0.5 * (1 + np.cos(np.pi * (r - p[1]) / p[2]))
+            out = np.where(r <= p[1], 1.0, 0.0)
+            return np.where((r > p[1]) & (r < p[0]), taper, out)
+    raise ValueError(f"unknown apodization kind {k}")
 
-    seg: one _abi.SEGMENT record (host scalars EPD, EPL, vx, vy, x_off, y_off, z0)."""
+
+def generate_rays(seg, px, py, apod=None):
+    """ray_generator.py:49-106 with AngleField / ObjectHeightField get_ray_origins
+    (field_types.py:139-181, 255-275), object-space telecentric aiming (:56-73) and the
+    pupil apodization (:91-95).
+
+    seg: one _abi.SEGMENT record (host scalars EPD, EPL, vx, vy, x_off, y_off, z0);
+    apod: one _abi.APODIZATION record or None (intensity 1)."""
     epd, epl = float(seg["epd"]), float(seg["epl"])
     vx, vy = float(seg["vx"]), float(seg["vy"])
-    if int(seg["mode"]) == _abi.GEN_INFINITE:
+    mode = int(seg["mode"])
+    if mode == _abi.GEN_INFINITE:
         x0 = px * epd / 2 * vx + float(seg["x_off"])  # field_types.py:166
         y0 = py * epd / 2 * vy + float(seg["y_off"])  # field_types.py:167
     else:
         x0 = np.full_like(px, float(seg["x_off"]))  # field_types.py:173-178
         y0 = np.full_like(px, float(seg["y_off"]))
     z0 = np.full_like(px, float(seg["z0"]))
-    x1 = px * epd * vx / 2  # ray_generator.py:76
-    y1 = py * epd * vy / 2  # ray_generator.py:77
+    if mode == _abi.GEN_TELECENTRIC:  # ray_generator.py:70-73
+        x1 = px * vx + x0
+        y1 = py * vy + y0
+    else:
+        x1 = px * epd * vx / 2  # ray_generator.py:76
+        y1 = py * epd * vy / 2  # ray_generator.py:77
     z1 = np.full_like(px, epl)
     mag = np.sqrt((x1 - x0) ** 2 + (y1 - y0) ** 2 + (z1 - z0) ** 2)  # :80
     is_zero = mag < 1e-9
@@ -94,7 +128,8 @@ def generate_rays(seg, px, py):
     L = np.where(is_zero, 0.0, (x1 - x0) / mag)
     M = np.where(is_zero, 0.0, (y1 - y0) / mag)
     N = np.where(is_zero, 1.0, (z1 - z0) / mag)
-    return Rays(x0, y0, z0, L, M, N, np.ones_like(px))
+    i = np.ones_like(px) if apod is None else apodize(apod, px, py)
+    return Rays(x0, y0, z0, L, M, N, i)
 
 
 # --------------------------------------------------------------------------------------

@@ -429,6 +429,23 @@ def grid_lens():
     return lens
 
 
+def cooke_apod(kind, **kwargs):
+    """CookeTriplet with a pupil apodization (optic.set_apodization, optic.py:401-419;
+    applied in ray_generator.py:91-95)."""
+    def build():
+        lens = CookeTriplet()
+        lens.set_apodization(kind, **kwargs)
+        return lens
+    return build
+
+
+def uv_projection():
+    """samples/lithography.py: 43-surface object-space telecentric projection lens."""
+    from optiland.samples.lithography import UVProjectionLens
+
+    return UVProjectionLens()
+
+
 def json_lens(name):
     """A lens file from the reference's docs/samples (copied as data to tests/golden/lenses),
     loaded with the reference's own Optic.from_dict (optic.py:674-713)."""
@@ -475,6 +492,19 @@ CASES = {
     "grating_tilted": (lambda: grating("curved", angle=0.35), [(0, 0), (0.2, 0.8)], [0.587],
                        "uniform", 24),
     "grid_lens": (grid_lens, [(0, 0), (0, 1), (0.6, 0.6)], [0.48, 0.55], "uniform", 24),
+    "uv_projection": (uv_projection, [(0, 0), (0, 0.7), (0, 1)], [0.248], "uniform", 24),
+    "apod_gaussian": (cooke_apod("GaussianApodization", sigma=0.6), [(0, 0), (0, 1)], [0.55],
+                      "uniform", 24),
+    "apod_cos2": (cooke_apod("CosineSquaredApodization", R=0.9), [(0, 0), (0, 1)], [0.55],
+                  "uniform", 24),
+    "apod_hann": (cooke_apod("HannApodization", D=1.8), [(0, 0), (0, 1)], [0.55], "uniform", 24),
+    "apod_poly": (cooke_apod("PolynomialApodization", R=0.95, p=1.5), [(0, 0), (0, 1)], [0.55],
+                  "uniform", 24),
+    "apod_supergauss": (cooke_apod("SuperGaussianApodization", w=0.7, n=3.5), [(0, 0), (0, 1)],
+                        [0.55], "uniform", 24),
+    "apod_tukey": (cooke_apod("TukeyApodization", R=0.9, alpha=0.6), [(0, 0), (0, 1)], [0.55],
+                   "uniform", 24),
+    "apod_uniform": (cooke_apod("UniformApodization"), [(0, 0), (0, 1)], [0.55], "uniform", 24),
 }
 
 

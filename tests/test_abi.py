@@ -19,6 +19,7 @@ STRUCTS = {
     "ort_cs_op": (_abi.CS_OP, None),
     "ort_zernike_term": (_abi.ZERNIKE_TERM, None),
     "ort_segment": (_abi.SEGMENT, None),
+    "ort_apodization": (_abi.APODIZATION, None),
     "ort_newton_stat": (_abi.NEWTON_STAT, None),
     "ort_lens": (None, _native.ort_lens),
     "ort_rays": (None, _native.ort_rays),
@@ -71,6 +72,14 @@ def test_enums_match_header():
                          ("ORT_CS_TRANSLATE", _abi.CS_TRANSLATE), ("ORT_CS_ROT_X", _abi.CS_ROT_X),
                          ("ORT_CS_ROT_Y", _abi.CS_ROT_Y), ("ORT_CS_ROT_Z", _abi.CS_ROT_Z),
                          ("ORT_GEN_INFINITE", _abi.GEN_INFINITE), ("ORT_GEN_FINITE", _abi.GEN_FINITE),
+                         ("ORT_GEN_TELECENTRIC", _abi.GEN_TELECENTRIC),
+                         ("ORT_APOD_UNIFORM", _abi.APOD_UNIFORM),
+                         ("ORT_APOD_GAUSSIAN", _abi.APOD_GAUSSIAN),
+                         ("ORT_APOD_COSINE_SQUARED", _abi.APOD_COSINE_SQUARED),
+                         ("ORT_APOD_HANN", _abi.APOD_HANN),
+                         ("ORT_APOD_POLYNOMIAL", _abi.APOD_POLYNOMIAL),
+                         ("ORT_APOD_SUPER_GAUSSIAN", _abi.APOD_SUPER_GAUSSIAN),
+                         ("ORT_APOD_TUKEY", _abi.APOD_TUKEY),
                          ("ORT_NEWTON_SCHEDULE", _abi.NEWTON_SCHEDULE),
                          ("ORT_NEWTON_WAVE", _abi.NEWTON_WAVE),
                          ("ORT_VJP_UNROLLED", _abi.VJP_UNROLLED),

@@ -21,7 +21,7 @@ def run_oracle(name, meta, record=False):
     n_p = meta["n_pupil"]
     gen, out, ups, recs = [], [], [], []
     for k, seg in enumerate(segs):
-        r0 = trace_np.generate_rays(seg, g["Px"], g["Py"])
+        r0 = trace_np.generate_rays(seg, g["Px"], g["Py"], table.apod)
         gen.append(r0.copy())
         res = trace_np.trace_segment(table, r0, int(seg["lambda_idx"]), record=record)
         out.append(res.rays)
