@@ -238,7 +238,11 @@ typedef struct ort_zernike_term {
 enum ort_material_kind {
   ORT_MAT_IDEAL = 0,
   ORT_MAT_FORMULA_1 = 1, /* ... ORT_MAT_FORMULA_9 = 9: refractiveindex.info formulas */
-  ORT_MAT_TABULATED = 10
+  ORT_MAT_TABULATED = 10,
+  /* AbbeMaterial (materials/abbe.py:37-51): n = polyval(p, lambda), p_0 .. p_3 in coef
+   * (highest power first, numpy.polyval's Horner order), defined on 0.380 .. 0.750 um
+   * (outside: NaN here; the host raises the reference's ValueError first), k = 0 */
+  ORT_MAT_ABBE = 11
 };
 typedef struct ort_material {
   int32_t kind;     /* enum ort_material_kind                                          */

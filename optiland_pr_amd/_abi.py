@@ -182,6 +182,7 @@ assert APODIZATION.itemsize == 40
 # enum ort_material_kind
 MAT_IDEAL = 0
 MAT_TABULATED = 10
+MAT_ABBE = 11
 
 MATERIAL = np.dtype(
     [

@@ -67,6 +67,8 @@ class _RefMaterial(BaseMaterial):
         m = self.m
         if type(m).__name__ == "IdealMaterial":
             return 0, [], [], [], _f(m.index), _f(m.absorp)
+        if type(m).__name__ == "AbbeMaterial":  # abbe.py: polyval(p, w)
+            return _abi.MAT_ABBE, [float(v) for v in np.ravel(_np(m._p))], [], [], 0.0, 0.0
         return lower_dispersion(m._n_formula, m.coefficients, m._k_wavelength, m._k,
                                 getattr(m, "_n_wavelength", None), getattr(m, "_n", None))
 
@@ -75,6 +77,8 @@ class _RefMaterial(BaseMaterial):
         m = self.m
         if type(m).__name__ == "IdealMaterial":
             return ("ideal", _f(m.index), _f(m.absorp))
+        if type(m).__name__ == "AbbeMaterial":
+            return ("abbe", _f(m.index), _f(m.abbe))
         fn = getattr(m, "filename", None)
         if fn:
             import os

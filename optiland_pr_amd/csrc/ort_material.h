@@ -96,6 +96,12 @@ ORT_INLINE double material_n(const ort_material& m, PD coef, double w) {
       const double n = c[0] + c[1] / (w * w - c[2]) + c[3] * e / (e * e + c[5]);
       return sqrt(n);
     }
+    case ORT_MAT_ABBE: {  // numpy.polyval: y = y * w + p_i from y = 0 (abbe.py:37-51)
+      if (!(w >= 0.380 && w <= 0.750)) return __builtin_nan("");
+      double y = 0.0;
+      for (int k = 0; k < nc; ++k) y = y * w + c[k];
+      return y;
+    }
     default:  // ORT_MAT_TABULATED
       return np_interp(w, c, c + nc, nc);
   }

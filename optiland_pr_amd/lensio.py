@@ -40,7 +40,7 @@ from .geometries import (
     scalar,
 )
 from .interactions import BaseInteractionModel, RefractiveReflectiveModel
-from .materials import IdealMaterial, Material
+from .materials import AbbeMaterial, IdealMaterial, Material
 from .apertures import BaseAperture
 from .surfaces import ObjectSurface, Surface
 
@@ -199,10 +199,18 @@ def material_from_dict(d):
         return IdealMaterial(_f(d.get("index"), 1.0), _f(d.get("absorp")))
     if t in ("Material", "MaterialFile"):
         return Material(d["name"], d.get("reference"))
+    if t == "AbbeMaterial":  # abbe.py:100-126
+        for key in ("index", "abbe"):
+            if key not in d:
+                raise ValueError(f"Missing required key: {key}")
+        return AbbeMaterial(d["index"], d["abbe"])
     raise ValueError(f"Unsupported material type: {t}")
 
 
 def material_to_dict(m):
+    if isinstance(m, AbbeMaterial):
+        return {"type": "AbbeMaterial", "propagation_model": {"class": "HomogeneousPropagation"},
+                "index": float(m.index[0]), "abbe": float(m.abbe[0])}
     if isinstance(m, IdealMaterial):
         return {"type": "IdealMaterial", "index": float(np.ravel(m.index)[0]),
                 "absorp": float(np.ravel(m.absorp)[0])}

@@ -199,6 +199,46 @@ class Material(BaseMaterial):
         return np.interp(w, self._n_wavelength, self._n)
 
 
+_ABBE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "abbe_coefficients.json")
+_ABBE_COEF = None
+
+
+class AbbeMaterial(BaseMaterial):
+    """materials/abbe.py:19-126: a model glass from nd and the Abbe number, n(w) a cubic
+    polynomial in w whose coefficients are a fixed linear map (the reference's
+    database/glass_model_coefficients.npy, baked into data/abbe_coefficients.json) of
+    (nd, vd, nd^2, vd^2, nd^3, vd^3); valid for 0.380 <= w <= 0.750 um, k = 0."""
+
+    def __init__(self, n, abbe):
+        global _ABBE_COEF
+        if _ABBE_COEF is None:
+            with open(_ABBE) as f:
+                _ABBE_COEF = np.array(json.load(f)["coefficients"], dtype=np.float64)
+        self.index = np.array([n], dtype=np.float64)
+        self.abbe = np.array([abbe], dtype=np.float64)
+        x = np.ravel(np.array([self.index, self.abbe, self.index**2, self.abbe**2,
+                               self.index**3, self.abbe**3]))
+        self._p = np.matmul(x, _ABBE_COEF)  # abbe.py:67-98
+
+    def _calculate_n(self, w):  # abbe.py:37-51
+        if np.any(w < 0.380) or np.any(w > 0.750):
+            raise ValueError("Wavelength out of range for this model.")
+        return np.atleast_1d(np.polyval(self._p, w))
+
+    def _calculate_k(self, w):  # abbe.py:53-65 (zeros_like(0))
+        return np.zeros_like(w)
+
+    def key(self):
+        return ("abbe", float(self.index[0]), float(self.abbe[0]))
+
+    def lower(self):
+        """ORT_MAT_ABBE: the 4 polynomial coefficients (highest power first)."""
+        return 11, [float(v) for v in self._p], [], [], 0.0, 0.0
+
+    def __repr__(self):
+        return f"AbbeMaterial(n={self.index[0]}, abbe={self.abbe[0]})"
+
+
 def lower_dispersion(formula, coefficients, k_wavelength, k, n_wavelength, n):
     """Per-ray dispersion record of a catalog material (include/optiland_rt.h
     ort_material) -> (kind, coefficients, k wavelengths, k values, n_const, k_const):

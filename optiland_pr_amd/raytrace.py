@@ -396,6 +396,11 @@ def trace_rays(dlens: DeviceLens, rays_in: RealRays, rays_out: RealRays, group_l
         w_keep = w_keep.expand(n).contiguous() if w_keep.numel() == 1 else w_keep.contiguous()
         if w_keep.numel() != n:
             raise ValueError("rays.w must hold one wavelength per ray")
+        mt = dlens.table.mat_table
+        if mt is not None and np.any(mt["kind"] == _abi.MAT_ABBE):
+            # abbe.py:47-48 raises before any n is used; the device would only give NaN
+            if bool(((w_keep < 0.380) | (w_keep > 0.750)).any()):
+                raise ValueError("Wavelength out of range for this model.")
         batch.w = w_keep.data_ptr()
     in_c, out_c = rays_in.c_struct(), rays_out.c_struct()
 

@@ -512,6 +512,34 @@ class CookeTripletApodized(CookeTriplet):
         self.set_apodization(apodization, **kwargs)
 
 
+class CookeTripletAbbe(Optic):
+    """The Cooke triplet prescription with AbbeMaterial model glasses (materials/abbe.py)
+    in place of SK16 / F2 (tests/golden/gen_golden.py cooke_abbe)."""
+
+    def __init__(self):
+        from .materials import AbbeMaterial
+
+        super().__init__()
+        sk16 = AbbeMaterial(1.62041, 60.32)
+        f2 = AbbeMaterial(1.62004, 36.37)
+        self.add_surface(index=0, radius=np.inf, thickness=np.inf)
+        self.add_surface(index=1, radius=22.01359, thickness=3.25896, material=sk16)
+        self.add_surface(index=2, radius=-435.76044, thickness=6.00755)
+        self.add_surface(index=3, radius=-22.21328, thickness=0.99997, material=f2)
+        self.add_surface(index=4, radius=20.29192, thickness=4.75041, is_stop=True)
+        self.add_surface(index=5, radius=79.68360, thickness=2.95208, material=sk16)
+        self.add_surface(index=6, radius=-18.39533, thickness=42.20778)
+        self.add_surface(index=7)
+        self.set_aperture(aperture_type="EPD", value=10)
+        self.set_field_type(field_type="angle")
+        self.add_field(y=0)
+        self.add_field(y=14)
+        self.add_field(y=20)
+        self.add_wavelength(value=0.48)
+        self.add_wavelength(value=0.55, is_primary=True)
+        self.add_wavelength(value=0.65)
+
+
 GOLDEN_LENSES = {
     "cooke": CookeTriplet,
     "dg": DoubleGauss,
@@ -545,4 +573,5 @@ GOLDEN_LENSES = {
     "apod_supergauss": lambda: CookeTripletApodized("SuperGaussianApodization", w=0.7, n=3.5),
     "apod_tukey": lambda: CookeTripletApodized("TukeyApodization", R=0.9, alpha=0.6),
     "apod_uniform": lambda: CookeTripletApodized("UniformApodization"),
+    "cooke_abbe": CookeTripletAbbe,
 }

@@ -980,6 +980,10 @@ def material_n(table, mi, w):
     if kind == 9:
         n = c[0] + c[1] / (w**2 - c[2]) + c[3] * (w - c[4]) / ((w - c[4]) ** 2 + c[5])
         return np.sqrt(n)
+    if kind == _abi.MAT_ABBE:  # abbe.py:37-51
+        if np.any(w < 0.380) or np.any(w > 0.750):
+            raise ValueError("Wavelength out of range for this model.")
+        return np.atleast_1d(np.polyval(c, w))
     raise ValueError(kind)
 
 

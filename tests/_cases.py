@@ -45,7 +45,7 @@ CLOSED_FORM = ("cooke", "dg", "rt", "cooke_aperture", "cooke_shapes", "decentere
                "json_heliar", "json_rt", "cooke_pih", "finite_pih", "paraxial_lens",
                "paraxial_mirror", "grating_flat", "grating_curved", "grating_reflective",
                "grating_tilted", "uv_projection", "apod_gaussian", "apod_cos2", "apod_hann",
-               "apod_poly", "apod_supergauss", "apod_tukey", "apod_uniform")
+               "apod_poly", "apod_supergauss", "apod_tukey", "apod_uniform", "cooke_abbe")
 NEWTON = ("rt_asph", "rt_odd", "tma_fringe", "tma_standard", "tma_noll", "freeform",
           "forbes", "forbes_q2d", "phase_plate", "grid_lens")
 ALL_CASES = CLOSED_FORM + NEWTON

@@ -446,6 +446,33 @@ def uv_projection():
     return UVProjectionLens()
 
 
+def cooke_abbe():
+    """The Cooke triplet prescription with AbbeMaterial model glasses (materials/abbe.py)
+    in place of its catalog glasses (SK16 ~ 1.62041 / 60.32, F2 ~ 1.62004 / 36.37)."""
+    from optiland.materials.abbe import AbbeMaterial
+
+    lens = ref_optic.Optic()
+    sk16 = AbbeMaterial(1.62041, 60.32)
+    f2 = AbbeMaterial(1.62004, 36.37)
+    lens.add_surface(index=0, radius=be.inf, thickness=be.inf)
+    lens.add_surface(index=1, radius=22.01359, thickness=3.25896, material=sk16)
+    lens.add_surface(index=2, radius=-435.76044, thickness=6.00755)
+    lens.add_surface(index=3, radius=-22.21328, thickness=0.99997, material=f2)
+    lens.add_surface(index=4, radius=20.29192, thickness=4.75041, is_stop=True)
+    lens.add_surface(index=5, radius=79.68360, thickness=2.95208, material=sk16)
+    lens.add_surface(index=6, radius=-18.39533, thickness=42.20778)
+    lens.add_surface(index=7)
+    lens.set_aperture(aperture_type="EPD", value=10)
+    lens.set_field_type(field_type="angle")
+    lens.add_field(y=0)
+    lens.add_field(y=14)
+    lens.add_field(y=20)
+    lens.add_wavelength(value=0.48)
+    lens.add_wavelength(value=0.55, is_primary=True)
+    lens.add_wavelength(value=0.65)
+    return lens
+
+
 def json_lens(name):
     """A lens file from the reference's docs/samples (copied as data to tests/golden/lenses),
     loaded with the reference's own Optic.from_dict (optic.py:674-713)."""
@@ -492,6 +519,7 @@ CASES = {
     "grating_tilted": (lambda: grating("curved", angle=0.35), [(0, 0), (0.2, 0.8)], [0.587],
                        "uniform", 24),
     "grid_lens": (grid_lens, [(0, 0), (0, 1), (0.6, 0.6)], [0.48, 0.55], "uniform", 24),
+    "cooke_abbe": (cooke_abbe, [(0, 0), (0, 1)], [0.48, 0.55, 0.65], "uniform", 24),
     "uv_projection": (uv_projection, [(0, 0), (0, 0.7), (0, 1)], [0.248], "uniform", 24),
     "apod_gaussian": (cooke_apod("GaussianApodization", sigma=0.6), [(0, 0), (0, 1)], [0.55],
                       "uniform", 24),
@@ -695,6 +723,34 @@ def glass_table():
         json.dump(out, f, indent=1)
 
 
+ABBE_GLASSES = [(1.5168, 64.17), (1.62, 36.37), (1.7552, 27.58), (1.4875, 70.4), (1.8, 46.5)]
+
+
+def abbe_table():
+    """Bake the AbbeMaterial model-glass fit (materials/abbe.py:67-98: the coefficient
+    matrix of database/glass_model_coefficients.npy, read without pickle) into
+    optiland_pr_amd/data/abbe_coefficients.json, with n(w) of a few (nd, vd) pairs on a
+    wavelength sweep as golden values."""
+    from optiland.materials.abbe import AbbeMaterial
+
+    import optiland
+
+    path = os.path.join(os.path.dirname(optiland.__file__), "database",
+                        "glass_model_coefficients.npy")
+    coef = np.load(path, allow_pickle=False)
+    sweep = np.linspace(0.38, 0.75, 38)
+    checks = []
+    for nd, vd in ABBE_GLASSES:
+        m = AbbeMaterial(nd, vd)
+        checks.append(dict(index=nd, abbe=vd, p=[float(v) for v in np.ravel(m._p)],
+                           n=[float(v) for v in np.ravel(m.n(sweep))],
+                           k=float(np.ravel(m.k(sweep))[0])))
+    out = dict(source="optiland/database/glass_model_coefficients.npy",
+               coefficients=coef.tolist(), check_wavelength=sweep.tolist(), checks=checks)
+    with open(os.path.join(REPO, "optiland_pr_amd", "data", "abbe_coefficients.json"), "w") as f:
+        json.dump(out, f, indent=1)
+
+
 def analysis_goldens():
     """SpotDiagram radii (tests/test_analysis.py:69-100 goldens) and OPD rms
     (tests/test_wavefront.py:135-139) recomputed from the reference."""
@@ -751,6 +807,7 @@ MIXED_W_CASES = {  # name -> (builder, field (Hx, Hy), pupil n, wavelength range
     "phase_plate": (phase_plate, (0.3, -0.6), 20, (0.45, 0.70)),
     "grating_curved": (lambda: grating("curved"), (0.2, 0.8), 20, (0.45, 0.70)),
     "grating_reflective": (lambda: grating("reflective"), (0.2, 0.8), 20, (0.45, 0.70)),
+    "cooke_abbe": (cooke_abbe, (0.0, 0.7), 24, (0.42, 0.74)),
 }
 
 
@@ -874,6 +931,9 @@ def main():
     if "--glasses" in sys.argv:  # re-bake optiland_pr_amd/data/glasses.json only
         glass_table()
         return
+    if "--abbe" in sys.argv:  # re-bake optiland_pr_amd/data/abbe_coefficients.json only
+        abbe_table()
+        return
     only = sys.argv[sys.argv.index("--only") + 1:] if "--only" in sys.argv else None
     if only:
         with open(os.path.join(HERE, "index.json")) as f:
@@ -885,6 +945,7 @@ def main():
             json.dump(index, f, indent=1)
         return
     glass_table()
+    abbe_table()
     index = {}
     for name, (builder, fields, wls, dist, num) in CASES.items():
         t0 = time.perf_counter()

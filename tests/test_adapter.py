@@ -51,7 +51,7 @@ def test_reference_lowering_equals_native(ref, name, wls):
                                   "cooke_aperture", "forbes", "forbes_q2d", "paraxial_lens",
                                   "paraxial_mirror", "phase_plate", "grating_flat",
                                   "grating_curved", "grating_reflective", "grating_tilted",
-                                  "grid_lens"])
+                                  "grid_lens", "cooke_abbe", "uv_projection"])
 def test_reference_lowering_equals_native_newton(ref, name):
     """Newton geometries (incl. the freeform kinds): the adapter's lowering of the
     reference lens equals the native lens's bytes, coefficient blocks included."""

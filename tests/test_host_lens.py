@@ -85,3 +85,41 @@ def test_surface_table_flags():
     t = lower_surface_group(lens.surface_group, [0.55])
     assert int(t.surfaces[2]["flags"]) & _abi.SURF_APERTURE
     assert t.surfaces[2]["ap_rmax2"] == 4.5**2
+
+
+def test_abbe_material_matches_reference():
+    """materials/abbe.py: the polynomial coefficients and n(w) of the baked model-glass
+    fit, against the reference's values (data/abbe_coefficients.json checks, written by
+    tests/golden/gen_golden.py --abbe); the range error and the lowered record."""
+    from types import SimpleNamespace
+
+    from oracle import trace_np
+    from optiland_pr_amd.materials import AbbeMaterial
+
+    d = json.load(open(os.path.join(REPO, "optiland_pr_amd", "data", "abbe_coefficients.json")))
+    w = np.array(d["check_wavelength"])
+    for c in d["checks"]:
+        m = AbbeMaterial(c["index"], c["abbe"])
+        np.testing.assert_array_equal(m._p, c["p"])
+        np.testing.assert_array_equal(m.n(w), c["n"])
+        assert np.all(m.k(w) == c["k"])
+        kind, cc, kw, kv, n_const, k_const = m.lower()
+        assert kind == _abi.MAT_ABBE and len(cc) == 4
+        rec = np.zeros(1, dtype=_abi.MATERIAL)
+        rec[0] = (kind, len(cc), 0, 0, 0, 0, n_const, k_const)
+        table = SimpleNamespace(mat_table=rec, coef=np.array(cc, dtype=np.float64))
+        np.testing.assert_array_equal(trace_np.material_n(table, 0, w), c["n"])
+    with pytest.raises(ValueError, match="Wavelength out of range for this model"):
+        AbbeMaterial(1.5, 60).n(0.8)
+    with pytest.raises(ValueError, match="Wavelength out of range for this model"):
+        AbbeMaterial(1.5, 60).n(np.array([0.5, 0.3]))
+
+
+def test_abbe_material_dict_round_trip():
+    from optiland_pr_amd.lensio import material_from_dict, material_to_dict
+    from optiland_pr_amd.materials import AbbeMaterial
+
+    m = material_from_dict(material_to_dict(AbbeMaterial(1.62, 36.37)))
+    assert isinstance(m, AbbeMaterial) and m.index[0] == 1.62 and m.abbe[0] == 36.37
+    with pytest.raises(ValueError, match="Missing required key: abbe"):
+        material_from_dict({"type": "AbbeMaterial", "index": 1.5})

@@ -19,7 +19,7 @@ from tests._cases import build_lens
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "mixed_w.npz")
 CASES = ("cooke", "dg", "freeform", "paraxial_lens", "phase_plate", "grating_curved",
-         "grating_reflective")
+         "grating_reflective", "cooke_abbe")
 
 
 def _golden():
