@@ -12,13 +12,17 @@ x, y, z, L, M, N, i, opd to HBM: exactly RealRayTracer.trace's work
 (real_ray_tracer.py:37-97) for one (field, wavelength) on 1M rays.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--rays R] [--no-cpu]
-                    [--config {2,3,4,5}]
+                    [--config {1,2,3,4,5}]
 
 N > 1: launched by torch.distributed.run, one process per GPU; every rank traces its
 own 1M-ray shard (weak scaling, no collective on the data path); the elapsed time is
 the max over ranks. value = N * R * S * K / time.
 
 The other BASELINE configs are secondary measurements, same JSON shape:
+  --config 1  Cooke triplet spot diagram (the reference's CPU-runnable case): 3 fields x
+              1 lambda x uniform 128 pupil grid (12,644 rays per field), one step = the
+              fused trace of the 3 pairs + the device spot statistics (ort_spot_stats:
+              centroid, rms and max radius per pair), replayed as one HIP graph
   --config 3  RT-asph (even aspheres, Newton sag): 5 fields x 3 lambda x 4M pupil rays
               (60M rays, one launch, one Newton group per (field, lambda))
   --config 4  ReverseTelephoto 7 fields x 7 lambda x 2M rays per pair (seed = pair),
@@ -81,6 +85,56 @@ def _pupil(seed, n, dev, torch):
     d.generate_points(n)
     return (torch.as_tensor(np.ascontiguousarray(d.x), device=dev),
             torch.as_tensor(np.ascontiguousarray(d.y), device=dev), d)
+
+
+def config1(args, dev, rank, world, torch):
+    from optiland_pr_amd.analysis import SpotStatistics
+    from optiland_pr_amd.lowering import segment_params
+    from optiland_pr_amd.pupil import pupil_arrays
+    from optiland_pr_amd.raytrace import RealRays, lens_for, trace_pupil, upload_segments
+    from optiland_pr_amd.samples import CookeTriplet
+
+    wl, fields = 0.55, [(0.0, 0.0), (0.0, 0.7), (0.0, 1.0)]
+    lens = CookeTriplet()
+    dl = lens_for(lens, [wl])
+    S = dl.table.n_surfaces
+    px, py = pupil_arrays("uniform", 128, dev)
+    n_p = px.numel()
+    seg_dev = upload_segments(np.stack([segment_params(lens, hx, hy, 0) for hx, hy in fields]),
+                              dev)
+    n = n_p * len(fields)
+    out = RealRays.empty(n, wl, device=dev)
+    img = lens.image_surface
+
+    spot = SpotStatistics(len(fields), 1, n_p, 0, img, dev)
+
+    def once():
+        trace_pupil(dl, seg_dev, px, py, out, n, n_p, n_p)
+        return spot.run(out)
+
+    once()  # closed-form lens: one launch, no host sync, no allocation -> capturable
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        stats = once()
+    state = {"stats": stats}
+
+    def step():
+        graph.replay()
+
+    return Workload(
+        metric="ray-surface intersections/sec, Cooke triplet spot diagram (3 fields x "
+               "uniform-128 pupil) incl. device spot statistics",
+        unit="intersections/s", units=world * n * S, step=step, scaling="weak",
+        config={"workload": "CookeTriplet (samples/objectives.py:46-72), fields Hy 0 / 0.7 / 1 "
+                            "(0 / 14 / 20 deg), lambda 0.55 um, uniform 128 (12,644 rays per "
+                            "field): fused trace of the 3 pairs + ort_spot_stats, one HIP "
+                            "graph replay per step",
+                "rays_per_gpu": n, "surfaces": S,
+                "parallelism": f"dp{world} (replicas, no collective)"},
+        kernel="trace_closed_kernel<F_GEN> + 4 spot-statistics kernels (graph)", launches=5,
+        bytes_per_launch=None, flops_per_ray=None, pmc_file=None, rays=n, state=state,
+        spot=True, data="synthetic (the reference's uniform 128 pupil grid)")
 
 
 def config2(args, dev, rank, world, torch):
@@ -240,7 +294,7 @@ def config5(args, dev, rank, world, torch):
         bytes_per_launch=None, flops_per_ray=None, pmc_file=None, rays=R, state=state)
 
 
-CONFIGS = {2: config2, 3: config3, 4: config4, 5: config5}
+CONFIGS = {1: config1, 2: config2, 3: config3, 4: config4, 5: config5}
 
 
 def main():
@@ -333,7 +387,7 @@ def main():
             "scaling": w.scaling,
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (random pupil rays, numpy default_rng seed = rank)",
+            "data": getattr(w, "data", "synthetic (random pupil rays, numpy default_rng seed = rank)"),
             "config": w.config,
             "roofline": _roofline(w, kern_ms),
             "timing": {"clock_ramp_s": args.ramp_seconds,
@@ -342,7 +396,11 @@ def main():
         }
         if w.flops_per_ray is not None:
             line["roofline_fp64"] = _roofline_fp64(w, kern_ms)
-        if getattr(w, "state", None):
+        if getattr(w, "spot", False):
+            st = w.state["stats"].cpu().numpy()
+            line["config"]["rms_spot_radius_mm"] = [float(v) for v in st[:, 3]]
+            line["config"]["geo_spot_radius_mm"] = [float(v) for v in st[:, 4]]
+        elif getattr(w, "state", None):
             loss = w.state.get("loss")
             line["config"]["final_loss"] = None if loss is None else float(loss)
         line["cpu_baseline"] = cpu_line
@@ -353,6 +411,11 @@ def main():
 
 
 def _roofline(w, kern_ms):
+    if getattr(w, "spot", False):
+        return {"bound": "launch", "achieved": None, "peak": None, "unit": None, "frac": None,
+                "traffic": None, "kernel": w.kernel, "step_device_ms": kern_ms,
+                "note": "38K rays per step: launch / latency bound (5 kernels in one graph); "
+                        "the per-intersection roofline is config 2's"}
     if w.bytes_per_launch is None:
         return {"bound": "fp64_valu", "achieved": None, "peak": SPEC_FP64_VEC_TFLOPS,
                 "unit": "TFLOP/s", "frac": None, "traffic": None, "kernel": w.kernel,
@@ -416,6 +479,11 @@ def _cpu_workload(args):
     from optiland_pr_amd.lowering import lower_surface_group, segment_params
     from optiland_pr_amd import samples
 
+    if args.config == 1:
+        lens = samples.CookeTriplet()
+        table = lower_surface_group(lens.surface_group, [0.55])
+        segs = np.stack([segment_params(lens, 0.0, h, 0) for h in (0.0, 0.7, 1.0)])
+        return table, segs, None, "Cooke (uniform 128)"
     if args.config == 2:
         lens = samples.DoubleGauss()
         table = lower_surface_group(lens.surface_group, [0.5876])
@@ -468,8 +536,15 @@ def _cpu_baseline(args):
     from optiland_pr_amd.distribution import RandomDistribution
 
     table, segs, n_rays, label = _cpu_workload(args)
-    d = RandomDistribution(seed=0)
-    d.generate_points(n_rays)
+    if n_rays is None:  # config 1: the uniform 128 grid of the reference's spot diagram
+        from optiland_pr_amd.distribution import create_distribution
+
+        d = create_distribution("uniform")
+        d.generate_points(128)
+        n_rays = int(np.asarray(d.x).size)
+    else:
+        d = RandomDistribution(seed=0)
+        d.generate_points(n_rays)
     px, py = np.asarray(d.x), np.asarray(d.y)
     _CPU["w"] = (table, segs, px, py)
     S = table.n_surfaces

@@ -544,6 +544,33 @@ int ort_generate_pupil(const ort_pupil* pupil, double* px, double* py, void* str
 int ort_material_nk(const ort_lens* lens, int32_t mat, const double* w, int64_t n,
                     double* n_out, double* k_out, void* stream);
 
+/* ---- spot-diagram statistics (analysis/spot_diagram.py:317-357, 425-437) ----------
+ * Traced rays laid out as n_fields x n_wl pairs of n_pupil consecutive rays
+ * (pair = field * n_wl + wavelength, the order SpotDiagram traces them in one launch).
+ * Points with i > 0 count (spot_diagram.py:425-427); their (x, y, z) are taken into the
+ * image-surface frame by local_ops (the surface's localize ops applied to points,
+ * visualization/system/utils.py:16-46; n_local_ops = 0: global coordinates). Per pair
+ * out[pair][5] = { count, centroid x, centroid y (mean of the pair's points),
+ * rms radius, max radius } with both radii about the centroid of the field's ref_wl
+ * pair (spot_diagram.py:_center_spots). NaN points propagate as in NumPy; a pair without
+ * points gives NaN statistics. Deterministic: fixed-order reductions, no atomics. */
+typedef struct ort_spot_layout {
+  int64_t n_pupil;            /* rays per pair                                        */
+  int32_t n_fields;
+  int32_t n_wl;               /* >= 1                                                 */
+  int32_t ref_wl;             /* the reference wavelength's index, 0 <= ref_wl < n_wl */
+  int32_t n_local_ops;
+  const ort_cs_op* local_ops; /* device [n_local_ops], or NULL when n_local_ops == 0   */
+} ort_spot_layout;
+
+/* Bytes of device workspace ort_spot_stats needs for this layout (< 0: ORT_ERR_ARG). */
+int64_t ort_spot_workspace_size(const ort_spot_layout* layout);
+
+/* rays: device x, y, z, i of n_fields * n_wl * n_pupil rays (other fields unused);
+ * out: device [n_fields * n_wl][5]. Four launches on `stream`, no synchronisation. */
+int ort_spot_stats(const ort_rays* rays, const ort_spot_layout* layout, void* workspace,
+                   int64_t workspace_size, double* out, void* stream);
+
 /* Ray generation only (ray_generator.py:28-106): fills rays_out from pupil points. */
 int ort_generate_rays(const double* px, const double* py, ort_rays* rays_out,
                       const ort_batch* batch, void* stream);

@@ -92,10 +92,21 @@ class ort_options(C.Structure):
     ]
 
 
+class ort_spot_layout(C.Structure):
+    _fields_ = [
+        ("n_pupil", C.c_int64),
+        ("n_fields", C.c_int32),
+        ("n_wl", C.c_int32),
+        ("ref_wl", C.c_int32),
+        ("n_local_ops", C.c_int32),
+        ("local_ops", C.c_void_p),
+    ]
+
+
 EXPORTS = ("ort_abi_version", "ort_trace_sequential", "ort_trace_pupil", "ort_trace_pupil_vjp",
            "ort_vjp_workspace_size", "ort_generate_pupil",
            "ort_surface_sag_normal", "ort_surface_distance", "ort_generate_rays",
-           "ort_material_nk")
+           "ort_material_nk", "ort_spot_workspace_size", "ort_spot_stats")
 
 _lib = None
 
@@ -149,6 +160,11 @@ def load(path: str | None = None):
     lib.ort_generate_rays.restype = C.c_int
     lib.ort_generate_rays.argtypes = [C.c_void_p, C.c_void_p, P(ort_rays), P(ort_batch),
                                       C.c_void_p]
+    lib.ort_spot_workspace_size.restype = C.c_int64
+    lib.ort_spot_workspace_size.argtypes = [P(ort_spot_layout)]
+    lib.ort_spot_stats.restype = C.c_int
+    lib.ort_spot_stats.argtypes = [P(ort_rays), P(ort_spot_layout), C.c_void_p, C.c_int64,
+                                   C.c_void_p, C.c_void_p]
     v = lib.ort_abi_version()
     if v != _abi.ABI_VERSION:
         raise NativeLibraryError(f"ABI version mismatch: library {v}, host {_abi.ABI_VERSION}")

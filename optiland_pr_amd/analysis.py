@@ -76,6 +76,59 @@ class SpotData:
     intensity: object
 
 
+class SpotStatistics:
+    """ort_spot_stats for a fixed layout: per (field, wavelength) pair of a pair-major
+    ray batch (n_pupil rays each) -> device tensor [n_fields * n_wl][5] = count,
+    centroid x, centroid y, rms radius, max radius; the radii about the centroid of the
+    field's ref_wl pair (spot_diagram.py:317-357), points with i > 0 (:425-427), taken
+    into `surface`'s frame when given (coordinates="local").
+
+    The constructor uploads the image frame's ops and allocates the workspace and the
+    output; run() only launches (four small kernels, no host sync, no allocation), so it
+    can be captured in a HIP graph."""
+
+    def __init__(self, n_fields, n_wl, n_pupil, ref_wl, surface=None, device=None):
+        import ctypes as C
+
+        from . import _native
+
+        self._lib = _native.load()
+        dev = device if device is not None else torch.device("cuda")
+        ops = surface.geometry.cs.localize_ops() if surface is not None else []
+        self._ops = None
+        if ops:
+            cs = np.zeros(len(ops), dtype=_abi.CS_OP)
+            for k, (kind, p) in enumerate(ops):
+                cs[k]["kind"] = kind
+                cs[k]["p"] = p
+            self._ops = torch.tensor(np.frombuffer(cs.tobytes(), dtype=np.uint8), device=dev)
+        self._lay = _native.ort_spot_layout(
+            int(n_pupil), int(n_fields), int(n_wl), int(ref_wl), len(ops),
+            None if self._ops is None else self._ops.data_ptr())
+        size = int(self._lib.ort_spot_workspace_size(C.byref(self._lay)))
+        _native.check(size if size < 0 else 0, "ort_spot_workspace_size")
+        self._size = size
+        self._ws = torch.empty(max(size, 8) // 8, dtype=torch.float64, device=dev)
+        self.out = torch.empty((n_fields * n_wl, 5), dtype=torch.float64, device=dev)
+
+    def run(self, rays):
+        import ctypes as C
+
+        from . import _native
+        from .raytrace import _stream_handle
+
+        rc = self._lib.ort_spot_stats(C.byref(rays.c_struct()), C.byref(self._lay),
+                                      C.c_void_p(self._ws.data_ptr()), self._size,
+                                      C.c_void_p(self.out.data_ptr()), _stream_handle())
+        _native.check(rc, "ort_spot_stats")
+        return self.out
+
+
+def spot_statistics(rays, n_fields, n_wl, n_pupil, ref_wl, surface=None):
+    """One-shot SpotStatistics(...).run(rays)."""
+    return SpotStatistics(n_fields, n_wl, n_pupil, ref_wl, surface, rays.x.device).run(rays)
+
+
 class SpotDiagram:
     """analysis/spot_diagram.py:40-438 (data generation + statistics; plotting is out
     of scope)."""
@@ -94,9 +147,13 @@ class SpotDiagram:
         primary = optic.primary_wavelength
         self._analysis_ref_wavelength_index = (
             self.wavelengths.index(primary) if primary in self.wavelengths else 0)
-        self.data = self._generate_data()
+        self._data = None
+        self._stats = None
+        self._trace()
 
-    def _generate_data(self):
+    def _trace(self):
+        """Every (field, wavelength) pair in ONE fused launch, then the statistics kernel
+        (ort_spot_stats) on the image rays: nothing is copied to the host here."""
         optic = self.optic
         for hx, hy in self.fields:  # real_ray_tracer.py:59 validation
             if not (-1 <= hx <= 1 and -1 <= hy <= 1):
@@ -114,9 +171,25 @@ class SpotDiagram:
                 for hx, hy in self.fields for w in self.wavelengths]
         trace_pupil(dl, segs, px, py, out, n, n_p, n_p, keys=keys, newton_mode=self.newton_mode)
         self.rays = out
+        self._n_p = n_p
+        self._stats = spot_statistics(
+            out, len(self.fields), len(self.wavelengths), n_p,
+            self._analysis_ref_wavelength_index,
+            optic.image_surface if self.coordinates == "local" else None)
+
+    @property
+    def data(self):
+        """spot_diagram.py:381-438: [field][wavelength] SpotData of the i > 0 points
+        (device tensors, built on first use: boolean masking synchronises)."""
+        if self._data is None:
+            self._data = self._generate_data()
+        return self._data
+
+    def _generate_data(self):
+        out, n_p = self.rays, self._n_p
         data = []
         k = 0
-        img = optic.image_surface
+        img = self.optic.image_surface
         for _ in self.fields:
             row = []
             for _ in self.wavelengths:
@@ -131,22 +204,29 @@ class SpotDiagram:
             data.append(row)
         return data
 
-    # -- statistics (spot_diagram.py:317-379) --
-    def centroid(self):
-        ref = self._analysis_ref_wavelength_index
-        return [(torch.mean(f[ref].x), torch.mean(f[ref].y)) for f in self.data]
+    # -- statistics (spot_diagram.py:317-379), from the device statistics kernel --
+    def _stat(self, col):
+        nw = len(self.wavelengths)
+        st = self._stats
+        return [[st[f * nw + w, col] for w in range(nw)] for f in range(len(self.fields))]
 
-    def _center_spots(self):
-        out = []
-        for (cx, cy), fl in zip(self.centroid(), self.data, strict=True):
-            out.append([SpotData(x=sd.x - cx, y=sd.y - cy, intensity=sd.intensity) for sd in fl])
-        return out
+    def centroid(self):
+        """Centroid of each field's reference-wavelength spot (spot_diagram.py:317-328)."""
+        ref = self._analysis_ref_wavelength_index
+        nw = len(self.wavelengths)
+        st = self._stats
+        return [(st[f * nw + ref, 1], st[f * nw + ref, 2]) for f in range(len(self.fields))]
 
     def geometric_spot_radius(self):
-        return [[torch.max(torch.sqrt(w.x**2 + w.y**2)) for w in f] for f in self._center_spots()]
+        """spot_diagram.py:330-343 (be.max over an empty spot raises, as NumPy does)."""
+        if bool((self._stats[:, 0] == 0).any()):
+            raise ValueError("zero-size array to reduction operation maximum which has no "
+                             "identity")
+        return self._stat(4)
 
     def rms_spot_radius(self):
-        return [[torch.sqrt(torch.mean(w.x**2 + w.y**2)) for w in f] for f in self._center_spots()]
+        """spot_diagram.py:345-357."""
+        return self._stat(3)
 
 
 # --------------------------------------------------------------------------------------

@@ -27,6 +27,7 @@ STRUCTS = {
     "ort_options": (None, _native.ort_options),
     "ort_vjp_params": (None, _native.ort_vjp_params),
     "ort_pupil": (None, _native.ort_pupil),
+    "ort_spot_layout": (None, _native.ort_spot_layout),
 }
 
 
