@@ -132,7 +132,7 @@ def config1(args, dev, rank, world, torch):
                             "graph replay per step",
                 "rays_per_gpu": n, "surfaces": S,
                 "parallelism": f"dp{world} (replicas, no collective)"},
-        kernel="trace_closed_kernel<F_GEN> + 4 spot-statistics kernels (graph)", launches=5,
+        kernel="trace_closed_kernel<F_GEN> + 3 spot-statistics kernels (graph)", launches=4,
         bytes_per_launch=None, flops_per_ray=None, pmc_file=None, rays=n, state=state,
         spot=True, data="synthetic (the reference's uniform 128 pupil grid)")
 
@@ -414,7 +414,7 @@ def _roofline(w, kern_ms):
     if getattr(w, "spot", False):
         return {"bound": "launch", "achieved": None, "peak": None, "unit": None, "frac": None,
                 "traffic": None, "kernel": w.kernel, "step_device_ms": kern_ms,
-                "note": "38K rays per step: launch / latency bound (5 kernels in one graph); "
+                "note": "38K rays per step: launch / latency bound (4 kernels in one graph); "
                         "the per-intersection roofline is config 2's"}
     if w.bytes_per_launch is None:
         return {"bound": "fp64_valu", "achieved": None, "peak": SPEC_FP64_VEC_TFLOPS,

@@ -553,7 +553,8 @@ int ort_material_nk(const ort_lens* lens, int32_t mat, const double* w, int64_t 
  * out[pair][5] = { count, centroid x, centroid y (mean of the pair's points),
  * rms radius, max radius } with both radii about the centroid of the field's ref_wl
  * pair (spot_diagram.py:_center_spots). NaN points propagate as in NumPy; a pair without
- * points gives NaN statistics. Deterministic: fixed-order reductions, no atomics. */
+ * points gives NaN statistics. Deterministic: every reduction runs in a fixed order,
+ * no atomics. */
 typedef struct ort_spot_layout {
   int64_t n_pupil;            /* rays per pair                                        */
   int32_t n_fields;
@@ -566,8 +567,9 @@ typedef struct ort_spot_layout {
 /* Bytes of device workspace ort_spot_stats needs for this layout (< 0: ORT_ERR_ARG). */
 int64_t ort_spot_workspace_size(const ort_spot_layout* layout);
 
-/* rays: device x, y, z, i of n_fields * n_wl * n_pupil rays (other fields unused);
- * out: device [n_fields * n_wl][5]. Four launches on `stream`, no synchronisation. */
+/* rays: device x, y, z, i of n_fields * n_wl * n_pupil rays (other fields unused; z
+ * only with local_ops); out: device [n_fields * n_wl][5]. Three launches on `stream`,
+ * no synchronisation, no allocation (graph-capturable). */
 int ort_spot_stats(const ort_rays* rays, const ort_spot_layout* layout, void* workspace,
                    int64_t workspace_size, double* out, void* stream);
 

@@ -3,12 +3,18 @@
 // the image surface frame), so a SpotDiagram's numbers leave HBM as a few doubles per
 // (field, wavelength) pair instead of as masked ray arrays.
 //
-// Two passes, each a partial-sum kernel over fixed 2048-ray chunks of one pair followed
-// by a one-block-per-pair kernel that reduces the chunk partials in index order: the
-// result is deterministic (bit-identical run to run). Pass 1: count, sum x, sum y ->
-// centroids; pass 2: sum and max of (x - cx)^2 + (y - cy)^2 about the centroid of the
-// field's reference-wavelength pair. NaN points propagate as in NumPy (the sums carry
-// them; the max takes an explicit NaN flag, since fmax would drop it).
+// Two kernels over fixed chunks of one pair (<= 256 chunks per pair: one ray per thread
+// for a small spot diagram, so it still spreads over many CUs, several for a large one):
+//   spot_sum_kernel    count, sum x, sum y of the chunk -> part1[pair][chunk]
+//   spot_dev_kernel    the centroid of the field's reference-wavelength pair, reduced by
+//                      every block from part1 in index order (<= 768 doubles,
+//                      L2-resident), then sum and max of (x - cx)^2 + (y - cy)^2 over the
+//                      chunk -> part2[pair][chunk]
+//   spot_final_kernel  one block per pair: the pair's partials in index order -> out[pair]
+// Every reduction runs in a fixed order, so the result is bit-identical run to run (no
+// atomics: kernel boundaries order the passes, no cross-block fence). NaN points
+// propagate as in NumPy (the sums carry them; the max keeps an explicit NaN flag, since
+// fmax would drop it).
 
 #include "ort_kernels.h"
 
@@ -16,8 +22,8 @@ namespace ortk {
 namespace {
 
 constexpr int kSpotThreads = 256;
-constexpr int kSpotPerThread = 8;
-constexpr int64_t kSpotChunk = (int64_t)kSpotThreads * kSpotPerThread;
+constexpr int64_t kSpotMaxChunks = 256;  // chunks per pair at most: a chunk is 256 rays
+                                         // times ceil(n_pupil / (256 * 256)) per thread
 
 struct SpotArgs {
   const double* x;
@@ -29,10 +35,11 @@ struct SpotArgs {
   int32_t ref_wl;
   int32_t n_ops;
   const ort_cs_op* ops;
-  int32_t n_chunks;  // chunks per pair
-  double* part;      // [n_pairs][n_chunks][3]
-  double* cent;      // [n_pairs][2]
-  double* out;       // [n_pairs][5]
+  int32_t n_chunks;     // chunks per pair
+  int32_t per_thread;   // rays per thread (chunk = per_thread * 256 rays)
+  double* part1;        // [n_pairs][n_chunks][3]: count, sum x, sum y
+  double* part2;        // [n_pairs][n_chunks][3]: sum r^2, max r, NaN flag
+  double* out;          // [n_pairs][5]
 };
 
 // one image point in the surface frame (visualization/system/utils.py:16-46: the point
@@ -41,19 +48,30 @@ __device__ inline void local_point(const SpotArgs& a, int64_t r, double& x, doub
   ort::Ray p;
   p.x = a.x[r];
   p.y = a.y[r];
-  p.z = a.z[r];
+  p.z = a.n_ops ? a.z[r] : 0.0;
   p.L = 0.0; p.M = 0.0; p.N = 0.0;
   for (int k = 0; k < a.n_ops; ++k) ort::apply_cs_op(p, cst(a.ops)[k]);
   x = p.x;
   y = p.y;
 }
 
+__device__ inline double wave_sum(double v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ inline double wave_max(double v) {
+  for (int o = 32; o > 0; o >>= 1) v = ::fmax(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// block-wide sums of NV values (fixed order: lanes by xor butterfly, then waves 0..3);
+// every thread gets the totals. lds: >= 4 * NV doubles
 template <int NV>
 __device__ inline void block_sum(double (&v)[NV], double* lds) {
 #pragma unroll
-  for (int k = 0; k < NV; ++k)
-    for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o, 64);
+  for (int k = 0; k < NV; ++k) v[k] = wave_sum(v[k]);
   const int w = threadIdx.x >> 6;
+  __syncthreads();
   if ((threadIdx.x & 63) == 0)
 #pragma unroll
     for (int k = 0; k < NV; ++k) lds[w * NV + k] = v[k];
@@ -66,129 +84,126 @@ __device__ inline void block_sum(double (&v)[NV], double* lds) {
   }
 }
 
-// pass 1 / 2 partials of one chunk
-template <int PASS>
-__global__ __launch_bounds__(kSpotThreads) void spot_partial_kernel(const SpotArgs a) {
-  const int64_t pair = blockIdx.y;
-  const int64_t c0 = (int64_t)blockIdx.x * kSpotChunk;
-  const int64_t base = pair * a.n_pupil;
-  double v[3] = {0.0, 0.0, 0.0};
-  double cx = 0.0, cy = 0.0;
-  if (PASS == 2) {
-    const int64_t ref = (pair / a.n_wl) * a.n_wl + a.ref_wl;
-    cx = a.cent[ref * 2 + 0];
-    cy = a.cent[ref * 2 + 1];
+// sums of the 3 columns of part[0 .. n) (index-strided per thread, then block_sum)
+__device__ inline void reduce_rows(const double* part, int n, double (&v)[3], double* lds) {
+  v[0] = v[1] = v[2] = 0.0;
+  for (int c = threadIdx.x; c < n; c += kSpotThreads) {
+    v[0] += part[c * 3 + 0];
+    v[1] += part[c * 3 + 1];
+    v[2] += part[c * 3 + 2];
   }
-  for (int k = 0; k < kSpotPerThread; ++k) {
-    const int64_t j = c0 + (int64_t)k * kSpotThreads + threadIdx.x;
+  block_sum<3>(v, lds);
+}
+
+__global__ __launch_bounds__(kSpotThreads) void spot_sum_kernel(const SpotArgs a) {
+  const int64_t pair = blockIdx.y;
+  const int64_t j0 = (int64_t)blockIdx.x * a.per_thread * kSpotThreads + threadIdx.x;
+  double v[3] = {0.0, 0.0, 0.0};
+  for (int k = 0; k < a.per_thread; ++k) {
+    const int64_t j = j0 + (int64_t)k * kSpotThreads;
     if (j >= a.n_pupil) break;
-    const int64_t r = base + j;
-    if (!(a.i[r] > 0.0)) continue;  // spot_diagram.py:425-427
-    double x, y;
-    local_point(a, r, x, y);
-    if (PASS == 1) {
+    const int64_t r = pair * a.n_pupil + j;
+    if (a.i[r] > 0.0) {  // spot_diagram.py:425-427
+      double x, y;
+      local_point(a, r, x, y);
       v[0] += 1.0;
       v[1] += x;
       v[2] += y;
-    } else {
-      const double dx = x - cx, dy = y - cy;
-      const double r2 = dx * dx + dy * dy;  // x**2 + y**2 of the centred spot
-      v[0] += r2;
-      const double rad = ::sqrt(r2);
-      if (rad != rad) v[2] = 1.0;  // NaN seen
-      else if (rad > v[1]) v[1] = rad;
     }
   }
-  __shared__ double lds[(kSpotThreads / 64) * 3];
-  if (PASS == 1) {
-    block_sum<3>(v, lds);
-  } else {
-    double s[1] = {v[0]};
-    block_sum<1>(s, lds);
-    __syncthreads();
-    // max and NaN flag: wave then block maximum (order-independent)
-    double m = v[1], f = v[2];
-    for (int o = 32; o > 0; o >>= 1) {
-      m = ::fmax(m, __shfl_xor(m, o, 64));
-      f = ::fmax(f, __shfl_xor(f, o, 64));
-    }
-    const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) {
-      lds[w * 2 + 0] = m;
-      lds[w * 2 + 1] = f;
-    }
-    __syncthreads();
-    m = 0.0;
-    f = 0.0;
-    for (int ww = 0; ww < kSpotThreads / 64; ++ww) {
-      m = ::fmax(m, lds[ww * 2 + 0]);
-      f = ::fmax(f, lds[ww * 2 + 1]);
-    }
-    v[0] = s[0];
-    v[1] = m;
-    v[2] = f;
-  }
+  __shared__ double lds[4 * 3];
+  block_sum<3>(v, lds);
   if (threadIdx.x == 0) {
-    double* p = a.part + (pair * a.n_chunks + blockIdx.x) * 3;
+    double* p = a.part1 + (pair * a.n_chunks + blockIdx.x) * 3;
     p[0] = v[0];
     p[1] = v[1];
     p[2] = v[2];
   }
 }
 
-// reduce the chunk partials of one pair in index order
-template <int PASS>
+__global__ __launch_bounds__(kSpotThreads) void spot_dev_kernel(const SpotArgs a) {
+  const int64_t pair = blockIdx.y;
+  __shared__ double lds[4 * 3];
+  // centroid of the field's reference-wavelength spot (spot_diagram.py:317-328)
+  const int64_t ref = (pair / a.n_wl) * a.n_wl + a.ref_wl;
+  double c[3];
+  reduce_rows(a.part1 + ref * a.n_chunks * 3, a.n_chunks, c, lds);
+  const double cx = c[1] / c[0], cy = c[2] / c[0];
+
+  const int64_t j0 = (int64_t)blockIdx.x * a.per_thread * kSpotThreads + threadIdx.x;
+  double s = 0.0, m = 0.0, f = 0.0;
+  for (int k = 0; k < a.per_thread; ++k) {
+    const int64_t j = j0 + (int64_t)k * kSpotThreads;
+    if (j >= a.n_pupil) break;
+    const int64_t r = pair * a.n_pupil + j;
+    if (a.i[r] > 0.0) {
+      double x, y;
+      local_point(a, r, x, y);
+      const double dx = x - cx, dy = y - cy;
+      const double r2 = dx * dx + dy * dy;  // x**2 + y**2 of the centred spot
+      s += r2;
+      const double rad = ::sqrt(r2);
+      if (rad != rad) f = 1.0;  // NaN seen
+      else m = ::fmax(m, rad);
+    }
+  }
+  double v[1] = {s};
+  block_sum<1>(v, lds);
+  m = wave_max(m);
+  f = wave_max(f);
+  __shared__ double mx[4][2];
+  if ((threadIdx.x & 63) == 0) {
+    mx[threadIdx.x >> 6][0] = m;
+    mx[threadIdx.x >> 6][1] = f;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < kSpotThreads / 64; ++w) {
+      m = ::fmax(m, mx[w][0]);
+      f = ::fmax(f, mx[w][1]);
+    }
+    double* p = a.part2 + (pair * a.n_chunks + blockIdx.x) * 3;
+    p[0] = v[0];
+    p[1] = m;
+    p[2] = f;
+  }
+}
+
+// one block per pair: the pair's totals, every reduction in index order
 __global__ __launch_bounds__(kSpotThreads) void spot_final_kernel(const SpotArgs a) {
   const int64_t pair = blockIdx.x;
-  const double* p = a.part + pair * a.n_chunks * 3;
-  __shared__ double lds[(kSpotThreads / 64) * 3];
-  if (PASS == 1) {
-    double v[3] = {0.0, 0.0, 0.0};
-    for (int c = threadIdx.x; c < a.n_chunks; c += kSpotThreads) {
-      v[0] += p[c * 3 + 0];
-      v[1] += p[c * 3 + 1];
-      v[2] += p[c * 3 + 2];
+  __shared__ double lds[4 * 3];
+  __shared__ double mx[4][2];
+  double own[3];
+  reduce_rows(a.part1 + pair * a.n_chunks * 3, a.n_chunks, own, lds);
+  const double* p2 = a.part2 + pair * a.n_chunks * 3;
+  double t[1] = {0.0};
+  double m = 0.0, f = 0.0;
+  for (int k = threadIdx.x; k < a.n_chunks; k += kSpotThreads) {
+    t[0] += p2[k * 3 + 0];
+    m = ::fmax(m, p2[k * 3 + 1]);
+    f = ::fmax(f, p2[k * 3 + 2]);
+  }
+  block_sum<1>(t, lds);
+  m = wave_max(m);
+  f = wave_max(f);
+  if ((threadIdx.x & 63) == 0) {
+    mx[threadIdx.x >> 6][0] = m;
+    mx[threadIdx.x >> 6][1] = f;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < kSpotThreads / 64; ++w) {
+      m = ::fmax(m, mx[w][0]);
+      f = ::fmax(f, mx[w][1]);
     }
-    block_sum<3>(v, lds);
-    if (threadIdx.x == 0) {
-      const double n = v[0];
-      const double cx = v[1] / n, cy = v[2] / n;  // be.mean: sum / count (0 / 0 = NaN)
-      a.cent[pair * 2 + 0] = cx;
-      a.cent[pair * 2 + 1] = cy;
-      a.out[pair * 5 + 0] = n;
-      a.out[pair * 5 + 1] = cx;
-      a.out[pair * 5 + 2] = cy;
-    }
-  } else {
-    double s[1] = {0.0};
-    double m = 0.0, f = 0.0;
-    for (int c = threadIdx.x; c < a.n_chunks; c += kSpotThreads) {
-      s[0] += p[c * 3 + 0];
-      m = ::fmax(m, p[c * 3 + 1]);
-      f = ::fmax(f, p[c * 3 + 2]);
-    }
-    block_sum<1>(s, lds);
-    __syncthreads();
-    for (int o = 32; o > 0; o >>= 1) {
-      m = ::fmax(m, __shfl_xor(m, o, 64));
-      f = ::fmax(f, __shfl_xor(f, o, 64));
-    }
-    const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) {
-      lds[w * 2 + 0] = m;
-      lds[w * 2 + 1] = f;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      for (int ww = 0; ww < kSpotThreads / 64; ++ww) {
-        m = ::fmax(m, lds[ww * 2 + 0]);
-        f = ::fmax(f, lds[ww * 2 + 1]);
-      }
-      const double n = a.out[pair * 5 + 0];
-      const bool nan = f != 0.0 || s[0] != s[0];
-      a.out[pair * 5 + 3] = ::sqrt(s[0] / n);  // be.sqrt(be.mean(x**2 + y**2))
-      a.out[pair * 5 + 4] = (nan || n == 0.0) ? __builtin_nan("") : m;  // be.max
-    }
+    const double n = own[0];
+    double* o = a.out + pair * 5;
+    o[0] = n;
+    o[1] = own[1] / n;  // be.mean: sum / count (0 / 0 = NaN)
+    o[2] = own[2] / n;
+    o[3] = ::sqrt(t[0] / n);  // be.sqrt(be.mean(x**2 + y**2))
+    o[4] = (f != 0.0 || t[0] != t[0] || n == 0.0) ? __builtin_nan("") : m;  // be.max
   }
 }
 
@@ -199,11 +214,19 @@ using namespace ortk;
 
 extern "C" {
 
+static int64_t spot_per_thread(const ort_spot_layout* lay) {
+  const int64_t cap = kSpotMaxChunks * kSpotThreads;
+  return lay->n_pupil > cap ? (lay->n_pupil + cap - 1) / cap : 1;
+}
+static int64_t spot_chunks(const ort_spot_layout* lay) {
+  const int64_t chunk = spot_per_thread(lay) * kSpotThreads;
+  return lay->n_pupil > 0 ? (lay->n_pupil + chunk - 1) / chunk : 1;
+}
+
 int64_t ort_spot_workspace_size(const ort_spot_layout* lay) {
   if (!lay || lay->n_pupil < 0 || lay->n_fields < 0 || lay->n_wl < 1) return ORT_ERR_ARG;
   const int64_t pairs = (int64_t)lay->n_fields * lay->n_wl;
-  const int64_t chunks = lay->n_pupil > 0 ? (lay->n_pupil + kSpotChunk - 1) / kSpotChunk : 1;
-  return (pairs * chunks * 3 + pairs * 2) * (int64_t)sizeof(double);
+  return pairs * spot_chunks(lay) * 3 * 2 * (int64_t)sizeof(double);
 }
 
 int ort_spot_stats(const ort_rays* rays, const ort_spot_layout* lay, void* workspace,
@@ -216,9 +239,10 @@ int ort_spot_stats(const ort_rays* rays, const ort_spot_layout* lay, void* works
   const int64_t pairs = (int64_t)lay->n_fields * lay->n_wl;
   if (pairs == 0) return ORT_OK;
   if (!workspace || workspace_size < need) return ORT_ERR_ARG;
-  if (lay->n_pupil > 0 && (!rays->x || !rays->y || !rays->z || !rays->i)) return ORT_ERR_ARG;
-  const int64_t chunks = lay->n_pupil > 0 ? (lay->n_pupil + kSpotChunk - 1) / kSpotChunk : 1;
-  if (chunks > 0x7fffffff || pairs > 65535) return ORT_ERR_ARG;
+  if (lay->n_pupil > 0 && (!rays->x || !rays->y || !rays->i)) return ORT_ERR_ARG;
+  if (lay->n_pupil > 0 && lay->n_local_ops > 0 && !rays->z) return ORT_ERR_ARG;
+  const int64_t chunks = spot_chunks(lay);
+  if (spot_per_thread(lay) > 0x7fffffff || pairs > 65535) return ORT_ERR_ARG;
   SpotArgs a{};
   a.x = rays->x;
   a.y = rays->y;
@@ -230,15 +254,15 @@ int ort_spot_stats(const ort_rays* rays, const ort_spot_layout* lay, void* works
   a.n_ops = lay->n_local_ops;
   a.ops = lay->local_ops;
   a.n_chunks = (int32_t)chunks;
-  a.part = (double*)workspace;
-  a.cent = a.part + pairs * chunks * 3;
+  a.per_thread = (int32_t)spot_per_thread(lay);
+  a.part1 = (double*)workspace;
+  a.part2 = a.part1 + pairs * chunks * 3;
   a.out = out;
   hipStream_t s = (hipStream_t)stream;
-  const dim3 grid((unsigned)chunks, (unsigned)pairs);
-  hipLaunchKernelGGL(spot_partial_kernel<1>, grid, dim3(kSpotThreads), 0, s, a);
-  hipLaunchKernelGGL(spot_final_kernel<1>, dim3((unsigned)pairs), dim3(kSpotThreads), 0, s, a);
-  hipLaunchKernelGGL(spot_partial_kernel<2>, grid, dim3(kSpotThreads), 0, s, a);
-  hipLaunchKernelGGL(spot_final_kernel<2>, dim3((unsigned)pairs), dim3(kSpotThreads), 0, s, a);
+  const dim3 grid((unsigned)chunks, (unsigned)pairs);  // n_pupil == 0: one empty chunk
+  hipLaunchKernelGGL(spot_sum_kernel, grid, dim3(kSpotThreads), 0, s, a);
+  hipLaunchKernelGGL(spot_dev_kernel, grid, dim3(kSpotThreads), 0, s, a);
+  hipLaunchKernelGGL(spot_final_kernel, dim3((unsigned)pairs), dim3(kSpotThreads), 0, s, a);
   return hipGetLastError() == hipSuccess ? ORT_OK : ORT_ERR_LAUNCH;
 }
 
