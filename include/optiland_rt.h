@@ -573,6 +573,41 @@ int64_t ort_spot_workspace_size(const ort_spot_layout* layout);
 int ort_spot_stats(const ort_rays* rays, const ort_spot_layout* layout, void* workspace,
                    int64_t workspace_size, double* out, void* stream);
 
+/* ---- chief-ray wavefront (wavefront/strategy.py:68-239, opd.py:143-157) ------------
+ * Host-formed constants of one (field, wavelength): the reference sphere centred on the
+ * chief ray's image point (xc, yc, zc) with r2 = R**2 (R from the chief ray and the exit
+ * pupil, strategy.py:236-241), the image-space index, the chief ray's own reference OPD
+ * opd_ref (after its tilt correction), and for angle fields (tilt = 1) the launch-plane
+ * tilt direction (ux, uy) and EPD (:118-166). xc2 / yc2 / zc2 = xc**2 ... as NumPy forms
+ * them; wl_mm = wavelength * 1e-3. */
+typedef struct ort_wavefront_ref {
+  double xc, yc, zc;
+  double xc2, yc2, zc2;
+  double r2;
+  double n_image;
+  double opd_ref;
+  double ux, uy;
+  double epd;
+  double wl_mm;
+  int32_t tilt;
+  int32_t reserved;
+} ort_wavefront_ref; /* 112 bytes */
+
+/* Bytes of device workspace ort_wavefront_opd needs for n rays (< 0: ORT_ERR_ARG). */
+int64_t ort_wavefront_workspace_size(int64_t n);
+
+/* rays: the n traced rays at the image (device x, y, z, L, M, N, i, opd); px, py: their
+ * pupil coordinates (device, read only when ref->tilt). Writes opd_wv[n] (OPD in waves,
+ * strategy.py:226) and, when non-NULL, the exit-pupil points pupil_x / y / z[n]
+ * (:227-230), and sums[11] (device): count and sum of opd_wv^2 over i > 0 (opd.py rms)
+ * and the intensity-weighted sums w, wx, wy, wxx, wxy, wyy, w opd, wx opd, wy opd of the
+ * pupil points for the piston / tilt fit (wavefront.py:97-143). Two launches on
+ * `stream`, fixed-order reductions, no synchronisation. */
+int ort_wavefront_opd(const ort_rays* rays, const double* px, const double* py, int64_t n,
+                      const ort_wavefront_ref* ref, double* opd_wv, double* pupil_x,
+                      double* pupil_y, double* pupil_z, void* workspace,
+                      int64_t workspace_size, double* sums, void* stream);
+
 /* Ray generation only (ray_generator.py:28-106): fills rays_out from pupil points. */
 int ort_generate_rays(const double* px, const double* py, ort_rays* rays_out,
                       const ort_batch* batch, void* stream);

@@ -103,10 +103,17 @@ class ort_spot_layout(C.Structure):
     ]
 
 
+class ort_wavefront_ref(C.Structure):
+    _fields_ = [(f, C.c_double) for f in ("xc", "yc", "zc", "xc2", "yc2", "zc2", "r2",
+                                          "n_image", "opd_ref", "ux", "uy", "epd", "wl_mm")]
+    _fields_ += [("tilt", C.c_int32), ("reserved", C.c_int32)]
+
+
 EXPORTS = ("ort_abi_version", "ort_trace_sequential", "ort_trace_pupil", "ort_trace_pupil_vjp",
            "ort_vjp_workspace_size", "ort_generate_pupil",
            "ort_surface_sag_normal", "ort_surface_distance", "ort_generate_rays",
-           "ort_material_nk", "ort_spot_workspace_size", "ort_spot_stats")
+           "ort_material_nk", "ort_spot_workspace_size", "ort_spot_stats",
+           "ort_wavefront_workspace_size", "ort_wavefront_opd")
 
 _lib = None
 
@@ -165,6 +172,13 @@ def load(path: str | None = None):
     lib.ort_spot_stats.restype = C.c_int
     lib.ort_spot_stats.argtypes = [P(ort_rays), P(ort_spot_layout), C.c_void_p, C.c_int64,
                                    C.c_void_p, C.c_void_p]
+    lib.ort_wavefront_workspace_size.restype = C.c_int64
+    lib.ort_wavefront_workspace_size.argtypes = [C.c_int64]
+    lib.ort_wavefront_opd.restype = C.c_int
+    lib.ort_wavefront_opd.argtypes = [P(ort_rays), C.c_void_p, C.c_void_p, C.c_int64,
+                                      P(ort_wavefront_ref), C.c_void_p, C.c_void_p,
+                                      C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64,
+                                      C.c_void_p, C.c_void_p]
     v = lib.ort_abi_version()
     if v != _abi.ABI_VERSION:
         raise NativeLibraryError(f"ABI version mismatch: library {v}, host {_abi.ABI_VERSION}")

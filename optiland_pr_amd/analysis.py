@@ -4,9 +4,10 @@ wavefront/strategy.py:68-239, wavefront/opd.py:71-157).
 
 MI355X-first: SpotDiagram traces EVERY (field, wavelength) pair of the analysis in one
 fused launch (each pair its own Newton group = one reference Optic.trace call) and
-reduces centroid / RMS / max radius on the device; only the statistics leave HBM.
-The elementwise post-processing uses torch ops on the device (one IEEE operation each,
-in the reference's order); reductions differ from NumPy's pairwise order by ulps.
+reduces centroid / RMS / max radius on the device (ort_spot_stats); the wavefront's
+per-ray OPD, exit-pupil points, rms and tilt-fit sums are one fused kernel
+(ort_wavefront_opd) in the reference's operation order. Only statistics leave HBM;
+reductions run in a fixed order that differs from NumPy's pairwise sums by ulps.
 """
 
 from __future__ import annotations
@@ -243,7 +244,11 @@ class WavefrontData:
 
 
 class ChiefRayStrategy:
-    """wavefront/strategy.py:168-239."""
+    """wavefront/strategy.py:168-239 on the device: the chief ray and the full ray set
+    are traced by the HIP kernels; the chief ray's reference sphere is formed on the
+    host from its 7 doubles (the reference reads R with .item() too), and the per-ray
+    OPD, exit-pupil points, rms and tilt-fit sums come from one fused kernel
+    (ort_wavefront_opd) instead of a chain of elementwise array operations."""
 
     def __init__(self, optic, distribution):
         self.optic = optic
@@ -251,64 +256,101 @@ class ChiefRayStrategy:
         self.n_image = optic.n()[-1]
         self.pupil_z = optic.paraxial.XPL() + optic.surface_group.positions[-1]
 
-    def _opd_image_to_xp(self, rays, xc, yc, zc, R):
-        """strategy.py:68-116: ray to reference-sphere distance from the image plane."""
-        xr, yr, zr = rays.x, rays.y, rays.z
-        L, M, N = -rays.L, -rays.M, -rays.N
+    # -- host restatements for the single chief ray (NumPy, the reference's order) --
+    def _opd_image_to_xp_np(self, c, xc, yc, zc, R):
+        """strategy.py:68-116 on the chief ray's 1-element arrays."""
+        xr, yr, zr = c["x"], c["y"], c["z"]
+        L, M, N = -c["L"], -c["M"], -c["N"]
         a = L**2 + M**2 + N**2
         b = 2 * (L * (xr - xc) + M * (yr - yc) + N * (zr - zc))
-        c = (xr**2 + yr**2 + zr**2 - 2 * (xr * xc + yr * yc + zr * zc)
-             + xc**2 + yc**2 + zc**2 - R**2)
-        d = b**2 - 4 * a * c
-        d = torch.where(d < 0, torch.zeros_like(d), d)
-        t = (-b - torch.sqrt(d)) / (2 * a)
-        mask = t < 0
-        t = torch.where(mask, (-b + torch.sqrt(d)) / (2 * a), t)
+        cc = (xr**2 + yr**2 + zr**2 - 2 * (xr * xc + yr * yc + zr * zc)
+              + xc**2 + yc**2 + zc**2 - R**2)
+        d = b**2 - 4 * a * cc
+        d = np.where(d < 0, 0, d)
+        with np.errstate(invalid="ignore", divide="ignore"):
+            t = (-b - np.sqrt(d)) / (2 * a)
+            t = np.where(t < 0, (-b + np.sqrt(d)) / (2 * a), t)
         return self.n_image * t
 
-    def _correct_tilt(self, field, opd, x=None, y=None):
-        """strategy.py:118-166 (angle fields only)."""
+    def _tilt_direction(self, field):
+        """strategy.py:141-153: (ux, uy) of an angle field, None otherwise."""
         if self.optic.field_type != "angle":
-            return opd
+            return None
         hx, hy = field
         max_field_deg = self.optic.fields.max_field
-        fx_rad = np.deg2rad(hx * max_field_deg)
-        fy_rad = np.deg2rad(hy * max_field_deg)
-        tx, ty = np.tan(fx_rad), np.tan(fy_rad)
+        tx, ty = np.tan(np.deg2rad(hx * max_field_deg)), np.tan(np.deg2rad(hy * max_field_deg))
         uz = 1.0 / np.sqrt(1.0 + tx**2 + ty**2)
-        ux, uy = tx * uz, ty * uz
-        dev = opd.device
-        xs = torch.as_tensor(np.asarray(self.distribution.x if x is None else x, dtype=np.float64),
-                             device=dev)
-        ys = torch.as_tensor(np.asarray(self.distribution.y if y is None else y, dtype=np.float64),
-                             device=dev)
-        epd = self.optic.paraxial.EPD()
-        X_m = xs * epd / 2
-        Y_m = ys * epd / 2
-        tilt = float(ux) * X_m + float(uy) * Y_m
-        return opd + tilt
+        return tx * uz, ty * uz
 
     def compute_wavefront_data(self, field, wavelength):
+        import ctypes as C
+
+        from . import _native
+        from .raytrace import _stream_handle
+
         optic = self.optic
         chief = optic.trace_generic(*field, Px=0.0, Py=0.0, wavelength=wavelength)
-        x, y, z = chief.x, chief.y, chief.z
-        if x.numel() != 1:
+        if chief.x.numel() != 1:
             raise ValueError("Chief ray cannot be determined. It must be traced alone.")
-        R = float(torch.sqrt(x**2 + y**2 + (z - float(np.ravel(self.pupil_z)[0])) ** 2).item())
-        xc, yc, zc = x, y, z
-        opd_img_ref = self._opd_image_to_xp(chief, xc, yc, zc, R)
-        opd_ref = chief.opd - opd_img_ref
-        opd_ref = self._correct_tilt(field, opd_ref, x=0.0, y=0.0)
+        c = {a: chief_v for a, chief_v in zip(
+            ("x", "y", "z", "L", "M", "N", "opd"),
+            torch.stack([chief.x, chief.y, chief.z, chief.L, chief.M, chief.N,
+                         chief.opd]).reshape(7, 1).cpu().numpy(), strict=True)}
+        xc, yc, zc = c["x"], c["y"], c["z"]
+        R = float(np.sqrt(xc**2 + yc**2 + (zc - self.pupil_z) ** 2).item())  # :236-241
+        opd_ref = c["opd"] - self._opd_image_to_xp_np(c, xc, yc, zc, R)
+        tilt = self._tilt_direction(field)
+        epd = optic.paraxial.EPD() if tilt is not None else 0.0
+        if tilt is not None:  # _correct_tilt(field, opd_ref, x=0, y=0)
+            X_m = np.array(0.0) * epd / 2
+            Y_m = np.array(0.0) * epd / 2
+            opd_ref = opd_ref + (tilt[0] * X_m + tilt[1] * Y_m)
+
         rays = optic.trace(*field, wavelength, None, self.distribution)
-        intensity = rays.i
-        opd_img = self._opd_image_to_xp(rays, xc, yc, zc, R)
-        opd = rays.opd - opd_img
-        opd = self._correct_tilt(field, opd)
-        opd_wv = (opd_ref - opd) / (wavelength * 1e-3)
-        t = opd_img / self.n_image
-        return WavefrontData(pupil_x=rays.x - t * rays.L, pupil_y=rays.y - t * rays.M,
-                             pupil_z=rays.z - t * rays.N, opd=opd_wv, intensity=intensity,
-                             radius=R)
+        n = len(rays)
+        dev = rays.x.device
+        px = py = None
+        if tilt is not None:
+            px = torch.as_tensor(np.ascontiguousarray(self.distribution.x, dtype=np.float64),
+                                 device=dev)
+            py = torch.as_tensor(np.ascontiguousarray(self.distribution.y, dtype=np.float64),
+                                 device=dev)
+        f1 = lambda v: float(np.ravel(v)[0])  # noqa: E731
+        ref = _native.ort_wavefront_ref(
+            f1(xc), f1(yc), f1(zc), f1(xc**2), f1(yc**2), f1(zc**2), R**2,
+            float(self.n_image), f1(opd_ref), 0.0 if tilt is None else float(tilt[0]),
+            0.0 if tilt is None else float(tilt[1]), float(np.ravel(epd)[0]),
+            float(wavelength * 1e-3), int(tilt is not None), 0)
+        lib = _native.load()
+        opd_wv = torch.empty(n, dtype=torch.float64, device=dev)
+        pup = [torch.empty(n, dtype=torch.float64, device=dev) for _ in range(3)]
+        size = int(lib.ort_wavefront_workspace_size(n))
+        _native.check(size if size < 0 else 0, "ort_wavefront_workspace_size")
+        ws = torch.empty(max(size, 8) // 8, dtype=torch.float64, device=dev)
+        sums = torch.empty(11, dtype=torch.float64, device=dev)
+        ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+        rc = lib.ort_wavefront_opd(C.byref(rays.c_struct()), ptr(px), ptr(py), n, C.byref(ref),
+                                   ptr(opd_wv), ptr(pup[0]), ptr(pup[1]), ptr(pup[2]),
+                                   ptr(ws), size, ptr(sums), _stream_handle())
+        _native.check(rc, "ort_wavefront_opd")
+        data = WavefrontData(pupil_x=pup[0], pupil_y=pup[1], pupil_z=pup[2], opd=opd_wv,
+                             intensity=rays.i, radius=R)
+        data.sums = sums
+        return data
+
+
+def fit_and_remove_tilt(data, remove_piston=False, ridge=1e-12):
+    """wavefront.py:97-143: weighted least-squares piston / tilt plane removed from the
+    OPD, the normal equations' sums from the wavefront kernel (data.sums), the 3 x 3
+    solve on the host and the plane subtracted on the device."""
+    s = data.sums.cpu().numpy()
+    _, _, w, wx, wy, wxx, wxy, wyy, wz, wxz, wyz = s
+    XT_X = np.array([[w, wx, wy], [wx, wxx, wxy], [wy, wxy, wyy]]) + ridge * np.eye(3)
+    coeffs = np.linalg.solve(XT_X, np.array([wz, wxz, wyz]))
+    if not remove_piston:
+        coeffs = coeffs.copy()
+        coeffs[0] = 0.0
+    return data.opd - (coeffs[0] + data.pupil_x * coeffs[1] + data.pupil_y * coeffs[2])
 
 
 class Wavefront:
@@ -334,7 +376,11 @@ class Wavefront:
         self.data = {}
         for f in self.fields:
             for wl in self.wavelengths:
-                self.data[(tuple(f), wl)] = self.strategy.compute_wavefront_data(tuple(f), wl)
+                data = self.strategy.compute_wavefront_data(tuple(f), wl)
+                if remove_tilt:  # wavefront.py:164-165
+                    data.opd = fit_and_remove_tilt(data)
+                    data.sums = None
+                self.data[(tuple(f), wl)] = data
 
     def get_data(self, field, wl):
         return self.data[(tuple(field), wl)]
@@ -355,8 +401,13 @@ class OPD(Wavefront):
                          remove_tilt=remove_tilt)
 
     def rms(self):
-        """opd.py:143-157."""
+        """opd.py:143-157 (from the wavefront kernel's sums unless the tilt was removed)."""
         data = self.get_data(self.fields[0], self.wavelengths[0])
+        if getattr(data, "sums", None) is not None:
+            cnt, s2 = (float(v) for v in data.sums[:2].cpu())
+            if cnt == 0:
+                raise ValueError("No valid rays with non-zero intensity for RMS calculation.")
+            return torch.sqrt(data.sums[1] / data.sums[0])
         mask = data.intensity > 0
         if not bool(torch.any(mask)):
             raise ValueError("No valid rays with non-zero intensity for RMS calculation.")

@@ -16,12 +16,12 @@
 // propagate as in NumPy (the sums carry them; the max keeps an explicit NaN flag, since
 // fmax would drop it).
 
-#include "ort_kernels.h"
+#include "ort_reduce.h"
 
 namespace ortk {
 namespace {
 
-constexpr int kSpotThreads = 256;
+constexpr int kSpotThreads = kRedThreads;
 constexpr int64_t kSpotMaxChunks = 256;  // chunks per pair at most: a chunk is 256 rays
                                          // times ceil(n_pupil / (256 * 256)) per thread
 
@@ -53,35 +53,6 @@ __device__ inline void local_point(const SpotArgs& a, int64_t r, double& x, doub
   for (int k = 0; k < a.n_ops; ++k) ort::apply_cs_op(p, cst(a.ops)[k]);
   x = p.x;
   y = p.y;
-}
-
-__device__ inline double wave_sum(double v) {
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-__device__ inline double wave_max(double v) {
-  for (int o = 32; o > 0; o >>= 1) v = ::fmax(v, __shfl_xor(v, o, 64));
-  return v;
-}
-
-// block-wide sums of NV values (fixed order: lanes by xor butterfly, then waves 0..3);
-// every thread gets the totals. lds: >= 4 * NV doubles
-template <int NV>
-__device__ inline void block_sum(double (&v)[NV], double* lds) {
-#pragma unroll
-  for (int k = 0; k < NV; ++k) v[k] = wave_sum(v[k]);
-  const int w = threadIdx.x >> 6;
-  __syncthreads();
-  if ((threadIdx.x & 63) == 0)
-#pragma unroll
-    for (int k = 0; k < NV; ++k) lds[w * NV + k] = v[k];
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < NV; ++k) {
-    double s = 0.0;
-    for (int ww = 0; ww < kSpotThreads / 64; ++ww) s += lds[ww * NV + k];
-    v[k] = s;
-  }
 }
 
 // sums of the 3 columns of part[0 .. n) (index-strided per thread, then block_sum)

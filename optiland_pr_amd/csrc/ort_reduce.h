@@ -1,0 +1,53 @@
+// ort_reduce.h -- deterministic block reductions for the analysis kernels
+// (ort_k_spot.hip, ort_k_wavefront.hip): xor-butterfly wave sums, then the block's waves
+// in index order, so a reduction over fixed chunks is bit-identical run to run.
+#pragma once
+
+#include "ort_kernels.h"
+
+namespace ortk {
+
+constexpr int kRedThreads = 256;  // threads per block of the analysis kernels
+
+__device__ inline double wave_sum_xor(double v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ inline double wave_max(double v) {
+  for (int o = 32; o > 0; o >>= 1) v = ::fmax(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// block-wide sums of NV values (lanes by xor butterfly, then waves 0..3 in order); every
+// thread gets the totals. lds: >= 4 * NV doubles; safe to call back to back.
+template <int NV>
+__device__ inline void block_sum(double (&v)[NV], double* lds) {
+#pragma unroll
+  for (int k = 0; k < NV; ++k) v[k] = wave_sum_xor(v[k]);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0)
+#pragma unroll
+    for (int k = 0; k < NV; ++k) lds[w * NV + k] = v[k];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    double s = 0.0;
+    for (int ww = 0; ww < kRedThreads / 64; ++ww) s += lds[ww * NV + k];
+    v[k] = s;
+  }
+}
+
+// column sums of rows part[0 .. n) of NV doubles, each thread striding over rows in
+// index order, then block_sum
+template <int NV>
+__device__ inline void reduce_rows_n(const double* part, int n, double (&v)[NV], double* lds) {
+#pragma unroll
+  for (int k = 0; k < NV; ++k) v[k] = 0.0;
+  for (int c = threadIdx.x; c < n; c += kRedThreads)
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] += part[c * NV + k];
+  block_sum<NV>(v, lds);
+}
+
+}  // namespace ortk

@@ -766,7 +766,29 @@ def analysis_goldens():
     dg = DoubleGauss()
     res["dg_opd_rms_0_1_05876"] = float(OPD(dg, (0, 1), 0.5876).rms())
     res["dg_opd_rms_0_0_05876"] = float(OPD(DoubleGauss(), (0, 0), 0.5876).rms())
+    # piston / tilt removal (wavefront.py:97-143, 164-165)
+    res["cooke_opd_rms_0_1_055_notilt"] = float(
+        OPD(CookeTriplet(), (0, 1), 0.55, remove_tilt=True).rms())
+    res["dg_opd_rms_0_1_05876_notilt"] = float(
+        OPD(DoubleGauss(), (0, 1), 0.5876, remove_tilt=True).rms())
+    # per-ray wavefront data (pupil points, OPD in waves, intensity) of a few cases
+    arrays = {}
+    for key, (builder, field, wl, kw) in WAVEFRONT_CASES.items():
+        w = OPD(builder(), field, wl, **kw)
+        d = w.get_data(w.fields[0], w.wavelengths[0])
+        for a in ("pupil_x", "pupil_y", "pupil_z", "opd", "intensity"):
+            arrays[f"{key}/{a}"] = np.asarray(getattr(d, a), dtype=np.float64)
+        arrays[f"{key}/radius"] = np.array(float(d.radius))
+    np.savez_compressed(os.path.join(HERE, "wavefront.npz"), **arrays)
     return res
+
+
+WAVEFRONT_CASES = {  # name -> (lens builder, field, wavelength, OPD keywords)
+    "cooke_0_1": (CookeTriplet, (0, 1), 0.55, {}),
+    "cooke_0_07_notilt": (CookeTriplet, (0, 0.7), 0.48, {"remove_tilt": True}),
+    "dg_0_1": (DoubleGauss, (0, 1), 0.5876, {"num_rays": 20}),
+    "finite_pih_03_07": (None, (0.3, 0.7), 0.55, {}),  # paraxial image height: no tilt
+}
 
 
 def full_size_summaries():
@@ -934,6 +956,14 @@ def main():
     if "--abbe" in sys.argv:  # re-bake optiland_pr_amd/data/abbe_coefficients.json only
         abbe_table()
         return
+    if "--analysis" in sys.argv:  # index.json "_analysis" + wavefront.npz only
+        WAVEFRONT_CASES["finite_pih_03_07"] = (finite_pih,) + WAVEFRONT_CASES["finite_pih_03_07"][1:]
+        with open(os.path.join(HERE, "index.json")) as f:
+            index = json.load(f)
+        index["_analysis"] = analysis_goldens()
+        with open(os.path.join(HERE, "index.json"), "w") as f:
+            json.dump(index, f, indent=1)
+        return
     only = sys.argv[sys.argv.index("--only") + 1:] if "--only" in sys.argv else None
     if only:
         with open(os.path.join(HERE, "index.json")) as f:
@@ -955,6 +985,7 @@ def main():
     distribution_goldens()
     aperture_goldens()
     mixed_wavelength_goldens()
+    WAVEFRONT_CASES["finite_pih_03_07"] = (finite_pih,) + WAVEFRONT_CASES["finite_pih_03_07"][1:]
     index["_analysis"] = analysis_goldens()
     index["_full"] = full_size_summaries()
     with open(os.path.join(HERE, "index.json"), "w") as f:

@@ -28,6 +28,7 @@ STRUCTS = {
     "ort_vjp_params": (None, _native.ort_vjp_params),
     "ort_pupil": (None, _native.ort_pupil),
     "ort_spot_layout": (None, _native.ort_spot_layout),
+    "ort_wavefront_ref": (None, _native.ort_wavefront_ref),
 }
 
 

@@ -51,3 +51,51 @@ def test_opd_rms(gpu, golden_index, case):
     np.testing.assert_allclose(rms, golden_index["_analysis"][key], rtol=1e-10)
     if key == "cooke_opd_rms_0_1_055":
         np.testing.assert_allclose(rms, 0.9709788038168692, rtol=1e-5)  # test_wavefront.py:139
+
+
+@pytest.mark.parametrize("key, rms_key", [("cooke_0_1", None),
+                                          ("cooke_0_07_notilt", None),
+                                          ("dg_0_1", None),
+                                          ("finite_pih_03_07", None)])
+def test_wavefront_per_ray(gpu, key, rms_key):
+    """The fused wavefront kernel (ort_wavefront_opd) per ray against the reference's
+    WavefrontData (strategy.py:168-239): pupil points and OPD in waves bit-exact (same
+    IEEE operations in the same order on bit-identical traced rays); with the piston /
+    tilt removed (wavefront.py:97-143) to 1e-9 waves (the fit's sums are reduced in a
+    different order)."""
+    import os
+
+    from optiland_pr_amd.analysis import OPD
+    from optiland_pr_amd.samples import CookeTriplet, DoubleGauss, FiniteTripletImageHeight
+
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                             "wavefront.npz"), allow_pickle=False)
+    builders = {"cooke_0_1": (CookeTriplet, (0, 1), 0.55, {}),
+                "cooke_0_07_notilt": (CookeTriplet, (0, 0.7), 0.48, {"remove_tilt": True}),
+                "dg_0_1": (DoubleGauss, (0, 1), 0.5876, {"num_rays": 20}),
+                "finite_pih_03_07": (FiniteTripletImageHeight, (0.3, 0.7), 0.55, {})}
+    builder, field, wl, kw = builders[key]
+    w = OPD(builder(), field, wl, **kw)
+    d = w.get_data(w.fields[0], w.wavelengths[0])
+    assert d.radius == float(g[f"{key}/radius"])
+    for a in ("pupil_x", "pupil_y", "pupil_z"):
+        np.testing.assert_array_equal(getattr(d, a).cpu().numpy(), g[f"{key}/{a}"], err_msg=a)
+    # intensity: the trace's stated rel 1e-12 (absorption exponent accumulated per ray)
+    np.testing.assert_allclose(d.intensity.cpu().numpy(), g[f"{key}/intensity"], rtol=1e-12)
+    got = d.opd.cpu().numpy()
+    if kw.get("remove_tilt"):
+        np.testing.assert_allclose(got, g[f"{key}/opd"], rtol=0, atol=1e-9)
+    else:
+        np.testing.assert_array_equal(got, g[f"{key}/opd"])
+
+
+@pytest.mark.parametrize("case", [("cooke", (0, 1), 0.55, "cooke_opd_rms_0_1_055_notilt"),
+                                  ("dg", (0, 1), 0.5876, "dg_opd_rms_0_1_05876_notilt")])
+def test_opd_rms_remove_tilt(gpu, golden_index, case):
+    from optiland_pr_amd.analysis import OPD
+    from optiland_pr_amd.samples import CookeTriplet, DoubleGauss
+
+    name, field, wl, key = case
+    lens = CookeTriplet() if name == "cooke" else DoubleGauss()
+    rms = float(OPD(lens, field, wl, remove_tilt=True).rms())
+    np.testing.assert_allclose(rms, golden_index["_analysis"][key], rtol=1e-10)
