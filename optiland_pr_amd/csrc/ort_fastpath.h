@@ -18,6 +18,17 @@
 //              yields +0 * sign(b) exactly (q0 carries the sign, r = +0); -0 and every
 //              other value outside the range takes the exact path.
 //
+// Upper bounds (and the divisors' lower bound) are not tested per operation. Past them the short sequences do not return
+// a wrong FINITE value, only a non-finite one: sqrt(+inf) gives NaN (rsq = 0, g = inf*0);
+// a numerator large enough to matter overflows q0 = a y to inf and the quotient to inf or
+// NaN. Non-finite values are sticky in the ray state -- a non-finite t makes the OPD
+// (opd += |t n|, a sum of non-negative terms) non-finite for good, a non-finite direction
+// or position makes the next t non-finite or is itself an output -- so the kernel tests
+// the finished state once (state_ok) and re-traces such lanes exactly. Only the
+// numerators' and sqrt's lower bounds (where the sequences would underflow into a finite,
+// wrongly rounded result) and the divisors' upper bound (a reciprocal small enough to
+// underflow a quotient) stay per operation.
+//
 // Formulas and their order follow ort_core.h (and through it the reference files cited
 // there); only the check placement differs. Host compilation: plain IEEE operations.
 #pragma once
@@ -49,10 +60,6 @@ namespace fast {
 #define ORT_CHK(bad, cond) ((bad) = (bad) | (cond))
 #endif
 
-ORT_INLINE bool in_div_range(double v) {
-  const double av = ::fabs(v);
-  return av >= 0x1p-300 && av <= 0x1p300;  // false for 0, inf, NaN
-}
 ORT_INLINE bool is_pos_zero(double v) {
 #if defined(__HIP_DEVICE_COMPILE__)
   return __builtin_amdgcn_class(v, 1 << 6);  // v_cmp_class_f64: +0 only
@@ -74,7 +81,7 @@ ORT_INLINE double sqrt(double x, bool& bad) {
   g = fma(d, h, g);
   d = fma(-g, g, x);
   g = fma(d, h, g);
-  ORT_CHK(bad, !(x >= 0x1p-767 && x < __builtin_inf()));
+  ORT_CHK(bad, !(x >= 0x1p-767));  // +inf gives NaN: left to state_ok
   return g;
 #else
   (void)bad;
@@ -82,7 +89,8 @@ ORT_INLINE double sqrt(double x, bool& bad) {
 #endif
 }
 
-// sqrt(x) where x >= 1 unless NaN (sums of squares plus 1): only the upper bound is live
+// sqrt(x) where x >= 1 unless NaN (sums of squares plus 1): only the upper bound could
+// fail, and +inf / NaN give NaN, which state_ok catches: no test
 ORT_INLINE double sqrt_ge1(double x, bool& bad) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const double y = __builtin_amdgcn_rsq(x);
@@ -95,7 +103,7 @@ ORT_INLINE double sqrt_ge1(double x, bool& bad) {
   g = fma(d, h, g);
   d = fma(-g, g, x);
   g = fma(d, h, g);
-  ORT_CHK(bad, !(x < __builtin_inf()));
+  (void)bad;
   return g;
 #else
   (void)bad;
@@ -114,7 +122,12 @@ ORT_INLINE SharedDiv shared_div(double b, bool& bad) {
   e = fma(-b, y, 1.0);
   y = fma(y, e, y);
   d.y = y;
-  ORT_CHK(bad, !in_div_range(b));
+  // |b| <= 2^300 (false for NaN). Below 2^-1021 (zero and subnormal divisors included)
+  // the reciprocal is infinite and every quotient non-finite -- NaN for a zero
+  // numerator, +-inf or NaN otherwise -- which state_ok catches; in between the
+  // refined reciprocal is accurate and, as every numerator is >= 2^-300 or an exact zero
+  // (sdiv / sdiv0 / num_ok), q0 = a y cannot underflow (|q| >= 2^-600).
+  ORT_CHK(bad, !(::fabs(b) <= 0x1p300));
 #else
   (void)bad;
   d.y = 0.0;
@@ -167,14 +180,18 @@ ORT_INLINE double quot_pos(double a, const SharedDiv& d) {
 #endif
 }
 
-// a / b, |a| in range
+// |a| >= 2^-300 (false for 0 and NaN); a numerator past 2^300 overflows into a
+// non-finite quotient (see the header)
+ORT_INLINE bool num_ok(double a) { return ::fabs(a) >= 0x1p-300; }
+
+// a / b, |a| >= 2^-300
 ORT_INLINE double sdiv(double a, const SharedDiv& d, bool& bad) {
-  ORT_CHK(bad, !in_div_range(a));
+  ORT_CHK(bad, !num_ok(a));
   return quot(a, d);
 }
-// a / b, |a| in range or a == +0 (coordinates on a symmetry plane)
+// a / b, |a| >= 2^-300 or a == +0 (coordinates on a symmetry plane)
 ORT_INLINE double sdiv0(double a, const SharedDiv& d, bool& bad) {
-  ORT_CHK(bad, !(in_div_range(a) || is_pos_zero(a)));
+  ORT_CHK(bad, !(num_ok(a) || is_pos_zero(a)));
   return quot(a, d);
 }
 
@@ -211,8 +228,8 @@ ORT_INLINE Ray generate_ray(const ort_segment& s, double px, double py,
   ORT_CHK(bad, (mag < 1e-9));  // the (0, 0, 1) branch of ray_generator.py:82-89
   const SharedDiv dm = shared_div(mag, bad);
   // mag > 0: quot_pos is exact for zero numerators of either sign
-  ORT_CHK(bad, !((in_div_range(dx) || dx == 0.0) && (in_div_range(dy) || dy == 0.0) &&
-                 (in_div_range(dz) || dz == 0.0)));
+  ORT_CHK(bad, !((num_ok(dx) || dx == 0.0) && (num_ok(dy) || dy == 0.0) &&
+                 (num_ok(dz) || dz == 0.0)));
   r.L = quot_pos(dx, dm);
   r.M = quot_pos(dy, dm);
   r.N = quot_pos(dz, dm);
@@ -223,6 +240,16 @@ ORT_INLINE Ray generate_ray(const ort_segment& s, double px, double py,
   r.opd = 0.0;
   r.att = 0.0;
   return r;
+}
+
+// The end-of-trace test of the header: every output of the ray state finite and below
+// 2^1000 (false for NaN / inf; the bound also covers a quotient that would overflow only
+// in the short sequence, |q| ~ 2^1023). The intensity is not tested: only the clip tests
+// write it, on positions that are themselves tested here.
+ORT_INLINE bool state_ok(const Ray& r) {
+  constexpr double kMax = 0x1p1000;
+  return ::fabs(r.x) < kMax && ::fabs(r.y) < kMax && ::fabs(r.z) < kMax &&
+         ::fabs(r.L) < kMax && ::fabs(r.M) < kMax && ::fabs(r.N) < kMax && ::fabs(r.opd) < kMax;
 }
 
 // plane.py:61-77 (-z / N) and the plane branch of standard.py:100-103
@@ -253,12 +280,12 @@ ORT_INLINE double distance_conic(const Ray& r, const ort_surface& s, bool radius
   const SharedDiv a2 = shared_div(2.0 * a, bad);
   // nonzero numerators (checked): quot_pos and quot agree for either sign of a
   const double n1 = -b + sd, n2 = -b - sd;
-  ORT_CHK(bad, !(in_div_range(n1) && in_div_range(n2)));
+  ORT_CHK(bad, !(num_ok(n1) && num_ok(n2)));
   const double t1 = quot_pos(n1, a2);
   const double t2 = quot_pos(n2, a2);
   const double z1 = r.z + t1 * r.N;
   const double zz2 = r.z + t2 * r.N;
-  ORT_CHK(bad, (a == 0.0));  // the -c / b branch (standard.py:138)
+  // a == 0 (the -c / b branch, standard.py:138) fails shared_div's range test
   return ::fabs(z1) <= ::fabs(zz2) ? t1 : t2;
 }
 

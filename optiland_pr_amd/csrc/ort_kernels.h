@@ -645,6 +645,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
 #ifndef ORT_NO_DEFERRED_CHECKS
   ort::Ray r = closed_ray_in<FEAT, true>(a, r_ld, lam, wl, bad);
   closed_surfaces<FEAT, true>(a, r, lam, wl, rid, active, bad, geom_bad);
+  bad = bad | !ort::fast::state_ok(r);  // the upper-range failures (ort_fastpath.h)
   if (__builtin_expect(bad, 0)) {  // this lane left the fast path's ranges: exact re-trace
     r = closed_ray_in<FEAT, false>(a, r_ld, lam, wl, bad);
     closed_surfaces<FEAT, false>(a, r, lam, wl, rid, active, bad, geom_bad);
