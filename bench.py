@@ -190,7 +190,7 @@ def config3(args, dev, rank, world, torch):
     keys = [("bench3", k) for k in range(len(seg))]
 
     def step():
-        trace_pupil(dl, seg_dev, px, py, out, n, n_p, n_p, keys=keys)
+        trace_pupil(dl, seg_dev, px, py, out, n, n_p, n_p, keys=keys, newton_mode=args.newton_mode)
 
     return Workload(
         metric="ray-surface intersections/sec, RT-asph even-asphere (Newton sag), 5 fields x "
@@ -199,6 +199,7 @@ def config3(args, dev, rank, world, torch):
         config={"workload": "ReverseTelephoto + even aspheres on surfaces 2, 13 (SURVEY 8d.3), "
                             "5 fields x 3 lambda, one launch, Newton group per pair",
                 "rays_per_gpu": n, "pupil_per_pair": n_p, "surfaces": S,
+                "newton_mode": args.newton_mode,
                 "parallelism": f"dp{world} (ray shards, no collective)"},
         kernel="trace_kernel<F_GEN|KM_EVEN> (ort_trace_pupil)", launches=1,
         bytes_per_launch=n_p * 16 + n * 64, flops_per_ray=None, pmc_file="hbm_traffic_c3.json",
@@ -305,6 +306,9 @@ def main():
     ap.add_argument("--rays", type=int, default=1_000_000)
     ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--newton-mode", default="reference", choices=["reference", "wave"],
+                    help="config 3: the reference's global Newton stop rule (exact) or the "
+                         "per-wavefront stop (within the Newton tolerance)")
     ap.add_argument("--cpu-rays", type=int, default=1_000_000)
     ap.add_argument("--cpu-seconds", type=float, default=1.5,
                     help="wall time of the multi-process CPU baseline leg")

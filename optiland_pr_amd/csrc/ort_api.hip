@@ -90,7 +90,9 @@ int fill_args(KArgs& a, const ort_lens* lens, const ort_batch* batch, const ort_
     a.w = batch->w;
     a.mats = lens->materials;
     feat |= F_WRAY;
-  } else if (lens->n_lambda == 1) {
+  } else if (lens->n_lambda == 1 || batch->n_seg <= 1 || batch->seg_len % 64 == 0) {
+    // every wave reads one wavelength row: one row, one segment, or segment boundaries
+    // on the 64-ray wave boundaries (ray r is in segment r / seg_len)
     feat |= F_MONO;
   }
   if (lens->interaction_mask & ~(1u << ORT_IA_REFRACT_REFLECT)) {
@@ -109,7 +111,7 @@ int launch(const KArgs& a, uint32_t feat, hipStream_t stream) {
   if (a.n_rays == 0) return ORT_OK;
   KernelFn fn = (feat & F_IA) != 0    ? select_trace_ia(feat & ~F_AXIAL)
                 : (feat & F_KM) == 0 ? select_closed(feat)
-                                     : select_trace(feat & ~(F_MONO | F_AXIAL));
+                                     : select_trace(feat & ~F_AXIAL);
   if (!fn) return ORT_ERR_ARG;
   const int64_t blocks = (a.n_rays + kBlock - 1) / kBlock;
   if (blocks > 0x7fffffff) return ORT_ERR_ARG;

@@ -323,6 +323,28 @@ template <int P>
 ORT_INLINE Dual<P> sdiv(double a, const PlainDiv<P>& d) {
   return a / d.b;
 }
+template <int P>
+ORT_INLINE Dual<P> sdiv(const Dual<P>& a, const SharedDiv& d) {
+  return a / d.b;
+}
+
+// a / d and b / d: two IEEE divisions sharing one reciprocal refinement
+template <class T, class D>
+ORT_INLINE void div2(const T& a, const T& b, const D& d, T& qa, T& qb) {
+  const auto sd = shared_div(d);
+  qa = sdiv(a, sd);
+  qb = sdiv(b, sd);
+}
+
+// the normalised normal (dzdx, dzdy, -1) / norm of every Newton geometry
+// (nx = dzdx / norm, ny = dzdy / norm, nz = -1 / norm): one reciprocal refinement
+template <class T>
+ORT_INLINE void unit_normal3(const T& dzdx, const T& dzdy, const T& norm, T& nx, T& ny, T& nz) {
+  const auto sd = shared_div(norm);
+  nx = sdiv(dzdx, sd);
+  ny = sdiv(dzdy, sd);
+  nz = sdiv(-1.0, sd);
+}
 
 // Zernike coefficient tangent seeds for the derivative kernels: term j (global index in
 // lens.zern) is parameter param[j] (< 0: not differentiated); tangent slot k of this
@@ -604,8 +626,8 @@ ORT_INLINE T sagnorm_even(const T& x, const T& y, const S& R, const S& k, PD C, 
   }
   if (want_normal) {
     const T denom = R * q;
-    T dfdx = x / denom;
-    T dfdy = y / denom;
+    T dfdx, dfdy;
+    div2(x, y, denom, dfdx, dfdy);
     T rq = T(1.0);  // r2 ** i
     for (int i = 0; i < nc; ++i) {
       const double f = 2.0 * (double)(i + 1);
@@ -614,9 +636,7 @@ ORT_INLINE T sagnorm_even(const T& x, const T& y, const S& R, const S& k, PD C, 
       rq = rq * r2;
     }
     const T mag = sqrt(dfdx * dfdx + dfdy * dfdy + 1.0);
-    nx = dfdx / mag;
-    ny = dfdy / mag;
-    nz = -1.0 / mag;
+    unit_normal3(dfdx, dfdy, mag, nx, ny, nz);
   }
   return z;
 }
@@ -637,8 +657,8 @@ ORT_INLINE T sagnorm_odd(const T& x, const T& y, const S& R, const S& k, PD C, i
   }
   if (want_normal) {
     const T denom = R * q;
-    T dfdx = x / denom;
-    T dfdy = y / denom;
+    T dfdx, dfdy;
+    div2(x, y, denom, dfdx, dfdy);
     T rq = 1.0 / r;  // r ** (i - 1): 1/r, 1, r, r*r, r*r*r, ...
     for (int i = 0; i < nc; ++i) {
       const double f = (double)(i + 1);
@@ -651,9 +671,7 @@ ORT_INLINE T sagnorm_odd(const T& x, const T& y, const S& R, const S& k, PD C, i
       dfdy = dfdy + yt;
     }
     const T mag = sqrt(dfdx * dfdx + dfdy * dfdy + 1.0);
-    nx = dfdx / mag;
-    ny = dfdy / mag;
-    nz = -1.0 / mag;
+    unit_normal3(dfdx, dfdy, mag, nx, ny, nz);
   }
   return z;
 }
@@ -689,8 +707,8 @@ ORT_INLINE T sagnorm_poly(const T& x, const T& y, const S& R, const S& k, PD B,
   }
   if (want_normal) {
     const T denom = R * q;
-    T dzdx = x / denom;
-    T dzdy = y / denom;
+    T dzdx, dzdy;
+    div2(x, y, denom, dzdx, dzdy);
     T xm = T(1.0);  // x ** (i - 1)
     for (int i = 1; i < ni; ++i) {
       T yj = T(1.0);
@@ -712,9 +730,7 @@ ORT_INLINE T sagnorm_poly(const T& x, const T& y, const S& R, const S& k, PD B,
       xi2 = xi2 * x;
     }
     const T norm = sqrt(dzdx * dzdx + dzdy * dzdy + 1.0);
-    nx = dzdx / norm;
-    ny = dzdy / norm;
-    nz = -1.0 / norm;
+    unit_normal3(dzdx, dzdy, norm, nx, ny, nz);
   }
   return z;
 }
@@ -747,8 +763,7 @@ ORT_INLINE T sagnorm_cheb(const T& x, const T& y, const S& R, const S& k, PD B,
   T dzdx, dzdy;
   if (want_normal) {
     const T denom = R * q;
-    dzdx = x / denom;
-    dzdy = y / denom;
+    div2(x, y, denom, dzdx, dzdy);
   }
   for (int i = 0; i < ni; ++i) {
 #pragma unroll 1
@@ -765,9 +780,7 @@ ORT_INLINE T sagnorm_cheb(const T& x, const T& y, const S& R, const S& k, PD B,
   }
   if (want_normal) {
     const T norm = sqrt(dzdx * dzdx + dzdy * dzdy + 1.0);
-    nx = dzdx / norm;
-    ny = dzdy / norm;
-    nz = -1.0 / norm;
+    unit_normal3(dzdx, dzdy, norm, nx, ny, nz);
   }
   return z;
 }
@@ -802,9 +815,7 @@ ORT_INLINE T sagnorm_biconic(const T& x, const T& y, PD B, bool want_normal, T& 
     const T dfdy = cy == 0.0 ? T(0.0) : biconic_slope(cy, ky, y);
     const T mag = sqrt(dfdx * dfdx + dfdy * dfdy + 1.0);
     const T smag = vv(mag) < 1e-14 ? T(1.0) : mag;
-    nx = dfdx / smag;
-    ny = dfdy / smag;
-    nz = -1.0 / smag;
+    unit_normal3(dfdx, dfdy, smag, nx, ny, nz);
   }
   return zx + zy;
 }
@@ -916,8 +927,7 @@ ORT_INLINE bool zseeded(const ZSeed& zs, int j, Dual<P>*) {
 template <class T>
 ORT_INLINE void polar_unit(const T& xn, const T& yn, const T& rho, T& c1, T& s1) {
   if (vv(rho) > 0.0) {
-    c1 = xn / rho;
-    s1 = yn / rho;
+    div2(xn, yn, rho, c1, s1);
   } else {  // atan2(0, 0) = 0
     c1 = T(1.0);
     s1 = T(0.0);
@@ -931,8 +941,8 @@ template <class T, class S, class PD, class PZ>
 ORT_INLINE T sagnorm_zernike(const T& x, const T& y, const S& R, const S& k, double Rn, PZ Tm,
                              int t0, int nt, PD coef, const ZSeed& zs, bool want_normal,
                              bool& range_error, T& nx, T& ny, T& nz) {
-  const T xn = x / Rn;
-  const T yn = y / Rn;
+  T xn, yn;
+  div2(x, y, Rn, xn, yn);
   if (::fabs(vv(xn)) > 1.0 || ::fabs(vv(yn)) > 1.0) range_error = true;
   const T rho = sqrt(xn * xn + yn * yn);
   T c1, s1;
@@ -947,16 +957,18 @@ ORT_INLINE T sagnorm_zernike(const T& x, const T& y, const S& R, const S& k, dou
   T dzdx, dzdy, drho_dx, drho_dy, dphi_dx, dphi_dy;
   if (want_normal) {
     const T denominator = R * q;
-    dzdx = x / denominator;
-    dzdy = y / denominator;
+    div2(x, y, denominator, dzdx, dzdy);
     const double Rn2 = Rn * Rn;
     // (the reference returns zeros when EVERY rho is 0; per ray (x/Rn^2)/(0+eps) = 0 too)
-    drho_dx = (x / Rn2) / (rho + eps);
-    drho_dy = (y / Rn2) / (rho + eps);
+    T xr, yr;
+    div2(x, y, Rn2, xr, yr);
+    div2(xr, yr, rho + eps, drho_dx, drho_dy);
     const T rho2e = rho2 + eps;
     const double inv_rn = 1.0 / Rn;
-    dphi_dx = -(yn) / rho2e * inv_rn;
-    dphi_dy = (xn) / rho2e * inv_rn;  // "+(x_norm)": unary plus
+    T qy, qx;
+    div2(T(-(yn)), xn, rho2e, qy, qx);
+    dphi_dx = qy * inv_rn;
+    dphi_dy = qx * inv_rn;  // "+(x_norm)": unary plus
   }
   for (int j = 0; j < nt; ++j) {
     const ort_zernike_term t = Tm[t0 + j];
@@ -1014,9 +1026,7 @@ ORT_INLINE T sagnorm_zernike(const T& x, const T& y, const S& R, const S& k, dou
   if (want_normal) {
     T norm = sqrt(dzdx * dzdx + dzdy * dzdy + 1.0);
     norm = vv(norm) < eps ? T(1.0) : norm;
-    nx = dzdx / norm;
-    ny = dzdy / norm;
-    nz = -1.0 / norm;
+    unit_normal3(dzdx, dzdy, norm, nx, ny, nz);
   }
   return z + total;
 }
@@ -1031,13 +1041,12 @@ template <class PD, class PZ, class F>
 ORT_INLINE void zernike_coef_adjoint(double x, double y, double Rn, PZ Tm, int t0, int nt,
                                      PD coef, double w_sag, double w_dx, double w_dy,
                                      F&& emit) {
-  const double xn = x / Rn;
-  const double yn = y / Rn;
+  double xn, yn;
+  div2(x, y, Rn, xn, yn);
   const double rho = sqrt(xn * xn + yn * yn);
   double c1, s1;
   if (rho > 0.0) {
-    c1 = xn / rho;
-    s1 = yn / rho;
+    div2(xn, yn, rho, c1, s1);
   } else {
     c1 = 1.0;
     s1 = 0.0;
@@ -1045,12 +1054,15 @@ ORT_INLINE void zernike_coef_adjoint(double x, double y, double Rn, PZ Tm, int t
   const double rho2 = rho * rho;
   const double eps = 1e-14;
   const double Rn2 = Rn * Rn;
-  const double drho_dx = (x / Rn2) / (rho + eps);
-  const double drho_dy = (y / Rn2) / (rho + eps);
+  double xr, yr, drho_dx, drho_dy;
+  div2(x, y, Rn2, xr, yr);
+  div2(xr, yr, rho + eps, drho_dx, drho_dy);
   const double rho2e = rho2 + eps;
   const double inv_rn = 1.0 / Rn;
-  const double dphi_dx = -(yn) / rho2e * inv_rn;
-  const double dphi_dy = (xn) / rho2e * inv_rn;
+  double qy, qx;
+  div2(-(yn), xn, rho2e, qy, qx);
+  const double dphi_dx = qy * inv_rn;
+  const double dphi_dy = qx * inv_rn;
   for (int j = 0; j < nt; ++j) {
     const ort_zernike_term t = Tm[t0 + j];
     const int am = t.m >= 0 ? t.m : -t.m;
@@ -1556,8 +1568,8 @@ template <class T>
 ORT_INLINE T newton_step(const RayT<T>& r, const T& t, const T& f, const T& nx, const T& ny,
                          const T& nz) {
   const T nzs = ::fabs(vv(nz)) > 1e-14 ? nz : T(1e-14);
-  const T fx = -nx / nzs;
-  const T fy = -ny / nzs;
+  T fx, fy;
+  div2(T(-nx), T(-ny), nzs, fx, fy);
   const T df = fx * r.L + fy * r.M - r.N;
   const T dfs = ::fabs(vv(df)) > 1e-14 ? df : T(1e-14);
   return t - f / dfs;

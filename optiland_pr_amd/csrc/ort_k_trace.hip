@@ -13,6 +13,12 @@ KernelFn select_trace_rec(uint32_t feat);  // ort_k_trace_rec.hip
 
 KernelFn select_trace(uint32_t feat) {
   if (feat & F_WRAY) return select_trace_w(feat);
+  if (feat & F_MONO) {
+    // scalar optics loads: instantiated for generated rays without records (the pupil
+    // traces); other combinations read the rows per lane
+    if ((feat & ~(F_KM | F_MONO)) == F_GEN) return select_trace_mono(feat);
+    feat &= ~F_MONO;
+  }
   if (feat & F_REC) return select_trace_rec(feat);
   switch (feat) {
 #define ORT_CASE(F) \

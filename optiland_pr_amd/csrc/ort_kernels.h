@@ -58,7 +58,8 @@ enum : uint32_t {
   F_KM = 15u,
   F_GEN = 1u << 4,
   F_REC = 1u << 5,   // some surfaces are recorded (standard_surface.py:266-286)
-  F_MONO = 1u << 6,  // one wavelength in the lens tables (closed-form kernels only)
+  F_MONO = 1u << 6,  // the wavelength row is wave-uniform (one wavelength in the lens
+                     // tables, or segments aligned to 64 rays): scalar table loads
   F_WRAY = 1u << 7,  // per-ray wavelengths: n, k from lens.materials (ort_batch.w)
   F_IA = 1u << 8,    // thin-lens / phase / grating interactions (ort_interaction)
   F_AXIAL = 1u << 9, // ORT_LENS_AXIAL: every frame a +z translation (closed-form kernels)
@@ -137,12 +138,17 @@ __device__ inline double tab(const double* t, int n_lambda, int n_mat, int lam, 
 }
 
 // Optical constants of surface si at the ray's wavelength (same scalar-load batch as the
-// surface record when the lens is traced at one wavelength). F_MONO makes that a
-// compile-time fact: with a run-time test the compiler merges both loads into one
-// per-lane vector load through a selected address, a dependent round trip per surface.
+// surface record when the row is wave-uniform). F_MONO makes that a compile-time fact:
+// with a run-time test the compiler merges both loads into one per-lane vector load
+// through a selected address, a dependent round trip per surface. Under F_MONO the host
+// guarantees every lane of a wave has the same wavelength row (one row, or (field, lambda)
+// segments whose boundaries are multiples of 64 rays), so the row index is read from the
+// first active lane into an SGPR.
+__device__ inline int uniform_row(int lam) { return __builtin_amdgcn_readfirstlane(lam); }
+
 template <uint32_t FEAT = 0>
 __device__ inline ort_surface_optics optics_at(const KArgs& a, int lam, int si) {
-  if constexpr ((FEAT & F_MONO) != 0) return cst(a.optics)[si];
+  if constexpr ((FEAT & F_MONO) != 0) return cst(a.optics)[uniform_row(lam) * a.n_surf + si];
   if (a.n_lambda == 1) return cst(a.optics)[si];
   return a.optics[lam * a.n_surf + si];
 }
@@ -175,7 +181,7 @@ template <uint32_t FEAT>
 __device__ inline double final_alpha(const KArgs& a, int lam, double w) {
   if constexpr ((FEAT & F_WRAY) != 0)
     return ort::absorption_alpha(ort::material_k(cst(a.mats)[a.final_mat], a.coef, w), w);
-  if constexpr ((FEAT & F_MONO) != 0) return cst(a.alpha_tab)[a.final_mat];
+  if constexpr ((FEAT & F_MONO) != 0) return cst(a.alpha_tab)[uniform_row(lam) * a.n_mat + a.final_mat];
   return tab(a.alpha_tab, a.n_lambda, a.n_mat, lam, a.final_mat);
 }
 
@@ -904,6 +910,8 @@ KernelFn select_trace(uint32_t feat);      // Newton lenses, any F_GEN / F_REC  
 KernelFn select_closed(uint32_t feat);     // closed-form lenses                (ort_k_closed.hip)
 KernelFn select_generate();                // ray generation only               (ort_k_closed.hip)
 KernelFn select_trace_w(uint32_t feat);    // Newton lenses, per-ray wavelengths (ort_k_trace_w.hip)
+KernelFn select_trace_mono(uint32_t feat); // Newton lenses, F_GEN, wave-uniform wavelength row
+                                           // (ort_k_trace_mono.hip)
 KernelFn select_trace_ia(uint32_t feat);   // thin-lens / phase / grating lenses (ort_k_trace_ia.hip)
 // n(w), k(w) of one material (ort_material_nk)                            (ort_k_closed.hip)
 void launch_material_nk(const ort_material* mats, const double* coef, int32_t mat,
