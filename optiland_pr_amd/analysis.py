@@ -1,6 +1,6 @@
 """Consumers of the trace: SpotDiagram (analysis/spot_diagram.py:40-438) and
-Wavefront / OPD with the chief-ray reference sphere (wavefront/wavefront.py:56-167,
-wavefront/strategy.py:68-239, wavefront/opd.py:71-157).
+Wavefront / OPD with the chief-ray, centroid-anchored and best-fit reference spheres
+(wavefront/wavefront.py:56-167, wavefront/strategy.py:68-514, wavefront/opd.py:71-157).
 
 MI355X-first: SpotDiagram traces EVERY (field, wavelength) pair of the analysis in one
 fused launch (each pair its own Newton group = one reference Optic.trace call) and
@@ -243,6 +243,17 @@ class WavefrontData:
     radius: float
 
 
+def _tilt_direction(optic, field):
+    """strategy.py:141-153: (ux, uy) of an angle field, None otherwise."""
+    if optic.field_type != "angle":
+        return None
+    hx, hy = field
+    max_field_deg = optic.fields.max_field
+    tx, ty = np.tan(np.deg2rad(hx * max_field_deg)), np.tan(np.deg2rad(hy * max_field_deg))
+    uz = 1.0 / np.sqrt(1.0 + tx**2 + ty**2)
+    return tx * uz, ty * uz
+
+
 class ChiefRayStrategy:
     """wavefront/strategy.py:168-239 on the device: the chief ray and the full ray set
     are traced by the HIP kernels; the chief ray's reference sphere is formed on the
@@ -250,7 +261,7 @@ class ChiefRayStrategy:
     OPD, exit-pupil points, rms and tilt-fit sums come from one fused kernel
     (ort_wavefront_opd) instead of a chain of elementwise array operations."""
 
-    def __init__(self, optic, distribution):
+    def __init__(self, optic, distribution, **kwargs):
         self.optic = optic
         self.distribution = distribution
         self.n_image = optic.n()[-1]
@@ -273,14 +284,7 @@ class ChiefRayStrategy:
         return self.n_image * t
 
     def _tilt_direction(self, field):
-        """strategy.py:141-153: (ux, uy) of an angle field, None otherwise."""
-        if self.optic.field_type != "angle":
-            return None
-        hx, hy = field
-        max_field_deg = self.optic.fields.max_field
-        tx, ty = np.tan(np.deg2rad(hx * max_field_deg)), np.tan(np.deg2rad(hy * max_field_deg))
-        uz = 1.0 / np.sqrt(1.0 + tx**2 + ty**2)
-        return tx * uz, ty * uz
+        return _tilt_direction(self.optic, field)
 
     def compute_wavefront_data(self, field, wavelength):
         import ctypes as C
@@ -339,10 +343,180 @@ class ChiefRayStrategy:
         return data
 
 
+def _full(like, v):
+    """A divisor as a device tensor: torch divides by a Python scalar as a multiplication
+    by its reciprocal (not the IEEE quotient the reference's NumPy forms)."""
+    return torch.full_like(like, float(np.ravel(v)[0]))
+
+
+class CentroidReferenceSphereStrategy:
+    """strategy.py:242-402: the reference sphere centred on the (optionally outlier-
+    trimmed) centroid of the image-plane points, its radius the mean distance from that
+    centre to the wavefront points p - (opd / n_image) d; OPD relative to the mean over
+    the rays with i > 0.
+
+    The traced rays and every per-ray array stay on the device (the trace is the HIP
+    kernel, the elementwise chain -- launch-plane tilt, the image-to-sphere distance, OPD
+    in waves, exit-pupil points -- runs there in the reference's operation order). The
+    few reductions that fix the sphere (centroid, mean / std of the distances, the
+    radius, the mean OPD; the best-fit sphere's 4-column least squares) read host copies
+    of the point set and use NumPy exactly as the reference does, so the sphere and
+    every per-ray output are bit-identical to the reference's."""
+
+    def __init__(self, optic, distribution, robust_trim_std=3.0):
+        self.optic = optic
+        self.distribution = distribution
+        self.n_image = optic.n()[-1]
+        self.robust_trim_std = robust_trim_std
+
+    def _points_from_rays(self, h, opd):
+        """strategy.py:325-351 (host arrays)."""
+        valid = (np.isfinite(h["x"]) & np.isfinite(h["y"]) & np.isfinite(h["z"])
+                 & np.isfinite(h["L"]) & np.isfinite(h["M"]) & np.isfinite(h["N"])
+                 & np.isfinite(opd) & (h["i"] != 0))
+        if not np.any(valid):
+            raise ValueError("No valid ray samples found for best-fit sphere.")
+        p = np.stack((h["x"], h["y"], h["z"]), axis=1)[valid]
+        d = np.stack((h["L"], h["M"], h["N"]), axis=1)[valid]
+        s = opd[valid] / self.n_image
+        return p - s[:, None] * d, valid
+
+    def _calculate_reference_sphere(self, h, opd):
+        """strategy.py:353-402 (host arrays)."""
+        wavefront_points, valid_mask = self._points_from_rays(h, opd)
+        image_points = np.stack((h["x"], h["y"], h["z"]), axis=1)[valid_mask]
+        weights = h["i"][valid_mask]
+        weights = np.where(weights < 0.0, 0.0, weights)
+        total_weight = np.sum(weights)
+        if total_weight == 0:
+            weights = np.ones_like(weights)
+        else:  # the reference then weighs every valid point equally (:377-379)
+            weights = np.ones((image_points.shape[0],))
+        total_weight = np.sum(weights)
+        centroid = np.sum(image_points * weights[:, None], axis=0) / total_weight
+        if self.robust_trim_std and self.robust_trim_std > 0:
+            distances_img = np.linalg.norm(image_points - centroid, axis=1)
+            mean_d = np.mean(distances_img)
+            std_d = np.std(distances_img)
+            if std_d > 0:
+                keep_mask = distances_img <= (mean_d + self.robust_trim_std * std_d)
+                if np.sum(keep_mask) >= 4:
+                    weights = weights * np.array(keep_mask)
+                    total_weight = np.sum(weights)
+                    centroid = np.sum(image_points * weights[:, None], axis=0) / total_weight
+        distances_wf = np.linalg.norm(wavefront_points - centroid, axis=1)
+        radius = float(np.sum(weights * distances_wf) / np.sum(weights))
+        return float(centroid[0]), float(centroid[1]), float(centroid[2]), radius
+
+    def _opd_image_to_xp(self, rays, xc, yc, zc, R):
+        """strategy.py:68-116 on the device (tensor ops in the reference's order; the
+        centre's squares formed as the reference forms them, from Python floats)."""
+        xr, yr, zr = rays.x, rays.y, rays.z
+        L, M, N = -rays.L, -rays.M, -rays.N
+        a = L**2 + M**2 + N**2
+        b = 2 * (L * (xr - xc) + M * (yr - yc) + N * (zr - zc))
+        c = (xr**2 + yr**2 + zr**2 - 2 * (xr * xc + yr * yc + zr * zc)
+             + xc**2 + yc**2 + zc**2 - R**2)
+        d = b**2 - 4 * a * c
+        d = torch.where(d < 0, torch.zeros_like(d), d)
+        t = (-b - torch.sqrt(d)) / (2 * a)
+        t = torch.where(t < 0, (-b + torch.sqrt(d)) / (2 * a), t)
+        return float(self.n_image) * t
+
+    def _correct_tilt(self, field, opd, dev):
+        """strategy.py:118-166 over the whole pupil (device)."""
+        tilt = _tilt_direction(self.optic, field)
+        if tilt is None:
+            return opd
+        ux, uy = (float(v) for v in tilt)
+        epd = float(np.ravel(self.optic.paraxial.EPD())[0])
+        xs = torch.as_tensor(np.asarray(self.distribution.x, dtype=np.float64), device=dev)
+        ys = torch.as_tensor(np.asarray(self.distribution.y, dtype=np.float64), device=dev)
+        X_m = xs * epd / 2
+        Y_m = ys * epd / 2
+        return opd + (ux * X_m + uy * Y_m)
+
+    def compute_wavefront_data(self, field, wavelength):
+        """strategy.py:273-323."""
+        rays = self.optic.trace(*field, wavelength, None, self.distribution)
+        dev = rays.x.device
+        opd_c = self._correct_tilt(field, rays.opd, dev)
+        h = {a: getattr(rays, a).cpu().numpy() for a in ("x", "y", "z", "L", "M", "N", "i")}
+        xc, yc, zc, radius = self._calculate_reference_sphere(h, opd_c.cpu().numpy())
+        opd_img = self._opd_image_to_xp(rays, xc, yc, zc, radius)
+        opd = opd_c - opd_img
+        valid = h["i"] > 0
+        if not np.any(valid):
+            raise ValueError("No valid rays with non-zero intensity for OPD calculation.")
+        mean_opd = float(np.mean(opd.cpu().numpy()[valid]))
+        opd_waves = (mean_opd - opd) / _full(opd, wavelength * 1e-3)
+        t = opd_img / _full(opd_img, self.n_image)
+        data = WavefrontData(pupil_x=rays.x - t * rays.L, pupil_y=rays.y - t * rays.M,
+                             pupil_z=rays.z - t * rays.N, opd=opd_waves, intensity=rays.i,
+                             radius=radius)
+        data.sums = None
+        return data
+
+
+class BestFitSphereStrategy(CentroidReferenceSphereStrategy):
+    """strategy.py:405-479: the sphere through the wavefront points in the least-squares
+    sense, 2 x xc + 2 y yc + 2 z zc + (R^2 - |c|^2) = |p|^2, solved by the same LAPACK
+    least squares (numpy.linalg.lstsq) on the same bit-identical point set."""
+
+    def __init__(self, optic, distribution, **kwargs):
+        super().__init__(optic, distribution, **kwargs)
+        self.center = None
+
+    def _calculate_reference_sphere(self, h, opd):
+        wavefront_points, _ = self._points_from_rays(h, opd)
+        if wavefront_points.shape[0] < 4:
+            raise ValueError("Need at least 4 valid ray samples for a best-fit sphere.")
+        x, y, z = wavefront_points[:, 0], wavefront_points[:, 1], wavefront_points[:, 2]
+        A = np.stack([x, y, z, np.ones_like(x)], axis=1)
+        b = x**2 + y**2 + z**2
+        try:
+            c, _, _, _ = np.linalg.lstsq(A, b, rcond=None)
+        except np.linalg.LinAlgError as e:
+            raise RuntimeError(f"Least-squares sphere fit failed: {e}") from e
+        xc, yc, zc = c[0] / 2, c[1] / 2, c[2] / 2
+        radius = np.sqrt(c[3] + xc**2 + yc**2 + zc**2)
+        self.center = (float(xc), float(yc), float(zc))
+        return self.center[0], self.center[1], self.center[2], float(radius)
+
+
+STRATEGIES = {"chief_ray": ChiefRayStrategy,
+              "centroid_sphere": CentroidReferenceSphereStrategy,
+              "best_fit_sphere": BestFitSphereStrategy}
+
+
+def create_strategy(strategy_name, optic, distribution, **kwargs):
+    """strategy.py:489-514."""
+    cls = STRATEGIES.get(strategy_name)
+    if cls is None:
+        raise ValueError(f"Unknown wavefront strategy: {strategy_name}")
+    return cls(optic, distribution, **kwargs)
+
+
 def fit_and_remove_tilt(data, remove_piston=False, ridge=1e-12):
     """wavefront.py:97-143: weighted least-squares piston / tilt plane removed from the
-    OPD, the normal equations' sums from the wavefront kernel (data.sums), the 3 x 3
-    solve on the host and the plane subtracted on the device."""
+    OPD. Chief-ray data carries the normal equations' sums from the wavefront kernel
+    (data.sums): the 3 x 3 solve on the host and the plane subtracted on the device.
+    Otherwise the reference's own NumPy expressions on host copies (a few hundred rays)."""
+    if getattr(data, "sums", None) is None:
+        x, y, w, opd = (t.cpu().numpy() for t in (data.pupil_x, data.pupil_y, data.intensity,
+                                                   data.opd))
+        one = np.ones_like(x)
+        X = np.stack([one, x, y], axis=1)
+        W = np.sqrt(w)[:, None]
+        Xw = X * W
+        yw = opd * np.sqrt(w)
+        XT_X = np.matmul(Xw.T, Xw) + ridge * np.eye(3)
+        XT_y = np.matmul(Xw.T, yw)
+        coeffs = np.linalg.solve(XT_X, XT_y)
+        if not remove_piston:
+            coeffs = coeffs.copy()
+            coeffs[0] = 0.0
+        return torch.as_tensor(opd - X @ coeffs, device=data.opd.device)
     s = data.sums.cpu().numpy()
     _, _, w, wx, wy, wxx, wxy, wyy, wz, wxz, wyz = s
     XT_X = np.array([[w, wx, wy], [wx, wxx, wxy], [wy, wxy, wyy]]) + ridge * np.eye(3)
@@ -354,12 +528,12 @@ def fit_and_remove_tilt(data, remove_piston=False, ridge=1e-12):
 
 
 class Wavefront:
-    """wavefront/wavefront.py:56-167 (chief_ray strategy)."""
+    """wavefront/wavefront.py:56-167 ("chief_ray", "centroid_sphere", "best_fit_sphere";
+    keyword arguments go to the strategy, e.g. robust_trim_std)."""
 
     def __init__(self, optic, fields="all", wavelengths="all", num_rays=12,
-                 distribution="hexapolar", strategy="chief_ray", remove_tilt=False):
-        if strategy != "chief_ray":
-            raise ValueError(f"strategy {strategy!r} is not implemented on the trace core")
+                 distribution="hexapolar", strategy="chief_ray", remove_tilt=False,
+                 **kwargs):
         self.optic = optic
         self.fields = resolve_fields(optic, fields)
         self.wavelengths = resolve_wavelengths(optic, wavelengths)
@@ -371,7 +545,7 @@ class Wavefront:
         if not isinstance(distribution, BaseDistribution) and not hasattr(distribution, "x"):
             raise ValueError("Invalid distribution")
         self.distribution = distribution
-        self.strategy = ChiefRayStrategy(optic, distribution)
+        self.strategy = create_strategy(strategy, optic, distribution, **kwargs)
         self.remove_tilt = remove_tilt
         self.data = {}
         for f in self.fields:
@@ -390,7 +564,7 @@ class OPD(Wavefront):
     """wavefront/opd.py:19-157."""
 
     def __init__(self, optic, field, wavelength, num_rays=15, distribution="hexapolar",
-                 strategy="chief_ray", remove_tilt=False):
+                 strategy="chief_ray", remove_tilt=False, **kwargs):
         if isinstance(wavelength, str):
             if wavelength != "primary":
                 raise ValueError("Invalid wavelength string. For a single wavelength, it "
@@ -398,7 +572,7 @@ class OPD(Wavefront):
             wavelength = optic.primary_wavelength
         super().__init__(optic, fields=[tuple(field)], wavelengths=[float(wavelength)],
                          num_rays=num_rays, distribution=distribution, strategy=strategy,
-                         remove_tilt=remove_tilt)
+                         remove_tilt=remove_tilt, **kwargs)
 
     def rms(self):
         """opd.py:143-157 (from the wavefront kernel's sums unless the tilt was removed)."""

@@ -791,6 +791,39 @@ WAVEFRONT_CASES = {  # name -> (lens builder, field, wavelength, OPD keywords)
 }
 
 
+WAVEFRONT_STRATEGY_CASES = {  # name -> (lens builder, field, wavelength, OPD keywords)
+    "cooke_0_1_centroid": (CookeTriplet, (0, 1), 0.55, {"strategy": "centroid_sphere"}),
+    "cooke_0_07_bestfit": (CookeTriplet, (0, 0.7), 0.48, {"strategy": "best_fit_sphere"}),
+    "cooke_0_1_centroid_notrim": (CookeTriplet, (0, 1), 0.55,
+                                  {"strategy": "centroid_sphere", "robust_trim_std": 0.0}),
+    "dg_0_1_centroid": (DoubleGauss, (0, 1), 0.5876,
+                        {"strategy": "centroid_sphere", "num_rays": 20}),
+    "dg_0_0_bestfit": (DoubleGauss, (0, 0), 0.5876, {"strategy": "best_fit_sphere"}),
+    "dg_0_1_bestfit_notilt": (DoubleGauss, (0, 1), 0.5876,
+                              {"strategy": "best_fit_sphere", "remove_tilt": True}),
+    "finite_pih_03_07_centroid": (None, (0.3, 0.7), 0.55, {"strategy": "centroid_sphere"}),
+}
+
+
+def wavefront_strategy_goldens():
+    """Per-ray WavefrontData of the centroid-anchored and best-fit reference spheres
+    (wavefront/strategy.py:242-479) -> wavefront_strategies.npz: pupil points, OPD in
+    waves, intensity, radius and (best fit) the fitted centre, plus OPD.rms()."""
+    arrays = {}
+    for key, (builder, field, wl, kw) in WAVEFRONT_STRATEGY_CASES.items():
+        builder = builder or finite_pih
+        w = OPD(builder(), field, wl, **kw)
+        d = w.get_data(w.fields[0], w.wavelengths[0])
+        for a in ("pupil_x", "pupil_y", "pupil_z", "opd", "intensity"):
+            arrays[f"{key}/{a}"] = np.asarray(getattr(d, a), dtype=np.float64)
+        arrays[f"{key}/radius"] = np.array(float(d.radius))
+        arrays[f"{key}/rms"] = np.array(float(w.rms()))
+        center = getattr(w.strategy, "center", None)
+        if center is not None:
+            arrays[f"{key}/center"] = np.array([float(c) for c in center])
+    np.savez_compressed(os.path.join(HERE, "wavefront_strategies.npz"), **arrays)
+
+
 def full_size_summaries():
     """Size-independent checks at the BASELINE sizes: DoubleGauss 1M random rays (seed 0)
     and the Cooke config-1 workload (uniform 128, 3 fields)."""
@@ -956,6 +989,9 @@ def main():
     if "--abbe" in sys.argv:  # re-bake optiland_pr_amd/data/abbe_coefficients.json only
         abbe_table()
         return
+    if "--wavefront-strategies" in sys.argv:  # wavefront_strategies.npz only
+        wavefront_strategy_goldens()
+        return
     if "--analysis" in sys.argv:  # index.json "_analysis" + wavefront.npz only
         WAVEFRONT_CASES["finite_pih_03_07"] = (finite_pih,) + WAVEFRONT_CASES["finite_pih_03_07"][1:]
         with open(os.path.join(HERE, "index.json")) as f:
@@ -987,6 +1023,7 @@ def main():
     mixed_wavelength_goldens()
     WAVEFRONT_CASES["finite_pih_03_07"] = (finite_pih,) + WAVEFRONT_CASES["finite_pih_03_07"][1:]
     index["_analysis"] = analysis_goldens()
+    wavefront_strategy_goldens()
     index["_full"] = full_size_summaries()
     with open(os.path.join(HERE, "index.json"), "w") as f:
         json.dump(index, f, indent=1)
