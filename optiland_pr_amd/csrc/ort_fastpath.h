@@ -165,16 +165,17 @@ ORT_INLINE double quot(double a, const SharedDiv& d) {
 #endif
 }
 
-// The same quotient for a divisor known to be > 0: -fma(-r, y, -q0) rounds q0 + r y
-// exactly as fma(r, y, q0) does (round-to-nearest is symmetric), but an exact-zero
-// numerator now keeps its sign (+-0 / b = +-0): fma(r, y, q0) turns -0 / b into +0
-// because r = +0 (an exact sum of opposite zeros), the negated form does not. (For
+// The same quotient for a divisor known to be > 0 with the residual formed negated:
+// rn = fma(b, q0, -a) = -r exactly, and fma(-rn, y, q0) rounds q0 + r y exactly as
+// fma(r, y, q0) does, but an exact-zero numerator keeps its sign (+-0 / b = +-0): for
+// a = -0, rn = (-0) + (+0) = +0 and (-rn) y + q0 = (-0) + (-0) = -0, where the plain
+// form's r = +0 turns -0 / b into +0. The negations are free operand modifiers. (For
 // b < 0 the plain form is the one that is right for both zeros.)
 ORT_INLINE double quot_pos(double a, const SharedDiv& d) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const double q0 = a * d.y;
-  const double r = fma(-d.b, q0, a);
-  return -fma(-r, d.y, -q0);
+  const double rn = fma(d.b, q0, -a);
+  return fma(-rn, d.y, q0);
 #else
   return a / d.b;
 #endif

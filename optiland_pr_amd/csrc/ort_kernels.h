@@ -571,7 +571,10 @@ __device__ inline void closed_surfaces(const KArgs& a, ort::Ray& r, int lam, dou
     } else {
       t = is_plane ? ort::distance_plane(r) : ort::distance_conic(r, s.radius, s.conic, radius_inf);
     }
-    if (!is_plane && s.geometry != ORT_GEOM_STANDARD) {  // not a closed-form id: NaN rays
+    if constexpr (FAST) {
+      // not a closed-form id: a uniform test, left to the exact pass (below)
+      ORT_CHK(bad, s.geometry > ORT_GEOM_STANDARD || s.geometry < ORT_GEOM_PLANE);
+    } else if (!is_plane && s.geometry != ORT_GEOM_STANDARD) {  // NaN rays + status
       t = __builtin_nan("");
       geom_bad = true;
     }
