@@ -104,8 +104,23 @@ __device__ inline double replay_distance(const KArgs& a, const ort_surface& s, i
 }
 
 // P = 2: duals seeded on the point (x, y); P = 4: also on the radius and conic.
+//
+// Occupancy: the Zernike kernels without freeform kinds (KM 4-7, P = 2) need ~230 VGPRs,
+// i.e. 2 waves per SIMD; capped at 128 VGPRs (4 waves, ~400 B of scratch per lane) they
+// run 11% faster on the MI355X (TMA 1M rays: 1283 -> 1135 us per adjoint launch,
+// rocprofv3); 3 waves: 1177 us, 5 waves: 1719 us. Other kernels keep the compiler's
+// choice. ORT_ADJ_WAVES overrides the target for A/B builds.
 template <uint32_t KM, int P>
-__global__ __launch_bounds__(kBlock) void adj_kernel(const KArgs a, const AArgs j) {
+struct AdjWaves {
+  static constexpr int value = (P == 2 && (KM & ort::KM_ZERN) != 0 && KM < ort::KM_FREE) ? 4 : 1;
+};
+#ifdef ORT_ADJ_WAVES
+#define ORT_ADJ_OCC __attribute__((amdgpu_waves_per_eu(ORT_ADJ_WAVES)))
+#else
+#define ORT_ADJ_OCC __attribute__((amdgpu_waves_per_eu(AdjWaves<KM, P>::value)))
+#endif
+template <uint32_t KM, int P>
+__global__ __launch_bounds__(kBlock) ORT_ADJ_OCC void adj_kernel(const KArgs a, const AArgs j) {
   using D = ort::Dual<P>;
   const int64_t rid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool active = rid < a.n_rays;
