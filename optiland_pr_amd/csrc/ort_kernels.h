@@ -382,8 +382,23 @@ __device__ inline void interact(const KArgs& a, const ort_surface& s, ort::Ray& 
     ort::diffract(r, p, nx, ny, nz, o.n_pre, o.n_post, refl, w);
 }
 
+// Occupancy of the Newton kernels: the Zernike kernels (without freeform kinds) need
+// ~115 VGPRs (4 waves per SIMD); capped at 80 (6 waves, ~128 B scratch per lane) the TMA
+// forward runs 9% faster on the MI355X (334 -> 305 us per 1M-ray launch, rocprofv3; 5
+// waves: 313 us). The even-asphere kernels already fit 6 waves; the rest keep the
+// compiler's choice. ORT_TRACE_WAVES overrides the target for A/B builds.
 template <uint32_t FEAT>
-__global__ __launch_bounds__(kBlock) void trace_kernel(const KArgs a) {
+struct TraceWaves {
+  static constexpr int value =
+      ((FEAT & ort::KM_ZERN) != 0 && (FEAT & (ort::KM_FREE | F_IA)) == 0) ? 6 : 1;
+};
+#ifdef ORT_TRACE_WAVES
+#define ORT_TRACE_OCC __attribute__((amdgpu_waves_per_eu(ORT_TRACE_WAVES)))
+#else
+#define ORT_TRACE_OCC __attribute__((amdgpu_waves_per_eu(TraceWaves<FEAT>::value)))
+#endif
+template <uint32_t FEAT>
+__global__ __launch_bounds__(kBlock) ORT_TRACE_OCC void trace_kernel(const KArgs a) {
   const int64_t rid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool active = rid < a.n_rays;
   const int64_t r_ld = active ? rid : 0;  // inactive lanes compute on ray 0, store nothing

@@ -854,6 +854,34 @@ def full_size_summaries():
     return res
 
 
+def full_size_newton():
+    """Size-independent checks of the Newton lenses at the BASELINE ray count: RT-asph
+    (config 3's lens, Hy = 1, 0.5876 um) and the fringe-Zernike TMA (config 5's, Hy = 1,
+    0.587 um), 1M random pupil rays (seed 0) each: NumPy sums of the image x, y, opd, the
+    NaN count, the first / last ray and the Newton update count of every surface."""
+    res = {}
+    for key, builder, hy, wl in (("rt_asph_1m", rt_asph, 1.0, 0.5876),
+                                 ("tma_1m", tma, 1.0, 0.587)):
+        lens = builder()
+        _instrument_newton(lens)
+        _newton_counts.clear()
+        d = RandomDistribution(seed=0)
+        d.generate_points(1_000_000)
+        t0 = time.perf_counter()
+        rays = lens.trace(0.0, hy, wl, num_rays=1_000_000, distribution=d)
+        secs = time.perf_counter() - t0
+        x, y, opd = (np.asarray(getattr(rays, a)) for a in ("x", "y", "opd"))
+        res[key] = dict(
+            n=int(x.size), nan=int(np.isnan(x).sum()), seconds=secs,
+            sum_x=float(np.sum(x)), sum_y=float(np.sum(y)), sum_opd=float(np.sum(opd)),
+            sum_x2=float(np.sum(x * x)),
+            first=[float(x[0]), float(y[0]), float(opd[0])],
+            last=[float(x[-1]), float(y[-1]), float(opd[-1])],
+            newton_updates={str(k): int(v) for k, v in sorted(_newton_counts.items())},
+        )
+    return res
+
+
 MIXED_W_CASES = {  # name -> (builder, field (Hx, Hy), pupil n, wavelength range)
     "cooke": (CookeTriplet, (0.0, 0.7), 24, (0.42, 0.75)),
     "dg": (DoubleGauss, (0.0, 1.0), 24, (0.45, 0.70)),
@@ -989,6 +1017,13 @@ def main():
     if "--abbe" in sys.argv:  # re-bake optiland_pr_amd/data/abbe_coefficients.json only
         abbe_table()
         return
+    if "--full-newton" in sys.argv:  # index.json "_full" Newton entries only
+        with open(os.path.join(HERE, "index.json")) as f:
+            index = json.load(f)
+        index["_full"].update(full_size_newton())
+        with open(os.path.join(HERE, "index.json"), "w") as f:
+            json.dump(index, f, indent=1)
+        return
     if "--wavefront-strategies" in sys.argv:  # wavefront_strategies.npz only
         wavefront_strategy_goldens()
         return
@@ -1025,6 +1060,7 @@ def main():
     index["_analysis"] = analysis_goldens()
     wavefront_strategy_goldens()
     index["_full"] = full_size_summaries()
+    index["_full"].update(full_size_newton())
     with open(os.path.join(HERE, "index.json"), "w") as f:
         json.dump(index, f, indent=1)
 
