@@ -291,7 +291,7 @@ def config5(args, dev, rank, world, torch):
                             "rms_spot_size + backward (VJP) + Adam",
                 "rays_per_gpu": R, "surfaces": S, "parameters": 30,
                 "parallelism": f"dp{world} (independent replicas)"},
-        kernel="vjp_kernel<4, KM_ZERN> (ort_trace_pupil_vjp)", launches=None,
+        kernel="adj_kernel<KM_ZERN, 2> (ort_trace_pupil_vjp, adjoint mode)", launches=None,
         bytes_per_launch=None, flops_per_ray=None, pmc_file=None, rays=R, state=state)
 
 

@@ -1,6 +1,7 @@
 """Summarise rocprofv3 runs of bench.py into profiles/ (measurement tooling, not product).
 
-usage: python tools/profile_hbm.py <round tag> <kernel-trace dir> [<pmc dir> ...]
+usage: python tools/profile_hbm.py <round tag> <kernel-trace dir | -> [<pmc dir> ...]
+                                  [--traffic NAME]   (default hbm_traffic.json)
 
 Writes
   profiles/<tag>_kernel_stats.csv   copy of rocprofv3 --kernel-trace --stats summary
@@ -26,11 +27,19 @@ KERNEL_KEYS = ("trace_kernel", "trace_closed_kernel")
 
 
 def main():
+    argv = list(sys.argv)
+    traffic = "hbm_traffic.json"
+    if "--traffic" in argv:
+        i = argv.index("--traffic")
+        traffic = argv[i + 1]
+        del argv[i:i + 2]
+    sys.argv = argv
     tag, ktrace = sys.argv[1], sys.argv[2]
     prof = os.path.join(REPO, "profiles")
     os.makedirs(prof, exist_ok=True)
-    for f in glob.glob(os.path.join(ktrace, "**", "*kernel_stats.csv"), recursive=True):
-        shutil.copy(f, os.path.join(prof, f"{tag}_kernel_stats.csv"))
+    if ktrace != "-":
+        for f in glob.glob(os.path.join(ktrace, "**", "*kernel_stats.csv"), recursive=True):
+            shutil.copy(f, os.path.join(prof, f"{tag}_kernel_stats.csv"))
     acc = {}
     for d in sys.argv[3:]:
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
@@ -53,7 +62,7 @@ def main():
     out["source"] = f"rocprofv3 PMC passes, round tag {tag}"
     with open(os.path.join(prof, f"{tag}_pmc_summary.json"), "w") as fh:
         json.dump(out, fh, indent=1)
-    with open(os.path.join(prof, "hbm_traffic.json"), "w") as fh:
+    with open(os.path.join(prof, traffic), "w") as fh:
         json.dump(out, fh, indent=1)
     print(json.dumps(out, indent=1))
 
