@@ -107,14 +107,20 @@ int fill_args(KArgs& a, const ort_lens* lens, const ort_batch* batch, const ort_
   return ORT_OK;
 }
 
-int launch(const KArgs& a, uint32_t feat, hipStream_t stream) {
-  if (a.n_rays == 0) return ORT_OK;
+int launch(const KArgs& a_in, uint32_t feat, hipStream_t stream) {
+  if (a_in.n_rays == 0) return ORT_OK;
   KernelFn fn = (feat & F_IA) != 0    ? select_trace_ia(feat & ~F_AXIAL)
                 : (feat & F_KM) == 0 ? select_closed(feat)
                                      : select_trace(feat & ~F_AXIAL);
   if (!fn) return ORT_ERR_ARG;
-  const int64_t blocks = (a.n_rays + kBlock - 1) / kBlock;
+  const int64_t blocks = (a_in.n_rays + kBlock - 1) / kBlock;
   if (blocks > 0x7fffffff) return ORT_ERR_ARG;
+  KArgs a = a_in;
+  // Newton kernels on generated rays whose segments share one pupil: chunk-major block
+  // order (pair_major_ray), where it is a bijection over whole blocks
+  a.block_remap = (feat & F_KM) != 0 && (feat & F_IA) == 0 && (feat & F_GEN) != 0 &&
+                  !a.pupil_per_ray && a.seg && a.n_seg > 1 && a.seg_len % kBlock == 0 &&
+                  a.n_rays == (int64_t)a.n_seg * a.seg_len;
   hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(kBlock), 0, stream, a);
   return hipGetLastError() == hipSuccess ? ORT_OK : ORT_ERR_LAUNCH;
 }

@@ -107,7 +107,30 @@ struct KArgs {
   const double* lambdas;
   // pupil apodization of generated rays (NULL: intensity 1)
   const ort_apodization* apod;
+  // trace_kernel: blocks walk the pupil chunk by chunk over all (field, lambda) segments
+  // (pair_major_ray); set by the host only when it is a bijection (see launch)
+  int32_t block_remap;
 };
+
+// Ray of this thread when every (field, lambda) segment traces the SAME pupil samples
+// (real_ray_tracer.py:74-77 field-major layout: ray = segment * seg_len + p): block b
+// would read pupil chunk b % chunks once per segment, i.e. n_seg times from HBM (the
+// chunks of a 4M-ray pupil do not stay in a 4 MB L2). Blocks are dealt round-robin over
+// the 8 XCDs (MI355X_MICROARCH.md, dispatch), so the blocks sharing an XCD (b % 8) get a
+// contiguous range of the chunk-major order L = chunk * n_seg + segment: every XCD reads
+// each of its pupil chunks once and serves all segments from its L2. Any dispatch order
+// gives the same results (a bijection over blocks); only the traffic depends on it.
+// Requires n_rays == n_seg * seg_len and seg_len % kBlock == 0 (host-checked).
+__device__ inline int64_t pair_major_ray(const KArgs& a) {
+  const int64_t B = gridDim.x;
+  const int64_t b = blockIdx.x;
+  const int64_t x = b & 7, local = b >> 3;
+  int64_t start = 0;
+  for (int64_t y = 0; y < x; ++y) start += (B - y + 7) >> 3;  // blocks of the lower XCD slots
+  const int64_t L = start + local;
+  const int64_t seg = L % a.n_seg, chunk = L / a.n_seg;
+  return seg * a.seg_len + chunk * kBlock + threadIdx.x;
+}
 
 __device__ inline uint64_t wave_and_u64(uint64_t v) {
   for (int o = 32; o > 0; o >>= 1) v &= __shfl_xor(v, o, 64);
@@ -399,7 +422,8 @@ struct TraceWaves {
 #endif
 template <uint32_t FEAT>
 __global__ __launch_bounds__(kBlock) ORT_TRACE_OCC void trace_kernel(const KArgs a) {
-  const int64_t rid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t rid =
+      a.block_remap ? pair_major_ray(a) : (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool active = rid < a.n_rays;
   const int64_t r_ld = active ? rid : 0;  // inactive lanes compute on ray 0, store nothing
 
