@@ -427,3 +427,47 @@ def test_extreme_operands_bit_exact(torch, lens_name):
         np.testing.assert_array_equal(np.signbit(g[ok]), np.signbit(r[ok]),
                                       err_msg=f"{lens_name} sign of {a}")
     assert np.isfinite(got["x"]).sum() > n // 20  # the set is not all NaN
+
+
+@pytest.mark.parametrize("lens_name", ["cooke", "rt_asph"])
+def test_wave_uniform_rows_and_chunk_major_blocks(torch, lens_name):
+    """3 fields x 3 wavelengths of one shared 1024-point pupil: the segments sit on 64- and
+    256-ray boundaries, so the launch takes the scalar wavelength-row kernels (F_MONO with
+    n_lambda > 1) and, for the Newton lens, the XCD-aware chunk-major block order
+    (pair_major_ray). Every pair must equal the oracle's trace of that pair alone:
+    bit-exact for the closed-form lens, the Newton tolerances for RT-asph (incl. the
+    reference's per-pair Newton update counts)."""
+    from oracle import trace_np
+    from optiland_pr_amd.lowering import segment_params
+    from optiland_pr_amd.raytrace import RealRays, lens_for, trace_pupil
+    from optiland_pr_amd.samples import CookeTriplet, ReverseTelephotoAsphere
+
+    lens = CookeTriplet() if lens_name == "cooke" else ReverseTelephotoAsphere()
+    wls = [0.4861, 0.5876, 0.6563]
+    fields = [(0.0, 0.0), (0.0, 0.7), (0.3, 1.0)]
+    n_p = 1024
+    rng = np.random.default_rng(7)
+    rr = np.sqrt(rng.uniform(size=n_p))
+    th = rng.uniform(0.0, 2.0 * np.pi, size=n_p)
+    px, py = rr * np.cos(th), rr * np.sin(th)
+    dl = lens_for(lens, wls)
+    seg = np.stack([segment_params(lens, hx, hy, wi) for hx, hy in fields
+                    for wi in range(len(wls))])
+    n = n_p * len(seg)
+    out = RealRays.empty(n, 0.0)
+    keys = [("wave_uniform", k) for k in range(len(seg))]
+    trace_pupil(dl, seg, torch.as_tensor(px, device="cuda"), torch.as_tensor(py, device="cuda"),
+                out, n, n_p, n_p, keys=keys)
+    torch.cuda.synchronize()
+    got = out.numpy()
+    closed = lens_name == "cooke"
+    for k, sg in enumerate(seg):
+        with np.errstate(all="ignore"):
+            res = trace_np.trace_segment(dl.table, trace_np.generate_rays(sg, px, py),
+                                         int(sg["lambda_idx"]))
+        sl = slice(k * n_p, (k + 1) * n_p)
+        assert_parity(f"{lens_name}[pair {k}]", {a: got[a][sl] for a in FIELDS},
+                      res.rays.as_dict(), closed)
+        if not closed:
+            for s in dl.newton:
+                assert int(dl.sched_cache[keys[k]][s]) == int(res.newton_updates[s]), (k, s)
