@@ -752,7 +752,32 @@ struct JArgs {
   double* grad;            // [n_param], accumulated with atomics
 };
 
+// Sum over the 64 lanes of a wave. With the whole wave active: DPP row operations
+// (VALU moves, no LDS round trip per step): quad_perm xor 1 and xor 2, row_half_mirror,
+// row_mirror (a row of 16 summed in every lane), row_bcast15 / row_bcast31 (rows
+// accumulated into lane 63), then lane 63 read into a scalar. Otherwise the xor
+// butterfly through ds_bpermute. Either way a fixed order: deterministic run to run.
+template <int CTRL, int ROW_MASK>
+__device__ inline double dpp_step(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffll), CTRL, ROW_MASK, 0xf,
+                                             false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, ROW_MASK, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
 __device__ inline double wave_sum(double v) {
+  if (__builtin_amdgcn_read_exec() == ~0ull) {
+    v += dpp_step<0xB1, 0xf>(v);   // quad_perm [1,0,3,2]
+    v += dpp_step<0x4E, 0xf>(v);   // quad_perm [2,3,0,1]
+    v += dpp_step<0x141, 0xf>(v);  // row_half_mirror
+    v += dpp_step<0x140, 0xf>(v);  // row_mirror
+    v += dpp_step<0x142, 0xa>(v);  // row_bcast15 -> rows 1, 3
+    v += dpp_step<0x143, 0xc>(v);  // row_bcast31 -> rows 2, 3
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), 63);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
+    return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+  }
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }

@@ -1,5 +1,5 @@
 // ort_reduce.h -- deterministic block reductions for the analysis kernels
-// (ort_k_spot.hip, ort_k_wavefront.hip): xor-butterfly wave sums, then the block's waves
+// (ort_k_spot.hip, ort_k_wavefront.hip): wave sums (DPP), then the block's waves
 // in index order, so a reduction over fixed chunks is bit-identical run to run.
 #pragma once
 
@@ -9,10 +9,9 @@ namespace ortk {
 
 constexpr int kRedThreads = 256;  // threads per block of the analysis kernels
 
-__device__ inline double wave_sum_xor(double v) {
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
+// wave sums: ort_kernels.h wave_sum (DPP row operations with the whole wave active,
+// the xor butterfly otherwise; a fixed order either way)
+__device__ inline double wave_sum_xor(double v) { return wave_sum(v); }
 __device__ inline double wave_max(double v) {
   for (int o = 32; o > 0; o >>= 1) v = ::fmax(v, __shfl_xor(v, o, 64));
   return v;
