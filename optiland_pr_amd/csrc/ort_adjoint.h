@@ -133,11 +133,19 @@ __global__ __launch_bounds__(kBlock) ORT_ADJ_OCC void adj_kernel(const KArgs a, 
   const int64_t p = a.pupil_per_ray ? r_ld : (r_ld - sidx * a.seg_len);
   const int64_t group = r_ld / a.group_len;
 
-  // wave sum of a per-ray contribution into its slot (one writer per slot and wave)
-  auto emit = [&](int slot, double v) {
+  // wave sum of a per-ray contribution into its slot (one writer per slot and wave).
+  // first: the slot's first contribution from this wave -- a plain store instead of a
+  // read-modify-write whose load the wave would wait for (the same value: 0 + w == w)
+  auto emit = [&](int slot, double v, bool first) {
     if (!cst(j.need)[slot]) return;  // uniform
     const double w = wave_sum(active ? v : 0.0);
-    if ((threadIdx.x & 63) == 0) j.partial[(int64_t)slot * j.n_wave + wave] += w;
+    if ((threadIdx.x & 63) == 0) {
+      double* dst = j.partial + (int64_t)slot * j.n_wave + wave;
+      if (first)
+        *dst = w;
+      else
+        *dst += w;
+    }
   };
 
   // sag and normal of surface s at local (x, y) as duals (sag only for Newton kinds)
@@ -184,9 +192,9 @@ __global__ __launch_bounds__(kBlock) ORT_ADJ_OCC void adj_kernel(const KArgs a, 
 
   // Zernike coefficients at local (x, y): w_sag * d sag / d c plus the slopes' share of
   // the normal's adjoint bn (n = (dzdx, dzdy, -1) / q, q = -1 / nz)
-  auto zern_adj = [&](const ort_surface& s, bool on, double x, double y, double w_sag,
-                      double bnx, double bny, double bnz, double nxv, double nyv,
-                      double nzv) {
+  auto zern_adj = [&](const ort_surface& s, bool on, bool first, double x, double y,
+                      double w_sag, double bnx, double bny, double bnz, double nxv,
+                      double nyv, double nzv) {
     if constexpr ((KM & ort::KM_ZERN) != 0) {
       if (s.geometry == ORT_GEOM_ZERNIKE && j.zparam) {
         const double bn = bnx * nxv + bny * nyv + bnz * nzv;
@@ -195,7 +203,9 @@ __global__ __launch_bounds__(kBlock) ORT_ADJ_OCC void adj_kernel(const KArgs a, 
         const int base = 3 * a.n_surf;
         ort::zernike_coef_adjoint(x, y, s.norm_radius, cst(a.zern), s.coef_off, s.n_coef,
                                   cst(a.coef), w_sag, bdx, bdy,
-                                  [&](int term, double g) { emit(base + term, on ? g : 0.0); });
+                                  [&](int term, double g) {
+                                    emit(base + term, on ? g : 0.0, first);
+                                  });
       }
     }
   };
@@ -278,7 +288,7 @@ __global__ __launch_bounds__(kBlock) ORT_ADJ_OCC void adj_kernel(const KArgs a, 
   if (a.final_mat >= 0) {
     double bd = b.x * r.L + b.y * r.M + b.z * r.N;
     if (alpha_f > 0.0) bd += batt * (-alpha_f * 1e3);
-    emit(3 * a.n_surf + j.n_zern, bd);
+    emit(3 * a.n_surf + j.n_zern, bd, true);
     const double d = a.final_thickness;
     b.L += d * b.x;
     b.M += d * b.y;
@@ -356,7 +366,7 @@ __global__ __launch_bounds__(kBlock) ORT_ADJ_OCC void adj_kernel(const KArgs a, 
       bR = bnx * nx.d[2] + bny * ny.d[2] + bnz * nz.d[2];
       bk = bnx * nx.d[3] + bny * ny.d[3] + bnz * nz.d[3];
     }
-    zern_adj(s, true, x1, y1, 0.0, bnx, bny, bnz, nx.v, ny.v, nz.v);
+    zern_adj(s, true, true, x1, y1, 0.0, bnx, bny, bnz, nx.v, ny.v, nz.v);
 
     // propagation, OPD (|t n|) and absorption adjoint -> t
     double bt = bx1 * q.L + by1 * q.M + bz1 * q.N;
@@ -418,7 +428,7 @@ __global__ __launch_bounds__(kBlock) ORT_ADJ_OCC void adj_kernel(const KArgs a, 
           b.N += tk * bzk;
           tb = tbo + bxk * q.L + byk * q.M + bzk * q.N;
         }
-        zern_adj(s, on, xk, yk, bf, knx, kny, knz, kx.v, ky.v, kz.v);
+        zern_adj(s, on, false, xk, yk, bf, knx, kny, knz, kx.v, ky.v, kz.v);
       }
       // initial guess: the base conic's closed form (newton_raphson.py:131-135). More than
       // kHist updates: the earlier ones are dropped -- their share is scaled by the
@@ -433,9 +443,9 @@ __global__ __launch_bounds__(kBlock) ORT_ADJ_OCC void adj_kernel(const KArgs a, 
       adj_cs_op(b, op);
     }
     bCZ -= b.z;
-    emit(3 * si + 0, bR);
-    emit(3 * si + 1, bk);
-    emit(3 * si + 2, bCZ);
+    emit(3 * si + 0, bR, true);
+    emit(3 * si + 1, bk, true);
+    emit(3 * si + 2, bCZ, true);
   }
 }
 
