@@ -242,6 +242,24 @@ def config4(args, dev, rank, world, torch):
         if world > 1:
             distributed.gather_image_plane(out.x, out.y, n_loc, len(pairs), n_p)
 
+    def gather_report(reps=5):
+        """The gather alone, after the timed region (every rank): bytes each rank sends
+        and the max-over-ranks time per gather."""
+        sent = 2 * 8 * n  # x, y doubles of this rank's slices
+        if world == 1:
+            return {"gather_bytes_per_rank": 0, "gather_ms": 0.0}
+        import torch.distributed as dist
+
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            distributed.gather_image_plane(out.x, out.y, n_loc, len(pairs), n_p)
+        torch.cuda.synchronize()
+        t = torch.tensor([(time.perf_counter() - t0) / reps], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return {"gather_bytes_per_rank": sent, "gather_ms": float(t.item()) * 1e3}
+
     return Workload(
         metric="ray-surface intersections/sec, ReverseTelephoto 7 fields x 7 lambda x 2M rays, "
                "sharded + RCCL gather of image-plane hits",
@@ -252,7 +270,7 @@ def config4(args, dev, rank, world, torch):
                 "parallelism": f"dp{world} (pupil shards of every pair) + all_gather"},
         kernel="trace_closed_kernel<F_GEN> (ort_trace_pupil)", launches=1,
         bytes_per_launch=n * (16 + 64), flops_per_ray=None, pmc_file="hbm_traffic_c4.json",
-        rays=n)
+        rays=n, extra=gather_report)
 
 
 def config5(args, dev, rank, world, torch):
@@ -377,6 +395,7 @@ def main():
 
     value = w.units * args.steps / elapsed
     ms_per_step = elapsed / args.steps * 1e3
+    extra = w.extra() if getattr(w, "extra", None) else None  # every rank (collectives)
 
     if rank == 0:
         line = {
@@ -407,6 +426,8 @@ def main():
         elif getattr(w, "state", None):
             loss = w.state.get("loss")
             line["config"]["final_loss"] = None if loss is None else float(loss)
+        if extra:
+            line["config"].update(extra)
         line["cpu_baseline"] = cpu_line
         print(json.dumps(line), flush=True)
     if world > 1:
