@@ -471,3 +471,37 @@ def test_wave_uniform_rows_and_chunk_major_blocks(torch, lens_name):
         if not closed:
             for s in dl.newton:
                 assert int(dl.sched_cache[keys[k]][s]) == int(res.newton_updates[s]), (k, s)
+
+
+def test_resident_rays_wave_uniform_rows(torch):
+    """ort_trace_sequential on resident rays of 3 (field, wavelength) segments of 256 rays
+    each (segment boundaries on waves: the scalar wavelength-row closed-form kernel):
+    every segment bit-exact against the oracle's trace of its rays at its wavelength."""
+    from oracle import trace_np
+    from optiland_pr_amd.lowering import segment_params
+    from optiland_pr_amd.raytrace import RealRays, lens_for, trace_rays
+    from optiland_pr_amd.samples import CookeTriplet
+
+    lens = CookeTriplet()
+    wls = [0.48, 0.55, 0.65]
+    dl = lens_for(lens, wls)
+    n_p = 256
+    rng = np.random.default_rng(3)
+    rr = np.sqrt(rng.uniform(size=n_p))
+    th = rng.uniform(0.0, 2.0 * np.pi, size=n_p)
+    px, py = rr * np.cos(th), rr * np.sin(th)
+    seg = np.stack([segment_params(lens, 0.0, hy, wi) for wi, hy in enumerate((0.0, 0.5, 1.0))])
+    gen = [trace_np.generate_rays(sg, px, py) for sg in seg]
+    cat = {a: np.concatenate([getattr(g, a) for g in gen]) for a in ("x", "y", "z", "L", "M", "N")}
+    rin = RealRays(cat["x"], cat["y"], cat["z"], cat["L"], cat["M"], cat["N"], 1.0, 0.0)
+    rout = RealRays.empty(len(rin), 0.0)
+    trace_rays(dl, rin, rout, group_len=n_p, keys=[("res_wu", k) for k in range(len(seg))],
+               segments=seg, seg_len=n_p)
+    torch.cuda.synchronize()
+    got = rout.numpy()
+    for k, sg in enumerate(seg):
+        ref = trace_np.trace_segment(dl.table, trace_np.generate_rays(sg, px, py),
+                                     int(sg["lambda_idx"])).rays
+        sl = slice(k * n_p, (k + 1) * n_p)
+        assert_parity(f"cooke resident[seg {k}]", {a: got[a][sl] for a in FIELDS},
+                      ref.as_dict(), True)
