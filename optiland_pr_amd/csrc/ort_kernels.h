@@ -318,10 +318,17 @@ __device__ inline double grid_distance(const KArgs& a, const ort_surface& s, int
 }
 
 // Newton refinement of t at surface s for one lane (newton_raphson.py:119-168).
+// hn: set when (nnx, nny, nnz) hold the normal at the returned t -- the last evaluation
+// is at P(t) itself (the stop test), and the point r + t D it evaluates is, operation
+// for operation, the propagated point Surface.trace takes the normal at
+// (standard_surface.py:215-225, homogeneous.py:45-47), so that normal is the
+// interaction's normal: one sag + normal evaluation per Newton surface saved.
 template <uint32_t FEAT>
 __device__ inline double newton_distance(const KArgs& a, const ort_surface& s, int si,
                                          const ort::Ray& r, bool active, int64_t group,
-                                         bool group_uniform, int& range_bits) {
+                                         bool group_uniform, int& range_bits, bool& hn,
+                                         double& nnx, double& nny, double& nnz) {
+  hn = false;
   if constexpr ((FEAT & ort::KM_FREE) != 0) {
     if (s.geometry == ORT_GEOM_GRID_SAG)
       return grid_distance<FEAT>(a, s, si, r, active, group, group_uniform);
@@ -340,7 +347,13 @@ __device__ inline double newton_distance(const KArgs& a, const ort_surface& s, i
                                                       t, true, rerr, nx, ny, nz);
       if (active && rerr) range_bits |= range_bit(s);
       const bool conv = !active || !(fabs(f) >= tol);
-      if (__all(conv)) break;
+      if (__all(conv)) {
+        hn = true;
+        nnx = nx;
+        nny = ny;
+        nnz = nz;
+        break;
+      }
       t = ort::newton_step(r, t, f, nx, ny, nz);
     }
     if (a.stats && (threadIdx.x & 63) == 0)
@@ -357,19 +370,27 @@ __device__ inline double newton_distance(const KArgs& a, const ort_surface& s, i
     if (lane_on) {
       bool rerr = false;
       double nx, ny, nz;
-      const bool upd = j < U;  // sag + normal at P(t) for an update, the sag alone after
+      const bool upd = j < U;  // sag + normal at P(t): for the update, or (j == U) for the
+                               // interaction at the returned t
       const double f = ort::newton_eval<(FEAT & F_KM)>(s, s.radius, s.conic, cst(a.coef), cst(a.zern), kNoSeed, r,
-                                                      t, upd, rerr, nx, ny, nz);
+                                                      t, true, rerr, nx, ny, nz);
       // the reference evaluates sag at j = 0..U-1 always, and at j = U only when the
       // loop broke there (U < max_iter)
       if (rerr && (j < U || U < max_iter)) range_bits |= range_bit(s);
       const bool conv = fabs(f) < tol;  // NaN never converges (np.max propagates NaN)
       if (conv) mask.set(j, a.conv_base);
       if (!conv) last_bad = j;
-      if (upd) t = ort::newton_step(r, t, f, nx, ny, nz);
+      if (upd) {
+        t = ort::newton_step(r, t, f, nx, ny, nz);
+      } else {
+        nnx = nx;
+        nny = ny;
+        nnz = nz;
+      }
     }
   }
   report_newton(a, si, active, group, group_uniform, mask, last_bad);
+  hn = true;  // every active lane evaluated j == U (inactive lanes store nothing)
   return t;
 }
 
@@ -465,6 +486,8 @@ __global__ __launch_bounds__(kBlock) ORT_TRACE_OCC void trace_kernel(const KArgs
     const ort_surface_optics o = surface_optics<FEAT>(a, s, lam, si, wl);
     localize(a, s, r);
     double t;
+    bool hn = false;  // (hnx, hny, hnz): the Newton geometry's normal at t
+    double hnx = 0.0, hny = 0.0, hnz = 0.0;
     if (!known_geometry(s.geometry)) range_bits |= ORT_STATUS_BAD_GEOMETRY;
     if (s.geometry == ORT_GEOM_PLANE) {
       t = ort::distance_plane(r);
@@ -472,7 +495,8 @@ __global__ __launch_bounds__(kBlock) ORT_TRACE_OCC void trace_kernel(const KArgs
       t = ort::distance_conic(r, s.radius, s.conic, (s.flags & ORT_SURF_RADIUS_INF) != 0);
     } else {
       if constexpr ((FEAT & F_KM) != 0) {
-        t = newton_distance<FEAT>(a, s, si, r, active, group, group_uniform, range_bits);
+        t = newton_distance<FEAT>(a, s, si, r, active, group, group_uniform, range_bits, hn,
+                                  hnx, hny, hnz);
       } else {
         t = __builtin_nan("");  // unreachable: the host sets geometry_mask
       }
@@ -489,8 +513,19 @@ __global__ __launch_bounds__(kBlock) ORT_TRACE_OCC void trace_kernel(const KArgs
       if (s.flags & ORT_SURF_APERTURE_PROG) ort::clip_program(r, cst(a.coef) + s.ap_off, s.ap_len);
       interact<FEAT>(a, s, r, o, lam, wl, unnorm);
     } else if constexpr ((FEAT & F_KM) != 0) {
-      ort::finish_surface<(FEAT & F_KM)>(r, s, s.radius, s.conic, cst(a.coef), cst(a.zern), kNoSeed, t, n_pre, u,
-                                         alpha);
+      if (hn) {  // finish_surface with the normal of the last Newton evaluation
+        ort::propagate(r, t, alpha);
+        ort::add_opd(r, t, n_pre);
+        if (s.flags & ORT_SURF_APERTURE) ort::clip_radial(r, s.ap_rmax2, s.ap_rmin2);
+        if (s.flags & ORT_SURF_APERTURE_PROG) ort::clip_program(r, cst(a.coef) + s.ap_off, s.ap_len);
+        if (s.flags & ORT_SURF_REFLECTIVE)
+          ort::reflect(r, hnx, hny, hnz);
+        else
+          ort::refract(r, hnx, hny, hnz, u);
+      } else {
+        ort::finish_surface<(FEAT & F_KM)>(r, s, s.radius, s.conic, cst(a.coef), cst(a.zern), kNoSeed, t, n_pre, u,
+                                           alpha);
+      }
     } else {
       // closed-form geometries only: plane / conic normal inline
       ort::propagate(r, t, alpha);
@@ -957,7 +992,10 @@ __global__ __launch_bounds__(kBlock) void geom_kernel(const KArgs a, const GArgs
       t = ort::distance_conic(r, s.radius, s.conic, (s.flags & ORT_SURF_RADIUS_INF) != 0);
     } else {
       if constexpr (KM != 0) {
-        t = newton_distance<KM>(a, s, g.surface, r, active, 0, true, range_bits);
+        bool hn;
+        double hnx, hny, hnz;
+        t = newton_distance<KM>(a, s, g.surface, r, active, 0, true, range_bits, hn, hnx, hny,
+                                hnz);
       } else {
         t = __builtin_nan("");
       }
