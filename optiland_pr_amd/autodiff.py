@@ -160,14 +160,15 @@ class _TracePupilFn(torch.autograd.Function if torch is not None else object):
         from .raytrace import RealRays, trace_pupil
 
         dl = plan["dlens"]
-        out = RealRays.empty(plan["n"], plan["wavelength"], device=dl.device)
+        out = RealRays.__new__(RealRays)  # the 8 traced fields (w is not an output)
+        for a in _abi.RAY_FIELDS:
+            setattr(out, a, torch.empty(plan["n"], dtype=torch.float64, device=dl.device))
         trace_pupil(dl, plan["seg_dev"], plan["px"], plan["py"], out, plan["n"],
                     plan["seg_len"], plan["n"], keys=plan["keys"])
         sched = dl.last_schedule
         ctx.plan = plan
         ctx.set_materialize_grads(False)
-        ctx.sched_dev = (None if sched is None else
-                         torch.from_numpy(np.ascontiguousarray(sched.reshape(-1))).to(dl.device))
+        ctx.sched_dev = None if sched is None else dl.resident("sched", sched.reshape(-1))
         ctx.shapes = [(t.numel(), t.shape, t.device, t.dtype) for t in tensors]
         return tuple(getattr(out, a) for a in _abi.RAY_FIELDS)
 
@@ -260,9 +261,8 @@ def trace_pupil_grad(optic, dlens, seg_dev, px, py, n, seg_len, wavelength, keys
     parameter tensors of parameters(optic)."""
     params = parameters(optic)
     zp, st, ft, n_param, _ = tangent_tables(dlens.table, params)
-    dev = dlens.device
-    tables = tuple(None if a is None else torch.from_numpy(np.ascontiguousarray(a)).to(dev)
-                   for a in (zp, st, ft))
+    tables = tuple(None if a is None else dlens.resident(("tangent", i), a)
+                   for i, a in enumerate((zp, st, ft)))
     plan = dict(dlens=dlens, seg_dev=seg_dev, px=px, py=py, n=n, seg_len=seg_len,
                 wavelength=wavelength, keys=keys, n_param=n_param, tables=tables)
     return _TracePupilFn.apply(plan, *[t for _, _, t in params])

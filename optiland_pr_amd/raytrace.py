@@ -155,6 +155,24 @@ class DeviceLens:
         self.apod = None if table.apod is None else _to_device_bytes(table.apod, d)
         self.newton = table.newton_surfaces
         self.sched_cache: dict = {}
+        self._resident: dict = {}
+
+    def resident(self, slot, arr):
+        """A read-only HBM copy of a small host array, reused while its bytes are
+        unchanged: segment descriptors, Newton schedules and tangent tables are the same
+        from one optimisation step to the next, and each fresh upload is a pageable
+        host-to-device copy the host waits on."""
+        a = np.ascontiguousarray(arr)
+        raw = a.tobytes()
+        hit = self._resident.get(slot)
+        if hit is not None and hit[0] == raw and hit[1] == a.dtype:
+            return hit[2]
+        if a.dtype.fields is not None:
+            t = torch.from_numpy(np.frombuffer(raw, dtype=np.uint8).copy()).to(self.device)
+        else:
+            t = torch.from_numpy(a.copy()).to(self.device)
+        self._resident[slot] = (raw, a.dtype, t)
+        return t
 
     def patch_coefficients(self, device_coeffs):
         """Write device-resident Zernike coefficients into the uploaded term table
@@ -296,8 +314,10 @@ def _run(dlens: DeviceLens, launch, n_rays, group_len, keys, newton_mode="refere
     S = dlens.table.n_surfaces
     n_groups = max(1, -(-n_rays // group_len))
     need_status = with_status and dlens.table.has_range_check
-    status = torch.zeros(1, dtype=torch.int32, device=dev) if need_status else None
     dlens.last_schedule = None  # the verified [n_groups][S] update counts (VJP replay)
+    status = None
+    if need_status and (not dlens.newton or n_rays == 0 or newton_mode == "wave"):
+        status = torch.zeros(1, dtype=torch.int32, device=dev)
     if not dlens.newton or n_rays == 0:
         opt = _native.ort_options(_abi.NEWTON_SCHEDULE, 0, None)
         launch(opt, None, status)
@@ -312,22 +332,31 @@ def _run(dlens: DeviceLens, launch, n_rays, group_len, keys, newton_mode="refere
     if len(keys) != n_groups:
         keys = [("group", g) for g in range(n_groups)]
     sched = dlens.initial_schedule(keys)
-    stats = torch.empty(n_groups * S * _abi.NEWTON_STAT.itemsize, dtype=torch.uint8, device=dev)
+    # the Newton statistics and the status word share one buffer: the host reads both
+    # with the one copy the schedule check needs (no second synchronising read)
+    nb = n_groups * S * _abi.NEWTON_STAT.itemsize
+    buf = torch.empty(nb + (8 if need_status else 0), dtype=torch.uint8, device=dev)
+    stats = buf[:nb]
+    if need_status:
+        status = buf[nb:nb + 4].view(torch.int32)
+        status.zero_()
     for _ in range(64):
-        sched_dev = torch.from_numpy(sched.reshape(-1).copy()).to(dev)
+        sched_dev = dlens.resident("sched", sched.reshape(-1))
         windows = {}
         base = 0
         while True:  # conv_mask windows of this schedule until verify can decide
             opt = _native.ort_options(_abi.NEWTON_SCHEDULE, 0, sched_dev.data_ptr(), base)
             launch(opt, stats, status)
-            windows[base] = stats.cpu().numpy().view(_abi.NEWTON_STAT).reshape(n_groups, S)
+            host = buf.cpu().numpy()
+            windows[base] = host[:nb].view(_abi.NEWTON_STAT).reshape(n_groups, S)
             ok, new, base = dlens.verify(sched, windows)
             if base is None:
                 break
         if ok:
             dlens.remember(keys, sched)
             dlens.last_schedule = sched
-            _raise_status(status)
+            if need_status:
+                _raise_status_value(int(host[nb:nb + 4].view(np.int32)[0]))
             return
         sched = new
     raise RuntimeError("Newton schedule did not settle")
@@ -336,7 +365,10 @@ def _run(dlens: DeviceLens, launch, n_rays, group_len, keys, newton_mode="refere
 def _raise_status(status):
     if status is None:
         return
-    v = int(status.item())
+    _raise_status_value(int(status.item()))
+
+
+def _raise_status_value(v):
     if v & _abi.STATUS_BAD_GEOMETRY:
         raise ValueError("the lens table holds a geometry id the trace core does not know "
                          "(library / host ABI mismatch?)")
@@ -357,7 +389,8 @@ def trace_pupil(dlens: DeviceLens, segments, px, py, out: RealRays, n_rays,
     """Generate + trace in one launch (ort_trace_pupil). `segments` is a host SEGMENT array
     or the device tensor returned by upload_segments (no per-call copy)."""
     lib = _native.load()
-    seg_dev = segments if torch.is_tensor(segments) else upload_segments(segments, dlens.device)
+    seg_dev = (segments if torch.is_tensor(segments) else
+               dlens.resident("segments", np.asarray(segments, dtype=_abi.SEGMENT)))
     n_seg = seg_dev.numel() // _abi.SEGMENT.itemsize
     batch = _native.ort_batch(n_rays, seg_len, group_len, n_seg, int(pupil_per_ray),
                               seg_dev.data_ptr())
@@ -543,18 +576,21 @@ class RealRayTracer:
         if float(dlens.table.final_thickness) != 0.0:
             raise NotImplementedError("differentiable trace with a non-zero image-space "
                                       "thickness (last surface) is not supported")
-        seg_dev = upload_segments(segs, dlens.device)
+        seg_dev = dlens.resident("segments", np.asarray(segs, dtype=_abi.SEGMENT))
         if record_all:  # non-differentiable records of every surface first
             rec = torch.empty(dlens.table.n_rec * 8 * n, dtype=torch.float64, device=dlens.device)
             tmp = RealRays.empty(n, wavelength, device=dlens.device)
             trace_pupil(dlens, seg_dev, px, py, tmp, n, n_p, n, keys=keys, rec=rec)
             self._record(dlens, tmp, rec, n, segs, px, py, n_p)
+        # queued ahead of the trace: the host waits on the trace's Newton check, and what
+        # it issues after that is on the step's critical path
+        w = torch.full((n,), float(wavelength), dtype=torch.float64, device=dlens.device)
         outs = autodiff.trace_pupil_grad(self.optic, dlens, seg_dev, px, py, n, n_p,
                                          wavelength, keys)
         out = RealRays.__new__(RealRays)
         for a, t in zip(_abi.RAY_FIELDS, outs, strict=True):
             setattr(out, a, t)
-        out.w = torch.full((n,), float(wavelength), dtype=torch.float64, device=dlens.device)
+        out.w = w
         out.is_normalized = True
         sg = self.optic.surface_group
         if not record_all:

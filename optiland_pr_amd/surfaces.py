@@ -188,6 +188,23 @@ def _make_geometry(surface_type, cs, kw):
         "polynomial, chebyshev, biconic, toroidal, forbes_qbfs, forbes_q2d, grid_sag).")
 
 
+_NAN_ROWS: dict = {}
+
+
+def _nan_rows(k, n, device):
+    """A [k][n] float64 NaN block (never handed out: only read by torch.cat)."""
+    import torch
+
+    key = (k, n, str(device))
+    t = _NAN_ROWS.get(key)
+    if t is None:
+        if len(_NAN_ROWS) >= 4:
+            _NAN_ROWS.clear()
+        t = torch.full((k, n), float("nan"), dtype=torch.float64, device=device)
+        _NAN_ROWS[key] = t
+    return t
+
+
 class SurfaceGroup:
     """surface_group.py:30-330."""
 
@@ -227,6 +244,12 @@ class SurfaceGroup:
         if torch is not None and any(torch.is_tensor(v) for v in vals):
             n = max(int(v.numel()) if torch.is_tensor(v) else len(v) for v in vals)
             dev = next(v.device for v in vals if torch.is_tensor(v))
+            last = vals[-1]
+            if (torch.is_tensor(last) and last.numel() == n and last.dtype == torch.float64
+                    and not any(torch.is_tensor(v) and v.numel() == n for v in vals[:-1])):
+                # the default: only the image surface is recorded -- one copy of a cached
+                # NaN block instead of a fill per unrecorded surface
+                return torch.cat((_nan_rows(len(vals) - 1, n, dev), last.reshape(1, n)))
             # surfaces without a record (only the image surface is recorded by default)
             rows = [v if torch.is_tensor(v) and v.numel() == n
                     else torch.full((n,), float("nan"), dtype=torch.float64, device=dev)
