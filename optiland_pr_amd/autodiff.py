@@ -209,6 +209,10 @@ def vjp_mode(table):
 
 _WORKSPACE = {}
 
+# Measurement hook (bench.py config 5): when a list, every vjp() appends a pair of
+# timing events recorded on the launch stream around ort_trace_pupil_vjp
+VJP_EVENTS = None
+
 
 def _workspace(device, nbytes):
     """Device scratch for the adjoint VJP, grown on demand and reused (per device)."""
@@ -250,10 +254,17 @@ def vjp(dlens, seg_dev, px, py, n, seg_len, sched_dev, tables, n_param, cot, gra
         params.workspace = ws.data_ptr()
         params.workspace_size = ws.numel()
     cot_c = _native.ort_rays(*(0 if c is None else c.data_ptr() for c in cot))
+    timer = VJP_EVENTS
+    if timer is not None:
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record(torch.cuda.current_stream())
     rc = lib.ort_trace_pupil_vjp(C.byref(dlens.c), _ptr(px), _ptr(py), C.byref(batch),
                                  C.byref(opt), C.byref(params), C.byref(cot_c), _ptr(grad),
                                  _stream_handle())
     _native.check(rc, "ort_trace_pupil_vjp")
+    if timer is not None:
+        ev[1].record(torch.cuda.current_stream())
+        timer.append(ev)
 
 
 def trace_pupil_grad(optic, dlens, seg_dev, px, py, n, seg_len, wavelength, keys):

@@ -2,6 +2,7 @@
 
 usage: python tools/profile_hbm.py <round tag> <kernel-trace dir | -> [<pmc dir> ...]
                                   [--traffic NAME]   (default hbm_traffic.json)
+                                  [--kernel SUBSTR]  (default: the trace kernels)
 
 Writes
   profiles/<tag>_kernel_stats.csv   copy of rocprofv3 --kernel-trace --stats summary
@@ -33,6 +34,11 @@ def main():
         i = argv.index("--traffic")
         traffic = argv[i + 1]
         del argv[i:i + 2]
+    keys = KERNEL_KEYS
+    if "--kernel" in argv:
+        i = argv.index("--kernel")
+        keys = (argv[i + 1],)
+        del argv[i:i + 2]
     sys.argv = argv
     tag, ktrace = sys.argv[1], sys.argv[2]
     prof = os.path.join(REPO, "profiles")
@@ -44,12 +50,12 @@ def main():
     for d in sys.argv[3:]:
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             for r in csv.DictReader(open(f)):
-                if not any(k in r.get("Kernel_Name", "") for k in KERNEL_KEYS):
+                if not any(k in r.get("Kernel_Name", "") for k in keys):
                     continue
                 acc.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
     per = {c: sum(v) / len(v) for c, v in acc.items()}
     if not per:
-        print("no PMC rows for the trace kernel")
+        print(f"no PMC rows for {keys}")
         return
     out = {"per_dispatch": per}
     if "FETCH_SIZE" in per and "WRITE_SIZE" in per:
