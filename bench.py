@@ -242,6 +242,20 @@ def config4(args, dev, rank, world, torch):
         if world > 1:
             distributed.gather_image_plane(out.x, out.y, n_loc, len(pairs), n_p)
 
+    def trace_ms(steps):
+        """Device time of the trace launch alone (at N > 1 the step also gathers): events
+        on the launch stream around each launch, over extra steps after the timed region."""
+        stream = torch.cuda.current_stream()
+        spans = []
+        for _ in range(steps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            trace_pupil(dl, seg_dev, px, py, out, n, n_loc, n, pupil_per_ray=True)
+            e1.record(stream)
+            spans.append((e0, e1))
+        torch.cuda.synchronize()
+        return sum(a.elapsed_time(b) for a, b in spans) / steps
+
     def gather_report(reps=5):
         """The gather alone, after the timed region (every rank): bytes each rank sends
         and the max-over-ranks time per gather."""
@@ -270,7 +284,8 @@ def config4(args, dev, rank, world, torch):
                 "parallelism": f"dp{world} (pupil shards of every pair) + all_gather"},
         kernel="trace_closed_kernel<F_GEN> (ort_trace_pupil)", launches=1,
         bytes_per_launch=n * (16 + 64), flops_per_ray=None, pmc_file="hbm_traffic_c4.json",
-        rays=n, extra=gather_report)
+        rays=n, extra=gather_report, trace_timer=trace_ms if world > 1 else None,
+        traffic_scale=n / (n_p * len(pairs)))  # the PMC pass traced all pairs on one GPU
 
 
 def config5(args, dev, rank, world, torch):
@@ -354,6 +369,10 @@ def main():
                     help="untimed steps before the warmup until the GPU clock has ramped "
                          "(MI355X power management raises the engine clock only under "
                          "sustained load: the first ~50 ms of launches run up to 15%% slower)")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process group for N > 1 (nccl = RCCL, one GPU per rank); gloo "
+                         "lets several ranks share a GPU (rank r on device r mod count) to "
+                         "rehearse the multi-rank path on a one-GPU box")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -368,10 +387,15 @@ def main():
     import torch
     import torch.distributed as dist
 
+    dev_idx = 0
     if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    dev = torch.device("cuda", local_rank if world > 1 else 0)
+        dev_idx = local_rank if args.backend == "nccl" else local_rank % torch.cuda.device_count()
+        torch.cuda.set_device(dev_idx)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_idx))
+        else:
+            dist.init_process_group("gloo")
+    dev = torch.device("cuda", dev_idx)
 
     from optiland_pr_amd import _native
 
@@ -407,7 +431,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = ev0.elapsed_time(ev1) / args.steps
+    kern_ms = step_dev_ms = ev0.elapsed_time(ev1) / args.steps
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -418,6 +442,8 @@ def main():
     extra = w.extra() if getattr(w, "extra", None) else None  # every rank (collectives)
     if getattr(w, "vjp_timer", None):
         w.vjp_ms = w.vjp_timer(w.step, max(3, min(args.steps, 20)), torch)
+    if getattr(w, "trace_timer", None):
+        kern_ms = w.trace_timer(max(3, min(args.steps, 20)))
 
     if rank == 0:
         line = {
@@ -436,8 +462,11 @@ def main():
             "config": w.config,
             "roofline": _roofline(w, kern_ms),
             "timing": {"clock_ramp_s": args.ramp_seconds,
-                       "device_ms_per_step": kern_ms,
-                       "kernel_time": "HIP events at both ends of the timed region / steps"},
+                       "device_ms_per_step": step_dev_ms,
+                       "kernel_time": "HIP events at both ends of the timed region / steps"
+                       + ("; roofline kernel_ms = the trace launch alone (events around "
+                          "each launch, after the timed region: the step also gathers)"
+                          if getattr(w, "trace_timer", None) else "")},
         }
         if w.flops_per_ray is not None:
             line["roofline_fp64"] = _roofline_fp64(w, kern_ms)
@@ -494,7 +523,8 @@ def _roofline(w, kern_ms):
         "peak": SPEC_HBM_TBPS * 1e3,
         "unit": "GB/s",
         "frac": achieved / (SPEC_HBM_TBPS * 1e3),
-        "traffic": pmc.get("bytes_per_launch"),
+        "traffic": None if pmc.get("bytes_per_launch") is None else
+        pmc["bytes_per_launch"] * getattr(w, "traffic_scale", 1.0),
         "kernel": w.kernel,
         "kernel_ms": kern_ms,
         "algorithmic_bytes_per_launch": w.bytes_per_launch,
