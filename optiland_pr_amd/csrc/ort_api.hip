@@ -109,11 +109,13 @@ int fill_args(KArgs& a, const ort_lens* lens, const ort_batch* batch, const ort_
 
 int launch(const KArgs& a_in, uint32_t feat, hipStream_t stream) {
   if (a_in.n_rays == 0) return ORT_OK;
-  KernelFn fn = (feat & F_IA) != 0    ? select_trace_ia(feat & ~F_AXIAL)
-                : (feat & F_KM) == 0 ? select_closed(feat)
-                                     : select_trace(feat & ~F_AXIAL);
+  const bool closed = (feat & F_IA) == 0 && (feat & F_KM) == 0;
+  KernelFn fn = (feat & F_IA) != 0 ? select_trace_ia(feat & ~F_AXIAL)
+                : closed           ? select_closed(feat)
+                                   : select_trace(feat & ~F_AXIAL);
   if (!fn) return ORT_ERR_ARG;
-  const int64_t blocks = (a_in.n_rays + kBlock - 1) / kBlock;
+  const int bs = closed ? closed_block() : kBlock;
+  const int64_t blocks = (a_in.n_rays + bs - 1) / bs;
   if (blocks > 0x7fffffff) return ORT_ERR_ARG;
   KArgs a = a_in;
   // Newton kernels on generated rays whose segments share one pupil: chunk-major block
@@ -121,7 +123,7 @@ int launch(const KArgs& a_in, uint32_t feat, hipStream_t stream) {
   a.block_remap = (feat & F_KM) != 0 && (feat & F_IA) == 0 && (feat & F_GEN) != 0 &&
                   !a.pupil_per_ray && a.seg && a.n_seg > 1 && a.seg_len % kBlock == 0 &&
                   a.n_rays == (int64_t)a.n_seg * a.seg_len;
-  hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(kBlock), 0, stream, a);
+  hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(bs), 0, stream, a);
   return hipGetLastError() == hipSuccess ? ORT_OK : ORT_ERR_LAUNCH;
 }
 

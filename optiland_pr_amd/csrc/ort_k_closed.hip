@@ -43,6 +43,8 @@ void launch_material_nk(const ort_material* mats, const double* coef, int32_t ma
                      mats, coef, mat, w, n, n_out, k_out);
 }
 
+int closed_block() { return kClosedBlock; }
+
 KernelFn select_closed(uint32_t feat) {
 #ifdef ORT_NO_AXIAL  // A/B timing only
   feat &= ~F_AXIAL;

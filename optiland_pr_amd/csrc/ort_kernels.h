@@ -33,6 +33,12 @@
 namespace ortk {
 
 constexpr int kBlock = 256;
+// trace_closed_kernel's block size (ort_k_closed.hip; its launch asks closed_block()):
+// a per-TU constant so A/B builds of that TU alone can change it
+#ifndef ORT_CLOSED_BLOCK
+#define ORT_CLOSED_BLOCK 256
+#endif
+constexpr int kClosedBlock = ORT_CLOSED_BLOCK;
 
 // Lens tables are read-only for the whole launch and indexed by wave-uniform values, so
 // they are read through the constant address space: the compiler then emits scalar
@@ -718,8 +724,8 @@ __device__ inline void closed_surfaces(const KArgs& a, ort::Ray& r, int lam, dou
 }
 
 template <uint32_t FEAT>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) void trace_closed_kernel(const KArgs a) {
-  const int64_t rid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+__global__ __launch_bounds__(kClosedBlock) __attribute__((amdgpu_waves_per_eu(8))) void trace_closed_kernel(const KArgs a) {
+  const int64_t rid = (int64_t)blockIdx.x * kClosedBlock + threadIdx.x;
   const bool active = rid < a.n_rays;
   const int64_t r_ld = active ? rid : 0;
   int lam = 0;
@@ -1012,6 +1018,7 @@ typedef void (*GeomFn)(const KArgs, const GArgs);
 
 // kernel selection (defined in the ort_k_*.hip translation units)
 KernelFn select_trace(uint32_t feat);      // Newton lenses, any F_GEN / F_REC  (ort_k_trace*.hip)
+int closed_block();                        // its block size                   (ort_k_closed.hip)
 KernelFn select_closed(uint32_t feat);     // closed-form lenses                (ort_k_closed.hip)
 KernelFn select_generate();                // ray generation only               (ort_k_closed.hip)
 KernelFn select_trace_w(uint32_t feat);    // Newton lenses, per-ray wavelengths (ort_k_trace_w.hip)
