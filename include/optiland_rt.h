@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define ORT_ABI_VERSION 11
+#define ORT_ABI_VERSION 12
 #define ORT_MAX_SURFACES 64
 
 /* ---- geometry kinds ----------------------------------- */
@@ -514,6 +514,28 @@ int ort_trace_pupil_vjp(const ort_lens* lens, const double* px, const double* py
                         const ort_batch* batch, const ort_options* opt,
                         const ort_vjp_params* params, const ort_rays* cotangent,
                         double* grad, void* stream);
+
+/* Backward of ort_trace_sequential (resident rays in, SurfaceGroup.trace under autograd:
+ * optimization/optimizer/torch/base.py:116-131 traces under be.grad_mode, and the
+ * reference's torch backend differentiates every be.* op of surface_group.py:232-244):
+ *   grad[p]      += sum_rays  cotangent . d rays_out / d param_p
+ *                           + rec_cotangent . d rec / d param_p
+ *   grad_in.f[r]  = d (cotangent . rays_out + rec_cotangent . rec) / d rays_in.f[r]
+ * with parameters as for ort_trace_pupil_vjp (params: tangent tables, mode, workspace of
+ * ort_vjp_workspace_size bytes for ORT_VJP_ADJOINT). rays_in is the trace's input (the
+ * primal must not have traced in place over it); per-ray wavelengths (batch->w) allowed.
+ * rec_cotangent (nullable): [n_rec][8][n_rays] cotangents of the record buffer the primal
+ * wrote (ORT_SURF_RECORD slots); then rec, that primal record buffer, is required (its
+ * intensity rows weight the absorption adjoint). grad_in (nullable; NULL fields are not
+ * written): cotangents of the input rays x, y, z, L, M, N, i, opd -- ORT_VJP_ADJOINT only
+ * (forward mode carries parameter tangents only: ORT_ERR_ARG). grad is accumulated (zero
+ * it first); grad may be NULL when n_param == 0. opt: ORT_NEWTON_SCHEDULE with the
+ * schedule the verified primal ran. */
+int ort_trace_sequential_vjp(const ort_lens* lens, const ort_rays* rays_in,
+                             const ort_batch* batch, const ort_options* opt,
+                             const ort_vjp_params* params, const ort_rays* cotangent,
+                             const double* rec_cotangent, const double* rec, double* grad,
+                             const ort_rays* grad_in, void* stream);
 
 /* Per-geometry primitives of traced surface `surface` of `lens`, in the surface's local
  * frame (no localize / globalize), for n points or rays:

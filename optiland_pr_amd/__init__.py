@@ -7,6 +7,7 @@ SurfaceGroup / RealRays / SpotDiagram / Wavefront interface.
 """
 
 from . import _abi
+from . import ops  # noqa: F401  (registers torch.ops.ort.trace_sequential / trace_pupil)
 from .distribution import create_distribution
 from .materials import IdealMaterial, Material
 from .optic import Optic

@@ -110,6 +110,7 @@ class ort_wavefront_ref(C.Structure):
 
 
 EXPORTS = ("ort_abi_version", "ort_trace_sequential", "ort_trace_pupil", "ort_trace_pupil_vjp",
+           "ort_trace_sequential_vjp",
            "ort_vjp_workspace_size", "ort_generate_pupil",
            "ort_surface_sag_normal", "ort_surface_distance", "ort_generate_rays",
            "ort_material_nk", "ort_spot_workspace_size", "ort_spot_stats",
@@ -149,6 +150,11 @@ def load(path: str | None = None):
     lib.ort_trace_pupil_vjp.argtypes = [P(ort_lens), C.c_void_p, C.c_void_p, P(ort_batch),
                                         P(ort_options), P(ort_vjp_params), P(ort_rays),
                                         C.c_void_p, C.c_void_p]
+    lib.ort_trace_sequential_vjp.restype = C.c_int
+    lib.ort_trace_sequential_vjp.argtypes = [P(ort_lens), P(ort_rays), P(ort_batch),
+                                             P(ort_options), P(ort_vjp_params), P(ort_rays),
+                                             C.c_void_p, C.c_void_p, C.c_void_p, P(ort_rays),
+                                             C.c_void_p]
     lib.ort_vjp_workspace_size.restype = C.c_int64
     lib.ort_vjp_workspace_size.argtypes = [P(ort_lens), P(ort_batch), P(ort_vjp_params)]
     lib.ort_surface_sag_normal.restype = C.c_int

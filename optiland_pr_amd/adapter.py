@@ -1,17 +1,29 @@
 """Drop-in adapter for the reference package (Optiland, `import optiland`).
 
 `install()` replaces optiland.surfaces.surface_group.SurfaceGroup.trace
-(surface_group.py:232-244) -- the seam SURVEY 8b names -- with the MI355X trace when:
+(surface_group.py:232-244) -- the seam SURVEY 8b names -- with the MI355X trace, reached
+through the PyTorch custom op torch.ops.ort.trace_sequential (ops.py), when:
   * the rays are RealRays (not Paraxial/Polarized) held as torch float64 tensors on the
     HIP device (be.set_backend("torch"); be.set_device("cuda"); be.set_precision("float64")),
+    one wavelength or one per ray (per-ray wavelengths run the in-kernel dispersion
+    formulas, ort_batch.w),
   * every traced surface is lowerable (plane / standard / even / odd asphere / Zernike /
-    XY-polynomial / Chebyshev / biconic / toroidal / Forbes Q-bfs / Q-2D geometry, refractive-reflective interaction without coating or BSDF, any physical
-    aperture (radial, offset, elliptical, rectangular, polygon, file, boolean
-    combinations) or none, homogeneous propagation),
-  * autograd is not requested on the ray tensors.
-Otherwise the original Python loop runs unchanged. The rays are traced IN PLACE (the
-reference mutates its RealRays) and every surface's record (_record,
+    XY-polynomial / Chebyshev / biconic / toroidal / Forbes Q-bfs / Q-2D / grid sag
+    geometry, refractive-reflective / thin-lens / phase / grating interaction without
+    coating or BSDF, any physical aperture or none, homogeneous propagation),
+  * under autograd, every lens value that requires grad is one the trace core
+    differentiates -- radius, conic, Zernike coefficients, vertex z (the surface
+    coordinate system's z, which the reference's set_thickness writes) -- or does not
+    depend on a trainable tensor (see _grad_params). Gradients flow to the input rays and
+    to every surface record too (ort_trace_sequential_vjp).
+Otherwise the original Python loop runs unchanged (it differentiates everything
+itself). The rays are updated in place as the reference does (its attributes are
+reassigned, surface.py's be ops); every surface's record (_record,
 standard_surface.py:266-286) is filled from the kernel's record buffer.
+
+The lowered lens is cached on the group per wavelength key and re-uploaded only when
+the lowered bytes change (the Newton schedules stay with it), so a repeated trace is the
+host lowering plus one launch.
 
 `lower_reference_group()` turns reference objects into the same LensTable bytes the
 native host API produces (tested equal in tests/test_adapter.py).
@@ -75,6 +87,8 @@ class _RefMaterial(BaseMaterial):
     def key(self):
         # same dedup keys as the native materials (materials.py), so tables match
         m = self.m
+        if isinstance(m, BaseMaterial):  # a native material passed through the seam
+            return m.key()
         if type(m).__name__ == "IdealMaterial":
             return ("ideal", _f(m.index), _f(m.absorp))
         if type(m).__name__ == "AbbeMaterial":
@@ -253,42 +267,201 @@ def uninstall():
         sg_mod.SurfaceGroup.trace = _ORIGINAL.pop("trace")
 
 
+# geometries whose radius / conic the derivative kernels seed (the conic base of
+# standard.py and of the Newton geometries built on it)
+_RK_GEOMETRIES = ("StandardGeometry", "EvenAsphere", "OddAsphere", "ZernikePolynomialGeometry",
+                  "PolynomialGeometry", "ChebyshevPolynomialGeometry")
+
+
+def _grad_mode_on():
+    try:
+        import optiland.backend as be
+
+        return bool(be.grad_mode.requires_grad)
+    except Exception:  # pragma: no cover - numpy backend / older reference
+        return False
+
+
+def _reaches_parameter(t, memo):
+    """Does the autograd graph of t reach a torch.nn.Parameter (a trainable tensor)?
+    memo: id(grad_fn) -> (grad_fn, answer), shared by the queries of one trace call (the
+    ray fields and lens values share most of their graphs); it holds every node it names,
+    so no id is reused while it lives."""
+    import torch
+
+    if isinstance(t, torch.nn.Parameter):
+        return True
+    root = t.grad_fn
+    if root is None:
+        return False
+    stack = [(root, False)]
+    while stack:
+        node, expanded = stack.pop()
+        if not expanded:
+            if id(node) in memo:
+                continue
+            var = getattr(node, "variable", None)  # AccumulateGrad: a leaf
+            if var is not None:
+                memo[id(node)] = (node, isinstance(var, torch.nn.Parameter))
+                continue
+            memo[id(node)] = (node, None)  # in progress (the graph is acyclic)
+            stack.append((node, True))
+            stack.extend((c, False) for c, _ in node.next_functions
+                         if c is not None and id(c) not in memo)
+        else:
+            memo[id(node)] = (node, any(memo[id(c)][1] for c, _ in node.next_functions
+                                        if c is not None))
+    return bool(memo[id(root)][1])
+
+
+def _live(v, grad_mode, memo):
+    """v is a tensor whose gradient someone wants. Under the reference's be.grad_mode
+    (TorchOptimizer) every be.array is a requires-grad leaf, so there only values that
+    depend on a torch.nn.Parameter count; outside it any requires-grad tensor does."""
+    import torch
+
+    if not (torch.is_tensor(v) and v.requires_grad):
+        return False
+    return _reaches_parameter(v, memo) if grad_mode else True
+
+
+def _tensor_attrs(obj, skip=()):
+    import torch
+
+    try:
+        items = vars(obj).items()
+    except TypeError:
+        return []
+    return [(k, v) for k, v in items if k not in skip and torch.is_tensor(v)]
+
+
+def _grad_params(group):
+    """-> [(kind, traced-surface index, tensor)] for the differentiable lens values that
+    require grad (ops.SPEC_KINDS). Raises Unsupported when a lens value the trace core does
+    not differentiate (decenters, tilts, reference_cs chains, normalisation radii, asphere
+    coefficients, material data, apertures ...) depends on a trainable tensor: the
+    reference loop then runs and differentiates it."""
+    import torch
+
+    if not torch.is_grad_enabled():
+        return []
+    grad_mode = _grad_mode_on()
+    memo: dict = {}
+    out = []
+
+    def refuse(where, name, v):
+        if _live(v, grad_mode, memo):
+            raise Unsupported(f"gradient through {where}.{name}")
+
+    def cs_chain(cs, where, allow_z):
+        for k, v in _tensor_attrs(cs, skip=("z",) if allow_z else ()):
+            refuse(where, k, v)
+        if cs.reference_cs is not None:
+            cs_chain(cs.reference_cs, where + ".reference_cs", False)
+
+    for ti, s in enumerate(group.surfaces[1:]):
+        g = s.geometry
+        name = type(g).__name__
+        diff = {}
+        if name in _RK_GEOMETRIES:
+            diff["radius"] = getattr(g, "radius", None)
+            diff["k"] = getattr(g, "k", None)
+        if name == "ZernikePolynomialGeometry":
+            diff["coefficients"] = g.coefficients
+        for k, v in _tensor_attrs(g, skip=tuple(diff)):
+            refuse(f"surface {ti + 1} geometry", k, v)
+        cs = g.cs
+        z_ok = cs.reference_cs is None
+        cs_chain(cs, f"surface {ti + 1} cs", z_ok)
+        for m in (s.material_pre, s.material_post):
+            for k, v in _tensor_attrs(m):
+                refuse(f"surface {ti + 1} material", k, v)
+        if s.aperture is not None:
+            for k, v in _tensor_attrs(s.aperture):
+                refuse(f"surface {ti + 1} aperture", k, v)
+        kinds = (("radius", "radius"), ("k", "conic"), ("coefficients", "zernike"))
+        for attr, kind in kinds:
+            v = diff.get(attr)
+            if torch.is_tensor(v) and v.requires_grad:
+                if kind != "zernike" and v.numel() != 1:
+                    raise Unsupported(f"surface {ti + 1}: non-scalar {attr}")
+                out.append((kind, ti, v))
+        if z_ok and torch.is_tensor(cs.z) and cs.z.requires_grad:
+            out.append(("vertex", ti, cs.z))
+    return out
+
+
+def _device_lens(group, wavelengths, per_ray, device):
+    """Lowered + uploaded lens of a reference group, cached on it per wavelength key and
+    re-uploaded only when the lowered bytes change (Newton schedules kept across edits)."""
+    from .raytrace import DeviceLens
+
+    table = lower_reference_group(group, wavelengths, record=True)
+    table.final_mat = -1  # SurfaceGroup.trace has no image-space propagate
+    fp = table.fingerprint()
+    cache = group.__dict__.setdefault("_ort_lenses", {})
+    key = (tuple(float(w) for w in wavelengths), bool(per_ray), str(device))
+    hit = cache.get(key)
+    if hit is None or hit.fingerprint != fp:
+        old = hit
+        hit = DeviceLens(table, device=device)
+        hit.fingerprint = fp
+        if old is not None and old.table.surfaces.shape == table.surfaces.shape:
+            hit.sched_cache = old.sched_cache
+        cache[key] = hit
+    return hit
+
+
 def _trace_on_mi355x(group, rays, skip):
     import torch
 
-    from .raytrace import DeviceLens, RealRays, trace_rays
+    from . import ops
 
     if type(rays).__name__ != "RealRays":
         raise Unsupported(type(rays).__name__)
     x = rays.x
     if not (torch.is_tensor(x) and x.is_cuda and x.dtype == torch.float64):
         raise Unsupported("rays must be float64 torch tensors on the HIP device")
-    if any(getattr(rays, a).requires_grad for a in ("x", "y", "z", "L", "M", "N")):
-        raise Unsupported("autograd")
-    w = torch.unique(rays.w)
-    if w.numel() != 1:
-        raise Unsupported("several wavelengths in one call")
-    table = lower_reference_group(group, [float(w.item())], record=True)
-    table.final_mat = -1  # SurfaceGroup.trace has no image-space propagate
-    dl = DeviceLens(table, device=x.device)
-    mine = RealRays.__new__(RealRays)
     n = x.numel()
-    for a in _abi.RAY_FIELDS:
-        setattr(mine, a, getattr(rays, a).contiguous())
-    mine.w = rays.w
-    rec = torch.empty(table.n_rec * 8 * n, dtype=torch.float64, device=x.device)
+    fields = [getattr(rays, a) for a in _abi.RAY_FIELDS]
+    if any(not torch.is_tensor(t) or t.numel() != n or not t.is_cuda for t in fields):
+        raise Unsupported("ray fields of mixed sizes / devices")
+    params = _grad_params(group)
+    w = rays.w
+    if not torch.is_tensor(w):
+        w = torch.as_tensor(w, dtype=torch.float64, device=x.device)
+    w = w.detach().to(device=x.device, dtype=torch.float64).reshape(-1)
+    if n == 0:
+        raise Unsupported("empty ray batch")
+    lo_hi = torch.aminmax(w)  # one read decides table rows vs per-ray dispersion
+    lo, hi = (float(v) for v in torch.stack(lo_hi).cpu())
+    per_ray = lo != hi
+    dl = _device_lens(group, [lo], per_ray, x.device)
+    if torch.is_grad_enabled():
+        # ray fields count as differentiable inputs under the same rule as lens values
+        grad_mode, memo = _grad_mode_on(), {}
+        fields = [t if _live(t, grad_mode, memo) else t.detach() for t in fields]
+        if params or any(t.requires_grad for t in fields):
+            try:
+                ops._check_differentiable(dl.table)
+            except NotImplementedError as e:  # no derivative kernels: the reference loop
+                raise Unsupported(str(e)) from e
+    start = max(int(skip) - 1, 0)
+    outs = torch.ops.ort.trace_sequential(
+        ops.handle(dl), fields, w if per_ray else None, [t for _, _, t in params],
+        ops.encode_spec([(k, si) for k, si, _ in params]), start, per_ray)
     group.reset()
-    obj = group.surfaces[0]
-    snap = {a: getattr(mine, a).clone() for a in _abi.RAY_FIELDS}
-    trace_rays(dl, mine, mine, rec=rec, start_surface=max(int(skip) - 1, 0))
-    for a in _abi.RAY_FIELDS:
-        setattr(rays, a, getattr(mine, a))
-    view = rec.view(table.n_rec, 8, n)
     names = ("x", "y", "z", "L", "M", "N", "intensity", "opd")
-    if skip == 0:
-        for nm, a in zip(names, _abi.RAY_FIELDS, strict=True):
-            setattr(obj, nm, snap[a])
-    for slot, si in enumerate(table.rec_surfaces):
+    if skip == 0:  # the object surface records the incoming rays (object_surface.py:56-72)
+        obj = group.surfaces[0]
+        for nm, t in zip(names, fields, strict=True):
+            setattr(obj, nm, t)
+    for a, t in zip(_abi.RAY_FIELDS, outs[:8], strict=True):
+        setattr(rays, a, t)
+    view = outs[8].view(dl.table.n_rec, 8, n)
+    for slot, si in enumerate(dl.table.rec_surfaces):
+        if si < start:  # surfaces[:skip] are not traced: their records stay reset
+            continue
         s = group.surfaces[si + 1]
         for f, nm in enumerate(names):
             setattr(s, nm, view[slot, f])

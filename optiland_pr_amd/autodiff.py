@@ -109,86 +109,6 @@ def parameter_map(table, params):
     return zp, off
 
 
-def tangent_tables(table, params):
-    """Lay the parameters out for ort_vjp_params: -> (zern_param or None, surf_tangent
-    [n_param][S][3] or None, final_tangent [n_param] or None, n_param, sizes)."""
-    from . import _abi
-
-    S = table.n_surfaces
-    n_param = sum(int(t.numel()) for _, _, t in params)
-    zp = None
-    surf = None
-    final = None
-    off = 0
-    sizes = []
-    for kind, si, t in params:
-        n = int(t.numel())
-        sizes.append(n)
-        row = table.surfaces[si]
-        if kind == "zernike":
-            if zp is None:
-                zp = np.full(max(1, len(table.zern)), -1, dtype=np.int32)
-            if n != int(row["n_coef"]):
-                raise ValueError(f"surface {si}: {n} coefficients, lowered {int(row['n_coef'])}")
-            base = int(row["coef_off"])
-            zp[base:base + n] = np.arange(off, off + n, dtype=np.int32)
-        else:
-            if surf is None:
-                surf = np.zeros((n_param, S, 3), dtype=np.float64)
-            g = int(row["geometry"])
-            if kind in ("radius", "conic"):
-                if g in (_abi.GEOM_PLANE, _abi.GEOM_BICONIC, _abi.GEOM_TOROIDAL):
-                    raise NotImplementedError(f"surface {si}: {kind} of this geometry is "
-                                              "not a differentiable parameter here")
-                surf[off, si, 0 if kind == "radius" else 1] = 1.0
-            else:  # thickness after surface si moves every later vertex (set_thickness)
-                surf[off, si + 1:, 2] = 1.0
-                if si == S - 1:  # the image surface's thickness: the final propagate
-                    if final is None:
-                        final = np.zeros(n_param, dtype=np.float64)
-                    final[off] = 1.0
-        off += n
-    return zp, surf, final, n_param, sizes
-
-
-class _TracePupilFn(torch.autograd.Function if torch is not None else object):
-    """outputs (x, y, z, L, M, N, i, opd) of ort_trace_pupil as functions of the lens
-    parameter tensors."""
-
-    @staticmethod
-    def forward(ctx, plan, *tensors):
-        from .raytrace import RealRays, trace_pupil
-
-        dl = plan["dlens"]
-        out = RealRays.__new__(RealRays)  # the 8 traced fields (w is not an output)
-        for a in _abi.RAY_FIELDS:
-            setattr(out, a, torch.empty(plan["n"], dtype=torch.float64, device=dl.device))
-        trace_pupil(dl, plan["seg_dev"], plan["px"], plan["py"], out, plan["n"],
-                    plan["seg_len"], plan["n"], keys=plan["keys"])
-        sched = dl.last_schedule
-        ctx.plan = plan
-        ctx.set_materialize_grads(False)
-        ctx.sched_dev = None if sched is None else dl.resident("sched", sched.reshape(-1))
-        ctx.shapes = [(t.numel(), t.shape, t.device, t.dtype) for t in tensors]
-        return tuple(getattr(out, a) for a in _abi.RAY_FIELDS)
-
-    @staticmethod
-    def backward(ctx, *grads):
-        plan = ctx.plan
-        dl = plan["dlens"]
-        n_param = plan["n_param"]
-        g = torch.zeros(n_param, dtype=torch.float64, device=dl.device)
-        cot = [None if gr is None else gr.to(torch.float64).contiguous() for gr in grads]
-        vjp(dl, plan["seg_dev"], plan["px"], plan["py"], plan["n"], plan["seg_len"],
-            ctx.sched_dev, plan["tables"], n_param, cot, g)
-        res = [None]
-        off = 0
-        for numel, shape, dev, dtype in ctx.shapes:
-            res.append(g[off:off + numel].reshape(shape).to(device=dev, dtype=dtype))
-            off += numel
-        return tuple(res)
-
-
 def vjp_mode(table):
     """ORT_VJP_ADJOINT (one reverse-mode pass) unless a Zernike surface's Newton slope is
     not its sag's derivative -- the standard / noll normal omits the normalisation
@@ -269,11 +189,12 @@ def vjp(dlens, seg_dev, px, py, n, seg_len, sched_dev, tables, n_param, cot, gra
 
 def trace_pupil_grad(optic, dlens, seg_dev, px, py, n, seg_len, wavelength, keys):
     """Differentiable fused trace: returns the 8 output tensors connected to the
-    parameter tensors of parameters(optic)."""
+    parameter tensors of parameters(optic), through the torch.ops.ort.trace_pupil custom
+    op (ops.py) whose autograd formula is ort_trace_pupil_vjp."""
+    from . import ops
+
     params = parameters(optic)
-    zp, st, ft, n_param, _ = tangent_tables(dlens.table, params)
-    tables = tuple(None if a is None else dlens.resident(("tangent", i), a)
-                   for i, a in enumerate((zp, st, ft)))
-    plan = dict(dlens=dlens, seg_dev=seg_dev, px=px, py=py, n=n, seg_len=seg_len,
-                wavelength=wavelength, keys=keys, n_param=n_param, tables=tables)
-    return _TracePupilFn.apply(plan, *[t for _, _, t in params])
+    plan = ops.PupilPlan(dlens, seg_dev, px, py, n, seg_len, keys)
+    outs = torch.ops.ort.trace_pupil(ops.handle(plan), [t for _, _, t in params],
+                                     ops.encode_spec([(k, si) for k, si, _ in params]))
+    return outs[:8]

@@ -48,7 +48,12 @@ struct AArgs {
   int32_t n_surf;
   int64_t n_wave;           // waves of the main launch
   ort_rays cot;             // cotangents of the outputs (NULL field: zero)
-  double* tape;             // [n_surf][7][n_rays]
+  // cotangents of the per-surface record buffer [n_rec][8][n_rays] (NULL: zero) and the
+  // primal's record buffer (its intensity rows weight the absorption adjoint)
+  const double* rec_cot;
+  const double* rec;
+  ort_rays gin;             // RES: d / d rays_in (NULL field: not wanted)
+  double* tape;             // [n_surf][kTapeRows][n_rays]
   double* partial;          // [n_slot][n_wave]
   double* slot_sum;         // [n_slot]
   int32_t* need;            // [n_slot]: some parameter depends on this slot
@@ -119,7 +124,13 @@ struct AdjWaves {
 #else
 #define ORT_ADJ_OCC __attribute__((amdgpu_waves_per_eu(AdjWaves<KM, P>::value)))
 #endif
-template <uint32_t KM, int P>
+// RES = false: rays generated from pupil samples (ort_trace_pupil_vjp);
+// RES = true: resident input rays a.in (ort_trace_sequential_vjp, SurfaceGroup.trace under
+// autograd), optionally with per-ray wavelengths (a.w), and the cotangents of the input
+// rays written to j.gin. The forward then runs with i = 1, so intensity(r) is the factor
+// d i_out / d i_in (0 when clipped, exp(att) otherwise; i_in times it is the primal's
+// intensity, operation for operation).
+template <uint32_t KM, int P, bool RES>
 __global__ __launch_bounds__(kBlock) ORT_ADJ_OCC void adj_kernel(const KArgs a, const AArgs j) {
   using D = ort::Dual<P>;
   const int64_t rid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -127,11 +138,37 @@ __global__ __launch_bounds__(kBlock) ORT_ADJ_OCC void adj_kernel(const KArgs a, 
   const int64_t r_ld = active ? rid : 0;
   const int64_t wave = rid >> 6;
   const int64_t NR = a.n_rays;
-  const int64_t sidx = r_ld / a.seg_len;
-  const ort_segment sg = a.seg[sidx];
-  const int lam = sg.lambda_idx;
-  const int64_t p = a.pupil_per_ray ? r_ld : (r_ld - sidx * a.seg_len);
+  const int64_t sidx = (RES && !a.seg) ? 0 : r_ld / a.seg_len;
+  int lam = 0;
+  double wl = 0.0, i_in = 1.0;
+  ort::Ray r;
+  if constexpr (RES) {
+    if (a.seg) lam = a.seg[sidx].lambda_idx;
+    if (a.w) wl = a.w[r_ld];
+    r.x = a.in.x[r_ld];
+    r.y = a.in.y[r_ld];
+    r.z = a.in.z[r_ld];
+    r.L = a.in.L[r_ld];
+    r.M = a.in.M[r_ld];
+    r.N = a.in.N[r_ld];
+    i_in = a.in.i[r_ld];
+    r.i = 1.0;
+    r.opd = a.in.opd[r_ld];
+    r.att = 0.0;
+  } else {
+    const ort_segment sg = a.seg[sidx];
+    lam = sg.lambda_idx;
+    const int64_t p = a.pupil_per_ray ? r_ld : (r_ld - sidx * a.seg_len);
+    r = ort::generate_ray(sg, a.px[p], a.py[p], a.apod);
+  }
   const int64_t group = r_ld / a.group_len;
+  // optical constants of surface si at this ray's wavelength (table row, or per ray)
+  auto optics_of = [&](const ort_surface& s, int si) -> ort_surface_optics {
+    if constexpr (RES) {
+      if (a.w) return optics_ray(a, s, wl);
+    }
+    return optics_at(a, lam, si);
+  };
 
   // wave sum of a per-ray contribution into its slot (one writer per slot and wave).
   // first: the slot's first contribution from this wave -- a plain store instead of a
@@ -236,10 +273,10 @@ __global__ __launch_bounds__(kBlock) ORT_ADJ_OCC void adj_kernel(const KArgs a, 
   };
 
   // ---- forward: the primal trace, taping (incoming ray, t, Newton iterates) per surface
-  ort::Ray r = ort::generate_ray(sg, a.px[p], a.py[p], a.apod);
+  double gi = 0.0;  // RES: d (recorded intensities) / d i_in, contracted with rec_cot
   for (int si = a.start_surface; si < a.n_surf; ++si) {
     const ort_surface s = cst(a.surf)[si];
-    const ort_surface_optics o = optics_at(a, lam, si);
+    const ort_surface_optics o = optics_of(s, si);
     double* tp = j.tape + (int64_t)si * kTapeRows * NR + rid;
     if (active) {
       tp[0] = r.x;
@@ -262,10 +299,17 @@ __global__ __launch_bounds__(kBlock) ORT_ADJ_OCC void adj_kernel(const KArgs a, 
     ort::finish_surface<KM>(r, s, s.radius, s.conic, cst(a.coef), cst(a.zern), kNoSeed, t,
                             o.n_pre, o.u, o.alpha_pre);
     globalize(a, s, r);
+    if constexpr (RES) {
+      if (j.rec_cot && (s.flags & ORT_SURF_RECORD) && active)
+        gi += j.rec_cot[((int64_t)s.rec_slot * 8 + 6) * NR + rid] * ort::intensity(r);
+    }
   }
   double alpha_f = 0.0;
   if (a.final_mat >= 0) {
-    alpha_f = tab(a.alpha_tab, a.n_lambda, a.n_mat, lam, a.final_mat);
+    if (RES && a.w)
+      alpha_f = ort::absorption_alpha(ort::material_k(cst(a.mats)[a.final_mat], a.coef, wl), wl);
+    else
+      alpha_f = tab(a.alpha_tab, a.n_lambda, a.n_mat, lam, a.final_mat);
     ort::propagate(r, a.final_thickness, alpha_f);
   }
 
@@ -282,8 +326,9 @@ __global__ __launch_bounds__(kBlock) ORT_ADJ_OCC void adj_kernel(const KArgs a, 
     if (j.cot.M) b.M = j.cot.M[rid];
     if (j.cot.N) b.N = j.cot.N[rid];
     if (j.cot.opd) bopd = j.cot.opd[rid];
-    if (j.cot.i) batt = j.cot.i[rid] * ort::intensity(r);
+    if (j.cot.i) batt = j.cot.i[rid] * (RES ? i_in * ort::intensity(r) : ort::intensity(r));
   }
+  const double factor_f = ort::intensity(r);  // RES: d i_out / d i_in
   // image-space propagate (real_ray_tracer.py:84-89): x = x' + d L, ...
   if (a.final_mat >= 0) {
     double bd = b.x * r.L + b.y * r.M + b.z * r.N;
@@ -298,7 +343,22 @@ __global__ __launch_bounds__(kBlock) ORT_ADJ_OCC void adj_kernel(const KArgs a, 
   // ---- reverse over the surfaces
   for (int si = a.n_surf - 1; si >= a.start_surface; --si) {
     const ort_surface s = cst(a.surf)[si];
-    const ort_surface_optics o = optics_at(a, lam, si);
+    const ort_surface_optics o = optics_of(s, si);
+    // cotangent of this surface's record (the state after its globalize): the adjoint of
+    // the state there gains it; its intensity row through att (d I / d att = I, the
+    // primal's recorded value)
+    if (j.rec_cot && (s.flags & ORT_SURF_RECORD) && active) {
+      const double* rc = j.rec_cot + (int64_t)s.rec_slot * 8 * NR + rid;
+      b.x += rc[0];
+      b.y += rc[NR];
+      b.z += rc[2 * NR];
+      b.L += rc[3 * NR];
+      b.M += rc[4 * NR];
+      b.N += rc[5 * NR];
+      bopd += rc[7 * NR];
+      const double ci = rc[6 * NR];
+      if (ci != 0.0) batt += ci * j.rec[((int64_t)s.rec_slot * 8 + 6) * NR + rid];
+    }
     const double* tp = j.tape + (int64_t)si * kTapeRows * NR + r_ld;
     ort::Ray q;
     q.x = tp[0];
@@ -447,14 +507,30 @@ __global__ __launch_bounds__(kBlock) ORT_ADJ_OCC void adj_kernel(const KArgs a, 
     emit(3 * si + 1, bk, true);
     emit(3 * si + 2, bCZ, true);
   }
+  if constexpr (RES) {
+    // cotangents of the input rays: the adjoint state at the first traced surface; opd
+    // passes straight through, i through the clip / absorption factors
+    if (active) {
+      if (j.gin.x) j.gin.x[rid] = b.x;
+      if (j.gin.y) j.gin.y[rid] = b.y;
+      if (j.gin.z) j.gin.z[rid] = b.z;
+      if (j.gin.L) j.gin.L[rid] = b.L;
+      if (j.gin.M) j.gin.M[rid] = b.M;
+      if (j.gin.N) j.gin.N[rid] = b.N;
+      if (j.gin.opd) j.gin.opd[rid] = bopd;
+      if (j.gin.i) j.gin.i[rid] = (j.cot.i ? j.cot.i[rid] * factor_f : 0.0) + gi;
+    }
+  }
 }
 
 typedef void (*AdjFn)(const KArgs, const AArgs);
-AdjFn select_adj2(uint32_t km);  // ort_k_adj2.hip
-AdjFn select_adj4(uint32_t km);  // ort_k_adj4.hip
+AdjFn select_adj2(uint32_t km);   // ort_k_adj2.hip   (generated rays)
+AdjFn select_adj4(uint32_t km);   // ort_k_adj4.hip
+AdjFn select_adj2r(uint32_t km);  // ort_k_adj2r.hip  (resident rays)
+AdjFn select_adj4r(uint32_t km);  // ort_k_adj4r.hip
 // zero the partials, flag the needed slots, run the adjoint kernel, reduce, contract
 // (ort_k_adj.hip)
-int adj_run(const KArgs& a, const AArgs& j, int tangents, uint32_t km, int64_t blocks,
-            hipStream_t stream);
+int adj_run(const KArgs& a, const AArgs& j, int tangents, uint32_t km, bool resident,
+            int64_t blocks, hipStream_t stream);
 
 }  // namespace ortk

@@ -226,14 +226,25 @@ int64_t ort_vjp_workspace_size(const ort_lens* lens, const ort_batch* batch,
   return L.total;
 }
 
-int ort_trace_pupil_vjp(const ort_lens* lens, const double* px, const double* py,
-                        const ort_batch* batch, const ort_options* opt,
-                        const ort_vjp_params* params, const ort_rays* cotangent,
-                        double* grad, void* stream) {
+// Shared body of the two VJP entry points: generated rays (px, py) or resident rays
+// (rays_in, resident = true).
+static int vjp_run(const ort_lens* lens, const double* px, const double* py,
+                   const ort_rays* rays_in, bool resident, const ort_batch* batch,
+                   const ort_options* opt, const ort_vjp_params* params,
+                   const ort_rays* cotangent, const double* rec_cotangent, const double* rec,
+                   double* grad, const ort_rays* grad_in, void* stream) {
   if (!batch || !cotangent || !params || params->n_param < 0) return ORT_ERR_ARG;
   const int32_t n_param = params->n_param;
-  if (batch->n_rays == 0 || n_param == 0) return ORT_OK;
-  if (!px || !py || !batch->seg || !grad || batch->w) return ORT_ERR_ARG;
+  const bool want_in = grad_in && (grad_in->x || grad_in->y || grad_in->z || grad_in->L ||
+                                   grad_in->M || grad_in->N || grad_in->i || grad_in->opd);
+  if (batch->n_rays == 0 || (n_param == 0 && !want_in)) return ORT_OK;
+  if (n_param > 0 && !grad) return ORT_ERR_ARG;
+  if (rec_cotangent && !rec) return ORT_ERR_ARG;  // intensity rows weight the absorption
+  if (resident) {
+    if (!rays_in) return ORT_ERR_ARG;
+  } else if (!px || !py || !batch->seg || batch->w) {
+    return ORT_ERR_ARG;
+  }
   KArgs a{};
   uint32_t feat = 0;
   int rc = fill_args(a, lens, batch, opt, nullptr, nullptr, nullptr, feat);
@@ -242,15 +253,12 @@ int ort_trace_pupil_vjp(const ort_lens* lens, const double* px, const double* py
   if (params->zern_param && (feat & ort::KM_ZERN) == 0) return ORT_ERR_ARG;
   if (feat & F_IA) return ORT_ERR_ARG;  // no derivative kernels for thin-lens / phase / grating
   if (lens->geometry_mask & (1u << ORT_GEOM_GRID_SAG)) return ORT_ERR_ARG;  // nor grid sags
-  a.px = px;
-  a.py = py;
-  JArgs j{};
-  j.zparam = params->zern_param;
-  j.tan_surf = params->surf_tangent;
-  j.tan_final = params->final_tangent;
-  j.n_param = n_param;
-  j.cot = *cotangent;
-  j.grad = grad;
+  if (resident) {
+    a.in = *rays_in;
+  } else {
+    a.px = px;
+    a.py = py;
+  }
   const int64_t blocks = (a.n_rays + kBlock - 1) / kBlock;
   if (blocks > 0x7fffffff) return ORT_ERR_ARG;
   const uint32_t km = feat & F_KM;
@@ -270,15 +278,27 @@ int ort_trace_pupil_vjp(const ort_lens* lens, const double* px, const double* py
     aj.n_surf = lens->n_surfaces;
     aj.n_wave = L.n_wave;
     aj.cot = *cotangent;
+    aj.rec_cot = rec_cotangent;
+    aj.rec = rec;
+    if (want_in) aj.gin = *grad_in;
     aj.tape = (double*)(w + L.tape);
     aj.partial = (double*)(w + L.partial);
     aj.slot_sum = (double*)(w + L.slot_sum);
     aj.need = (int32_t*)(w + L.need);
     aj.grad = grad;
     // radius / conic tangents need duals seeded on them too
-    return adj_run(a, aj, params->surf_tangent ? 4 : 2, km, blocks, s);
+    return adj_run(a, aj, params->surf_tangent ? 4 : 2, km, resident, blocks, s);
   }
   if (params->mode != ORT_VJP_UNROLLED) return ORT_ERR_ARG;
+  if (want_in) return ORT_ERR_ARG;  // forward mode carries parameter tangents only
+  JArgs j{};
+  j.zparam = params->zern_param;
+  j.tan_surf = params->surf_tangent;
+  j.tan_final = params->final_tangent;
+  j.n_param = n_param;
+  j.cot = *cotangent;
+  j.rec_cot = rec_cotangent;
+  j.grad = grad;
   for (int p0 = 0; p0 < n_param;) {
     const int left = n_param - p0;
     // tangents per launch: ORT_VJP_TANGENTS overrides (A/B timing)
@@ -293,6 +313,23 @@ int ort_trace_pupil_vjp(const ort_lens* lens, const double* px, const double* py
     p0 += P;
   }
   return ORT_OK;
+}
+
+int ort_trace_pupil_vjp(const ort_lens* lens, const double* px, const double* py,
+                        const ort_batch* batch, const ort_options* opt,
+                        const ort_vjp_params* params, const ort_rays* cotangent,
+                        double* grad, void* stream) {
+  return vjp_run(lens, px, py, nullptr, false, batch, opt, params, cotangent, nullptr, nullptr,
+                 grad, nullptr, stream);
+}
+
+int ort_trace_sequential_vjp(const ort_lens* lens, const ort_rays* rays_in,
+                             const ort_batch* batch, const ort_options* opt,
+                             const ort_vjp_params* params, const ort_rays* cotangent,
+                             const double* rec_cotangent, const double* rec, double* grad,
+                             const ort_rays* grad_in, void* stream) {
+  return vjp_run(lens, nullptr, nullptr, rays_in, true, batch, opt, params, cotangent,
+                 rec_cotangent, rec, grad, grad_in, stream);
 }
 
 int ort_generate_pupil(const ort_pupil* pupil, double* px, double* py, void* stream) {

@@ -46,9 +46,10 @@ __global__ __launch_bounds__(kBlock) void adj_contract_kernel(const AArgs j) {
   }
 }
 
-int adj_run(const KArgs& a, const AArgs& j, int tangents, uint32_t km, int64_t blocks,
-            hipStream_t stream) {
-  AdjFn fn = tangents == 4 ? select_adj4(km) : select_adj2(km);
+int adj_run(const KArgs& a, const AArgs& j, int tangents, uint32_t km, bool resident,
+            int64_t blocks, hipStream_t stream) {
+  AdjFn fn = resident ? (tangents == 4 ? select_adj4r(km) : select_adj2r(km))
+                      : (tangents == 4 ? select_adj4(km) : select_adj2(km));
   if (!fn) return ORT_ERR_ARG;
   if (hipMemsetAsync(j.partial, 0, (size_t)j.n_slot * (size_t)j.n_wave * sizeof(double),
                      stream) != hipSuccess)

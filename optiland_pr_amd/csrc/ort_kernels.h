@@ -632,9 +632,13 @@ __device__ inline ort::Ray closed_ray_in(const KArgs& a, int64_t r_ld, int& lam,
   return r;
 }
 
+// apod: F_GEN | F_REC with an apodization, the pupil factor of this ray, multiplied into
+// every recorded intensity (the generated ray would carry it from the start,
+// ray_generator.py:91-95); 1 otherwise
 template <uint32_t FEAT, bool FAST>
 __device__ inline void closed_surfaces(const KArgs& a, ort::Ray& r, int lam, double wl,
-                                       int64_t rid, bool active, bool& bad, bool& geom_bad) {
+                                       int64_t rid, bool active, bool& bad, bool& geom_bad,
+                                       double apod = 1.0) {
   for (int si = a.start_surface; si < a.n_surf; ++si) {
     const ort_surface s = cst(a.surf)[si];
     const ort_surface_optics o = surface_optics<FEAT>(a, s, lam, si, wl);
@@ -716,7 +720,10 @@ __device__ inline void closed_surfaces(const KArgs& a, ort::Ray& r, int lam, dou
         b[3 * a.n_rays] = r.L;
         b[4 * a.n_rays] = r.M;
         b[5 * a.n_rays] = r.N;
-        b[6 * a.n_rays] = ort::intensity(r);
+        if constexpr ((FEAT & F_GEN) != 0)
+          b[6 * a.n_rays] = a.apod ? apod * ort::intensity(r) : ort::intensity(r);
+        else
+          b[6 * a.n_rays] = ort::intensity(r);
         b[7 * a.n_rays] = r.opd;
       }
     }
@@ -731,17 +738,27 @@ __global__ __launch_bounds__(kClosedBlock) __attribute__((amdgpu_waves_per_eu(8)
   int lam = 0;
   double wl = 0.0;  // F_WRAY: this ray's wavelength
   bool bad = false, geom_bad = false;
+  // recorded intensities of apodized generated rays carry the pupil factor (the stored
+  // image intensity gets it below); the record kernels alone pay for it up front
+  double apod_f = 1.0;
+  if constexpr ((FEAT & F_GEN) != 0 && (FEAT & F_REC) != 0) {
+    if (a.apod) {
+      const int64_t sidx = a.n_seg == 1 ? 0 : r_ld / a.seg_len;
+      const int64_t p = a.pupil_per_ray ? r_ld : (r_ld - sidx * a.seg_len);
+      apod_f = ort::apodize(*cst(a.apod), a.px[p], a.py[p]);
+    }
+  }
 #ifndef ORT_NO_DEFERRED_CHECKS
   ort::Ray r = closed_ray_in<FEAT, true>(a, r_ld, lam, wl, bad);
-  closed_surfaces<FEAT, true>(a, r, lam, wl, rid, active, bad, geom_bad);
+  closed_surfaces<FEAT, true>(a, r, lam, wl, rid, active, bad, geom_bad, apod_f);
   bad = bad | !ort::fast::state_ok(r);  // the upper-range failures (ort_fastpath.h)
   if (__builtin_expect(bad, 0)) {  // this lane left the fast path's ranges: exact re-trace
     r = closed_ray_in<FEAT, false>(a, r_ld, lam, wl, bad);
-    closed_surfaces<FEAT, false>(a, r, lam, wl, rid, active, bad, geom_bad);
+    closed_surfaces<FEAT, false>(a, r, lam, wl, rid, active, bad, geom_bad, apod_f);
   }
 #else
   ort::Ray r = closed_ray_in<FEAT, false>(a, r_ld, lam, wl, bad);
-  closed_surfaces<FEAT, false>(a, r, lam, wl, rid, active, bad, geom_bad);
+  closed_surfaces<FEAT, false>(a, r, lam, wl, rid, active, bad, geom_bad, apod_f);
 #endif
   if (a.final_mat >= 0) ort::propagate(r, a.final_thickness, final_alpha<FEAT>(a, lam, wl));
   if (geom_bad && a.status && threadIdx.x == 0) atomicOr(a.status, (int)ORT_STATUS_BAD_GEOMETRY);
@@ -790,6 +807,7 @@ struct JArgs {
   int32_t n_param;
   int32_t p0;              // first parameter of this launch
   ort_rays cot;            // cotangents of the outputs (NULL field: zero)
+  const double* rec_cot;   // cotangents of the record buffer [n_rec][8][n_rays] (or NULL)
   double* grad;            // [n_param], accumulated with atomics
 };
 
@@ -847,24 +865,48 @@ __device__ inline ort::Dual<P> seeded(double v, const double* tan, int64_t strid
   return r;
 }
 
+// a.px set: rays generated from pupil samples (ort_trace_pupil_vjp); NULL: resident input
+// rays a.in (ort_trace_sequential_vjp), per-ray wavelengths when a.w is set
 template <int P, uint32_t KM>
 __global__ __launch_bounds__(kBlock) void vjp_kernel(const KArgs a, const JArgs j) {
   using D = ort::Dual<P>;
   const int64_t rid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool active = rid < a.n_rays;
   const int64_t r_ld = active ? rid : 0;
-  const int64_t sidx = r_ld / a.seg_len;
-  const ort_segment sg = a.seg[sidx];
-  const int lam = sg.lambda_idx;
-  const int64_t p = a.pupil_per_ray ? r_ld : (r_ld - sidx * a.seg_len);
-  ort::RayT<D> r = ort::promote<D>(ort::generate_ray(sg, a.px[p], a.py[p], a.apod));
+  const int64_t sidx = a.seg ? r_ld / a.seg_len : 0;
+  int lam = 0;
+  double wl = 0.0;
+  ort::RayT<D> r;
+  if (a.px) {
+    const ort_segment sg = a.seg[sidx];
+    lam = sg.lambda_idx;
+    const int64_t p = a.pupil_per_ray ? r_ld : (r_ld - sidx * a.seg_len);
+    r = ort::promote<D>(ort::generate_ray(sg, a.px[p], a.py[p], a.apod));
+  } else {
+    if (a.seg) lam = a.seg[sidx].lambda_idx;
+    if (a.w) wl = a.w[r_ld];
+    ort::Ray q;
+    q.x = a.in.x[r_ld];
+    q.y = a.in.y[r_ld];
+    q.z = a.in.z[r_ld];
+    q.L = a.in.L[r_ld];
+    q.M = a.in.M[r_ld];
+    q.N = a.in.N[r_ld];
+    q.i = a.in.i[r_ld];
+    q.opd = a.in.opd[r_ld];
+    q.att = 0.0;
+    r = ort::promote<D>(q);
+  }
   const int64_t group = r_ld / a.group_len;
   const ort::ZSeed zs{j.zparam, j.p0};
   const int64_t ts = (int64_t)a.n_surf * 3;
+  double acc[P];
+#pragma unroll
+  for (int k = 0; k < P; ++k) acc[k] = 0.0;
 
   for (int si = a.start_surface; si < a.n_surf; ++si) {
     const ort_surface s = cst(a.surf)[si];
-    const ort_surface_optics o = optics_at(a, lam, si);
+    const ort_surface_optics o = a.w ? optics_ray(a, s, wl) : optics_at(a, lam, si);
     const D R = seeded<P>(s.radius, j.tan_surf, ts, si * 3 + 0, j);
     const D K = seeded<P>(s.conic, j.tan_surf, ts, si * 3 + 1, j);
     const D CZ = seeded<P>(s.cs_t[2], j.tan_surf, ts, si * 3 + 2, j);
@@ -898,14 +940,23 @@ __global__ __launch_bounds__(kBlock) void vjp_kernel(const KArgs a, const JArgs 
     r.x = r.x + s.cs_t[0];
     r.y = r.y + s.cs_t[1];
     r.z = r.z + CZ;
+    if (j.rec_cot && (s.flags & ORT_SURF_RECORD) && active) {  // this surface's record
+      const double* rc = j.rec_cot + (int64_t)s.rec_slot * 8 * a.n_rays;
+      cot_acc(acc, rc, rid, r.x);
+      cot_acc(acc, rc + a.n_rays, rid, r.y);
+      cot_acc(acc, rc + 2 * a.n_rays, rid, r.z);
+      cot_acc(acc, rc + 3 * a.n_rays, rid, r.L);
+      cot_acc(acc, rc + 4 * a.n_rays, rid, r.M);
+      cot_acc(acc, rc + 5 * a.n_rays, rid, r.N);
+      cot_acc(acc, rc + 6 * a.n_rays, rid, ort::intensity(r));
+      cot_acc(acc, rc + 7 * a.n_rays, rid, r.opd);
+    }
   }
   if (a.final_mat >= 0)
     ort::propagate(r, seeded<P>(a.final_thickness, j.tan_final, 1, 0, j),
-                   tab(a.alpha_tab, a.n_lambda, a.n_mat, lam, a.final_mat));
+                   a.w ? ort::absorption_alpha(ort::material_k(cst(a.mats)[a.final_mat], a.coef, wl), wl)
+                       : tab(a.alpha_tab, a.n_lambda, a.n_mat, lam, a.final_mat));
 
-  double acc[P];
-#pragma unroll
-  for (int k = 0; k < P; ++k) acc[k] = 0.0;
   if (active) {
     cot_acc(acc, j.cot.x, rid, r.x);
     cot_acc(acc, j.cot.y, rid, r.y);

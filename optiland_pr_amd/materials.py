@@ -31,8 +31,21 @@ def _glass_db():
     return _GLASSES
 
 
+class HomogeneousPropagation:
+    """propagation/homogeneous.py:18-57: straight-line propagation with absorption, the
+    only propagation model of the trace core (BaseMaterial.propagation_model)."""
+
+    def __init__(self, material):
+        self.material = material
+
+
 class BaseMaterial:
-    """materials/base.py:23-119 interface: n(wavelength), k(wavelength)."""
+    """materials/base.py:23-119 interface: n(wavelength), k(wavelength),
+    propagation_model (base.py:60-71: HomogeneousPropagation by default)."""
+
+    @property
+    def propagation_model(self):
+        return HomogeneousPropagation(self)
 
     def n(self, wavelength):
         w = np.atleast_1d(np.asarray(wavelength, dtype=np.float64))

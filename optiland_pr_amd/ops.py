@@ -1,0 +1,381 @@
+"""PyTorch custom ops over the C ABI: ``torch.ops.ort.trace_sequential`` and
+``torch.ops.ort.trace_pupil`` (SURVEY.md 8b "Torch custom op").
+
+The reference differentiates a trace by running every ``be.*`` primitive of
+``SurfaceGroup.trace`` (surfaces/surface_group.py:232-244) under torch autograd
+(backend/torch_backend.py:45-148, driven by optimization/optimizer/torch/base.py:116-131).
+Here the whole trace is ONE dispatcher op whose CUDA (HIP) kernel is the fused trace
+(ort_trace_sequential / ort_trace_pupil) and whose autograd formula is the adjoint (or
+forward-mode) VJP of the trace core (ort_trace_sequential_vjp / ort_trace_pupil_vjp), so
+autograd sees one node per trace call:
+
+  ort::trace_sequential(lens, rays[8], w, params, spec, start_surface, per_ray_w)
+      -> (x, y, z, L, M, N, i, opd, rec, sched)
+      resident rays in (SurfaceGroup.trace, the drop-in seam); rec = every traced
+      surface's record [S][8][n] (standard_surface.py:266-286); differentiable w.r.t. the
+      input rays, the record buffer's cotangents included, and the lens parameters in
+      `params`.
+  ort::trace_pupil(plan, params) -> (x, y, z, L, M, N, i, opd, sched)
+      rays generated from pupil samples in the same launch (Optic.trace's fused path,
+      raytrace/real_ray_tracer.py:37-97); differentiable w.r.t. the lens parameters.
+
+``lens`` / ``plan`` are integer handles of host objects (the uploaded lens tables, the
+pupil samples and segment descriptors): the dispatcher passes ints, and the tables they
+name are a few KB that the kernels read from HBM. ``params`` are the lens-parameter
+tensors that require grad and ``spec`` says which lens value each one is, as flattened
+(kind, traced-surface index) pairs with kind in SPEC_KINDS: the forward ignores their
+values (the lowered lens already holds them), the backward returns d loss / d each.
+
+There is no CPU kernel: on a CPU tensor the dispatcher raises (the product path has no
+fallback).
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import weakref
+
+import numpy as np
+import torch
+
+from . import _abi, _native
+
+SPEC_KINDS = ("zernike", "radius", "conic", "thickness", "vertex")
+
+# handle -> host object (DeviceLens / pupil plan); weak, so a handle never keeps a lens
+# alive (the autograd context holds the object itself for the backward)
+_HANDLES: "weakref.WeakValueDictionary[int, object]" = weakref.WeakValueDictionary()
+
+
+def handle(obj) -> int:
+    """Integer handle of a host object for the ops' `lens` / `plan` argument."""
+    h = id(obj)
+    _HANDLES[h] = obj
+    return h
+
+
+def _lookup(h):
+    obj = _HANDLES.get(int(h))
+    if obj is None:
+        raise RuntimeError(f"ort op: stale handle {h} (the lens / plan object was freed)")
+    return obj
+
+
+class PupilPlan:
+    """Everything ort::trace_pupil needs besides the parameter tensors."""
+
+    def __init__(self, dlens, seg_dev, px, py, n, seg_len, keys=(), pupil_per_ray=False):
+        self.dlens = dlens
+        self.seg_dev = seg_dev
+        self.px = px
+        self.py = py
+        self.n = int(n)
+        self.seg_len = int(seg_len)
+        self.keys = list(keys)
+        self.pupil_per_ray = bool(pupil_per_ray)
+
+
+def _spec_pairs(spec):
+    if len(spec) % 2:
+        raise ValueError("spec holds (kind, surface) pairs")
+    return [(SPEC_KINDS[int(spec[i])], int(spec[i + 1])) for i in range(0, len(spec), 2)]
+
+
+def encode_spec(pairs):
+    """[(kind name, traced-surface index)] -> the flat int list the ops take."""
+    out = []
+    for kind, si in pairs:
+        out += [SPEC_KINDS.index(kind), int(si)]
+    return out
+
+
+def tangent_tables(table, pairs, params):
+    """ort_vjp_params tables for the parameter tensors: (zern_param, surf_tangent,
+    final_tangent, n_param) -- numpy arrays or None. "vertex" is the vertex z of one
+    surface (its coordinate system's z, coordinate_system.py:73-107); "thickness" moves
+    every later vertex (optic_updater.py set_thickness)."""
+    S = table.n_surfaces
+    n_param = sum(int(t.numel()) for t in params)
+    zp = surf = final = None
+    off = 0
+    for (kind, si), t in zip(pairs, params, strict=True):
+        n = int(t.numel())
+        row = table.surfaces[si]
+        if kind == "zernike":
+            if int(row["geometry"]) != _abi.GEOM_ZERNIKE:
+                raise ValueError(f"surface {si}: Zernike coefficients of a non-Zernike surface")
+            if zp is None:
+                zp = np.full(max(1, len(table.zern)), -1, dtype=np.int32)
+            if n != int(row["n_coef"]):
+                raise ValueError(f"surface {si}: {n} coefficients, lowered {int(row['n_coef'])}")
+            base = int(row["coef_off"])
+            zp[base:base + n] = np.arange(off, off + n, dtype=np.int32)
+        else:
+            if n != 1:
+                raise ValueError(f"surface {si}: {kind} must be a scalar tensor")
+            if surf is None:
+                surf = np.zeros((n_param, S, 3), dtype=np.float64)
+            g = int(row["geometry"])
+            if kind in ("radius", "conic"):
+                if g in (_abi.GEOM_PLANE, _abi.GEOM_BICONIC, _abi.GEOM_TOROIDAL, _abi.GEOM_GRID_SAG):
+                    raise NotImplementedError(f"surface {si}: {kind} of this geometry is not a "
+                                              "differentiable parameter of the trace core")
+                surf[off, si, 0 if kind == "radius" else 1] = 1.0
+            elif kind == "vertex":
+                surf[off, si, 2] = 1.0
+            else:  # thickness after surface si moves every later vertex
+                surf[off, si + 1:, 2] = 1.0
+                if si == S - 1:  # the image surface's thickness: the final propagate
+                    if final is None:
+                        final = np.zeros(n_param, dtype=np.float64)
+                    final[off] = 1.0
+        off += n
+    return zp, surf, final, n_param
+
+
+def _check_differentiable(table):
+    if np.any(table.surfaces["geometry"] == _abi.GEOM_GRID_SAG):
+        raise NotImplementedError("autograd through grid-sag surfaces is not implemented by "
+                                  "the trace core (no derivative kernels)")
+    if table.interaction_mask & ~(1 << _abi.IA_REFRACT_REFLECT):
+        raise NotImplementedError("autograd through thin-lens, phase or grating surfaces is "
+                                  "not implemented by the trace core (no derivative kernels)")
+
+
+_WORKSPACE: dict = {}
+
+
+def _workspace(device, nbytes):
+    ws = _WORKSPACE.get(device)
+    if ws is None or ws.numel() < nbytes:
+        _WORKSPACE.pop(device, None)
+        ws = torch.empty(int(nbytes), dtype=torch.uint8, device=device)
+        _WORKSPACE[device] = ws
+    return ws
+
+
+def _ray_struct(ts):
+    return _native.ort_rays(*(0 if t is None else t.data_ptr() for t in ts))
+
+
+# --------------------------------------------------------------------------------------
+# ort::trace_sequential
+# --------------------------------------------------------------------------------------
+@torch.library.custom_op("ort::trace_sequential", mutates_args=(), device_types="cuda")
+def trace_sequential(lens: int, rays: list[torch.Tensor], w: torch.Tensor | None,
+                     params: list[torch.Tensor], spec: list[int], start_surface: int,
+                     per_ray_w: bool) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor,
+                                               torch.Tensor, torch.Tensor, torch.Tensor,
+                                               torch.Tensor, torch.Tensor, torch.Tensor,
+                                               torch.Tensor]:
+    from .raytrace import RealRays, trace_rays
+
+    dl = _lookup(lens)
+    if len(rays) != 8:
+        raise ValueError("rays: x, y, z, L, M, N, i, opd")
+    n = rays[0].numel()
+    dev = dl.device
+    rin = RealRays.__new__(RealRays)
+    for a, t in zip(_abi.RAY_FIELDS, rays, strict=True):
+        setattr(rin, a, t.detach().to(device=dev, dtype=torch.float64).reshape(-1).contiguous())
+    rin.w = w.detach() if w is not None else torch.zeros(1, dtype=torch.float64, device=dev)
+    rout = RealRays.__new__(RealRays)
+    for a in _abi.RAY_FIELDS:
+        setattr(rout, a, torch.empty(n, dtype=torch.float64, device=dev))
+    n_rec = dl.table.n_rec
+    rec = torch.empty(n_rec * 8 * n, dtype=torch.float64, device=dev)
+    trace_rays(dl, rin, rout, rec=rec if n_rec else None, start_surface=int(start_surface),
+               per_ray_w=bool(per_ray_w))
+    sched = dl.last_schedule
+    sched_t = (torch.empty(0, dtype=torch.int32, device=dev) if sched is None else
+               torch.from_numpy(np.ascontiguousarray(sched.reshape(-1), dtype=np.int32)).to(dev))
+    return (*(getattr(rout, a) for a in _abi.RAY_FIELDS), rec, sched_t)
+
+
+@trace_sequential.register_fake
+def _(lens, rays, w, params, spec, start_surface, per_ray_w):
+    dl = _lookup(lens)
+    n = rays[0].numel()
+    outs = [rays[0].new_empty(n, dtype=torch.float64) for _ in range(8)]
+    rec = rays[0].new_empty(dl.table.n_rec * 8 * n, dtype=torch.float64)
+    ns = dl.table.n_surfaces if dl.newton else 0
+    return (*outs, rec, rays[0].new_empty(ns, dtype=torch.int32))
+
+
+def _seq_setup(ctx, inputs, output):
+    lens, rays, w, params, spec, start_surface, per_ray_w = inputs
+    ctx.dlens = _lookup(lens)  # a strong reference for the backward
+    ctx.pairs = _spec_pairs(spec)
+    ctx.start_surface = int(start_surface)
+    ctx.per_ray_w = bool(per_ray_w)
+    ctx.shapes = [(p.shape, p.dtype, p.device) for p in params]
+    ctx.ray_meta = [(r.shape, r.dtype) for r in rays]
+    ctx.set_materialize_grads(False)
+    rec, sched = output[8], output[9]
+    saved = [r.detach() for r in rays] + [rec, sched]
+    if w is not None:
+        saved.append(w.detach())
+    ctx.has_w = w is not None
+    ctx.save_for_backward(*saved)
+
+
+def _seq_backward(ctx, *grads):
+    saved = ctx.saved_tensors
+    rays_in, rec, sched = saved[:8], saved[8], saved[9]
+    w = saved[10] if ctx.has_w else None
+    dl = ctx.dlens
+    table = dl.table
+    n = rays_in[0].numel()
+    dev = dl.device
+    # list inputs: needs_input_grad holds one bool per list element
+    want_rays = any(ctx.needs_input_grad[1])
+    want_params = any(ctx.needs_input_grad[3]) and len(ctx.shapes) > 0
+    cot = [None if g is None else g.detach().to(torch.float64).reshape(-1).contiguous()
+           for g in grads[:8]]
+    rec_cot = grads[8]
+    if rec_cot is not None:
+        rec_cot = rec_cot.detach().to(torch.float64).reshape(-1).contiguous()
+    none_rays, none_params = [None] * 8, [None] * len(ctx.shapes)
+    if not (want_rays or want_params) or (all(c is None for c in cot) and rec_cot is None):
+        return None, none_rays, None, none_params, None, None, None
+    _check_differentiable(table)
+    params_like = [torch.empty(s, dtype=d, device="meta") for s, d, _ in ctx.shapes]
+    zp, st, ft, n_param = tangent_tables(table, ctx.pairs, params_like)
+    g = torch.zeros(max(1, n_param), dtype=torch.float64, device=dev)
+    gin = [torch.zeros(n, dtype=torch.float64, device=dev) if want_rays else None
+           for _ in range(8)]
+    from .autodiff import vjp_mode
+
+    mode = vjp_mode(table)
+    if want_params and n_param:
+        _seq_vjp(dl, rays_in, w, ctx.per_ray_w, ctx.start_surface, sched, zp, st, ft,
+                 n_param, cot, rec_cot, rec, g, gin if mode == _abi.VJP_ADJOINT else None,
+                 mode)
+    if want_rays and not (want_params and n_param and mode == _abi.VJP_ADJOINT):
+        # input-ray cotangents come from the reverse-mode pass (forward mode carries only
+        # the parameter tangents): one adjoint launch with no parameters
+        _seq_vjp(dl, rays_in, w, ctx.per_ray_w, ctx.start_surface, sched, None, None, None,
+                 0, cot, rec_cot, rec, None, gin, _abi.VJP_ADJOINT)
+    ray_grads = none_rays
+    if want_rays:
+        ray_grads = [gi.reshape(s).to(d) for gi, (s, d) in zip(gin, ctx.ray_meta, strict=True)]
+    param_grads = none_params
+    if want_params:
+        param_grads = []
+        off = 0
+        for shape, dtype, pdev in ctx.shapes:
+            k = int(np.prod(shape)) if len(shape) else 1
+            param_grads.append(g[off:off + k].reshape(shape).to(device=pdev, dtype=dtype))
+            off += k
+    return None, ray_grads, None, param_grads, None, None, None
+
+
+def _seq_vjp(dl, rays_in, w, per_ray_w, start_surface, sched, zp, st, ft, n_param, cot,
+             rec_cot, rec, grad, gin, mode):
+    """One ort_trace_sequential_vjp call (grad += J^T cot, gin = input-ray cotangents)."""
+    from .raytrace import _ptr, _stream_handle
+
+    lib = _native.load()
+    n = rays_in[0].numel()
+    batch = _native.ort_batch(n, max(n, 1), max(n, 1), 0, 0, None)
+    w_keep = None
+    if per_ray_w:
+        w_keep = w.to(device=dl.device, dtype=torch.float64).reshape(-1)
+        w_keep = w_keep.expand(n).contiguous() if w_keep.numel() == 1 else w_keep.contiguous()
+        batch.w = w_keep.data_ptr()
+    sched_dev = sched if sched is not None and sched.numel() else None
+    opt = _native.ort_options(_abi.NEWTON_SCHEDULE, int(start_surface),
+                              None if sched_dev is None else sched_dev.data_ptr())
+    tabs = [None if a is None else torch.from_numpy(np.ascontiguousarray(a)).to(dl.device)
+            for a in (zp, st, ft)]
+    params = _native.ort_vjp_params(int(n_param), int(mode), _ptr(tabs[0]).value,
+                                    _ptr(tabs[1]).value, _ptr(tabs[2]).value,
+                                    0 if tabs[0] is None else int(tabs[0].numel()), 0, None, 0)
+    if mode == _abi.VJP_ADJOINT:
+        size = lib.ort_vjp_workspace_size(C.byref(dl.c), C.byref(batch), C.byref(params))
+        _native.check(int(size) if size < 0 else 0, "ort_vjp_workspace_size")
+        ws = _workspace(dl.device, size)
+        params.workspace = ws.data_ptr()
+        params.workspace_size = ws.numel()
+    rin_c = _ray_struct(rays_in)
+    cot_c = _ray_struct(cot)
+    gin_c = _ray_struct(gin if gin is not None else [None] * 8)
+    rc = lib.ort_trace_sequential_vjp(C.byref(dl.c), C.byref(rin_c), C.byref(batch),
+                                      C.byref(opt), C.byref(params), C.byref(cot_c),
+                                      _ptr(rec_cot), _ptr(rec if rec_cot is not None else None),
+                                      _ptr(grad), C.byref(gin_c), _stream_handle())
+    _native.check(rc, "ort_trace_sequential_vjp")
+    del w_keep, tabs  # ordered on the stream before any reuse of their memory
+
+
+trace_sequential.register_autograd(_seq_backward, setup_context=_seq_setup)
+
+
+# --------------------------------------------------------------------------------------
+# ort::trace_pupil
+# --------------------------------------------------------------------------------------
+@torch.library.custom_op("ort::trace_pupil", mutates_args=(), device_types="cuda")
+def trace_pupil(plan: int, params: list[torch.Tensor], spec: list[int]) -> tuple[
+        torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor,
+        torch.Tensor, torch.Tensor, torch.Tensor]:
+    from .raytrace import RealRays
+    from .raytrace import trace_pupil as _trace
+
+    p = _lookup(plan)
+    dl = p.dlens
+    out = RealRays.__new__(RealRays)
+    for a in _abi.RAY_FIELDS:
+        setattr(out, a, torch.empty(p.n, dtype=torch.float64, device=dl.device))
+    _trace(dl, p.seg_dev, p.px, p.py, out, p.n, p.seg_len, p.n, keys=p.keys,
+           pupil_per_ray=p.pupil_per_ray)
+    sched = dl.last_schedule
+    sched_t = (torch.empty(0, dtype=torch.int32, device=dl.device) if sched is None else
+               dl.resident("sched", sched.reshape(-1)).clone())
+    return (*(getattr(out, a) for a in _abi.RAY_FIELDS), sched_t)
+
+
+@trace_pupil.register_fake
+def _(plan, params, spec):
+    p = _lookup(plan)
+    ref = p.px
+    outs = [ref.new_empty(p.n, dtype=torch.float64) for _ in range(8)]
+    ns = p.dlens.table.n_surfaces if p.dlens.newton else 0
+    return (*outs, ref.new_empty(ns, dtype=torch.int32))
+
+
+def _pupil_setup(ctx, inputs, output):
+    plan, params, spec = inputs
+    ctx.plan = _lookup(plan)
+    ctx.pairs = _spec_pairs(spec)
+    ctx.shapes = [(p.shape, p.dtype, p.device) for p in params]
+    ctx.set_materialize_grads(False)
+    ctx.save_for_backward(output[8])
+
+
+def _pupil_backward(ctx, *grads):
+    from .autodiff import vjp
+
+    (sched,) = ctx.saved_tensors
+    p = ctx.plan
+    dl = p.dlens
+    if not any(ctx.needs_input_grad[1]) or not ctx.shapes:
+        return None, [None] * len(ctx.shapes), None
+    _check_differentiable(dl.table)
+    params_like = [torch.empty(s, dtype=d, device="meta") for s, d, _ in ctx.shapes]
+    zp, st, ft, n_param = tangent_tables(dl.table, ctx.pairs, params_like)
+    tables = tuple(None if a is None else dl.resident(("tangent", i), a)
+                   for i, a in enumerate((zp, st, ft)))
+    g = torch.zeros(n_param, dtype=torch.float64, device=dl.device)
+    cot = [None if gr is None else gr.to(torch.float64).contiguous() for gr in grads[:8]]
+    vjp(dl, p.seg_dev, p.px, p.py, p.n, p.seg_len, sched if sched.numel() else None, tables,
+        n_param, cot, g, pupil_per_ray=p.pupil_per_ray)
+    res = []
+    off = 0
+    for shape, dtype, pdev in ctx.shapes:
+        k = int(np.prod(shape)) if len(shape) else 1
+        res.append(g[off:off + k].reshape(shape).to(device=pdev, dtype=dtype))
+        off += k
+    return None, res, None
+
+
+trace_pupil.register_autograd(_pupil_backward, setup_context=_pupil_setup)
