@@ -662,17 +662,51 @@ def _cpu_baseline(args):
             t = time.perf_counter() - t0
             if t >= args.cpu_seconds and reps >= 2:
                 break
-    return {
-        "value": units * reps / t,
+    ratio = _ref_over_oracle()
+    value = units * reps / t
+    line = {
+        "value": value,
         "unit": "intersections/s",
         "cores": workers,
         "kind": "port",
         "single_process_value": units / t_single,
+        "host_cpus": os.cpu_count(),
+        "cpu_model": _cpu_model(),
         "sample": f"{label}: {n_rays} rays x {len(segs)} (field, lambda) pair(s) x {S} "
                   f"surfaces (generation + trace), NumPy oracle, {workers} processes x {reps} "
-                  f"repetitions: {t:.2f} s wall (1 process, 1 repetition: {t_single:.2f} s) on "
-                  f"{platform.processor() or platform.machine()}",
+                  f"repetitions: {t:.2f} s wall (1 process, 1 repetition: {t_single:.2f} s); "
+                  f"{workers} of the {os.cpu_count()} host CPUs = the GPU box's CPU share",
     }
+    if ratio:
+        # the reference itself (Optiland's NumPy backend) is slower than its restatement:
+        # tests/golden/cpu_ratio.json times both single-process on one host
+        line["ref_over_oracle"] = ratio["ref_over_oracle"]
+        line["reference_estimate_value"] = value / ratio["ref_over_oracle"]
+        line["ref_over_oracle_source"] = (
+            f"tests/golden/cpu_ratio.json: {ratio['workload']}; reference "
+            f"{ratio['reference_seconds']:.2f} s, oracle {ratio['oracle_seconds']:.2f} s on "
+            f"{ratio['cpu_model']} ({ratio['method']})")
+    return line
+
+
+def _cpu_model():
+    """The host CPU's model name (/proc/cpuinfo), as lscpu prints it."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or platform.machine()
+
+
+def _ref_over_oracle():
+    try:
+        with open(os.path.join(HERE, "tests", "golden", "cpu_ratio.json")) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
 
 
 if __name__ == "__main__":

@@ -195,6 +195,6 @@ def trace_pupil_grad(optic, dlens, seg_dev, px, py, n, seg_len, wavelength, keys
 
     params = parameters(optic)
     plan = ops.PupilPlan(dlens, seg_dev, px, py, n, seg_len, keys)
-    outs = torch.ops.ort.trace_pupil(ops.handle(plan), [t for _, _, t in params],
+    outs = torch.ops.ort.trace_pupil(ops.handle(plan), px, py, [t for _, _, t in params],
                                      ops.encode_spec([(k, si) for k, si, _ in params]))
     return outs[:8]

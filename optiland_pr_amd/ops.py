@@ -15,7 +15,7 @@ autograd sees one node per trace call:
       surface's record [S][8][n] (standard_surface.py:266-286); differentiable w.r.t. the
       input rays, the record buffer's cotangents included, and the lens parameters in
       `params`.
-  ort::trace_pupil(plan, params) -> (x, y, z, L, M, N, i, opd, sched)
+  ort::trace_pupil(plan, px, py, params, spec) -> (x, y, z, L, M, N, i, opd, sched)
       rays generated from pupil samples in the same launch (Optic.trace's fused path,
       raytrace/real_ray_tracer.py:37-97); differentiable w.r.t. the lens parameters.
 
@@ -209,6 +209,7 @@ def _seq_setup(ctx, inputs, output):
     ctx.start_surface = int(start_surface)
     ctx.per_ray_w = bool(per_ray_w)
     ctx.shapes = [(p.shape, p.dtype, p.device) for p in params]
+    ctx.n_spec = len(spec)
     ctx.ray_meta = [(r.shape, r.dtype) for r in rays]
     ctx.set_materialize_grads(False)
     rec, sched = output[8], output[9]
@@ -235,9 +236,10 @@ def _seq_backward(ctx, *grads):
     rec_cot = grads[8]
     if rec_cot is not None:
         rec_cot = rec_cot.detach().to(torch.float64).reshape(-1).contiguous()
-    none_rays, none_params = [None] * 8, [None] * len(ctx.shapes)
+    # list arguments (the int list `spec` too) take a list of Nones
+    none_rays, none_params, none_spec = [None] * 8, [None] * len(ctx.shapes), [None] * ctx.n_spec
     if not (want_rays or want_params) or (all(c is None for c in cot) and rec_cot is None):
-        return None, none_rays, None, none_params, None, None, None
+        return None, none_rays, None, none_params, none_spec, None, None
     _check_differentiable(table)
     params_like = [torch.empty(s, dtype=d, device="meta") for s, d, _ in ctx.shapes]
     zp, st, ft, n_param = tangent_tables(table, ctx.pairs, params_like)
@@ -267,7 +269,7 @@ def _seq_backward(ctx, *grads):
             k = int(np.prod(shape)) if len(shape) else 1
             param_grads.append(g[off:off + k].reshape(shape).to(device=pdev, dtype=dtype))
             off += k
-    return None, ray_grads, None, param_grads, None, None, None
+    return None, ray_grads, None, param_grads, none_spec, None, None
 
 
 def _seq_vjp(dl, rays_in, w, per_ray_w, start_surface, sched, zp, st, ft, n_param, cot,
@@ -315,7 +317,8 @@ trace_sequential.register_autograd(_seq_backward, setup_context=_seq_setup)
 # ort::trace_pupil
 # --------------------------------------------------------------------------------------
 @torch.library.custom_op("ort::trace_pupil", mutates_args=(), device_types="cuda")
-def trace_pupil(plan: int, params: list[torch.Tensor], spec: list[int]) -> tuple[
+def trace_pupil(plan: int, px: torch.Tensor, py: torch.Tensor, params: list[torch.Tensor],
+                spec: list[int]) -> tuple[
         torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor,
         torch.Tensor, torch.Tensor, torch.Tensor]:
     from .raytrace import RealRays
@@ -326,7 +329,7 @@ def trace_pupil(plan: int, params: list[torch.Tensor], spec: list[int]) -> tuple
     out = RealRays.__new__(RealRays)
     for a in _abi.RAY_FIELDS:
         setattr(out, a, torch.empty(p.n, dtype=torch.float64, device=dl.device))
-    _trace(dl, p.seg_dev, p.px, p.py, out, p.n, p.seg_len, p.n, keys=p.keys,
+    _trace(dl, p.seg_dev, px, py, out, p.n, p.seg_len, p.n, keys=p.keys,
            pupil_per_ray=p.pupil_per_ray)
     sched = dl.last_schedule
     sched_t = (torch.empty(0, dtype=torch.int32, device=dl.device) if sched is None else
@@ -335,18 +338,19 @@ def trace_pupil(plan: int, params: list[torch.Tensor], spec: list[int]) -> tuple
 
 
 @trace_pupil.register_fake
-def _(plan, params, spec):
+def _(plan, px, py, params, spec):
     p = _lookup(plan)
-    ref = p.px
+    ref = px
     outs = [ref.new_empty(p.n, dtype=torch.float64) for _ in range(8)]
     ns = p.dlens.table.n_surfaces if p.dlens.newton else 0
     return (*outs, ref.new_empty(ns, dtype=torch.int32))
 
 
 def _pupil_setup(ctx, inputs, output):
-    plan, params, spec = inputs
+    plan, px, py, params, spec = inputs
     ctx.plan = _lookup(plan)
     ctx.pairs = _spec_pairs(spec)
+    ctx.n_spec = len(spec)
     ctx.shapes = [(p.shape, p.dtype, p.device) for p in params]
     ctx.set_materialize_grads(False)
     ctx.save_for_backward(output[8])
@@ -358,8 +362,9 @@ def _pupil_backward(ctx, *grads):
     (sched,) = ctx.saved_tensors
     p = ctx.plan
     dl = p.dlens
-    if not any(ctx.needs_input_grad[1]) or not ctx.shapes:
-        return None, [None] * len(ctx.shapes), None
+    none_spec = [None] * ctx.n_spec
+    if not any(ctx.needs_input_grad[3]) or not ctx.shapes:
+        return None, None, None, [None] * len(ctx.shapes), none_spec
     _check_differentiable(dl.table)
     params_like = [torch.empty(s, dtype=d, device="meta") for s, d, _ in ctx.shapes]
     zp, st, ft, n_param = tangent_tables(dl.table, ctx.pairs, params_like)
@@ -375,7 +380,7 @@ def _pupil_backward(ctx, *grads):
         k = int(np.prod(shape)) if len(shape) else 1
         res.append(g[off:off + k].reshape(shape).to(device=pdev, dtype=dtype))
         off += k
-    return None, res, None
+    return None, None, None, res, none_spec
 
 
 trace_pupil.register_autograd(_pupil_backward, setup_context=_pupil_setup)
