@@ -236,11 +236,13 @@ def config4(args, dev, rank, world, torch):
     seg_dev = upload_segments(seg, dev)
     n = n_loc * len(pairs)
     out = RealRays.empty(n, 0.0, device=dev)
+    # the image-plane gather into rank 0: send / receive buffers allocated here, once
+    gather = distributed.ImageGather(len(pairs), n_p, dev) if world > 1 else None
 
     def step():
         trace_pupil(dl, seg_dev, px, py, out, n, n_loc, n, pupil_per_ray=True)
-        if world > 1:
-            distributed.gather_image_plane(out.x, out.y, n_loc, len(pairs), n_p)
+        if gather is not None:
+            gather.gather(out.x, out.y)
 
     def trace_ms(steps):
         """Device time of the trace launch alone (at N > 1 the step also gathers): events
@@ -257,31 +259,33 @@ def config4(args, dev, rank, world, torch):
         return sum(a.elapsed_time(b) for a, b in spans) / steps
 
     def gather_report(reps=5):
-        """The gather alone, after the timed region (every rank): bytes each rank sends
-        and the max-over-ranks time per gather."""
-        sent = 2 * 8 * n  # x, y doubles of this rank's slices
-        if world == 1:
-            return {"gather_bytes_per_rank": 0, "gather_ms": 0.0}
+        """The gather alone, after the timed region (every rank): bytes a rank sends, bytes
+        rank 0 receives, and the max-over-ranks time per gather."""
+        if gather is None:
+            return {"gather_bytes_per_rank": 0, "gather_bytes_into_rank0": 0, "gather_ms": 0.0}
         import torch.distributed as dist
 
         dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(reps):
-            distributed.gather_image_plane(out.x, out.y, n_loc, len(pairs), n_p)
+            gather.gather(out.x, out.y)
         torch.cuda.synchronize()
         t = torch.tensor([(time.perf_counter() - t0) / reps], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return {"gather_bytes_per_rank": sent, "gather_ms": float(t.item()) * 1e3}
+        recv = torch.tensor([gather.bytes_received], dtype=torch.float64, device=dev)
+        dist.all_reduce(recv, op=dist.ReduceOp.MAX)
+        return {"gather_bytes_per_rank": gather.send.numel() * 8,
+                "gather_bytes_into_rank0": int(recv.item()), "gather_ms": float(t.item()) * 1e3}
 
     return Workload(
         metric="ray-surface intersections/sec, ReverseTelephoto 7 fields x 7 lambda x 2M rays, "
                "sharded + RCCL gather of image-plane hits",
         unit="intersections/s", units=n_p * len(pairs) * S, step=step, scaling="strong",
         config={"workload": "ReverseTelephoto (samples/objectives.py:117-173), 49 (field, "
-                            "lambda) pairs x 2M rays (seed = pair), all_gather of image x,y",
+                            "lambda) pairs x 2M rays (seed = pair), gather of image x,y to rank 0",
                 "rays_total": n_p * len(pairs), "surfaces": S,
-                "parallelism": f"dp{world} (pupil shards of every pair) + all_gather"},
+                "parallelism": f"dp{world} (pupil shards of every pair) + gather to rank 0"},
         kernel="trace_closed_kernel<F_GEN> (ort_trace_pupil)", launches=1,
         bytes_per_launch=n * (16 + 64), flops_per_ray=None, pmc_file="hbm_traffic_c4.json",
         rays=n, extra=gather_report, trace_timer=trace_ms if world > 1 else None,

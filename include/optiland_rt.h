@@ -595,6 +595,20 @@ int64_t ort_spot_workspace_size(const ort_spot_layout* layout);
 int ort_spot_stats(const ort_rays* rays, const ort_spot_layout* layout, void* workspace,
                    int64_t workspace_size, double* out, void* stream);
 
+/* Sharded spot statistics: rays holds THIS rank's slice of every pair (layout->n_pupil
+ * rays per pair, the same pair order on every rank). Two phases, each two launches:
+ *   phase 1: out[pair][3] = { count, sum x, sum y } of this rank's i > 0 points (image
+ *            frame); the caller sums them over the ranks (all_reduce) -> sums1;
+ *   phase 2: the centroid of each field's ref_wl pair from the reduced sums1, then
+ *            out[pair][3] = { sum of (x - cx)^2 + (y - cy)^2, max radius, NaN flag } of
+ *            this rank's points; the caller reduces SUM, MAX, MAX over the ranks.
+ * Then, as spot_diagram.py:317-357 forms them: centroid = sum / count, rms radius =
+ * sqrt(sum r^2 / count), geometric radius = max radius (NaN when the flag is set or the
+ * spot is empty). workspace: ort_spot_workspace_size(layout) bytes. */
+int ort_spot_partials(const ort_rays* rays, const ort_spot_layout* layout, int32_t phase,
+                      const double* sums1, void* workspace, int64_t workspace_size,
+                      double* out, void* stream);
+
 /* ---- chief-ray wavefront (wavefront/strategy.py:68-239, opd.py:143-157) ------------
  * Host-formed constants of one (field, wavelength): the reference sphere centred on the
  * chief ray's image point (xc, yc, zc) with r2 = R**2 (R from the chief ray and the exit

@@ -113,7 +113,7 @@ EXPORTS = ("ort_abi_version", "ort_trace_sequential", "ort_trace_pupil", "ort_tr
            "ort_trace_sequential_vjp",
            "ort_vjp_workspace_size", "ort_generate_pupil",
            "ort_surface_sag_normal", "ort_surface_distance", "ort_generate_rays",
-           "ort_material_nk", "ort_spot_workspace_size", "ort_spot_stats",
+           "ort_material_nk", "ort_spot_workspace_size", "ort_spot_stats", "ort_spot_partials",
            "ort_wavefront_workspace_size", "ort_wavefront_opd")
 
 _lib = None
@@ -178,6 +178,9 @@ def load(path: str | None = None):
     lib.ort_spot_stats.restype = C.c_int
     lib.ort_spot_stats.argtypes = [P(ort_rays), P(ort_spot_layout), C.c_void_p, C.c_int64,
                                    C.c_void_p, C.c_void_p]
+    lib.ort_spot_partials.restype = C.c_int
+    lib.ort_spot_partials.argtypes = [P(ort_rays), P(ort_spot_layout), C.c_int32, C.c_void_p,
+                                      C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p]
     lib.ort_wavefront_workspace_size.restype = C.c_int64
     lib.ort_wavefront_workspace_size.argtypes = [C.c_int64]
     lib.ort_wavefront_opd.restype = C.c_int

@@ -39,7 +39,10 @@ struct SpotArgs {
   int32_t per_thread;   // rays per thread (chunk = per_thread * 256 rays)
   double* part1;        // [n_pairs][n_chunks][3]: count, sum x, sum y
   double* part2;        // [n_pairs][n_chunks][3]: sum r^2, max r, NaN flag
-  double* out;          // [n_pairs][5]
+  double* out;          // [n_pairs][5] (ort_spot_partials: [n_pairs][3])
+  // ort_spot_partials phase 2: the pairs' (count, sum x, sum y) reduced over every rank;
+  // the centroids come from these instead of this rank's part1
+  const double* gsum;
 };
 
 // one image point in the surface frame (visualization/system/utils.py:16-46: the point
@@ -98,7 +101,13 @@ __global__ __launch_bounds__(kSpotThreads) void spot_dev_kernel(const SpotArgs a
   // centroid of the field's reference-wavelength spot (spot_diagram.py:317-328)
   const int64_t ref = (pair / a.n_wl) * a.n_wl + a.ref_wl;
   double c[3];
-  reduce_rows(a.part1 + ref * a.n_chunks * 3, a.n_chunks, c, lds);
+  if (a.gsum) {
+    c[0] = a.gsum[ref * 3 + 0];
+    c[1] = a.gsum[ref * 3 + 1];
+    c[2] = a.gsum[ref * 3 + 2];
+  } else {
+    reduce_rows(a.part1 + ref * a.n_chunks * 3, a.n_chunks, c, lds);
+  }
   const double cx = c[1] / c[0], cy = c[2] / c[0];
 
   const int64_t j0 = (int64_t)blockIdx.x * a.per_thread * kSpotThreads + threadIdx.x;
@@ -178,6 +187,51 @@ __global__ __launch_bounds__(kSpotThreads) void spot_final_kernel(const SpotArgs
   }
 }
 
+// ort_spot_partials: one block per pair, the pair's chunk partials in index order ->
+// out[pair][3] (PASS 1: count, sum x, sum y; PASS 2: sum r^2, max r, NaN flag)
+template <int PASS>
+__global__ __launch_bounds__(kSpotThreads) void spot_pair_kernel(const SpotArgs a) {
+  const int64_t pair = blockIdx.x;
+  __shared__ double lds[4 * 3];
+  __shared__ double mx[4][2];
+  double* o = a.out + pair * 3;
+  if constexpr (PASS == 1) {
+    double v[3];
+    reduce_rows(a.part1 + pair * a.n_chunks * 3, a.n_chunks, v, lds);
+    if (threadIdx.x == 0) {
+      o[0] = v[0];
+      o[1] = v[1];
+      o[2] = v[2];
+    }
+  } else {
+    const double* p2 = a.part2 + pair * a.n_chunks * 3;
+    double t[1] = {0.0};
+    double m = 0.0, f = 0.0;
+    for (int k = threadIdx.x; k < a.n_chunks; k += kSpotThreads) {
+      t[0] += p2[k * 3 + 0];
+      m = ::fmax(m, p2[k * 3 + 1]);
+      f = ::fmax(f, p2[k * 3 + 2]);
+    }
+    block_sum<1>(t, lds);
+    m = wave_max(m);
+    f = wave_max(f);
+    if ((threadIdx.x & 63) == 0) {
+      mx[threadIdx.x >> 6][0] = m;
+      mx[threadIdx.x >> 6][1] = f;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int w = 1; w < kSpotThreads / 64; ++w) {
+        m = ::fmax(m, mx[w][0]);
+        f = ::fmax(f, mx[w][1]);
+      }
+      o[0] = t[0];
+      o[1] = m;
+      o[2] = f;
+    }
+  }
+}
+
 }  // namespace
 }  // namespace ortk
 
@@ -200,21 +254,21 @@ int64_t ort_spot_workspace_size(const ort_spot_layout* lay) {
   return pairs * spot_chunks(lay) * 3 * 2 * (int64_t)sizeof(double);
 }
 
-int ort_spot_stats(const ort_rays* rays, const ort_spot_layout* lay, void* workspace,
-                   int64_t workspace_size, double* out, void* stream) {
+static int spot_args(const ort_rays* rays, const ort_spot_layout* lay, void* workspace,
+                     int64_t workspace_size, double* out, SpotArgs& a, int64_t& pairs,
+                     int64_t& chunks) {
   if (!rays || !lay || !out) return ORT_ERR_ARG;
   const int64_t need = ort_spot_workspace_size(lay);
   if (need < 0) return (int)need;
   if (lay->ref_wl < 0 || lay->ref_wl >= lay->n_wl) return ORT_ERR_ARG;
   if (lay->n_local_ops < 0 || (lay->n_local_ops > 0 && !lay->local_ops)) return ORT_ERR_ARG;
-  const int64_t pairs = (int64_t)lay->n_fields * lay->n_wl;
+  pairs = (int64_t)lay->n_fields * lay->n_wl;
   if (pairs == 0) return ORT_OK;
   if (!workspace || workspace_size < need) return ORT_ERR_ARG;
   if (lay->n_pupil > 0 && (!rays->x || !rays->y || !rays->i)) return ORT_ERR_ARG;
   if (lay->n_pupil > 0 && lay->n_local_ops > 0 && !rays->z) return ORT_ERR_ARG;
-  const int64_t chunks = spot_chunks(lay);
+  chunks = spot_chunks(lay);
   if (spot_per_thread(lay) > 0x7fffffff || pairs > 65535) return ORT_ERR_ARG;
-  SpotArgs a{};
   a.x = rays->x;
   a.y = rays->y;
   a.z = rays->z;
@@ -229,11 +283,42 @@ int ort_spot_stats(const ort_rays* rays, const ort_spot_layout* lay, void* works
   a.part1 = (double*)workspace;
   a.part2 = a.part1 + pairs * chunks * 3;
   a.out = out;
+  return ORT_OK;
+}
+
+int ort_spot_stats(const ort_rays* rays, const ort_spot_layout* lay, void* workspace,
+                   int64_t workspace_size, double* out, void* stream) {
+  SpotArgs a{};
+  int64_t pairs = 0, chunks = 0;
+  const int rc = spot_args(rays, lay, workspace, workspace_size, out, a, pairs, chunks);
+  if (rc || pairs == 0) return rc;
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid((unsigned)chunks, (unsigned)pairs);  // n_pupil == 0: one empty chunk
   hipLaunchKernelGGL(spot_sum_kernel, grid, dim3(kSpotThreads), 0, s, a);
   hipLaunchKernelGGL(spot_dev_kernel, grid, dim3(kSpotThreads), 0, s, a);
   hipLaunchKernelGGL(spot_final_kernel, dim3((unsigned)pairs), dim3(kSpotThreads), 0, s, a);
+  return hipGetLastError() == hipSuccess ? ORT_OK : ORT_ERR_LAUNCH;
+}
+
+int ort_spot_partials(const ort_rays* rays, const ort_spot_layout* lay, int32_t phase,
+                      const double* sums1, void* workspace, int64_t workspace_size,
+                      double* out, void* stream) {
+  if (phase != 1 && phase != 2) return ORT_ERR_ARG;
+  if (phase == 2 && !sums1) return ORT_ERR_ARG;
+  SpotArgs a{};
+  int64_t pairs = 0, chunks = 0;
+  const int rc = spot_args(rays, lay, workspace, workspace_size, out, a, pairs, chunks);
+  if (rc || pairs == 0) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 grid((unsigned)chunks, (unsigned)pairs);
+  if (phase == 1) {
+    hipLaunchKernelGGL(spot_sum_kernel, grid, dim3(kSpotThreads), 0, s, a);
+    hipLaunchKernelGGL(spot_pair_kernel<1>, dim3((unsigned)pairs), dim3(kSpotThreads), 0, s, a);
+  } else {
+    a.gsum = sums1;
+    hipLaunchKernelGGL(spot_dev_kernel, grid, dim3(kSpotThreads), 0, s, a);
+    hipLaunchKernelGGL(spot_pair_kernel<2>, dim3((unsigned)pairs), dim3(kSpotThreads), 0, s, a);
+  }
   return hipGetLastError() == hipSuccess ? ORT_OK : ORT_ERR_LAUNCH;
 }
 

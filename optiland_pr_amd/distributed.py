@@ -6,10 +6,12 @@ each rank traces all pairs on its slice with the same lowered lens (no broadcast
 rank lowers the lens itself). There is no collective on the trace's data path.
 
 Two collectives exist only for the consumers:
-  * gather_image_plane: image-plane intercepts to rank 0 (SpotDiagram plots, parity),
-    one all_gather of equal-size padded shards (RCCL ring over xGMI);
-  * spot_statistics: centroid / RMS / max radius from per-pair partial sums, two
-    all_reduce calls of a few doubles per pair -- no intercepts move.
+  * ImageGather / gather_image_plane: image-plane intercepts to rank 0 (SpotDiagram
+    plots, parity), one torch.distributed.gather into pre-allocated buffers (RCCL
+    send / recv over xGMI: only rank 0 receives);
+  * ShardedSpotStatistics / spot_statistics: centroid / RMS / max radius from per-rank
+    partials of the device kernel (ort_spot_partials), two all-gathers of a few doubles
+    per pair combined in rank order -- no intercepts move.
 """
 
 from __future__ import annotations
@@ -102,61 +104,189 @@ def _agree_newton_schedule(dl, keys, segs, px, py, out, n, n_loc, group):
     del S
 
 
-def gather_image_plane(x, y, n_loc_pairs, n_pairs, n_p, group=None):
-    """All-gather image-plane (x, y) of every rank's [pair][local] rays and reassemble
-    the reference order [pair][pupil] (real_ray_tracer.py:74-77). Returns (X, Y) of
-    shape [n_pairs * n_p] on every rank."""
-    rank, world = world_info(group)
-    if world == 1:
-        return x, y
-    sizes = [shard_range(n_p, r, world) for r in range(world)]
-    maxloc = max(b - a for a, b in sizes)
-    buf = torch.full((2, n_pairs, maxloc), float("nan"), dtype=torch.float64, device=x.device)
-    nl = n_loc_pairs
-    if nl:
-        buf[0, :, :nl] = x.view(n_pairs, nl)
-        buf[1, :, :nl] = y.view(n_pairs, nl)
-    parts = [torch.empty_like(buf) for _ in range(world)]
-    dist.all_gather(parts, buf, group=group)
-    X = torch.empty((n_pairs, n_p), dtype=torch.float64, device=x.device)
-    Y = torch.empty_like(X)
-    for r, (a, b) in enumerate(sizes):
-        X[:, a:b] = parts[r][0, :, : b - a]
-        Y[:, a:b] = parts[r][1, :, : b - a]
-    return X.reshape(-1), Y.reshape(-1)
+class ImageGather:
+    """Image-plane intercepts of every rank to ONE rank (the RCCL gather of the
+    final intercepts over xGMI): torch.distributed.gather (ncclSend / ncclRecv pairs under
+    RCCL, each peer on its own xGMI link into rank dst), not an all-gather -- only dst
+    receives. Buffers are allocated once (constructor) and reused by every gather():
+    the per-rank send slab [fields][n_pairs][max local] (the tail of the shorter shards
+    stays NaN) and, on dst, one receive slab per rank plus the reassembled [n_pairs][n_p]
+    planes in the reference's order (real_ray_tracer.py:74-77).
+
+    Bytes: each rank sends fields x n_pairs x ceil(n_p / world) x 8; dst receives world - 1
+    such slabs (config 4 at N = 8, (x, y): 196 MB out of every rank, 1.37 GB into rank 0;
+    the all-gather this replaces moved 1.37 GB into EVERY rank)."""
+
+    def __init__(self, n_pairs, n_p, device, fields=2, dst=0, group=None):
+        self.rank, self.world = world_info(group)
+        self.group = group
+        self.dst = dst
+        self.n_pairs, self.n_p, self.fields = n_pairs, n_p, fields
+        self.sizes = [shard_range(n_p, r, self.world) for r in range(self.world)]
+        self.maxloc = max(b - a for a, b in self.sizes)
+        self.send = torch.full((fields, n_pairs, self.maxloc), float("nan"),
+                               dtype=torch.float64, device=device)
+        self.recv = None
+        self.planes = None
+        if self.rank == dst:
+            self.recv = [torch.empty_like(self.send) for _ in range(self.world)]
+            self.planes = torch.empty((fields, n_pairs, n_p), dtype=torch.float64,
+                                      device=device)
+
+    @property
+    def bytes_sent(self):
+        return 0 if self.world == 1 or self.rank == self.dst else self.send.numel() * 8
+
+    @property
+    def bytes_received(self):
+        return (self.world - 1) * self.send.numel() * 8 if self.rank == self.dst else 0
+
+    def gather(self, *cols):
+        """cols: this rank's [pair][local] arrays (flat), one per field. Returns the
+        [fields][n_pairs * n_p] planes on dst (None elsewhere)."""
+        a, b = self.sizes[self.rank]
+        nl = b - a
+        if self.world == 1:
+            for f, c in enumerate(cols):
+                self.planes[f].copy_(c.view(self.n_pairs, self.n_p))
+            return self.planes.view(self.fields, -1)
+        if nl:
+            for f, c in enumerate(cols):
+                self.send[f, :, :nl].copy_(c.view(self.n_pairs, nl))
+        dist.gather(self.send, self.recv if self.rank == self.dst else None, dst=self.dst,
+                    group=self.group)
+        if self.rank != self.dst:
+            return None
+        for r, (ra, rb) in enumerate(self.sizes):
+            src = self.send if r == self.rank else self.recv[r]
+            self.planes[:, :, ra:rb].copy_(src[:, :, : rb - ra])
+        return self.planes.view(self.fields, -1)
 
 
-def spot_statistics(x, y, i, n_fields, n_wl, ref_wl_index, group=None):
-    """Centroid (reference wavelength), RMS and max spot radius per (field, wl) from
-    sharded image-plane rays (spot_diagram.py:317-379) with two all_reduce calls.
-    x, y, i: this rank's rays laid out [field][wl][local]."""
-    n_pairs = n_fields * n_wl
-    X = x.view(n_pairs, -1)
-    Y = y.view(n_pairs, -1)
-    m = (i.view(n_pairs, -1) > 0).to(torch.float64)
-    Xm = torch.where(m > 0, X, torch.zeros_like(X))
-    Ym = torch.where(m > 0, Y, torch.zeros_like(Y))
-    sums = torch.stack([m.sum(1), Xm.sum(1), Ym.sum(1), (Xm * Xm).sum(1), (Ym * Ym).sum(1)], 1)
-    if world_info(group)[1] > 1:
-        dist.all_reduce(sums, group=group)
-    cnt, sx, sy, sxx, syy = sums.unbind(1)
-    mx = (sx / cnt).view(n_fields, n_wl)
-    my = (sy / cnt).view(n_fields, n_wl)
-    cx = mx[:, ref_wl_index].repeat_interleave(n_wl)
-    cy = my[:, ref_wl_index].repeat_interleave(n_wl)
-    # mean((x-cx)^2 + (y-cy)^2) = E[x^2] - 2 cx E[x] + cx^2 + (same in y)
-    ex, ey = sx / cnt, sy / cnt
-    ms = (sxx / cnt - 2 * cx * ex + cx * cx) + (syy / cnt - 2 * cy * ey + cy * cy)
-    rms = torch.sqrt(torch.clamp(ms, min=0.0))
-    r = torch.sqrt((X - cx[:, None]) ** 2 + (Y - cy[:, None]) ** 2)
-    r = torch.where(m > 0, r, torch.full_like(r, -1.0))
-    rmax = r.max(1).values if r.shape[1] else torch.full((n_pairs,), -1.0, dtype=torch.float64,
-                                                            device=x.device)
-    if world_info(group)[1] > 1:
-        dist.all_reduce(rmax, op=dist.ReduceOp.MAX, group=group)
-    return {
-        "centroid": torch.stack([mx[:, ref_wl_index], my[:, ref_wl_index]], 1),
-        "rms": rms.view(n_fields, n_wl),
-        "geo": rmax.view(n_fields, n_wl),
-        "count": cnt.view(n_fields, n_wl),
+def gather_image_plane(x, y, n_loc_pairs, n_pairs, n_p, group=None, dst=0):
+    """One-shot ImageGather: (X, Y) of shape [n_pairs * n_p] on rank dst, (None, None)
+    on the other ranks."""
+    g = ImageGather(n_pairs, n_p, x.device, 2, dst, group)
+    planes = g.gather(x, y)
+    if planes is None:
+        return None, None
+    return planes[0], planes[1]
+
+
+def combine_spot_partials(parts1, parts2=None):
+    """Fixed-order (rank 0, 1, ...) combination of every rank's ort_spot_partials:
+    parts1 [world][pairs][3] (count, sum x, sum y) -> sums1; parts2 [world][pairs][3]
+    (sum r^2, max r, NaN flag) -> (sum r^2, max r, flag). The same order on every rank,
+    so every rank holds the same bits."""
+    s1 = parts1[0].clone()
+    for r in range(1, parts1.shape[0]):
+        s1 += parts1[r]
+    if parts2 is None:
+        return s1
+    s2 = parts2[0].clone()
+    for r in range(1, parts2.shape[0]):
+        s2[:, 0] += parts2[r][:, 0]
+        s2[:, 1:] = torch.maximum(s2[:, 1:], parts2[r][:, 1:])
+    return s1, s2
+
+
+def finalize_spot(s1, s2, n_fields, n_wl, ref_wl):
+    """spot_diagram.py:317-357 from the combined sums: per pair (count, centroid x,
+    centroid y, rms radius, max radius) -- the ort_spot_stats row layout -- and the
+    dict of the earlier API (centroid of the reference wavelength, rms, geo, count)."""
+    n = s1[:, 0]
+    out = torch.empty((n_fields * n_wl, 5), dtype=torch.float64, device=s1.device)
+    out[:, 0] = n
+    out[:, 1] = s1[:, 1] / n
+    out[:, 2] = s1[:, 2] / n
+    out[:, 3] = torch.sqrt(s2[:, 0] / n)
+    bad = (s2[:, 2] != 0) | torch.isnan(s2[:, 0]) | (n == 0)
+    out[:, 4] = torch.where(bad, torch.full_like(n, float("nan")), s2[:, 1])
+    pairs = out.view(n_fields, n_wl, 5)
+    return out, {
+        "centroid": pairs[:, ref_wl, 1:3],
+        "rms": pairs[:, :, 3],
+        "geo": pairs[:, :, 4],
+        "count": pairs[:, :, 0],
     }
+
+
+class ShardedSpotStatistics:
+    """Spot-diagram statistics of sharded image rays (every rank holds its contiguous
+    slice of every (field, wavelength) pair), with the reference's formulas
+    (spot_diagram.py:317-357): two all-gathers of a few doubles per pair -- per-rank
+    (count, sum x, sum y) from ort_spot_partials phase 1, combined in rank order into the
+    global centroids; then per-rank (sum r^2, max r, NaN flag) about those centroids
+    (phase 2) -- so no intercepts move and the rms is sqrt(sum r^2 / n) about the global
+    centroid, as the reference forms it, not a one-pass E[x^2] - E[x]^2.
+
+    phase_fn(phase, sums1) -> this rank's [pairs][3] partials (default: ort_spot_partials
+    on `rays`, see run()); tests on CPU inject a NumPy restatement of it."""
+
+    def __init__(self, n_fields, n_wl, n_loc, ref_wl, surface=None, device=None, group=None):
+        self.n_fields, self.n_wl, self.n_loc, self.ref_wl = n_fields, n_wl, n_loc, ref_wl
+        self.group = group
+        self.rank, self.world = world_info(group)
+        self.device = device
+        self.pairs = n_fields * n_wl
+        self._dev = None
+        if device is not None and torch.device(device).type == "cuda":
+            from .analysis import SpotStatistics
+
+            # layout, image-frame ops and workspace of the local slice (no launch here)
+            self._dev = SpotStatistics(n_fields, n_wl, n_loc, ref_wl, surface, device)
+        dev = device if device is not None else "cpu"
+        self.local = torch.zeros((2, self.pairs, 3), dtype=torch.float64, device=dev)
+        self.gathered = torch.zeros((2, self.world, self.pairs, 3), dtype=torch.float64,
+                                    device=dev)
+
+    def _partials(self, rays, phase, sums1):
+        import ctypes as C
+
+        from . import _native
+        from .raytrace import _ptr, _stream_handle
+
+        d = self._dev
+        out = self.local[phase - 1]
+        rc = d._lib.ort_spot_partials(C.byref(rays.c_struct()), C.byref(d._lay), phase,
+                                      _ptr(sums1), C.c_void_p(d._ws.data_ptr()), d._size,
+                                      C.c_void_p(out.data_ptr()), _stream_handle())
+        _native.check(rc, "ort_spot_partials")
+        return out
+
+    def run(self, rays=None, phase_fn=None):
+        if phase_fn is None:
+            if self._dev is None:
+                raise RuntimeError("ShardedSpotStatistics needs the HIP device (ort_spot_partials)")
+            phase_fn = lambda ph, s: self._partials(rays, ph, s)  # noqa: E731
+        p1 = phase_fn(1, None)
+        g1 = self._gather(0, p1)
+        s1 = combine_spot_partials(g1)
+        p2 = phase_fn(2, s1)
+        g2 = self._gather(1, p2)
+        s1, s2 = combine_spot_partials(g1, g2)
+        return finalize_spot(s1, s2, self.n_fields, self.n_wl, self.ref_wl)
+
+    def _gather(self, k, part):
+        if self.world == 1:
+            return part.unsqueeze(0)
+        # rank r's rows land in gathered[k][r] (views of the pre-allocated buffer)
+        dist.all_gather(list(self.gathered[k].unbind(0)), part.contiguous(), group=self.group)
+        return self.gathered[k]
+
+
+def spot_statistics(x, y, i, n_fields, n_wl, ref_wl_index, group=None, z=None):
+    """Centroid (reference wavelength), RMS and max spot radius per (field, wl) of sharded
+    image-plane rays (spot_diagram.py:317-379): ShardedSpotStatistics on the device.
+    x, y, i: this rank's rays laid out [field][wl][local] (global image coordinates)."""
+    from .raytrace import RealRays
+
+    n_pairs = n_fields * n_wl
+    n_loc = x.numel() // max(1, n_pairs)
+    r = RealRays.__new__(RealRays)
+    r.x, r.y, r.i = x, y, i
+    r.z = z if z is not None else x
+    r.L = r.M = r.N = r.opd = x
+    st = ShardedSpotStatistics(n_fields, n_wl, n_loc, ref_wl_index, device=x.device,
+                               group=group)
+    return st.run(r)[1]

@@ -1,0 +1,96 @@
+"""GPU parity at the BASELINE configs' own sizes, against summaries the
+reference produced here (tests/golden/config_sizes.json, gen_config_sizes.py; and
+index.json _full, gen_golden.py):
+
+  config 1  the exact spot-diagram workload: Cooke triplet, Hy = 0 / 0.7 / 1, 0.55 um,
+            uniform 128 (37,932 rays): image-plane sums per field equal the reference's
+            (bit-exact trace => identical NumPy reductions), SpotDiagram centroids / radii
+            (device reduction, another summation order) rtol 1e-12;
+  config 4  3 of the 49 ReverseTelephoto (field, lambda) pairs at the full 2M random
+            rays (seed = pair index) through the bench's per-ray-pupil launch: NumPy sums of
+            x, y, opd, x^2, first / last ray identical to the reference's.
+"""
+
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.fail("needs the MI355X")
+    from optiland_pr_amd import _native
+
+    _native.load()
+    return torch
+
+
+@pytest.fixture(scope="module")
+def sizes():
+    with open(os.path.join(HERE, "golden", "config_sizes.json")) as f:
+        return json.load(f)
+
+
+def test_config1_spot_diagram_workload(torch, sizes, golden_index):
+    from optiland_pr_amd.analysis import SpotDiagram
+    from optiland_pr_amd.samples import CookeTriplet
+
+    ref = sizes["config1"]
+    lens = CookeTriplet()
+    spot = SpotDiagram(lens, wavelengths=[0.55], num_rings=128, distribution="uniform")
+    assert spot.rays.x.numel() == 3 * 12644
+    geo = [[float(v) for v in row] for row in spot.geometric_spot_radius()]
+    rms = [[float(v) for v in row] for row in spot.rms_spot_radius()]
+    cen = [[float(a), float(b)] for a, b in spot.centroid()]
+    np.testing.assert_allclose(geo, ref["geo"], rtol=1e-12)
+    np.testing.assert_allclose(rms, ref["rms"], rtol=1e-12)
+    np.testing.assert_allclose(cen, ref["centroid"], rtol=1e-12, atol=1e-15)
+    # the image-plane rays of each field: the reference's own NumPy sums, bit for bit
+    full = golden_index["_full"]["cooke_uniform128"]
+    x = spot.rays.x.cpu().numpy().reshape(3, -1)
+    y = spot.rays.y.cpu().numpy().reshape(3, -1)
+    for f in range(3):
+        assert x[f].size == full[f]["n"]
+        assert float(np.sum(x[f])) == full[f]["sum_x"]
+        assert float(np.sum(y[f])) == full[f]["sum_y"]
+        assert float(np.mean(y[f])) == full[f]["mean_y"]
+        assert float(np.std(y[f])) == full[f]["std_y"]
+
+
+@pytest.mark.parametrize("pair", [0, 24, 48])
+def test_config4_pairs_at_2m_rays(torch, sizes, pair):
+    from optiland_pr_amd.distribution import RandomDistribution
+    from optiland_pr_amd.lowering import segment_params
+    from optiland_pr_amd.raytrace import RealRays, lens_for, trace_pupil
+    from optiland_pr_amd.samples import ReverseTelephoto
+
+    ref = sizes["config4"][str(pair)]
+    lens = ReverseTelephoto()
+    wls = [float(w) for w in np.linspace(0.4861, 0.6563, 7)]
+    dl = lens_for(lens, wls)
+    seg = np.stack([segment_params(lens, 0.0, ref["hy"], pair % 7)])
+    assert wls[pair % 7] == ref["wavelength"]
+    d = RandomDistribution(seed=pair)
+    d.generate_points(2_000_000)
+    px = torch.as_tensor(np.asarray(d.x), device="cuda")
+    py = torch.as_tensor(np.asarray(d.y), device="cuda")
+    n = px.numel()
+    out = RealRays.empty(n, 0.0)
+    trace_pupil(dl, seg, px, py, out, n, n, n, pupil_per_ray=True)
+    x, y, opd = (getattr(out, a).cpu().numpy() for a in ("x", "y", "opd"))
+    assert x.size == ref["n"] and int(np.isnan(x).sum()) == ref["nan"]
+    assert float(np.sum(x)) == ref["sum_x"]
+    assert float(np.sum(y)) == ref["sum_y"]
+    assert float(np.sum(opd)) == ref["sum_opd"]
+    assert float(np.sum(x * x)) == ref["sum_x2"]
+    assert [float(x[0]), float(y[0]), float(opd[0])] == ref["first"]
+    assert [float(x[-1]), float(y[-1]), float(opd[-1])] == ref["last"]

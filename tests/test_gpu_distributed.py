@@ -13,7 +13,7 @@ import sys
 import numpy as np
 import pytest
 
-from tests.dist_worker_gpu import FIELDS, N_P, WAVELENGTHS, run
+from tests.dist_worker_gpu import case, run
 from tests.test_distributed_cpu import _free_port
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -29,7 +29,7 @@ def torch():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["dg", "rt_asph", "rt_asph_nan"])
+@pytest.mark.parametrize("name", ["dg", "rt_asph", "rt_asph_nan", "rt77"])
 def test_sharded_trace_equals_unsharded(torch, tmp_path, name):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
                OMP_NUM_THREADS="1")
@@ -45,6 +45,7 @@ def test_sharded_trace_equals_unsharded(torch, tmp_path, name):
     assert rcs == [0, 0]
     got = np.load(out)
 
+    FIELDS, WAVELENGTHS, N_P = case(name)
     rays, n, sched = run(name)  # no process group here: the whole batch in one launch
     assert n == N_P
     # every shard ran the whole pair's schedule (the agreement); with the NaN ray in the
@@ -64,15 +65,26 @@ def test_sharded_trace_equals_unsharded(torch, tmp_path, name):
         return
     assert not np.isnan(x).any()
 
-    # spot statistics from the per-rank partial sums vs the reference's formulas on the
-    # unsharded image plane (spot_diagram.py:317-357)
+    # spot statistics from the per-rank device partials vs ort_spot_stats on the unsharded
+    # image (counts exact; sums in another order: rtol 1e-12) and the reference's formulas
+    # (spot_diagram.py:317-357) on the unsharded image plane
+    from optiland_pr_amd.analysis import spot_statistics as unsharded_stats
+
     nf, nw = len(FIELDS), len(WAVELENGTHS)
+    ref_wl = nw // 2
+    rows = unsharded_stats(rays, nf, nw, N_P, ref_wl).cpu().numpy().reshape(nf, nw, 5)
+    np.testing.assert_array_equal(got["count"], rows[:, :, 0])
+    np.testing.assert_allclose(got["rms"], rows[:, :, 3], rtol=1e-12)
+    np.testing.assert_allclose(got["geo"], rows[:, :, 4], rtol=1e-12)
+    np.testing.assert_allclose(got["centroid"], rows[:, ref_wl, 1:3], rtol=1e-12)
     X, Y = x.reshape(nf * nw, N_P), y.reshape(nf * nw, N_P)
     for f in range(nf):
-        cx, cy = X[f * nw + 1].mean(), Y[f * nw + 1].mean()
+        cx, cy = X[f * nw + ref_wl].mean(), Y[f * nw + ref_wl].mean()
         for w in range(nw):
             p = f * nw + w
             d2 = (X[p] - cx) ** 2 + (Y[p] - cy) ** 2
-            np.testing.assert_allclose(got["rms"][f, w], np.sqrt(d2.mean()), rtol=1e-9)
+            np.testing.assert_allclose(got["rms"][f, w], np.sqrt(d2.mean()), rtol=1e-12)
             np.testing.assert_allclose(got["geo"][f, w], np.sqrt(d2.max()), rtol=1e-12)
             assert got["count"][f, w] == N_P
+    half = -(-N_P // 2)  # rank 0 received one padded (x, y) slab from rank 1
+    assert int(got["received"]) == 2 * nf * nw * half * 8
