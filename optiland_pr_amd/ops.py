@@ -236,8 +236,10 @@ def _seq_backward(ctx, *grads):
     rec_cot = grads[8]
     if rec_cot is not None:
         rec_cot = rec_cot.detach().to(torch.float64).reshape(-1).contiguous()
-    # list arguments (the int list `spec` too) take a list of Nones
-    none_rays, none_params, none_spec = [None] * 8, [None] * len(ctx.shapes), [None] * ctx.n_spec
+    # Tensor-list arguments take a list of Nones; the int list `spec` is one leaf of the
+    # argument structure, except when empty (then it reads as an empty tensor list)
+    none_rays, none_params = [None] * 8, [None] * len(ctx.shapes)
+    none_spec = [] if ctx.n_spec == 0 else None
     if not (want_rays or want_params) or (all(c is None for c in cot) and rec_cot is None):
         return None, none_rays, None, none_params, none_spec, None, None
     _check_differentiable(table)
@@ -362,7 +364,7 @@ def _pupil_backward(ctx, *grads):
     (sched,) = ctx.saved_tensors
     p = ctx.plan
     dl = p.dlens
-    none_spec = [None] * ctx.n_spec
+    none_spec = [] if ctx.n_spec == 0 else None  # see _seq_backward
     if not any(ctx.needs_input_grad[3]) or not ctx.shapes:
         return None, None, None, [None] * len(ctx.shapes), none_spec
     _check_differentiable(dl.table)
