@@ -299,6 +299,10 @@ def config5(args, dev, rank, world, torch):
     R = args.rays
     _, _, d = _pupil(rank, R, dev, torch)
     lens = ThreeMirrorAnastigmat()
+    # Newton schedules verified on the device once warm (ort_newton_fixup): the same
+    # schedules and results as the host check, without its per-step host round trip;
+    # range errors / unsettled schedules surface at raytrace.check_all_pending (below)
+    lens.newton_mode = "device"
     leaves = []
     for si in (1, 2, 3):
         g = lens.surface_group.surfaces[si].geometry
@@ -308,7 +312,8 @@ def config5(args, dev, rank, world, torch):
                          requires_grad=True)
         g.coefficients = t
         leaves.append(t)
-    opt = torch.optim.Adam(leaves, lr=1e-7)
+    # one fused Adam kernel for the 30 coefficients (instead of the foreach sequence)
+    opt = torch.optim.Adam(leaves, lr=1e-7, fused=True)
     S = 4
     state = {}
 
@@ -336,7 +341,7 @@ def config5(args, dev, rank, world, torch):
 
 def vjp_timer(step, steps, torch):
     """Device time of the backward's ort_trace_pupil_vjp launch sequence (adj_need +
-    adj_kernel + adj_reduce + adj_contract; adj_kernel is ~97% of it): events recorded on
+    adj_kernel + adj_param_reduce; adj_kernel is ~97% of it): events recorded on
     the launch stream around every call (autodiff.VJP_EVENTS), over `steps` extra steps
     run after the timed region so the event pairs do not touch the timed steps."""
     from optiland_pr_amd import autodiff
@@ -479,6 +484,9 @@ def main():
             line["config"]["rms_spot_radius_mm"] = [float(v) for v in st[:, 3]]
             line["config"]["geo_spot_radius_mm"] = [float(v) for v in st[:, 4]]
         elif getattr(w, "state", None):
+            from optiland_pr_amd import raytrace
+
+            raytrace.check_all_pending()  # device-verified Newton schedules: raise here
             loss = w.state.get("loss")
             line["config"]["final_loss"] = None if loss is None else float(loss)
         if extra:

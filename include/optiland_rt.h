@@ -406,8 +406,14 @@ typedef struct ort_options {
   /* first stop index of the ort_newton_stat.conv_mask window (>= 0; 0 covers every
    * schedule up to 127 updates -- the default max_iter is 100) */
   int32_t conv_base;
-  int32_t reserved;
+  int32_t flags;          /* ORT_OPT_NO_INIT: newton_stat / status are already initialised */
+                          /* (by ort_newton_fixup): the call issues no memset            */
+  /* nullable device int32: the launch does nothing unless *run_if == 1 (read on the
+   * device; lenses with Newton surfaces only). With ort_newton_fixup this re-traces on a
+   * corrected schedule without a host round trip. */
+  const int32_t* run_if;
 } ort_options;
+enum ort_option_flags { ORT_OPT_NO_INIT = 1 };
 
 /* status bits written with atomicOr into *status (device int32) */
 enum ort_status {
@@ -493,6 +499,12 @@ typedef struct ort_vjp_params {
   int32_t reserved;
   void* workspace;             /* ADJOINT: device scratch (tape + wave partials)        */
   int64_t workspace_size;      /* bytes available at workspace                          */
+  /* ADJOINT, nullable: device int32 [n_slot] (n_slot = 3 n_surfaces + n_zern + 1, slot
+   * order: radius, conic, vertex z of each surface, the Zernike terms, the final
+   * thickness), nonzero where some tangent is nonzero -- the slots the kernel must sum.
+   * It depends only on the tangent tables, so a caller that keeps them resident can keep
+   * this too; NULL: derived on the device by one extra launch per call. */
+  const int32_t* slot_need;
 } ort_vjp_params;
 
 /* Workspace bytes ORT_VJP_ADJOINT needs for this lens, batch and parameter set. */
@@ -554,6 +566,24 @@ int ort_surface_distance(const ort_lens* lens, int32_t surface, const ort_rays* 
                          int64_t n, const ort_options* opt, double* t,
                          ort_newton_stat* newton_stat, int32_t* status, void* stream);
 
+/* Device-side check of a Newton schedule (the host's speculate / verify step, see
+ * ORT_NEWTON_SCHEDULE), so a warm schedule is verified without a host round trip:
+ * reads the statistics `stats` [n_groups][n_surfaces] of a launch that ran `sched` and
+ * applies the reference's stopping rule (newton_raphson.py:140-149) per (group, Newton
+ * surface): the first stop index k < sched that every ray passed -> sched = k; sched below
+ * max_iter with a ray failing at sched -> sched grown (2 sched + 2, at least 8, then
+ * max_iter); sched is updated in place. *flag (device int32) = 0 when every schedule was
+ * right, 1 when one changed (re-launch with run_if = flag), 2 when a decision needs a
+ * conv_mask window beyond the one stats holds (the host must finish). prev_flag
+ * (nullable): when *prev_flag != 1 the stats belong to a launch that did not run, so
+ * nothing is checked and *flag = *prev_flag. One single-block launch. */
+int ort_newton_fixup(const ort_lens* lens, int64_t n_groups, const ort_newton_stat* stats,
+                     int32_t conv_base, int32_t* sched, const int32_t* prev_flag,
+                     int32_t* flag, ort_newton_stat* next_stats, int32_t* next_status,
+                     void* stream);
+/* next_stats / next_status (nullable): when *flag becomes 1 they are initialised for the
+ * re-launch (launch it with ORT_OPT_NO_INIT), so a round costs two launches. */
+
 /* Pupil coordinates of a distribution on the device: px[k], py[k] for k < n_points
  * (distribution.py:72-408; the grid kinds bit-identical to NumPy, cos / sin correctly
  * rounded). Feeds ort_trace_pupil without host-side sampling or a host-to-device copy. */
@@ -594,6 +624,19 @@ int64_t ort_spot_workspace_size(const ort_spot_layout* layout);
  * no synchronisation, no allocation (graph-capturable). */
 int ort_spot_stats(const ort_rays* rays, const ort_spot_layout* layout, void* workspace,
                    int64_t workspace_size, double* out, void* stream);
+
+/* RayOperand.rms_spot_size's reduction (optimization/operand/ray.py:300-340):
+ * rms = sqrt(mean((x - mean x)^2 + (y - mean y)^2)) over all n points (no intensity mask),
+ * two passes in a fixed order (the spot-statistics kernels with one pair). stats (device
+ * double[5]) = { n, mean x, mean y, rms, max radius }; rms (device double, nullable) gets
+ * the rms again as its own scalar (the autograd op's output). Three launches.
+ * ort_rms_spot_vjp: gx[i] = g (x_i - mean x) / (n rms), gy likewise, g = *grad_out (a
+ * device scalar, read on the device: no host synchronisation). One launch. */
+int64_t ort_rms_spot_workspace_size(int64_t n);
+int ort_rms_spot(const double* x, const double* y, int64_t n, void* workspace,
+                 int64_t workspace_size, double* stats, double* rms, void* stream);
+int ort_rms_spot_vjp(const double* x, const double* y, int64_t n, const double* stats,
+                     const double* grad_out, double* gx, double* gy, void* stream);
 
 /* Sharded spot statistics: rays holds THIS rank's slice of every pair (layout->n_pupil
  * rays per pair, the same pair order on every rank). Two phases, each two launches:

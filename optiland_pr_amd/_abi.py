@@ -203,6 +203,7 @@ NEWTON_STAT = np.dtype(
     [("conv_mask", "<u8", (2,)), ("last_bad", "<i4"), ("max_updates", "<i4")], align=True
 )
 assert NEWTON_STAT.itemsize == 24
+OPT_NO_INIT = 1  # ort_options.flags: ORT_OPT_NO_INIT
 CONV_WINDOW = 128  # stop indices per conv_mask window (ort_options.conv_base)
 
 RAY_FIELDS = ("x", "y", "z", "L", "M", "N", "i", "opd")

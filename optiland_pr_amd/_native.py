@@ -64,6 +64,7 @@ class ort_vjp_params(C.Structure):
         ("reserved", C.c_int32),
         ("workspace", C.c_void_p),
         ("workspace_size", C.c_int64),
+        ("slot_need", C.c_void_p),
     ]
 
 
@@ -88,7 +89,8 @@ class ort_options(C.Structure):
         ("start_surface", C.c_int32),
         ("sched", C.c_void_p),
         ("conv_base", C.c_int32),
-        ("reserved", C.c_int32),
+        ("flags", C.c_int32),
+        ("run_if", C.c_void_p),
     ]
 
 
@@ -111,9 +113,10 @@ class ort_wavefront_ref(C.Structure):
 
 EXPORTS = ("ort_abi_version", "ort_trace_sequential", "ort_trace_pupil", "ort_trace_pupil_vjp",
            "ort_trace_sequential_vjp",
-           "ort_vjp_workspace_size", "ort_generate_pupil",
+           "ort_vjp_workspace_size", "ort_generate_pupil", "ort_newton_fixup",
            "ort_surface_sag_normal", "ort_surface_distance", "ort_generate_rays",
            "ort_material_nk", "ort_spot_workspace_size", "ort_spot_stats", "ort_spot_partials",
+           "ort_rms_spot_workspace_size", "ort_rms_spot", "ort_rms_spot_vjp",
            "ort_wavefront_workspace_size", "ort_wavefront_opd")
 
 _lib = None
@@ -165,6 +168,10 @@ def load(path: str | None = None):
     lib.ort_surface_distance.argtypes = [P(ort_lens), C.c_int32, P(ort_rays), C.c_int64,
                                          P(ort_options), C.c_void_p, C.c_void_p, C.c_void_p,
                                          C.c_void_p]
+    lib.ort_newton_fixup.restype = C.c_int
+    lib.ort_newton_fixup.argtypes = [P(ort_lens), C.c_int64, C.c_void_p, C.c_int32,
+                                     C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                     C.c_void_p, C.c_void_p]
     lib.ort_generate_pupil.restype = C.c_int
     lib.ort_generate_pupil.argtypes = [P(ort_pupil), C.c_void_p, C.c_void_p, C.c_void_p]
     lib.ort_material_nk.restype = C.c_int
@@ -181,6 +188,14 @@ def load(path: str | None = None):
     lib.ort_spot_partials.restype = C.c_int
     lib.ort_spot_partials.argtypes = [P(ort_rays), P(ort_spot_layout), C.c_int32, C.c_void_p,
                                       C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p]
+    lib.ort_rms_spot_workspace_size.restype = C.c_int64
+    lib.ort_rms_spot_workspace_size.argtypes = [C.c_int64]
+    lib.ort_rms_spot.restype = C.c_int
+    lib.ort_rms_spot.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64,
+                                 C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.ort_rms_spot_vjp.restype = C.c_int
+    lib.ort_rms_spot_vjp.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p,
+                                     C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
     lib.ort_wavefront_workspace_size.restype = C.c_int64
     lib.ort_wavefront_workspace_size.argtypes = [C.c_int64]
     lib.ort_wavefront_opd.restype = C.c_int

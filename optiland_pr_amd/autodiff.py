@@ -162,11 +162,12 @@ def vjp(dlens, seg_dev, px, py, n, seg_len, sched_dev, tables, n_param, cot, gra
     batch.apod = None if dlens.apod is None else dlens.apod.data_ptr()
     opt = _native.ort_options(_abi.NEWTON_SCHEDULE, 0,
                               None if sched_dev is None else sched_dev.data_ptr())
-    zp, st, ft = tables
+    zp, st, ft = tables[:3]
+    need = tables[3] if len(tables) > 3 else None  # ort_vjp_params.slot_need (resident)
     mode = vjp_mode(dlens.table) if mode is None else mode
     params = _native.ort_vjp_params(int(n_param), int(mode), _ptr(zp).value, _ptr(st).value,
                                     _ptr(ft).value, 0 if zp is None else int(zp.numel()), 0,
-                                    None, 0)
+                                    None, 0, _ptr(need).value)
     if mode == _abi.VJP_ADJOINT:
         size = lib.ort_vjp_workspace_size(C.byref(dlens.c), C.byref(batch), C.byref(params))
         _native.check(int(size) if size < 0 else 0, "ort_vjp_workspace_size")
@@ -187,14 +188,15 @@ def vjp(dlens, seg_dev, px, py, n, seg_len, sched_dev, tables, n_param, cot, gra
         timer.append(ev)
 
 
-def trace_pupil_grad(optic, dlens, seg_dev, px, py, n, seg_len, wavelength, keys):
+def trace_pupil_grad(optic, dlens, seg_dev, px, py, n, seg_len, wavelength, keys,
+                     newton_mode="reference"):
     """Differentiable fused trace: returns the 8 output tensors connected to the
     parameter tensors of parameters(optic), through the torch.ops.ort.trace_pupil custom
     op (ops.py) whose autograd formula is ort_trace_pupil_vjp."""
     from . import ops
 
     params = parameters(optic)
-    plan = ops.PupilPlan(dlens, seg_dev, px, py, n, seg_len, keys)
+    plan = ops.PupilPlan(dlens, seg_dev, px, py, n, seg_len, keys, newton_mode=newton_mode)
     outs = torch.ops.ort.trace_pupil(ops.handle(plan), px, py, [t for _, _, t in params],
                                      ops.encode_spec([(k, si) for k, si, _ in params]))
     return outs[:8]

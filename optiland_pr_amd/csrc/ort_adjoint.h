@@ -29,9 +29,10 @@
 // numbers seeded on those inputs; the Zernike coefficients from one transposed pass
 // over the terms (ort::zernike_coef_adjoint). Each per-ray contribution to a parameter
 // "slot" (radius / conic / vertex z of each surface, each Zernike term, the image-space
-// propagation distance) is summed over the wave and written to partial[slot][wave];
-// adj_reduce_kernel sums the waves in a fixed order (deterministic) and
-// adj_contract_kernel maps slots to parameters through the tangent tables.
+// propagation distance) is summed over the wave and written to partial[slot][wave] (every
+// needed (slot, wave) entry by this launch: no memset); adj_param_reduce_kernel sums, per
+// parameter, the waves of its slots in a fixed order (deterministic) weighted by the
+// tangent tables.
 #pragma once
 
 #include "ort_kernels.h"
@@ -56,7 +57,9 @@ struct AArgs {
   double* tape;             // [n_surf][kTapeRows][n_rays]
   double* partial;          // [n_slot][n_wave]
   double* slot_sum;         // [n_slot]
-  int32_t* need;            // [n_slot]: some parameter depends on this slot
+  const int32_t* need;      // [n_slot]: some parameter depends on this slot
+  int32_t zero_partials;    // adj_run: memset the partials first (start_surface > 0: the
+                            // earlier surfaces' slots are never written)
   double* grad;             // [n_param], accumulated
 };
 
@@ -507,6 +510,9 @@ __global__ __launch_bounds__(kBlock) ORT_ADJ_OCC void adj_kernel(const KArgs a, 
     emit(3 * si + 1, bk, true);
     emit(3 * si + 2, bCZ, true);
   }
+  // no image-space propagate: the final-thickness slot still gets its (zero) partial,
+  // so every needed (slot, wave) partial is written by this launch (no memset)
+  if (a.final_mat < 0) emit(3 * a.n_surf + j.n_zern, 0.0, true);
   if constexpr (RES) {
     // cotangents of the input rays: the adjoint state at the first traced surface; opd
     // passes straight through, i through the clip / absorption factors
@@ -530,7 +536,7 @@ AdjFn select_adj2r(uint32_t km);  // ort_k_adj2r.hip  (resident rays)
 AdjFn select_adj4r(uint32_t km);  // ort_k_adj4r.hip
 // zero the partials, flag the needed slots, run the adjoint kernel, reduce, contract
 // (ort_k_adj.hip)
-int adj_run(const KArgs& a, const AArgs& j, int tangents, uint32_t km, bool resident,
-            int64_t blocks, hipStream_t stream);
+int adj_run(const KArgs& a, AArgs j, int32_t* need_ws, int tangents, uint32_t km,
+            bool resident, int64_t blocks, hipStream_t stream);
 
 }  // namespace ortk

@@ -68,6 +68,8 @@ int fill_args(KArgs& a, const ort_lens* lens, const ort_batch* batch, const ort_
   a.start_surface = opt->start_surface;
   a.sched = opt->sched;
   a.conv_base = opt->conv_base;
+  a.run_if = opt->run_if;
+  a.no_init = (opt->flags & ORT_OPT_NO_INIT) != 0;
   if (opt->conv_base < 0) return ORT_ERR_ARG;
   // geometry ids this library knows (enum ort_geometry): anything else is refused here
   // rather than traced as some other kind
@@ -128,6 +130,7 @@ int launch(const KArgs& a_in, uint32_t feat, hipStream_t stream) {
 }
 
 int init_outputs(const KArgs& a, hipStream_t stream) {
+  if (a.no_init) return ORT_OK;  // ORT_OPT_NO_INIT: ort_newton_fixup initialised them
   if (a.stats) {
     const int64_t groups = (a.n_rays + a.group_len - 1) / a.group_len;
     // conv_mask = {~0, ~0}, last_bad = -1, max_updates = -1 (all 0xFF bytes)
@@ -284,10 +287,12 @@ static int vjp_run(const ort_lens* lens, const double* px, const double* py,
     aj.tape = (double*)(w + L.tape);
     aj.partial = (double*)(w + L.partial);
     aj.slot_sum = (double*)(w + L.slot_sum);
-    aj.need = (int32_t*)(w + L.need);
+    aj.need = params->slot_need;  // NULL: adj_run derives it into the workspace
+    aj.zero_partials = opt->start_surface > 0;
     aj.grad = grad;
     // radius / conic tangents need duals seeded on them too
-    return adj_run(a, aj, params->surf_tangent ? 4 : 2, km, resident, blocks, s);
+    return adj_run(a, aj, (int32_t*)(w + L.need), params->surf_tangent ? 4 : 2, km, resident,
+                   blocks, s);
   }
   if (params->mode != ORT_VJP_UNROLLED) return ORT_ERR_ARG;
   if (want_in) return ORT_ERR_ARG;  // forward mode carries parameter tangents only

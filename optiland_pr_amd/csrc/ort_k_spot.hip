@@ -43,6 +43,7 @@ struct SpotArgs {
   // ort_spot_partials phase 2: the pairs' (count, sum x, sum y) reduced over every rank;
   // the centroids come from these instead of this rank's part1
   const double* gsum;
+  double* rms_out;      // ort_rms_spot: the rms radius of pair 0 again, as its own scalar
 };
 
 // one image point in the surface frame (visualization/system/utils.py:16-46: the point
@@ -77,7 +78,7 @@ __global__ __launch_bounds__(kSpotThreads) void spot_sum_kernel(const SpotArgs a
     const int64_t j = j0 + (int64_t)k * kSpotThreads;
     if (j >= a.n_pupil) break;
     const int64_t r = pair * a.n_pupil + j;
-    if (a.i[r] > 0.0) {  // spot_diagram.py:425-427
+    if (!a.i || a.i[r] > 0.0) {  // spot_diagram.py:425-427 (i == NULL: every point)
       double x, y;
       local_point(a, r, x, y);
       v[0] += 1.0;
@@ -116,7 +117,7 @@ __global__ __launch_bounds__(kSpotThreads) void spot_dev_kernel(const SpotArgs a
     const int64_t j = j0 + (int64_t)k * kSpotThreads;
     if (j >= a.n_pupil) break;
     const int64_t r = pair * a.n_pupil + j;
-    if (a.i[r] > 0.0) {
+    if (!a.i || a.i[r] > 0.0) {
       double x, y;
       local_point(a, r, x, y);
       const double dx = x - cx, dy = y - cy;
@@ -184,6 +185,7 @@ __global__ __launch_bounds__(kSpotThreads) void spot_final_kernel(const SpotArgs
     o[2] = own[2] / n;
     o[3] = ::sqrt(t[0] / n);  // be.sqrt(be.mean(x**2 + y**2))
     o[4] = (f != 0.0 || t[0] != t[0] || n == 0.0) ? __builtin_nan("") : m;  // be.max
+    if (a.rms_out && pair == 0) *a.rms_out = o[3];
   }
 }
 
@@ -230,6 +232,20 @@ __global__ __launch_bounds__(kSpotThreads) void spot_pair_kernel(const SpotArgs 
       o[2] = f;
     }
   }
+}
+
+// d rms / d (x_i, y_i) = (x_i - mean x, y_i - mean y) / (n rms) times the upstream
+// gradient (torch's chain through sqrt, mean and the squares; the mean's own share,
+// sum_k (x_k - mean x) / n, is zero up to rounding and dropped)
+__global__ __launch_bounds__(kSpotThreads) void rms_spot_vjp_kernel(
+    const double* x, const double* y, int64_t n, const double* stats, const double* grad_out,
+    double* gx, double* gy) {
+  const int64_t i = (int64_t)blockIdx.x * kSpotThreads + threadIdx.x;
+  if (i >= n) return;
+  const double cx = stats[1], cy = stats[2];
+  const double w = *grad_out / (stats[0] * stats[3]);
+  gx[i] = (x[i] - cx) * w;
+  gy[i] = (y[i] - cy) * w;
 }
 
 }  // namespace
@@ -297,6 +313,53 @@ int ort_spot_stats(const ort_rays* rays, const ort_spot_layout* lay, void* works
   hipLaunchKernelGGL(spot_sum_kernel, grid, dim3(kSpotThreads), 0, s, a);
   hipLaunchKernelGGL(spot_dev_kernel, grid, dim3(kSpotThreads), 0, s, a);
   hipLaunchKernelGGL(spot_final_kernel, dim3((unsigned)pairs), dim3(kSpotThreads), 0, s, a);
+  return hipGetLastError() == hipSuccess ? ORT_OK : ORT_ERR_LAUNCH;
+}
+
+// ---- RayOperand.rms_spot_size (optimization/operand/ray.py:300-340) -----------------
+// rms = sqrt(mean((x - mean x)^2 + (y - mean y)^2)) over ALL n points (no intensity mask),
+// by the spot-statistics passes above with one pair: stats[5] as ort_spot_stats' row.
+int64_t ort_rms_spot_workspace_size(int64_t n) {
+  ort_spot_layout lay{};
+  lay.n_pupil = n;
+  lay.n_fields = 1;
+  lay.n_wl = 1;
+  return ort_spot_workspace_size(&lay);
+}
+
+int ort_rms_spot(const double* x, const double* y, int64_t n, void* workspace,
+                 int64_t workspace_size, double* stats, double* rms, void* stream) {
+  if (n < 0 || !stats || (n > 0 && (!x || !y))) return ORT_ERR_ARG;
+  ort_spot_layout lay{};
+  lay.n_pupil = n;
+  lay.n_fields = 1;
+  lay.n_wl = 1;
+  ort_rays r{};
+  r.x = (double*)x;
+  r.y = (double*)y;
+  r.i = (double*)x;  // validated as present, then replaced by "no mask" below
+  SpotArgs a{};
+  int64_t pairs = 0, chunks = 0;
+  int rc = spot_args(&r, &lay, workspace, workspace_size, stats, a, pairs, chunks);
+  if (rc) return rc;
+  a.i = nullptr;  // every point counts (the operand does not mask vignetted rays)
+  a.rms_out = rms;
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 grid((unsigned)chunks, 1u);
+  hipLaunchKernelGGL(spot_sum_kernel, grid, dim3(kSpotThreads), 0, s, a);
+  hipLaunchKernelGGL(spot_dev_kernel, grid, dim3(kSpotThreads), 0, s, a);
+  hipLaunchKernelGGL(spot_final_kernel, dim3(1u), dim3(kSpotThreads), 0, s, a);
+  return hipGetLastError() == hipSuccess ? ORT_OK : ORT_ERR_LAUNCH;
+}
+
+int ort_rms_spot_vjp(const double* x, const double* y, int64_t n, const double* stats,
+                     const double* grad_out, double* gx, double* gy, void* stream) {
+  if (n < 0 || !stats || !grad_out || (n > 0 && (!x || !y || !gx || !gy))) return ORT_ERR_ARG;
+  if (n == 0) return ORT_OK;
+  const int64_t blocks = (n + kSpotThreads - 1) / kSpotThreads;
+  if (blocks > 0x7fffffff) return ORT_ERR_ARG;
+  hipLaunchKernelGGL(rms_spot_vjp_kernel, dim3((unsigned)blocks), dim3(kSpotThreads), 0,
+                     (hipStream_t)stream, x, y, n, stats, grad_out, gx, gy);
   return hipGetLastError() == hipSuccess ? ORT_OK : ORT_ERR_LAUNCH;
 }
 

@@ -116,6 +116,9 @@ struct KArgs {
   // trace_kernel: blocks walk the pupil chunk by chunk over all (field, lambda) segments
   // (pair_major_ray); set by the host only when it is a bijection (see launch)
   int32_t block_remap;
+  // nullable: the launch is a no-op unless *run_if != 0 (ort_options.run_if)
+  const int32_t* run_if;
+  int32_t no_init;  // host side only: ORT_OPT_NO_INIT (skip init_outputs)
 };
 
 // Ray of this thread when every (field, lambda) segment traces the SAME pupil samples
@@ -449,6 +452,7 @@ struct TraceWaves {
 #endif
 template <uint32_t FEAT>
 __global__ __launch_bounds__(kBlock) ORT_TRACE_OCC void trace_kernel(const KArgs a) {
+  if (a.run_if && *cst(a.run_if) != 1) return;  // a device-side re-trace that is not needed
   const int64_t rid =
       a.block_remap ? pair_major_ray(a) : (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool active = rid < a.n_rays;

@@ -279,6 +279,17 @@ def radial_coefficients(n, m_abs):
     return tuple(a), tuple(d)
 
 
+@functools.lru_cache(maxsize=None)
+def _zernike_structure(kind, n_c):
+    """(norm, n, m, a_k, d_k) of the first n_c terms of a scheme: value-independent, so
+    computed once (the lowering runs on every trace call)."""
+    out = []
+    for n, m in zernike_indices(kind, n_c):
+        a, d = radial_coefficients(n, abs(m))
+        out.append((float(_norm_constant(kind, n, m)), n, m, a, d))
+    return tuple(out)
+
+
 class ZernikePolynomialGeometry(NewtonRaphsonGeometry):
     """geometries/zernike.py:33-246: conic + sum_j c_j N_nm R_n^|m|(rho) {cos|sin}(m phi)."""
 
@@ -312,12 +323,8 @@ class ZernikePolynomialGeometry(NewtonRaphsonGeometry):
             coeffs = np.zeros(n_c)
         elif hasattr(coeffs, "detach"):  # torch tensor (autograd leaf, autodiff.py)
             coeffs = coeffs.detach().cpu().numpy()
-        idx = zernike_indices(self.zernike_type, n_c)
-        out = []
-        for (n, m), c in zip(idx, coeffs, strict=True):
-            a, d = radial_coefficients(n, abs(m))
-            out.append((float(c), float(_norm_constant(self.zernike_type, n, m)), n, m, a, d))
-        return out
+        return [(float(c), *st) for c, st in
+                zip(coeffs, _zernike_structure(self.zernike_type, n_c), strict=True)]
 
 
 class PolynomialGeometry(NewtonRaphsonGeometry):

@@ -4,7 +4,8 @@ RayOperand.rms_spot_size (optimization/operand/ray.py:300-340) is the loss of co
 (torch-autograd step): it reads the image record after Optic.trace. With torch-tensor
 Zernike coefficients that require grad, Optic.trace runs the differentiable trace
 (autodiff.py) and the value returned here back-propagates to the coefficients through
-ort_trace_pupil_vjp. The reductions (mean, sqrt) are torch ops on the device.
+ort_trace_pupil_vjp. The reduction is the custom op torch.ops.ort.rms_spot (ops.py:
+ort_rms_spot's two deterministic passes, ort_rms_spot_vjp for its gradient).
 """
 
 from __future__ import annotations
@@ -33,10 +34,28 @@ class RayOperand:
             r2 = [(x - mx) ** 2 + (y - my) ** 2 for x, y in zip(xs, ys, strict=True)]
             return torch.sqrt(torch.mean(torch.cat(r2)))
         optic.trace(Hx, Hy, wavelength, num_rays, distribution)
-        x = optic.surface_group.x[surface_number, :].flatten()
-        y = optic.surface_group.y[surface_number, :].flatten()
+        x = _record_row(optic.surface_group, "x", surface_number)
+        y = _record_row(optic.surface_group, "y", surface_number)
+        if torch.is_tensor(x) and x.is_cuda:
+            # the reduction (and its gradient) as one custom op: ort_rms_spot's two
+            # deterministic passes on the device instead of ~10 eager kernels
+            from . import ops
+
+            return torch.ops.ort.rms_spot(x, y)[0]
         r2 = (x - torch.mean(x)) ** 2 + (y - torch.mean(y)) ** 2
         return torch.sqrt(torch.mean(r2))
+
+
+def _record_row(sg, name, index):
+    """surface_group.x[index, :] (surface_group.py:95-140; the reference records every
+    surface it traces, so row k is surface k) read from the surface's own record without
+    building the [S+1][n] stack; surfaces without a record fall back to the stack (NaN
+    rows, SurfaceGroup._stack)."""
+    v = getattr(sg.surfaces[index], name)
+    n = v.numel() if torch is not None and torch.is_tensor(v) else len(v)
+    if n == 0:
+        return getattr(sg, name)[index, :].flatten()
+    return v.flatten()
 
 
 rms_spot_size = RayOperand.rms_spot_size

@@ -64,7 +64,8 @@ def _lookup(h):
 class PupilPlan:
     """Everything ort::trace_pupil needs besides the parameter tensors."""
 
-    def __init__(self, dlens, seg_dev, px, py, n, seg_len, keys=(), pupil_per_ray=False):
+    def __init__(self, dlens, seg_dev, px, py, n, seg_len, keys=(), pupil_per_ray=False,
+                 newton_mode="reference"):
         self.dlens = dlens
         self.seg_dev = seg_dev
         self.px = px
@@ -73,6 +74,7 @@ class PupilPlan:
         self.seg_len = int(seg_len)
         self.keys = list(keys)
         self.pupil_per_ray = bool(pupil_per_ray)
+        self.newton_mode = newton_mode
 
 
 def _spec_pairs(spec):
@@ -133,6 +135,22 @@ def tangent_tables(table, pairs, params):
     return zp, surf, final, n_param
 
 
+def slot_need(table, zp, surf, final):
+    """ort_vjp_params.slot_need of the tangent tables: nonzero for every slot (radius,
+    conic, vertex z of each surface; each Zernike term; the final thickness) some
+    parameter depends on. Host NumPy, kept resident with the tables."""
+    S = table.n_surfaces
+    n_z = 0 if zp is None else len(zp)
+    need = np.zeros(3 * S + n_z + 1, dtype=np.int32)
+    if surf is not None:
+        need[:3 * S] = np.any(surf != 0.0, axis=0).reshape(-1)
+    if zp is not None:
+        need[3 * S:3 * S + n_z] = zp >= 0
+    if final is not None:
+        need[-1] = np.any(final != 0.0)
+    return need
+
+
 def _check_differentiable(table):
     if np.any(table.surfaces["geometry"] == _abi.GEOM_GRID_SAG):
         raise NotImplementedError("autograd through grid-sag surfaces is not implemented by "
@@ -187,8 +205,12 @@ def trace_sequential(lens: int, rays: list[torch.Tensor], w: torch.Tensor | None
     trace_rays(dl, rin, rout, rec=rec if n_rec else None, start_surface=int(start_surface),
                per_ray_w=bool(per_ray_w))
     sched = dl.last_schedule
-    sched_t = (torch.empty(0, dtype=torch.int32, device=dev) if sched is None else
-               torch.from_numpy(np.ascontiguousarray(sched.reshape(-1), dtype=np.int32)).to(dev))
+    if dl.last_schedule_dev is not None:  # device-verified: the settled device schedule
+        sched_t = dl.last_schedule_dev.clone()
+    elif sched is None:
+        sched_t = torch.empty(0, dtype=torch.int32, device=dev)
+    else:
+        sched_t = torch.from_numpy(np.ascontiguousarray(sched.reshape(-1), dtype=np.int32)).to(dev)
     return (*(getattr(rout, a) for a in _abi.RAY_FIELDS), rec, sched_t)
 
 
@@ -290,11 +312,13 @@ def _seq_vjp(dl, rays_in, w, per_ray_w, start_surface, sched, zp, st, ft, n_para
     sched_dev = sched if sched is not None and sched.numel() else None
     opt = _native.ort_options(_abi.NEWTON_SCHEDULE, int(start_surface),
                               None if sched_dev is None else sched_dev.data_ptr())
-    tabs = [None if a is None else torch.from_numpy(np.ascontiguousarray(a)).to(dl.device)
-            for a in (zp, st, ft)]
+    tabs = [None if a is None else dl.resident(("seq_tangent", i), a)
+            for i, a in enumerate((zp, st, ft))]
+    need = dl.resident("seq_need", slot_need(dl.table, zp, st, ft))
     params = _native.ort_vjp_params(int(n_param), int(mode), _ptr(tabs[0]).value,
                                     _ptr(tabs[1]).value, _ptr(tabs[2]).value,
-                                    0 if tabs[0] is None else int(tabs[0].numel()), 0, None, 0)
+                                    0 if tabs[0] is None else int(tabs[0].numel()), 0, None, 0,
+                                    need.data_ptr())
     if mode == _abi.VJP_ADJOINT:
         size = lib.ort_vjp_workspace_size(C.byref(dl.c), C.byref(batch), C.byref(params))
         _native.check(int(size) if size < 0 else 0, "ort_vjp_workspace_size")
@@ -332,10 +356,14 @@ def trace_pupil(plan: int, px: torch.Tensor, py: torch.Tensor, params: list[torc
     for a in _abi.RAY_FIELDS:
         setattr(out, a, torch.empty(p.n, dtype=torch.float64, device=dl.device))
     _trace(dl, p.seg_dev, px, py, out, p.n, p.seg_len, p.n, keys=p.keys,
-           pupil_per_ray=p.pupil_per_ray)
+           pupil_per_ray=p.pupil_per_ray, newton_mode=p.newton_mode)
     sched = dl.last_schedule
-    sched_t = (torch.empty(0, dtype=torch.int32, device=dl.device) if sched is None else
-               dl.resident("sched", sched.reshape(-1)).clone())
+    if dl.last_schedule_dev is not None:  # device-verified: the settled device schedule
+        sched_t = dl.last_schedule_dev.clone()
+    elif sched is None:
+        sched_t = torch.empty(0, dtype=torch.int32, device=dl.device)
+    else:
+        sched_t = dl.resident("sched", sched.reshape(-1)).clone()
     return (*(getattr(out, a) for a in _abi.RAY_FIELDS), sched_t)
 
 
@@ -372,6 +400,7 @@ def _pupil_backward(ctx, *grads):
     zp, st, ft, n_param = tangent_tables(dl.table, ctx.pairs, params_like)
     tables = tuple(None if a is None else dl.resident(("tangent", i), a)
                    for i, a in enumerate((zp, st, ft)))
+    tables = (*tables, dl.resident("tangent_need", slot_need(dl.table, zp, st, ft)))
     g = torch.zeros(n_param, dtype=torch.float64, device=dl.device)
     cot = [None if gr is None else gr.to(torch.float64).contiguous() for gr in grads[:8]]
     vjp(dl, p.seg_dev, p.px, p.py, p.n, p.seg_len, sched if sched.numel() else None, tables,
@@ -386,3 +415,77 @@ def _pupil_backward(ctx, *grads):
 
 
 trace_pupil.register_autograd(_pupil_backward, setup_context=_pupil_setup)
+
+
+# --------------------------------------------------------------------------------------
+# ort::rms_spot -- RayOperand.rms_spot_size's reduction (optimization/operand/ray.py:300-340)
+# --------------------------------------------------------------------------------------
+_RMS_WS: dict = {}
+
+
+def _rms_workspace(device, n):
+    lib = _native.load()
+    size = int(lib.ort_rms_spot_workspace_size(int(n)))
+    _native.check(size if size < 0 else 0, "ort_rms_spot_workspace_size")
+    return _workspace_named(_RMS_WS, device, size), size
+
+
+def _workspace_named(cache, device, nbytes):
+    ws = cache.get(device)
+    if ws is None or ws.numel() < nbytes:
+        cache.pop(device, None)
+        ws = torch.empty(max(int(nbytes), 8), dtype=torch.uint8, device=device)
+        cache[device] = ws
+    return ws
+
+
+@torch.library.custom_op("ort::rms_spot", mutates_args=(), device_types="cuda")
+def rms_spot(x: torch.Tensor, y: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """(rms, stats[5] = n, mean x, mean y, rms, max radius): sqrt(mean((x - mean x)^2 +
+    (y - mean y)^2)) as the reference's operand forms it, two deterministic passes on the
+    device (ort_rms_spot), no host synchronisation."""
+    from .raytrace import _ptr, _stream_handle
+
+    lib = _native.load()
+    x = x.detach().reshape(-1).contiguous()
+    y = y.detach().reshape(-1).contiguous()
+    n = x.numel()
+    ws, size = _rms_workspace(x.device, n)
+    stats = torch.empty(5, dtype=torch.float64, device=x.device)
+    rms = torch.empty((), dtype=torch.float64, device=x.device)
+    rc = lib.ort_rms_spot(_ptr(x), _ptr(y), n, _ptr(ws), size, _ptr(stats), _ptr(rms),
+                          _stream_handle())
+    _native.check(rc, "ort_rms_spot")
+    return rms, stats
+
+
+@rms_spot.register_fake
+def _(x, y):
+    return x.new_empty((), dtype=torch.float64), x.new_empty(5, dtype=torch.float64)
+
+
+def _rms_setup(ctx, inputs, output):
+    x, y = inputs
+    ctx.shapes = (x.shape, y.shape)
+    ctx.set_materialize_grads(False)
+    ctx.save_for_backward(x.detach(), y.detach(), output[1])
+
+
+def _rms_backward(ctx, g_rms, g_stats):
+    from .raytrace import _ptr, _stream_handle
+
+    if g_rms is None:
+        return None, None
+    x, y, stats = ctx.saved_tensors
+    xf = x.reshape(-1).contiguous()
+    yf = y.reshape(-1).contiguous()
+    g = g_rms.detach().to(torch.float64).contiguous()
+    gx = torch.empty_like(xf)
+    gy = torch.empty_like(yf)
+    rc = _native.load().ort_rms_spot_vjp(_ptr(xf), _ptr(yf), xf.numel(), _ptr(stats), _ptr(g),
+                                         _ptr(gx), _ptr(gy), _stream_handle())
+    _native.check(rc, "ort_rms_spot_vjp")
+    return gx.reshape(ctx.shapes[0]), gy.reshape(ctx.shapes[1])
+
+
+rms_spot.register_autograd(_rms_backward, setup_context=_rms_setup)

@@ -32,6 +32,12 @@ class Optic:
         self.polarization = "ignore"
         self.apodization = None
         self._lowered = None  # lowering cache (raytrace.LoweredLens), reset on edits
+        # Newton schedule verification of trace(): "reference" checks each launch's
+        # schedule on the host (one read per launch); "device" checks warm schedules on
+        # the device (ort_newton_fixup: same schedules, same results, no host round trip;
+        # a range error or an unsettled schedule is raised at the next trace call or
+        # raytrace.check_all_pending) -- for optimisation loops
+        self.newton_mode = "reference"
 
     # -- building ---------------------------------------------------------------------
     def add_surface(self, new_surface=None, surface_type="standard", comment="",

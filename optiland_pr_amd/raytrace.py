@@ -156,6 +156,11 @@ class DeviceLens:
         self.newton = table.newton_surfaces
         self.sched_cache: dict = {}
         self._resident: dict = {}
+        self.last_schedule = None      # host [n_groups][S] of the last verified launch
+        self.last_schedule_dev = None  # device int32 [n_groups * S] (device-verified launches)
+        self._dev_sched: dict = {}     # keys -> the device-resident schedule (device mode)
+        self._async_bufs: dict = {}
+        self.pending: list = []        # device-verified launches whose flags are unread
 
     def resident(self, slot, arr):
         """A read-only HBM copy of a small host array, reused while its bytes are
@@ -307,10 +312,125 @@ def lens_for(optic_or_group, wavelengths, record=False, image_record=False):
 # --------------------------------------------------------------------------------------
 # launches
 # --------------------------------------------------------------------------------------
+# device-verified Newton schedules (newton_mode="device"): re-launch rounds after the first
+# launch, each one an ort_newton_fixup (check + correct the first wrong surface of each
+# group, initialise the next round's statistics) and a launch that runs only when the
+# check corrected something. A surface needs one round when its schedule was too long
+# (the exact index is read from the statistics) and at most two when too short (grown,
+# then exact), so 2 x (Newton surfaces) + 1 rounds settle any wrong warm schedule;
+# MAX_DEVICE_ROUNDS caps the cost of the no-op rounds (two small launches each).
+MAX_DEVICE_ROUNDS = 7
+
+
+def device_rounds(dlens):
+    return max(1, min(MAX_DEVICE_ROUNDS, 2 * len(dlens.newton) + 1))
+
+
+class NewtonScheduleError(RuntimeError):
+    pass
+
+
+_PENDING_LENSES: "weakref.WeakSet" = None
+
+
+def check_pending(dlens: DeviceLens, block=False):
+    """Read the flags of earlier device-verified launches (newton_mode="device") whose
+    copies have landed (all of them with block=True). The device's settled schedules go
+    into the host cache; an unsettled schedule (NewtonScheduleError) or a range error of the
+    launch that ran last (ZernikeRangeError, ...) is raised here -- at the first trace call
+    or check_pending after the launch, not inside it."""
+    while dlens.pending:
+        p = dlens.pending[0]
+        R = p["rounds"]
+        if not block and not p["event"].query():
+            return
+        p["event"].synchronize()
+        dlens.pending.pop(0)
+        host = p["host"].numpy()
+        flags, status = host[:R + 1], host[R + 1:2 * R + 2]
+        dlens.remember(p["keys"], host[2 * R + 2:].reshape(len(p["keys"]), -1))
+        ran = [0] + [r for r in range(1, R + 1) if flags[r - 1] == 1]
+        if flags[R] != 0:
+            raise NewtonScheduleError(
+                "the Newton schedule did not settle in the device-verified rounds "
+                f"(flag {int(flags[R])}): trace again with newton_mode='reference'")
+        if p["status"]:
+            _raise_status_value(int(status[ran[-1]]))
+
+
+def check_all_pending():
+    """Blocking check_pending of every lens with device-verified launches in flight."""
+    if _PENDING_LENSES is not None:
+        for dl in list(_PENDING_LENSES):
+            check_pending(dl, block=True)
+
+
+def _run_device(dlens: DeviceLens, launch, n_rays, group_len, keys, need_status):
+    """The warm-schedule path of newton_mode="device": no host synchronisation. The first
+    launch runs the cached schedule; ort_newton_fixup checks it on the device and
+    device_rounds() conditional re-launches correct it; the flags, statuses and the settled
+    schedule are copied to pinned host memory and read by a later check_pending."""
+    lib = _native.load()
+    dev = dlens.device
+    S = dlens.table.n_surfaces
+    n_groups = len(keys)
+    R = device_rounds(dlens)
+    kk = tuple(keys)
+    sched_dev = dlens._dev_sched.get(kk)
+    if sched_dev is None:
+        sched_dev = torch.from_numpy(dlens.initial_schedule(keys).reshape(-1).copy()).to(dev)
+        dlens._dev_sched[kk] = sched_dev
+    nb = n_groups * S * _abi.NEWTON_STAT.itemsize
+    bufs = dlens._async_bufs.get((n_groups, R))
+    if bufs is None:
+        stats = torch.empty((R + 1, nb), dtype=torch.uint8, device=dev)
+        small = torch.zeros(2 * R + 2, dtype=torch.int32, device=dev)  # flags, statuses
+        bufs = (stats, small)
+        dlens._async_bufs[(n_groups, R)] = bufs
+    stats, small = bufs
+    flags, status = small[:R + 1], small[R + 1:]
+    stream = _stream_handle()
+    for r in range(R + 1):
+        if r > 0:
+            prev = None if r == 1 else flags[r - 2]
+            rc = lib.ort_newton_fixup(C.byref(dlens.c), n_groups, _ptr(stats[r - 1]), 0,
+                                      _ptr(sched_dev), _ptr(prev), _ptr(flags[r - 1]),
+                                      _ptr(stats[r]), _ptr(status[r]), stream)
+            _native.check(rc, "ort_newton_fixup")
+        opt = _native.ort_options(_abi.NEWTON_SCHEDULE, 0, sched_dev.data_ptr(), 0,
+                                  0 if r == 0 else _abi.OPT_NO_INIT,
+                                  None if r == 0 else flags[r - 1].data_ptr())
+        launch(opt, stats[r], status[r] if need_status else None)
+    rc = lib.ort_newton_fixup(C.byref(dlens.c), n_groups, _ptr(stats[R]), 0, _ptr(sched_dev),
+                              _ptr(flags[R - 1]), _ptr(flags[R]), None, None, stream)
+    _native.check(rc, "ort_newton_fixup")
+    host = torch.empty(2 * R + 2 + n_groups * S, dtype=torch.int32, pin_memory=True)
+    host[:2 * R + 2].copy_(small, non_blocking=True)
+    host[2 * R + 2:].copy_(sched_dev, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream())
+    dlens.pending.append(dict(event=ev, host=host, keys=list(keys), status=need_status,
+                              rounds=R))
+    global _PENDING_LENSES
+    if _PENDING_LENSES is None:
+        import weakref
+
+        _PENDING_LENSES = weakref.WeakSet()
+    _PENDING_LENSES.add(dlens)
+    dlens.last_schedule = None
+    dlens.last_schedule_dev = sched_dev
+
+
 def _run(dlens: DeviceLens, launch, n_rays, group_len, keys, newton_mode="reference",
          with_status=True):
-    """Run `launch(opt, stats, status)` under the Newton speculate-and-verify protocol."""
+    """Run `launch(opt, stats, status)` under the Newton speculate-and-verify protocol.
+    newton_mode "reference": verified on the host (one read per launch); "device": the
+    same rule checked on the device once the schedules are warm (no host round trip,
+    errors surface at a later check_pending); "wave": per-wavefront stop."""
     dev = dlens.device
+    if dlens.pending:
+        check_pending(dlens)
+    dlens.last_schedule_dev = None
     S = dlens.table.n_surfaces
     n_groups = max(1, -(-n_rays // group_len))
     need_status = with_status and dlens.table.has_range_check
@@ -331,6 +451,9 @@ def _run(dlens: DeviceLens, launch, n_rays, group_len, keys, newton_mode="refere
         return
     if len(keys) != n_groups:
         keys = [("group", g) for g in range(n_groups)]
+    if newton_mode == "device" and all(k in dlens.sched_cache for k in keys):
+        _run_device(dlens, launch, n_rays, group_len, keys, need_status)
+        return
     sched = dlens.initial_schedule(keys)
     # the Newton statistics and the status word share one buffer: the host reads both
     # with the one copy the schedule check needs (no second synchronising read)
@@ -354,6 +477,7 @@ def _run(dlens: DeviceLens, launch, n_rays, group_len, keys, newton_mode="refere
                 break
         if ok:
             dlens.remember(keys, sched)
+            dlens._dev_sched.pop(tuple(keys), None)  # re-seeded from this on device use
             dlens.last_schedule = sched
             if need_status:
                 _raise_status_value(int(host[nb:nb + 4].view(np.int32)[0]))
@@ -505,8 +629,10 @@ class RealRayTracer:
         self.optic = optic
 
     def trace(self, Hx, Hy, wavelength, num_rays=100, distribution="hexapolar",
-              newton_mode="reference"):
+              newton_mode=None):
         optic = self.optic
+        if newton_mode is None:  # Optic.newton_mode: "reference" (default) or "device"
+            newton_mode = getattr(optic, "newton_mode", "reference")
         _validate_normalized(Hx, Hy, "field")
         Hx = np.atleast_1d(np.asarray(Hx, dtype=np.float64))
         Hy = np.atleast_1d(np.asarray(Hy, dtype=np.float64))
@@ -523,7 +649,7 @@ class RealRayTracer:
         keys = [("trace", tuple(np.round(Hx, 15)), tuple(np.round(Hy, 15)), float(wavelength), n_p)]
         if autodiff.wants_grad(optic):
             return self._trace_grad(dlens, segs, px, py, n, n_p, wavelength, keys,
-                                    record == "all")
+                                    record == "all", newton_mode)
         out = RealRays.empty(n, wavelength, device=dev)
         rec = None
         if record == "all":
@@ -569,7 +695,8 @@ class RealRayTracer:
         self._record(dlens, out, rec, n, segs, px, py, 1, pupil_per_ray=True)
         return out
 
-    def _trace_grad(self, dlens, segs, px, py, n, n_p, wavelength, keys, record_all):
+    def _trace_grad(self, dlens, segs, px, py, n, n_p, wavelength, keys, record_all,
+                    newton_mode="reference"):
         """Optic.trace with torch-tensor Zernike coefficients that require grad (the
         reference's torch-autograd path): returned rays and the image
         record are autograd-connected to the coefficients (autodiff.py)."""
@@ -586,7 +713,7 @@ class RealRayTracer:
         # it issues after that is on the step's critical path
         w = torch.full((n,), float(wavelength), dtype=torch.float64, device=dlens.device)
         outs = autodiff.trace_pupil_grad(self.optic, dlens, seg_dev, px, py, n, n_p,
-                                         wavelength, keys)
+                                         wavelength, keys, newton_mode)
         out = RealRays.__new__(RealRays)
         for a, t in zip(_abi.RAY_FIELDS, outs, strict=True):
             setattr(out, a, t)

@@ -21,7 +21,8 @@ lens = ThreeMirrorAnastigmat()
 leaves = []
 for si in (1, 2, 3):
     g = lens.surface_group.surfaces[si].geometry
-    t = torch.tensor(np.asarray(g.coefficients), dtype=torch.float64, requires_grad=True)
+    t = torch.tensor(np.asarray(g.coefficients), dtype=torch.float64, device="cuda",
+                     requires_grad=True)
     g.coefficients = t
     leaves.append(t)
 opt = torch.optim.Adam(leaves, lr=1e-7)
