@@ -412,6 +412,12 @@ typedef struct ort_options {
    * device; lenses with Newton surfaces only). With ort_newton_fixup this re-traces on a
    * corrected schedule without a host round trip. */
   const int32_t* run_if;
+  /* nullable device double [n_surfaces][11][n_rays] (ort_vjp_tape_size bytes): a
+   * ORT_NEWTON_SCHEDULE launch of ort_trace_pupil on a lens with Newton surfaces writes
+   * the adjoint tape of its own rays as it traces (each surface's incoming global ray,
+   * its distance t and the Newton iterates before the last four updates), so the
+   * backward (ort_vjp_params.tape) runs the reverse sweep only */
+  double* tape;
 } ort_options;
 enum ort_option_flags { ORT_OPT_NO_INIT = 1 };
 
@@ -505,11 +511,19 @@ typedef struct ort_vjp_params {
    * It depends only on the tangent tables, so a caller that keeps them resident can keep
    * this too; NULL: derived on the device by one extra launch per call. */
   const int32_t* slot_need;
+  /* ADJOINT, nullable: the tape the primal ort_trace_pupil wrote (ort_options.tape, with
+   * the schedule of opt): the kernel skips its own forward re-trace and reads the final
+   * ray state from `primal` (that launch's outputs: L, M, N and i are read). */
+  const double* tape;
+  ort_rays primal;
 } ort_vjp_params;
 
-/* Workspace bytes ORT_VJP_ADJOINT needs for this lens, batch and parameter set. */
+/* Workspace bytes ORT_VJP_ADJOINT needs for this lens, batch and parameter set (without
+ * the tape when params->tape is set). */
 int64_t ort_vjp_workspace_size(const ort_lens* lens, const ort_batch* batch,
                                const ort_vjp_params* params);
+/* Bytes of the adjoint tape of one trace (ort_options.tape, ort_vjp_params.tape). */
+int64_t ort_vjp_tape_size(const ort_lens* lens, const ort_batch* batch);
 
 /* Backward of ort_trace_pupil: the vector-Jacobian product
  *   grad[p] += sum_rays sum_f cotangent.f[ray] * d out.f[ray] / d param_p

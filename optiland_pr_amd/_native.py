@@ -65,6 +65,8 @@ class ort_vjp_params(C.Structure):
         ("workspace", C.c_void_p),
         ("workspace_size", C.c_int64),
         ("slot_need", C.c_void_p),
+        ("tape", C.c_void_p),
+        ("primal", ort_rays),
     ]
 
 
@@ -91,6 +93,7 @@ class ort_options(C.Structure):
         ("conv_base", C.c_int32),
         ("flags", C.c_int32),
         ("run_if", C.c_void_p),
+        ("tape", C.c_void_p),
     ]
 
 
@@ -113,7 +116,7 @@ class ort_wavefront_ref(C.Structure):
 
 EXPORTS = ("ort_abi_version", "ort_trace_sequential", "ort_trace_pupil", "ort_trace_pupil_vjp",
            "ort_trace_sequential_vjp",
-           "ort_vjp_workspace_size", "ort_generate_pupil", "ort_newton_fixup",
+           "ort_vjp_workspace_size", "ort_vjp_tape_size", "ort_generate_pupil", "ort_newton_fixup",
            "ort_surface_sag_normal", "ort_surface_distance", "ort_generate_rays",
            "ort_material_nk", "ort_spot_workspace_size", "ort_spot_stats", "ort_spot_partials",
            "ort_rms_spot_workspace_size", "ort_rms_spot", "ort_rms_spot_vjp",
@@ -158,6 +161,8 @@ def load(path: str | None = None):
                                              P(ort_options), P(ort_vjp_params), P(ort_rays),
                                              C.c_void_p, C.c_void_p, C.c_void_p, P(ort_rays),
                                              C.c_void_p]
+    lib.ort_vjp_tape_size.restype = C.c_int64
+    lib.ort_vjp_tape_size.argtypes = [P(ort_lens), P(ort_batch)]
     lib.ort_vjp_workspace_size.restype = C.c_int64
     lib.ort_vjp_workspace_size.argtypes = [P(ort_lens), P(ort_batch), P(ort_vjp_params)]
     lib.ort_surface_sag_normal.restype = C.c_int

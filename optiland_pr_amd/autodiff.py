@@ -129,6 +129,10 @@ def vjp_mode(table):
 
 _WORKSPACE = {}
 
+# the forward of a differentiable Newton-lens trace writes the adjoint tape (F_TAPE), so
+# the backward skips its re-trace; ORT_TAPED_FORWARD=0 keeps the re-trace (A/B checks)
+TAPED_FORWARD = os.environ.get("ORT_TAPED_FORWARD", "1") != "0"
+
 # Measurement hook (bench.py config 5): when a list, every vjp() appends a pair of
 # timing events recorded on the launch stream around ort_trace_pupil_vjp
 VJP_EVENTS = None
@@ -145,7 +149,7 @@ def _workspace(device, nbytes):
 
 
 def vjp(dlens, seg_dev, px, py, n, seg_len, sched_dev, tables, n_param, cot, grad,
-        pupil_per_ray=False, mode=None):
+        pupil_per_ray=False, mode=None, tape=None, primal=None):
     """grad += J^T cot through ort_trace_pupil_vjp. tables: device tensors
     (zern_param, surf_tangent, final_tangent), each possibly None; cot: 8 tensors / None."""
     from .raytrace import _ptr, _stream_handle
@@ -168,6 +172,11 @@ def vjp(dlens, seg_dev, px, py, n, seg_len, sched_dev, tables, n_param, cot, gra
     params = _native.ort_vjp_params(int(n_param), int(mode), _ptr(zp).value, _ptr(st).value,
                                     _ptr(ft).value, 0 if zp is None else int(zp.numel()), 0,
                                     None, 0, _ptr(need).value)
+    if tape is not None and mode == _abi.VJP_ADJOINT:
+        # the forward wrote the tape (ort_options.tape): reverse sweep only, the final
+        # state read from the forward's outputs
+        params.tape = tape.data_ptr()
+        params.primal = _native.ort_rays(*(t.data_ptr() for t in primal))
     if mode == _abi.VJP_ADJOINT:
         size = lib.ort_vjp_workspace_size(C.byref(dlens.c), C.byref(batch), C.byref(params))
         _native.check(int(size) if size < 0 else 0, "ort_vjp_workspace_size")
@@ -197,6 +206,11 @@ def trace_pupil_grad(optic, dlens, seg_dev, px, py, n, seg_len, wavelength, keys
 
     params = parameters(optic)
     plan = ops.PupilPlan(dlens, seg_dev, px, py, n, seg_len, keys, newton_mode=newton_mode)
+    # adjoint-mode backward of a Newton lens: let the forward write the tape
+    plan.want_tape = (bool(params) and bool(dlens.newton) and TAPED_FORWARD
+                      and vjp_mode(dlens.table) == _abi.VJP_ADJOINT
+                      and not dlens.table.interaction_mask & ~(1 << _abi.IA_REFRACT_REFLECT)
+                      and not np.any(dlens.table.surfaces["geometry"] == _abi.GEOM_GRID_SAG))
     outs = torch.ops.ort.trace_pupil(ops.handle(plan), px, py, [t for _, _, t in params],
                                      ops.encode_spec([(k, si) for k, si, _ in params]))
     return outs[:8]

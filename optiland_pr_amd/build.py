@@ -20,7 +20,7 @@ LIB_PATH = os.path.join(LIB_DIR, "liboptiland_rt.so")
 CSRC = os.path.join(HERE, "csrc")
 # one translation unit per kernel family, compiled in parallel, linked into one .so
 SOURCES = [os.path.join(CSRC, f) for f in (
-    "ort_api.hip", "ort_k_closed.hip", "ort_k_trace.hip", "ort_k_trace_mono.hip", "ort_k_trace_rec.hip",
+    "ort_api.hip", "ort_k_closed.hip", "ort_k_trace.hip", "ort_k_trace_mono.hip", "ort_k_trace_tape.hip", "ort_k_trace_rec.hip",
     "ort_k_trace_w.hip", "ort_k_vjp.hip", "ort_k_vjp1.hip", "ort_k_vjp2.hip", "ort_k_vjp4.hip", "ort_k_geom.hip",
     "ort_k_adj.hip", "ort_k_adj2.hip", "ort_k_adj4.hip", "ort_k_adj2r.hip", "ort_k_adj4r.hip", "ort_k_pupil.hip", "ort_k_trace_ia.hip",
     "ort_k_spot.hip", "ort_k_wavefront.hip")]

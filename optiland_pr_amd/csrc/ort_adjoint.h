@@ -60,6 +60,8 @@ struct AArgs {
   const int32_t* need;      // [n_slot]: some parameter depends on this slot
   int32_t zero_partials;    // adj_run: memset the partials first (start_surface > 0: the
                             // earlier surfaces' slots are never written)
+  int32_t tape_ready;       // the primal trace wrote the tape (F_TAPE): reverse sweep only,
+  ort_rays primal;          // the final ray state read from its outputs (L, M, N, i)
   double* grad;             // [n_param], accumulated
 };
 
@@ -80,8 +82,6 @@ __device__ inline void adj_cs_op(ort::Ray& b, const ort_cs_op& op) {
   ort::apply_cs_op(b, t);
 }
 
-constexpr int kTapeRows = 11;  // incoming global x y z L M N, t, last kHist Newton iterates
-constexpr int kHist = 4;
 
 // Distance along the ray to surface s in its local frame, as the primal computes it
 // (ort_trace_pupil with ORT_NEWTON_SCHEDULE: exactly sched[group][si] Newton updates),
@@ -275,37 +275,49 @@ __global__ __launch_bounds__(kBlock) ORT_ADJ_OCC void adj_kernel(const KArgs a, 
     bk += lm * Gk;
   };
 
-  // ---- forward: the primal trace, taping (incoming ray, t, Newton iterates) per surface
+  // ---- forward: the primal trace, taping (incoming ray, t, Newton iterates) per surface;
+  // skipped when the primal launch wrote the tape itself (F_TAPE, tape_ready): the final
+  // state is then that launch's output (the same values, operation for operation)
   double gi = 0.0;  // RES: d (recorded intensities) / d i_in, contracted with rec_cot
-  for (int si = a.start_surface; si < a.n_surf; ++si) {
-    const ort_surface s = cst(a.surf)[si];
-    const ort_surface_optics o = optics_of(s, si);
-    double* tp = j.tape + (int64_t)si * kTapeRows * NR + rid;
-    if (active) {
-      tp[0] = r.x;
-      tp[NR] = r.y;
-      tp[2 * NR] = r.z;
-      tp[3 * NR] = r.L;
-      tp[4 * NR] = r.M;
-      tp[5 * NR] = r.N;
-    }
-    localize(a, s, r);
-    double hist[kHist];
-    const double t = replay_distance<KM>(a, s, si, r, group, hist);
-    if (active) {
-      tp[6 * NR] = t;
-      if (s.geometry != ORT_GEOM_PLANE && s.geometry != ORT_GEOM_STANDARD) {
+  bool replay = true;
+  if constexpr (!RES) replay = !j.tape_ready;
+  if (replay) {
+    for (int si = a.start_surface; si < a.n_surf; ++si) {
+      const ort_surface s = cst(a.surf)[si];
+      const ort_surface_optics o = optics_of(s, si);
+      double* tp = j.tape + (int64_t)si * kTapeRows * NR + rid;
+      if (active) {
+        tp[0] = r.x;
+        tp[NR] = r.y;
+        tp[2 * NR] = r.z;
+        tp[3 * NR] = r.L;
+        tp[4 * NR] = r.M;
+        tp[5 * NR] = r.N;
+      }
+      localize(a, s, r);
+      double hist[kHist];
+      const double t = replay_distance<KM>(a, s, si, r, group, hist);
+      if (active) {
+        tp[6 * NR] = t;
+        if (s.geometry != ORT_GEOM_PLANE && s.geometry != ORT_GEOM_STANDARD) {
 #pragma unroll
-        for (int h = 0; h < kHist; ++h) tp[(7 + h) * NR] = hist[h];
+          for (int h = 0; h < kHist; ++h) tp[(7 + h) * NR] = hist[h];
+        }
+      }
+      ort::finish_surface<KM>(r, s, s.radius, s.conic, cst(a.coef), cst(a.zern), kNoSeed, t,
+                              o.n_pre, o.u, o.alpha_pre);
+      globalize(a, s, r);
+      if constexpr (RES) {
+        if (j.rec_cot && (s.flags & ORT_SURF_RECORD) && active)
+          gi += j.rec_cot[((int64_t)s.rec_slot * 8 + 6) * NR + rid] * ort::intensity(r);
       }
     }
-    ort::finish_surface<KM>(r, s, s.radius, s.conic, cst(a.coef), cst(a.zern), kNoSeed, t,
-                            o.n_pre, o.u, o.alpha_pre);
-    globalize(a, s, r);
-    if constexpr (RES) {
-      if (j.rec_cot && (s.flags & ORT_SURF_RECORD) && active)
-        gi += j.rec_cot[((int64_t)s.rec_slot * 8 + 6) * NR + rid] * ort::intensity(r);
-    }
+  } else {
+    r.L = j.primal.L[r_ld];
+    r.M = j.primal.M[r_ld];
+    r.N = j.primal.N[r_ld];
+    r.i = j.primal.i[r_ld];  // the stored intensity: i exp(att), apodization included
+    r.att = 0.0;
   }
   double alpha_f = 0.0;
   if (a.final_mat >= 0) {
@@ -313,7 +325,7 @@ __global__ __launch_bounds__(kBlock) ORT_ADJ_OCC void adj_kernel(const KArgs a, 
       alpha_f = ort::absorption_alpha(ort::material_k(cst(a.mats)[a.final_mat], a.coef, wl), wl);
     else
       alpha_f = tab(a.alpha_tab, a.n_lambda, a.n_mat, lam, a.final_mat);
-    ort::propagate(r, a.final_thickness, alpha_f);
+    if (replay) ort::propagate(r, a.final_thickness, alpha_f);
   }
 
   // ---- output cotangents (intensity = i exp(att): d/d att = intensity)

@@ -70,6 +70,7 @@ int fill_args(KArgs& a, const ort_lens* lens, const ort_batch* batch, const ort_
   a.conv_base = opt->conv_base;
   a.run_if = opt->run_if;
   a.no_init = (opt->flags & ORT_OPT_NO_INIT) != 0;
+  a.tape = opt->tape;
   if (opt->conv_base < 0) return ORT_ERR_ARG;
   // geometry ids this library knows (enum ort_geometry): anything else is refused here
   // rather than traced as some other kind
@@ -168,6 +169,7 @@ int ort_trace_sequential(const ort_lens* lens, const ort_rays* rays_in, ort_rays
                          ort_newton_stat* newton_stat, int32_t* status, void* stream) {
   if (!rays_in || !rays_out || !batch) return ORT_ERR_ARG;
   if (batch->n_rays == 0) return ORT_OK;
+  if (opt && opt->tape) return ORT_ERR_ARG;  // the tape is ort_trace_pupil's
   KArgs a{};
   uint32_t feat = 0;
   int rc = fill_args(a, lens, batch, opt, rec, newton_stat, status, feat);
@@ -194,6 +196,12 @@ int ort_trace_pupil(const ort_lens* lens, const double* px, const double* py,
   a.py = py;
   a.out = *rays_out;
   feat |= F_GEN;
+  if (opt->tape) {  // the adjoint tape of a differentiable trace (Newton lenses)
+    if ((feat & F_KM) == 0 || (feat & (F_REC | F_IA | F_WRAY)) != 0 ||
+        opt->newton_mode != ORT_NEWTON_SCHEDULE || opt->start_surface != 0)
+      return ORT_ERR_ARG;
+    feat |= F_TAPE;
+  }
   hipStream_t s = (hipStream_t)stream;
   if ((rc = init_outputs(a, s))) return rc;
   return launch(a, feat, s);
@@ -215,11 +223,18 @@ static bool adj_layout(const ort_lens* lens, const ort_batch* batch,
   L.n_slot = (int32_t)(3 * S + params->n_zern + 1);
   L.n_wave = (n + kBlock - 1) / kBlock * (kBlock / 64);
   L.tape = 0;
-  L.partial = al(L.tape + S * kTapeRows * n * (int64_t)sizeof(double));
+  // a tape the primal wrote (params->tape) lives outside the workspace
+  const int64_t tape_bytes = params->tape ? 0 : S * kTapeRows * n * (int64_t)sizeof(double);
+  L.partial = al(L.tape + tape_bytes);
   L.slot_sum = al(L.partial + (int64_t)L.n_slot * L.n_wave * (int64_t)sizeof(double));
   L.need = al(L.slot_sum + (int64_t)L.n_slot * (int64_t)sizeof(double));
   L.total = al(L.need + (int64_t)L.n_slot * (int64_t)sizeof(int32_t));
   return true;
+}
+
+int64_t ort_vjp_tape_size(const ort_lens* lens, const ort_batch* batch) {
+  if (!lens || !batch || batch->n_rays < 0 || lens->n_surfaces < 0) return ORT_ERR_ARG;
+  return (int64_t)lens->n_surfaces * kTapeRows * batch->n_rays * (int64_t)sizeof(double);
 }
 
 int64_t ort_vjp_workspace_size(const ort_lens* lens, const ort_batch* batch,
@@ -285,6 +300,14 @@ static int vjp_run(const ort_lens* lens, const double* px, const double* py,
     aj.rec = rec;
     if (want_in) aj.gin = *grad_in;
     aj.tape = (double*)(w + L.tape);
+    if (params->tape) {  // the primal wrote the tape: reverse sweep only
+      if (resident || !params->primal.L || !params->primal.M || !params->primal.N ||
+          !params->primal.i)
+        return ORT_ERR_ARG;
+      aj.tape = (double*)params->tape;
+      aj.tape_ready = 1;
+      aj.primal = params->primal;
+    }
     aj.partial = (double*)(w + L.partial);
     aj.slot_sum = (double*)(w + L.slot_sum);
     aj.need = params->slot_need;  // NULL: adj_run derives it into the workspace

@@ -12,6 +12,7 @@ KernelFn pick() {
 KernelFn select_trace_rec(uint32_t feat);  // ort_k_trace_rec.hip
 
 KernelFn select_trace(uint32_t feat) {
+  if (feat & F_TAPE) return select_trace_tape(feat);
   if (feat & F_WRAY) return select_trace_w(feat);
   if (feat & F_MONO) {
     // scalar optics loads: instantiated for generated rays without records (the pupil

@@ -69,7 +69,13 @@ enum : uint32_t {
   F_WRAY = 1u << 7,  // per-ray wavelengths: n, k from lens.materials (ort_batch.w)
   F_IA = 1u << 8,    // thin-lens / phase / grating interactions (ort_interaction)
   F_AXIAL = 1u << 9, // ORT_LENS_AXIAL: every frame a +z translation (closed-form kernels)
+  F_TAPE = 1u << 10, // write the adjoint tape as the trace runs (ort_options.tape)
 };
+
+// Adjoint tape (ort_adjoint.h): per traced surface, rows of n_rays doubles -- the incoming
+// global x y z L M N, the distance t, the Newton iterates before the last kHist updates
+constexpr int kTapeRows = 11;
+constexpr int kHist = 4;
 
 struct KArgs {
   // lens
@@ -116,9 +122,10 @@ struct KArgs {
   // trace_kernel: blocks walk the pupil chunk by chunk over all (field, lambda) segments
   // (pair_major_ray); set by the host only when it is a bijection (see launch)
   int32_t block_remap;
-  // nullable: the launch is a no-op unless *run_if != 0 (ort_options.run_if)
+  // nullable: the launch is a no-op unless *run_if == 1 (ort_options.run_if)
   const int32_t* run_if;
   int32_t no_init;  // host side only: ORT_OPT_NO_INIT (skip init_outputs)
+  double* tape;     // F_TAPE: [n_surf][kTapeRows][n_rays] (ort_options.tape)
 };
 
 // Ray of this thread when every (field, lambda) segment traces the SAME pupil samples
@@ -332,12 +339,19 @@ __device__ inline double grid_distance(const KArgs& a, const ort_surface& s, int
 // for operation, the propagated point Surface.trace takes the normal at
 // (standard_surface.py:215-225, homogeneous.py:45-47), so that normal is the
 // interaction's normal: one sag + normal evaluation per Newton surface saved.
+// F_TAPE: hist[m] = the iterate before the m-th last update (t_{U-1-m}), 0 beyond U, as
+// the adjoint's replay_distance tapes it.
 template <uint32_t FEAT>
 __device__ inline double newton_distance(const KArgs& a, const ort_surface& s, int si,
                                          const ort::Ray& r, bool active, int64_t group,
                                          bool group_uniform, int& range_bits, bool& hn,
-                                         double& nnx, double& nny, double& nnz) {
+                                         double& nnx, double& nny, double& nnz,
+                                         double (&hist)[kHist]) {
   hn = false;
+  if constexpr ((FEAT & F_TAPE) != 0) {
+#pragma unroll
+    for (int h = 0; h < kHist; ++h) hist[h] = 0.0;
+  }
   if constexpr ((FEAT & ort::KM_FREE) != 0) {
     if (s.geometry == ORT_GEOM_GRID_SAG)
       return grid_distance<FEAT>(a, s, si, r, active, group, group_uniform);
@@ -390,6 +404,11 @@ __device__ inline double newton_distance(const KArgs& a, const ort_surface& s, i
       if (conv) mask.set(j, a.conv_base);
       if (!conv) last_bad = j;
       if (upd) {
+        if constexpr ((FEAT & F_TAPE) != 0) {
+#pragma unroll
+          for (int h = kHist - 1; h > 0; --h) hist[h] = hist[h - 1];
+          hist[0] = t;
+        }
         t = ort::newton_step(r, t, f, nx, ny, nz);
       } else {
         nnx = nx;
@@ -494,10 +513,23 @@ __global__ __launch_bounds__(kBlock) ORT_TRACE_OCC void trace_kernel(const KArgs
   for (int si = a.start_surface; si < a.n_surf; ++si) {
     const ort_surface s = cst(a.surf)[si];
     const ort_surface_optics o = surface_optics<FEAT>(a, s, lam, si, wl);
+    double* tp = nullptr;  // F_TAPE: this surface's tape rows of this ray
+    if constexpr ((FEAT & F_TAPE) != 0) {
+      tp = a.tape + (int64_t)si * kTapeRows * a.n_rays + rid;
+      if (active) {
+        tp[0] = r.x;
+        tp[a.n_rays] = r.y;
+        tp[2 * a.n_rays] = r.z;
+        tp[3 * a.n_rays] = r.L;
+        tp[4 * a.n_rays] = r.M;
+        tp[5 * a.n_rays] = r.N;
+      }
+    }
     localize(a, s, r);
     double t;
     bool hn = false;  // (hnx, hny, hnz): the Newton geometry's normal at t
     double hnx = 0.0, hny = 0.0, hnz = 0.0;
+    double hist[kHist];
     if (!known_geometry(s.geometry)) range_bits |= ORT_STATUS_BAD_GEOMETRY;
     if (s.geometry == ORT_GEOM_PLANE) {
       t = ort::distance_plane(r);
@@ -506,10 +538,19 @@ __global__ __launch_bounds__(kBlock) ORT_TRACE_OCC void trace_kernel(const KArgs
     } else {
       if constexpr ((FEAT & F_KM) != 0) {
         t = newton_distance<FEAT>(a, s, si, r, active, group, group_uniform, range_bits, hn,
-                                  hnx, hny, hnz);
+                                  hnx, hny, hnz, hist);
+        if constexpr ((FEAT & F_TAPE) != 0) {
+          if (active) {
+#pragma unroll
+            for (int h = 0; h < kHist; ++h) tp[(7 + h) * a.n_rays] = hist[h];
+          }
+        }
       } else {
         t = __builtin_nan("");  // unreachable: the host sets geometry_mask
       }
+    }
+    if constexpr ((FEAT & F_TAPE) != 0) {
+      if (active) tp[6 * a.n_rays] = t;
     }
     const double n_pre = o.n_pre, u = o.u, alpha = o.alpha_pre;
     if constexpr ((FEAT & F_IA) != 0) {
@@ -1054,9 +1095,9 @@ __global__ __launch_bounds__(kBlock) void geom_kernel(const KArgs a, const GArgs
     } else {
       if constexpr (KM != 0) {
         bool hn;
-        double hnx, hny, hnz;
+        double hnx, hny, hnz, hist[kHist];
         t = newton_distance<KM>(a, s, g.surface, r, active, 0, true, range_bits, hn, hnx, hny,
-                                hnz);
+                                hnz, hist);
       } else {
         t = __builtin_nan("");
       }
@@ -1080,6 +1121,8 @@ KernelFn select_trace_w(uint32_t feat);    // Newton lenses, per-ray wavelengths
 KernelFn select_trace_mono(uint32_t feat); // Newton lenses, F_GEN, wave-uniform wavelength row
                                            // (ort_k_trace_mono.hip)
 KernelFn select_trace_ia(uint32_t feat);   // thin-lens / phase / grating lenses (ort_k_trace_ia.hip)
+KernelFn select_trace_tape(uint32_t feat); // Newton lenses, F_GEN, writing the adjoint tape
+                                           // (ort_k_trace_tape.hip)
 // n(w), k(w) of one material (ort_material_nk)                            (ort_k_closed.hip)
 void launch_material_nk(const ort_material* mats, const double* coef, int32_t mat,
                         const double* w, int64_t n, double* n_out, double* k_out,

@@ -75,6 +75,8 @@ class PupilPlan:
         self.keys = list(keys)
         self.pupil_per_ray = bool(pupil_per_ray)
         self.newton_mode = newton_mode
+        self.want_tape = False  # set by the caller when the backward is an adjoint sweep
+        self.tape = None
 
 
 def _spec_pairs(spec):
@@ -149,6 +151,15 @@ def slot_need(table, zp, surf, final):
     if final is not None:
         need[-1] = np.any(final != 0.0)
     return need
+
+
+def tape_doubles(dl, n):
+    """Doubles of the adjoint tape of an n-ray trace of this lens (ort_vjp_tape_size)."""
+    lib = _native.load()
+    batch = _native.ort_batch(n, max(n, 1), max(n, 1), 0, 0, None)
+    size = int(lib.ort_vjp_tape_size(C.byref(dl.c), C.byref(batch)))
+    _native.check(size if size < 0 else 0, "ort_vjp_tape_size")
+    return size // 8
 
 
 def _check_differentiable(table):
@@ -355,8 +366,11 @@ def trace_pupil(plan: int, px: torch.Tensor, py: torch.Tensor, params: list[torc
     out = RealRays.__new__(RealRays)
     for a in _abi.RAY_FIELDS:
         setattr(out, a, torch.empty(p.n, dtype=torch.float64, device=dl.device))
+    p.tape = None
+    if p.want_tape:  # the forward writes the adjoint tape: the backward is the reverse sweep
+        p.tape = torch.empty(tape_doubles(dl, p.n), dtype=torch.float64, device=dl.device)
     _trace(dl, p.seg_dev, px, py, out, p.n, p.seg_len, p.n, keys=p.keys,
-           pupil_per_ray=p.pupil_per_ray, newton_mode=p.newton_mode)
+           pupil_per_ray=p.pupil_per_ray, newton_mode=p.newton_mode, tape=p.tape)
     sched = dl.last_schedule
     if dl.last_schedule_dev is not None:  # device-verified: the settled device schedule
         sched_t = dl.last_schedule_dev.clone()
@@ -383,13 +397,13 @@ def _pupil_setup(ctx, inputs, output):
     ctx.n_spec = len(spec)
     ctx.shapes = [(p.shape, p.dtype, p.device) for p in params]
     ctx.set_materialize_grads(False)
-    ctx.save_for_backward(output[8])
+    ctx.save_for_backward(output[8], *output[:8])
 
 
 def _pupil_backward(ctx, *grads):
     from .autodiff import vjp
 
-    (sched,) = ctx.saved_tensors
+    sched, *primal = ctx.saved_tensors
     p = ctx.plan
     dl = p.dlens
     none_spec = [] if ctx.n_spec == 0 else None  # see _seq_backward
@@ -404,7 +418,9 @@ def _pupil_backward(ctx, *grads):
     g = torch.zeros(n_param, dtype=torch.float64, device=dl.device)
     cot = [None if gr is None else gr.to(torch.float64).contiguous() for gr in grads[:8]]
     vjp(dl, p.seg_dev, p.px, p.py, p.n, p.seg_len, sched if sched.numel() else None, tables,
-        n_param, cot, g, pupil_per_ray=p.pupil_per_ray)
+        n_param, cot, g, pupil_per_ray=p.pupil_per_ray,
+        tape=p.tape, primal=primal if p.tape is not None else None)
+    p.tape = None  # one backward per forward: release the tape
     res = []
     off = 0
     for shape, dtype, pdev in ctx.shapes:

@@ -509,9 +509,11 @@ def upload_segments(segments: np.ndarray, device):
 
 def trace_pupil(dlens: DeviceLens, segments, px, py, out: RealRays, n_rays,
                 seg_len, group_len, pupil_per_ray=False, keys=(), rec=None,
-                newton_mode="reference", start_surface=0):
+                newton_mode="reference", start_surface=0, tape=None):
     """Generate + trace in one launch (ort_trace_pupil). `segments` is a host SEGMENT array
-    or the device tensor returned by upload_segments (no per-call copy)."""
+    or the device tensor returned by upload_segments (no per-call copy). tape: a device
+    buffer of ort_vjp_tape_size bytes the launch writes the adjoint tape into (Newton
+    lenses; the backward then runs the reverse sweep only)."""
     lib = _native.load()
     seg_dev = (segments if torch.is_tensor(segments) else
                dlens.resident("segments", np.asarray(segments, dtype=_abi.SEGMENT)))
@@ -523,6 +525,7 @@ def trace_pupil(dlens: DeviceLens, segments, px, py, out: RealRays, n_rays,
 
     def launch(opt, stats, status):
         opt.start_surface = start_surface
+        opt.tape = _addr(tape)
         rc = lib.ort_trace_pupil(C.byref(dlens.c), _ptr(px), _ptr(py), C.byref(out_c),
                                  C.byref(batch), C.byref(opt), _ptr(rec), _ptr(stats),
                                  _ptr(status), _stream_handle())
