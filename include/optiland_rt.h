@@ -425,8 +425,10 @@ enum ort_option_flags { ORT_OPT_NO_INIT = 1 };
 enum ort_status {
   ORT_STATUS_ZERNIKE_RANGE = 1u << 0,   /* zernike.py:234-246 ValueError            */
   ORT_STATUS_CHEBYSHEV_RANGE = 1u << 1, /* chebyshev.py:203-215 ValueError          */
-  ORT_STATUS_BAD_GEOMETRY = 1u << 2     /* a surface with an unknown geometry id: its
+  ORT_STATUS_BAD_GEOMETRY = 1u << 2,    /* a surface with an unknown geometry id: its
                                            rays are NaN (never a silent substitute)  */
+  ORT_STATUS_BAD_APODIZATION = 1u << 3  /* ort_batch.apod holds an unknown kind: the
+                                           generated intensities are NaN             */
 };
 
 /* Pupil distribution generated on the device (distribution.py:72-408), see

@@ -94,6 +94,7 @@ NEWTON_WAVE = 1
 STATUS_ZERNIKE_RANGE = 1 << 0
 STATUS_CHEBYSHEV_RANGE = 1 << 1
 STATUS_BAD_GEOMETRY = 1 << 2
+STATUS_BAD_APODIZATION = 1 << 3
 
 CS_OP = np.dtype(
     [("kind", "<i4"), ("reserved", "<i4"), ("p", "<f8", (3,))], align=True

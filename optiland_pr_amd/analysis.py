@@ -186,6 +186,13 @@ class SpotDiagram:
             self._data = self._generate_data()
         return self._data
 
+    @data.setter
+    def data(self, value):
+        """The reference's SpotDiagram.data is a plain attribute its helpers may reassign
+        (e.g. re-centred spots). Assigned data is kept as given; the device statistics
+        (centroid / rms / geometric radius) keep describing the traced rays."""
+        self._data = value
+
     def _generate_data(self):
         out, n_p = self.rays, self._n_p
         data = []

@@ -459,10 +459,15 @@ __device__ inline void interact(const KArgs& a, const ort_surface& s, ort::Ray& 
 // forward runs 9% faster on the MI355X (334 -> 305 us per 1M-ray launch, rocprofv3; 5
 // waves: 313 us). The even-asphere kernels already fit 6 waves; the rest keep the
 // compiler's choice. ORT_TRACE_WAVES overrides the target for A/B builds.
+// The taping forward (F_TAPE: the hist registers and 11 rows of stores per surface) runs
+// best unspilled at 4 waves: TMA 1M rays, taped trace 374 / 328 / 300 us at 6 / 5 / 4
+// waves per SIMD (rocprofv3 A/B).
 template <uint32_t FEAT>
 struct TraceWaves {
   static constexpr int value =
-      ((FEAT & ort::KM_ZERN) != 0 && (FEAT & (ort::KM_FREE | F_IA)) == 0) ? 6 : 1;
+      ((FEAT & ort::KM_ZERN) != 0 && (FEAT & (ort::KM_FREE | F_IA)) == 0)
+          ? ((FEAT & F_TAPE) != 0 ? 4 : 6)
+          : 1;
 };
 #ifdef ORT_TRACE_WAVES
 #define ORT_TRACE_OCC __attribute__((amdgpu_waves_per_eu(ORT_TRACE_WAVES)))
@@ -509,6 +514,10 @@ __global__ __launch_bounds__(kBlock) ORT_TRACE_OCC void trace_kernel(const KArgs
   }
   int range_bits = 0;
   bool unnorm = false;  // F_IA: rays.is_normalized == False after a thin lens
+  if constexpr ((FEAT & F_GEN) != 0) {
+    if (a.apod && (uint32_t)cst(a.apod)->kind > (uint32_t)ORT_APOD_TUKEY)
+      range_bits |= ORT_STATUS_BAD_APODIZATION;
+  }
 
   for (int si = a.start_surface; si < a.n_surf; ++si) {
     const ort_surface s = cst(a.surf)[si];
@@ -807,6 +816,11 @@ __global__ __launch_bounds__(kClosedBlock) __attribute__((amdgpu_waves_per_eu(8)
 #endif
   if (a.final_mat >= 0) ort::propagate(r, a.final_thickness, final_alpha<FEAT>(a, lam, wl));
   if (geom_bad && a.status && threadIdx.x == 0) atomicOr(a.status, (int)ORT_STATUS_BAD_GEOMETRY);
+  if constexpr ((FEAT & F_GEN) != 0) {
+    if (a.apod && a.status && threadIdx.x == 0 &&
+        (uint32_t)cst(a.apod)->kind > (uint32_t)ORT_APOD_TUKEY)
+      atomicOr(a.status, (int)ORT_STATUS_BAD_APODIZATION);
+  }
   if (!active) return;
   a.out.x[rid] = r.x;
   a.out.y[rid] = r.y;

@@ -440,6 +440,13 @@ def segment_params(optic, Hx, Hy, lambda_idx, EPL=None, EPD=None):
         raise ValueError(f"field type {optic.field_type!r} not supported")
     if telecentric:  # ray_generator.py:56-73: aim at z = sqrt(1 - NA^2) / NA + z0
         _telecentric_checks(optic)
+        if int(seg["mode"]) != _abi.GEN_FINITE:
+            # ORT_GEN_TELECENTRIC takes the origin as (x_off, y_off, z0), the finite-object
+            # origin; an infinite object's origin also depends on the pupil point (the
+            # Px EPD / 2 vx term), which this mode does not carry -- refuse, never trace
+            # it from the wrong origins
+            raise ValueError("object-space telecentric ray generation needs a finite "
+                             "object (object_height / paraxial_image_height field)")
         sin = optic.aperture.value
         seg["mode"] = _abi.GEN_TELECENTRIC
         seg["epd"] = 0.0

@@ -493,6 +493,8 @@ def _raise_status(status):
 
 
 def _raise_status_value(v):
+    if v & _abi.STATUS_BAD_APODIZATION:
+        raise ValueError("the apodization record holds a kind the trace core does not know")
     if v & _abi.STATUS_BAD_GEOMETRY:
         raise ValueError("the lens table holds a geometry id the trace core does not know "
                          "(library / host ABI mismatch?)")
