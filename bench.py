@@ -51,14 +51,19 @@ SPEC_HBM_TBPS = 8.0        # MI355X_MICROARCH.md: 8.0 TB/s spec HBM3E
 SPEC_FP64_VEC_TFLOPS = 78.6  # AMD MI355X FP64 vector spec (not in the local guide)
 
 
-def _flops_per_ray(table):
+def _flops_per_ray(table, sched=None):
     """Algorithmic fp64 operations per ray (+,-,*,/,sqrt each 1) counted from
     optiland_pr_amd/csrc/ort_core.h for the lowered surfaces (DESIGN.md 'Roofline').
-    Closed-form surfaces only (the config-2 kernel)."""
+    Closed-form surfaces, and even aspheres given the Newton schedule `sched` [S] (updates
+    per surface; every ray makes them, plus the stop-test evaluation whose normal the
+    interaction takes): the conic start (45), per evaluation the point P(t) (6), the sag +
+    normal with nc coefficients (23 + 12 nc: even_asphere.py:82-129 as written in
+    sagnorm_even) and f = sag - z (1), per update the step t - f / f' (8). None when a
+    surface kind is not counted."""
     from optiland_pr_amd import _abi
 
     f = 20  # ray generation (ray_generator.py:71-89)
-    for s in table.surfaces:
+    for si, s in enumerate(table.surfaces):
         g = int(s["geometry"])
         f += 3 * int(s["n_cs_loc"]) + 3 * int(s["n_cs_glob"])  # translate ops (no tilts here)
         f += 6 + 2 + 33  # propagate, opd, refract
@@ -66,6 +71,11 @@ def _flops_per_ray(table):
             f += 45 + 20  # conic distance + normal
         elif g == _abi.GEOM_PLANE:
             f += 1
+        elif g == _abi.GEOM_EVEN_ASPHERE and sched is not None:
+            U = int(sched[si])
+            f += 45 + (U + 1) * (30 + 12 * int(s["n_coef"])) + 8 * U
+        else:
+            return None
         if table.alpha_tab[0, int(s["mat_pre"])] > 0:
             f += 3
     return f
@@ -108,9 +118,8 @@ def config1(args, dev, rank, world, torch):
 
     spot = SpotStatistics(len(fields), 1, n_p, 0, img, dev)
 
-    def once():
-        trace_pupil(dl, seg_dev, px, py, out, n, n_p, n_p)
-        return spot.run(out)
+    def once():  # trace + statistics pass 1 in one kernel, then the 2 other passes
+        return spot.trace(dl, seg_dev, px, py, out)
 
     once()  # closed-form lens: one launch, no host sync, no allocation -> capturable
     torch.cuda.synchronize()
@@ -128,11 +137,13 @@ def config1(args, dev, rank, world, torch):
         unit="intersections/s", units=world * n * S, step=step, scaling="weak",
         config={"workload": "CookeTriplet (samples/objectives.py:46-72), fields Hy 0 / 0.7 / 1 "
                             "(0 / 14 / 20 deg), lambda 0.55 um, uniform 128 (12,644 rays per "
-                            "field): fused trace of the 3 pairs + ort_spot_stats, one HIP "
-                            "graph replay per step",
+                            "field): fused trace of the 3 pairs with the statistics' first "
+                            "pass in its epilogue + the second pass whose last block per pair "
+                            "forms the totals (ort_trace_spot), one HIP graph replay per step",
                 "rays_per_gpu": n, "surfaces": S,
                 "parallelism": f"dp{world} (replicas, no collective)"},
-        kernel="trace_closed_kernel<F_GEN> + 3 spot-statistics kernels (graph)", launches=4,
+        kernel="trace_closed_kernel<F_GEN|F_SPOT> + spot_dev_kernel (graph)",
+        launches=2,
         bytes_per_launch=None, flops_per_ray=None, pmc_file=None, rays=n, state=state,
         spot=True, data="synthetic (the reference's uniform 128 pupil grid)")
 
@@ -192,6 +203,14 @@ def config3(args, dev, rank, world, torch):
     def step():
         trace_pupil(dl, seg_dev, px, py, out, n, n_p, n_p, keys=keys, newton_mode=args.newton_mode)
 
+    # the verified Newton schedule fixes the work per ray: count the algorithmic flops with
+    # the mean updates per surface over the (field, lambda) groups
+    flops = None
+    if args.newton_mode == "reference":
+        step()
+        sched = np.mean(np.stack([dl.sched_cache[k] for k in keys]), axis=0)
+        flops = _flops_per_ray(dl.table, np.rint(sched))
+
     return Workload(
         metric="ray-surface intersections/sec, RT-asph even-asphere (Newton sag), 5 fields x "
                "3 lambda x 4M pupil rays",
@@ -202,7 +221,7 @@ def config3(args, dev, rank, world, torch):
                 "newton_mode": args.newton_mode,
                 "parallelism": f"dp{world} (ray shards, no collective)"},
         kernel="trace_kernel<F_GEN|KM_EVEN> (ort_trace_pupil)", launches=1,
-        bytes_per_launch=n_p * 16 + n * 64, flops_per_ray=None, pmc_file="hbm_traffic_c3.json",
+        bytes_per_launch=n_p * 16 + n * 64, flops_per_ray=flops, pmc_file="hbm_traffic_c3.json",
         rays=n)
 
 

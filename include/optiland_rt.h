@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define ORT_ABI_VERSION 12
+#define ORT_ABI_VERSION 13
 #define ORT_MAX_SURFACES 64
 
 /* ---- geometry kinds ----------------------------------- */
@@ -636,16 +636,31 @@ typedef struct ort_spot_layout {
 int64_t ort_spot_workspace_size(const ort_spot_layout* layout);
 
 /* rays: device x, y, z, i of n_fields * n_wl * n_pupil rays (other fields unused; z
- * only with local_ops); out: device [n_fields * n_wl][5]. Three launches on `stream`,
- * no synchronisation, no allocation (graph-capturable). */
+ * only with local_ops); out: device [n_fields * n_wl][5]. Two launches on `stream` (the
+ * second pass's last block per pair forms the totals), no synchronisation, no allocation
+ * (graph-capturable); the workspace needs no initialisation. */
 int ort_spot_stats(const ort_rays* rays, const ort_spot_layout* layout, void* workspace,
+                   int64_t workspace_size, double* out, void* stream);
+
+/* SpotDiagram's trace + statistics (spot_diagram.py:381-438 then :317-357) for a lens
+ * without Newton geometries: ort_trace_pupil of the n_fields * n_wl pairs (segments in
+ * pair order, batch->seg_len == layout->n_pupil, shared pupil) into rays_out, then
+ * out[pair][5] as ort_spot_stats computes it. When each pair's chunks hold one ray per
+ * thread (n_pupil <= 65,536) the closed-form kernel writes the statistics' first pass from
+ * its epilogue (2 launches: the trace, then the second pass + totals); otherwise 3. The numbers are
+ * bit-identical to ort_trace_pupil followed by ort_spot_stats either way. Replaces
+ * SpotDiagram._generate_field_data's trace loop + the statistics over its data
+ * (analysis/spot_diagram.py:317-357, 381-438). Newton lenses: ORT_ERR_ARG. */
+int ort_trace_spot(const ort_lens* lens, const double* px, const double* py,
+                   ort_rays* rays_out, const ort_batch* batch, const ort_options* opt,
+                   int32_t* status, const ort_spot_layout* layout, void* workspace,
                    int64_t workspace_size, double* out, void* stream);
 
 /* RayOperand.rms_spot_size's reduction (optimization/operand/ray.py:300-340):
  * rms = sqrt(mean((x - mean x)^2 + (y - mean y)^2)) over all n points (no intensity mask),
  * two passes in a fixed order (the spot-statistics kernels with one pair). stats (device
  * double[5]) = { n, mean x, mean y, rms, max radius }; rms (device double, nullable) gets
- * the rms again as its own scalar (the autograd op's output). Three launches.
+ * the rms again as its own scalar (the autograd op's output). Two launches.
  * ort_rms_spot_vjp: gx[i] = g (x_i - mean x) / (n rms), gy likewise, g = *grad_out (a
  * device scalar, read on the device: no host synchronisation). One launch. */
 int64_t ort_rms_spot_workspace_size(int64_t n);

@@ -118,7 +118,7 @@ EXPORTS = ("ort_abi_version", "ort_trace_sequential", "ort_trace_pupil", "ort_tr
            "ort_trace_sequential_vjp",
            "ort_vjp_workspace_size", "ort_vjp_tape_size", "ort_generate_pupil", "ort_newton_fixup",
            "ort_surface_sag_normal", "ort_surface_distance", "ort_generate_rays",
-           "ort_material_nk", "ort_spot_workspace_size", "ort_spot_stats", "ort_spot_partials",
+           "ort_material_nk", "ort_spot_workspace_size", "ort_spot_stats", "ort_trace_spot", "ort_spot_partials",
            "ort_rms_spot_workspace_size", "ort_rms_spot", "ort_rms_spot_vjp",
            "ort_wavefront_workspace_size", "ort_wavefront_opd")
 
@@ -190,6 +190,11 @@ def load(path: str | None = None):
     lib.ort_spot_stats.restype = C.c_int
     lib.ort_spot_stats.argtypes = [P(ort_rays), P(ort_spot_layout), C.c_void_p, C.c_int64,
                                    C.c_void_p, C.c_void_p]
+    lib.ort_trace_spot.restype = C.c_int
+    lib.ort_trace_spot.argtypes = [P(ort_lens), C.c_void_p, C.c_void_p, P(ort_rays),
+                                   P(ort_batch), P(ort_options), C.c_void_p,
+                                   P(ort_spot_layout), C.c_void_p, C.c_int64, C.c_void_p,
+                                   C.c_void_p]
     lib.ort_spot_partials.restype = C.c_int
     lib.ort_spot_partials.argtypes = [P(ort_rays), P(ort_spot_layout), C.c_int32, C.c_void_p,
                                       C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p]

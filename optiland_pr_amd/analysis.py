@@ -85,7 +85,7 @@ class SpotStatistics:
     into `surface`'s frame when given (coordinates="local").
 
     The constructor uploads the image frame's ops and allocates the workspace and the
-    output; run() only launches (three small kernels, no host sync, no allocation), so
+    output; run() only launches (two small kernels, no host sync, no allocation), so
     it can be captured in a HIP graph."""
 
     def __init__(self, n_fields, n_wl, n_pupil, ref_wl, surface=None, device=None):
@@ -123,6 +123,15 @@ class SpotStatistics:
                                       C.c_void_p(self.out.data_ptr()), _stream_handle())
         _native.check(rc, "ort_spot_stats")
         return self.out
+
+    def trace(self, dlens, segments, px, py, rays):
+        """Trace the pairs of a lens without Newton geometries into `rays` and run the
+        statistics, the first pass fused into the trace kernel (ort_trace_spot): the same
+        numbers as trace_pupil + run(rays), one launch fewer. Capturable like run()."""
+        from .raytrace import trace_spot
+
+        n_p = int(self._lay.n_pupil)
+        return trace_spot(dlens, segments, px, py, rays, len(rays), n_p, self)
 
 
 def spot_statistics(rays, n_fields, n_wl, n_pupil, ref_wl, surface=None):
@@ -170,13 +179,17 @@ class SpotDiagram:
         out = RealRays.empty(n, 0.0, device=dev)
         keys = [("trace", (float(hx),), (float(hy),), float(w), n_p)
                 for hx, hy in self.fields for w in self.wavelengths]
-        trace_pupil(dl, segs, px, py, out, n, n_p, n_p, keys=keys, newton_mode=self.newton_mode)
         self.rays = out
         self._n_p = n_p
-        self._stats = spot_statistics(
-            out, len(self.fields), len(self.wavelengths), n_p,
-            self._analysis_ref_wavelength_index,
-            optic.image_surface if self.coordinates == "local" else None)
+        spot = SpotStatistics(len(self.fields), len(self.wavelengths), n_p,
+                              self._analysis_ref_wavelength_index,
+                              optic.image_surface if self.coordinates == "local" else None, dev)
+        if dl.newton:
+            trace_pupil(dl, segs, px, py, out, n, n_p, n_p, keys=keys,
+                        newton_mode=self.newton_mode)
+            self._stats = spot.run(out)
+        else:  # statistics pass 1 in the trace kernel's epilogue (ort_trace_spot)
+            self._stats = spot.trace(dl, segs, px, py, out)
 
     @property
     def data(self):

@@ -356,6 +356,9 @@ __global__ __launch_bounds__(kBlock) ORT_ADJ_OCC void adj_kernel(const KArgs a, 
   }
 
   // ---- reverse over the surfaces
+  // LDS slots of this lane's adjoint state, parked across the Newton replay's dual-number
+  // evaluation (see there): 10 x 256 doubles = 20 KB per block
+  __shared__ double park[10][kBlock];
   for (int si = a.n_surf - 1; si >= a.start_surface; --si) {
     const ort_surface s = cst(a.surf)[si];
     const ort_surface_optics o = optics_of(s, si);
@@ -470,7 +473,35 @@ __global__ __launch_bounds__(kBlock) ORT_ADJ_OCC void adj_kernel(const KArgs a, 
         const double tk = tp[(7 + m) * NR];
         const double xk = q.x + tk * q.L, yk = q.y + tk * q.M, zk = q.z + tk * q.N;
         D kx, ky, kz;
+        // The dual-number sag / normal alone needs ~124 VGPRs (the plain one 42), so with the
+        // adjoint state live across it the kernel spills at its 128-VGPR cap. The state is
+        // parked in LDS instead (the empty asm is a compiler memory barrier: the values are
+        // reloaded, their registers are free during the evaluation): TMA adjoint 909 ->
+        // 851 us per 1M-ray launch (rocprofv3 A/B); parking more values, or at the hit-point
+        // and coefficient evaluations too, measured no better.
+        park[0][threadIdx.x] = b.x;
+        park[1][threadIdx.x] = b.y;
+        park[2][threadIdx.x] = b.z;
+        park[3][threadIdx.x] = b.L;
+        park[4][threadIdx.x] = b.M;
+        park[5][threadIdx.x] = b.N;
+        park[6][threadIdx.x] = bopd;
+        park[7][threadIdx.x] = batt;
+        park[8][threadIdx.x] = tb;
+        park[9][threadIdx.x] = bCZ;
+        asm volatile("" ::: "memory");
         const D sk = sagnorm(s, xk, yk, kx, ky, kz);
+        asm volatile("" ::: "memory");
+        b.x = park[0][threadIdx.x];
+        b.y = park[1][threadIdx.x];
+        b.z = park[2][threadIdx.x];
+        b.L = park[3][threadIdx.x];
+        b.M = park[4][threadIdx.x];
+        b.N = park[5][threadIdx.x];
+        bopd = park[6][threadIdx.x];
+        batt = park[7][threadIdx.x];
+        tb = park[8][threadIdx.x];
+        bCZ = park[9][threadIdx.x];
         const double f = sk.v - zk;
         const bool zg = fabs(kz.v) > 1e-14;
         const double nzs = zg ? kz.v : 1e-14;

@@ -118,7 +118,9 @@ int launch(const KArgs& a_in, uint32_t feat, hipStream_t stream) {
                                    : select_trace(feat & ~F_AXIAL);
   if (!fn) return ORT_ERR_ARG;
   const int bs = closed ? closed_block() : kBlock;
-  const int64_t blocks = (a_in.n_rays + bs - 1) / bs;
+  // F_SPOT: one block per (pair, chunk) of seg_len rays
+  const int64_t blocks = (feat & F_SPOT) != 0 ? (int64_t)a_in.n_seg * a_in.spot_chunks
+                                              : (a_in.n_rays + bs - 1) / bs;
   if (blocks > 0x7fffffff) return ORT_ERR_ARG;
   KArgs a = a_in;
   // Newton kernels on generated rays whose segments share one pupil: chunk-major block
@@ -185,6 +187,19 @@ int ort_trace_pupil(const ort_lens* lens, const double* px, const double* py,
                     ort_rays* rays_out, const ort_batch* batch, const ort_options* opt,
                     double* rec, ort_newton_stat* newton_stat, int32_t* status,
                     void* stream) {
+  return trace_pupil_impl(lens, px, py, rays_out, batch, opt, rec, newton_stat, status, stream,
+                          nullptr);
+}
+
+}  // extern "C"
+
+namespace ortk {
+
+int trace_pupil_impl(const ort_lens* lens, const double* px, const double* py,
+                     ort_rays* rays_out, const ort_batch* batch, const ort_options* opt,
+                     double* rec, ort_newton_stat* newton_stat, int32_t* status, void* stream,
+                     SpotFuse* fuse) {
+  if (fuse) fuse->fused = false;
   if (!rays_out || !batch) return ORT_ERR_ARG;
   if (batch->n_rays == 0) return ORT_OK;
   if (!px || !py || !batch->seg || batch->w) return ORT_ERR_ARG;
@@ -202,10 +217,28 @@ int ort_trace_pupil(const ort_lens* lens, const double* px, const double* py,
       return ORT_ERR_ARG;
     feat |= F_TAPE;
   }
+  // ort_trace_spot: spot pass 1 in the closed-form kernel's epilogue when its blocks can be
+  // the spot chunks (one ray per thread, each (field, lambda) segment one pair)
+  if (fuse && (feat & F_KM) != 0) return ORT_ERR_ARG;  // no schedule protocol here
+  if (fuse && (feat & (F_KM | F_IA | F_REC | F_WRAY)) == 0 && closed_block() == 256 &&
+      !a.pupil_per_ray && a.n_seg == fuse->pairs && a.n_rays == fuse->pairs * a.seg_len &&
+      fuse->chunks * (int64_t)256 >= a.seg_len && (fuse->chunks - 1) * (int64_t)256 < a.seg_len) {
+    a.spot_part1 = fuse->part1;
+    a.spot_count = fuse->count;
+    a.spot_ops = fuse->ops;
+    a.spot_n_ops = fuse->n_ops;
+    a.spot_chunks = fuse->chunks;
+    feat |= F_SPOT;
+    fuse->fused = true;
+  }
   hipStream_t s = (hipStream_t)stream;
   if ((rc = init_outputs(a, s))) return rc;
   return launch(a, feat, s);
 }
+
+}  // namespace ortk
+
+extern "C" {
 
 // ORT_VJP_ADJOINT workspace: tape [S][kTapeRows][n_rays], partial [n_slot][n_wave],
 // slot_sum [n_slot], need [n_slot] (each 256-byte aligned)

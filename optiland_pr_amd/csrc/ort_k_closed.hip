@@ -1,7 +1,7 @@
 // ort_k_closed.hip -- closed-form-lens kernels and the generation-only kernel
 // (kernel templates: ort_kernels.h; compiled as its own translation unit)
 
-#include "ort_kernels.h"
+#include "ort_reduce.h"
 
 namespace ortk {
 __global__ __launch_bounds__(kBlock) void generate_kernel(const KArgs a) {
@@ -49,7 +49,7 @@ KernelFn select_closed(uint32_t feat) {
 #ifdef ORT_NO_AXIAL  // A/B timing only
   feat &= ~F_AXIAL;
 #endif
-  switch (feat & (F_GEN | F_REC | F_MONO | F_WRAY | F_AXIAL)) {
+  switch (feat & (F_GEN | F_REC | F_MONO | F_WRAY | F_AXIAL | F_SPOT)) {
 #define ORT_C(F) \
   case (F):      \
     return trace_closed_kernel<(F)>;        \
@@ -58,6 +58,7 @@ KernelFn select_closed(uint32_t feat) {
     ORT_C(0) ORT_C(F_GEN) ORT_C(F_REC) ORT_C(F_GEN | F_REC)
     ORT_C(F_MONO) ORT_C(F_MONO | F_GEN) ORT_C(F_MONO | F_REC) ORT_C(F_MONO | F_GEN | F_REC)
     ORT_C(F_WRAY) ORT_C(F_WRAY | F_REC)
+    ORT_C(F_GEN | F_SPOT) ORT_C(F_MONO | F_GEN | F_SPOT)
 #undef ORT_C
     default: return nullptr;
   }

@@ -10,11 +10,15 @@
 //                      every block from part1 in index order (<= 768 doubles,
 //                      L2-resident), then sum and max of (x - cx)^2 + (y - cy)^2 over the
 //                      chunk -> part2[pair][chunk]
-//   spot_final_kernel  one block per pair: the pair's partials in index order -> out[pair]
-// Every reduction runs in a fixed order, so the result is bit-identical run to run (no
-// atomics: kernel boundaries order the passes, no cross-block fence). NaN points
-// propagate as in NumPy (the sums carry them; the max keeps an explicit NaN flag, since
-// fmax would drop it).
+//   spot_final         the pair's partials in index order -> out[pair], run by the LAST
+//                      block of the pair to finish spot_dev_kernel (a per-pair arrival
+//                      count, agent-scope release / acquire: the partial rows of every
+//                      XCD's blocks are visible to it), so the statistics are two launches
+//                      after pass 1; pass 1 zeroes the counts for the same call
+// Every reduction runs in a fixed order, so the result is bit-identical run to run (the
+// arrival count only picks WHICH block reduces, not the order). NaN points propagate as
+// in NumPy (the sums carry them; the max keeps an explicit NaN flag, since fmax would
+// drop it).
 
 #include "ort_reduce.h"
 
@@ -44,6 +48,7 @@ struct SpotArgs {
   // the centroids come from these instead of this rank's part1
   const double* gsum;
   double* rms_out;      // ort_rms_spot: the rms radius of pair 0 again, as its own scalar
+  uint32_t* count;      // [n_pairs] arrivals in spot_dev_kernel (NULL: no final there)
 };
 
 // one image point in the surface frame (visualization/system/utils.py:16-46: the point
@@ -72,6 +77,7 @@ __device__ inline void reduce_rows(const double* part, int n, double (&v)[3], do
 
 __global__ __launch_bounds__(kSpotThreads) void spot_sum_kernel(const SpotArgs a) {
   const int64_t pair = blockIdx.y;
+  if (a.count && blockIdx.x == 0 && threadIdx.x == 0) a.count[pair] = 0u;  // this call's
   const int64_t j0 = (int64_t)blockIdx.x * a.per_thread * kSpotThreads + threadIdx.x;
   double v[3] = {0.0, 0.0, 0.0};
   for (int k = 0; k < a.per_thread; ++k) {
@@ -95,6 +101,8 @@ __global__ __launch_bounds__(kSpotThreads) void spot_sum_kernel(const SpotArgs a
     p[2] = v[2];
   }
 }
+
+__device__ void spot_final(const SpotArgs& a, int64_t pair);
 
 __global__ __launch_bounds__(kSpotThreads) void spot_dev_kernel(const SpotArgs a) {
   const int64_t pair = blockIdx.y;
@@ -148,11 +156,22 @@ __global__ __launch_bounds__(kSpotThreads) void spot_dev_kernel(const SpotArgs a
     p[1] = m;
     p[2] = f;
   }
+  if (!a.count) return;
+  // the pair's last block to get here reduces its partials (spot_final)
+  __shared__ int last;
+  if (threadIdx.x == 0) {
+    const uint32_t prev = __hip_atomic_fetch_add(a.count + pair, 1u, __ATOMIC_ACQ_REL,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+    last = prev == (uint32_t)a.n_chunks - 1u;
+  }
+  __syncthreads();
+  if (!last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  spot_final(a, pair);
 }
 
-// one block per pair: the pair's totals, every reduction in index order
-__global__ __launch_bounds__(kSpotThreads) void spot_final_kernel(const SpotArgs a) {
-  const int64_t pair = blockIdx.x;
+// the pair's totals, every reduction in index order (one block)
+__device__ void spot_final(const SpotArgs& a, int64_t pair) {
   __shared__ double lds[4 * 3];
   __shared__ double mx[4][2];
   double own[3];
@@ -267,7 +286,9 @@ static int64_t spot_chunks(const ort_spot_layout* lay) {
 int64_t ort_spot_workspace_size(const ort_spot_layout* lay) {
   if (!lay || lay->n_pupil < 0 || lay->n_fields < 0 || lay->n_wl < 1) return ORT_ERR_ARG;
   const int64_t pairs = (int64_t)lay->n_fields * lay->n_wl;
-  return pairs * spot_chunks(lay) * 3 * 2 * (int64_t)sizeof(double);
+  // part1, part2 [pairs][chunks][3] doubles, then the arrival counts [pairs] (uint32)
+  return pairs * spot_chunks(lay) * 3 * 2 * (int64_t)sizeof(double) +
+         (pairs + 1) / 2 * (int64_t)sizeof(double);
 }
 
 static int spot_args(const ort_rays* rays, const ort_spot_layout* lay, void* workspace,
@@ -298,8 +319,32 @@ static int spot_args(const ort_rays* rays, const ort_spot_layout* lay, void* wor
   a.per_thread = (int32_t)spot_per_thread(lay);
   a.part1 = (double*)workspace;
   a.part2 = a.part1 + pairs * chunks * 3;
+  a.count = (uint32_t*)(a.part2 + pairs * chunks * 3);
   a.out = out;
   return ORT_OK;
+}
+
+int ort_trace_spot(const ort_lens* lens, const double* px, const double* py,
+                   ort_rays* rays_out, const ort_batch* batch, const ort_options* opt,
+                   int32_t* status, const ort_spot_layout* lay, void* workspace,
+                   int64_t workspace_size, double* out, void* stream) {
+  if (!batch || !lay || !rays_out) return ORT_ERR_ARG;
+  if (batch->n_rays != (int64_t)lay->n_fields * lay->n_wl * lay->n_pupil) return ORT_ERR_ARG;
+  if (batch->n_rays == 0) return ORT_OK;
+  SpotArgs a{};
+  int64_t pairs = 0, chunks = 0;
+  int rc = spot_args(rays_out, lay, workspace, workspace_size, out, a, pairs, chunks);
+  if (rc) return rc;
+  SpotFuse f{a.part1, a.count, lay->local_ops, lay->n_local_ops, (int32_t)chunks, pairs, false};
+  if (a.per_thread != 1) f.pairs = -1;  // a chunk spans several rays per thread: unfused
+  rc = trace_pupil_impl(lens, px, py, rays_out, batch, opt, nullptr, nullptr, status, stream,
+                        &f);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 grid((unsigned)chunks, (unsigned)pairs);
+  if (!f.fused) hipLaunchKernelGGL(spot_sum_kernel, grid, dim3(kSpotThreads), 0, s, a);
+  hipLaunchKernelGGL(spot_dev_kernel, grid, dim3(kSpotThreads), 0, s, a);  // + spot_final
+  return hipGetLastError() == hipSuccess ? ORT_OK : ORT_ERR_LAUNCH;
 }
 
 int ort_spot_stats(const ort_rays* rays, const ort_spot_layout* lay, void* workspace,
@@ -311,8 +356,7 @@ int ort_spot_stats(const ort_rays* rays, const ort_spot_layout* lay, void* works
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid((unsigned)chunks, (unsigned)pairs);  // n_pupil == 0: one empty chunk
   hipLaunchKernelGGL(spot_sum_kernel, grid, dim3(kSpotThreads), 0, s, a);
-  hipLaunchKernelGGL(spot_dev_kernel, grid, dim3(kSpotThreads), 0, s, a);
-  hipLaunchKernelGGL(spot_final_kernel, dim3((unsigned)pairs), dim3(kSpotThreads), 0, s, a);
+  hipLaunchKernelGGL(spot_dev_kernel, grid, dim3(kSpotThreads), 0, s, a);  // + spot_final
   return hipGetLastError() == hipSuccess ? ORT_OK : ORT_ERR_LAUNCH;
 }
 
@@ -347,8 +391,7 @@ int ort_rms_spot(const double* x, const double* y, int64_t n, void* workspace,
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid((unsigned)chunks, 1u);
   hipLaunchKernelGGL(spot_sum_kernel, grid, dim3(kSpotThreads), 0, s, a);
-  hipLaunchKernelGGL(spot_dev_kernel, grid, dim3(kSpotThreads), 0, s, a);
-  hipLaunchKernelGGL(spot_final_kernel, dim3(1u), dim3(kSpotThreads), 0, s, a);
+  hipLaunchKernelGGL(spot_dev_kernel, grid, dim3(kSpotThreads), 0, s, a);  // + spot_final
   return hipGetLastError() == hipSuccess ? ORT_OK : ORT_ERR_LAUNCH;
 }
 
@@ -372,6 +415,7 @@ int ort_spot_partials(const ort_rays* rays, const ort_spot_layout* lay, int32_t 
   int64_t pairs = 0, chunks = 0;
   const int rc = spot_args(rays, lay, workspace, workspace_size, out, a, pairs, chunks);
   if (rc || pairs == 0) return rc;
+  a.count = nullptr;  // the caller reduces over the ranks between the passes
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid((unsigned)chunks, (unsigned)pairs);
   if (phase == 1) {

@@ -70,6 +70,7 @@ enum : uint32_t {
   F_IA = 1u << 8,    // thin-lens / phase / grating interactions (ort_interaction)
   F_AXIAL = 1u << 9, // ORT_LENS_AXIAL: every frame a +z translation (closed-form kernels)
   F_TAPE = 1u << 10, // write the adjoint tape as the trace runs (ort_options.tape)
+  F_SPOT = 1u << 11, // closed-form kernel: spot pass 1 in the epilogue (ort_trace_spot)
 };
 
 // Adjoint tape (ort_adjoint.h): per traced surface, rows of n_rays doubles -- the incoming
@@ -126,7 +127,36 @@ struct KArgs {
   const int32_t* run_if;
   int32_t no_init;  // host side only: ORT_OPT_NO_INIT (skip init_outputs)
   double* tape;     // F_TAPE: [n_surf][kTapeRows][n_rays] (ort_options.tape)
+  // F_SPOT (ort_trace_spot): block b traces chunk b % spot_chunks of pair b / spot_chunks
+  // (kClosedBlock rays of seg_len, the tail lanes idle) and writes the chunk's count, sum x,
+  // sum y of its i > 0 image points, in the image frame, to spot_part1[b][3] -- the rows
+  // spot_sum_kernel would write (ort_k_spot.hip), by the same block reduction
+  double* spot_part1;
+  uint32_t* spot_count;  // [pairs] the statistics' arrival counts: zeroed here for this call
+  const ort_cs_op* spot_ops;
+  int32_t spot_n_ops;
+  int32_t spot_chunks;
 };
+
+// ort_trace_spot -> trace_pupil_impl (ort_api.hip): where the fused spot pass 1 writes;
+// fused reports whether the launch took it
+struct SpotFuse {
+  double* part1;
+  uint32_t* count;
+  const ort_cs_op* ops;
+  int32_t n_ops;
+  int32_t chunks;
+  int64_t pairs;
+  bool fused;
+};
+int trace_pupil_impl(const ort_lens* lens, const double* px, const double* py,
+                     ort_rays* rays_out, const ort_batch* batch, const ort_options* opt,
+                     double* rec, ort_newton_stat* newton_stat, int32_t* status, void* stream,
+                     SpotFuse* fuse);
+
+// the F_SPOT epilogue (ort_reduce.h): every thread of the block calls it
+template <uint32_t FEAT>
+__device__ void spot_epilogue(const KArgs& a, const ort::Ray& r, double inten, bool active);
 
 // Ray of this thread when every (field, lambda) segment traces the SAME pupil samples
 // (real_ray_tracer.py:74-77 field-major layout: ray = segment * seg_len + p): block b
@@ -786,8 +816,17 @@ __device__ inline void closed_surfaces(const KArgs& a, ort::Ray& r, int lam, dou
 
 template <uint32_t FEAT>
 __global__ __launch_bounds__(kClosedBlock) __attribute__((amdgpu_waves_per_eu(8))) void trace_closed_kernel(const KArgs a) {
-  const int64_t rid = (int64_t)blockIdx.x * kClosedBlock + threadIdx.x;
-  const bool active = rid < a.n_rays;
+  int64_t rid;
+  bool active;
+  if constexpr ((FEAT & F_SPOT) != 0) {  // pair-aligned chunks (KArgs.spot_part1)
+    const int64_t pair = blockIdx.x / a.spot_chunks;
+    const int64_t j = (int64_t)(blockIdx.x - pair * a.spot_chunks) * kClosedBlock + threadIdx.x;
+    rid = pair * a.seg_len + j;
+    active = j < a.seg_len && rid < a.n_rays;
+  } else {
+    rid = (int64_t)blockIdx.x * kClosedBlock + threadIdx.x;
+    active = rid < a.n_rays;
+  }
   const int64_t r_ld = active ? rid : 0;
   int lam = 0;
   double wl = 0.0;  // F_WRAY: this ray's wavelength
@@ -821,13 +860,6 @@ __global__ __launch_bounds__(kClosedBlock) __attribute__((amdgpu_waves_per_eu(8)
         (uint32_t)cst(a.apod)->kind > (uint32_t)ORT_APOD_TUKEY)
       atomicOr(a.status, (int)ORT_STATUS_BAD_APODIZATION);
   }
-  if (!active) return;
-  a.out.x[rid] = r.x;
-  a.out.y[rid] = r.y;
-  a.out.z[rid] = r.z;
-  a.out.L[rid] = r.L;
-  a.out.M[rid] = r.M;
-  a.out.N[rid] = r.N;
   double inten = ort::intensity(r);
 #ifndef ORT_NO_APOD
   if constexpr ((FEAT & F_GEN) != 0) {
@@ -836,12 +868,20 @@ __global__ __launch_bounds__(kClosedBlock) __attribute__((amdgpu_waves_per_eu(8)
     // apod * (1 * e^att or 0) is the value the ray would carry from an apodized start,
     // with the apodization code outside the traced loop.
     if (a.apod) {
-      const int64_t sidx = a.n_seg == 1 ? 0 : rid / a.seg_len;
-      const int64_t p = a.pupil_per_ray ? rid : (rid - sidx * a.seg_len);
+      const int64_t sidx = a.n_seg == 1 ? 0 : r_ld / a.seg_len;
+      const int64_t p = a.pupil_per_ray ? r_ld : (r_ld - sidx * a.seg_len);
       inten = ort::apodize(*cst(a.apod), a.px[p], a.py[p]) * inten;
     }
   }
 #endif
+  if constexpr ((FEAT & F_SPOT) != 0) spot_epilogue<FEAT>(a, r, inten, active);
+  if (!active) return;
+  a.out.x[rid] = r.x;
+  a.out.y[rid] = r.y;
+  a.out.z[rid] = r.z;
+  a.out.L[rid] = r.L;
+  a.out.M[rid] = r.M;
+  a.out.N[rid] = r.N;
   a.out.i[rid] = inten;
   a.out.opd[rid] = r.opd;
 }

@@ -49,4 +49,34 @@ __device__ inline void reduce_rows_n(const double* part, int n, double (&v)[NV],
   block_sum<NV>(v, lds);
 }
 
+// F_SPOT epilogue of trace_closed_kernel: spot_sum_kernel's pass over one chunk
+// (ort_k_spot.hip, one ray per thread), on the rays still in registers -- the same
+// per-thread values (the point localized by the same ops, masked by i > 0) and the same
+// block_sum, so the partial rows are bit-identical to that kernel's
+template <uint32_t FEAT>
+__device__ void spot_epilogue(const KArgs& a, const ort::Ray& r, double inten, bool active) {
+  static_assert(kClosedBlock == kRedThreads, "one chunk per trace block");
+  double v[3] = {0.0, 0.0, 0.0};
+  if (active && inten > 0.0) {  // spot_diagram.py:425-427
+    ort::Ray p;
+    p.x = r.x;
+    p.y = r.y;
+    p.z = a.spot_n_ops ? r.z : 0.0;
+    p.L = 0.0; p.M = 0.0; p.N = 0.0;
+    for (int k = 0; k < a.spot_n_ops; ++k) ort::apply_cs_op(p, cst(a.spot_ops)[k]);
+    v[0] = 1.0;
+    v[1] = 0.0 + p.x;  // as spot_sum_kernel's 0.0 += x (-0.0 -> +0.0)
+    v[2] = 0.0 + p.y;
+  }
+  __shared__ double lds[4 * 3];
+  block_sum<3>(v, lds);
+  if (threadIdx.x == 0) {
+    if (blockIdx.x % a.spot_chunks == 0) a.spot_count[blockIdx.x / a.spot_chunks] = 0u;
+    double* o = a.spot_part1 + (int64_t)blockIdx.x * 3;
+    o[0] = v[0];
+    o[1] = v[1];
+    o[2] = v[2];
+  }
+}
+
 }  // namespace ortk

@@ -537,6 +537,32 @@ def trace_pupil(dlens: DeviceLens, segments, px, py, out: RealRays, n_rays,
     return seg_dev
 
 
+def trace_spot(dlens: DeviceLens, segments, px, py, out: RealRays, n_rays, seg_len, spot):
+    """Trace + spot statistics of a lens without Newton geometries (ort_trace_spot): the
+    pairs' rays into `out` and spot.out [pairs][5] as SpotStatistics.run(out) gives them,
+    with the statistics' first pass in the trace kernel's epilogue (2 launches)."""
+    if dlens.newton:
+        raise ValueError("trace_spot: Newton lenses trace through trace_pupil + "
+                         "SpotStatistics.run (the Newton schedule protocol)")
+    lib = _native.load()
+    seg_dev = (segments if torch.is_tensor(segments) else
+               dlens.resident("segments", np.asarray(segments, dtype=_abi.SEGMENT)))
+    n_seg = seg_dev.numel() // _abi.SEGMENT.itemsize
+    batch = _native.ort_batch(n_rays, seg_len, seg_len, n_seg, 0, seg_dev.data_ptr())
+    batch.apod = _addr(dlens.apod)
+    out_c = out.c_struct()
+
+    def launch(opt, stats, status):
+        rc = lib.ort_trace_spot(C.byref(dlens.c), _ptr(px), _ptr(py), C.byref(out_c),
+                                C.byref(batch), C.byref(opt), _ptr(status), C.byref(spot._lay),
+                                C.c_void_p(spot._ws.data_ptr()), spot._size,
+                                C.c_void_p(spot.out.data_ptr()), _stream_handle())
+        _native.check(rc, "ort_trace_spot")
+
+    _run(dlens, launch, n_rays, seg_len, [], "reference")
+    return spot.out
+
+
 def trace_rays(dlens: DeviceLens, rays_in: RealRays, rays_out: RealRays, group_len=None,
                keys=(), rec=None, newton_mode="reference", start_surface=0, segments=None,
                seg_len=None, per_ray_w=False):

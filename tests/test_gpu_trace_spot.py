@@ -1,0 +1,114 @@
+"""GPU: ort_trace_spot (trace + spot statistics with the statistics' first pass in the
+closed-form kernel's epilogue) against the unfused path on the same inputs -- ort_trace_pupil
+followed by ort_spot_stats. Both the image rays and the statistics must be bit-identical:
+the epilogue forms the same per-thread values and the same block reduction as
+spot_sum_kernel (ort_reduce.h spot_epilogue). The reference side of these numbers is
+pinned by test_gpu_spot_stats.py (NumPy statistics, spot_diagram.py:317-357) and
+test_gpu_config_sizes.py (config 1's own workload).
+"""
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.fail("needs the MI355X")
+    from optiland_pr_amd import _native
+
+    _native.load()
+    return torch
+
+
+def both(torch, lens, fields, wls, distribution, rings, ref_wl=0, local=True):
+    from optiland_pr_amd.analysis import SpotStatistics
+    from optiland_pr_amd.lowering import pupil_scalars, segment_params
+    from optiland_pr_amd.pupil import pupil_arrays
+    from optiland_pr_amd.raytrace import RealRays, lens_for, trace_pupil
+
+    dl = lens_for(lens, wls)
+    EPL, EPD = pupil_scalars(lens)
+    segs = np.stack([segment_params(lens, hx, hy, wi, EPL, EPD)
+                     for hx, hy in fields for wi in range(len(wls))])
+    px, py = pupil_arrays(distribution, rings, dl.device)
+    n_p = px.numel()
+    n = n_p * len(segs)
+    img = lens.image_surface if local else None
+    a = RealRays.empty(n, 0.0, device=dl.device)
+    sa = SpotStatistics(len(fields), len(wls), n_p, ref_wl, img, dl.device)
+    fused = sa.trace(dl, segs, px, py, a).clone()
+    b = RealRays.empty(n, 0.0, device=dl.device)
+    trace_pupil(dl, segs, px, py, b, n, n_p, n_p)
+    sb = SpotStatistics(len(fields), len(wls), n_p, ref_wl, img, dl.device)
+    plain = sb.run(b).clone()
+    for f in ("x", "y", "z", "L", "M", "N", "i", "opd"):
+        assert torch.equal(getattr(a, f).isnan(), getattr(b, f).isnan()), f
+        ga, gb = getattr(a, f).nan_to_num(), getattr(b, f).nan_to_num()
+        assert torch.equal(ga.view(torch.int64), gb.view(torch.int64)), f
+    fa, fb = fused.cpu().numpy(), plain.cpu().numpy()
+    np.testing.assert_array_equal(np.isnan(fa), np.isnan(fb))
+    assert np.array_equal(np.nan_to_num(fa).view(np.int64), np.nan_to_num(fb).view(np.int64))
+    return fa, n_p
+
+
+def test_config1_workload(torch):
+    """Config 1 exactly: Cooke, Hy 0 / 0.7 / 1, 0.55 um, uniform 128 (12,644 rays per pair:
+    50 chunks, the last one partial)."""
+    from optiland_pr_amd.samples import CookeTriplet
+
+    st, n_p = both(torch, CookeTriplet(), [(0.0, 0.0), (0.0, 0.7), (0.0, 1.0)], [0.55],
+                   "uniform", 128)
+    assert n_p == 12644 and np.all(st[:, 0] > 0)
+
+
+def test_small_pupil_and_wavelengths(torch):
+    """Pairs shorter than one block (hexapolar 6: 127 rays), three wavelengths with the
+    centroid of the middle one, global coordinates."""
+    from optiland_pr_amd.samples import CookeTriplet
+
+    both(torch, CookeTriplet(), [(0.0, 0.0), (0.0, 1.0)], [0.4861, 0.5876, 0.6563],
+         "hexapolar", 6, ref_wl=1, local=False)
+
+
+def test_local_frame_ops_and_clipping(torch):
+    """Image-frame ops applied in the epilogue (tilted / decentred image plane) and an
+    aperture that clips rays (i = 0 points leave the sums)."""
+    from optiland_pr_amd.samples import CookeTripletApertures, DecenteredTriplet
+
+    lens = DecenteredTriplet()
+    lens.surface_group.surfaces[-1].geometry.cs.rx = 0.05
+    lens.surface_group.surfaces[-1].geometry.cs.y = 0.3
+    lens.invalidate()
+    both(torch, lens, [(0.0, 0.0), (0.0, 1.0)], [0.5876], "uniform", 40)
+    both(torch, CookeTripletApertures(), [(0.0, 0.0), (0.0, 1.0)], [0.5876], "hexapolar", 10)
+
+
+def test_large_pairs_take_the_unfused_path(torch):
+    """More than 65,536 rays per pair: a chunk holds several rays per thread, so
+    ort_trace_spot runs the separate first pass -- still the same numbers."""
+    from optiland_pr_amd.samples import DoubleGauss
+
+    _, n_p = both(torch, DoubleGauss(), [(0.0, 0.0), (0.0, 1.0)], [0.5876], "uniform", 400)
+    assert n_p > 65536
+
+
+def test_newton_lens_refused(torch):
+    from optiland_pr_amd.analysis import SpotStatistics
+    from optiland_pr_amd.lowering import segment_params
+    from optiland_pr_amd.pupil import pupil_arrays
+    from optiland_pr_amd.raytrace import RealRays, lens_for
+    from optiland_pr_amd.samples import ReverseTelephotoAsphere
+
+    lens = ReverseTelephotoAsphere()
+    dl = lens_for(lens, [0.5876])
+    px, py = pupil_arrays("hexapolar", 3, dl.device)
+    segs = np.stack([segment_params(lens, 0.0, 0.0, 0)])
+    out = RealRays.empty(px.numel(), 0.0, device=dl.device)
+    spot = SpotStatistics(1, 1, px.numel(), 0, None, dl.device)
+    with pytest.raises(ValueError):
+        spot.trace(dl, segs, px, py, out)
