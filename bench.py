@@ -138,12 +138,12 @@ def config1(args, dev, rank, world, torch):
         config={"workload": "CookeTriplet (samples/objectives.py:46-72), fields Hy 0 / 0.7 / 1 "
                             "(0 / 14 / 20 deg), lambda 0.55 um, uniform 128 (12,644 rays per "
                             "field): fused trace of the 3 pairs with the statistics' first "
-                            "pass in its epilogue + the second pass whose last block per pair "
-                            "forms the totals (ort_trace_spot), one HIP graph replay per step",
+                            "pass in its epilogue, then the second pass and the totals "
+                            "(ort_trace_spot), one HIP graph replay per step",
                 "rays_per_gpu": n, "surfaces": S,
                 "parallelism": f"dp{world} (replicas, no collective)"},
-        kernel="trace_closed_kernel<F_GEN|F_SPOT> + spot_dev_kernel (graph)",
-        launches=2,
+        kernel="trace_closed_kernel<F_GEN|F_SPOT> + spot_dev + spot_final (graph)",
+        launches=3,
         bytes_per_launch=None, flops_per_ray=None, pmc_file=None, rays=n, state=state,
         spot=True, data="synthetic (the reference's uniform 128 pupil grid)")
 

@@ -636,9 +636,8 @@ typedef struct ort_spot_layout {
 int64_t ort_spot_workspace_size(const ort_spot_layout* layout);
 
 /* rays: device x, y, z, i of n_fields * n_wl * n_pupil rays (other fields unused; z
- * only with local_ops); out: device [n_fields * n_wl][5]. Two launches on `stream` (the
- * second pass's last block per pair forms the totals), no synchronisation, no allocation
- * (graph-capturable); the workspace needs no initialisation. */
+ * only with local_ops); out: device [n_fields * n_wl][5]. Three launches on `stream`,
+ * no synchronisation, no allocation (graph-capturable). */
 int ort_spot_stats(const ort_rays* rays, const ort_spot_layout* layout, void* workspace,
                    int64_t workspace_size, double* out, void* stream);
 
@@ -647,7 +646,7 @@ int ort_spot_stats(const ort_rays* rays, const ort_spot_layout* layout, void* wo
  * pair order, batch->seg_len == layout->n_pupil, shared pupil) into rays_out, then
  * out[pair][5] as ort_spot_stats computes it. When each pair's chunks hold one ray per
  * thread (n_pupil <= 65,536) the closed-form kernel writes the statistics' first pass from
- * its epilogue (2 launches: the trace, then the second pass + totals); otherwise 3. The numbers are
+ * its epilogue (3 launches: the trace, the second pass, the totals); otherwise 4. The numbers are
  * bit-identical to ort_trace_pupil followed by ort_spot_stats either way. Replaces
  * SpotDiagram._generate_field_data's trace loop + the statistics over its data
  * (analysis/spot_diagram.py:317-357, 381-438). Newton lenses: ORT_ERR_ARG. */
@@ -660,7 +659,7 @@ int ort_trace_spot(const ort_lens* lens, const double* px, const double* py,
  * rms = sqrt(mean((x - mean x)^2 + (y - mean y)^2)) over all n points (no intensity mask),
  * two passes in a fixed order (the spot-statistics kernels with one pair). stats (device
  * double[5]) = { n, mean x, mean y, rms, max radius }; rms (device double, nullable) gets
- * the rms again as its own scalar (the autograd op's output). Two launches.
+ * the rms again as its own scalar (the autograd op's output). Three launches.
  * ort_rms_spot_vjp: gx[i] = g (x_i - mean x) / (n rms), gy likewise, g = *grad_out (a
  * device scalar, read on the device: no host synchronisation). One launch. */
 int64_t ort_rms_spot_workspace_size(int64_t n);

@@ -85,7 +85,7 @@ class SpotStatistics:
     into `surface`'s frame when given (coordinates="local").
 
     The constructor uploads the image frame's ops and allocates the workspace and the
-    output; run() only launches (two small kernels, no host sync, no allocation), so
+    output; run() only launches (three small kernels, no host sync, no allocation), so
     it can be captured in a HIP graph."""
 
     def __init__(self, n_fields, n_wl, n_pupil, ref_wl, surface=None, device=None):

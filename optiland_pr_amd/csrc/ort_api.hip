@@ -224,7 +224,6 @@ int trace_pupil_impl(const ort_lens* lens, const double* px, const double* py,
       !a.pupil_per_ray && a.n_seg == fuse->pairs && a.n_rays == fuse->pairs * a.seg_len &&
       fuse->chunks * (int64_t)256 >= a.seg_len && (fuse->chunks - 1) * (int64_t)256 < a.seg_len) {
     a.spot_part1 = fuse->part1;
-    a.spot_count = fuse->count;
     a.spot_ops = fuse->ops;
     a.spot_n_ops = fuse->n_ops;
     a.spot_chunks = fuse->chunks;

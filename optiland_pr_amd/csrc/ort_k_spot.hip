@@ -10,15 +10,17 @@
 //                      every block from part1 in index order (<= 768 doubles,
 //                      L2-resident), then sum and max of (x - cx)^2 + (y - cy)^2 over the
 //                      chunk -> part2[pair][chunk]
-//   spot_final         the pair's partials in index order -> out[pair], run by the LAST
-//                      block of the pair to finish spot_dev_kernel (a per-pair arrival
-//                      count, agent-scope release / acquire: the partial rows of every
-//                      XCD's blocks are visible to it), so the statistics are two launches
-//                      after pass 1; pass 1 zeroes the counts for the same call
-// Every reduction runs in a fixed order, so the result is bit-identical run to run (the
-// arrival count only picks WHICH block reduces, not the order). NaN points propagate as
-// in NumPy (the sums carry them; the max keeps an explicit NaN flag, since fmax would
-// drop it).
+//   spot_final_kernel  one block per pair: the pair's partials in index order -> out[pair]
+// Every reduction runs in a fixed order, so the result is bit-identical run to run (no
+// atomics: kernel boundaries order the passes, no cross-block fence). NaN points
+// propagate as in NumPy (the sums carry them; the max keeps an explicit NaN flag, since
+// fmax would drop it). Measured and dropped: spot_final as the last block of
+// spot_dev_kernel to arrive (a per-pair atomic count with agent-scope release / acquire):
+// 8.8 us for that kernel vs 4.5 + 3.9 us for the two -- every block's release writes back
+// its L2 and the final reduction still runs after the last arrival.
+//
+// Each pass issues its per-ray loads before the reduction of the previous pass's
+// partials, so the two memory round trips overlap.
 
 #include "ort_reduce.h"
 
@@ -48,7 +50,6 @@ struct SpotArgs {
   // the centroids come from these instead of this rank's part1
   const double* gsum;
   double* rms_out;      // ort_rms_spot: the rms radius of pair 0 again, as its own scalar
-  uint32_t* count;      // [n_pairs] arrivals in spot_dev_kernel (NULL: no final there)
 };
 
 // one image point in the surface frame (visualization/system/utils.py:16-46: the point
@@ -77,7 +78,6 @@ __device__ inline void reduce_rows(const double* part, int n, double (&v)[3], do
 
 __global__ __launch_bounds__(kSpotThreads) void spot_sum_kernel(const SpotArgs a) {
   const int64_t pair = blockIdx.y;
-  if (a.count && blockIdx.x == 0 && threadIdx.x == 0) a.count[pair] = 0u;  // this call's
   const int64_t j0 = (int64_t)blockIdx.x * a.per_thread * kSpotThreads + threadIdx.x;
   double v[3] = {0.0, 0.0, 0.0};
   for (int k = 0; k < a.per_thread; ++k) {
@@ -102,11 +102,21 @@ __global__ __launch_bounds__(kSpotThreads) void spot_sum_kernel(const SpotArgs a
   }
 }
 
-__device__ void spot_final(const SpotArgs& a, int64_t pair);
-
 __global__ __launch_bounds__(kSpotThreads) void spot_dev_kernel(const SpotArgs a) {
   const int64_t pair = blockIdx.y;
   __shared__ double lds[4 * 3];
+  // one ray per thread: its point is loaded before the centroid's reduction below, so the
+  // two memory round trips overlap (same arithmetic as the loop further down)
+  bool on = false;
+  double px = 0.0, py = 0.0;
+  if (a.per_thread == 1) {
+    const int64_t j = (int64_t)blockIdx.x * kSpotThreads + threadIdx.x;
+    if (j < a.n_pupil) {
+      const int64_t r = pair * a.n_pupil + j;
+      on = !a.i || a.i[r] > 0.0;
+      if (on) local_point(a, r, px, py);
+    }
+  }
   // centroid of the field's reference-wavelength spot (spot_diagram.py:317-328)
   const int64_t ref = (pair / a.n_wl) * a.n_wl + a.ref_wl;
   double c[3];
@@ -121,19 +131,26 @@ __global__ __launch_bounds__(kSpotThreads) void spot_dev_kernel(const SpotArgs a
 
   const int64_t j0 = (int64_t)blockIdx.x * a.per_thread * kSpotThreads + threadIdx.x;
   double s = 0.0, m = 0.0, f = 0.0;
-  for (int k = 0; k < a.per_thread; ++k) {
-    const int64_t j = j0 + (int64_t)k * kSpotThreads;
-    if (j >= a.n_pupil) break;
-    const int64_t r = pair * a.n_pupil + j;
-    if (!a.i || a.i[r] > 0.0) {
-      double x, y;
-      local_point(a, r, x, y);
-      const double dx = x - cx, dy = y - cy;
-      const double r2 = dx * dx + dy * dy;  // x**2 + y**2 of the centred spot
-      s += r2;
-      const double rad = ::sqrt(r2);
-      if (rad != rad) f = 1.0;  // NaN seen
-      else m = ::fmax(m, rad);
+  auto add = [&](double x, double y) {
+    const double dx = x - cx, dy = y - cy;
+    const double r2 = dx * dx + dy * dy;  // x**2 + y**2 of the centred spot
+    s += r2;
+    const double rad = ::sqrt(r2);
+    if (rad != rad) f = 1.0;  // NaN seen
+    else m = ::fmax(m, rad);
+  };
+  if (a.per_thread == 1) {
+    if (on) add(px, py);
+  } else {
+    for (int k = 0; k < a.per_thread; ++k) {
+      const int64_t j = j0 + (int64_t)k * kSpotThreads;
+      if (j >= a.n_pupil) break;
+      const int64_t r = pair * a.n_pupil + j;
+      if (!a.i || a.i[r] > 0.0) {
+        double x, y;
+        local_point(a, r, x, y);
+        add(x, y);
+      }
     }
   }
   double v[1] = {s};
@@ -156,34 +173,24 @@ __global__ __launch_bounds__(kSpotThreads) void spot_dev_kernel(const SpotArgs a
     p[1] = m;
     p[2] = f;
   }
-  if (!a.count) return;
-  // the pair's last block to get here reduces its partials (spot_final)
-  __shared__ int last;
-  if (threadIdx.x == 0) {
-    const uint32_t prev = __hip_atomic_fetch_add(a.count + pair, 1u, __ATOMIC_ACQ_REL,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-    last = prev == (uint32_t)a.n_chunks - 1u;
-  }
-  __syncthreads();
-  if (!last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  spot_final(a, pair);
 }
 
-// the pair's totals, every reduction in index order (one block)
-__device__ void spot_final(const SpotArgs& a, int64_t pair) {
+// one block per pair: the pair's totals, every reduction in index order
+__global__ __launch_bounds__(kSpotThreads) void spot_final_kernel(const SpotArgs a) {
+  const int64_t pair = blockIdx.x;
   __shared__ double lds[4 * 3];
   __shared__ double mx[4][2];
   double own[3];
-  reduce_rows(a.part1 + pair * a.n_chunks * 3, a.n_chunks, own, lds);
   const double* p2 = a.part2 + pair * a.n_chunks * 3;
   double t[1] = {0.0};
   double m = 0.0, f = 0.0;
+  // pass-2 partials read before pass 1's reduction (overlapping round trips)
   for (int k = threadIdx.x; k < a.n_chunks; k += kSpotThreads) {
     t[0] += p2[k * 3 + 0];
     m = ::fmax(m, p2[k * 3 + 1]);
     f = ::fmax(f, p2[k * 3 + 2]);
   }
+  reduce_rows(a.part1 + pair * a.n_chunks * 3, a.n_chunks, own, lds);
   block_sum<1>(t, lds);
   m = wave_max(m);
   f = wave_max(f);
@@ -206,6 +213,16 @@ __device__ void spot_final(const SpotArgs& a, int64_t pair) {
     o[4] = (f != 0.0 || t[0] != t[0] || n == 0.0) ? __builtin_nan("") : m;  // be.max
     if (a.rms_out && pair == 0) *a.rms_out = o[3];
   }
+}
+
+// pass 2 + totals. Measured and dropped: both in one block per pair for small pairs
+// (each wave summing its chunks' four 64-lane sub-chunks in block_sum's order,
+// bit-identical): 46.9 us for config 1 against 4.6 + 4.0 us -- the serial per-sub-chunk
+// load round trips of three blocks cost more than a launch.
+void launch_pass2(const SpotArgs& a, int64_t pairs, int64_t chunks, hipStream_t s) {
+  hipLaunchKernelGGL(spot_dev_kernel, dim3((unsigned)chunks, (unsigned)pairs), dim3(kSpotThreads),
+                     0, s, a);
+  hipLaunchKernelGGL(spot_final_kernel, dim3((unsigned)pairs), dim3(kSpotThreads), 0, s, a);
 }
 
 // ort_spot_partials: one block per pair, the pair's chunk partials in index order ->
@@ -286,9 +303,7 @@ static int64_t spot_chunks(const ort_spot_layout* lay) {
 int64_t ort_spot_workspace_size(const ort_spot_layout* lay) {
   if (!lay || lay->n_pupil < 0 || lay->n_fields < 0 || lay->n_wl < 1) return ORT_ERR_ARG;
   const int64_t pairs = (int64_t)lay->n_fields * lay->n_wl;
-  // part1, part2 [pairs][chunks][3] doubles, then the arrival counts [pairs] (uint32)
-  return pairs * spot_chunks(lay) * 3 * 2 * (int64_t)sizeof(double) +
-         (pairs + 1) / 2 * (int64_t)sizeof(double);
+  return pairs * spot_chunks(lay) * 3 * 2 * (int64_t)sizeof(double);
 }
 
 static int spot_args(const ort_rays* rays, const ort_spot_layout* lay, void* workspace,
@@ -319,7 +334,6 @@ static int spot_args(const ort_rays* rays, const ort_spot_layout* lay, void* wor
   a.per_thread = (int32_t)spot_per_thread(lay);
   a.part1 = (double*)workspace;
   a.part2 = a.part1 + pairs * chunks * 3;
-  a.count = (uint32_t*)(a.part2 + pairs * chunks * 3);
   a.out = out;
   return ORT_OK;
 }
@@ -335,7 +349,7 @@ int ort_trace_spot(const ort_lens* lens, const double* px, const double* py,
   int64_t pairs = 0, chunks = 0;
   int rc = spot_args(rays_out, lay, workspace, workspace_size, out, a, pairs, chunks);
   if (rc) return rc;
-  SpotFuse f{a.part1, a.count, lay->local_ops, lay->n_local_ops, (int32_t)chunks, pairs, false};
+  SpotFuse f{a.part1, lay->local_ops, lay->n_local_ops, (int32_t)chunks, pairs, false};
   if (a.per_thread != 1) f.pairs = -1;  // a chunk spans several rays per thread: unfused
   rc = trace_pupil_impl(lens, px, py, rays_out, batch, opt, nullptr, nullptr, status, stream,
                         &f);
@@ -343,7 +357,7 @@ int ort_trace_spot(const ort_lens* lens, const double* px, const double* py,
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid((unsigned)chunks, (unsigned)pairs);
   if (!f.fused) hipLaunchKernelGGL(spot_sum_kernel, grid, dim3(kSpotThreads), 0, s, a);
-  hipLaunchKernelGGL(spot_dev_kernel, grid, dim3(kSpotThreads), 0, s, a);  // + spot_final
+  launch_pass2(a, pairs, chunks, s);
   return hipGetLastError() == hipSuccess ? ORT_OK : ORT_ERR_LAUNCH;
 }
 
@@ -356,7 +370,7 @@ int ort_spot_stats(const ort_rays* rays, const ort_spot_layout* lay, void* works
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid((unsigned)chunks, (unsigned)pairs);  // n_pupil == 0: one empty chunk
   hipLaunchKernelGGL(spot_sum_kernel, grid, dim3(kSpotThreads), 0, s, a);
-  hipLaunchKernelGGL(spot_dev_kernel, grid, dim3(kSpotThreads), 0, s, a);  // + spot_final
+  launch_pass2(a, pairs, chunks, s);
   return hipGetLastError() == hipSuccess ? ORT_OK : ORT_ERR_LAUNCH;
 }
 
@@ -391,7 +405,7 @@ int ort_rms_spot(const double* x, const double* y, int64_t n, void* workspace,
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid((unsigned)chunks, 1u);
   hipLaunchKernelGGL(spot_sum_kernel, grid, dim3(kSpotThreads), 0, s, a);
-  hipLaunchKernelGGL(spot_dev_kernel, grid, dim3(kSpotThreads), 0, s, a);  // + spot_final
+  launch_pass2(a, pairs, chunks, s);
   return hipGetLastError() == hipSuccess ? ORT_OK : ORT_ERR_LAUNCH;
 }
 
@@ -415,7 +429,6 @@ int ort_spot_partials(const ort_rays* rays, const ort_spot_layout* lay, int32_t 
   int64_t pairs = 0, chunks = 0;
   const int rc = spot_args(rays, lay, workspace, workspace_size, out, a, pairs, chunks);
   if (rc || pairs == 0) return rc;
-  a.count = nullptr;  // the caller reduces over the ranks between the passes
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid((unsigned)chunks, (unsigned)pairs);
   if (phase == 1) {

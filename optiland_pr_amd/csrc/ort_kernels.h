@@ -132,7 +132,6 @@ struct KArgs {
   // sum y of its i > 0 image points, in the image frame, to spot_part1[b][3] -- the rows
   // spot_sum_kernel would write (ort_k_spot.hip), by the same block reduction
   double* spot_part1;
-  uint32_t* spot_count;  // [pairs] the statistics' arrival counts: zeroed here for this call
   const ort_cs_op* spot_ops;
   int32_t spot_n_ops;
   int32_t spot_chunks;
@@ -142,7 +141,6 @@ struct KArgs {
 // fused reports whether the launch took it
 struct SpotFuse {
   double* part1;
-  uint32_t* count;
   const ort_cs_op* ops;
   int32_t n_ops;
   int32_t chunks;

@@ -71,7 +71,6 @@ __device__ void spot_epilogue(const KArgs& a, const ort::Ray& r, double inten, b
   __shared__ double lds[4 * 3];
   block_sum<3>(v, lds);
   if (threadIdx.x == 0) {
-    if (blockIdx.x % a.spot_chunks == 0) a.spot_count[blockIdx.x / a.spot_chunks] = 0u;
     double* o = a.spot_part1 + (int64_t)blockIdx.x * 3;
     o[0] = v[0];
     o[1] = v[1];

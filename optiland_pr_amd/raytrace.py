@@ -540,7 +540,7 @@ def trace_pupil(dlens: DeviceLens, segments, px, py, out: RealRays, n_rays,
 def trace_spot(dlens: DeviceLens, segments, px, py, out: RealRays, n_rays, seg_len, spot):
     """Trace + spot statistics of a lens without Newton geometries (ort_trace_spot): the
     pairs' rays into `out` and spot.out [pairs][5] as SpotStatistics.run(out) gives them,
-    with the statistics' first pass in the trace kernel's epilogue (2 launches)."""
+    with the statistics' first pass in the trace kernel's epilogue (3 launches for pairs of <= 65,536 rays)."""
     if dlens.newton:
         raise ValueError("trace_spot: Newton lenses trace through trace_pupil + "
                          "SpotStatistics.run (the Newton schedule protocol)")

@@ -112,3 +112,4 @@ def test_newton_lens_refused(torch):
     spot = SpotStatistics(1, 1, px.numel(), 0, None, dl.device)
     with pytest.raises(ValueError):
         spot.trace(dl, segs, px, py, out)
+
