@@ -521,7 +521,7 @@ def _roofline(w, kern_ms):
     if getattr(w, "spot", False):
         return {"bound": "launch", "achieved": None, "peak": None, "unit": None, "frac": None,
                 "traffic": None, "kernel": w.kernel, "step_device_ms": kern_ms,
-                "note": "38K rays per step: launch / latency bound (4 kernels in one graph); "
+                "note": "38K rays per step: launch / latency bound (3 kernels in one graph); "
                         "the per-intersection roofline is config 2's"}
     if getattr(w, "vjp_ms", None):
         # multi-launch optimisation step: the roofline is the backward's adjoint kernel,

@@ -18,26 +18,46 @@ __global__ void adj_need_kernel(const AArgs j, int32_t* need) {
 // One block per PARAMETER: grad[p] += sum over the slots p depends on of
 // d slot / d p * (the slot's wave partials summed in index order) -- the reduction and
 // the contraction with the tangent tables in one launch, deterministic (a fixed order,
-// no atomics; a slot shared by several parameters is summed once per parameter).
+// no atomics; a slot shared by several parameters is summed once per parameter). The
+// slot weights are read by all threads at once (256 slots per pass into LDS) rather than
+// one dependent table load per slot, and each thread's strided partial loads are issued
+// eight at a time ahead of their (in-order) additions: 27 -> see DESIGN for the TMA's 43
+// slots x 30 parameters.
 __global__ __launch_bounds__(kBlock) void adj_param_reduce_kernel(const AArgs j) {
   const int p = blockIdx.x;
   __shared__ double ws[kBlock / 64];
+  __shared__ double wt[kBlock];
   double g = 0.0;  // meaningful in thread 0
-  for (int slot = 0; slot < j.n_slot; ++slot) {
-    const double w = slot_weight(j, slot, p);  // uniform: tables in constant memory
-    if (w == 0.0) continue;
-    double v = 0.0;
-    const double* src = j.partial + (int64_t)slot * j.n_wave;
-    for (int64_t k = threadIdx.x; k < j.n_wave; k += kBlock) v += src[k];
-    v = wave_sum(v);
-    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = v;
+  for (int base = 0; base < j.n_slot; base += kBlock) {
+    const int my = base + threadIdx.x;
+    __syncthreads();  // the previous pass's wt reads are done
+    wt[threadIdx.x] = my < j.n_slot ? slot_weight(j, my, p) : 0.0;
     __syncthreads();
-    if (threadIdx.x == 0) {
-      double s = 0.0;
-      for (int k = 0; k < kBlock / 64; ++k) s += ws[k];
-      g += s * w;
+    const int end = min(kBlock, j.n_slot - base);
+    for (int c = 0; c < end; ++c) {
+      const double w = wt[c];  // uniform
+      if (w == 0.0) continue;
+      const double* src = j.partial + (int64_t)(base + c) * j.n_wave;
+      double v = 0.0;
+      int64_t k = threadIdx.x;
+      for (; k + 7 * kBlock < j.n_wave; k += 8 * kBlock) {
+        double x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[u] = src[k + u * kBlock];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v += x[u];
+      }
+      for (; k < j.n_wave; k += kBlock) v += src[k];
+      v = wave_sum(v);
+      if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = v;
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        double s = 0.0;
+        for (int q = 0; q < kBlock / 64; ++q) s += ws[q];
+        g += s * w;
+      }
+      __syncthreads();
     }
-    __syncthreads();
   }
   if (threadIdx.x == 0) j.grad[p] += g;
 }

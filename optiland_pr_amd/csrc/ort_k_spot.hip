@@ -65,6 +65,49 @@ __device__ inline void local_point(const SpotArgs& a, int64_t r, double& x, doub
   y = p.y;
 }
 
+// the same for a point already loaded (x, y, z)
+__device__ inline void local_xyz(const SpotArgs& a, double x, double y, double z, double& ox,
+                                 double& oy) {
+  ort::Ray p;
+  p.x = x;
+  p.y = y;
+  p.z = a.n_ops ? z : 0.0;
+  p.L = 0.0; p.M = 0.0; p.N = 0.0;
+  for (int k = 0; k < a.n_ops; ++k) ort::apply_cs_op(p, cst(a.ops)[k]);
+  ox = p.x;
+  oy = p.y;
+}
+
+// A thread's rays j0 + k * 256 (k < per_thread, j < n_pupil) of a chunk, visited in k
+// order, their loads issued four rays at a time ahead of the use (the intensity test no
+// longer gates the coordinate loads): fn(x, y) for each point with i > 0 (every point
+// when i is NULL), in the same order as the one-ray-at-a-time loop.
+template <class F>
+__device__ inline void chunk_points(const SpotArgs& a, int64_t pair, int64_t j0, F&& fn) {
+  for (int k0 = 0; k0 < a.per_thread; k0 += 4) {
+    double xs[4], ys[4], zs[4], is[4];
+    bool in[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t j = j0 + (int64_t)(k0 + u) * kSpotThreads;
+      in[u] = k0 + u < a.per_thread && j < a.n_pupil;
+      const int64_t r = pair * a.n_pupil + (in[u] ? j : 0);
+      is[u] = (in[u] && a.i) ? a.i[r] : 1.0;
+      xs[u] = in[u] ? a.x[r] : 0.0;
+      ys[u] = in[u] ? a.y[r] : 0.0;
+      zs[u] = (in[u] && a.n_ops) ? a.z[r] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (in[u] && is[u] > 0.0) {  // spot_diagram.py:425-427
+        double x, y;
+        local_xyz(a, xs[u], ys[u], zs[u], x, y);
+        fn(x, y);
+      }
+    }
+  }
+}
+
 // sums of the 3 columns of part[0 .. n) (index-strided per thread, then block_sum)
 __device__ inline void reduce_rows(const double* part, int n, double (&v)[3], double* lds) {
   v[0] = v[1] = v[2] = 0.0;
@@ -80,18 +123,11 @@ __global__ __launch_bounds__(kSpotThreads) void spot_sum_kernel(const SpotArgs a
   const int64_t pair = blockIdx.y;
   const int64_t j0 = (int64_t)blockIdx.x * a.per_thread * kSpotThreads + threadIdx.x;
   double v[3] = {0.0, 0.0, 0.0};
-  for (int k = 0; k < a.per_thread; ++k) {
-    const int64_t j = j0 + (int64_t)k * kSpotThreads;
-    if (j >= a.n_pupil) break;
-    const int64_t r = pair * a.n_pupil + j;
-    if (!a.i || a.i[r] > 0.0) {  // spot_diagram.py:425-427 (i == NULL: every point)
-      double x, y;
-      local_point(a, r, x, y);
-      v[0] += 1.0;
-      v[1] += x;
-      v[2] += y;
-    }
-  }
+  chunk_points(a, pair, j0, [&](double x, double y) {
+    v[0] += 1.0;
+    v[1] += x;
+    v[2] += y;
+  });
   __shared__ double lds[4 * 3];
   block_sum<3>(v, lds);
   if (threadIdx.x == 0) {
@@ -142,16 +178,7 @@ __global__ __launch_bounds__(kSpotThreads) void spot_dev_kernel(const SpotArgs a
   if (a.per_thread == 1) {
     if (on) add(px, py);
   } else {
-    for (int k = 0; k < a.per_thread; ++k) {
-      const int64_t j = j0 + (int64_t)k * kSpotThreads;
-      if (j >= a.n_pupil) break;
-      const int64_t r = pair * a.n_pupil + j;
-      if (!a.i || a.i[r] > 0.0) {
-        double x, y;
-        local_point(a, r, x, y);
-        add(x, y);
-      }
-    }
+    chunk_points(a, pair, j0, add);
   }
   double v[1] = {s};
   block_sum<1>(v, lds);

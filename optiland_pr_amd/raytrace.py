@@ -376,19 +376,26 @@ def _run_device(dlens: DeviceLens, launch, n_rays, group_len, keys, need_status)
     n_groups = len(keys)
     R = device_rounds(dlens)
     kk = tuple(keys)
-    sched_dev = dlens._dev_sched.get(kk)
-    if sched_dev is None:
-        sched_dev = torch.from_numpy(dlens.initial_schedule(keys).reshape(-1).copy()).to(dev)
-        dlens._dev_sched[kk] = sched_dev
     nb = n_groups * S * _abi.NEWTON_STAT.itemsize
-    bufs = dlens._async_bufs.get((n_groups, R))
+    bufs = dlens._async_bufs.get((kk, R))
     if bufs is None:
         stats = torch.empty((R + 1, nb), dtype=torch.uint8, device=dev)
-        small = torch.zeros(2 * R + 2, dtype=torch.int32, device=dev)  # flags, statuses
+        # flags [R + 1], statuses [R + 1], then the schedule the rounds settle: one buffer,
+        # so one device-to-host copy per call reads all three
+        small = torch.zeros(2 * R + 2 + n_groups * S, dtype=torch.int32, device=dev)
         bufs = (stats, small)
-        dlens._async_bufs[(n_groups, R)] = bufs
+        dlens._async_bufs[(kk, R)] = bufs
     stats, small = bufs
-    flags, status = small[:R + 1], small[R + 1:]
+    sched_dev = small[2 * R + 2:]
+    prev = dlens._dev_sched.get(kk)
+    if prev is None or prev.data_ptr() != sched_dev.data_ptr():
+        # (re-)seed: the device schedule of another round count, or the host's cache
+        # (after a host-verified trace dropped the device copy)
+        init = prev if prev is not None else torch.from_numpy(
+            dlens.initial_schedule(keys).reshape(-1).copy())
+        sched_dev.copy_(init)
+        dlens._dev_sched[kk] = sched_dev
+    flags, status = small[:R + 1], small[R + 1:2 * R + 2]
     stream = _stream_handle()
     for r in range(R + 1):
         if r > 0:
@@ -405,8 +412,7 @@ def _run_device(dlens: DeviceLens, launch, n_rays, group_len, keys, need_status)
                               _ptr(flags[R - 1]), _ptr(flags[R]), None, None, stream)
     _native.check(rc, "ort_newton_fixup")
     host = torch.empty(2 * R + 2 + n_groups * S, dtype=torch.int32, pin_memory=True)
-    host[:2 * R + 2].copy_(small, non_blocking=True)
-    host[2 * R + 2:].copy_(sched_dev, non_blocking=True)
+    host.copy_(small, non_blocking=True)
     ev = torch.cuda.Event()
     ev.record(torch.cuda.current_stream())
     dlens.pending.append(dict(event=ev, host=host, keys=list(keys), status=need_status,

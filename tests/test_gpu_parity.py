@@ -520,3 +520,22 @@ def test_unknown_apodization_kind_raises(torch):
     dl.apod.view(torch.int32)[0] = 99  # the uploaded record's kind
     with pytest.raises(ValueError, match="apodization"):
         lens.trace(0.0, 1.0, 0.587, num_rays=8, distribution="uniform")
+
+
+@pytest.mark.parametrize("name", ["apod_gaussian", "apod_tukey"])
+def test_apodized_records_carry_the_pupil_factor(torch, name, golden_index):
+    """with records on, the closed-form kernel's per-surface intensity
+    rows of an apodized lens carry the pupil factor (ray_generator.py:91-95 starts the
+    rays apodized). The image surface's record equals the reference's image-plane rays
+    (x, y bit-exact, i rel 1e-12), and it is the stored output intensity exactly."""
+    meta = golden_index[name]
+    dl, g, got, rec, _ = gpu_trace_case(torch, name, meta, record=True)
+    n_p = meta["n_pupil"]
+    n_pairs = len(meta["fields"]) * len(meta["wavelengths"])
+    recs = rec.view(dl.table.n_rec, 8, n_pairs * n_p).cpu().numpy()
+    last = list(dl.table.rec_surfaces).index(max(dl.table.rec_surfaces))
+    np.testing.assert_array_equal(recs[last, 0], g["x"])
+    np.testing.assert_array_equal(recs[last, 1], g["y"])
+    np.testing.assert_allclose(recs[last, 6], g["i"], rtol=1e-12)
+    np.testing.assert_array_equal(recs[last, 6], np.asarray(got["i"]))
+    assert np.any(recs[last, 6] < 1.0)  # the pupil factor is really there

@@ -10,7 +10,7 @@ run bench_c1 300 python3 bench.py --config 1 --steps 200 --warmup 5
 run bench_c2 300 python3 bench.py --config 2 --steps 50 --warmup 5
 run bench_c3 400 python3 bench.py --config 3 --steps 10 --warmup 2
 run bench_c4 400 python3 bench.py --config 4 --steps 10 --warmup 2
-run bench_c5 400 python3 bench.py --config 5 --steps 10 --warmup 2
+run bench_c5 400 python3 bench.py --config 5 --steps 100 --warmup 5
 if [ "${1:-}" = prof ]; then
   cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
   for c in 1 3 4 5; do
