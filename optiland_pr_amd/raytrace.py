@@ -160,6 +160,7 @@ class DeviceLens:
         self.last_schedule_dev = None  # device int32 [n_groups * S] (device-verified launches)
         self._dev_sched: dict = {}     # keys -> the device-resident schedule (device mode)
         self._async_bufs: dict = {}
+        self._async_plans: dict = {}  # (keys, rounds) -> the rounds' launch arguments
         self.pending: list = []        # device-verified launches whose flags are unread
 
     def resident(self, slot, arr):
@@ -395,21 +396,34 @@ def _run_device(dlens: DeviceLens, launch, n_rays, group_len, keys, need_status)
             dlens.initial_schedule(keys).reshape(-1).copy())
         sched_dev.copy_(init)
         dlens._dev_sched[kk] = sched_dev
-    flags, status = small[:R + 1], small[R + 1:2 * R + 2]
+    plan = dlens._async_plans.get((kk, R))
+    if plan is None:  # the rounds' argument structs, built once per buffer set
+        flags, status = small[:R + 1], small[R + 1:2 * R + 2]
+        rounds = []
+        for r in range(R + 1):
+            fix = None
+            if r > 0:
+                fix = (_ptr(stats[r - 1]), _ptr(sched_dev),
+                       _ptr(None if r == 1 else flags[r - 2]), _ptr(flags[r - 1]),
+                       _ptr(stats[r]), _ptr(status[r]))
+            opt = _native.ort_options(_abi.NEWTON_SCHEDULE, 0, sched_dev.data_ptr(), 0,
+                                      0 if r == 0 else _abi.OPT_NO_INIT,
+                                      None if r == 0 else flags[r - 1].data_ptr())
+            rounds.append((fix, opt, stats[r], status[r]))
+        final = (_ptr(stats[R]), _ptr(sched_dev), _ptr(flags[R - 1]), _ptr(flags[R]))
+        plan = (rounds, final)
+        dlens._async_plans[(kk, R)] = plan
+    rounds, final = plan
     stream = _stream_handle()
-    for r in range(R + 1):
-        if r > 0:
-            prev = None if r == 1 else flags[r - 2]
-            rc = lib.ort_newton_fixup(C.byref(dlens.c), n_groups, _ptr(stats[r - 1]), 0,
-                                      _ptr(sched_dev), _ptr(prev), _ptr(flags[r - 1]),
-                                      _ptr(stats[r]), _ptr(status[r]), stream)
+    lens_c = C.byref(dlens.c)
+    for fix, opt, st, stt in rounds:
+        if fix is not None:
+            rc = lib.ort_newton_fixup(lens_c, n_groups, fix[0], 0, fix[1], fix[2], fix[3],
+                                      fix[4], fix[5], stream)
             _native.check(rc, "ort_newton_fixup")
-        opt = _native.ort_options(_abi.NEWTON_SCHEDULE, 0, sched_dev.data_ptr(), 0,
-                                  0 if r == 0 else _abi.OPT_NO_INIT,
-                                  None if r == 0 else flags[r - 1].data_ptr())
-        launch(opt, stats[r], status[r] if need_status else None)
-    rc = lib.ort_newton_fixup(C.byref(dlens.c), n_groups, _ptr(stats[R]), 0, _ptr(sched_dev),
-                              _ptr(flags[R - 1]), _ptr(flags[R]), None, None, stream)
+        launch(opt, st, stt if need_status else None)
+    rc = lib.ort_newton_fixup(lens_c, n_groups, final[0], 0, final[1], final[2], final[3],
+                              None, None, stream)
     _native.check(rc, "ort_newton_fixup")
     host = torch.empty(2 * R + 2 + n_groups * S, dtype=torch.int32, pin_memory=True)
     host.copy_(small, non_blocking=True)
@@ -530,13 +544,14 @@ def trace_pupil(dlens: DeviceLens, segments, px, py, out: RealRays, n_rays,
                               seg_dev.data_ptr())
     batch.apod = _addr(dlens.apod)
     out_c = out.c_struct()
+    stream = _stream_handle()  # one stream for all the launches of this call
+    args = (C.byref(dlens.c), _ptr(px), _ptr(py), C.byref(out_c), C.byref(batch))
+    rec_p, tape_p = _ptr(rec), _addr(tape)
 
     def launch(opt, stats, status):
         opt.start_surface = start_surface
-        opt.tape = _addr(tape)
-        rc = lib.ort_trace_pupil(C.byref(dlens.c), _ptr(px), _ptr(py), C.byref(out_c),
-                                 C.byref(batch), C.byref(opt), _ptr(rec), _ptr(stats),
-                                 _ptr(status), _stream_handle())
+        opt.tape = tape_p
+        rc = lib.ort_trace_pupil(*args, C.byref(opt), rec_p, _ptr(stats), _ptr(status), stream)
         _native.check(rc, "ort_trace_pupil")
 
     _run(dlens, launch, n_rays, group_len, list(keys), newton_mode)
