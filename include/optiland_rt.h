@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define ORT_ABI_VERSION 13
+#define ORT_ABI_VERSION 14
 #define ORT_MAX_SURFACES 64
 
 /* ---- geometry kinds ----------------------------------- */
@@ -418,7 +418,21 @@ typedef struct ort_options {
    * its distance t and the Newton iterates before the last four updates), so the
    * backward (ort_vjp_params.tape) runs the reverse sweep only */
   double* tape;
+  /* Verify-and-re-trace (ABI v14; nullable): with verify_stats set, the launch first
+   * applies ort_newton_fixup's rule to verify_stats (the ort_newton_stat of the launch that
+   * ran *sched) -- every workgroup derives the same decision -- writes the decision to
+   * *verify_flag and the schedule to sched_out (device int32 [n_groups][n_surfaces], not
+   * sched), and traces on the corrected schedule only when the decision is 1; a
+   * verify_prev_flag (nullable) other than 1 is passed on to *verify_flag and nothing is
+   * traced. One launch in place of ort_newton_fixup + a run_if re-launch. Needs a lens
+   * with Newton surfaces, ORT_NEWTON_SCHEDULE, ORT_OPT_NO_INIT (newton_stat / status
+   * initialised by the caller) and n_groups * n_surfaces <= ORT_VERIFY_MAX_SCHED. */
+  const ort_newton_stat* verify_stats;
+  const int32_t* verify_prev_flag;
+  int32_t* verify_flag;
+  int32_t* sched_out;
 } ort_options;
+#define ORT_VERIFY_MAX_SCHED 1024
 enum ort_option_flags { ORT_OPT_NO_INIT = 1 };
 
 /* status bits written with atomicOr into *status (device int32) */

@@ -94,6 +94,10 @@ class ort_options(C.Structure):
         ("flags", C.c_int32),
         ("run_if", C.c_void_p),
         ("tape", C.c_void_p),
+        ("verify_stats", C.c_void_p),
+        ("verify_prev_flag", C.c_void_p),
+        ("verify_flag", C.c_void_p),
+        ("sched_out", C.c_void_p),
     ]
 
 

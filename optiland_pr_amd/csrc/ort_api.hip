@@ -23,6 +23,7 @@ int launch_geom(const ort_lens* lens, int32_t surface, int64_t n, const ort_rays
   b.group_len = n;  // one reference call: the Newton stop rule spans all n rays
   KArgs a{};
   uint32_t feat = 0;
+  if (opt && opt->verify_stats) return ORT_ERR_ARG;  // trace launches only
   int rc = fill_args(a, lens, &b, opt ? opt : &dflt, nullptr, stats, status, feat);
   if (rc) return rc;
   if (rays) a.in = *rays;
@@ -107,6 +108,17 @@ int fill_args(KArgs& a, const ort_lens* lens, const ort_batch* batch, const ort_
   if (lens->frame_flags & ORT_LENS_AXIAL) feat |= F_AXIAL;
   if (opt->newton_mode != ORT_NEWTON_SCHEDULE && opt->newton_mode != ORT_NEWTON_WAVE)
     return ORT_ERR_ARG;
+  a.vstats = opt->verify_stats;
+  a.vprev = opt->verify_prev_flag;
+  a.vflag = opt->verify_flag;
+  a.sched_out = opt->sched_out;
+  if (opt->verify_stats) {  // verify-and-re-trace (see ort_options)
+    const int64_t ng = (batch->n_rays + batch->group_len - 1) / batch->group_len;
+    if ((feat & F_KM) == 0 || opt->newton_mode != ORT_NEWTON_SCHEDULE || !opt->sched ||
+        !opt->verify_flag || !opt->sched_out || !(opt->flags & ORT_OPT_NO_INIT) ||
+        opt->run_if || ng * (int64_t)lens->n_surfaces > ORT_VERIFY_MAX_SCHED)
+      return ORT_ERR_ARG;
+  }
   return ORT_OK;
 }
 
@@ -297,6 +309,7 @@ static int vjp_run(const ort_lens* lens, const double* px, const double* py,
   }
   KArgs a{};
   uint32_t feat = 0;
+  if (opt && opt->verify_stats) return ORT_ERR_ARG;  // trace launches only
   int rc = fill_args(a, lens, batch, opt, nullptr, nullptr, nullptr, feat);
   if (rc) return rc;
   if (opt->newton_mode != ORT_NEWTON_SCHEDULE) return ORT_ERR_ARG;

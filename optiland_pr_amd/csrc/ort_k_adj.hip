@@ -84,82 +84,23 @@ int adj_run(const KArgs& a, AArgs j, int32_t* need_ws, int tangents, uint32_t km
 }
 
 // ---- device-side Newton schedule check (ort_newton_fixup) ---------------------------
-// The host's DeviceLens.verify (raytrace.py) per (group, Newton surface), one thread per
-// group: the stop rule of newton_raphson.py:140-149 (grid_sag.py:108-140: index >= 1)
-// read from the conv_mask window and last_bad of the launch that ran `sched`. Only the
-// first wrong surface of a group is corrected (the later surfaces' statistics depend on
-// it). code: 0 right, 1 corrected (re-run), 2 the window cannot decide (host).
+// One workgroup: newton_decide (ort_kernels.h) on the global schedule, the code to *flag,
+// and for a re-launch the next launch's statistics and status initialised here (instead of
+// two memsets).
 __global__ __launch_bounds__(kBlock) void newton_fixup_kernel(
     const ort_surface* surf, int32_t n_surf, int64_t n_groups, const ort_newton_stat* stats,
     int32_t conv_base, int32_t* sched, const int32_t* prev_flag, int32_t* flag,
     ort_newton_stat* next_stats, int32_t* next_status) {
   __shared__ int32_t codes[kBlock / 64];
-  __shared__ int32_t final_code;
   if (prev_flag && *prev_flag != 1) {  // the launch these stats belong to did not run:
     if (threadIdx.x == 0) *flag = *prev_flag;  // settled (0) or undecidable (2) stays so
     return;
   }
-  constexpr int W = 128;  // stop indices per conv_mask window
-  int code = 0;
-  for (int64_t g = threadIdx.x; g < n_groups; g += kBlock) {
-    for (int s = 0; s < n_surf; ++s) {
-      const ort_surface sf = surf[s];
-      if (sf.geometry == ORT_GEOM_PLANE || sf.geometry == ORT_GEOM_STANDARD) continue;
-      int32_t* U_p = sched + g * n_surf + s;
-      const int U = *U_p;
-      const int max_iter = sf.max_iter;
-      const int k_min = sf.geometry == ORT_GEOM_GRID_SAG ? 1 : 0;
-      if (U < k_min) {  // grid_sag.py:111-129 always makes the first update
-        *U_p = k_min;
-        code = max(code, 1);
-        break;
-      }
-      const ort_newton_stat st = stats[g * n_surf + s];
-      // first stop index k in [k_min, U) every ray passed, from the window
-      int k = -1;
-      bool undecided = false;
-      for (int i = k_min; i < U; ++i) {
-        const int b = i - conv_base;
-        if (b < 0 || b >= W) {
-          undecided = true;
-          break;
-        }
-        const uint64_t word = b < 64 ? st.conv_mask[0] : st.conv_mask[1];
-        if ((word >> (b & 63)) & 1ull) {
-          k = i;
-          break;
-        }
-      }
-      if (undecided) {
-        code = 2;
-        break;
-      }
-      if (k >= 0) {  // every ray passed before update U: the reference stops there
-        *U_p = k;
-        code = max(code, 1);
-        break;
-      }
-      if (U < max_iter && st.last_bad >= U) {  // not all passed at U: it goes on
-        *U_p = U >= 8 ? max_iter : min(max_iter, max(2 * U + 2, 8));
-        code = max(code, 1);
-        break;
-      }
-    }
-  }
-  // block max of the codes (fixed order, LDS)
-  for (int o = 32; o > 0; o >>= 1) code = max(code, __shfl_xor(code, o, 64));
-  if ((threadIdx.x & 63) == 0) codes[threadIdx.x >> 6] = code;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int c = 0;
-    for (int w = 0; w < kBlock / 64; ++w) c = max(c, codes[w]);
-    *flag = c;
-    final_code = c;
-  }
-  __syncthreads();
+  const int c = newton_decide(surf, n_surf, n_groups, stats, conv_base, sched, codes);
+  if (threadIdx.x == 0) *flag = c;
   // a re-launch follows: initialise its statistics (conv_mask all ones, last_bad and
   // max_updates -1: every byte 0xFF) and status word here, instead of two memsets
-  if (final_code == 1) {
+  if (c == 1) {
     if (next_stats) {
       const int64_t words = n_groups * n_surf * (int64_t)(sizeof(ort_newton_stat) / 8);
       uint64_t* w = reinterpret_cast<uint64_t*>(next_stats);

@@ -126,6 +126,11 @@ struct KArgs {
   // nullable: the launch is a no-op unless *run_if == 1 (ort_options.run_if)
   const int32_t* run_if;
   int32_t no_init;  // host side only: ORT_OPT_NO_INIT (skip init_outputs)
+  // verify-and-re-trace (ort_options.verify_*): the launch decides from vstats first
+  const ort_newton_stat* vstats;
+  const int32_t* vprev;
+  int32_t* vflag;
+  int32_t* sched_out;
   double* tape;     // F_TAPE: [n_surf][kTapeRows][n_rays] (ort_options.tape)
   // F_SPOT (ort_trace_spot): block b traces chunk b % spot_chunks of pair b / spot_chunks
   // (kClosedBlock rays of seg_len, the tail lanes idle) and writes the chunk's count, sum x,
@@ -326,7 +331,7 @@ __device__ inline void report_newton(const KArgs& a, int si, bool active, int64_
 template <uint32_t FEAT>
 __device__ inline double grid_distance(const KArgs& a, const ort_surface& s, int si,
                                        const ort::Ray& r, bool active, int64_t group,
-                                       bool group_uniform) {
+                                       bool group_uniform, const int32_t* sched) {
   const ort::GridView g = ort::grid_view(a.coef + s.coef_off);
   const double tol = s.tol;
   const int max_iter = s.max_iter;
@@ -343,7 +348,7 @@ __device__ inline double grid_distance(const KArgs& a, const ort_surface& s, int
       max_if_changes(&a.stats[(group_uniform ? group : 0) * a.n_surf + si].max_updates, j);
     return ort::grid_final(g, r, t);
   }
-  const int U = a.sched ? a.sched[group * a.n_surf + si] : max_iter;
+  const int U = sched ? sched[group * a.n_surf + si] : max_iter;
   ConvBits mask;
   int last_bad = -1;
   for (int j = 0;; ++j) {
@@ -374,7 +379,7 @@ __device__ inline double newton_distance(const KArgs& a, const ort_surface& s, i
                                          const ort::Ray& r, bool active, int64_t group,
                                          bool group_uniform, int& range_bits, bool& hn,
                                          double& nnx, double& nny, double& nnz,
-                                         double (&hist)[kHist]) {
+                                         double (&hist)[kHist], const int32_t* sched) {
   hn = false;
   if constexpr ((FEAT & F_TAPE) != 0) {
 #pragma unroll
@@ -382,7 +387,7 @@ __device__ inline double newton_distance(const KArgs& a, const ort_surface& s, i
   }
   if constexpr ((FEAT & ort::KM_FREE) != 0) {
     if (s.geometry == ORT_GEOM_GRID_SAG)
-      return grid_distance<FEAT>(a, s, si, r, active, group, group_uniform);
+      return grid_distance<FEAT>(a, s, si, r, active, group, group_uniform, sched);
   }
   double t = ort::distance_conic(r, s.radius, s.conic, (s.flags & ORT_SURF_RADIUS_INF) != 0);
   const double tol = s.tol;
@@ -412,7 +417,7 @@ __device__ inline double newton_distance(const KArgs& a, const ort_surface& s, i
     return t;
   }
   // ORT_NEWTON_SCHEDULE: exactly U updates, plus the check evaluation at j = U.
-  const int U = a.sched ? a.sched[group * a.n_surf + si] : max_iter;
+  const int U = sched ? sched[group * a.n_surf + si] : max_iter;
   ConvBits mask;
   int last_bad = -1;
   for (int j = 0;; ++j) {
@@ -502,9 +507,107 @@ struct TraceWaves {
 #else
 #define ORT_TRACE_OCC __attribute__((amdgpu_waves_per_eu(TraceWaves<FEAT>::value)))
 #endif
+// The device side of the host's DeviceLens.verify (raytrace.py) for one workgroup: per
+// (group, Newton surface) the stop rule of newton_raphson.py:140-149 (grid_sag.py:108-140:
+// index >= 1) read from the conv_mask window and last_bad of the launch that ran `sched`.
+// Only the first wrong surface of a group is corrected (the later surfaces' statistics
+// depend on it), in place in `sched` (memory this workgroup may write: global in
+// ort_newton_fixup, LDS in a verify-and-re-trace launch). Returns the workgroup-wide
+// code: 0 right, 1 corrected (re-run), 2 the window cannot decide (host). codes: LDS
+// [kBlock / 64]. Every thread of the workgroup must call it.
+__device__ inline int newton_decide(const ort_surface* surf, int32_t n_surf, int64_t n_groups,
+                                    const ort_newton_stat* stats, int32_t conv_base,
+                                    int32_t* sched, int32_t* codes) {
+  constexpr int W = 128;  // stop indices per conv_mask window
+  int code = 0;
+  for (int64_t g = threadIdx.x; g < n_groups; g += kBlock) {
+    for (int s = 0; s < n_surf; ++s) {
+      const ort_surface sf = surf[s];
+      if (sf.geometry == ORT_GEOM_PLANE || sf.geometry == ORT_GEOM_STANDARD) continue;
+      int32_t* U_p = sched + g * n_surf + s;
+      const int U = *U_p;
+      const int max_iter = sf.max_iter;
+      const int k_min = sf.geometry == ORT_GEOM_GRID_SAG ? 1 : 0;
+      if (U < k_min) {  // grid_sag.py:111-129 always makes the first update
+        *U_p = k_min;
+        code = max(code, 1);
+        break;
+      }
+      const ort_newton_stat st = stats[g * n_surf + s];
+      // first stop index k in [k_min, U) every ray passed, from the window
+      int k = -1;
+      bool undecided = false;
+      for (int i = k_min; i < U; ++i) {
+        const int b = i - conv_base;
+        if (b < 0 || b >= W) {
+          undecided = true;
+          break;
+        }
+        const uint64_t word = b < 64 ? st.conv_mask[0] : st.conv_mask[1];
+        if ((word >> (b & 63)) & 1ull) {
+          k = i;
+          break;
+        }
+      }
+      if (undecided) {
+        code = 2;
+        break;
+      }
+      if (k >= 0) {  // every ray passed before update U: the reference stops there
+        *U_p = k;
+        code = max(code, 1);
+        break;
+      }
+      if (U < max_iter && st.last_bad >= U) {  // not all passed at U: it goes on
+        *U_p = U >= 8 ? max_iter : min(max_iter, max(2 * U + 2, 8));
+        code = max(code, 1);
+        break;
+      }
+    }
+  }
+  // workgroup max of the codes (fixed order, LDS)
+  for (int o = 32; o > 0; o >>= 1) code = max(code, __shfl_xor(code, o, 64));
+  if ((threadIdx.x & 63) == 0) codes[threadIdx.x >> 6] = code;
+  __syncthreads();
+  int c = 0;
+  for (int w = 0; w < kBlock / 64; ++w) c = max(c, codes[w]);
+  __syncthreads();  // codes free for reuse
+  return c;
+}
+
 template <uint32_t FEAT>
 __global__ __launch_bounds__(kBlock) ORT_TRACE_OCC void trace_kernel(const KArgs a) {
   if (a.run_if && *cst(a.run_if) != 1) return;  // a device-side re-trace that is not needed
+  // verify-and-re-trace (ort_options.verify_*): every workgroup derives the decision of
+  // ort_newton_fixup from the previous launch's statistics into its own copy of the
+  // schedule, workgroup 0 publishes it (verify_flag, sched_out), and the rays are traced
+  // on that copy only when the schedule was corrected
+  const int32_t* sched = a.sched;
+  __shared__ int32_t vsched[ORT_VERIFY_MAX_SCHED];
+  __shared__ int32_t vcodes[kBlock / 64];
+  if constexpr ((FEAT & F_KM) != 0) {
+    if (a.vstats) {
+      const int prev = a.vprev ? *a.vprev : 1;
+      const int64_t ng = (a.n_rays + a.group_len - 1) / a.group_len;
+      const int nsch = (int)ng * a.n_surf;  // <= ORT_VERIFY_MAX_SCHED (host-checked)
+      if (prev != 1) {  // the previous launch did not run: nothing to verify
+        if (blockIdx.x == 0) {
+          for (int k = threadIdx.x; k < nsch; k += kBlock) a.sched_out[k] = a.sched[k];
+          if (threadIdx.x == 0) *a.vflag = prev;
+        }
+        return;
+      }
+      for (int k = threadIdx.x; k < nsch; k += kBlock) vsched[k] = a.sched[k];
+      __syncthreads();
+      const int c = newton_decide(a.surf, a.n_surf, ng, a.vstats, a.conv_base, vsched, vcodes);
+      if (blockIdx.x == 0) {
+        for (int k = threadIdx.x; k < nsch; k += kBlock) a.sched_out[k] = vsched[k];
+        if (threadIdx.x == 0) *a.vflag = c;
+      }
+      if (c != 1) return;
+      sched = vsched;
+    }
+  }
   const int64_t rid =
       a.block_remap ? pair_major_ray(a) : (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool active = rid < a.n_rays;
@@ -575,7 +678,7 @@ __global__ __launch_bounds__(kBlock) ORT_TRACE_OCC void trace_kernel(const KArgs
     } else {
       if constexpr ((FEAT & F_KM) != 0) {
         t = newton_distance<FEAT>(a, s, si, r, active, group, group_uniform, range_bits, hn,
-                                  hnx, hny, hnz, hist);
+                                  hnx, hny, hnz, hist, sched);
         if constexpr ((FEAT & F_TAPE) != 0) {
           if (active) {
 #pragma unroll
@@ -1149,7 +1252,7 @@ __global__ __launch_bounds__(kBlock) void geom_kernel(const KArgs a, const GArgs
         bool hn;
         double hnx, hny, hnz, hist[kHist];
         t = newton_distance<KM>(a, s, g.surface, r, active, 0, true, range_bits, hn, hnx, hny,
-                                hnz, hist);
+                                hnz, hist, a.sched);
       } else {
         t = __builtin_nan("");
       }

@@ -161,6 +161,7 @@ class DeviceLens:
         self._dev_sched: dict = {}     # keys -> the device-resident schedule (device mode)
         self._async_bufs: dict = {}
         self._async_plans: dict = {}  # (keys, rounds) -> the rounds' launch arguments
+        self._patch_index: dict = {}  # device-coefficient layout -> term-row indices
         self.pending: list = []        # device-verified launches whose flags are unread
 
     def resident(self, slot, arr):
@@ -185,9 +186,20 @@ class DeviceLens:
         (ort_zernike_term.c, the first double of each 32-byte row): a device-to-device
         copy ordered on the current stream, no host round trip."""
         rows = self.zern.view(torch.float64).view(-1, _abi.ZERNIKE_TERM.itemsize // 8)
-        for off, t in device_coeffs:
-            v = t.detach().reshape(-1).to(device=self.device, dtype=torch.float64)
-            rows[off:off + v.numel(), 0].copy_(v)
+        vals = [t.detach().reshape(-1).to(device=self.device, dtype=torch.float64)
+                for _, t in device_coeffs]
+        if len(vals) == 1:
+            rows[device_coeffs[0][0]:device_coeffs[0][0] + vals[0].numel(), 0].copy_(vals[0])
+            return
+        # several surfaces: one concatenation and one indexed copy instead of one strided
+        # copy per surface (the row indices cached per layout)
+        key = tuple((off, v.numel()) for (off, _), v in zip(device_coeffs, vals))
+        idx = self._patch_index.get(key)
+        if idx is None:
+            idx = torch.as_tensor(np.concatenate([np.arange(o, o + n) for o, n in key]),
+                                  dtype=torch.int64, device=self.device)
+            self._patch_index[key] = idx
+        rows[:, 0].index_copy_(0, idx, torch.cat(vals))
 
     # -- Newton schedule speculate / verify ---------------------------------------------
     def initial_schedule(self, keys):
@@ -349,7 +361,8 @@ def check_pending(dlens: DeviceLens, block=False):
         dlens.pending.pop(0)
         host = p["host"].numpy()
         flags, status = host[:R + 1], host[R + 1:2 * R + 2]
-        dlens.remember(p["keys"], host[2 * R + 2:].reshape(len(p["keys"]), -1))
+        a, b = p["sched"]
+        dlens.remember(p["keys"], host[a:b].reshape(len(p["keys"]), -1))
         ran = [0] + [r for r in range(1, R + 1) if flags[r - 1] == 1]
         if flags[R] != 0:
             raise NewtonScheduleError(
@@ -366,28 +379,40 @@ def check_all_pending():
             check_pending(dl, block=True)
 
 
+VERIFY_MAX_SCHED = 1024  # include/optiland_rt.h ORT_VERIFY_MAX_SCHED
+
+
 def _run_device(dlens: DeviceLens, launch, n_rays, group_len, keys, need_status):
     """The warm-schedule path of newton_mode="device": no host synchronisation. The first
-    launch runs the cached schedule; ort_newton_fixup checks it on the device and
-    device_rounds() conditional re-launches correct it; the flags, statuses and the settled
-    schedule are copied to pinned host memory and read by a later check_pending."""
+    launch runs the cached schedule; device_rounds() verify-and-re-trace launches
+    (ort_options.verify_*: each checks the previous launch's statistics with
+    ort_newton_fixup's rule in every workgroup and re-traces only on a corrected schedule)
+    settle it, and a last ort_newton_fixup checks the final launch; the flags, statuses
+    and the settled schedule are copied to pinned host memory (one copy) and read by a
+    later check_pending. Schedules larger than ORT_VERIFY_MAX_SCHED entries take the
+    two-launch rounds (ort_newton_fixup + a run_if re-launch)."""
     lib = _native.load()
     dev = dlens.device
     S = dlens.table.n_surfaces
     n_groups = len(keys)
     R = device_rounds(dlens)
     kk = tuple(keys)
-    nb = n_groups * S * _abi.NEWTON_STAT.itemsize
+    ngs = n_groups * S
+    fused = ngs <= VERIFY_MAX_SCHED
+    nb = ngs * _abi.NEWTON_STAT.itemsize
     bufs = dlens._async_bufs.get((kk, R))
     if bufs is None:
         stats = torch.empty((R + 1, nb), dtype=torch.uint8, device=dev)
-        # flags [R + 1], statuses [R + 1], then the schedule the rounds settle: one buffer,
-        # so one device-to-host copy per call reads all three
-        small = torch.zeros(2 * R + 2 + n_groups * S, dtype=torch.int32, device=dev)
-        bufs = (stats, small)
+        # flags [R + 1], statuses [R + 1], then the schedule (two slots with the fused
+        # rounds: each round reads one and publishes the other): one buffer, so one
+        # device-to-host copy per call reads all of it
+        small = torch.zeros(2 * R + 2 + (2 if fused else 1) * ngs, dtype=torch.int32,
+                            device=dev)
+        bufs = [stats, small, 0]  # [2]: the slot holding the current schedule
         dlens._async_bufs[(kk, R)] = bufs
-    stats, small = bufs
-    sched_dev = small[2 * R + 2:]
+    stats, small, cur = bufs
+    slots = [small[2 * R + 2 + k * ngs:2 * R + 2 + (k + 1) * ngs] for k in range(2 if fused else 1)]
+    sched_dev = slots[cur]
     prev = dlens._dev_sched.get(kk)
     if prev is None or prev.data_ptr() != sched_dev.data_ptr():
         # (re-)seed: the device schedule of another round count, or the host's cache
@@ -396,26 +421,44 @@ def _run_device(dlens: DeviceLens, launch, n_rays, group_len, keys, need_status)
             dlens.initial_schedule(keys).reshape(-1).copy())
         sched_dev.copy_(init)
         dlens._dev_sched[kk] = sched_dev
-    plan = dlens._async_plans.get((kk, R))
-    if plan is None:  # the rounds' argument structs, built once per buffer set
-        flags, status = small[:R + 1], small[R + 1:2 * R + 2]
-        rounds = []
-        for r in range(R + 1):
-            fix = None
-            if r > 0:
-                fix = (_ptr(stats[r - 1]), _ptr(sched_dev),
-                       _ptr(None if r == 1 else flags[r - 2]), _ptr(flags[r - 1]),
-                       _ptr(stats[r]), _ptr(status[r]))
-            opt = _native.ort_options(_abi.NEWTON_SCHEDULE, 0, sched_dev.data_ptr(), 0,
-                                      0 if r == 0 else _abi.OPT_NO_INIT,
-                                      None if r == 0 else flags[r - 1].data_ptr())
-            rounds.append((fix, opt, stats[r], status[r]))
-        final = (_ptr(stats[R]), _ptr(sched_dev), _ptr(flags[R - 1]), _ptr(flags[R]))
-        plan = (rounds, final)
-        dlens._async_plans[(kk, R)] = plan
-    rounds, final = plan
     stream = _stream_handle()
     lens_c = C.byref(dlens.c)
+    plan = dlens._async_plans.get((kk, R, cur))
+    if plan is None:  # the rounds' argument structs, built once per buffer set and slot
+        flags, status = small[:R + 1], small[R + 1:2 * R + 2]
+        rounds = []
+        if fused:
+            for r in range(R + 1):
+                src = slots[(cur + r - 1) % 2] if r > 0 else slots[cur]
+                opt = _native.ort_options(_abi.NEWTON_SCHEDULE, 0, src.data_ptr(), 0,
+                                          _abi.OPT_NO_INIT, None)
+                if r > 0:
+                    opt.verify_stats = stats[r - 1].data_ptr()
+                    opt.verify_prev_flag = None if r == 1 else flags[r - 2].data_ptr()
+                    opt.verify_flag = flags[r - 1].data_ptr()
+                    opt.sched_out = slots[(cur + r) % 2].data_ptr()
+                rounds.append((None, opt, stats[r], status[r]))
+            last = slots[(cur + R) % 2]
+        else:
+            for r in range(R + 1):
+                fix = None
+                if r > 0:
+                    fix = (_ptr(stats[r - 1]), _ptr(sched_dev),
+                           _ptr(None if r == 1 else flags[r - 2]), _ptr(flags[r - 1]),
+                           _ptr(stats[r]), _ptr(status[r]))
+                opt = _native.ort_options(_abi.NEWTON_SCHEDULE, 0, sched_dev.data_ptr(), 0,
+                                          0 if r == 0 else _abi.OPT_NO_INIT,
+                                          None if r == 0 else flags[r - 1].data_ptr())
+                rounds.append((fix, opt, stats[r], status[r]))
+            last = sched_dev
+        final = (_ptr(stats[R]), _ptr(last), _ptr(flags[R - 1]), _ptr(flags[R]))
+        plan = (rounds, final, last, (cur + R) % 2 if fused else cur,
+                small[R + 1:2 * R + 2])
+        dlens._async_plans[(kk, R, cur)] = plan
+    rounds, final, last, new_cur, statuses = plan
+    if fused:  # every round's statistics and status initialised up front (two fills)
+        stats.fill_(255)
+        statuses.zero_()
     for fix, opt, st, stt in rounds:
         if fix is not None:
             rc = lib.ort_newton_fixup(lens_c, n_groups, fix[0], 0, fix[1], fix[2], fix[3],
@@ -425,12 +468,15 @@ def _run_device(dlens: DeviceLens, launch, n_rays, group_len, keys, need_status)
     rc = lib.ort_newton_fixup(lens_c, n_groups, final[0], 0, final[1], final[2], final[3],
                               None, None, stream)
     _native.check(rc, "ort_newton_fixup")
-    host = torch.empty(2 * R + 2 + n_groups * S, dtype=torch.int32, pin_memory=True)
+    bufs[2] = new_cur
+    dlens._dev_sched[kk] = last
+    host = torch.empty(small.numel(), dtype=torch.int32, pin_memory=True)
     host.copy_(small, non_blocking=True)
     ev = torch.cuda.Event()
     ev.record(torch.cuda.current_stream())
+    off = 2 * R + 2 + (new_cur * ngs if fused else 0)
     dlens.pending.append(dict(event=ev, host=host, keys=list(keys), status=need_status,
-                              rounds=R))
+                              rounds=R, sched=(off, off + ngs)))
     global _PENDING_LENSES
     if _PENDING_LENSES is None:
         import weakref
@@ -438,7 +484,7 @@ def _run_device(dlens: DeviceLens, launch, n_rays, group_len, keys, need_status)
         _PENDING_LENSES = weakref.WeakSet()
     _PENDING_LENSES.add(dlens)
     dlens.last_schedule = None
-    dlens.last_schedule_dev = sched_dev
+    dlens.last_schedule_dev = last
 
 
 def _run(dlens: DeviceLens, launch, n_rays, group_len, keys, newton_mode="reference",
@@ -763,7 +809,9 @@ class RealRayTracer:
             self._record(dlens, tmp, rec, n, segs, px, py, n_p)
         # queued ahead of the trace: the host waits on the trace's Newton check, and what
         # it issues after that is on the step's critical path
-        w = torch.full((n,), float(wavelength), dtype=torch.float64, device=dlens.device)
+        # one wavelength for every ray: a broadcast view (no 8 B/ray fill per step)
+        w = torch.full((1,), float(wavelength), dtype=torch.float64,
+                       device=dlens.device).expand(n)
         outs = autodiff.trace_pupil_grad(self.optic, dlens, seg_dev, px, py, n, n_p,
                                          wavelength, keys, newton_mode)
         out = RealRays.__new__(RealRays)
