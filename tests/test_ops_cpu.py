@@ -113,3 +113,18 @@ def test_seq_vjp_entry_declared():
     assert re.search(r"int ort_trace_spot\(", text)
     m = re.search(r"#define ORT_ABI_VERSION (\d+)", text)
     assert m and int(m.group(1)) == _abi.ABI_VERSION >= 13
+
+
+def test_verify_max_sched_matches_header():
+    import re
+
+    from optiland_pr_amd import raytrace
+    from tests.conftest import REPO
+
+    with open(f"{REPO}/include/optiland_rt.h") as f:
+        text = f.read()
+    m = re.search(r"#define ORT_VERIFY_MAX_SCHED (\d+)", text)
+    assert m and int(m.group(1)) == raytrace.VERIFY_MAX_SCHED
+    for field in ("verify_stats", "verify_prev_flag", "verify_flag", "sched_out"):
+        assert re.search(rf"\b{field};", text)
+        assert field in [f for f, _ in __import__("optiland_pr_amd._native", fromlist=["x"]).ort_options._fields_]
