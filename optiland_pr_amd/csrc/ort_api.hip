@@ -115,7 +115,8 @@ int fill_args(KArgs& a, const ort_lens* lens, const ort_batch* batch, const ort_
   if (opt->verify_stats) {  // verify-and-re-trace (see ort_options)
     const int64_t ng = (batch->n_rays + batch->group_len - 1) / batch->group_len;
     if ((feat & F_KM) == 0 || opt->newton_mode != ORT_NEWTON_SCHEDULE || !opt->sched ||
-        !opt->verify_flag || !opt->sched_out || !(opt->flags & ORT_OPT_NO_INIT) ||
+        !opt->verify_flag || !opt->sched_out || opt->sched_out == opt->sched ||
+        !(opt->flags & ORT_OPT_NO_INIT) ||
         opt->run_if || ng * (int64_t)lens->n_surfaces > ORT_VERIFY_MAX_SCHED)
       return ORT_ERR_ARG;
   }
