@@ -518,7 +518,8 @@ typedef struct ort_vjp_params {
   const double* surf_tangent;  /* [n_param][n_surfaces][3]                              */
   const double* final_tangent; /* [n_param]                                             */
   int32_t n_zern;              /* entries of zern_param (terms of lens->zern)           */
-  int32_t reserved;
+  int32_t grad_init;           /* 1: grad is overwritten with the VJP (no zeroing first; */
+                               /* v14, formerly reserved = 0: accumulate)               */
   void* workspace;             /* ADJOINT: device scratch (tape + wave partials)        */
   int64_t workspace_size;      /* bytes available at workspace                          */
   /* ADJOINT, nullable: device int32 [n_slot] (n_slot = 3 n_surfaces + n_zern + 1, slot
@@ -547,7 +548,7 @@ int64_t ort_vjp_tape_size(const ort_lens* lens, const ort_batch* batch);
  * counts as zero). opt must be ORT_NEWTON_SCHEDULE with the schedule the verified primal
  * trace ran (see ort_vjp_mode for how Newton surfaces are differentiated). grad is
  * accumulated (atomics for UNROLLED, a deterministic reduction for ADJOINT): zero it
- * first. Ray generation is not differentiated (the reference builds
+ * first, or set params->grad_init = 1 to have it overwritten. Ray generation is not differentiated (the reference builds
  * its paraxial quantities from detached copies, surface_group.py:143-153). Replaces
  * reverse-mode torch autograd through the trace (SurfaceGroup.trace under the torch
  * backend, driven by optimization/optimizer/torch/base.py:95-154; variables written by

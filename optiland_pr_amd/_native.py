@@ -53,7 +53,7 @@ class ort_batch(C.Structure):
     ]
 
 
-class ort_vjp_params(C.Structure):
+class ort_vjp_params(C.Structure):  # field 7 ("grad_init") was "reserved" before v14
     _fields_ = [
         ("n_param", C.c_int32),
         ("mode", C.c_int32),
@@ -61,7 +61,7 @@ class ort_vjp_params(C.Structure):
         ("surf_tangent", C.c_void_p),
         ("final_tangent", C.c_void_p),
         ("n_zern", C.c_int32),
-        ("reserved", C.c_int32),
+        ("grad_init", C.c_int32),
         ("workspace", C.c_void_p),
         ("workspace_size", C.c_int64),
         ("slot_need", C.c_void_p),

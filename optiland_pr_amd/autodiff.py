@@ -149,9 +149,10 @@ def _workspace(device, nbytes):
 
 
 def vjp(dlens, seg_dev, px, py, n, seg_len, sched_dev, tables, n_param, cot, grad,
-        pupil_per_ray=False, mode=None, tape=None, primal=None):
-    """grad += J^T cot through ort_trace_pupil_vjp. tables: device tensors
-    (zern_param, surf_tangent, final_tangent), each possibly None; cot: 8 tensors / None."""
+        pupil_per_ray=False, mode=None, tape=None, primal=None, overwrite=False):
+    """grad += J^T cot through ort_trace_pupil_vjp (overwrite: grad = J^T cot, grad need
+    not be initialised). tables: device tensors (zern_param, surf_tangent,
+    final_tangent), each possibly None; cot: 8 tensors / None."""
     from .raytrace import _ptr, _stream_handle
 
     if np.any(dlens.table.surfaces["geometry"] == _abi.GEOM_GRID_SAG):
@@ -170,8 +171,8 @@ def vjp(dlens, seg_dev, px, py, n, seg_len, sched_dev, tables, n_param, cot, gra
     need = tables[3] if len(tables) > 3 else None  # ort_vjp_params.slot_need (resident)
     mode = vjp_mode(dlens.table) if mode is None else mode
     params = _native.ort_vjp_params(int(n_param), int(mode), _ptr(zp).value, _ptr(st).value,
-                                    _ptr(ft).value, 0 if zp is None else int(zp.numel()), 0,
-                                    None, 0, _ptr(need).value)
+                                    _ptr(ft).value, 0 if zp is None else int(zp.numel()),
+                                    int(bool(overwrite)), None, 0, _ptr(need).value)
     if tape is not None and mode == _abi.VJP_ADJOINT:
         # the forward wrote the tape (ort_options.tape): reverse sweep only, the final
         # state read from the forward's outputs

@@ -62,7 +62,8 @@ struct AArgs {
                             // earlier surfaces' slots are never written)
   int32_t tape_ready;       // the primal trace wrote the tape (F_TAPE): reverse sweep only,
   ort_rays primal;          // the final ray state read from its outputs (L, M, N, i)
-  double* grad;             // [n_param], accumulated
+  double* grad;             // [n_param], accumulated (grad_store: overwritten)
+  int32_t grad_store;
 };
 
 // d(slot) / d(parameter p)

@@ -300,8 +300,15 @@ static int vjp_run(const ort_lens* lens, const double* px, const double* py,
   const int32_t n_param = params->n_param;
   const bool want_in = grad_in && (grad_in->x || grad_in->y || grad_in->z || grad_in->L ||
                                    grad_in->M || grad_in->N || grad_in->i || grad_in->opd);
-  if (batch->n_rays == 0 || (n_param == 0 && !want_in)) return ORT_OK;
   if (n_param > 0 && !grad) return ORT_ERR_ARG;
+  if (batch->n_rays == 0 || (n_param == 0 && !want_in)) {
+    // nothing to trace: an overwritten gradient is zero
+    if (params->grad_init && n_param > 0 &&
+        hipMemsetAsync(grad, 0, (size_t)n_param * sizeof(double), (hipStream_t)stream) !=
+            hipSuccess)
+      return ORT_ERR_LAUNCH;
+    return ORT_OK;
+  }
   if (rec_cotangent && !rec) return ORT_ERR_ARG;  // intensity rows weight the absorption
   if (resident) {
     if (!rays_in) return ORT_ERR_ARG;
@@ -359,6 +366,7 @@ static int vjp_run(const ort_lens* lens, const double* px, const double* py,
     aj.need = params->slot_need;  // NULL: adj_run derives it into the workspace
     aj.zero_partials = opt->start_surface > 0;
     aj.grad = grad;
+    aj.grad_store = params->grad_init != 0;
     // radius / conic tangents need duals seeded on them too
     return adj_run(a, aj, (int32_t*)(w + L.need), params->surf_tangent ? 4 : 2, km, resident,
                    blocks, s);
@@ -373,6 +381,9 @@ static int vjp_run(const ort_lens* lens, const double* px, const double* py,
   j.cot = *cotangent;
   j.rec_cot = rec_cotangent;
   j.grad = grad;
+  if (params->grad_init &&
+      hipMemsetAsync(grad, 0, (size_t)n_param * sizeof(double), s) != hipSuccess)
+    return ORT_ERR_LAUNCH;
   for (int p0 = 0; p0 < n_param;) {
     const int left = n_param - p0;
     // tangents per launch: ORT_VJP_TANGENTS overrides (A/B timing)

@@ -59,7 +59,12 @@ __global__ __launch_bounds__(kBlock) void adj_param_reduce_kernel(const AArgs j)
       __syncthreads();
     }
   }
-  if (threadIdx.x == 0) j.grad[p] += g;
+  if (threadIdx.x == 0) {
+    if (j.grad_store)
+      j.grad[p] = g;
+    else
+      j.grad[p] += g;
+  }
 }
 
 int adj_run(const KArgs& a, AArgs j, int32_t* need_ws, int tangents, uint32_t km,

@@ -415,11 +415,11 @@ def _pupil_backward(ctx, *grads):
     tables = tuple(None if a is None else dl.resident(("tangent", i), a)
                    for i, a in enumerate((zp, st, ft)))
     tables = (*tables, dl.resident("tangent_need", slot_need(dl.table, zp, st, ft)))
-    g = torch.zeros(n_param, dtype=torch.float64, device=dl.device)
+    g = torch.empty(n_param, dtype=torch.float64, device=dl.device)  # overwritten
     cot = [None if gr is None else gr.to(torch.float64).contiguous() for gr in grads[:8]]
     vjp(dl, p.seg_dev, p.px, p.py, p.n, p.seg_len, sched if sched.numel() else None, tables,
         n_param, cot, g, pupil_per_ray=p.pupil_per_ray,
-        tape=p.tape, primal=primal if p.tape is not None else None)
+        tape=p.tape, primal=primal if p.tape is not None else None, overwrite=True)
     p.tape = None  # one backward per forward: release the tape
     res = []
     off = 0
