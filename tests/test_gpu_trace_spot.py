@@ -113,3 +113,13 @@ def test_newton_lens_refused(torch):
     with pytest.raises(ValueError):
         spot.trace(dl, segs, px, py, out)
 
+
+
+def test_apodized_lens(torch):
+    """The epilogue's i > 0 test and the statistics see the apodized stored intensity (the
+    pupil factor applied at the store) exactly as the separate pass reads it back."""
+    from optiland_pr_amd.samples import CookeTriplet
+
+    lens = CookeTriplet()
+    lens.set_apodization("GaussianApodization", sigma=0.6)
+    both(torch, lens, [(0.0, 0.0), (0.0, 1.0)], [0.55], "uniform", 60)
