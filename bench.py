@@ -498,6 +498,12 @@ def main():
         }
         if w.flops_per_ray is not None:
             line["roofline_fp64"] = _roofline_fp64(w, kern_ms)
+        S = w.config.get("surfaces")
+        if S:  # the reference notebook counts len(surfaces) = S + 1 per ray
+            line["reference_convention"] = {
+                "value": value * (S + 1) / S, "surfaces_counted": S + 1,
+                "note": "the same run counted as the reference's notebook does "
+                        "(object surface included, no intersection computed for it)"}
         if getattr(w, "spot", False):
             st = w.state["stats"].cpu().numpy()
             line["config"]["rms_spot_radius_mm"] = [float(v) for v in st[:, 3]]
