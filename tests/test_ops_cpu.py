@@ -128,3 +128,25 @@ def test_verify_max_sched_matches_header():
     for field in ("verify_stats", "verify_prev_flag", "verify_flag", "sched_out"):
         assert re.search(rf"\b{field};", text)
         assert field in [f for f, _ in __import__("optiland_pr_amd._native", fromlist=["x"]).ort_options._fields_]
+
+
+def test_flops_per_ray_counts_newton_schedule():
+    """bench._flops_per_ray: RT-asph (config 3) with the verified schedule of one update per
+    asphere (two sag + normal evaluations of 66 flops with 3 coefficients); None for
+    surface kinds it does not count (Zernike without a schedule)."""
+    import numpy as np
+
+    import bench
+    from optiland_pr_amd import _abi
+    from optiland_pr_amd.lowering import lower_surface_group
+    from optiland_pr_amd.samples import ReverseTelephotoAsphere, ThreeMirrorAnastigmat
+
+    t = lower_surface_group(ReverseTelephotoAsphere().surface_group, [0.4861, 0.5876, 0.6563])
+    asph = t.surfaces["geometry"] == _abi.GEOM_EVEN_ASPHERE
+    assert int(asph.sum()) == 2
+    f0 = bench._flops_per_ray(t, np.where(asph, 0, 0))
+    f1 = bench._flops_per_ray(t, np.where(asph, 1, 0))
+    assert f1 - f0 == 2 * (66 + 8)  # one more evaluation and one update per asphere
+    assert f1 == 1634
+    tma = lower_surface_group(ThreeMirrorAnastigmat().surface_group, [0.587])
+    assert bench._flops_per_ray(tma, np.zeros(tma.n_surfaces)) is None
