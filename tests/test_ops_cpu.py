@@ -150,3 +150,37 @@ def test_flops_per_ray_counts_newton_schedule():
     assert f1 == 1634
     tma = lower_surface_group(ThreeMirrorAnastigmat().surface_group, [0.587])
     assert bench._flops_per_ray(tma, np.zeros(tma.n_surfaces)) is None
+
+
+def test_segment_cache_invalidation():
+    """raytrace._cached_segments: reused for an unchanged optic, recomputed when anything
+    segment_params reads changes (fields / vignetting, aperture, stop, object, lens bytes);
+    no caching when the primary wavelength is not the traced one."""
+    import numpy as np
+
+    from optiland_pr_amd import raytrace
+    from optiland_pr_amd.lowering import pupil_scalars, segment_params
+    from optiland_pr_amd.samples import CookeTriplet
+
+    class DL:
+        fingerprint = b"lens-a"
+
+    lens = CookeTriplet()
+    wl = lens.primary_wavelength
+    Hx, Hy = np.zeros(2), np.array([0.0, 1.0])
+    a = raytrace._cached_segments(lens, DL, wl, Hx, Hy)
+    assert raytrace._cached_segments(lens, DL, wl, Hx, Hy) is a
+    EPL, EPD = pupil_scalars(lens)
+    ref = np.stack([segment_params(lens, 0.0, h, 0, EPL, EPD) for h in (0.0, 1.0)])
+    assert a.tobytes() == ref.tobytes()
+    for edit in (lambda: setattr(lens.fields.fields[-1], "vy", 0.2),
+                 lambda: setattr(lens.aperture, "value", lens.aperture.value * 1.1),
+                 lambda: setattr(lens.surface_group.surfaces[2], "is_stop",
+                                 not lens.surface_group.surfaces[2].is_stop),
+                 lambda: setattr(DL, "fingerprint", b"lens-b")):
+        edit()
+        b = raytrace._cached_segments(lens, DL, wl, Hx, Hy)
+        assert b is not a
+        a = b
+    other = wl + 0.01
+    assert raytrace._segment_key(lens, DL, other, Hx, Hy) is None
