@@ -1,5 +1,5 @@
-"""GPU: Newton schedules verified on the device (newton_mode="device", ort_newton_fixup +
-conditional re-launches; raytrace._run_device): the same schedules and bit-identical rays
+"""GPU: Newton schedules verified on the device (newton_mode="device": verify-and-re-trace
+launches, or ort_newton_fixup + conditional re-launches; raytrace._run_device): the same schedules and bit-identical rays
 as the host-verified path, a wrong cached schedule corrected on the device (too long:
 the exact stop index; too short: grown, then exact), the settled schedule written back
 to the host cache, and errors raised at the next check (check_all_pending)."""
@@ -56,12 +56,18 @@ def test_device_mode_equals_reference(torch, name):
         np.testing.assert_array_equal(again[a], ref[a], err_msg=a)
 
 
+@pytest.mark.parametrize("path", ["verify_retrace", "fixup_run_if"])
 @pytest.mark.parametrize("offset", [+5, -1, -2])
-def test_device_fixup_corrects_a_wrong_schedule(torch, offset):
+def test_device_fixup_corrects_a_wrong_schedule(torch, offset, path, monkeypatch):
     """Seed the warm cache with a wrong schedule: the device rounds settle it to the
-    reference's stop index and the rays equal the host-verified trace."""
+    reference's stop index and the rays equal the host-verified trace -- through the
+    verify-and-re-trace launches (ort_options.verify_*, one launch per round) and through
+    the two-launch rounds (ort_newton_fixup + run_if) that larger schedules take."""
     from optiland_pr_amd import raytrace
     from tests._cases import build_lens
+
+    if path == "fixup_run_if":
+        monkeypatch.setattr(raytrace, "VERIFY_MAX_SCHED", 0)
 
     ref_lens, lens = build_lens("rt_asph"), build_lens("rt_asph")
     ref = _trace(ref_lens, "reference")
