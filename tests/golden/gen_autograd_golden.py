@@ -6,7 +6,8 @@ Test infrastructure only, run in the build container (never on the GPU box):
     PYTHONPATH=tests/golden/shims:/root/reference PYTHONDONTWRITEBYTECODE=1 \
         python tests/golden/gen_autograd_golden.py
 
-Writes tests/golden/autograd_tma.npz:
+Writes tests/golden/autograd_tma.npz (and with --full, autograd_tma_1m.json: config 5's
+own 1M-ray loss and gradient, see full_size):
   rms_*      RayOperand.rms_spot_size(optic, -1, 0, 1, 32, 0.587, "uniform")
              (operand/ray.py:300-340) and d rms / d c for the coefficients of the three
              Zernike mirrors (surfaces 1-3, 10 fringe coefficients each)
@@ -134,5 +135,39 @@ def shape_params():
     np.savez_compressed(os.path.join(HERE, "autograd_cooke.npz"), **out)
 
 
+def full_size():
+    """Config 5 at its own size (VERDICT r02 item 6 for config 5): the TMA loss
+    rms_spot_size(optic, -1, 0, 1, 1M, 0.587, RandomDistribution(seed=0)) -- the bench's
+    workload -- and d rms / d c for the 30 coefficients, from the reference's torch
+    backend; the pupil points are drawn with the NumPy backend (PCG64, seed 0) as the
+    native package draws them. Writes tests/golden/autograd_tma_1m.json."""
+    import json
+    import time
+
+    from optiland.distribution import RandomDistribution
+
+    be.set_backend("numpy")
+    d = RandomDistribution(seed=0)
+    d.generate_points(1_000_000)
+    px, py = np.asarray(d.x, dtype=np.float64), np.asarray(d.y, dtype=np.float64)
+    be.set_backend("torch")
+    be.set_precision("float64")
+    d.x, d.y = torch.as_tensor(px), torch.as_tensor(py)
+    lens = gen_golden.tma("fringe")
+    leaves = _leaf_coefficients(lens)
+    t0 = time.perf_counter()
+    rms = RayOperand.rms_spot_size(lens, -1, 0.0, 1.0, 1_000_000, 0.587, d)
+    rms.backward()
+    res = dict(rms=float(rms), grad=[[float(v) for v in t.grad.numpy()] for t in leaves],
+               seconds=time.perf_counter() - t0, n=int(px.size),
+               px_sum=float(np.sum(px)), py_sum=float(np.sum(py)))
+    with open(os.path.join(HERE, "autograd_tma_1m.json"), "w") as f:
+        json.dump(res, f, indent=1)
+    print(res["rms"], res["seconds"])
+
+
 if __name__ == "__main__":
-    main()
+    if "--full" in sys.argv:
+        full_size()
+    else:
+        main()
