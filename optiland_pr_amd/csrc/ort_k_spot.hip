@@ -242,10 +242,12 @@ __global__ __launch_bounds__(kSpotThreads) void spot_final_kernel(const SpotArgs
   }
 }
 
-// pass 2 + totals. Measured and dropped: both in one block per pair for small pairs
-// (each wave summing its chunks' four 64-lane sub-chunks in block_sum's order,
-// bit-identical): 46.9 us for config 1 against 4.6 + 4.0 us -- the serial per-sub-chunk
-// load round trips of three blocks cost more than a launch.
+// pass 2 + totals. Measured and dropped: both in one workgroup per pair for small pairs
+// (each wave forming its chunks' four 64-lane sub-chunk sums in block_sum's order,
+// bit-identical to these two kernels): 4 waves with one load round trip per sub-chunk
+// 46.9 us, 16 waves with eight sub-chunks' loads in flight per wave 17.3 us, against
+// 4.6 + 4.0 us -- three workgroups (three CUs) move and reduce the 38K points slower than
+// 150 chunk workgroups plus one extra launch.
 void launch_pass2(const SpotArgs& a, int64_t pairs, int64_t chunks, hipStream_t s) {
   hipLaunchKernelGGL(spot_dev_kernel, dim3((unsigned)chunks, (unsigned)pairs), dim3(kSpotThreads),
                      0, s, a);

@@ -123,3 +123,4 @@ def test_apodized_lens(torch):
     lens = CookeTriplet()
     lens.set_apodization("GaussianApodization", sigma=0.6)
     both(torch, lens, [(0.0, 0.0), (0.0, 1.0)], [0.55], "uniform", 60)
+
