@@ -36,6 +36,8 @@ def step():
     opt.step()
 
 
+if os.environ.get("PROF_BACKWARD_MAIN_THREAD"):  # let cProfile see the backward's Python
+    torch.autograd.set_multithreading_enabled(False)
 for _ in range(5):
     step()
 torch.cuda.synchronize()
