@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define ORT_ABI_VERSION 14
+#define ORT_ABI_VERSION 15
 #define ORT_MAX_SURFACES 64
 
 /* ---- geometry kinds ----------------------------------- */
@@ -504,7 +504,9 @@ int ort_trace_pupil(const ort_lens* lens, const double* px, const double* py,
  *
  * mode ORT_VJP_UNROLLED: forward-mode tangents through the primal's exact Newton
  *   update counts (the derivative of the unrolled iteration, as torch autograd computes
- *   it); one re-trace per 4 parameters, no workspace.
+ *   it); one re-trace per 4 parameters. Needs a device workspace of
+ *   ort_vjp_workspace_size() bytes (v15: the per-block partial sums, reduced in a fixed
+ *   order -- the gradient is the same bits run to run).
  * mode ORT_VJP_ADJOINT: one reverse-mode pass whatever n_param (the intersection
  *   distance differentiated through its implicit equation; equals the unrolled
  *   derivative to the Newton residual when the Newton slope is the sag's derivative --
@@ -520,7 +522,8 @@ typedef struct ort_vjp_params {
   int32_t n_zern;              /* entries of zern_param (terms of lens->zern)           */
   int32_t grad_init;           /* 1: grad is overwritten with the VJP (no zeroing first; */
                                /* v14, formerly reserved = 0: accumulate)               */
-  void* workspace;             /* ADJOINT: device scratch (tape + wave partials)        */
+  void* workspace;             /* device scratch (ADJOINT: tape + wave partials;         */
+                               /* UNROLLED: block partials)                             */
   int64_t workspace_size;      /* bytes available at workspace                          */
   /* ADJOINT, nullable: device int32 [n_slot] (n_slot = 3 n_surfaces + n_zern + 1, slot
    * order: radius, conic, vertex z of each surface, the Zernike terms, the final
@@ -535,8 +538,8 @@ typedef struct ort_vjp_params {
   ort_rays primal;
 } ort_vjp_params;
 
-/* Workspace bytes ORT_VJP_ADJOINT needs for this lens, batch and parameter set (without
- * the tape when params->tape is set). */
+/* Workspace bytes params->mode needs for this lens, batch and parameter set (ADJOINT:
+ * without the tape when params->tape is set). */
 int64_t ort_vjp_workspace_size(const ort_lens* lens, const ort_batch* batch,
                                const ort_vjp_params* params);
 /* Bytes of the adjoint tape of one trace (ort_options.tape, ort_vjp_params.tape). */
@@ -547,8 +550,8 @@ int64_t ort_vjp_tape_size(const ort_lens* lens, const ort_batch* batch);
  * for the output fields f of rays_out (x, y, z, L, M, N, i, opd; a NULL cotangent field
  * counts as zero). opt must be ORT_NEWTON_SCHEDULE with the schedule the verified primal
  * trace ran (see ort_vjp_mode for how Newton surfaces are differentiated). grad is
- * accumulated (atomics for UNROLLED, a deterministic reduction for ADJOINT): zero it
- * first, or set params->grad_init = 1 to have it overwritten. Ray generation is not differentiated (the reference builds
+ * accumulated (one addition per parameter of sums formed in a fixed order, both modes:
+ * deterministic): zero it first, or set params->grad_init = 1 to have it overwritten. Ray generation is not differentiated (the reference builds
  * its paraxial quantities from detached copies, surface_group.py:143-153). Replaces
  * reverse-mode torch autograd through the trace (SurfaceGroup.trace under the torch
  * backend, driven by optimization/optimizer/torch/base.py:95-154; variables written by

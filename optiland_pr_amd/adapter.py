@@ -1,12 +1,15 @@
 """Drop-in adapter for the reference package (Optiland, `import optiland`).
 
 `install()` replaces optiland.surfaces.surface_group.SurfaceGroup.trace
-(surface_group.py:232-244) -- the seam SURVEY 8b names -- with the MI355X trace, reached
+(surface_group.py:232-244) -- the seam SURVEY 8b names -- with the trace core, reached
 through the PyTorch custom op torch.ops.ort.trace_sequential (ops.py), when:
-  * the rays are RealRays (not Paraxial/Polarized) held as torch float64 tensors on the
-    HIP device (be.set_backend("torch"); be.set_device("cuda"); be.set_precision("float64")),
-    one wavelength or one per ray (per-ray wavelengths run the in-kernel dispersion
-    formulas, ort_batch.w),
+  * the rays are RealRays (not Paraxial/Polarized) held as float64 arrays -- torch tensors
+    on the HIP device (be.set_backend("torch"); be.set_device("cuda"):
+    the op's CUDA kernel, the MI355X trace), torch tensors on the CPU (the torch backend's
+    default device, and the reference's own test setting, tests/conftest.py:5-19: the op's
+    CPU kernel, the host build of the same core) or NumPy arrays (the numpy backend: the
+    CPU kernel on zero-copy tensor views) -- with one wavelength or one per ray (per-ray
+    wavelengths run the in-kernel dispersion formulas, ort_batch.w),
   * every traced surface is lowerable (plane / standard / even / odd asphere / Zernike /
     XY-polynomial / Chebyshev / biconic / toroidal / Forbes Q-bfs / Q-2D / grid sag
     geometry, refractive-reflective / thin-lens / phase / grating interaction without
@@ -58,6 +61,12 @@ from .materials import BaseMaterial, lower_dispersion
 
 _ORIGINAL = {}
 
+# calls served by the op per dispatch key, and calls handed to the reference's own loop
+# (Unsupported), since install() -- so a caller can see which path ran; REASONS counts the
+# fallbacks by their Unsupported message
+STATS = {"cuda": 0, "cpu": 0, "fallback": 0}
+REASONS: dict = {}
+
 
 class Unsupported(Exception):
     pass
@@ -70,10 +79,10 @@ class _RefMaterial(BaseMaterial):
         self.m = m
 
     def _calculate_n(self, w):
-        return np.asarray(_np(self.m.n(w)), dtype=np.float64) * np.ones_like(w)
+        return np.asarray(_np(self.m.n(_be_array(w))), dtype=np.float64) * np.ones_like(w)
 
     def _calculate_k(self, w):
-        return np.asarray(_np(self.m.k(w)), dtype=np.float64) * np.ones_like(w)
+        return np.asarray(_np(self.m.k(_be_array(w))), dtype=np.float64) * np.ones_like(w)
 
     def lower(self):
         m = self.m
@@ -81,8 +90,9 @@ class _RefMaterial(BaseMaterial):
             return 0, [], [], [], _f(m.index), _f(m.absorp)
         if type(m).__name__ == "AbbeMaterial":  # abbe.py: polyval(p, w)
             return _abi.MAT_ABBE, [float(v) for v in np.ravel(_np(m._p))], [], [], 0.0, 0.0
-        return lower_dispersion(m._n_formula, m.coefficients, m._k_wavelength, m._k,
-                                getattr(m, "_n_wavelength", None), getattr(m, "_n", None))
+        opt = [getattr(m, a, None) for a in ("_n_wavelength", "_n")]
+        return lower_dispersion(m._n_formula, _np(m.coefficients), _np(m._k_wavelength),
+                                _np(m._k), *(None if v is None else _np(v) for v in opt))
 
     def key(self):
         # same dedup keys as the native materials (materials.py), so tables match
@@ -99,6 +109,21 @@ class _RefMaterial(BaseMaterial):
 
             return ("glass", fn.split("database" + os.sep)[-1])
         return ("ref", id(m))
+
+
+def _be_array(w):
+    """A NumPy wavelength array as the reference's active backend holds arrays (the
+    material code calls be.* on it: a torch tensor under the torch backend)."""
+    try:
+        import optiland.backend as be
+
+        if be.get_backend() != "numpy":
+            import torch
+
+            return torch.as_tensor(w, dtype=torch.float64)
+    except ImportError:  # pragma: no cover - not running inside the reference
+        pass
+    return w
 
 
 def _np(v):
@@ -253,7 +278,9 @@ def install():
     def trace(self, rays, skip=0):
         try:
             return _trace_on_mi355x(self, rays, skip)
-        except Unsupported:
+        except Unsupported as e:
+            STATS["fallback"] += 1
+            REASONS[str(e)] = REASONS.get(str(e), 0) + 1
             return _ORIGINAL["trace"](self, rays, skip)
 
     cls.trace = trace
@@ -270,7 +297,8 @@ def uninstall():
 # geometries whose radius / conic the derivative kernels seed (the conic base of
 # standard.py and of the Newton geometries built on it)
 _RK_GEOMETRIES = ("StandardGeometry", "EvenAsphere", "OddAsphere", "ZernikePolynomialGeometry",
-                  "PolynomialGeometry", "ChebyshevPolynomialGeometry")
+                  "PolynomialGeometry", "ChebyshevPolynomialGeometry", "ForbesQbfsGeometry",
+                  "ForbesQ2dGeometry")
 
 
 def _grad_mode_on():
@@ -392,8 +420,11 @@ def _grad_params(group):
 
 
 def _device_lens(group, wavelengths, per_ray, device):
-    """Lowered + uploaded lens of a reference group, cached on it per wavelength key and
-    re-uploaded only when the lowered bytes change (Newton schedules kept across edits)."""
+    """Lowered lens of a reference group -- uploaded to HBM (DeviceLens) for device rays, in
+    host memory (host.HostLens) for CPU rays -- cached on the group per wavelength key and
+    device, and rebuilt only when the lowered bytes change (Newton schedules kept across
+    edits)."""
+    from .host import HostLens
     from .raytrace import DeviceLens
 
     table = lower_reference_group(group, wavelengths, record=True)
@@ -404,12 +435,39 @@ def _device_lens(group, wavelengths, per_ray, device):
     hit = cache.get(key)
     if hit is None or hit.fingerprint != fp:
         old = hit
-        hit = DeviceLens(table, device=device)
+        if device.type == "cpu":
+            hit = HostLens(table)
+        else:
+            hit = DeviceLens(table, device=device)
+            if old is not None and old.table.surfaces.shape == table.surfaces.shape:
+                hit.sched_cache = old.sched_cache
         hit.fingerprint = fp
-        if old is not None and old.table.surfaces.shape == table.surfaces.shape:
-            hit.sched_cache = old.sched_cache
         cache[key] = hit
     return hit
+
+
+def _ray_arrays(rays):
+    """The 8 ray fields as float64 torch tensors of one size on one device, and whether they
+    came as NumPy arrays (the numpy backend: zero-copy CPU tensor views). Raises Unsupported
+    for anything else (float32, mixed devices, scalars)."""
+    import torch
+
+    fields = [getattr(rays, a) for a in _abi.RAY_FIELDS]
+    if all(isinstance(t, np.ndarray) for t in fields):
+        if any(t.dtype != np.float64 or t.ndim != 1 for t in fields):
+            raise Unsupported("numpy rays must be 1-d float64 arrays")
+        return [torch.from_numpy(np.ascontiguousarray(t)) for t in fields], True
+    if not all(torch.is_tensor(t) for t in fields):
+        raise Unsupported("ray fields are neither all tensors nor all numpy arrays")
+    x = fields[0]
+    if x.dtype != torch.float64:
+        raise Unsupported("rays must be float64")
+    if any(t.dtype != torch.float64 or t.device != x.device or t.numel() != x.numel()
+           for t in fields):
+        raise Unsupported("ray fields of mixed sizes / devices / dtypes")
+    if x.device.type not in ("cuda", "cpu"):
+        raise Unsupported(f"rays on {x.device}")
+    return fields, False
 
 
 def _trace_on_mi355x(group, rays, skip):
@@ -419,17 +477,13 @@ def _trace_on_mi355x(group, rays, skip):
 
     if type(rays).__name__ != "RealRays":
         raise Unsupported(type(rays).__name__)
-    x = rays.x
-    if not (torch.is_tensor(x) and x.is_cuda and x.dtype == torch.float64):
-        raise Unsupported("rays must be float64 torch tensors on the HIP device")
+    fields, as_numpy = _ray_arrays(rays)
+    x = fields[0]
     n = x.numel()
-    fields = [getattr(rays, a) for a in _abi.RAY_FIELDS]
-    if any(not torch.is_tensor(t) or t.numel() != n or not t.is_cuda for t in fields):
-        raise Unsupported("ray fields of mixed sizes / devices")
-    params = _grad_params(group)
+    params = _grad_params(group) if not as_numpy else []
     w = rays.w
     if not torch.is_tensor(w):
-        w = torch.as_tensor(w, dtype=torch.float64, device=x.device)
+        w = torch.as_tensor(np.asarray(w, dtype=np.float64), device=x.device)
     w = w.detach().to(device=x.device, dtype=torch.float64).reshape(-1)
     if n == 0:
         raise Unsupported("empty ray batch")
@@ -450,19 +504,21 @@ def _trace_on_mi355x(group, rays, skip):
     outs = torch.ops.ort.trace_sequential(
         ops.handle(dl), fields, w if per_ray else None, [t for _, _, t in params],
         ops.encode_spec([(k, si) for k, si, _ in params]), start, per_ray)
+    STATS[x.device.type] += 1
+    conv = (lambda t: t.numpy()) if as_numpy else (lambda t: t)
     group.reset()
     names = ("x", "y", "z", "L", "M", "N", "intensity", "opd")
     if skip == 0:  # the object surface records the incoming rays (object_surface.py:56-72)
         obj = group.surfaces[0]
         for nm, t in zip(names, fields, strict=True):
-            setattr(obj, nm, t)
+            setattr(obj, nm, conv(t.clone()) if as_numpy else t)
     for a, t in zip(_abi.RAY_FIELDS, outs[:8], strict=True):
-        setattr(rays, a, t)
+        setattr(rays, a, conv(t))
     view = outs[8].view(dl.table.n_rec, 8, n)
     for slot, si in enumerate(dl.table.rec_surfaces):
         if si < start:  # surfaces[:skip] are not traced: their records stay reset
             continue
         s = group.surfaces[si + 1]
         for f, nm in enumerate(names):
-            setattr(s, nm, view[slot, f])
+            setattr(s, nm, conv(view[slot, f]))
     return rays

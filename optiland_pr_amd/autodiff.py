@@ -178,12 +178,12 @@ def vjp(dlens, seg_dev, px, py, n, seg_len, sched_dev, tables, n_param, cot, gra
         # state read from the forward's outputs
         params.tape = tape.data_ptr()
         params.primal = _native.ort_rays(*(t.data_ptr() for t in primal))
-    if mode == _abi.VJP_ADJOINT:
-        size = lib.ort_vjp_workspace_size(C.byref(dlens.c), C.byref(batch), C.byref(params))
-        _native.check(int(size) if size < 0 else 0, "ort_vjp_workspace_size")
-        ws = _workspace(grad.device, size)
-        params.workspace = ws.data_ptr()
-        params.workspace_size = ws.numel()
+    # both modes take a workspace (ABI v15: the unrolled mode's block partials)
+    size = lib.ort_vjp_workspace_size(C.byref(dlens.c), C.byref(batch), C.byref(params))
+    _native.check(int(size) if size < 0 else 0, "ort_vjp_workspace_size")
+    ws = _workspace(grad.device, size)
+    params.workspace = ws.data_ptr()
+    params.workspace_size = ws.numel()
     cot_c = _native.ort_rays(*(0 if c is None else c.data_ptr() for c in cot))
     timer = VJP_EVENTS
     if timer is not None:

@@ -1,9 +1,13 @@
-"""Build the HIP extension in-tree: optiland_pr_amd/lib/liboptiland_rt.so (gfx950).
+"""Build the native libraries in-tree:
+
+  optiland_pr_amd/lib/liboptiland_rt.so    the HIP trace core for gfx950 (hipcc)
+  optiland_pr_amd/lib/liboptiland_host.so  its host build, the CPU dispatch key of the torch
+                                           custom ops (g++ -fopenmp, include/optiland_host.h)
 
     python -m optiland_pr_amd.build
 
 hipcc cross-compiles for gfx950 without a GPU, so this runs in the CPU container too.
-The .so is git-ignored but travels to the GPU box with the repo snapshot.
+The .so files are git-ignored but travel to the GPU box with the repo snapshot.
 """
 
 from __future__ import annotations
@@ -17,6 +21,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 LIB_DIR = os.path.join(HERE, "lib")
 LIB_PATH = os.path.join(LIB_DIR, "liboptiland_rt.so")
+HOST_LIB_PATH = os.path.join(LIB_DIR, "liboptiland_host.so")
 CSRC = os.path.join(HERE, "csrc")
 # one translation unit per kernel family, compiled in parallel, linked into one .so
 SOURCES = [os.path.join(CSRC, f) for f in (
@@ -27,8 +32,16 @@ SOURCES = [os.path.join(CSRC, f) for f in (
 HEADERS = [os.path.join(CSRC, "ort_core.h"), os.path.join(CSRC, "ort_kernels.h"), os.path.join(CSRC, "ort_fastpath.h"),
            os.path.join(CSRC, "ort_adjoint.h"), os.path.join(CSRC, "ort_pupil.h"),
            os.path.join(CSRC, "ort_sincos_table.h"), os.path.join(CSRC, "ort_material.h"), os.path.join(CSRC, "ort_interact.h"), os.path.join(CSRC, "ort_reduce.h"),
-           os.path.join(REPO, "include", "optiland_rt.h")]
+           os.path.join(CSRC, "ort_sweep.h"), os.path.join(REPO, "include", "optiland_rt.h")]
 DEPS = SOURCES + HEADERS
+HOST_SOURCES = [os.path.join(CSRC, "ort_host.cpp")]
+HOST_DEPS = HOST_SOURCES + [os.path.join(CSRC, f) for f in ("ort_core.h", "ort_sweep.h",
+                                                           "ort_material.h", "ort_interact.h")] + [
+    os.path.join(REPO, "include", "optiland_rt.h"), os.path.join(REPO, "include", "optiland_host.h")]
+# the host build keeps the kernels' rounding: no contraction of a*b+c (as -ffp-contract=off
+# on hipcc), no fast-math
+HOST_FLAGS = ["-O2", "-ffp-contract=off", "-fno-fast-math", "-fopenmp", "-fPIC", "-shared",
+              "-std=c++17", "-Wall", "-Wno-unknown-pragmas"]
 
 # -ffp-contract=off: no a*b+c fusion, so each +,-,*,/ rounds exactly as NumPy does.
 HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-std=c++17", "-fPIC",
@@ -42,19 +55,49 @@ def hipcc():
     raise RuntimeError("hipcc not found (ROCm is required to build the MI355X trace core)")
 
 
-def needs_build(out=None):
+def needs_build(out=None, deps=None):
     out = out or LIB_PATH
     if not os.path.exists(out):
         return True
     t = os.path.getmtime(out)
-    return any(os.path.getmtime(d) > t for d in DEPS)
+    return any(os.path.getmtime(d) > t for d in (deps or DEPS))
+
+
+def _start_host_build(force=False, verbose=False):
+    """Start the g++ build of liboptiland_host.so (None when it is up to date)."""
+    if not force and not needs_build(HOST_LIB_PATH, HOST_DEPS):
+        return None
+    os.makedirs(LIB_DIR, exist_ok=True)
+    cxx = os.environ.get("CXX") or shutil.which("g++") or "g++"
+    cmd = [cxx, *HOST_FLAGS, "-I", os.path.join(REPO, "include"), "-o", HOST_LIB_PATH + ".tmp",
+           *HOST_SOURCES]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    return subprocess.Popen(cmd)
+
+
+def _finish_host_build(proc):
+    if proc is None:
+        return
+    if proc.wait() != 0:
+        raise subprocess.CalledProcessError(proc.returncode, "g++ ort_host.cpp")
+    os.replace(HOST_LIB_PATH + ".tmp", HOST_LIB_PATH)
+
+
+def build_host(force=False, verbose=False):
+    """Compile liboptiland_host.so alone (the CPU dispatch key)."""
+    _finish_host_build(_start_host_build(force, verbose))
+    return HOST_LIB_PATH
 
 
 def build(force=False, verbose=False, out=None, extra_flags=(), jobs=None):
-    """Compile every translation unit (in parallel) and link liboptiland_rt.so.
+    """Compile every translation unit (in parallel) and link liboptiland_rt.so; the host
+    library liboptiland_host.so is compiled alongside (default output only).
     out / extra_flags: build a variant library elsewhere (A/B timing)."""
+    host = None if out else _start_host_build(force, verbose)
     out = out or LIB_PATH
     if not force and not needs_build(out):
+        _finish_host_build(host)
         return out
     obj_dir = os.path.join(os.path.dirname(out), "obj" + ("" if out == LIB_PATH else "_" +
                            os.path.splitext(os.path.basename(out))[0]))
@@ -85,6 +128,7 @@ def build(force=False, verbose=False, out=None, extra_flags=(), jobs=None):
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
     os.replace(tmp, out)
+    _finish_host_build(host)
     return out
 
 

@@ -6,8 +6,6 @@
 
 namespace ortk {
 
-int fill_args(KArgs& a, const ort_lens* lens, const ort_batch* batch, const ort_options* opt,
-              double* rec, ort_newton_stat* stats, int32_t* status, uint32_t& feat);
 int init_outputs(const KArgs& a, hipStream_t stream);
 
 int launch_geom(const ort_lens* lens, int32_t surface, int64_t n, const ort_rays* rays,
@@ -34,93 +32,6 @@ int launch_geom(const ort_lens* lens, int32_t surface, int64_t n, const ort_rays
   hipLaunchKernelGGL(select_geom(feat & F_KM), dim3((unsigned)blocks), dim3(kBlock), 0, stream,
                      a, g);
   return hipGetLastError() == hipSuccess ? ORT_OK : ORT_ERR_LAUNCH;
-}
-
-int fill_args(KArgs& a, const ort_lens* lens, const ort_batch* batch, const ort_options* opt,
-              double* rec, ort_newton_stat* stats, int32_t* status, uint32_t& feat) {
-  if (!lens || !batch || !opt) return ORT_ERR_ARG;
-  if (lens->n_surfaces < 0 || lens->n_surfaces > ORT_MAX_SURFACES) return ORT_ERR_SURFACES;
-  if (lens->n_surfaces > 0 &&
-      (!lens->surfaces || !lens->n_tab || !lens->alpha_tab || !lens->optics))
-    return ORT_ERR_ARG;
-  if (batch->n_rays < 0 || batch->seg_len < 1 || batch->group_len < 1) return ORT_ERR_ARG;
-  if (lens->n_lambda < 1 || lens->n_mat < 1) return ORT_ERR_ARG;
-  if (opt->start_surface < 0) return ORT_ERR_ARG;
-  a.surf = lens->surfaces;
-  a.cs = lens->cs_ops;
-  a.coef = lens->coef;
-  a.zern = lens->zern;
-  a.n_tab = lens->n_tab;
-  a.alpha_tab = lens->alpha_tab;
-  a.optics = lens->optics;
-  a.n_surf = lens->n_surfaces;
-  a.n_lambda = lens->n_lambda;
-  a.n_mat = lens->n_mat;
-  a.final_mat = lens->final_mat;
-  a.final_thickness = lens->final_thickness;
-  a.n_rays = batch->n_rays;
-  a.seg_len = batch->seg_len;
-  a.group_len = batch->group_len;
-  a.seg = batch->seg;
-  a.n_seg = batch->n_seg;
-  a.pupil_per_ray = batch->pupil_per_ray;
-  a.apod = batch->apod;
-  a.newton_mode = opt->newton_mode;
-  a.start_surface = opt->start_surface;
-  a.sched = opt->sched;
-  a.conv_base = opt->conv_base;
-  a.run_if = opt->run_if;
-  a.no_init = (opt->flags & ORT_OPT_NO_INIT) != 0;
-  a.tape = opt->tape;
-  if (opt->conv_base < 0) return ORT_ERR_ARG;
-  // geometry ids this library knows (enum ort_geometry): anything else is refused here
-  // rather than traced as some other kind
-  if (lens->geometry_mask & ~((2u << ORT_GEOM_GRID_SAG) - 1u)) return ORT_ERR_ARG;
-  a.rec = rec;
-  a.stats = stats;
-  a.status = status;
-  feat = 0;
-  if (lens->geometry_mask & (1u << ORT_GEOM_EVEN_ASPHERE)) feat |= ort::KM_EVEN;
-  if (lens->geometry_mask & (1u << ORT_GEOM_ODD_ASPHERE)) feat |= ort::KM_ODD;
-  if (lens->geometry_mask & (1u << ORT_GEOM_ZERNIKE)) feat |= ort::KM_ZERN;
-  if (lens->geometry_mask & ((1u << ORT_GEOM_POLYNOMIAL) | (1u << ORT_GEOM_CHEBYSHEV) |
-                             (1u << ORT_GEOM_BICONIC) | (1u << ORT_GEOM_TOROIDAL) |
-                             (1u << ORT_GEOM_FORBES_QBFS) | (1u << ORT_GEOM_FORBES_Q2D) |
-                             (1u << ORT_GEOM_GRID_SAG)))
-    feat |= ort::KM_FREE;
-  if (rec) feat |= F_REC;
-  if (batch->w) {  // per-ray wavelengths: n, k from the material tables
-    if (!lens->materials) return ORT_ERR_ARG;
-    a.w = batch->w;
-    a.mats = lens->materials;
-    feat |= F_WRAY;
-  } else if (lens->n_lambda == 1 || batch->n_seg <= 1 || batch->seg_len % 64 == 0) {
-    // every wave reads one wavelength row: one row, one segment, or segment boundaries
-    // on the 64-ray wave boundaries (ray r is in segment r / seg_len)
-    feat |= F_MONO;
-  }
-  if (lens->interaction_mask & ~(1u << ORT_IA_REFRACT_REFLECT)) {
-    feat |= F_IA;
-    a.lambdas = lens->wavelengths;
-    const uint32_t need_w = (1u << ORT_IA_PHASE) | (1u << ORT_IA_DIFFRACTIVE);
-    if ((lens->interaction_mask & need_w) && !batch->w && !lens->wavelengths) return ORT_ERR_ARG;
-  }
-  if (lens->frame_flags & ORT_LENS_AXIAL) feat |= F_AXIAL;
-  if (opt->newton_mode != ORT_NEWTON_SCHEDULE && opt->newton_mode != ORT_NEWTON_WAVE)
-    return ORT_ERR_ARG;
-  a.vstats = opt->verify_stats;
-  a.vprev = opt->verify_prev_flag;
-  a.vflag = opt->verify_flag;
-  a.sched_out = opt->sched_out;
-  if (opt->verify_stats) {  // verify-and-re-trace (see ort_options)
-    const int64_t ng = (batch->n_rays + batch->group_len - 1) / batch->group_len;
-    if ((feat & F_KM) == 0 || opt->newton_mode != ORT_NEWTON_SCHEDULE || !opt->sched ||
-        !opt->verify_flag || !opt->sched_out || opt->sched_out == opt->sched ||
-        !(opt->flags & ORT_OPT_NO_INIT) ||
-        opt->run_if || ng * (int64_t)lens->n_surfaces > ORT_VERIFY_MAX_SCHED)
-      return ORT_ERR_ARG;
-  }
-  return ORT_OK;
 }
 
 int launch(const KArgs& a_in, uint32_t feat, hipStream_t stream) {
@@ -253,7 +164,8 @@ int trace_pupil_impl(const ort_lens* lens, const double* px, const double* py,
 extern "C" {
 
 // ORT_VJP_ADJOINT workspace: tape [S][kTapeRows][n_rays], partial [n_slot][n_wave],
-// slot_sum [n_slot], need [n_slot] (each 256-byte aligned)
+// slot_sum [n_slot], need [n_slot] (each 256-byte aligned).
+// ORT_VJP_UNROLLED workspace: the block partials [n_block][4] of one tangent chunk.
 struct AdjLayout {
   int32_t n_slot;
   int64_t n_wave, tape, partial, slot_sum, need, total;
@@ -265,6 +177,13 @@ static bool adj_layout(const ort_lens* lens, const ort_batch* batch,
   if (params->zern_param && params->n_zern == 0) return false;
   auto al = [](int64_t v) { return (v + 255) & ~(int64_t)255; };
   const int64_t S = lens->n_surfaces, n = batch->n_rays;
+  if (params->mode == ORT_VJP_UNROLLED) {
+    L.n_slot = 0;
+    L.n_wave = (n + kBlock - 1) / kBlock;  // blocks
+    L.tape = L.partial = L.slot_sum = L.need = 0;
+    L.total = al(L.n_wave * 4 * (int64_t)sizeof(double));
+    return true;
+  }
   L.n_slot = (int32_t)(3 * S + params->n_zern + 1);
   L.n_wave = (n + kBlock - 1) / kBlock * (kBlock / 64);
   L.tape = 0;
@@ -373,6 +292,9 @@ static int vjp_run(const ort_lens* lens, const double* px, const double* py,
   }
   if (params->mode != ORT_VJP_UNROLLED) return ORT_ERR_ARG;
   if (want_in) return ORT_ERR_ARG;  // forward mode carries parameter tangents only
+  AdjLayout L;
+  if (!adj_layout(lens, batch, params, L)) return ORT_ERR_ARG;
+  if (!params->workspace || params->workspace_size < L.total) return ORT_ERR_ARG;
   JArgs j{};
   j.zparam = params->zern_param;
   j.tan_surf = params->surf_tangent;
@@ -381,6 +303,7 @@ static int vjp_run(const ort_lens* lens, const double* px, const double* py,
   j.cot = *cotangent;
   j.rec_cot = rec_cotangent;
   j.grad = grad;
+  j.partial = (double*)params->workspace;
   if (params->grad_init &&
       hipMemsetAsync(grad, 0, (size_t)n_param * sizeof(double), s) != hipSuccess)
     return ORT_ERR_LAUNCH;
@@ -391,9 +314,13 @@ static int vjp_run(const ort_lens* lens, const double* px, const double* py,
     const int pref = e ? atoi(e) : 4;
     const int P = left >= 4 && pref >= 4 ? 4 : (left >= 2 && pref >= 2 ? 2 : 1);
     VjpFn fn = select_vjp(P, km);
-    if (!fn) return ORT_ERR_ARG;
+    VjpReduceFn red = select_vjp_reduce(P);
+    if (!fn || !red) return ORT_ERR_ARG;
     j.p0 = p0;
+    // the chunk's block partials, then their fixed-order sums into grad (the next chunk's
+    // launch reuses the partials after this reduction on the same stream)
     hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(kBlock), 0, s, a, j);
+    hipLaunchKernelGGL(red, dim3((unsigned)P), dim3(kBlock), 0, s, j, blocks);
     if (hipGetLastError() != hipSuccess) return ORT_ERR_LAUNCH;
     p0 += P;
   }

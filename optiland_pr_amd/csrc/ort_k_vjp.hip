@@ -17,4 +17,13 @@ VjpFn select_vjp(int tangents, uint32_t km) {
   }
 }
 
+VjpReduceFn select_vjp_reduce(int tangents) {
+  switch (tangents) {
+    case 1: return vjp_reduce_kernel<1>;
+    case 2: return vjp_reduce_kernel<2>;
+    case 4: return vjp_reduce_kernel<4>;
+    default: return nullptr;
+  }
+}
+
 }  // namespace ortk

@@ -29,6 +29,7 @@
 #include "ort_fastpath.h"
 #include "ort_interact.h"
 #include "ort_material.h"
+#include "ort_sweep.h"  // KArgs, fill_args, localize / globalize, the derivative sweeps
 
 namespace ortk {
 
@@ -39,108 +40,6 @@ constexpr int kBlock = 256;
 #define ORT_CLOSED_BLOCK 256
 #endif
 constexpr int kClosedBlock = ORT_CLOSED_BLOCK;
-
-// Lens tables are read-only for the whole launch and indexed by wave-uniform values, so
-// they are read through the constant address space: the compiler then emits scalar
-// loads (s_load -> SGPRs) instead of per-lane vector loads.
-#if defined(__HIP_DEVICE_COMPILE__)
-#define ORT_CONST_AS __attribute__((address_space(4)))
-#else
-#define ORT_CONST_AS
-#endif
-template <class T>
-using cptr = const ORT_CONST_AS T*;
-template <class T>
-__device__ inline cptr<T> cst(const T* p) {
-  return (cptr<T>)(p);
-}
-using PD = cptr<double>;
-using PZ = cptr<ort_zernike_term>;
-constexpr ort::ZSeed kNoSeed{nullptr, 0};
-
-// Kernel specialisation bits: bits 0-3 = Newton kinds present (ort::KM_*), bit 4 = rays
-// generated in-kernel from pupil coordinates.
-enum : uint32_t {
-  F_KM = 15u,
-  F_GEN = 1u << 4,
-  F_REC = 1u << 5,   // some surfaces are recorded (standard_surface.py:266-286)
-  F_MONO = 1u << 6,  // the wavelength row is wave-uniform (one wavelength in the lens
-                     // tables, or segments aligned to 64 rays): scalar table loads
-  F_WRAY = 1u << 7,  // per-ray wavelengths: n, k from lens.materials (ort_batch.w)
-  F_IA = 1u << 8,    // thin-lens / phase / grating interactions (ort_interaction)
-  F_AXIAL = 1u << 9, // ORT_LENS_AXIAL: every frame a +z translation (closed-form kernels)
-  F_TAPE = 1u << 10, // write the adjoint tape as the trace runs (ort_options.tape)
-  F_SPOT = 1u << 11, // closed-form kernel: spot pass 1 in the epilogue (ort_trace_spot)
-};
-
-// Adjoint tape (ort_adjoint.h): per traced surface, rows of n_rays doubles -- the incoming
-// global x y z L M N, the distance t, the Newton iterates before the last kHist updates
-constexpr int kTapeRows = 11;
-constexpr int kHist = 4;
-
-struct KArgs {
-  // lens
-  const ort_surface* surf;
-  const ort_cs_op* cs;
-  const double* coef;
-  const ort_zernike_term* zern;
-  const double* n_tab;
-  const double* alpha_tab;
-  const ort_surface_optics* optics;
-  int32_t n_surf;
-  int32_t n_lambda;
-  int32_t n_mat;
-  int32_t final_mat;
-  double final_thickness;
-  // rays
-  ort_rays in;
-  ort_rays out;
-  const double* px;
-  const double* py;
-  // batch
-  int64_t n_rays;
-  int64_t seg_len;
-  int64_t group_len;
-  const ort_segment* seg;
-  int32_t n_seg;
-  int32_t pupil_per_ray;
-  // options
-  int32_t newton_mode;
-  int32_t start_surface;
-  const int32_t* sched;
-  int32_t conv_base;  // first stop index of the ort_newton_stat.conv_mask window
-  // outputs
-  double* rec;
-  ort_newton_stat* stats;
-  int32_t* status;
-  // per-ray wavelengths (F_WRAY)
-  const double* w;
-  const ort_material* mats;
-  // wavelength of each table row (F_IA: phase / grating interactions)
-  const double* lambdas;
-  // pupil apodization of generated rays (NULL: intensity 1)
-  const ort_apodization* apod;
-  // trace_kernel: blocks walk the pupil chunk by chunk over all (field, lambda) segments
-  // (pair_major_ray); set by the host only when it is a bijection (see launch)
-  int32_t block_remap;
-  // nullable: the launch is a no-op unless *run_if == 1 (ort_options.run_if)
-  const int32_t* run_if;
-  int32_t no_init;  // host side only: ORT_OPT_NO_INIT (skip init_outputs)
-  // verify-and-re-trace (ort_options.verify_*): the launch decides from vstats first
-  const ort_newton_stat* vstats;
-  const int32_t* vprev;
-  int32_t* vflag;
-  int32_t* sched_out;
-  double* tape;     // F_TAPE: [n_surf][kTapeRows][n_rays] (ort_options.tape)
-  // F_SPOT (ort_trace_spot): block b traces chunk b % spot_chunks of pair b / spot_chunks
-  // (kClosedBlock rays of seg_len, the tail lanes idle) and writes the chunk's count, sum x,
-  // sum y of its i > 0 image points, in the image frame, to spot_part1[b][3] -- the rows
-  // spot_sum_kernel would write (ort_k_spot.hip), by the same block reduction
-  double* spot_part1;
-  const ort_cs_op* spot_ops;
-  int32_t spot_n_ops;
-  int32_t spot_chunks;
-};
 
 // ort_trace_spot -> trace_pupil_impl (ort_api.hip): where the fused spot pass 1 writes;
 // fused reports whether the launch took it
@@ -202,13 +101,6 @@ __device__ inline void max_if_changes(int32_t* p, int32_t v) {
   if (v > cur) atomicMax(p, v);
 }
 
-// Table lookup n_tab[lam][mat]: a uniform scalar load when the lens is traced at one
-// wavelength (the common case), else a per-lane load of the small L1-resident table.
-__device__ inline double tab(const double* t, int n_lambda, int n_mat, int lam, int mat) {
-  if (n_lambda == 1) return cst(t)[mat];
-  return t[lam * n_mat + mat];
-}
-
 // Optical constants of surface si at the ray's wavelength (same scalar-load batch as the
 // surface record when the row is wave-uniform). F_MONO makes that a compile-time fact:
 // with a run-time test the compiler merges both loads into one per-lane vector load
@@ -221,24 +113,7 @@ __device__ inline int uniform_row(int lam) { return __builtin_amdgcn_readfirstla
 template <uint32_t FEAT = 0>
 __device__ inline ort_surface_optics optics_at(const KArgs& a, int lam, int si) {
   if constexpr ((FEAT & F_MONO) != 0) return cst(a.optics)[uniform_row(lam) * a.n_surf + si];
-  if (a.n_lambda == 1) return cst(a.optics)[si];
-  return a.optics[lam * a.n_surf + si];
-}
-
-// F_WRAY: the surface's optical constants at this ray's own wavelength w, evaluated from
-// the material tables as the reference evaluates material.n(rays.w) / .k(rays.w)
-// (standard_surface.py:218, refractive_reflective_model.py:32-55, homogeneous.py:45-54)
-__device__ inline ort_surface_optics optics_ray(const KArgs& a, const ort_surface& s,
-                                                double w) {
-  const ort_material mp = cst(a.mats)[s.mat_pre];
-  const ort_material mq = cst(a.mats)[s.mat_post];
-  ort_surface_optics o;
-  o.n_pre = ort::material_n(mp, a.coef, w);
-  o.n_post = ort::material_n(mq, a.coef, w);
-  o.u = o.n_pre / o.n_post;
-  o.u_sq = o.u * o.u;
-  o.alpha_pre = ort::absorption_alpha(ort::material_k(mp, a.coef, w), w);
-  return o;
+  return optics_row(a, lam, si);
 }
 
 template <uint32_t FEAT>
@@ -255,28 +130,6 @@ __device__ inline double final_alpha(const KArgs& a, int lam, double w) {
     return ort::absorption_alpha(ort::material_k(cst(a.mats)[a.final_mat], a.coef, w), w);
   if constexpr ((FEAT & F_MONO) != 0) return cst(a.alpha_tab)[uniform_row(lam) * a.n_mat + a.final_mat];
   return tab(a.alpha_tab, a.n_lambda, a.n_mat, lam, a.final_mat);
-}
-
-// localize / globalize (coordinate_system.py:73-107): the root frame's translation
-// (cs_t) inline and unconditional, the rest (rotations, reference_cs chains) through the
-// op lists, which are empty for plain decentred surfaces (no branch, no register
-// shuffling around one)
-template <class T>
-__device__ inline void localize(const KArgs& a, const ort_surface& s, ort::RayT<T>& r) {
-  {
-    r.x = r.x + -s.cs_t[0];
-    r.y = r.y + -s.cs_t[1];
-  }
-  r.z = r.z + -s.cs_t[2];
-  for (int c = 0; c < s.n_cs_loc; ++c) ort::apply_cs_op(r, cst(a.cs)[s.cs_loc_off + c]);
-}
-
-template <class T>
-__device__ inline void globalize(const KArgs& a, const ort_surface& s, ort::RayT<T>& r) {
-  for (int c = 0; c < s.n_cs_glob; ++c) ort::apply_cs_op(r, cst(a.cs)[s.cs_glob_off + c]);
-  r.x = r.x + s.cs_t[0];
-  r.y = r.y + s.cs_t[1];
-  r.z = r.z + s.cs_t[2];
 }
 
 // geometry ids this library implements (enum ort_geometry); the kernels turn any other
@@ -987,30 +840,6 @@ __global__ __launch_bounds__(kClosedBlock) __attribute__((amdgpu_waves_per_eu(8)
   a.out.opd[rid] = r.opd;
 }
 
-// ---------------------------------------------------------------------------------
-// Vector-Jacobian product of ort_trace_pupil w.r.t. lens parameters (the autograd
-// backward; reference: torch autograd through the unrolled trace,
-// backend/torch_backend.py + optimization/optimizer/torch/base.py:95-154): Zernike
-// coefficients, surface radius and conic, surface vertex z (thickness variables) and
-// the image-space propagation distance.
-//
-// Forward mode: the ray state carries P tangents (ort::Dual<P>), one per parameter of
-// this launch's chunk, through exactly the Newton update counts of the primal trace
-// (opt.sched), so the derivative is that of the unrolled iteration the reference
-// differentiates. Each lane contracts its tangents with the ray cotangents; wave
-// shuffles, then LDS, then one atomic per block and parameter.
-// ---------------------------------------------------------------------------------
-struct JArgs {
-  const int32_t* zparam;   // [n_zern_terms] parameter index per term, < 0: constant
-  const double* tan_surf;  // [n_param][n_surf][3]: d radius, d conic, d vertex z
-  const double* tan_final; // [n_param]: d final_thickness
-  int32_t n_param;
-  int32_t p0;              // first parameter of this launch
-  ort_rays cot;            // cotangents of the outputs (NULL field: zero)
-  const double* rec_cot;   // cotangents of the record buffer [n_rec][8][n_rays] (or NULL)
-  double* grad;            // [n_param], accumulated with atomics
-};
-
 // Sum over the 64 lanes of a wave. With the whole wave active: DPP row operations
 // (VALU moves, no LDS round trip per step): quad_perm xor 1 and xor 2, row_half_mirror,
 // row_mirror (a row of 16 summed in every lane), row_bcast15 / row_bcast31 (rows
@@ -1041,133 +870,18 @@ __device__ inline double wave_sum(double v) {
   return v;
 }
 
-template <int P>
-__device__ inline void cot_acc(double (&acc)[P], const double* g, int64_t rid,
-                               const ort::Dual<P>& v) {
-  if (!g) return;
-  const double c = g[rid];
-#pragma unroll
-  for (int k = 0; k < P; ++k) acc[k] += c * v.d[k];
-}
-
-// v with the tangents of this chunk's parameters: tan[p * stride + off] (uniform loads)
-template <int P>
-__device__ inline ort::Dual<P> seeded(double v, const double* tan, int64_t stride, int off,
-                                      const JArgs& j) {
-  ort::Dual<P> r(v);
-  if (tan) {
-#pragma unroll
-    for (int k = 0; k < P; ++k) {
-      const int p = j.p0 + k;
-      r.d[k] = p < j.n_param ? cst(tan)[(int64_t)p * stride + off] : 0.0;
-    }
-  }
-  return r;
-}
-
-// a.px set: rays generated from pupil samples (ort_trace_pupil_vjp); NULL: resident input
-// rays a.in (ort_trace_sequential_vjp), per-ray wavelengths when a.w is set
+// ---------------------------------------------------------------------------------
+// Forward-mode VJP (ORT_VJP_UNROLLED): vjp_ray (ort_sweep.h) per lane; each block writes
+// its P sums (wave sums, then the block's four waves in order) to partial[block][P] and
+// vjp_reduce_kernel adds, per parameter, the blocks' sums in index order to grad: the
+// same bits run to run (no atomics).
+// ---------------------------------------------------------------------------------
 template <int P, uint32_t KM>
 __global__ __launch_bounds__(kBlock) void vjp_kernel(const KArgs a, const JArgs j) {
-  using D = ort::Dual<P>;
   const int64_t rid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool active = rid < a.n_rays;
-  const int64_t r_ld = active ? rid : 0;
-  const int64_t sidx = a.seg ? r_ld / a.seg_len : 0;
-  int lam = 0;
-  double wl = 0.0;
-  ort::RayT<D> r;
-  if (a.px) {
-    const ort_segment sg = a.seg[sidx];
-    lam = sg.lambda_idx;
-    const int64_t p = a.pupil_per_ray ? r_ld : (r_ld - sidx * a.seg_len);
-    r = ort::promote<D>(ort::generate_ray(sg, a.px[p], a.py[p], a.apod));
-  } else {
-    if (a.seg) lam = a.seg[sidx].lambda_idx;
-    if (a.w) wl = a.w[r_ld];
-    ort::Ray q;
-    q.x = a.in.x[r_ld];
-    q.y = a.in.y[r_ld];
-    q.z = a.in.z[r_ld];
-    q.L = a.in.L[r_ld];
-    q.M = a.in.M[r_ld];
-    q.N = a.in.N[r_ld];
-    q.i = a.in.i[r_ld];
-    q.opd = a.in.opd[r_ld];
-    q.att = 0.0;
-    r = ort::promote<D>(q);
-  }
-  const int64_t group = r_ld / a.group_len;
-  const ort::ZSeed zs{j.zparam, j.p0};
-  const int64_t ts = (int64_t)a.n_surf * 3;
   double acc[P];
-#pragma unroll
-  for (int k = 0; k < P; ++k) acc[k] = 0.0;
-
-  for (int si = a.start_surface; si < a.n_surf; ++si) {
-    const ort_surface s = cst(a.surf)[si];
-    const ort_surface_optics o = a.w ? optics_ray(a, s, wl) : optics_at(a, lam, si);
-    const D R = seeded<P>(s.radius, j.tan_surf, ts, si * 3 + 0, j);
-    const D K = seeded<P>(s.conic, j.tan_surf, ts, si * 3 + 1, j);
-    const D CZ = seeded<P>(s.cs_t[2], j.tan_surf, ts, si * 3 + 2, j);
-    // localize (coordinate_system.py:73-107) with the vertex z as a parameter
-    r.x = r.x + -s.cs_t[0];
-    r.y = r.y + -s.cs_t[1];
-    r.z = r.z + -CZ;
-    for (int c = 0; c < s.n_cs_loc; ++c) ort::apply_cs_op(r, cst(a.cs)[s.cs_loc_off + c]);
-    D t;
-    if (s.geometry == ORT_GEOM_PLANE) {
-      t = ort::distance_plane(r);
-    } else {
-      t = ort::distance_conic(r, R, K, (s.flags & ORT_SURF_RADIUS_INF) != 0);
-      if (s.geometry != ORT_GEOM_STANDARD) {
-        if constexpr (KM != 0) {
-          // replay the primal's update count (newton_raphson.py:137-166)
-          const int U = a.sched ? a.sched[group * a.n_surf + si] : s.max_iter;
-          bool rerr = false;
-          for (int it = 0; it < U; ++it) {
-            D nx, ny, nz;
-            const D f = ort::newton_eval<KM>(s, R, K, cst(a.coef), cst(a.zern), zs, r, t,
-                                             true, rerr, nx, ny, nz);
-            t = ort::newton_step(r, t, f, nx, ny, nz);
-          }
-        }
-      }
-    }
-    ort::finish_surface<KM>(r, s, R, K, cst(a.coef), cst(a.zern), zs, t, o.n_pre, o.u,
-                            o.alpha_pre);
-    for (int c = 0; c < s.n_cs_glob; ++c) ort::apply_cs_op(r, cst(a.cs)[s.cs_glob_off + c]);
-    r.x = r.x + s.cs_t[0];
-    r.y = r.y + s.cs_t[1];
-    r.z = r.z + CZ;
-    if (j.rec_cot && (s.flags & ORT_SURF_RECORD) && active) {  // this surface's record
-      const double* rc = j.rec_cot + (int64_t)s.rec_slot * 8 * a.n_rays;
-      cot_acc(acc, rc, rid, r.x);
-      cot_acc(acc, rc + a.n_rays, rid, r.y);
-      cot_acc(acc, rc + 2 * a.n_rays, rid, r.z);
-      cot_acc(acc, rc + 3 * a.n_rays, rid, r.L);
-      cot_acc(acc, rc + 4 * a.n_rays, rid, r.M);
-      cot_acc(acc, rc + 5 * a.n_rays, rid, r.N);
-      cot_acc(acc, rc + 6 * a.n_rays, rid, ort::intensity(r));
-      cot_acc(acc, rc + 7 * a.n_rays, rid, r.opd);
-    }
-  }
-  if (a.final_mat >= 0)
-    ort::propagate(r, seeded<P>(a.final_thickness, j.tan_final, 1, 0, j),
-                   a.w ? ort::absorption_alpha(ort::material_k(cst(a.mats)[a.final_mat], a.coef, wl), wl)
-                       : tab(a.alpha_tab, a.n_lambda, a.n_mat, lam, a.final_mat));
-
-  if (active) {
-    cot_acc(acc, j.cot.x, rid, r.x);
-    cot_acc(acc, j.cot.y, rid, r.y);
-    cot_acc(acc, j.cot.z, rid, r.z);
-    cot_acc(acc, j.cot.L, rid, r.L);
-    cot_acc(acc, j.cot.M, rid, r.M);
-    cot_acc(acc, j.cot.N, rid, r.N);
-    if (j.cot.i) cot_acc(acc, j.cot.i, rid, ort::intensity(r));
-    cot_acc(acc, j.cot.opd, rid, r.opd);
-  }
-  // wave sums -> LDS -> one atomic per block and parameter
+  vjp_ray<P, KM>(a, j, rid, active, acc);
   __shared__ double part[kBlock / 64][P];
 #pragma unroll
   for (int k = 0; k < P; ++k) {
@@ -1175,11 +889,30 @@ __global__ __launch_bounds__(kBlock) void vjp_kernel(const KArgs a, const JArgs 
     if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6][k] = v;
   }
   __syncthreads();
-  if (threadIdx.x < P && j.p0 + (int)threadIdx.x < j.n_param) {
+  if (threadIdx.x < P) {
     double v = 0.0;
 #pragma unroll
     for (int w = 0; w < kBlock / 64; ++w) v += part[w][threadIdx.x];
-    if (v != 0.0) atomicAdd(&j.grad[j.p0 + threadIdx.x], v);
+    j.partial[(int64_t)blockIdx.x * P + threadIdx.x] = v;
+  }
+}
+
+// One block per parameter k < P of the chunk: grad[p0 + k] += the blocks' partials summed
+// in a fixed order (strided per thread, wave sums, the four waves in order).
+template <int P>
+__global__ __launch_bounds__(kBlock) void vjp_reduce_kernel(const JArgs j, int64_t n_block) {
+  const int k = blockIdx.x;
+  if (j.p0 + k >= j.n_param) return;  // uniform
+  double v = 0.0;
+  for (int64_t b = threadIdx.x; b < n_block; b += kBlock) v += j.partial[b * P + k];
+  v = wave_sum(v);
+  __shared__ double ws[kBlock / 64];
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s = 0.0;
+    for (int w = 0; w < kBlock / 64; ++w) s += ws[w];
+    j.grad[j.p0 + k] += s;
   }
 }
 
@@ -1265,6 +998,7 @@ __global__ __launch_bounds__(kBlock) void geom_kernel(const KArgs a, const GArgs
 
 typedef void (*KernelFn)(const KArgs);
 typedef void (*VjpFn)(const KArgs, const JArgs);
+typedef void (*VjpReduceFn)(const JArgs, int64_t);
 typedef void (*GeomFn)(const KArgs, const GArgs);
 
 // kernel selection (defined in the ort_k_*.hip translation units)
@@ -1283,6 +1017,7 @@ void launch_material_nk(const ort_material* mats, const double* coef, int32_t ma
                         const double* w, int64_t n, double* n_out, double* k_out,
                         hipStream_t stream);
 VjpFn select_vjp(int tangents, uint32_t km);  // tangents 1, 2 or 4             (ort_k_vjp*.hip)
+VjpReduceFn select_vjp_reduce(int tangents); // its fixed-order reduction      (ort_k_vjp.hip)
 GeomFn select_geom(uint32_t km);           // per-geometry primitives           (ort_k_geom.hip)
 int launch_pupil(const ort_pupil& d, double* px, double* py, hipStream_t stream);  // ort_k_pupil.hip
 

@@ -26,8 +26,12 @@ tensors that require grad and ``spec`` says which lens value each one is, as fla
 (kind, traced-surface index) pairs with kind in SPEC_KINDS: the forward ignores their
 values (the lowered lens already holds them), the backward returns d loss / d each.
 
-There is no CPU kernel: on a CPU tensor the dispatcher raises (the product path has no
-fallback).
+ort::trace_sequential has two kernels, one per dispatch key (SURVEY.md 8b): CUDA (HIP) runs
+the fused GPU trace on a DeviceLens handle, CPU runs the host build of the same per-ray
+source (host.py, liboptiland_host.so, include/optiland_host.h) on a HostLens handle, with
+its VJP on the host too. Neither falls back to the other: the dispatcher picks the kernel
+by the tensors' device, and a handle of the other kind raises. trace_pupil and rms_spot
+are CUDA-only.
 """
 
 from __future__ import annotations
@@ -225,6 +229,30 @@ def trace_sequential(lens: int, rays: list[torch.Tensor], w: torch.Tensor | None
     return (*(getattr(rout, a) for a in _abi.RAY_FIELDS), rec, sched_t)
 
 
+@trace_sequential.register_kernel("cpu")
+def _trace_sequential_cpu(lens, rays, w, params, spec, start_surface, per_ray_w):
+    """The CPU dispatch key: the host build of the trace core on a HostLens (host.py)."""
+    from . import host
+
+    hl = _lookup(lens)
+    if not isinstance(hl, host.HostLens):
+        raise RuntimeError("ort::trace_sequential: CPU tensors need a HostLens handle "
+                           f"(got {type(hl).__name__})")
+    if len(rays) != 8:
+        raise ValueError("rays: x, y, z, L, M, N, i, opd")
+    n = rays[0].numel()
+    rin = [t.detach().to(dtype=torch.float64).reshape(-1).contiguous() for t in rays]
+    if any(t.numel() != n for t in rin):
+        raise ValueError("ray fields of different sizes")
+    n_rec = hl.table.n_rec
+    rec = torch.empty(n_rec * 8 * n, dtype=torch.float64)
+    outs, updates = host.trace_sequential(hl, rin, w, bool(per_ray_w), int(start_surface),
+                                          rec if n_rec else None)
+    hl.last_schedule = updates.numpy().reshape(1, -1) if hl.newton else None
+    sched = updates if hl.newton else torch.empty(0, dtype=torch.int32)
+    return (*outs, rec, sched)
+
+
 @trace_sequential.register_fake
 def _(lens, rays, w, params, spec, start_surface, per_ray_w):
     dl = _lookup(lens)
@@ -309,8 +337,18 @@ def _seq_backward(ctx, *grads):
 
 def _seq_vjp(dl, rays_in, w, per_ray_w, start_surface, sched, zp, st, ft, n_param, cot,
              rec_cot, rec, grad, gin, mode):
-    """One ort_trace_sequential_vjp call (grad += J^T cot, gin = input-ray cotangents)."""
+    """One ort_trace_sequential_vjp call (grad += J^T cot, gin = input-ray cotangents); on
+    a HostLens the host library's ort_host_trace_sequential_vjp."""
+    from . import host
     from .raytrace import _ptr, _stream_handle
+
+    if isinstance(dl, host.HostLens):
+        tabs = [None if a is None else dl.resident(("seq_tangent", i), a)
+                for i, a in enumerate((zp, st, ft))]
+        need = dl.resident("seq_need", slot_need(dl.table, zp, st, ft))
+        host.trace_sequential_vjp(dl, rays_in, w, per_ray_w, start_surface, sched, tabs, need,
+                                  n_param, mode, cot, rec_cot, rec, grad, gin)
+        return
 
     lib = _native.load()
     n = rays_in[0].numel()
@@ -330,12 +368,12 @@ def _seq_vjp(dl, rays_in, w, per_ray_w, start_surface, sched, zp, st, ft, n_para
                                     _ptr(tabs[1]).value, _ptr(tabs[2]).value,
                                     0 if tabs[0] is None else int(tabs[0].numel()), 0, None, 0,
                                     need.data_ptr())
-    if mode == _abi.VJP_ADJOINT:
-        size = lib.ort_vjp_workspace_size(C.byref(dl.c), C.byref(batch), C.byref(params))
-        _native.check(int(size) if size < 0 else 0, "ort_vjp_workspace_size")
-        ws = _workspace(dl.device, size)
-        params.workspace = ws.data_ptr()
-        params.workspace_size = ws.numel()
+    # both modes take a workspace (ABI v15: the unrolled mode's block partials)
+    size = lib.ort_vjp_workspace_size(C.byref(dl.c), C.byref(batch), C.byref(params))
+    _native.check(int(size) if size < 0 else 0, "ort_vjp_workspace_size")
+    ws = _workspace(dl.device, size)
+    params.workspace = ws.data_ptr()
+    params.workspace_size = ws.numel()
     rin_c = _ray_struct(rays_in)
     cot_c = _ray_struct(cot)
     gin_c = _ray_struct(gin if gin is not None else [None] * 8)
@@ -463,6 +501,7 @@ def rms_spot(x: torch.Tensor, y: torch.Tensor) -> tuple[torch.Tensor, torch.Tens
     from .raytrace import _ptr, _stream_handle
 
     lib = _native.load()
+    _check_rms_inputs(x, y)
     x = x.detach().reshape(-1).contiguous()
     y = y.detach().reshape(-1).contiguous()
     n = x.numel()
@@ -475,8 +514,20 @@ def rms_spot(x: torch.Tensor, y: torch.Tensor) -> tuple[torch.Tensor, torch.Tens
     return rms, stats
 
 
+def _check_rms_inputs(x, y):
+    """The kernels read x and y as n doubles each on one device: refuse anything else
+    (a shorter y would be read past its end, a float32 record read as doubles)."""
+    if x.dtype != torch.float64 or y.dtype != torch.float64:
+        raise ValueError(f"ort::rms_spot: x and y must be float64 (got {x.dtype}, {y.dtype})")
+    if x.numel() != y.numel():
+        raise ValueError(f"ort::rms_spot: x has {x.numel()} points, y {y.numel()}")
+    if x.device != y.device:
+        raise ValueError(f"ort::rms_spot: x on {x.device}, y on {y.device}")
+
+
 @rms_spot.register_fake
 def _(x, y):
+    _check_rms_inputs(x, y)
     return x.new_empty((), dtype=torch.float64), x.new_empty(5, dtype=torch.float64)
 
 
@@ -484,6 +535,9 @@ def _rms_setup(ctx, inputs, output):
     x, y = inputs
     ctx.shapes = (x.shape, y.shape)
     ctx.set_materialize_grads(False)
+    # stats (n, centroid, rms, max radius) are reported, not differentiated: mark them so a
+    # loss built on them raises instead of silently getting a zero gradient
+    ctx.mark_non_differentiable(output[1])
     ctx.save_for_backward(x.detach(), y.detach(), output[1])
 
 

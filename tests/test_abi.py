@@ -120,3 +120,23 @@ def test_library_exports_every_declared_symbol():
 def test_missing_library_fails_loudly(tmp_path):
     with pytest.raises(_native.NativeLibraryError):
         _native.load(str(tmp_path / "nope.so"))
+
+
+def test_host_library_exports_every_declared_symbol():
+    """liboptiland_host.so (the CPU dispatch key) exports every entry point
+    include/optiland_host.h declares, at the declared version."""
+    if not os.path.exists(_native.HOST_LIB_PATH):
+        pytest.skip("host library not built (run __graft_entry__.build())")
+    lib = _native.load_host()
+    text = open(os.path.join(REPO, "include", "optiland_host.h")).read()
+    declared = set(re.findall(r"^(?:int|void)(?:64_t)? (ort_host_\w+)\(", text, re.M))
+    assert declared == set(_native.HOST_EXPORTS)
+    for sym in declared:
+        assert hasattr(lib, sym), sym
+    v = re.search(r"#define ORT_HOST_ABI_VERSION (\d+)", text).group(1)
+    assert lib.ort_host_abi_version() == int(v) == _native.HOST_ABI_VERSION
+
+
+def test_missing_host_library_fails_loudly(tmp_path):
+    with pytest.raises(_native.NativeLibraryError):
+        _native.load_host(str(tmp_path / "nope.so"))

@@ -1,0 +1,96 @@
+"""The CPU dispatch key's VJP (ort_host_trace_sequential_vjp, liboptiland_host.so): the
+adjoint sweep and the forward-mode sweep of csrc/ort_sweep.h run per ray on the host.
+
+  * adjoint vs forward mode on every kind of lens and parameter through the seam (the same
+    cases and tolerances as the GPU's tests/test_gpu_adjoint.py);
+  * the gradient does not depend on the thread count (fixed-order chunk reductions);
+  * the forward-mode sweep against the reference's own gradient for the standard-scheme
+    Zernike TMA is covered through install() in tests/test_reference_install.py; here the
+    two sweeps agree on the fringe TMA, where both are exact.
+"""
+
+import os
+
+import numpy as np
+import pytest
+
+from tests.test_gpu_adjoint import CASES, FIELDS, _leaves
+from tests.test_seam_adapter import _generated
+
+
+def _seam_leaves(torch, lens, spec):
+    """_leaves, with a thickness entering as the reference's set_thickness writes it
+    (optic_updater.py:64-85): the vertex z of every later surface -- what the seam sees."""
+    leaves = []
+    for kind, si in spec:
+        if kind != "thickness":
+            leaves += _leaves(torch, lens, [(kind, si)])
+            continue
+        sg = lens.surface_group
+        t0 = float(sg.surfaces[si].thickness)
+        t = torch.tensor(t0, dtype=torch.float64, requires_grad=True)
+        for s in sg.surfaces[si + 1:]:
+            s.geometry.cs.z = float(s.geometry.cs.z) + (t - t0)
+        leaves.append(t)
+    return leaves
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch
+
+    from optiland_pr_amd import _native
+
+    _native.load_host()
+    return torch
+
+
+def _grad(torch, name, spec, mode, num_rays=12, dist="hexapolar", threads=0):
+    from optiland_pr_amd import _native
+    from optiland_pr_amd.adapter import _trace_on_mi355x
+    from tests._cases import build_lens
+
+    old = os.environ.get("ORT_VJP_MODE")
+    os.environ["ORT_VJP_MODE"] = mode
+    _native.load_host().ort_host_set_threads(threads)
+    try:
+        lens = build_lens(name)
+        rays = _generated(torch, lens, 0.0, 1.0, lens.primary_wavelength, num_rays, "cpu", dist)
+        leaves = _seam_leaves(torch, lens, spec)
+        _trace_on_mi355x(lens.surface_group, rays, 0)
+        gen = np.random.default_rng(11)
+        loss = 0.0
+        for f in FIELDS:
+            v = getattr(rays, f)
+            w = torch.as_tensor(gen.standard_normal(v.numel()))
+            loss = loss + torch.nansum(w * v)
+        loss.backward()
+        return np.concatenate([np.atleast_1d(t.grad.numpy()) for t in leaves])
+    finally:
+        _native.load_host().ort_host_set_threads(0)
+        if old is None:
+            os.environ.pop("ORT_VJP_MODE", None)
+        else:
+            os.environ["ORT_VJP_MODE"] = old
+
+
+@pytest.mark.parametrize("name,spec,rtol", CASES, ids=[c[0] for c in CASES])
+def test_host_adjoint_matches_unrolled(torch, name, spec, rtol):
+    try:
+        ga = _grad(torch, name, spec, "adjoint")
+    except NotImplementedError as e:  # a parameter this geometry does not expose
+        pytest.skip(str(e))
+    gu = _grad(torch, name, spec, "unrolled")
+    assert np.all(np.isfinite(ga))
+    scale = np.max(np.abs(gu))
+    np.testing.assert_allclose(ga, gu, rtol=rtol, atol=rtol * 1e-2 * scale)
+
+
+@pytest.mark.parametrize("mode", ["adjoint", "unrolled"])
+def test_host_vjp_independent_of_threads(torch, mode):
+    """4,921 rays (20 reduction chunks) on 1 and on 4 threads: the same bits."""
+    spec = [("zernike", 1), ("zernike", 2), ("radius", 3), ("thickness", 2)]
+    a = _grad(torch, "tma_fringe", spec, mode, num_rays=40, threads=1)
+    b = _grad(torch, "tma_fringe", spec, mode, num_rays=40, threads=4)
+    assert np.all(np.isfinite(a))
+    assert np.array_equal(a, b)

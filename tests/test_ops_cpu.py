@@ -1,8 +1,9 @@
 """CPU: the custom-op boundary (ops.py) and the adapter's gradient rules, without a GPU.
 
 * torch.ops.ort.trace_sequential / trace_pupil are registered with the schemas the
-  adapter and the native front-end call, and have no CPU kernel (the product path has
-  no fallback: a CPU tensor is refused by the dispatcher);
+  adapter and the native front-end call; trace_sequential has a CPU kernel (the host build,
+  liboptiland_host.so) that takes only a HostLens handle, trace_pupil none (the dispatcher
+  refuses a CPU tensor);
 * ops.tangent_tables lays the parameter kinds out as ort_vjp_params expects;
 * adapter._grad_params: which lens values are differentiated, which hand the call back to
   the reference loop (Unsupported), which are ignored (the reference's be.grad_mode makes
@@ -26,12 +27,26 @@ def test_ops_registered():
     assert "Tensor[] params" in s2
 
 
-def test_no_cpu_kernel():
+def test_cpu_kernel_needs_host_lens():
+    """The CPU key runs only on a HostLens (no device lens, no silent substitution);
+    trace_pupil has no CPU kernel at all."""
     lens = CookeTriplet()
-    h = ops.handle(lens)  # any object: the dispatcher refuses before the body runs
+    h = ops.handle(lens)  # not a HostLens
     z = torch.zeros(4, dtype=torch.float64)
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(RuntimeError, match="HostLens"):
         torch.ops.ort.trace_sequential(h, [z] * 8, None, [], [], 0, False)
+    with pytest.raises(NotImplementedError):
+        torch.ops.ort.trace_pupil(h, z, z, [], [])
+
+
+def test_rms_spot_refuses_mismatched_inputs():
+    """the op checks dtype, size and device before any pointer reaches the
+    kernels (here through the fake / meta path, no GPU needed)."""
+    x = torch.zeros(8, dtype=torch.float64, device="meta")
+    with pytest.raises(ValueError, match="points"):
+        torch.ops.ort.rms_spot(x, torch.zeros(7, dtype=torch.float64, device="meta"))
+    with pytest.raises(ValueError, match="float64"):
+        torch.ops.ort.rms_spot(x, torch.zeros(8, dtype=torch.float32, device="meta"))
 
 
 def test_spec_roundtrip():

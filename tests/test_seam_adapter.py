@@ -1,14 +1,18 @@
-"""GPU: the drop-in seam as the reference would call it -- adapter._trace_on_mi355x
-(the body install() puts behind optiland's SurfaceGroup.trace, surface_group.py:232-244)
-driven with the native classes, which carry the reference's class names and attributes
-(the reference itself is not on the GPU box). Everything goes through the custom op
-torch.ops.ort.trace_sequential and, under autograd, its VJP (ort_trace_sequential_vjp).
+"""The drop-in seam as the reference would call it -- adapter._trace_on_mi355x (the body
+install() puts behind optiland's SurfaceGroup.trace, surface_group.py:232-244) -- on BOTH
+dispatch keys of the custom op torch.ops.ort.trace_sequential: "cpu" (the host build of the
+trace core, liboptiland_host.so: runs here in the CPU suite) and "cuda" (the HIP kernels,
+-m gpu on the MI355X). Driven with the native classes, which carry the reference's class
+names and attributes (the reference itself is not on the GPU box; tests/
+test_reference_install.py drives the real reference objects through install()). Under
+autograd everything goes through the op's VJP (ort_trace_sequential_vjp /
+ort_host_trace_sequential_vjp).
 
-Checks (VERDICT r02 "next round" item 1): in-place rays and every surface record
-bit-exact to the dg / cooke goldens; a mixed-wavelength batch against mixed_w; gradients
-through the seam against the reference's torch autograd (autograd_tma: Zernike
-coefficients, autograd_cooke: radius / conic / thickness) at rtol 1e-8 / 1e-9; input-ray
-and record cotangents by gradcheck; skip, caching and the fall-back rules.
+Checks: in-place rays and every surface record bit-exact to the dg / cooke goldens; a
+mixed-wavelength batch against mixed_w; gradients through the seam against the reference's
+torch autograd (autograd_tma: Zernike coefficients, autograd_cooke: radius / conic /
+thickness) at rtol 1e-8 / 1e-9; input-ray and record cotangents by gradcheck; skip, caching
+and the fall-back rules.
 """
 
 import numpy as np
@@ -16,54 +20,63 @@ import pytest
 
 from tests.conftest import load_golden
 
-pytestmark = pytest.mark.gpu
-
 FIELDS = ("x", "y", "z", "L", "M", "N", "i", "opd")
 NAMES = ("x", "y", "z", "L", "M", "N", "intensity", "opd")
+
+
+@pytest.fixture(scope="module", params=["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def dev(request):
+    import torch
+
+    from optiland_pr_amd import _native
+
+    if request.param == "cuda":
+        if not torch.cuda.is_available():
+            pytest.fail("needs the MI355X")
+        _native.load()
+    else:
+        _native.load_host()
+    return request.param
 
 
 @pytest.fixture(scope="module")
 def torch():
     import torch
 
-    if not torch.cuda.is_available():
-        pytest.fail("needs the MI355X")
-    from optiland_pr_amd import _native
-
-    _native.load()
     return torch
 
 
-def _rays(torch, g, sl, w, requires_grad=False):
+def _rays(torch, g, sl, w, dev, requires_grad=False):
     from optiland_pr_amd.raytrace import RealRays
 
-    r = RealRays(*(torch.as_tensor(g[f"{a}0"][sl], device="cuda") for a in ("x", "y", "z", "L", "M", "N")),
-                 1.0, w)
+    r = RealRays(*(torch.as_tensor(g[f"{a}0"][sl], device=dev) for a in ("x", "y", "z", "L", "M", "N")),
+                 1.0, w, device=dev)
     if requires_grad:
         for a in ("x", "y", "L", "M"):
             setattr(r, a, getattr(r, a).clone().requires_grad_(True))
     return r
 
 
-def _generated(torch, lens, hx, hy, wl, num, dist="uniform"):
-    """Rays as RealRayTracer builds them (ray_generator.py:28-106), on the device."""
+def _generated(torch, lens, hx, hy, wl, num, dev, dist="uniform"):
+    """Rays as RealRayTracer builds them (ray_generator.py:28-106): the oracle's generation
+    (pinned bit-exact to the reference, tests/test_oracle_golden.py), moved to `dev`."""
+    from oracle import trace_np
     from optiland_pr_amd.distribution import create_distribution
     from optiland_pr_amd.lowering import segment_params
-    from optiland_pr_amd.raytrace import RealRays, generate_rays
+    from optiland_pr_amd.raytrace import RealRays
 
     d = create_distribution(dist)
     d.generate_points(num)
-    px = torch.as_tensor(np.asarray(d.x, dtype=np.float64), device="cuda")
-    py = torch.as_tensor(np.asarray(d.y, dtype=np.float64), device="cuda")
-    seg = np.stack([segment_params(lens, hx, hy, 0)])
-    n = px.numel()
-    out = RealRays.empty(n, wl, device=px.device)
-    generate_rays(seg, px, py, out, n, n)
-    return out
+    px = np.asarray(d.x, dtype=np.float64)
+    py = np.asarray(d.y, dtype=np.float64)
+    seg = segment_params(lens, hx, hy, 0)
+    q = trace_np.generate_rays(seg, px, py)
+    return RealRays(*(torch.as_tensor(np.ascontiguousarray(getattr(q, a)), device=dev)
+                      for a in ("x", "y", "z", "L", "M", "N")), 1.0, wl, device=dev)
 
 
 @pytest.mark.parametrize("case,pair", [("dg", 1), ("dg", 4), ("cooke", 4)])
-def test_seam_rays_and_records_bit_exact(torch, golden_index, case, pair):
+def test_seam_rays_and_records_bit_exact(torch, dev, golden_index, case, pair):
     from optiland_pr_amd.adapter import _trace_on_mi355x
     from optiland_pr_amd.samples import CookeTriplet, DoubleGauss
 
@@ -74,10 +87,11 @@ def test_seam_rays_and_records_bit_exact(torch, golden_index, case, pair):
     sl = slice(pair * n_p, (pair + 1) * n_p)
     lens = DoubleGauss() if case == "dg" else CookeTriplet()
     sg = lens.surface_group
-    rays = _rays(torch, g, sl, wl)
+    rays = _rays(torch, g, sl, wl, dev)
     x_in = rays.x
     out = _trace_on_mi355x(sg, rays, 0)
     assert out is rays  # the reference returns the same RealRays, updated in place
+    assert rays.x.device.type == dev
     for a in FIELDS:
         got = getattr(rays, a).cpu().numpy()
         if a == "i":
@@ -99,16 +113,16 @@ def test_seam_rays_and_records_bit_exact(torch, golden_index, case, pair):
 
 
 @pytest.mark.parametrize("name", ["dg", "cooke", "freeform"])
-def test_seam_mixed_wavelengths(torch, name):
+def test_seam_mixed_wavelengths(torch, dev, name):
     from optiland_pr_amd.adapter import _trace_on_mi355x
     from optiland_pr_amd.raytrace import RealRays
     from tests._cases import build_lens
 
     g = load_golden("mixed_w")
     lens = build_lens(name)
-    rays = RealRays(*(torch.as_tensor(g[f"{name}/in_{a}"], device="cuda")
+    rays = RealRays(*(torch.as_tensor(g[f"{name}/in_{a}"], device=dev)
                       for a in ("x", "y", "z", "L", "M", "N", "i")),
-                    torch.as_tensor(g[f"{name}/w"], device="cuda"))
+                    torch.as_tensor(g[f"{name}/w"], device=dev), device=dev)
     _trace_on_mi355x(lens.surface_group, rays, 0)
     for a in FIELDS:
         got = getattr(rays, a).cpu().numpy()
@@ -128,7 +142,7 @@ def _rms(torch, s):
     return torch.sqrt(torch.mean(r2))
 
 
-def test_seam_gradient_zernike_matches_reference(torch):
+def test_seam_gradient_zernike_matches_reference(torch, dev):
     """autograd_tma: d rms / d (30 Zernike coefficients) of the TMA at field (0, 1),
     uniform 32, 0.587 um, through SurfaceGroup.trace (the reference's operand reads the
     image record, rms_spot_size operand/ray.py:300-340)."""
@@ -137,11 +151,11 @@ def test_seam_gradient_zernike_matches_reference(torch):
 
     g = load_golden("autograd_tma")
     lens = ThreeMirrorAnastigmat()
-    rays = _generated(torch, lens, 0.0, 1.0, 0.587, 32)
+    rays = _generated(torch, lens, 0.0, 1.0, 0.587, 32, dev)
     leaves = []
     for si in (1, 2, 3):
         geo = lens.surface_group.surfaces[si].geometry
-        t = torch.tensor(np.asarray(geo.coefficients, dtype=np.float64), device="cuda",
+        t = torch.tensor(np.asarray(geo.coefficients, dtype=np.float64), device=dev,
                          requires_grad=True)
         geo.coefficients = t
         leaves.append(t)
@@ -155,7 +169,7 @@ def test_seam_gradient_zernike_matches_reference(torch):
 
 
 @pytest.mark.parametrize("th", [2, 6])
-def test_seam_gradient_radius_conic_thickness_matches_reference(torch, th):
+def test_seam_gradient_radius_conic_thickness_matches_reference(torch, dev, th):
     """autograd_cooke: d rms / d (radius 1, 3, 6, conic 5, thickness th) of the Cooke
     triplet, the thickness entering as the vertex z of every later surface (what the
     reference's set_thickness writes, optic_updater.py:64-85)."""
@@ -164,19 +178,19 @@ def test_seam_gradient_radius_conic_thickness_matches_reference(torch, th):
 
     g = load_golden("autograd_cooke")
     lens = CookeTriplet()
-    rays = _generated(torch, lens, 0.0, 1.0, 0.55, 24)
+    rays = _generated(torch, lens, 0.0, 1.0, 0.55, 24, dev)
     sg = lens.surface_group
     leaves = []
     for si in (1, 3, 6):
         t = torch.tensor(float(sg.surfaces[si].geometry.radius), dtype=torch.float64,
-                         device="cuda", requires_grad=True)
+                         device=dev, requires_grad=True)
         sg.surfaces[si].geometry.radius = t
         leaves.append(t)
-    t = torch.tensor(0.0, dtype=torch.float64, device="cuda", requires_grad=True)
+    t = torch.tensor(0.0, dtype=torch.float64, device=dev, requires_grad=True)
     sg.surfaces[5].geometry.k = t
     leaves.append(t)
     t0 = float(sg.surfaces[th].thickness)
-    t = torch.tensor(t0, dtype=torch.float64, device="cuda", requires_grad=True)
+    t = torch.tensor(t0, dtype=torch.float64, device=dev, requires_grad=True)
     for s in sg.surfaces[th + 1:]:
         s.geometry.cs.z = float(s.geometry.cs.z) + (t - t0)
     leaves.append(t)
@@ -188,7 +202,7 @@ def test_seam_gradient_radius_conic_thickness_matches_reference(torch, th):
     np.testing.assert_allclose(got, g[f"t{th}_grad"], rtol=1e-9, atol=1e-12)
 
 
-def test_seam_gradcheck_rays_and_records(torch):
+def test_seam_gradcheck_rays_and_records(torch, dev):
     """Input-ray cotangents and record cotangents (central differences of the HIP
     forward): image and intermediate-surface records of the Cooke triplet w.r.t. the input
     x, y, L, M and a radius, all in one backward."""
@@ -197,7 +211,7 @@ def test_seam_gradcheck_rays_and_records(torch):
     from optiland_pr_amd.samples import CookeTriplet
 
     lens = CookeTriplet()
-    base = _generated(torch, lens, 0.0, 0.7, 0.55, 2, "hexapolar")  # 7 rays
+    base = _generated(torch, lens, 0.0, 0.7, 0.55, 2, dev, "hexapolar")  # 7 rays
     sg = lens.surface_group
     R0 = float(sg.surfaces[3].geometry.radius)
 
@@ -212,19 +226,19 @@ def test_seam_gradcheck_rays_and_records(torch):
         return r.x, r.y, r.opd, s2.x, s2.L, s4.y, s4.opd
 
     inputs = tuple(getattr(base, a).clone().requires_grad_(True) for a in ("x", "y", "L", "M"))
-    R = torch.tensor(R0, dtype=torch.float64, device="cuda", requires_grad=True)
+    R = torch.tensor(R0, dtype=torch.float64, device=dev, requires_grad=True)
     assert torch.autograd.gradcheck(f, (*inputs, R), eps=1e-7, atol=1e-6, rtol=1e-5,
                                     nondet_tol=1e-12)
 
 
-def test_seam_intensity_cotangents(torch):
+def test_seam_intensity_cotangents(torch, dev):
     """d i / d i_in through clipping and absorption (record and output intensity rows)."""
     from optiland_pr_amd.adapter import _trace_on_mi355x
     from optiland_pr_amd.samples import GOLDEN_LENSES
 
     lens = GOLDEN_LENSES["cooke_aperture"]()
-    rays = _generated(torch, lens, 0.0, 1.0, 0.55, 8)
-    i_in = (0.5 + torch.arange(rays.i.numel(), dtype=torch.float64, device="cuda") / 100)
+    rays = _generated(torch, lens, 0.0, 1.0, 0.55, 8, dev)
+    i_in = (0.5 + torch.arange(rays.i.numel(), dtype=torch.float64, device=dev) / 100)
     rays.i = i_in.clone().requires_grad_(True)
     leaf = rays.i
     _trace_on_mi355x(lens.surface_group, rays, 0)
@@ -236,7 +250,7 @@ def test_seam_intensity_cotangents(torch):
                                rtol=1e-14)
 
 
-def test_seam_skip_and_cache(torch, golden_index):
+def test_seam_skip_and_cache(torch, dev, golden_index):
     """skip = 3: surfaces before it keep empty records (SurfaceGroup.reset); a second call
     with an unchanged lens reuses the uploaded tables, an edited one re-uploads."""
     from optiland_pr_amd.adapter import _trace_on_mi355x
@@ -254,8 +268,8 @@ def test_seam_skip_and_cache(torch, golden_index):
     from optiland_pr_amd.raytrace import RealRays
 
     rec = g["records"][pair]
-    rays = RealRays(*(torch.as_tensor(rec[2, f], device="cuda") for f in range(7)), wl)
-    rays.opd = torch.as_tensor(rec[2, 7], device="cuda")
+    rays = RealRays(*(torch.as_tensor(rec[2, f], device=dev) for f in range(7)), wl, device=dev)
+    rays.opd = torch.as_tensor(rec[2, 7], device=dev)
     _trace_on_mi355x(sg, rays, 3)
     for a in ("x", "y", "z", "L", "M", "N", "opd"):
         np.testing.assert_array_equal(getattr(rays, a).cpu().numpy(), g[a][sl], err_msg=a)
@@ -263,14 +277,14 @@ def test_seam_skip_and_cache(torch, golden_index):
         assert np.size(sg.surfaces[si].x) == 0
     np.testing.assert_array_equal(sg.surfaces[5].y.cpu().numpy(), rec[5, 1])
     (dl1,) = sg._ort_lenses.values()
-    _trace_on_mi355x(sg, _rays(torch, g, sl, wl), 0)
+    _trace_on_mi355x(sg, _rays(torch, g, sl, wl, dev), 0)
     assert list(sg._ort_lenses.values())[0] is dl1
     sg.surfaces[1].geometry.radius = float(sg.surfaces[1].geometry.radius) * 1.01
-    _trace_on_mi355x(sg, _rays(torch, g, sl, wl), 0)
+    _trace_on_mi355x(sg, _rays(torch, g, sl, wl, dev), 0)
     assert list(sg._ort_lenses.values())[0] is not dl1
 
 
-def test_seam_refuses_undifferentiated_values(torch):
+def test_seam_refuses_undifferentiated_values(torch, dev):
     """A lens value the derivative kernels do not carry (a decenter, a normalisation
     radius) that requires grad makes the seam hand the call back to the reference loop
     (Unsupported) instead of detaching it; values that need no grad pass."""
@@ -278,7 +292,7 @@ def test_seam_refuses_undifferentiated_values(torch):
     from optiland_pr_amd.samples import CookeTriplet, ThreeMirrorAnastigmat
 
     lens = CookeTriplet()
-    rays = _generated(torch, lens, 0.0, 1.0, 0.55, 4)
+    rays = _generated(torch, lens, 0.0, 1.0, 0.55, 4, dev)
     lens.surface_group.surfaces[2].geometry.cs.x = torch.tensor(0.0, dtype=torch.float64,
                                                                 requires_grad=True)
     with pytest.raises(Unsupported, match="cs.x"):
@@ -287,7 +301,7 @@ def test_seam_refuses_undifferentiated_values(torch):
         _trace_on_mi355x(lens.surface_group, rays, 0)
 
     tma = ThreeMirrorAnastigmat()
-    rays = _generated(torch, tma, 0.0, 1.0, 0.587, 4)
+    rays = _generated(torch, tma, 0.0, 1.0, 0.587, 4, dev)
     geo = tma.surface_group.surfaces[2].geometry
     geo.norm_radius = torch.tensor(float(geo.norm_radius), dtype=torch.float64,
                                    requires_grad=True)
@@ -295,15 +309,15 @@ def test_seam_refuses_undifferentiated_values(torch):
         _trace_on_mi355x(tma.surface_group, rays, 0)
 
 
-def test_op_is_registered_and_custom(torch):
+def test_op_is_registered_and_custom(torch, dev):
     """The seam's one autograd node is the registered custom op."""
     from optiland_pr_amd.adapter import _trace_on_mi355x
     from optiland_pr_amd.samples import CookeTriplet
 
     lens = CookeTriplet()
-    rays = _generated(torch, lens, 0.0, 1.0, 0.55, 4)
+    rays = _generated(torch, lens, 0.0, 1.0, 0.55, 4, dev)
     R = torch.tensor(float(lens.surface_group.surfaces[1].geometry.radius),
-                     dtype=torch.float64, device="cuda", requires_grad=True)
+                     dtype=torch.float64, device=dev, requires_grad=True)
     lens.surface_group.surfaces[1].geometry.radius = R
     _trace_on_mi355x(lens.surface_group, rays, 0)
     assert "trace_sequential" in type(rays.x.grad_fn).__name__ or \
