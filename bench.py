@@ -255,47 +255,72 @@ def config4(args, dev, rank, world, torch):
     seg_dev = upload_segments(seg, dev)
     n = n_loc * len(pairs)
     out = RealRays.empty(n, 0.0, device=dev)
-    # the image-plane gather into rank 0: send / receive buffers allocated here, once
-    gather = distributed.ImageGather(len(pairs), n_p, dev) if world > 1 else None
+    # N > 1: the image-plane gather into rank 0 (send / receive buffers allocated here,
+    # once), pipelined with the trace: 7 chunks of 7 pairs, each chunk's x, y traced into
+    # the send slab and gathered asynchronously (RCCL on its own stream) while the next
+    # chunk traces (distributed.PipelinedImageTrace). The gathered shards stay in rank 0's
+    # receive slabs (the reference-order reassembly is ImageGather.finish(assemble=True),
+    # outside the step)
+    gather = pipe = None
+    if world > 1:
+        gather = distributed.ImageGather(len(pairs), n_p, dev)
+        pipe = distributed.PipelinedImageTrace(dl, seg, px, py, gather, chunks=args.gather_chunks)
 
     def step():
-        trace_pupil(dl, seg_dev, px, py, out, n, n_loc, n, pupil_per_ray=True)
-        if gather is not None:
-            gather.gather(out.x, out.y)
+        if pipe is not None:
+            pipe.run(assemble=False)
+        else:
+            trace_pupil(dl, seg_dev, px, py, out, n, n_loc, n, pupil_per_ray=True)
 
     def trace_ms(steps):
-        """Device time of the trace launch alone (at N > 1 the step also gathers): events
-        on the launch stream around each launch, over extra steps after the timed region."""
+        """Device time of the trace launches alone (at N > 1 the step also gathers): events
+        on the launch stream around them, over extra steps after the timed region."""
         stream = torch.cuda.current_stream()
         spans = []
         for _ in range(steps):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-            trace_pupil(dl, seg_dev, px, py, out, n, n_loc, n, pupil_per_ray=True)
+            if pipe is not None:
+                pipe.trace_only()
+            else:
+                trace_pupil(dl, seg_dev, px, py, out, n, n_loc, n, pupil_per_ray=True)
             e1.record(stream)
             spans.append((e0, e1))
         torch.cuda.synchronize()
         return sum(a.elapsed_time(b) for a, b in spans) / steps
 
     def gather_report(reps=5):
-        """The gather alone, after the timed region (every rank): bytes a rank sends, bytes
-        rank 0 receives, and the max-over-ranks time per gather."""
+        """After the timed region (every rank): bytes a rank sends, bytes rank 0
+        receives, the max-over-ranks time of the gather alone (all chunks, nothing
+        tracing) and of the trace alone, and the pipelined step: gather_exposed_ms =
+        step - trace is what the overlap did not hide."""
         if gather is None:
             return {"gather_bytes_per_rank": 0, "gather_bytes_into_rank0": 0, "gather_ms": 0.0}
         import torch.distributed as dist
 
-        dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            gather.gather(out.x, out.y)
-        torch.cuda.synchronize()
-        t = torch.tensor([(time.perf_counter() - t0) / reps], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        def timed(fn):
+            dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                fn()
+            torch.cuda.synchronize()
+            t = torch.tensor([(time.perf_counter() - t0) / reps], dtype=torch.float64,
+                             device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            return float(t.item()) * 1e3
+
+        g_ms = timed(lambda: gather.finish(gather.gather_pairs(0, len(pairs)), assemble=False))
+        t_ms = timed(pipe.trace_only)
+        s_ms = timed(lambda: pipe.run(assemble=False))
         recv = torch.tensor([gather.bytes_received], dtype=torch.float64, device=dev)
         dist.all_reduce(recv, op=dist.ReduceOp.MAX)
         return {"gather_bytes_per_rank": gather.send.numel() * 8,
-                "gather_bytes_into_rank0": int(recv.item()), "gather_ms": float(t.item()) * 1e3}
+                "gather_bytes_into_rank0": int(recv.item()), "gather_ms": g_ms,
+                "trace_ms": t_ms, "pipelined_step_ms": s_ms,
+                "gather_exposed_ms": max(0.0, s_ms - t_ms),
+                "gather_hidden_ms": max(0.0, g_ms - max(0.0, s_ms - t_ms)),
+                "gather_chunks": len(pipe.chunks), "gather_zero_copy": pipe.zero_copy}
 
     return Workload(
         metric="ray-surface intersections/sec, ReverseTelephoto 7 fields x 7 lambda x 2M rays, "
@@ -331,17 +356,55 @@ def config5(args, dev, rank, world, torch):
                          requires_grad=True)
         g.coefficients = t
         leaves.append(t)
-    # one fused Adam kernel for the 30 coefficients (instead of the foreach sequence)
-    opt = torch.optim.Adam(leaves, lr=1e-7, fused=True)
+    # one fused Adam kernel for the 30 coefficients (instead of the foreach sequence);
+    # capturable: its step count lives on the device, so the step can be a graph replay
+    use_graph = not args.eager
+    opt = torch.optim.Adam(leaves, lr=1e-7, fused=True, capturable=use_graph)
     S = 4
     state = {}
 
-    def step():
+    def eager_step():
         opt.zero_grad()
         loss = RayOperand.rms_spot_size(lens, -1, 0.0, 1.0, R, 0.587, d)
         loss.backward()
         opt.step()
         state["loss"] = loss.detach()  # read once after the timed region (no per-step sync)
+
+    graph = {}
+
+    def graph_step():
+        """The whole optimisation step -- coefficient patch, taped trace with its
+        device-verified Newton rounds, rms_spot, the adjoint VJP, the fused Adam update --
+        as ONE HIP graph replay: the host issues one launch per step instead of ~40
+        (every op of the step is free of host synchronisation)."""
+        g = graph.get("g")
+        if g is None:
+            # warm the Newton schedules, workspaces and caches off the capture, then capture
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                for _ in range(3):
+                    eager_step()
+            torch.cuda.current_stream().wait_stream(side)
+            torch.cuda.synchronize()
+            opt.zero_grad(set_to_none=True)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                loss = RayOperand.rms_spot_size(lens, -1, 0.0, 1.0, R, 0.587, d)
+                loss.backward()
+                opt.step()
+            state["loss"] = loss.detach()
+            graph["g"] = g
+        g.replay()
+
+    def check():  # the captured device-verified Newton rounds: flags of the last replay
+        from optiland_pr_amd import raytrace
+
+        for dl in getattr(lens, "_lowered", {}).values():
+            raytrace.check_graph_flags(dl)
+
+    state["check"] = check
+    step = graph_step if use_graph else eager_step
 
     return Workload(
         metric="TMA Zernike optimisation steps: ray-surface intersections/sec of forward + "
@@ -351,11 +414,19 @@ def config5(args, dev, rank, world, torch):
                             "1M random rays, Hy=1, lambda 0.587: lens update + trace + "
                             "rms_spot_size + backward (VJP) + Adam",
                 "rays_per_gpu": R, "surfaces": S, "parameters": 30,
-                "parallelism": f"dp{world} (independent replicas)"},
+                "parallelism": f"dp{world} (independent replicas)",
+                "step_issue": "one HIP graph replay per step (captured after 3 eager steps)"
+                              if use_graph else "eager (torch ops + ctypes launches)"},
         kernel="adj_kernel<KM_ZERN, 2> (ort_trace_pupil_vjp, adjoint mode)", launches=None,
         bytes_per_launch=None, flops_per_ray=None, pmc_file="hbm_traffic_c5.json", rays=R,
-        state=state, vjp_timer=vjp_timer,
-        tape_bytes_per_launch=2 * S * 11 * 8 * R)  # ort_adjoint.h kTapeRows: written + read
+        state=state, vjp_timer=vjp_timer, eager_step=eager_step,
+        # the taped forward writes the tape, the adjoint only reads it: S x kTapeRows
+        # (ort_sweep.h) doubles per ray
+        tape_bytes_per_launch=S * 11 * 8 * R,
+        # the adjoint launch's algorithmic HBM bytes: the tape read, the pupil samples
+        # (16 B/ray), the primal outputs it reads (L, M, N, i: 32 B/ray), the cotangents
+        # (x, y: 16 B/ray) and the wave partials written (30 Zernike slots + 1 per 64 rays)
+        algorithmic_bytes_per_launch=S * 11 * 8 * R + (16 + 32 + 16) * R + 31 * 8 * (R // 64))
 
 
 def vjp_timer(step, steps, torch):
@@ -390,6 +461,11 @@ def main():
     ap.add_argument("--newton-mode", default="reference", choices=["reference", "wave"],
                     help="config 3: the reference's global Newton stop rule (exact) or the "
                          "per-wavefront stop (within the Newton tolerance)")
+    ap.add_argument("--gather-chunks", type=int, default=7,
+                    help="config 4 at N > 1: pair chunks of the pipelined trace + gather")
+    ap.add_argument("--eager", action="store_true",
+                    help="config 5: issue the optimisation step eagerly instead of as one HIP "
+                         "graph replay")
     ap.add_argument("--cpu-rays", type=int, default=1_000_000)
     ap.add_argument("--cpu-seconds", type=float, default=1.5,
                     help="wall time of the multi-process CPU baseline leg")
@@ -469,7 +545,8 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     extra = w.extra() if getattr(w, "extra", None) else None  # every rank (collectives)
     if getattr(w, "vjp_timer", None):
-        w.vjp_ms = w.vjp_timer(w.step, max(3, min(args.steps, 20)), torch)
+        w.vjp_ms = w.vjp_timer(getattr(w, "eager_step", w.step), max(3, min(args.steps, 20)),
+                               torch)
     if getattr(w, "trace_timer", None):
         kern_ms = w.trace_timer(max(3, min(args.steps, 20)))
 
@@ -500,10 +577,12 @@ def main():
             line["roofline_fp64"] = _roofline_fp64(w, kern_ms)
         S = w.config.get("surfaces")
         if S:  # the reference notebook counts len(surfaces) = S + 1 per ray
-            line["reference_convention"] = {
-                "value": value * (S + 1) / S, "surfaces_counted": S + 1,
-                "note": "the same run counted as the reference's notebook does "
-                        "(object surface included, no intersection computed for it)"}
+            line["counting_convention"] = {
+                "surfaces_counted_in_value": S,
+                "reference_notebook_surfaces_per_ray": S + 1,
+                "note": "value counts traced surfaces only; the reference's notebook counts "
+                        "len(surfaces) = S + 1 per ray (the object surface computes no "
+                        "intersection): multiply by (S + 1) / S to compare with its figures"}
         if getattr(w, "spot", False):
             st = w.state["stats"].cpu().numpy()
             line["config"]["rms_spot_radius_mm"] = [float(v) for v in st[:, 3]]
@@ -512,6 +591,8 @@ def main():
             from optiland_pr_amd import raytrace
 
             raytrace.check_all_pending()  # device-verified Newton schedules: raise here
+            if "check" in w.state:
+                w.state["check"]()
             loss = w.state.get("loss")
             line["config"]["final_loss"] = None if loss is None else float(loss)
         if extra:
@@ -541,12 +622,14 @@ def _roofline(w, kern_ms):
                 "traffic": pmc.get("bytes_per_launch"), "kernel": w.kernel,
                 "kernel_ms": w.vjp_ms, "step_device_ms": kern_ms,
                 "tape_bytes_per_launch": w.tape_bytes_per_launch,
+                "algorithmic_bytes_per_launch": w.algorithmic_bytes_per_launch,
                 "hbm_frac": None if pmc.get("bytes_per_launch") is None else
                 pmc["bytes_per_launch"] / (w.vjp_ms * 1e-3) / 1e9 / (SPEC_HBM_TBPS * 1e3),
                 "note": "achieved = hardware-counted FP64 FLOPs of adj_kernel "
                         f"(SQ_INSTS_VALU_FLOPS_FP64 x 64, profiles/{w.pmc_file}) / the live "
                         "device time of the ort_trace_pupil_vjp launch sequence; traffic = "
-                        "its rocprofv3 FETCH/WRITE bytes (the tape is written and read back)"}
+                        "its rocprofv3 FETCH/WRITE bytes; the taped forward writes the tape, "
+                        "the adjoint only reads it (tape_bytes_per_launch)"}
     if w.bytes_per_launch is None:
         return {"bound": "fp64_valu", "achieved": None, "peak": SPEC_FP64_VEC_TFLOPS,
                 "unit": "TFLOP/s", "frac": None, "traffic": None, "kernel": w.kernel,
@@ -658,10 +741,13 @@ def _cpu_task(k_lo_hi):
 def _cpu_baseline(args):
     """The oracle (NumPy restatement of the reference, oracle/trace_np.py) on this host's
     cores: a bounded sample of the bench workload (up to 3 (field, lambda) pairs) split
-    into contiguous ray chunks over a pool of min(16, cpu_count) forked worker processes
-    (each chunk is its own trace call: for Newton lenses the global stop rule then spans
-    a chunk), repeated for ~--cpu-seconds of wall time (pool start-up excluded); the
-    single-process rate of one repetition is reported alongside."""
+    into contiguous ray chunks over a pool of forked worker processes (each chunk is its
+    own trace call: for Newton lenses the global stop rule then spans a chunk). As
+    BASELINE.md's plan asks: one warm-up, then the median of (at least) 5 timed
+    repetitions, for the pool (repeated until ~--cpu-seconds of wall time) and for one
+    process. Workers: the CPUs this process may run on (sched_getaffinity), capped by the
+    box's CPU share (OMP_NUM_THREADS, 16 per GPU on the GPU pool: os.cpu_count() there is
+    the whole machine's 256)."""
     import multiprocessing as mp
 
     from optiland_pr_amd.distribution import RandomDistribution
@@ -680,27 +766,40 @@ def _cpu_baseline(args):
     _CPU["w"] = (table, segs, px, py)
     S = table.n_surfaces
     units = n_rays * len(segs) * S
-    t0 = time.perf_counter()
-    for k in range(len(segs)):
-        _cpu_task((k, 0, n_rays))
-    t_single = time.perf_counter() - t0
-    workers = max(1, min(16, os.cpu_count() or 1))
+
+    def sample():
+        for k in range(len(segs)):
+            _cpu_task((k, 0, n_rays))
+
+    sample()  # warm-up
+    singles = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        sample()
+        singles.append(time.perf_counter() - t0)
+    t_single = float(np.median(singles))
+    affinity = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (
+        os.cpu_count() or 1)
+    share = int(os.environ.get("OMP_NUM_THREADS") or affinity)
+    workers = max(1, min(affinity, share))
     chunk = -(-n_rays // workers)
     tasks = [(k, lo, min(n_rays, lo + chunk)) for k in range(len(segs))
              for lo in range(0, n_rays, chunk)]
     with mp.get_context("fork").Pool(workers) as pool:
-        pool.map(_cpu_task, [(0, 0, min(n_rays, 64))] * workers)  # warm the workers
-        # repeat the sample until ~args.cpu_seconds of wall time (x workers of CPU work)
-        reps = 0
-        t0 = time.perf_counter()
+        pool.map(_cpu_task, tasks, chunksize=1)  # warm-up repetition
+        # repeat the sample until ~args.cpu_seconds of wall time, at least 5 times
+        times = []
+        t_all = time.perf_counter()
         while True:
+            t0 = time.perf_counter()
             pool.map(_cpu_task, tasks, chunksize=1)
-            reps += 1
-            t = time.perf_counter() - t0
-            if t >= args.cpu_seconds and reps >= 2:
+            times.append(time.perf_counter() - t0)
+            if time.perf_counter() - t_all >= args.cpu_seconds and len(times) >= 5:
                 break
+    reps = len(times)
+    t = float(np.median(times))
     ratio = _ref_over_oracle()
-    value = units * reps / t
+    value = units / t
     line = {
         "value": value,
         "unit": "intersections/s",
@@ -708,11 +807,15 @@ def _cpu_baseline(args):
         "kind": "port",
         "single_process_value": units / t_single,
         "host_cpus": os.cpu_count(),
+        "affinity_cpus": affinity,
+        "cpu_share": share,
         "cpu_model": _cpu_model(),
+        "statistic": "median of the timed repetitions after one warm-up",
         "sample": f"{label}: {n_rays} rays x {len(segs)} (field, lambda) pair(s) x {S} "
-                  f"surfaces (generation + trace), NumPy oracle, {workers} processes x {reps} "
-                  f"repetitions: {t:.2f} s wall (1 process, 1 repetition: {t_single:.2f} s); "
-                  f"{workers} of the {os.cpu_count()} host CPUs = the GPU box's CPU share",
+                  f"surfaces (generation + trace), NumPy oracle; {workers} processes, median "
+                  f"of {reps} repetitions {t:.3f} s (1 process: median of 5, {t_single:.3f} s); "
+                  f"workers = min(CPUs in this process's affinity mask {affinity}, the box's CPU "
+                  f"share OMP_NUM_THREADS {share}) of the {os.cpu_count()} host CPUs",
     }
     if ratio:
         # the reference itself (Optiland's NumPy backend) is slower than its restatement:

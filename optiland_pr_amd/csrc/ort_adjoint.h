@@ -62,15 +62,20 @@ struct DevLane {
   }
   __device__ inline int64_t tape_stride() const { return n_rays; }
   __device__ inline int uniform_max(int v) const { return wave_max_i32(v); }
+  // ORT_ADJ_NO_PARK (A/B builds): keep the state in registers
   __device__ inline void park(const double (&v)[10]) {
+#ifndef ORT_ADJ_NO_PARK
 #pragma unroll
     for (int k = 0; k < 10; ++k) park_lds[k][threadIdx.x] = v[k];
     asm volatile("" ::: "memory");
+#endif
   }
   __device__ inline void unpark(double (&v)[10]) {
+#ifndef ORT_ADJ_NO_PARK
     asm volatile("" ::: "memory");
 #pragma unroll
     for (int k = 0; k < 10; ++k) v[k] = park_lds[k][threadIdx.x];
+#endif
   }
 };
 

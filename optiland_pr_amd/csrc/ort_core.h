@@ -1113,6 +1113,143 @@ ORT_INLINE void zernike_coef_adjoint(double x, double y, double Rn, PZ Tm, int t
   }
 }
 
+// Second-order local model of a Zernike surface at (x, y), in plain doubles, for the
+// adjoint VJP: the sag and its gradient, the slopes (dzdx, dzdy) the reference's normal is
+// built from (zernike.py:163-231: conic part x / (R q) plus the terms' chain rule through
+// rho and phi, without the normalisation constant) and their Jacobian. The adjoint needs
+// exactly these -- the Newton update's f, f_x, f_y and the normal's x / y derivatives --
+// and the dual-number evaluation of sagnorm_zernike it replaces carries three values
+// through every operation (with the adjoint state alive around it the kernel spilled).
+// Per term c R(rho) A(phi), R = H(rho^2) rho^|m| from the radial table, the sums
+//   Q_r = sum c R' A, Q_p = sum c R A', Q_rr = sum c R'' A, Q_rp = sum c R' A',
+//   Q_pp = sum c R A''  (A'' = -m^2 A)
+// are formed once over the terms and mapped to x, y by the derivatives of rho = r / R_n
+// and phi = atan2(y, x) (1 / rho guarded by the reference's eps, as its normal does).
+// Values agree with sagnorm_zernike's to rounding, not bit for bit: they enter only the
+// derivative. Zero coefficients are skipped, as the reference's normal skips them.
+struct SurfJet {
+  double z, zx, zy;      // sag, d sag / dx, d sag / dy (the terms' normalisation included)
+  double sx, sy;         // the normal's slopes
+  double sxx, sxy, syy;  // d sx / dx, d sx / dy (= d sy / dx), d sy / dy
+};
+
+template <class PD, class PZ>
+ORT_INLINE void zernike_jet(double x, double y, double R, double k, double Rn, PZ Tm, int t0,
+                            int nt, PD coef, SurfJet& J) {
+  // base conic (standard.py:73-87, 154-167): z = r2 / (R (1 + q)), slope x / (R q)
+  const double r2 = x * x + y * y;
+  const double q = sqrt(1.0 - (1.0 + k) * r2 / (R * R));
+  const double iRq = 1.0 / (R * q);
+  const double h = (1.0 + k) * iRq * iRq * iRq;  // (1 + k) / (R q)^3
+  J.z = r2 / (R * (1.0 + q));
+  J.sx = x * iRq;
+  J.sy = y * iRq;
+  J.sxx = iRq + h * x * x;
+  J.sxy = h * x * y;
+  J.syy = iRq + h * y * y;
+  const double xn = x / Rn, yn = y / Rn;
+  const double rho = sqrt(xn * xn + yn * yn);
+  double c1 = 1.0, s1 = 0.0;  // cos / sin phi (atan2(0, 0) = 0)
+  if (rho > 0.0) {
+    c1 = xn / rho;
+    s1 = yn / rho;
+  }
+  const double u = rho * rho;
+  double Z = 0.0, Gr = 0.0, Gp = 0.0, Qr = 0.0, Qp = 0.0, Qrr = 0.0, Qrp = 0.0, Qpp = 0.0;
+  for (int j = 0; j < nt; ++j) {
+    const ort_zernike_term t = Tm[t0 + j];
+    if (t.c == 0.0) continue;
+    const int am = t.m >= 0 ? t.m : -t.m;
+    double cm = 1.0, sm = 0.0, pw = 1.0;  // cos(am phi), sin(am phi), rho^am
+#pragma unroll 1
+    for (int qq = 0; qq < am; ++qq) {
+      const double cn = cm * c1 - sm * s1;
+      sm = sm * c1 + cm * s1;
+      cm = cn;
+      pw = pw * rho;
+    }
+    // H(u) and its first two derivatives (Horner), R = H rho^am
+    const PD a = coef + t.rad_off;
+    double H = a[0], H1 = 0.0, H2 = 0.0;
+#pragma unroll 1
+    for (int kk = 1; kk < t.n_rad; ++kk) {
+      H2 = H2 * u + H1;
+      H1 = H1 * u + H;
+      H = H * u + a[kk];
+    }
+    H2 = 2.0 * H2;
+    const double F = 2.0 * u * H1 + am * H;  // rho^(1 - am) R'
+    double P, P1, P2;  // R, R', R''
+    if (am == 0) {
+      P = H;
+      P1 = 2.0 * rho * H1;
+      P2 = 2.0 * H1 + 4.0 * u * H2;
+    } else if (am == 1) {
+      P = H * rho;
+      P1 = F;
+      P2 = 2.0 * rho * (3.0 * H1 + 2.0 * u * H2);
+    } else {
+      const double pw2 = pw / (rho * rho);  // rho^(am - 2) (rho > 0 here, else pw = 0)
+      P = H * pw;
+      P1 = rho > 0.0 ? F * (pw / rho) : 0.0;
+      P2 = rho > 0.0 ? pw2 * ((am - 1.0) * F + 2.0 * u * ((2.0 + am) * H1 + 2.0 * u * H2))
+                     : (am == 2 ? 2.0 * H : 0.0);
+    }
+    double A, A1;  // A(phi), dA / dphi (base.py:206-226: cos m phi, sin |m| phi)
+    if (t.m > 0) {
+      A = cm;
+      A1 = -(double)am * sm;
+    } else if (t.m < 0) {
+      A = sm;
+      A1 = (double)am * cm;
+    } else {
+      A = 1.0;
+      A1 = 0.0;
+    }
+    const double cz = t.c, cn = t.c * t.norm;
+    Z += cn * P * A;
+    Gr += cn * P1 * A;
+    Gp += cn * P * A1;
+    Qr += cz * P1 * A;
+    Qp += cz * P * A1;
+    Qrr += cz * P2 * A;
+    Qrp += cz * P1 * A1;
+    Qpp -= cz * (double)(am * am) * P * A;
+  }
+  const double eps = 1e-14;
+  const double ir = 1.0 / ((rho + eps) * Rn);  // 1 / (rho R_n), guarded
+  const double rx = c1 / Rn, ry = s1 / Rn;     // d rho / dx, d rho / dy
+  const double px = -s1 * ir, py = c1 * ir;    // d phi / dx, d phi / dy
+  const double rxx = s1 * s1 * ir / Rn, rxy = -c1 * s1 * ir / Rn, ryy = c1 * c1 * ir / Rn;
+  const double pxx = 2.0 * c1 * s1 * ir * ir, pxy = (s1 * s1 - c1 * c1) * ir * ir;
+  J.z += Z;
+  J.zx = J.sx + Gr * rx + Gp * px;
+  J.zy = J.sy + Gr * ry + Gp * py;
+  J.sx += Qr * rx + Qp * px;
+  J.sy += Qr * ry + Qp * py;
+  J.sxx += Qrr * rx * rx + 2.0 * Qrp * rx * px + Qpp * px * px + Qr * rxx + Qp * pxx;
+  J.sxy += Qrr * rx * ry + Qrp * (rx * py + ry * px) + Qpp * px * py + Qr * rxy + Qp * pxy;
+  J.syy += Qrr * ry * ry + 2.0 * Qrp * ry * py + Qpp * py * py + Qr * ryy - Qp * pxx;
+}
+
+// the unit normal n = (sx, sy, -1) / |(sx, sy, -1)| of a jet and its x / y derivatives:
+// dn = (dg - n (n . dg)) / |g| with dg = (sxx, sxy, 0) resp. (sxy, syy, 0)
+template <int P>
+ORT_INLINE void jet_normal(const SurfJet& J, Dual<P>& nx, Dual<P>& ny, Dual<P>& nz) {
+  const double g = sqrt(J.sx * J.sx + J.sy * J.sy + 1.0);
+  const double ig = 1.0 / g;
+  nx = Dual<P>(J.sx * ig);
+  ny = Dual<P>(J.sy * ig);
+  nz = Dual<P>(-ig);
+  const double ex = nx.v * J.sxx + ny.v * J.sxy, ey = nx.v * J.sxy + ny.v * J.syy;
+  nx.d[0] = (J.sxx - nx.v * ex) * ig;
+  ny.d[0] = (J.sxy - ny.v * ex) * ig;
+  nz.d[0] = -nz.v * ex * ig;
+  nx.d[1] = (J.sxy - nx.v * ey) * ig;
+  ny.d[1] = (J.syy - ny.v * ey) * ig;
+  nz.d[1] = -nz.v * ey * ig;
+}
+
 // ---- Forbes Q-polynomials: forbes/geometry.py:83-640 + forbes/qpoly.py --------------
 // The lens-only constants (orthonormal-basis coefficients, recurrence A/B/C, the Q-2D
 // vertex slope) come precomputed in the coefficient block (optiland_pr_amd/forbes.py);

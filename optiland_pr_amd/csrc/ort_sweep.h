@@ -455,6 +455,20 @@ ORT_INLINE void adj_ray(const KArgs& a, const AArgs& j, Lane& ln, int64_t rid, b
       return D(0.0);
     }
     bool rerr = false;
+    if constexpr (P == 2 && (KM & ort::KM_ZERN) != 0) {
+      // Zernike: the plain-double second-order model (ort::zernike_jet) instead of the
+      // dual-number evaluation -- the same derivatives, a fraction of the registers
+      if (KM == ort::KM_ZERN || s.geometry == ORT_GEOM_ZERNIKE) {
+        ort::SurfJet J;
+        ort::zernike_jet(x, y, s.radius, s.conic, s.norm_radius, cst(a.zern), s.coef_off,
+                         s.n_coef, cst(a.coef), J);
+        ort::jet_normal(J, nx, ny, nz);
+        D z(J.z);
+        z.d[0] = J.zx;
+        z.d[1] = J.zy;
+        return z;
+      }
+    }
     if constexpr (KM == 0) {
       nx = ny = nz = D(__builtin_nan(""));
       return D(__builtin_nan(""));
@@ -633,7 +647,11 @@ ORT_INLINE void adj_ray(const KArgs& a, const AArgs& j, Lane& ln, int64_t rid, b
     (void)sagnorm(s, x1, y1, nx, ny, nz);
 
     // globalize adjoint: + cs_t, then the op list transposed in reverse
-    double bCZ = b.z;
+    // surface slots (radius, conic, vertex z) have tangents only with P = 4: the launch
+    // takes P = 2 exactly when no surface tangent table is given (ort_api.hip vjp_run), so
+    // then their adjoints are not carried at all
+    constexpr bool kSurf = P == 4;
+    double bCZ = kSurf ? b.z : 0.0;
     for (int c = s.n_cs_glob - 1; c >= 0; --c) {
       const ort_cs_op op = cst(a.cs)[s.cs_glob_off + c];
       adj_cs_op(b, op);
@@ -713,7 +731,7 @@ ORT_INLINE void adj_ray(const KArgs& a, const AArgs& j, Lane& ln, int64_t rid, b
         // The dual-number sag / normal alone needs ~124 VGPRs (the plain one 42), so with the
         // adjoint state live across it the GPU kernel would spill at its 128-VGPR cap. The
         // lane parks the state outside the registers (LDS on the device) across it.
-        double pk[10] = {b.x, b.y, b.z, b.L, b.M, b.N, bopd, batt, tb, bCZ};
+        double pk[10] = {b.x, b.y, b.z, b.L, b.M, b.N, bopd, batt, tb, kSurf ? bCZ : 0.0};
         ln.park(pk);
         const D sk = sagnorm(s, xk, yk, kx, ky, kz);
         ln.unpark(pk);
@@ -726,7 +744,7 @@ ORT_INLINE void adj_ray(const KArgs& a, const AArgs& j, Lane& ln, int64_t rid, b
         bopd = pk[6];
         batt = pk[7];
         tb = pk[8];
-        bCZ = pk[9];
+        if constexpr (kSurf) bCZ = pk[9];
         const double f = sk.v - zk;
         const bool zg = fabs(kz.v) > 1e-14;
         const double nzs = zg ? kz.v : 1e-14;
@@ -773,10 +791,12 @@ ORT_INLINE void adj_ray(const KArgs& a, const AArgs& j, Lane& ln, int64_t rid, b
       const ort_cs_op op = cst(a.cs)[s.cs_loc_off + c];
       adj_cs_op(b, op);
     }
-    bCZ -= b.z;
-    ln.emit(3 * si + 0, bR, true);
-    ln.emit(3 * si + 1, bk, true);
-    ln.emit(3 * si + 2, bCZ, true);
+    if constexpr (kSurf) {
+      bCZ -= b.z;
+      ln.emit(3 * si + 0, bR, true);
+      ln.emit(3 * si + 1, bk, true);
+      ln.emit(3 * si + 2, bCZ, true);
+    }
   }
   // no image-space propagate: the final-thickness slot still gets its (zero) partial,
   // so every needed (slot, wave) partial is written by this launch (no memset)

@@ -108,11 +108,18 @@ class ImageGather:
     """Image-plane intercepts of every rank to ONE rank (the RCCL gather of the
     final intercepts over xGMI): torch.distributed.gather (ncclSend / ncclRecv pairs under
     RCCL, each peer on its own xGMI link into rank dst), not an all-gather -- only dst
-    receives. Buffers are allocated once (constructor) and reused by every gather():
-    the per-rank send slab [fields][n_pairs][max local] (the tail of the shorter shards
-    stays NaN) and, on dst, one receive slab per rank plus the reassembled [n_pairs][n_p]
-    planes in the reference's order (real_ray_tracer.py:74-77).
+    receives. Buffers are allocated once (constructor) and reused by every gather: the
+    per-rank send slab [fields][n_pairs][max local] (the tail of the shorter shards stays
+    NaN) and, on dst, one receive slab per rank plus the reassembled [n_pairs][n_p] planes
+    in the reference's order (real_ray_tracer.py:74-77).
 
+    Pipelining (gather_pairs): the pairs can be gathered in chunks, each an asynchronous
+    collective issued right after the launch that traced those pairs -- RCCL's stream
+    waits for that launch only, so chunk k moves over xGMI while chunk k + 1 traces (a
+    step costs max(trace, gather) instead of their sum). send_views() gives the send slab's
+    rows as the trace's output columns (even shards), so nothing is copied before sending.
+
+    dst is a rank of `group` (translated to the global rank the collective takes).
     Bytes: each rank sends fields x n_pairs x ceil(n_p / world) x 8; dst receives world - 1
     such slabs (config 4 at N = 8, (x, y): 196 MB out of every rank, 1.37 GB into rank 0;
     the all-gather this replaces moved 1.37 GB into EVERY rank)."""
@@ -121,6 +128,9 @@ class ImageGather:
         self.rank, self.world = world_info(group)
         self.group = group
         self.dst = dst
+        self.dst_global = dst
+        if group is not None and self.world > 1:
+            self.dst_global = dist.get_global_rank(group, dst)
         self.n_pairs, self.n_p, self.fields = n_pairs, n_p, fields
         self.sizes = [shard_range(n_p, r, self.world) for r in range(self.world)]
         self.maxloc = max(b - a for a, b in self.sizes)
@@ -141,26 +151,128 @@ class ImageGather:
     def bytes_received(self):
         return (self.world - 1) * self.send.numel() * 8 if self.rank == self.dst else 0
 
+    @property
+    def local(self):
+        a, b = self.sizes[self.rank]
+        return b - a
+
+    def send_views(self):
+        """This rank's send rows as flat [n_pairs * local] columns (one per field) that a
+        trace can write its outputs into directly, or None when this rank's shard is
+        shorter than the slab rows (then gather_pairs copies)."""
+        if self.local != self.maxloc:
+            return None
+        return [self.send[f].view(-1) for f in range(self.fields)]
+
+    def gather_pairs(self, lo, hi, *cols, async_op=True):
+        """Gather pairs [lo, hi): cols are this rank's [pair][local] columns (flat, the
+        whole batch), or nothing when the trace wrote into send_views(). Returns the
+        collectives' work handles (wait() them, or pass them to finish())."""
+        nl = self.local
+        if cols:
+            for f, c in enumerate(cols):
+                src = c.view(self.n_pairs, nl)[lo:hi]
+                dstv = self.send[f, lo:hi, :nl]
+                if src.data_ptr() != dstv.data_ptr():
+                    dstv.copy_(src)
+        works = []
+        for f in range(self.fields):
+            glist = [r[f, lo:hi] for r in self.recv] if self.rank == self.dst else None
+            w = dist.gather(self.send[f, lo:hi], glist, dst=self.dst_global, group=self.group,
+                            async_op=async_op)
+            if w is not None:
+                works.append(w)
+        return works
+
+    def finish(self, works, lo=0, hi=None, assemble=True):
+        """Wait for gather_pairs' work handles; on dst, with assemble, lay pairs [lo, hi)
+        out in the reference's order. Returns the [fields][n_pairs * n_p] planes on dst
+        (None elsewhere)."""
+        for w in works:
+            w.wait()
+        if self.rank != self.dst:
+            return None
+        hi = self.n_pairs if hi is None else hi
+        if assemble:
+            for r, (ra, rb) in enumerate(self.sizes):
+                src = self.send if r == self.rank else self.recv[r]
+                self.planes[:, lo:hi, ra:rb].copy_(src[:, lo:hi, : rb - ra])
+        return self.planes.view(self.fields, -1)
+
     def gather(self, *cols):
         """cols: this rank's [pair][local] arrays (flat), one per field. Returns the
         [fields][n_pairs * n_p] planes on dst (None elsewhere)."""
-        a, b = self.sizes[self.rank]
-        nl = b - a
         if self.world == 1:
             for f, c in enumerate(cols):
                 self.planes[f].copy_(c.view(self.n_pairs, self.n_p))
             return self.planes.view(self.fields, -1)
-        if nl:
-            for f, c in enumerate(cols):
-                self.send[f, :, :nl].copy_(c.view(self.n_pairs, nl))
-        dist.gather(self.send, self.recv if self.rank == self.dst else None, dst=self.dst,
-                    group=self.group)
-        if self.rank != self.dst:
-            return None
-        for r, (ra, rb) in enumerate(self.sizes):
-            src = self.send if r == self.rank else self.recv[r]
-            self.planes[:, :, ra:rb].copy_(src[:, :, : rb - ra])
-        return self.planes.view(self.fields, -1)
+        works = self.gather_pairs(0, self.n_pairs, *cols, async_op=False)
+        return self.finish(works)
+
+
+class PipelinedImageTrace:
+    """This rank's shard of every (field, wavelength) pair traced in pair chunks, each
+    chunk's image-plane x, y handed to an asynchronous ImageGather collective as soon as
+    its launch is queued: RCCL gathers chunk k over xGMI while chunk k + 1 traces, so the
+    step costs max(trace, gather) + one chunk instead of trace + gather (config 4 at
+    N > 1). The trace writes x, y straight into the gather's send slab (even
+    shards). Closed-form lenses only: a Newton lens's schedule check would synchronise
+    every chunk (trace_sharded + ImageGather.gather serve those).
+
+    px, py: this rank's pupil samples, [pair][local] on the device (pupil_per_ray);
+    segs: the pairs' SEGMENT records (host)."""
+
+    def __init__(self, dlens, segs, px, py, gather, chunks):
+        from .raytrace import RealRays, upload_segments
+
+        if dlens.newton:
+            raise ValueError("PipelinedImageTrace: lenses without Newton surfaces only")
+        self.dl, self.gather = dlens, gather
+        n_pairs, nl = gather.n_pairs, gather.local
+        n = n_pairs * nl
+        self.out = RealRays.empty(n, 0.0, device=dlens.device)
+        views = gather.send_views()
+        self.zero_copy = views is not None
+        if self.zero_copy:
+            self.out.x, self.out.y = views[0], views[1]
+        bounds = np.linspace(0, n_pairs, max(1, min(int(chunks), n_pairs)) + 1).astype(int)
+        self.chunks = []
+        for lo, hi in zip(bounds[:-1], bounds[1:], strict=True):
+            if hi == lo:
+                continue
+            sub = RealRays.__new__(RealRays)
+            for a in ("x", "y", "z", "L", "M", "N", "i", "opd"):
+                setattr(sub, a, getattr(self.out, a)[lo * nl:hi * nl])
+            sub.w = self.out.w
+            self.chunks.append((int(lo), int(hi), upload_segments(segs[lo:hi], dlens.device),
+                                px[lo * nl:hi * nl], py[lo * nl:hi * nl], sub))
+
+    def trace_only(self):
+        """The chunks' launches alone (timing)."""
+        from .raytrace import trace_pupil
+
+        nl = self.gather.local
+        for lo, hi, seg_dev, pxc, pyc, sub in self.chunks:
+            nc = (hi - lo) * nl
+            trace_pupil(self.dl, seg_dev, pxc, pyc, sub, nc, nl, nc, pupil_per_ray=True)
+
+    def run(self, assemble=True):
+        """Trace + gather; returns the planes on the gather's dst (assembled into the
+        reference's order when asked), None elsewhere."""
+        from .raytrace import trace_pupil
+
+        nl = self.gather.local
+        works = []
+        for lo, hi, seg_dev, pxc, pyc, sub in self.chunks:
+            nc = (hi - lo) * nl
+            if nc:
+                trace_pupil(self.dl, seg_dev, pxc, pyc, sub, nc, nl, nc, pupil_per_ray=True)
+            if self.gather.world > 1:
+                cols = () if self.zero_copy else (self.out.x, self.out.y)
+                works += self.gather.gather_pairs(lo, hi, *cols)
+        if self.gather.world == 1:
+            return self.gather.gather(self.out.x, self.out.y)
+        return self.gather.finish(works, assemble=assemble)
 
 
 def gather_image_plane(x, y, n_loc_pairs, n_pairs, n_p, group=None, dst=0):

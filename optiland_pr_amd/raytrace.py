@@ -326,17 +326,19 @@ def lens_for(optic_or_group, wavelengths, record=False, image_record=False):
 # launches
 # --------------------------------------------------------------------------------------
 # device-verified Newton schedules (newton_mode="device"): re-launch rounds after the first
-# launch, each one an ort_newton_fixup (check + correct the first wrong surface of each
-# group, initialise the next round's statistics) and a launch that runs only when the
-# check corrected something. A surface needs one round when its schedule was too long
-# (the exact index is read from the statistics) and at most two when too short (grown,
-# then exact), so 2 x (Newton surfaces) + 1 rounds settle any wrong warm schedule;
-# MAX_DEVICE_ROUNDS caps the cost of the no-op rounds (two small launches each).
-MAX_DEVICE_ROUNDS = 7
+# launch, each a verify-and-re-trace launch that corrects the first wrong surface of each
+# group and traces only when it corrected something. A surface needs one round when its
+# schedule was too long (the exact index is read from the statistics) and at most two when
+# too short (grown, then exact), so 2 x (Newton surfaces) + 1 rounds settle ANY wrong warm
+# schedule -- that many are always issued (a no-op round costs ~5 us), so an unsettled
+# schedule cannot reach the backward. MAX_DEVICE_ROUNDS (None: no cap) trades
+# that guarantee for fewer launches; the flag check_pending reads still reports it.
+MAX_DEVICE_ROUNDS = None
 
 
 def device_rounds(dlens):
-    return max(1, min(MAX_DEVICE_ROUNDS, 2 * len(dlens.newton) + 1))
+    r = 2 * len(dlens.newton) + 1
+    return max(1, r if MAX_DEVICE_ROUNDS is None else min(MAX_DEVICE_ROUNDS, r))
 
 
 class NewtonScheduleError(RuntimeError):
@@ -370,6 +372,28 @@ def check_pending(dlens: DeviceLens, block=False):
                 f"(flag {int(flags[R])}): trace again with newton_mode='reference'")
         if p["status"]:
             _raise_status_value(int(status[ran[-1]]))
+
+
+def check_graph_flags(dlens: DeviceLens):
+    """After replays of a HIP graph that captured device-verified traces of this lens
+    (newton_mode="device"): read the last replay's Newton flags and statuses (one
+    synchronising copy) and raise as check_pending would -- NewtonScheduleError when the
+    schedule did not settle in the captured rounds, the range errors' ValueErrors."""
+    p = getattr(dlens, "graph_flags", None)
+    if p is None:
+        return
+    R = p["rounds"]
+    host = p["small"].cpu().numpy()
+    flags, status = host[:R + 1], host[R + 1:2 * R + 2]
+    a, b = p["sched"]
+    dlens.remember(p["keys"], host[a:b].reshape(len(p["keys"]), -1))
+    ran = [0] + [r for r in range(1, R + 1) if flags[r - 1] == 1]
+    if flags[R] != 0:
+        raise NewtonScheduleError(
+            "the Newton schedule did not settle in the captured device-verified rounds "
+            f"(flag {int(flags[R])}): re-capture after a trace with newton_mode='reference'")
+    if p["status"]:
+        _raise_status_value(int(status[ran[-1]]))
 
 
 def check_all_pending():
@@ -470,11 +494,20 @@ def _run_device(dlens: DeviceLens, launch, n_rays, group_len, keys, need_status)
     _native.check(rc, "ort_newton_fixup")
     bufs[2] = new_cur
     dlens._dev_sched[kk] = last
+    off = 2 * R + 2 + (new_cur * ngs if fused else 0)
+    if torch.cuda.is_current_stream_capturing():
+        # captured into a HIP graph (e.g. a whole optimisation step): no host bookkeeping
+        # is replayed, so the flags stay on the device; check_graph_flags() reads them
+        # after the replays (once, with one synchronisation)
+        dlens.graph_flags = dict(small=small, keys=list(keys), status=need_status, rounds=R,
+                                 sched=(off, off + ngs))
+        dlens.last_schedule = None
+        dlens.last_schedule_dev = last
+        return
     host = torch.empty(small.numel(), dtype=torch.int32, pin_memory=True)
     host.copy_(small, non_blocking=True)
     ev = torch.cuda.Event()
     ev.record(torch.cuda.current_stream())
-    off = 2 * R + 2 + (new_cur * ngs if fused else 0)
     dlens.pending.append(dict(event=ev, host=host, keys=list(keys), status=need_status,
                               rounds=R, sched=(off, off + ngs)))
     global _PENDING_LENSES

@@ -58,6 +58,16 @@ def main(rank, world, out):
         else:
             assert planes is None
     res["sent"], res["received"] = g.bytes_sent, g.bytes_received
+    # the pipelined form: pairs gathered in 3 chunks with asynchronous collectives, then
+    # finished (and laid out) chunk by chunk
+    n_pairs = N_FIELDS * N_WL
+    xt, yt = torch.as_tensor(xl).reshape(-1), torch.as_tensor(yl).reshape(-1)
+    bounds = [0, 2, 5, n_pairs]
+    pending = [(lo, hi, g.gather_pairs(lo, hi, xt, yt)) for lo, hi in zip(bounds[:-1], bounds[1:])]
+    for lo, hi, works in pending:
+        planes = g.finish(works, lo, hi)
+    if rank == 0:
+        res["Xc"], res["Yc"] = planes[0].numpy().copy(), planes[1].numpy().copy()
     st = ShardedSpotStatistics(N_FIELDS, N_WL, b - a, REF_WL)
     rows, d = st.run(phase_fn=lambda ph, s1: spot_partials_np(
         xl, yl, il, ph, None if s1 is None else s1.numpy()))

@@ -75,6 +75,30 @@ def main(rank, world, name, out):
     g = ImageGather(n_pairs, n_p, rays.x.device)
     for _ in range(2):  # the pre-allocated buffers are reused
         planes = g.gather(rays.x, rays.y)
+    extra = {}
+    if name == "rt77":  # config 4's pipelined path: pair chunks traced into the send slab,
+        # each chunk gathered asynchronously while the next traces
+        from optiland_pr_amd.distribution import create_distribution  # noqa: F401
+        from optiland_pr_amd.lowering import pupil_scalars, segment_params
+        from optiland_pr_amd.distributed import PipelinedImageTrace, shard_range
+        from optiland_pr_amd.raytrace import lens_for
+
+        optic = LENSES[name]()
+        dl = lens_for(optic, wls)
+        EPL, EPD = pupil_scalars(optic)
+        segs = np.stack([segment_params(optic, float(hx), float(hy), wi, EPL, EPD)
+                         for hx, hy in fields for wi in range(len(wls))])
+        px, py = pupil(name)
+        a, b = shard_range(n_p, rank, world)
+        pxl = torch.as_tensor(np.tile(np.asarray(px[a:b]), n_pairs), device=rays.x.device)
+        pyl = torch.as_tensor(np.tile(np.asarray(py[a:b]), n_pairs), device=rays.x.device)
+        g2 = ImageGather(n_pairs, n_p, rays.x.device)
+        pipe = PipelinedImageTrace(dl, segs, pxl, pyl, g2, chunks=7)
+        for _ in range(2):
+            planes2 = pipe.run()
+        if rank == 0:
+            extra = {"X2": planes2[0].cpu().numpy(), "Y2": planes2[1].cpu().numpy(),
+                     "zero_copy": pipe.zero_copy}
     st = spot_statistics(rays.x, rays.y, rays.i, len(fields), len(wls), len(wls) // 2)
     torch.cuda.synchronize()
     scheds = [None] * world
@@ -82,7 +106,7 @@ def main(rank, world, name, out):
     if rank == 0:
         np.savez(out, X=planes[0].cpu().numpy(), Y=planes[1].cpu().numpy(),
                  sched=np.stack(scheds), received=g.bytes_received,
-                 **{k: v.cpu().numpy() for k, v in st.items()})
+                 **{k: v.cpu().numpy() for k, v in st.items()}, **extra)
     else:
         assert planes is None
     dist.barrier()

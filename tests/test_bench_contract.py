@@ -31,12 +31,16 @@ def test_config4_traffic_scaled_to_the_rank_share():
 
 
 def test_config5_adjoint_roofline():
-    w = _w(pmc_file="hbm_traffic_c5.json", vjp_ms=1.1, tape_bytes_per_launch=704_000_000)
+    R, S = 1_000_000, 4
+    w = _w(pmc_file="hbm_traffic_c5.json", vjp_ms=1.1, tape_bytes_per_launch=S * 11 * 8 * R,
+           algorithmic_bytes_per_launch=S * 11 * 8 * R + 64 * R + 31 * 8 * (R // 64))
     r = bench._roofline(w, 1.95)
     assert ROOFLINE_KEYS <= set(r)
     assert r["bound"] == "fp64_valu" and r["kernel_ms"] == 1.1 and r["step_device_ms"] == 1.95
     assert r["achieved"] > 0 and 0 < r["frac"] < 1
-    assert r["traffic"] > r["tape_bytes_per_launch"]  # tape + register spill
+    # the taped forward writes the tape, the adjoint reads it once (S x 11 doubles per ray)
+    assert r["tape_bytes_per_launch"] == 352_000_000
+    assert r["algorithmic_bytes_per_launch"] > r["tape_bytes_per_launch"]
 
 
 def test_launch_bound_spot_config_has_null_rates():

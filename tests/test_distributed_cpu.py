@@ -62,6 +62,9 @@ def test_gloo_world2_gather_and_stats(tmp_path):
     for rep in range(2):  # gathered into rank 0 only, reassembled in the reference order
         np.testing.assert_array_equal(r0[f"X{rep}"], x.reshape(-1))
         np.testing.assert_array_equal(r0[f"Y{rep}"], y.reshape(-1))
+    # pipelined: chunks of pairs gathered asynchronously, finished chunk by chunk
+    np.testing.assert_array_equal(r0["Xc"], x.reshape(-1))
+    np.testing.assert_array_equal(r0["Yc"], y.reshape(-1))
     assert "X0" not in r1.files
     loc = -(-N_P // 2)  # the padded slab: fields x pairs x ceil(n_p / world) doubles
     assert int(r1["sent"]) == 2 * N_FIELDS * N_WL * loc * 8 and int(r1["received"]) == 0

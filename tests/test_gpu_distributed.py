@@ -1,7 +1,8 @@
 """Sharded trace on the GPU (distributed.py): a world-size-2 job of two ranks on
 cuda:0 (gloo: RCCL refuses two ranks on one device) traces every (field, wavelength)
-pair's pupil slices, agrees the Newton schedule across the shards, all-gathers the image
-plane and reduces the spot statistics. The gathered image plane must be bit-identical to
+pair's pupil slices, agrees the Newton schedule across the shards, gathers the image plane
+into rank 0 (ImageGather; for config 4's shape also the pipelined trace + chunked
+asynchronous gather, PipelinedImageTrace) and reduces the spot statistics. The gathered image plane must be bit-identical to
 the unsharded trace of the whole batch: the shards are a partition of the rays, and the
 agreed schedule is the reference's global stopping rule over the whole pair
 (newton_raphson.py:148), so no ray may see a different number of Newton updates."""
@@ -58,6 +59,10 @@ def test_sharded_trace_equals_unsharded(torch, tmp_path, name):
     y = rays.y.cpu().numpy()
     np.testing.assert_array_equal(got["X"], x)  # NaNs compare equal here
     np.testing.assert_array_equal(got["Y"], y)
+    if name == "rt77":  # the pipelined trace + chunked asynchronous gather (config 4, N > 1)
+        assert bool(got["zero_copy"])  # 3,001 rays per pair split 1,501 / 1,500: rank 0 even
+        np.testing.assert_array_equal(got["X2"], x)
+        np.testing.assert_array_equal(got["Y2"], y)
     if name.endswith("_nan"):
         nf, nw = len(FIELDS), len(WAVELENGTHS)
         bad = np.isnan(x.reshape(nf * nw, N_P))
