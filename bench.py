@@ -387,6 +387,9 @@ def config5(args, dev, rank, world, torch):
                     eager_step()
             torch.cuda.current_stream().wait_stream(side)
             torch.cuda.synchronize()
+            from optiland_pr_amd import raytrace
+
+            raytrace.check_all_pending()  # the warm-up's Newton flags, before the capture
             opt.zero_grad(set_to_none=True)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):

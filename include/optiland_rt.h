@@ -407,7 +407,10 @@ typedef struct ort_options {
    * schedule up to 127 updates -- the default max_iter is 100) */
   int32_t conv_base;
   int32_t flags;          /* ORT_OPT_NO_INIT: newton_stat / status are already initialised */
-                          /* (by ort_newton_fixup): the call issues no memset            */
+                          /* (by ort_newton_fixup): the call issues no memset;            */
+                          /* ORT_OPT_EXACT: every ray on the per-operation exact sequences  */
+                          /* (no deferred-check pass; the results are the same bits --    */
+                          /* this is for checking exactly that)                            */
   /* nullable device int32: the launch does nothing unless *run_if == 1 (read on the
    * device; lenses with Newton surfaces only). With ort_newton_fixup this re-traces on a
    * corrected schedule without a host round trip. */
@@ -433,7 +436,7 @@ typedef struct ort_options {
   int32_t* sched_out;
 } ort_options;
 #define ORT_VERIFY_MAX_SCHED 1024
-enum ort_option_flags { ORT_OPT_NO_INIT = 1 };
+enum ort_option_flags { ORT_OPT_NO_INIT = 1, ORT_OPT_EXACT = 2 };
 
 /* status bits written with atomicOr into *status (device int32) */
 enum ort_status {

@@ -205,6 +205,7 @@ NEWTON_STAT = np.dtype(
 )
 assert NEWTON_STAT.itemsize == 24
 OPT_NO_INIT = 1  # ort_options.flags: ORT_OPT_NO_INIT
+OPT_EXACT = 2  # ort_options.flags: ORT_OPT_EXACT (no deferred-check pass)
 CONV_WINDOW = 128  # stop indices per conv_mask window (ort_options.conv_base)
 
 RAY_FIELDS = ("x", "y", "z", "L", "M", "N", "i", "opd")

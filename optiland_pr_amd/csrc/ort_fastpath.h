@@ -359,5 +359,113 @@ ORT_INLINE void refract_flat(Ray& r, double u, double u_sq, bool& bad) {
   r.N = (uN + sroot) - uN;
 }
 
+// ---- Newton geometries (trace_kernel's deferred-check pass) --------------------------
+// The quotient for a divisor of either sign with a numerator that may be +-0: IEEE's
+// signed zero is quot_pos's for b > 0 and the plain form's for b < 0 (see quot_pos)
+ORT_INLINE double quot_signed(double a, const SharedDiv& d) {
+  return d.b > 0.0 ? quot_pos(a, d) : quot(a, d);
+}
+// numerator in range or an exact zero of either sign (quot_signed / quot_pos keep its sign)
+ORT_INLINE bool num_ok0(double a) { return num_ok(a) || a == 0.0; }
+
+// even_asphere.py:82-129 (ort_core.h sagnorm_even): the same operations in the same order,
+// the divisions and square roots as the deferred-check sequences
+template <class PD>
+ORT_INLINE double sagnorm_even(double x, double y, const ort_surface& s, PD C,
+                               int nc, double& nx, double& ny, double& nz, bool& bad) {
+  const double R = s.radius;
+  const double r2 = x * x + y * y;
+  const double a = ORT_ONE_PLUS_K(s) * r2;  // (1 + k) r2: +-0 at the vertex
+  const SharedDiv rr = shared_div(ORT_R_SQ(s), bad);
+  ORT_CHK(bad, !num_ok0(a));
+  const double q = sqrt(1.0 - quot_pos(a, rr), bad);
+  const SharedDiv dz = shared_div(R * (1.0 + q), bad);
+  ORT_CHK(bad, !num_ok0(r2));
+  double z = quot_signed(r2, dz);
+  double rp = r2;  // r2 ** (i + 1)
+  for (int i = 0; i < nc; ++i) {
+    z = z + C[i] * rp;
+    rp = rp * r2;
+  }
+  const SharedDiv dd = shared_div(R * q, bad);
+  ORT_CHK(bad, !(num_ok0(x) && num_ok0(y)));
+  double dfdx = quot_signed(x, dd);
+  double dfdy = quot_signed(y, dd);
+  double rq = 1.0;  // r2 ** i
+  for (int i = 0; i < nc; ++i) {
+    const double f = 2.0 * (double)(i + 1);
+    dfdx = dfdx + f * x * C[i] * rq;
+    dfdy = dfdy + f * y * C[i] * rq;
+    rq = rq * r2;
+  }
+  const double mag = sqrt_ge1(dfdx * dfdx + dfdy * dfdy + 1.0, bad);
+  const SharedDiv dm = shared_div_ge1(mag, bad);
+  ORT_CHK(bad, !(num_ok0(dfdx) && num_ok0(dfdy)));
+  nx = quot_pos(dfdx, dm);
+  ny = quot_pos(dfdy, dm);
+  nz = quot(-1.0, dm);
+  return z;
+}
+
+// odd_asphere.py:73-130 (ort_core.h sagnorm_odd); non-finite per-term slopes zeroed
+template <class PD>
+ORT_INLINE double sagnorm_odd(double x, double y, const ort_surface& s, PD C,
+                              int nc, double& nx, double& ny, double& nz, bool& bad) {
+  const double R = s.radius;
+  const double r2 = x * x + y * y;
+  const double r = sqrt(r2, bad);  // the vertex itself (r2 = 0) takes the exact path
+  const double a = ORT_ONE_PLUS_K(s) * r2;
+  const SharedDiv rr = shared_div(ORT_R_SQ(s), bad);
+  ORT_CHK(bad, !num_ok0(a));
+  const double q = sqrt(1.0 - quot_pos(a, rr), bad);
+  const SharedDiv dz = shared_div(R * (1.0 + q), bad);
+  ORT_CHK(bad, !num_ok0(r2));
+  double z = quot_signed(r2, dz);
+  double rp = r;
+  for (int i = 0; i < nc; ++i) {
+    z = z + C[i] * rp;
+    rp = rp * r;
+  }
+  const SharedDiv dd = shared_div(R * q, bad);
+  ORT_CHK(bad, !(num_ok0(x) && num_ok0(y)));
+  double dfdx = quot_signed(x, dd);
+  double dfdy = quot_signed(y, dd);
+  const SharedDiv dr = shared_div(r, bad);
+  double rq = quot_pos(1.0, dr);  // 1 / r
+  for (int i = 0; i < nc; ++i) {
+    const double f = (double)(i + 1);
+    double xt = f * x * C[i] * rq;
+    double yt = f * y * C[i] * rq;
+    if (!isfinite(xt)) xt = 0.0;
+    if (!isfinite(yt)) yt = 0.0;
+    rq = (i == 0) ? 1.0 : (i == 1 ? r : rq * r);
+    dfdx = dfdx + xt;
+    dfdy = dfdy + yt;
+  }
+  const double mag = sqrt_ge1(dfdx * dfdx + dfdy * dfdy + 1.0, bad);
+  const SharedDiv dm = shared_div_ge1(mag, bad);
+  ORT_CHK(bad, !(num_ok0(dfdx) && num_ok0(dfdy)));
+  nx = quot_pos(dfdx, dm);
+  ny = quot_pos(dfdy, dm);
+  nz = quot(-1.0, dm);
+  return z;
+}
+
+// newton_raphson.py:154-166 (ort_core.h newton_step)
+ORT_INLINE double newton_step(const Ray& r, double t, double f, double nx, double ny,
+                              double nz, bool& bad) {
+  const double nzs = ::fabs(nz) > 1e-14 ? nz : 1e-14;
+  const SharedDiv dn = shared_div(nzs, bad);
+  const double mnx = -nx, mny = -ny;
+  ORT_CHK(bad, !(num_ok0(mnx) && num_ok0(mny)));
+  const double fx = quot_signed(mnx, dn);
+  const double fy = quot_signed(mny, dn);
+  const double df = fx * r.L + fy * r.M - r.N;
+  const double dfs = ::fabs(df) > 1e-14 ? df : 1e-14;
+  const SharedDiv dd = shared_div(dfs, bad);
+  ORT_CHK(bad, !num_ok0(f));
+  return t - quot_signed(f, dd);
+}
+
 }  // namespace fast
 }  // namespace ort

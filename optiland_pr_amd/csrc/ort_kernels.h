@@ -227,12 +227,44 @@ __device__ inline double grid_distance(const KArgs& a, const ort_surface& s, int
 // interaction's normal: one sag + normal evaluation per Newton surface saved.
 // F_TAPE: hist[m] = the iterate before the m-th last update (t_{U-1-m}), 0 beyond U, as
 // the adjoint's replay_distance tapes it.
-template <uint32_t FEAT>
-__device__ inline double newton_distance(const KArgs& a, const ort_surface& s, int si,
+// FAST (trace_kernel's deferred-check pass): the initial conic guess, the even / odd
+// asphere evaluations and the updates on ort_fastpath.h's sequences, range failures ORed
+// into `bad` (plus a non-finite f: such a lane's statistics come from the exact pass);
+// a lane reports its Newton statistics here only while it is not bad -- the values up to
+// then are bit-identical to the exact path's, and the exact pass reports the bad lanes
+template <uint32_t FEAT, bool FAST>
+__device__ inline __attribute__((always_inline)) double newton_eval_fast(const KArgs& a, const ort_surface& s,
+                                          const ort::Ray& r, double t, bool& rerr, double& nx,
+                                          double& ny, double& nz, bool& bad) {
+  constexpr uint32_t KM = FEAT & F_KM;
+  if constexpr (FAST && (KM & (ort::KM_EVEN | ort::KM_ODD)) != 0) {
+    const double xi = r.x + t * r.L;
+    const double yi = r.y + t * r.M;
+    const double zi = r.z + t * r.N;
+    double sag;
+    if ((KM & ort::KM_EVEN) != 0 && (KM == ort::KM_EVEN || s.geometry == ORT_GEOM_EVEN_ASPHERE))
+      sag = ort::fast::sagnorm_even(xi, yi, s, cst(a.coef) + s.coef_off, s.n_coef, nx, ny, nz, bad);
+    else if ((KM & ort::KM_ODD) != 0 && ((KM & ~ort::KM_ODD) == 0 || s.geometry == ORT_GEOM_ODD_ASPHERE))
+      sag = ort::fast::sagnorm_odd(xi, yi, s, cst(a.coef) + s.coef_off, s.n_coef, nx, ny, nz, bad);
+    else
+      sag = ort::newton_sagnorm<KM>(s, s.radius, s.conic, cst(a.coef), cst(a.zern), kNoSeed, xi,
+                                    yi, true, rerr, nx, ny, nz);
+    const double f = sag - zi;
+    ORT_CHK(bad, !(::fabs(f) < 0x1p1000));
+    return f;
+  } else {
+    return ort::newton_eval<KM>(s, s.radius, s.conic, cst(a.coef), cst(a.zern), kNoSeed, r, t,
+                                true, rerr, nx, ny, nz);
+  }
+}
+
+template <uint32_t FEAT, bool FAST = false>
+__device__ inline __attribute__((always_inline)) double newton_distance(const KArgs& a, const ort_surface& s, int si,
                                          const ort::Ray& r, bool active, int64_t group,
                                          bool group_uniform, int& range_bits, bool& hn,
                                          double& nnx, double& nny, double& nnz,
-                                         double (&hist)[kHist], const int32_t* sched) {
+                                         double (&hist)[kHist], const int32_t* sched,
+                                         bool& bad) {
   hn = false;
   if constexpr ((FEAT & F_TAPE) != 0) {
 #pragma unroll
@@ -242,7 +274,12 @@ __device__ inline double newton_distance(const KArgs& a, const ort_surface& s, i
     if (s.geometry == ORT_GEOM_GRID_SAG)
       return grid_distance<FEAT>(a, s, si, r, active, group, group_uniform, sched);
   }
-  double t = ort::distance_conic(r, s.radius, s.conic, (s.flags & ORT_SURF_RADIUS_INF) != 0);
+  const bool rinf = (s.flags & ORT_SURF_RADIUS_INF) != 0;
+  double t;
+  if constexpr (FAST)
+    t = ort::fast::distance_conic(r, s, rinf, bad);
+  else
+    t = ort::distance_conic(r, s.radius, s.conic, rinf);
   const double tol = s.tol;
   const int max_iter = s.max_iter;
   if (a.newton_mode == ORT_NEWTON_WAVE) {
@@ -281,11 +318,10 @@ __device__ inline double newton_distance(const KArgs& a, const ort_surface& s, i
       double nx, ny, nz;
       const bool upd = j < U;  // sag + normal at P(t): for the update, or (j == U) for the
                                // interaction at the returned t
-      const double f = ort::newton_eval<(FEAT & F_KM)>(s, s.radius, s.conic, cst(a.coef), cst(a.zern), kNoSeed, r,
-                                                      t, true, rerr, nx, ny, nz);
+      const double f = newton_eval_fast<FEAT, FAST>(a, s, r, t, rerr, nx, ny, nz, bad);
       // the reference evaluates sag at j = 0..U-1 always, and at j = U only when the
       // loop broke there (U < max_iter)
-      if (rerr && (j < U || U < max_iter)) range_bits |= range_bit(s);
+      if (rerr && (j < U || U < max_iter) && !(FAST && bad)) range_bits |= range_bit(s);
       const bool conv = fabs(f) < tol;  // NaN never converges (np.max propagates NaN)
       if (conv) mask.set(j, a.conv_base);
       if (!conv) last_bad = j;
@@ -295,7 +331,10 @@ __device__ inline double newton_distance(const KArgs& a, const ort_surface& s, i
           for (int h = kHist - 1; h > 0; --h) hist[h] = hist[h - 1];
           hist[0] = t;
         }
-        t = ort::newton_step(r, t, f, nx, ny, nz);
+        if constexpr (FAST)
+          t = ort::fast::newton_step(r, t, f, nx, ny, nz, bad);
+        else
+          t = ort::newton_step(r, t, f, nx, ny, nz);
       } else {
         nnx = nx;
         nny = ny;
@@ -303,7 +342,7 @@ __device__ inline double newton_distance(const KArgs& a, const ort_surface& s, i
       }
     }
   }
-  report_newton(a, si, active, group, group_uniform, mask, last_bad);
+  report_newton(a, si, active && !(FAST && bad), group, group_uniform, mask, last_bad);
   hn = true;  // every active lane evaluated j == U (inactive lanes store nothing)
   return t;
 }
@@ -428,6 +467,224 @@ __device__ inline int newton_decide(const ort_surface* surf, int32_t n_surf, int
   return c;
 }
 
+// The Newton kernels' deferred-check pass (FAST = true in trace_ray) is compiled for the
+// lenses whose Newton surfaces are even / odd aspheres (the kinds ort_fastpath.h has
+// sequences for) without interactions, per-ray wavelengths or a tape; ORT_NO_NEWTON_FAST
+// (A/B builds) keeps the single exact pass.
+template <uint32_t FEAT>
+constexpr bool kNewtonFast =
+#ifdef ORT_NO_NEWTON_FAST
+    false;
+#else
+    (FEAT & F_KM) != 0 && (FEAT & F_KM & ~(ort::KM_EVEN | ort::KM_ODD)) == 0 &&
+    (FEAT & (F_IA | F_WRAY | F_TAPE)) == 0;
+#endif
+
+__device__ inline void store_ray(const KArgs& a, int64_t rid, const ort::Ray& r) {
+  a.out.x[rid] = r.x;
+  a.out.y[rid] = r.y;
+  a.out.z[rid] = r.z;
+  a.out.L[rid] = r.L;
+  a.out.M[rid] = r.M;
+  a.out.N[rid] = r.N;
+  a.out.i[rid] = ort::intensity(r);
+  a.out.opd[rid] = r.opd;
+}
+
+// One ray through every surface (and the image-space propagate) for trace_kernel.
+// FAST: ort_fastpath.h's sequences with their range failures ORed into `bad` (see
+// kNewtonFast); the lane's records, tape rows and Newton statistics are written only while
+// it is active (the exact pass rewrites a bad lane's).
+template <uint32_t FEAT, bool FAST>
+__device__ inline __attribute__((always_inline)) ort::Ray trace_ray(const KArgs& a, int64_t rid, bool active, int64_t group,
+                                     bool group_uniform, const int32_t* sched, int& range_bits,
+                                     bool& bad) {
+  // lanes past the end compute on ray 0 and store nothing; a lane of a valid ray that is
+  // not active (the exact pass: its ray is stored already) traces its own ray, so a
+  // wave-uniform row (F_MONO's readfirstlane) is the wave's own
+  const int64_t r_ld = rid < a.n_rays ? rid : 0;
+  // segment / wavelength of this ray
+  const int64_t sidx = a.seg ? r_ld / a.seg_len : 0;
+  int lam = 0;
+  double wl = 0.0;  // F_WRAY: this ray's wavelength
+  ort::Ray r;
+  if constexpr (FEAT & F_GEN) {
+    const ort_segment sg = a.seg[sidx];
+    lam = sg.lambda_idx;
+    const int64_t p = a.pupil_per_ray ? r_ld : (r_ld - sidx * a.seg_len);
+    if constexpr (FAST)
+      r = ort::fast::generate_ray(sg, a.px[p], a.py[p], a.apod, bad);
+    else
+      r = ort::generate_ray(sg, a.px[p], a.py[p], a.apod);
+  } else {
+    if (a.seg) lam = a.seg[sidx].lambda_idx;
+    if constexpr ((FEAT & F_WRAY) != 0) wl = a.w[r_ld];
+    r.x = a.in.x[r_ld];
+    r.y = a.in.y[r_ld];
+    r.z = a.in.z[r_ld];
+    r.L = a.in.L[r_ld];
+    r.M = a.in.M[r_ld];
+    r.N = a.in.N[r_ld];
+    r.i = a.in.i[r_ld];
+    r.opd = a.in.opd[r_ld];
+    r.att = 0.0;
+    // the fast flat-surface refraction assumes finite directions (ort_fastpath.h)
+    if constexpr (FAST) ORT_CHK(bad, !(::fabs(r.L) < __builtin_inf() && ::fabs(r.M) < __builtin_inf()));
+  }
+  bool unnorm = false;  // F_IA: rays.is_normalized == False after a thin lens
+  if constexpr ((FEAT & F_GEN) != 0) {
+    if (a.apod && (uint32_t)cst(a.apod)->kind > (uint32_t)ORT_APOD_TUKEY)
+      range_bits |= ORT_STATUS_BAD_APODIZATION;
+  }
+
+  for (int si = a.start_surface; si < a.n_surf; ++si) {
+    const ort_surface s = cst(a.surf)[si];
+    const ort_surface_optics o = surface_optics<FEAT>(a, s, lam, si, wl);
+    double* tp = nullptr;  // F_TAPE: this surface's tape rows of this ray
+    if constexpr ((FEAT & F_TAPE) != 0) {
+      tp = a.tape + (int64_t)si * kTapeRows * a.n_rays + rid;
+      if (active) {
+        tp[0] = r.x;
+        tp[a.n_rays] = r.y;
+        tp[2 * a.n_rays] = r.z;
+        tp[3 * a.n_rays] = r.L;
+        tp[4 * a.n_rays] = r.M;
+        tp[5 * a.n_rays] = r.N;
+      }
+    }
+    localize(a, s, r);
+    double t;
+    bool hn = false;  // (hnx, hny, hnz): the Newton geometry's normal at t
+    double hnx = 0.0, hny = 0.0, hnz = 0.0;
+    double hist[kHist];
+    const bool radius_inf = (s.flags & ORT_SURF_RADIUS_INF) != 0;
+    if (!known_geometry(s.geometry)) range_bits |= ORT_STATUS_BAD_GEOMETRY;
+    if (s.geometry == ORT_GEOM_PLANE) {
+      if constexpr (FAST)
+        t = ort::fast::distance_plane(r, bad);
+      else
+        t = ort::distance_plane(r);
+    } else if (s.geometry == ORT_GEOM_STANDARD) {
+      if constexpr (FAST)
+        t = ort::fast::distance_conic(r, s, radius_inf, bad);
+      else
+        t = ort::distance_conic(r, s.radius, s.conic, radius_inf);
+    } else {
+      if constexpr ((FEAT & F_KM) != 0) {
+        t = newton_distance<FEAT, FAST>(a, s, si, r, active, group, group_uniform, range_bits,
+                                        hn, hnx, hny, hnz, hist, sched, bad);
+        if constexpr ((FEAT & F_TAPE) != 0) {
+          if (active) {
+#pragma unroll
+            for (int h = 0; h < kHist; ++h) tp[(7 + h) * a.n_rays] = hist[h];
+          }
+        }
+      } else {
+        t = __builtin_nan("");  // unreachable: the host sets geometry_mask
+      }
+    }
+    if constexpr ((FEAT & F_TAPE) != 0) {
+      if (active) tp[6 * a.n_rays] = t;
+    }
+    const double n_pre = o.n_pre, u = o.u, alpha = o.alpha_pre;
+    if constexpr ((FEAT & F_IA) != 0) {
+      ort::propagate(r, t, alpha);
+      if (unnorm) {  // homogeneous.py:55-57
+        ort::normalize_dir(r);
+        unnorm = false;
+      }
+      ort::add_opd(r, t, n_pre);
+      if (s.flags & ORT_SURF_APERTURE) ort::clip_radial(r, s.ap_rmax2, s.ap_rmin2);
+      if (s.flags & ORT_SURF_APERTURE_PROG) ort::clip_program(r, cst(a.coef) + s.ap_off, s.ap_len);
+      interact<FEAT>(a, s, r, o, lam, wl, unnorm);
+    } else if constexpr (FAST) {
+      // the closed kernel's fast surface step (closed_surfaces), the Newton surfaces with
+      // the normal of their last evaluation
+      ort::propagate(r, t, alpha);
+      ort::add_opd(r, t, n_pre);
+      if (s.flags & ORT_SURF_APERTURE) ort::clip_radial(r, s.ap_rmax2, s.ap_rmin2);
+      if (s.flags & ORT_SURF_APERTURE_PROG) ort::clip_program(r, cst(a.coef) + s.ap_off, s.ap_len);
+      const bool refl = (s.flags & ORT_SURF_REFLECTIVE) != 0;
+      const bool is_plane = s.geometry == ORT_GEOM_PLANE;
+      if (!hn && !refl && (is_plane || (radius_inf && s.geometry == ORT_GEOM_STANDARD))) {
+        ort::fast::refract_flat(r, u, o.u_sq, bad);  // normal (0, 0, +-1): reduced exactly
+      } else {
+        double nx, ny, nz;
+        if (hn) {
+          nx = hnx; ny = hny; nz = hnz;
+        } else if (is_plane) {
+          nx = 0.0; ny = 0.0; nz = 1.0;
+        } else if (s.flags & ORT_SURF_INV_R2) {
+          ort::fast::normal_conic_rcp(r.x, r.y, s, nx, ny, nz, bad);
+        } else {
+          ort::normal_conic(r.x, r.y, s.radius, s.conic, nx, ny, nz);
+        }
+        if (refl)
+          ort::reflect(r, nx, ny, nz);
+        else
+          ort::fast::refract(r, nx, ny, nz, u, o.u_sq, bad);
+      }
+    } else if constexpr ((FEAT & F_KM) != 0) {
+      if (hn) {  // finish_surface with the normal of the last Newton evaluation
+        ort::propagate(r, t, alpha);
+        ort::add_opd(r, t, n_pre);
+        if (s.flags & ORT_SURF_APERTURE) ort::clip_radial(r, s.ap_rmax2, s.ap_rmin2);
+        if (s.flags & ORT_SURF_APERTURE_PROG) ort::clip_program(r, cst(a.coef) + s.ap_off, s.ap_len);
+        if (s.flags & ORT_SURF_REFLECTIVE)
+          ort::reflect(r, hnx, hny, hnz);
+        else
+          ort::refract(r, hnx, hny, hnz, u);
+      } else {
+        ort::finish_surface<(FEAT & F_KM)>(r, s, s.radius, s.conic, cst(a.coef), cst(a.zern), kNoSeed, t, n_pre, u,
+                                           alpha);
+      }
+    } else {
+      // closed-form geometries only: plane / conic normal inline
+      ort::propagate(r, t, alpha);
+      ort::add_opd(r, t, n_pre);
+      if (s.flags & ORT_SURF_APERTURE) ort::clip_radial(r, s.ap_rmax2, s.ap_rmin2);
+#ifndef ORT_NO_AP_PROG
+      if (s.flags & ORT_SURF_APERTURE_PROG) ort::clip_program(r, cst(a.coef) + s.ap_off, s.ap_len);
+#endif
+      double nx, ny, nz;
+      if (s.geometry == ORT_GEOM_PLANE) {
+        nx = 0.0; ny = 0.0; nz = 1.0;
+      } else if (s.flags & ORT_SURF_INV_R2) {
+        ort::normal_conic_rcp(r.x, r.y, s.radius, s.conic, s.inv_r2, nx, ny, nz);
+      } else {
+        ort::normal_conic(r.x, r.y, s.radius, s.conic, nx, ny, nz);
+      }
+      if (s.flags & ORT_SURF_REFLECTIVE)
+        ort::reflect(r, nx, ny, nz);
+      else
+        ort::refract(r, nx, ny, nz, u);
+    }
+    globalize(a, s, r);
+    if constexpr ((FEAT & F_REC) != 0) {
+      if ((s.flags & ORT_SURF_RECORD) && active) {
+        double* base = a.rec + (int64_t)s.rec_slot * 8 * a.n_rays + rid;
+        base[0 * a.n_rays] = r.x;
+        base[1 * a.n_rays] = r.y;
+        base[2 * a.n_rays] = r.z;
+        base[3 * a.n_rays] = r.L;
+        base[4 * a.n_rays] = r.M;
+        base[5 * a.n_rays] = r.N;
+        base[6 * a.n_rays] = ort::intensity(r);
+        base[7 * a.n_rays] = r.opd;
+      }
+    }
+  }
+  // real_ray_tracer.py:84-89: image-space propagate by the last surface's thickness
+  // (final_mat < 0: plain SurfaceGroup.trace, no propagate)
+  if (a.final_mat >= 0) {
+    ort::propagate(r, a.final_thickness, final_alpha<FEAT>(a, lam, wl));
+    if constexpr ((FEAT & F_IA) != 0) {
+      if (unnorm) ort::normalize_dir(r);
+    }
+  }
+  return r;
+}
+
 template <uint32_t FEAT>
 __global__ __launch_bounds__(kBlock) ORT_TRACE_OCC void trace_kernel(const KArgs a) {
   if (a.run_if && *cst(a.run_if) != 1) return;  // a device-side re-trace that is not needed
@@ -465,6 +722,31 @@ __global__ __launch_bounds__(kBlock) ORT_TRACE_OCC void trace_kernel(const KArgs
       a.block_remap ? pair_major_ray(a) : (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool active = rid < a.n_rays;
   const int64_t r_ld = active ? rid : 0;  // inactive lanes compute on ray 0, store nothing
+  // kNewtonFast: first the whole ray on ort_fastpath.h's deferred-check sequences; the
+  // lanes that stayed inside their ranges store it (bit-identical to the exact path) and
+  // leave, the rest fall through to the exact trace below on their own (divergent, rare),
+  // reporting their Newton statistics per lane
+  bool redo = false;
+  if constexpr (kNewtonFast<FEAT>) {
+    if (a.newton_mode == ORT_NEWTON_SCHEDULE && !a.exact_only) {
+      bool bad = false;
+      int fast_bits = 0;
+      int64_t fgroup = 0;
+      bool fgroup_uniform = true;
+      fgroup = r_ld / a.group_len;
+      const int64_t g0 = __shfl(fgroup, 0, 64);
+      fgroup_uniform = __all(fgroup == g0);
+      const ort::Ray rf = trace_ray<FEAT, true>(a, rid, active, fgroup, fgroup_uniform, sched,
+                                                fast_bits, bad);
+      bad = bad | !ort::fast::state_ok(rf);
+      if (!bad) {
+        if (fast_bits && active && a.status) atomicOr(a.status, fast_bits);
+        if (active) store_ray(a, rid, rf);
+        return;
+      }
+      redo = true;
+    }
+  }
 
   // segment / wavelength / Newton group of this ray
   const int64_t sidx = a.seg ? r_ld / a.seg_len : 0;
@@ -493,8 +775,12 @@ __global__ __launch_bounds__(kBlock) ORT_TRACE_OCC void trace_kernel(const KArgs
   bool group_uniform = true;
   if constexpr ((FEAT & F_KM) != 0) {
     group = r_ld / a.group_len;
-    const int64_t g0 = __shfl(group, 0, 64);
-    group_uniform = __all(group == g0);
+    if (redo) {  // divergent (the fast pass's bad lanes only): no wave-wide reductions
+      group_uniform = false;
+    } else {
+      const int64_t g0 = __shfl(group, 0, 64);
+      group_uniform = __all(group == g0);
+    }
   }
   int range_bits = 0;
   bool unnorm = false;  // F_IA: rays.is_normalized == False after a thin lens
@@ -530,8 +816,9 @@ __global__ __launch_bounds__(kBlock) ORT_TRACE_OCC void trace_kernel(const KArgs
       t = ort::distance_conic(r, s.radius, s.conic, (s.flags & ORT_SURF_RADIUS_INF) != 0);
     } else {
       if constexpr ((FEAT & F_KM) != 0) {
+        bool unused = false;
         t = newton_distance<FEAT>(a, s, si, r, active, group, group_uniform, range_bits, hn,
-                                  hnx, hny, hnz, hist, sched);
+                                  hnx, hny, hnz, hist, sched, unused);
         if constexpr ((FEAT & F_TAPE) != 0) {
           if (active) {
 #pragma unroll
@@ -625,6 +912,7 @@ __global__ __launch_bounds__(kBlock) ORT_TRACE_OCC void trace_kernel(const KArgs
   a.out.N[rid] = r.N;
   a.out.i[rid] = ort::intensity(r);
   a.out.opd[rid] = r.opd;
+
 }
 
 // Closed-form lenses (planes, spheres, conics: no Newton surface) -- the DoubleGauss /
@@ -982,10 +1270,10 @@ __global__ __launch_bounds__(kBlock) void geom_kernel(const KArgs a, const GArgs
       t = ort::distance_conic(r, s.radius, s.conic, (s.flags & ORT_SURF_RADIUS_INF) != 0);
     } else {
       if constexpr (KM != 0) {
-        bool hn;
+        bool hn, bad = false;
         double hnx, hny, hnz, hist[kHist];
         t = newton_distance<KM>(a, s, g.surface, r, active, 0, true, range_bits, hn, hnx, hny,
-                                hnz, hist, a.sched);
+                                hnz, hist, a.sched, bad);
       } else {
         t = __builtin_nan("");
       }

@@ -113,6 +113,7 @@ struct KArgs {
   // nullable: the launch is a no-op unless *run_if == 1 (ort_options.run_if)
   const int32_t* run_if;
   int32_t no_init;  // host side only: ORT_OPT_NO_INIT (skip init_outputs)
+  int32_t exact_only;  // ORT_OPT_EXACT: no deferred-check pass (trace_kernel)
   // verify-and-re-trace (ort_options.verify_*): the launch decides from vstats first
   const ort_newton_stat* vstats;
   const int32_t* vprev;
@@ -167,6 +168,7 @@ inline int fill_args(KArgs& a, const ort_lens* lens, const ort_batch* batch,
   a.conv_base = opt->conv_base;
   a.run_if = opt->run_if;
   a.no_init = (opt->flags & ORT_OPT_NO_INIT) != 0;
+  a.exact_only = (opt->flags & ORT_OPT_EXACT) != 0;
   a.tape = opt->tape;
   if (opt->conv_base < 0) return ORT_ERR_ARG;
   // geometry ids this library knows (enum ort_geometry): anything else is refused here

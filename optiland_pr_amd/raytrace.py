@@ -527,8 +527,8 @@ def _run(dlens: DeviceLens, launch, n_rays, group_len, keys, newton_mode="refere
     same rule checked on the device once the schedules are warm (no host round trip,
     errors surface at a later check_pending); "wave": per-wavefront stop."""
     dev = dlens.device
-    if dlens.pending:
-        check_pending(dlens)
+    if dlens.pending and not torch.cuda.is_current_stream_capturing():
+        check_pending(dlens)  # (a capture only records launches: no event queries in it)
     dlens.last_schedule_dev = None
     S = dlens.table.n_surfaces
     n_groups = max(1, -(-n_rays // group_len))
@@ -610,7 +610,7 @@ def upload_segments(segments: np.ndarray, device):
 
 def trace_pupil(dlens: DeviceLens, segments, px, py, out: RealRays, n_rays,
                 seg_len, group_len, pupil_per_ray=False, keys=(), rec=None,
-                newton_mode="reference", start_surface=0, tape=None):
+                newton_mode="reference", start_surface=0, tape=None, exact_only=False):
     """Generate + trace in one launch (ort_trace_pupil). `segments` is a host SEGMENT array
     or the device tensor returned by upload_segments (no per-call copy). tape: a device
     buffer of ort_vjp_tape_size bytes the launch writes the adjoint tape into (Newton
@@ -630,6 +630,8 @@ def trace_pupil(dlens: DeviceLens, segments, px, py, out: RealRays, n_rays,
     def launch(opt, stats, status):
         opt.start_surface = start_surface
         opt.tape = tape_p
+        if exact_only:
+            opt.flags |= _abi.OPT_EXACT
         rc = lib.ort_trace_pupil(*args, C.byref(opt), rec_p, _ptr(stats), _ptr(status), stream)
         _native.check(rc, "ort_trace_pupil")
 
@@ -665,10 +667,11 @@ def trace_spot(dlens: DeviceLens, segments, px, py, out: RealRays, n_rays, seg_l
 
 def trace_rays(dlens: DeviceLens, rays_in: RealRays, rays_out: RealRays, group_len=None,
                keys=(), rec=None, newton_mode="reference", start_surface=0, segments=None,
-               seg_len=None, per_ray_w=False):
+               seg_len=None, per_ray_w=False, exact_only=False):
     """Trace resident rays (ort_trace_sequential); rays_out may be rays_in (in place).
     per_ray_w: n and k per ray from rays_in.w (the lens's material tables) instead of
-    the per-wavelength tables."""
+    the per-wavelength tables. exact_only: ORT_OPT_EXACT (no deferred-check pass; the same
+    bits -- for the tests that check exactly that)."""
     lib = _native.load()
     n = len(rays_in)
     group_len = group_len or max(n, 1)
@@ -694,6 +697,8 @@ def trace_rays(dlens: DeviceLens, rays_in: RealRays, rays_out: RealRays, group_l
 
     def launch(opt, stats, status):
         opt.start_surface = start_surface
+        if exact_only:
+            opt.flags |= _abi.OPT_EXACT
         rc = lib.ort_trace_sequential(C.byref(dlens.c), C.byref(in_c), C.byref(out_c),
                                       C.byref(batch), C.byref(opt), _ptr(rec), _ptr(stats),
                                       _ptr(status), _stream_handle())
