@@ -222,7 +222,7 @@ def config3(args, dev, rank, world, torch):
                 "parallelism": f"dp{world} (ray shards, no collective)"},
         kernel="trace_kernel<F_GEN|KM_EVEN> (ort_trace_pupil)", launches=1,
         bytes_per_launch=n_p * 16 + n * 64, flops_per_ray=flops, pmc_file="hbm_traffic_c3.json",
-        rays=n)
+        compute_pmc_file="r04_config3_pmc_compute.json", rays=n)
 
 
 def config4(args, dev, rank, world, torch):
@@ -659,6 +659,16 @@ def _roofline(w, kern_ms):
 def _roofline_fp64(w, kern_ms):
     pmc = _pmc_summary(w.pmc_file)
     hw_flops = pmc.get("fp64_flops_per_launch")
+    src = w.pmc_file
+    per_wave = {}
+    cpmc = _pmc_summary(getattr(w, "compute_pmc_file", None))
+    if cpmc.get("counters"):  # the kernel's compute counters (tools/pmc_c3.sh passes)
+        c = cpmc["counters"]
+        src = w.compute_pmc_file
+        hw_flops = c["SQ_INSTS_VALU_FLOPS_FP64"] * 64
+        per_wave = {k: cpmc["derived"][k] for k in (
+            "valu_insts_per_wave", "fp64_valu_insts_per_wave", "salu_insts_per_wave")
+            if k in cpmc.get("derived", {})}
     achieved_tf = w.flops_per_ray * w.rays / (kern_ms * 1e-3) / 1e12
     return {
         "bound": "fp64_valu",
@@ -673,7 +683,8 @@ def _roofline_fp64(w, kern_ms):
             "fp64_flops_per_launch": hw_flops,
             "achieved": hw_flops / (kern_ms * 1e-3) / 1e12,
             "frac": hw_flops / (kern_ms * 1e-3) / 1e12 / SPEC_FP64_VEC_TFLOPS,
-            "source": f"SQ_INSTS_VALU_FLOPS_FP64 x 64 (profiles/{w.pmc_file})",
+            "source": f"SQ_INSTS_VALU_FLOPS_FP64 x 64 (profiles/{src})",
+            **per_wave,
         },
     }
 

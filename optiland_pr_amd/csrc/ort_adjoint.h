@@ -15,14 +15,15 @@ namespace ortk {
 
 // P = 2: duals seeded on the point (x, y); P = 4: also on the radius and conic.
 //
-// Occupancy: the Zernike kernels without freeform kinds (KM 4-7, P = 2) need ~230 VGPRs,
-// i.e. 2 waves per SIMD; capped at 128 VGPRs (4 waves, ~400 B of scratch per lane) they
-// run 11% faster on the MI355X (TMA 1M rays: 1283 -> 1135 us per adjoint launch,
-// rocprofv3); 3 waves: 1177 us, 5 waves: 1719 us. Other kernels keep the compiler's
-// choice. ORT_ADJ_WAVES overrides the target for A/B builds.
+// Occupancy of the Zernike kernels without freeform kinds (KM 4-7, P = 2; TMA 1M rays,
+// rocprofv3 A/B per adjoint launch on the MI355X, round 4, with the plain-double Zernike
+// jet): 2 waves per SIMD (184 VGPRs, no scratch) 755-757 us, 3 waves (168 VGPRs, 56 B of
+// scratch) 582-588 us, 4 waves (128 VGPRs, 216 B) 591-595 us -- the compiler's choice is
+// the slowest. Other kernels keep the compiler's choice. ORT_ADJ_WAVES overrides the target
+// for A/B builds.
 template <uint32_t KM, int P>
 struct AdjWaves {
-  static constexpr int value = (P == 2 && (KM & ort::KM_ZERN) != 0 && KM < ort::KM_FREE) ? 4 : 1;
+  static constexpr int value = (P == 2 && (KM & ort::KM_ZERN) != 0 && KM < ort::KM_FREE) ? 3 : 1;
 };
 #ifdef ORT_ADJ_WAVES
 #define ORT_ADJ_OCC __attribute__((amdgpu_waves_per_eu(ORT_ADJ_WAVES)))
@@ -34,17 +35,27 @@ struct AdjWaves {
 // summed over the wave and stored by lane 0 into partial[slot][wave] (one writer per slot
 // and wave; `first`: a plain store instead of a read-modify-write whose load the wave
 // would wait for -- the same value, 0 + w == w); the tape rows of the ray in HBM
-// ([S][kTapeRows][n_rays], coalesced); the adjoint state parked in LDS across the Newton
-// replay's dual-number evaluation (the empty asm statements are compiler memory barriers,
-// so the ten values' registers are free during the evaluation): TMA adjoint 909 -> 851 us
-// per 1M-ray launch (rocprofv3 A/B).
+// ([S][kTapeRows][n_rays], coalesced). (Round 3 parked the adjoint state in LDS across the
+// Newton replay's dual-number Zernike evaluation; with the plain-double jet that costs
+// more than it saves: 657 vs 591 us at 4 waves, rocprofv3 A/B, so the state stays in
+// registers.)
+// Zernike coefficient contributions: the first kZAcc terms of a surface are added per lane
+// in LDS over the hit point and the (up to kHist) replayed Newton iterates, and summed over
+// the wave once per surface -- one DPP wave sum per term and surface instead of one per
+// term and evaluation (32 KB of LDS per block; TMA 1M rays: 582 -> 551 us per adjoint
+// launch, rocprofv3 A/B). ORT_ADJ_ZACC=0 (A/B builds): a wave sum per evaluation.
+#ifndef ORT_ADJ_ZACC
+#define ORT_ADJ_ZACC 16
+#endif
+constexpr int kZAcc = ORT_ADJ_ZACC;
+
 struct DevLane {
   const AArgs& j;
-  double (*park_lds)[kBlock];  // __shared__ [10][kBlock]
   int64_t r_ld;                // this lane's ray (0 for the idle tail lanes)
   int64_t n_rays;
   int64_t wave;
   bool active;
+  double (*zacc)[kBlock];      // __shared__ [kZAcc][kBlock] (kZAcc > 0)
 
   __device__ inline void emit(int slot, double v, bool first) {
     if (!cst(j.need)[slot]) return;  // uniform
@@ -62,20 +73,28 @@ struct DevLane {
   }
   __device__ inline int64_t tape_stride() const { return n_rays; }
   __device__ inline int uniform_max(int v) const { return wave_max_i32(v); }
-  // ORT_ADJ_NO_PARK (A/B builds): keep the state in registers
-  __device__ inline void park(const double (&v)[10]) {
-#ifndef ORT_ADJ_NO_PARK
-#pragma unroll
-    for (int k = 0; k < 10; ++k) park_lds[k][threadIdx.x] = v[k];
-    asm volatile("" ::: "memory");
-#endif
+  // Zernike coefficient contributions of one surface (term j of the surface, slot `slot`):
+  // with kZAcc > 0 the surface's terms j < kZAcc are added per lane in LDS over the hit
+  // point and the replayed Newton iterates and summed over the wave once, at zflush
+  __device__ inline void zemit(int slot, int jt, double v, bool first) {
+    if constexpr (kZAcc > 0) {
+      if (jt < kZAcc) {
+        if (!cst(j.need)[slot]) return;  // uniform
+        if (first)
+          zacc[jt][threadIdx.x] = v;
+        else
+          zacc[jt][threadIdx.x] += v;
+        return;
+      }
+    }
+    emit(slot, v, first);
   }
-  __device__ inline void unpark(double (&v)[10]) {
-#ifndef ORT_ADJ_NO_PARK
-    asm volatile("" ::: "memory");
-#pragma unroll
-    for (int k = 0; k < 10; ++k) v[k] = park_lds[k][threadIdx.x];
-#endif
+  __device__ inline void zflush(int slot0, int nt) {
+    if constexpr (kZAcc > 0) {
+      const int m = nt < kZAcc ? nt : kZAcc;
+      for (int jt = 0; jt < m; ++jt)
+        if (cst(j.need)[slot0 + jt]) emit(slot0 + jt, zacc[jt][threadIdx.x], true);
+    }
   }
 };
 
@@ -84,11 +103,16 @@ struct DevLane {
 // adj_ray (ort_sweep.h).
 template <uint32_t KM, int P, bool RES>
 __global__ __launch_bounds__(kBlock) ORT_ADJ_OCC void adj_kernel(const KArgs a, const AArgs j) {
-  __shared__ double park[10][kBlock];  // 20 KB per block
   const int64_t rid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool active = rid < a.n_rays;
-  DevLane ln{j, park, active ? rid : 0, a.n_rays, rid >> 6, active};
-  adj_ray<KM, P, RES>(a, j, ln, rid, active);
+  if constexpr (kZAcc > 0 && (KM & ort::KM_ZERN) != 0) {
+    __shared__ double zacc[kZAcc > 0 ? kZAcc : 1][kBlock];
+    DevLane ln{j, active ? rid : 0, a.n_rays, rid >> 6, active, zacc};
+    adj_ray<KM, P, RES>(a, j, ln, rid, active);
+  } else {
+    DevLane ln{j, active ? rid : 0, a.n_rays, rid >> 6, active, nullptr};
+    adj_ray<KM, P, RES>(a, j, ln, rid, active);
+  }
 }
 
 typedef void (*AdjFn)(const KArgs, const AArgs);

@@ -247,8 +247,8 @@ struct HostLane {
   double* tape(int si) const { return tp + (int64_t)si * kTapeRows; }
   int64_t tape_stride() const { return 1; }
   int uniform_max(int v) const { return v; }
-  void park(const double (&)[10]) {}
-  void unpark(double (&)[10]) {}
+  void zemit(int slot, int, double v, bool first) { emit(slot, v, first); }
+  void zflush(int, int) {}
 };
 
 template <uint32_t KM, int P>

@@ -739,6 +739,14 @@ __global__ __launch_bounds__(kBlock) ORT_TRACE_OCC void trace_kernel(const KArgs
       const ort::Ray rf = trace_ray<FEAT, true>(a, rid, active, fgroup, fgroup_uniform, sched,
                                                 fast_bits, bad);
       bad = bad | !ort::fast::state_ok(rf);
+#ifdef ORT_FAST_PROBE  // measurement builds only (tools/fast_probe.py): mark, do not redo
+      if (bad) {
+        ort::Ray rb = rf;
+        rb.x = __builtin_nan("");
+        if (active) store_ray(a, rid, rb);
+        return;
+      }
+#endif
       if (!bad) {
         if (fast_bits && active && a.status) atomicOr(a.status, fast_bits);
         if (active) store_ray(a, rid, rf);

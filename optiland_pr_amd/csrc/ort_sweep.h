@@ -14,8 +14,7 @@
 // "lane" policy object: where a per-ray contribution to a parameter slot goes (a wave sum
 // into partial[slot][wave] on the device, a per-chunk accumulator on the host), where the
 // adjoint tape lives (HBM rows [S][11][n_rays] on the device, a per-ray scratch array on
-// the host) and the register-pressure tricks the device needs (LDS parking). The
-// arithmetic is the same source, so the host gradients follow the GPU's operation for
+// the host) and how a wave-uniform loop bound is formed. The arithmetic is the same source, so the host gradients follow the GPU's operation for
 // operation (the reductions over rays run in a different fixed order).
 //
 // Reference files are cited as path:line under optiland/.
@@ -384,8 +383,10 @@ ORT_INLINE double replay_distance(const KArgs& a, const ort_surface& s, int si,
 //   double* tape(int si)                          this ray's tape rows of surface si
 //   int64_t tape_stride()                         distance between two tape rows
 //   int    uniform_max(int v)                     max over the rays sharing control flow
-//   void   park(double (&v)[10]), unpark(...)     keep v across the Newton replay's dual
-//                                                 evaluation outside the registers
+//   void   zemit(int slot, int j, double v, bool first), zflush(int slot0, int nt)
+//                                                 a Zernike term's contribution (term j of
+//                                                 the surface; first: the surface's first);
+//                                                 zflush after the surface's last one
 // RES = false: rays generated from pupil samples (ort_trace_pupil_vjp);
 // RES = true: resident input rays a.in (ort_trace_sequential_vjp, SurfaceGroup.trace under
 // autograd), optionally with per-ray wavelengths (a.w), and the cotangents of the input
@@ -500,7 +501,8 @@ ORT_INLINE void adj_ray(const KArgs& a, const AArgs& j, Lane& ln, int64_t rid, b
         ort::zernike_coef_adjoint(x, y, s.norm_radius, cst(a.zern), s.coef_off, s.n_coef,
                                   cst(a.coef), w_sag, bdx, bdy,
                                   [&](int term, double g) {
-                                    ln.emit(base + term, on ? g : 0.0, first);
+                                    ln.zemit(base + term, term - s.coef_off, on ? g : 0.0,
+                                             first);
                                   });
       }
     }
@@ -730,23 +732,7 @@ ORT_INLINE void adj_ray(const KArgs& a, const AArgs& j, Lane& ln, int64_t rid, b
         const double tk = tp[(7 + m) * TS];
         const double xk = q.x + tk * q.L, yk = q.y + tk * q.M, zk = q.z + tk * q.N;
         D kx, ky, kz;
-        // The dual-number sag / normal alone needs ~124 VGPRs (the plain one 42), so with the
-        // adjoint state live across it the GPU kernel would spill at its 128-VGPR cap. The
-        // lane parks the state outside the registers (LDS on the device) across it.
-        double pk[10] = {b.x, b.y, b.z, b.L, b.M, b.N, bopd, batt, tb, kSurf ? bCZ : 0.0};
-        ln.park(pk);
         const D sk = sagnorm(s, xk, yk, kx, ky, kz);
-        ln.unpark(pk);
-        b.x = pk[0];
-        b.y = pk[1];
-        b.z = pk[2];
-        b.L = pk[3];
-        b.M = pk[4];
-        b.N = pk[5];
-        bopd = pk[6];
-        batt = pk[7];
-        tb = pk[8];
-        if constexpr (kSurf) bCZ = pk[9];
         const double f = sk.v - zk;
         const bool zg = fabs(kz.v) > 1e-14;
         const double nzs = zg ? kz.v : 1e-14;
@@ -786,6 +772,10 @@ ORT_INLINE void adj_ray(const KArgs& a, const AArgs& j, Lane& ln, int64_t rid, b
       // products of f f'' / f'^2 over the kept updates, i.e. by converged residuals
       const double t0 = U == 0 ? t : tp[(int64_t)(7 + (U <= kHist ? U - 1 : 0)) * TS];
       closed_adj(s, q, t0, U <= kHist ? tb : 0.0, b, bR, bk);
+    }
+
+    if constexpr ((KM & ort::KM_ZERN) != 0) {
+      if (s.geometry == ORT_GEOM_ZERNIKE && j.zparam) ln.zflush(3 * a.n_surf + s.coef_off, s.n_coef);
     }
 
     // localize adjoint: the op list transposed in reverse, then - cs_t
