@@ -337,6 +337,7 @@ def config4(args, dev, rank, world, torch):
 
 
 def config5(args, dev, rank, world, torch):
+    from optiland_pr_amd.autodiff import CapturedStep
     from optiland_pr_amd.operands import RayOperand
     from optiland_pr_amd.samples import ThreeMirrorAnastigmat
 
@@ -365,46 +366,26 @@ def config5(args, dev, rank, world, torch):
 
     def eager_step():
         opt.zero_grad()
-        loss = RayOperand.rms_spot_size(lens, -1, 0.0, 1.0, R, 0.587, d)
+        loss = loss_fn()
         loss.backward()
         opt.step()
         state["loss"] = loss.detach()  # read once after the timed region (no per-step sync)
 
-    graph = {}
+    def loss_fn():
+        return RayOperand.rms_spot_size(lens, -1, 0.0, 1.0, R, 0.587, d)
+
+    # the whole optimisation step -- coefficient patch, taped trace with its device-verified
+    # Newton rounds, rms_spot, the adjoint VJP, the fused Adam update -- as ONE HIP graph
+    # replay (autodiff.CapturedStep): the host issues one launch per step instead of ~40
+    # 
+    captured = CapturedStep(loss_fn, opt, lenses=[lens])
 
     def graph_step():
-        """The whole optimisation step -- coefficient patch, taped trace with its
-        device-verified Newton rounds, rms_spot, the adjoint VJP, the fused Adam update --
-        as ONE HIP graph replay: the host issues one launch per step instead of ~40
-        (every op of the step is free of host synchronisation)."""
-        g = graph.get("g")
-        if g is None:
-            # warm the Newton schedules, workspaces and caches off the capture, then capture
-            side = torch.cuda.Stream()
-            side.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(side):
-                for _ in range(3):
-                    eager_step()
-            torch.cuda.current_stream().wait_stream(side)
-            torch.cuda.synchronize()
-            from optiland_pr_amd import raytrace
-
-            raytrace.check_all_pending()  # the warm-up's Newton flags, before the capture
-            opt.zero_grad(set_to_none=True)
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                loss = RayOperand.rms_spot_size(lens, -1, 0.0, 1.0, R, 0.587, d)
-                loss.backward()
-                opt.step()
-            state["loss"] = loss.detach()
-            graph["g"] = g
-        g.replay()
+        state["loss"] = captured()
 
     def check():  # the captured device-verified Newton rounds: flags of the last replay
-        from optiland_pr_amd import raytrace
-
-        for dl in getattr(lens, "_lowered", {}).values():
-            raytrace.check_graph_flags(dl)
+        if captured.graph is not None:
+            captured.check()
 
     state["check"] = check
     step = graph_step if use_graph else eager_step

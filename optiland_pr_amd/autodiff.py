@@ -215,3 +215,66 @@ def trace_pupil_grad(optic, dlens, seg_dev, px, py, n, seg_len, wavelength, keys
     outs = torch.ops.ort.trace_pupil(ops.handle(plan), px, py, [t for _, _, t in params],
                                      ops.encode_spec([(k, si) for k, si, _ in params]))
     return outs[:8]
+
+
+class CapturedStep:
+    """One optimisation step -- `loss = loss_fn(); loss.backward(); optimizer.step()` -- run
+    as ONE HIP graph replay (the driver loop of optimization/optimizer/torch/base.py:
+    95-154 without its per-step host work). Every op on the path is free of host
+    synchronisation once warm: the coefficient patch, the taped trace with
+    newton_mode="device" (its verify-and-re-trace rounds are captured as launches), the
+    rms_spot reduction, the adjoint VJP and a capturable optimizer
+    (`torch.optim.Adam(..., capturable=True)`).
+
+    The first call warms the Newton schedules, workspaces and caches with `warmup` eager
+    steps on a side stream, checks their pending Newton flags, and captures; every call
+    (the first included) then replays the graph once. `loss` is the graph's static loss
+    tensor (read it after a synchronisation). `check()` reads the last replay's Newton
+    flags of `lenses` (one synchronising copy) and raises as `raytrace.check_pending`
+    would: call it at the end of a run or every few steps."""
+
+    def __init__(self, loss_fn, optimizer, lenses=(), warmup=3):
+        self.loss_fn, self.opt, self.lenses, self.warmup = loss_fn, optimizer, list(lenses), warmup
+        self.graph = None
+        self.loss = None
+
+    def eager(self):
+        self.opt.zero_grad()
+        loss = self.loss_fn()
+        loss.backward()
+        self.opt.step()
+        return loss
+
+    def _capture(self):
+        import torch
+
+        from . import raytrace
+
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(self.warmup):
+                self.eager()
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        raytrace.check_all_pending()  # the warm-up's Newton flags, before the capture
+        self.opt.zero_grad(set_to_none=True)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            loss = self.loss_fn()
+            loss.backward()
+            self.opt.step()
+        self.graph, self.loss = g, loss.detach()
+
+    def __call__(self):
+        if self.graph is None:
+            self._capture()
+        self.graph.replay()
+        return self.loss
+
+    def check(self):
+        from . import raytrace
+
+        for lens in self.lenses:
+            for dl in getattr(lens, "_lowered", {}).values():
+                raytrace.check_graph_flags(dl)

@@ -387,12 +387,33 @@ __device__ inline void interact(const KArgs& a, const ort_surface& s, ort::Ray& 
 // The taping forward (F_TAPE: the hist registers and 11 rows of stores per surface) runs
 // best unspilled at 4 waves: TMA 1M rays, taped trace 374 / 328 / 300 us at 6 / 5 / 4
 // waves per SIMD (rocprofv3 A/B).
+// The Newton kernels' deferred-check pass (FAST = true in trace_ray) is compiled for the
+// lenses whose Newton surfaces are even / odd aspheres (the kinds ort_fastpath.h has
+// sequences for) without interactions, per-ray wavelengths or a tape; ORT_NO_NEWTON_FAST
+// (A/B builds) keeps the single exact pass. Measured (config 3, RT-asph 60M rays, rocprofv3
+// PMC + A/B on the MI355X, round 4): every ray stays inside the ranges
+// (tools/fast_probe.py: 0 re-traced waves), the pass issues 2,598 fp64 VALU instructions
+// per wave instead of 2,725 and 1,611 SALU instead of 2,363 -- but its range tests add as
+// many non-fp64 VALU instructions as the div / sqrt sequences save (4,079 vs 4,060 VALU
+// per wave in all), so the launch time is the exact pass's: 7.15-7.17 ms at 6 waves per
+// SIMD (80 VGPRs) vs 7.16-7.20 ms exact-only (79 VGPRs); at the compiler's 99 VGPRs
+// (5 waves) 7.29-7.31 ms. TraceWaves: 6 for the wave-uniform-row (F_MONO) kernels
+// measured here, the compiler's choice for the others.
+template <uint32_t FEAT>
+constexpr bool kNewtonFast =
+#ifdef ORT_NO_NEWTON_FAST
+    false;
+#else
+    (FEAT & F_KM) != 0 && (FEAT & F_KM & ~(ort::KM_EVEN | ort::KM_ODD)) == 0 &&
+    (FEAT & (F_IA | F_WRAY | F_TAPE)) == 0;
+#endif
+
 template <uint32_t FEAT>
 struct TraceWaves {
   static constexpr int value =
       ((FEAT & ort::KM_ZERN) != 0 && (FEAT & (ort::KM_FREE | F_IA)) == 0)
           ? ((FEAT & F_TAPE) != 0 ? 4 : 6)
-          : 1;
+          : ((kNewtonFast<FEAT> && (FEAT & F_MONO) != 0) ? 6 : 1);
 };
 #ifdef ORT_TRACE_WAVES
 #define ORT_TRACE_OCC __attribute__((amdgpu_waves_per_eu(ORT_TRACE_WAVES)))
@@ -467,18 +488,6 @@ __device__ inline int newton_decide(const ort_surface* surf, int32_t n_surf, int
   return c;
 }
 
-// The Newton kernels' deferred-check pass (FAST = true in trace_ray) is compiled for the
-// lenses whose Newton surfaces are even / odd aspheres (the kinds ort_fastpath.h has
-// sequences for) without interactions, per-ray wavelengths or a tape; ORT_NO_NEWTON_FAST
-// (A/B builds) keeps the single exact pass.
-template <uint32_t FEAT>
-constexpr bool kNewtonFast =
-#ifdef ORT_NO_NEWTON_FAST
-    false;
-#else
-    (FEAT & F_KM) != 0 && (FEAT & F_KM & ~(ort::KM_EVEN | ort::KM_ODD)) == 0 &&
-    (FEAT & (F_IA | F_WRAY | F_TAPE)) == 0;
-#endif
 
 __device__ inline void store_ray(const KArgs& a, int64_t rid, const ort::Ray& r) {
   a.out.x[rid] = r.x;

@@ -885,9 +885,10 @@ class RealRayTracer:
             self._record(dlens, tmp, rec, n, segs, px, py, n_p)
         # queued ahead of the trace: the host waits on the trace's Newton check, and what
         # it issues after that is on the step's critical path
-        # one wavelength for every ray: a broadcast view (no 8 B/ray fill per step)
-        w = torch.full((1,), float(wavelength), dtype=torch.float64,
-                       device=dlens.device).expand(n)
+        # one wavelength for every ray: a broadcast view of a resident scalar (no fill
+        # per step, and no launch for it inside a captured step)
+        w = dlens.resident(("w_const", float(wavelength)),
+                           np.array([float(wavelength)])).expand(n)
         outs = autodiff.trace_pupil_grad(self.optic, dlens, seg_dev, px, py, n, n_p,
                                          wavelength, keys, newton_mode)
         out = RealRays.__new__(RealRays)
