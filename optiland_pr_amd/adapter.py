@@ -64,7 +64,7 @@ _ORIGINAL = {}
 # calls served by the op per dispatch key, and calls handed to the reference's own loop
 # (Unsupported), since install() -- so a caller can see which path ran; REASONS counts the
 # fallbacks by their Unsupported message
-STATS = {"cuda": 0, "cpu": 0, "fallback": 0}
+STATS = {"cuda": 0, "cpu": 0, "fallback": 0, "w_hint": 0}
 REASONS: dict = {}
 
 
@@ -284,7 +284,46 @@ def install():
             return _ORIGINAL["trace"](self, rays, skip)
 
     cls.trace = trace
+    _hook_ray_wavelength()
     return cls
+
+
+def _hook_ray_wavelength():
+    """Rays generated for a host scalar wavelength (RayGenerator.generate_rays,
+    rays/ray_generator.py:28-106: w = ones_like(x) * wavelength, every element exactly the
+    scalar) remember it, so the trace picks the lens's table row without reading rays.w
+    back from the device (a synchronising copy per call). The hint holds only while rays.w
+    is that same, unmodified tensor (identity and torch's in-place version counter)."""
+    try:
+        from optiland.rays import ray_generator as rg_mod
+    except Exception:  # pragma: no cover - reference layout without this module
+        return
+    cls = rg_mod.RayGenerator
+    if "generate_rays" in _ORIGINAL:
+        return
+    gen = cls.generate_rays
+    _ORIGINAL["generate_rays"] = gen
+
+    def generate_rays(self, *args, **kwargs):
+        rays = gen(self, *args, **kwargs)
+        wl = args[4] if len(args) > 4 else kwargs.get("wavelength")
+        if isinstance(wl, (int, float, np.floating)) and not isinstance(wl, bool):
+            w = getattr(rays, "w", None)
+            rays._ort_w = (w, getattr(w, "_version", None), float(wl))
+        return rays
+
+    cls.generate_rays = generate_rays
+
+
+def _host_wavelength(rays):
+    """The scalar wavelength rays were built with, when rays.w is still that tensor."""
+    hint = getattr(rays, "_ort_w", None)
+    if hint is None:
+        return None
+    w, version, wl = hint
+    if rays.w is not w or getattr(w, "_version", None) != version:
+        return None
+    return wl
 
 
 def uninstall():
@@ -292,6 +331,10 @@ def uninstall():
 
     if "trace" in _ORIGINAL:
         sg_mod.SurfaceGroup.trace = _ORIGINAL.pop("trace")
+    if "generate_rays" in _ORIGINAL:
+        from optiland.rays import ray_generator as rg_mod
+
+        rg_mod.RayGenerator.generate_rays = _ORIGINAL.pop("generate_rays")
 
 
 # geometries whose radius / conic the derivative kernels seed (the conic base of
@@ -487,8 +530,13 @@ def _trace_on_mi355x(group, rays, skip):
     w = w.detach().to(device=x.device, dtype=torch.float64).reshape(-1)
     if n == 0:
         raise Unsupported("empty ray batch")
-    lo_hi = torch.aminmax(w)  # one read decides table rows vs per-ray dispersion
-    lo, hi = (float(v) for v in torch.stack(lo_hi).cpu())
+    wh = _host_wavelength(rays)
+    if wh is not None:  # built from a host scalar: no device read
+        lo = hi = wh
+        STATS["w_hint"] += 1
+    else:
+        lo_hi = torch.aminmax(w)  # one read decides table rows vs per-ray dispersion
+        lo, hi = (float(v) for v in torch.stack(lo_hi).cpu())
     per_ray = lo != hi
     dl = _device_lens(group, [lo], per_ray, x.device)
     if torch.is_grad_enabled():

@@ -74,7 +74,7 @@ def test_reference_tests_pass_through_install(tmp_path):
                        timeout=1200)
     tail = "\n".join((r.stdout + r.stderr).splitlines()[-25:])
     assert r.returncode == 0, tail
-    stats, reasons = {"cuda": 0, "cpu": 0, "fallback": 0}, {}
+    stats, reasons = {"cuda": 0, "cpu": 0, "fallback": 0, "w_hint": 0}, {}
     for f in glob.glob(os.path.join(str(tmp_path), "*.json")):
         with open(f) as fh:
             d = json.load(fh)
@@ -87,6 +87,8 @@ def test_reference_tests_pass_through_install(tmp_path):
     # take the reference loop: counted as fallback, with their reasons)
     assert stats["cpu"] > 500, stats
     assert stats["cpu"] > stats["fallback"], stats
+    # rays generated from a scalar wavelength carried it to the trace (no read of rays.w)
+    assert stats["w_hint"] > 100, stats
 
 
 def _run_opt(tmp_path, mode, case):
