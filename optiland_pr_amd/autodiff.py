@@ -231,7 +231,12 @@ class CapturedStep:
     (the first included) then replays the graph once. `loss` is the graph's static loss
     tensor (read it after a synchronisation). `check()` reads the last replay's Newton
     flags of `lenses` (one synchronising copy) and raises as `raytrace.check_pending`
-    would: call it at the end of a run or every few steps."""
+    would: call it at the end of a run or every few steps.
+
+    A replay traces the lens as it was lowered at capture, reading the device-resident
+    parameter tensors (the optimizer's leaves) afresh each time; any other edit of the
+    lens (a setter, an in-place array edit, a new surface) needs a new CapturedStep. The
+    eager path (`eager()`) re-lowers the lens on every call and sees every edit."""
 
     def __init__(self, loss_fn, optimizer, lenses=(), warmup=3):
         self.loss_fn, self.opt, self.lenses, self.warmup = loss_fn, optimizer, list(lenses), warmup

@@ -130,6 +130,37 @@ def _device_tensor(v):
     return hasattr(v, "is_cuda") and bool(v.is_cuda)
 
 
+# Material lowering results by material key (BaseMaterial.key(): the formula source or
+# the constants themselves, so equal keys mean equal materials) and by (key, wavelength):
+# the dispersion records and n / alpha at the lens's wavelengths are the same from one
+# trace call to the next.
+_MAT_LOWER: dict = {}
+_MAT_N_ALPHA: dict = {}
+
+
+def _material_lower(m):
+    key = m.key()
+    hit = _MAT_LOWER.get(key)
+    if hit is None:
+        if len(_MAT_LOWER) > 4096:
+            _MAT_LOWER.clear()
+        hit = _MAT_LOWER[key] = m.lower()
+    return hit
+
+
+def _material_n_alpha(m, w):
+    key = (m.key(), w)
+    hit = _MAT_N_ALPHA.get(key)
+    if hit is None:
+        if len(_MAT_N_ALPHA) > 65536:
+            _MAT_N_ALPHA.clear()
+        kv = m.k_scalar(w)
+        # homogeneous.py:49-54: applied only when k > 0; alpha = 4*pi*k/w
+        hit = (m.n_scalar(w), (4 * np.pi * np.float64(kv) / np.float64(w)) if kv > 0 else 0.0)
+        _MAT_N_ALPHA[key] = hit
+    return hit
+
+
 def lower_surface_group(surface_group, wavelengths, record=False, skip_object=True):
     """Lower every traced surface (index >= 1) of `surface_group`.
 
@@ -157,7 +188,9 @@ def lower_surface_group(surface_group, wavelengths, record=False, skip_object=Tr
     else:
         rec_set = []
 
-    table = np.zeros(len(surfs), dtype=_abi.SURFACE)
+    # per-surface fields gathered in plain dicts and written column by column at the end
+    # (numpy structured-row assignment costs ~1 us per field: most of a lowering)
+    rows = [{} for _ in surfs]
     ops, coef, zern = [], [], []
     ap_progs = []
     ia_blocks = []
@@ -165,7 +198,7 @@ def lower_surface_group(surface_group, wavelengths, record=False, skip_object=Tr
     for si, s in enumerate(surfs):
         g = s.geometry
         R, k, tol, max_iter, norm_radius, cc = g.lower_params()
-        row = table[si]
+        row = rows[si]
         row["geometry"] = g.geometry_id
         row["radius"] = R
         row["conic"] = k
@@ -249,11 +282,11 @@ def lower_surface_group(surface_group, wavelengths, record=False, skip_object=Tr
             row["flags"] = int(row["flags"]) | _abi.SURF_TRANSLATE
 
     for si, prog in ap_progs:  # after every geometry block (coef offsets fixed above)
-        table[si]["ap_off"] = len(coef)
-        table[si]["ap_len"] = len(prog)
+        rows[si]["ap_off"] = len(coef)
+        rows[si]["ap_len"] = len(prog)
         coef.extend(prog)
     for si, blk in ia_blocks:  # interaction parameter blocks (ort_interaction)
-        table[si]["ia_off"] = len(coef)
+        rows[si]["ia_off"] = len(coef)
         coef.extend(blk)
 
     final = surfs[-1]
@@ -263,7 +296,7 @@ def lower_surface_group(surface_group, wavelengths, record=False, skip_object=Tr
     # their coefficient / tabulated-k blocks after everything else in coef
     mat_table = np.zeros(len(mats), dtype=_abi.MATERIAL)
     for mi, m in enumerate(mats):
-        kind, cc, kw, kv, n_const, k_const = m.lower()
+        kind, cc, kw, kv, n_const, k_const = _material_lower(m)
         row = mat_table[mi]
         row["kind"] = kind
         row["n_coef"] = len(cc) // 2 if kind == _abi.MAT_TABULATED else len(cc)
@@ -277,27 +310,27 @@ def lower_surface_group(surface_group, wavelengths, record=False, skip_object=Tr
         row["k_const"] = k_const
 
     cs = np.zeros(max(1, len(ops)), dtype=_abi.CS_OP)
-    for i, (kind, p) in enumerate(ops):
-        cs[i]["kind"] = kind
-        cs[i]["p"] = p
+    if ops:
+        cs["kind"] = [kind for kind, _ in ops]
+        cs["p"] = [p for _, p in ops]
     z = np.zeros(max(1, len(zern)), dtype=_abi.ZERNIKE_TERM)
-    for i, (c, norm, n, m, off, nr) in enumerate(zern):
-        z[i] = (c, norm, n, m, off, nr)
+    if zern:
+        z[:] = zern  # (c, norm, n, m, rad_off, n_rad) rows in field order
 
     n_tab = np.zeros((len(wavelengths), len(mats)))
     alpha_tab = np.zeros((len(wavelengths), len(mats)))
     for j, w in enumerate(wavelengths):
         for mi, m in enumerate(mats):
-            n_tab[j, mi] = m.n_scalar(w)
-            kv = m.k_scalar(w)
-            # homogeneous.py:49-54: applied only when k > 0; alpha = 4*pi*k/w
-            alpha_tab[j, mi] = (4 * np.pi * np.float64(kv) / np.float64(w)) if kv > 0 else 0.0
-    for row in table:  # absorption decided per surface when every wavelength row agrees
-        a = alpha_tab[:, int(row["mat_pre"])]
+            n_tab[j, mi], alpha_tab[j, mi] = _material_n_alpha(m, w)
+    for row in rows:  # absorption decided per surface when every wavelength row agrees
+        a = alpha_tab[:, row["mat_pre"]]
         if np.all(a > 0):
-            row["flags"] = int(row["flags"]) | _abi.SURF_ALPHA_ALL
+            row["flags"] |= _abi.SURF_ALPHA_ALL
         elif np.all(a == 0):
-            row["flags"] = int(row["flags"]) | _abi.SURF_ALPHA_NONE
+            row["flags"] |= _abi.SURF_ALPHA_NONE
+    table = np.zeros(len(surfs), dtype=_abi.SURFACE)
+    for name in {k for row in rows for k in row}:
+        table[name] = [row.get(name, 0) for row in rows]
     return LensTable(
         surfaces=table,
         cs_ops=cs,
