@@ -584,8 +584,11 @@ __device__ inline __attribute__((always_inline)) ort::Ray trace_ray(const KArgs&
                                         hn, hnx, hny, hnz, hist, sched, bad);
         if constexpr ((FEAT & F_TAPE) != 0) {
           if (active) {
+            // only the iterates the adjoint replays (m < min(U, kHist), adj_ray) are written
+            const int U = sched ? sched[group * a.n_surf + si] : s.max_iter;
 #pragma unroll
-            for (int h = 0; h < kHist; ++h) tp[(7 + h) * a.n_rays] = hist[h];
+            for (int h = 0; h < kHist; ++h)
+              if (h < U) tp[(7 + h) * a.n_rays] = hist[h];
           }
         }
       } else {
@@ -838,8 +841,11 @@ __global__ __launch_bounds__(kBlock) ORT_TRACE_OCC void trace_kernel(const KArgs
                                   hnx, hny, hnz, hist, sched, unused);
         if constexpr ((FEAT & F_TAPE) != 0) {
           if (active) {
+            // only the iterates the adjoint replays (m < min(U, kHist), adj_ray) are written
+            const int U = sched ? sched[group * a.n_surf + si] : s.max_iter;
 #pragma unroll
-            for (int h = 0; h < kHist; ++h) tp[(7 + h) * a.n_rays] = hist[h];
+            for (int h = 0; h < kHist; ++h)
+              if (h < U) tp[(7 + h) * a.n_rays] = hist[h];
           }
         }
       } else {
