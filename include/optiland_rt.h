@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define ORT_ABI_VERSION 15
+#define ORT_ABI_VERSION 16
 #define ORT_MAX_SURFACES 64
 
 /* ---- geometry kinds ----------------------------------- */
@@ -169,7 +169,17 @@ typedef struct ort_surface {
   double two_r;
   double one_plus_k;
   double r_sq;
-} ort_surface; /* 168 bytes */
+  /* Zernike surfaces up to radial order 6 (v16): the term sum also in Cartesian form,
+   * a block at lens.coef[zm_off]: As[K] (the sag's monomial coefficients, normalisation
+   * included), An[K] (the normal's: zernike.py:163-231 omits the normalisation
+   * constant), then the per-term monomials Ms[nt][K] (= norm_j * Mn[j]) and Mn[nt][K],
+   * K = (zm_deg + 1)(zm_deg + 2) / 2 in p-major order of xn^p yn^q (q fastest), xn = x /
+   * norm_radius. zm_deg < 0: polar evaluation only. As / An are sum_j c_j M[j] in term
+   * order (acc = acc + c_j M[j][k]): formed by the host, or on the device by
+   * ort_patch_zernike after device-resident coefficients change. */
+  int32_t zm_off;
+  int32_t zm_deg;
+} ort_surface; /* 176 bytes */
 
 /* Aperture programs (the physical_apertures package): postfix, each op a double opcode followed
  * by its operands; primitives push contains(x, y) of the ray's local (x, y), the boolean
@@ -596,6 +606,16 @@ int ort_trace_sequential_vjp(const ort_lens* lens, const ort_rays* rays_in,
  *     follow the global stop rule over the n rays with opt / newton_stat exactly as
  *     ort_trace_sequential with group_len = n (opt NULL: max_iter updates).
  * status: ORT_STATUS_ZERNIKE_RANGE as for the trace (zernike.py:234-246). */
+/* Device-resident Zernike coefficients (v16): zern[rows[i]].c = c[i] for i < n, then every
+ * Cartesian block (ort_surface.zm_off) of the lens re-formed from the term table:
+ * As = sum_j c_j Ms[j], An = sum_j c_j Mn[j] in term order. Writes the lens's term table
+ * and coefficient array (caller-owned device memory the lens points to); one single-
+ * workgroup launch, no synchronisation. Replaces the host-side coefficient upload of
+ * ZernikeCoeffVariable.update_value (optimization/variable/zernike_coeff.py:71-95) for
+ * coefficients held in HBM. */
+int ort_patch_zernike(const ort_lens* lens, const double* c, const int64_t* rows, int64_t n,
+                      void* stream);
+
 int ort_surface_sag_normal(const ort_lens* lens, int32_t surface, const double* x,
                            const double* y, int64_t n, double* sag, double* nx, double* ny,
                            double* nz, int32_t* status, void* stream);

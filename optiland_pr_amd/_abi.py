@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import numpy as np
 
-ABI_VERSION = 15
+ABI_VERSION = 16
 VJP_UNROLLED = 0
 VJP_ADJOINT = 1
 AP_RADIAL = 1
@@ -130,10 +130,12 @@ SURFACE = np.dtype(
         ("two_r", "<f8"),
         ("one_plus_k", "<f8"),
         ("r_sq", "<f8"),
+        ("zm_off", "<i4"),
+        ("zm_deg", "<i4"),
     ],
     align=True,
 )
-assert SURFACE.itemsize == 168
+assert SURFACE.itemsize == 176
 
 SURFACE_OPTICS = np.dtype(
     [("n_pre", "<f8"), ("u", "<f8"), ("alpha_pre", "<f8"), ("n_post", "<f8"), ("u_sq", "<f8")],

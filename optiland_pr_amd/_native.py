@@ -126,7 +126,7 @@ EXPORTS = ("ort_abi_version", "ort_trace_sequential", "ort_trace_pupil", "ort_tr
            "ort_surface_sag_normal", "ort_surface_distance", "ort_generate_rays",
            "ort_material_nk", "ort_spot_workspace_size", "ort_spot_stats", "ort_trace_spot", "ort_spot_partials",
            "ort_rms_spot_workspace_size", "ort_rms_spot", "ort_rms_spot_vjp",
-           "ort_wavefront_workspace_size", "ort_wavefront_opd")
+           "ort_wavefront_workspace_size", "ort_wavefront_opd", "ort_patch_zernike")
 
 _lib = None
 
@@ -171,6 +171,9 @@ def load(path: str | None = None):
     lib.ort_vjp_tape_size.argtypes = [P(ort_lens), P(ort_batch)]
     lib.ort_vjp_workspace_size.restype = C.c_int64
     lib.ort_vjp_workspace_size.argtypes = [P(ort_lens), P(ort_batch), P(ort_vjp_params)]
+    lib.ort_patch_zernike.restype = C.c_int
+    lib.ort_patch_zernike.argtypes = [P(ort_lens), C.c_void_p, C.c_void_p, C.c_int64,
+                                      C.c_void_p]
     lib.ort_surface_sag_normal.restype = C.c_int
     lib.ort_surface_sag_normal.argtypes = [P(ort_lens), C.c_int32, C.c_void_p, C.c_void_p,
                                            C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p,

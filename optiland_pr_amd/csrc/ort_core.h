@@ -934,13 +934,119 @@ ORT_INLINE void polar_unit(const T& xn, const T& yn, const T& rho, T& c1, T& s1)
   }
 }
 
+// ---- Zernike term sums in Cartesian form (ort_surface.zm_off / zm_deg, ABI v16) --------
+// Up to radial order 6 the host also lowers sum_j c_j Z_j as a polynomial in the normalised
+// coordinates, A[p][q] xn^p yn^q (p-major, q fastest; geometries.zernike_monomials: the
+// exact integer expansion of R_n^|m|(rho) {cos|sin}(|m| phi) through Re / Im (xn + i yn)^a
+// and rho^2 = xn^2 + yn^2), so a Newton evaluation is a two-level Horner scheme instead of
+// a recurrence and a radial Horner per term. Nested Horner with derivatives (the inner
+// level in yn, the outer in xn): value, gradient and Hessian w.r.t. (xn, yn).
+template <class T>
+struct IsPlain {
+  static constexpr bool value = false;
+};
+template <>
+struct IsPlain<double> {
+  static constexpr bool value = true;
+};
+
+template <class PD>
+ORT_INLINE double zmono_value(PD A, int N, double x, double y) {
+  double F = 0.0;
+  for (int p = N; p >= 0; --p) {
+    const int o = p * (N + 1) - p * (p - 1) / 2, L = N - p;
+    double B = A[o + L];
+    for (int q = L - 1; q >= 0; --q) B = B * y + A[o + q];
+    F = F * x + B;
+  }
+  return F;
+}
+
+template <class PD>
+ORT_INLINE void zmono_grad(PD A, int N, double x, double y, double& F, double& Fx,
+                           double& Fy) {
+  F = 0.0;
+  Fx = 0.0;
+  Fy = 0.0;
+  for (int p = N; p >= 0; --p) {
+    const int o = p * (N + 1) - p * (p - 1) / 2, L = N - p;
+    double B = A[o + L], B1 = 0.0;
+    for (int q = L - 1; q >= 0; --q) {
+      B1 = B1 * y + B;
+      B = B * y + A[o + q];
+    }
+    Fx = Fx * x + F;
+    F = F * x + B;
+    Fy = Fy * x + B1;
+  }
+}
+
+template <class PD>
+ORT_INLINE void zmono_hess(PD A, int N, double x, double y, double& F, double& Fx, double& Fy,
+                           double& Fxx, double& Fxy, double& Fyy) {
+  F = Fx = Fy = Fxx = Fxy = Fyy = 0.0;
+  for (int p = N; p >= 0; --p) {
+    const int o = p * (N + 1) - p * (p - 1) / 2, L = N - p;
+    double B = A[o + L], B1 = 0.0, B2 = 0.0;
+    for (int q = L - 1; q >= 0; --q) {
+      B2 = B2 * y + 2.0 * B1;
+      B1 = B1 * y + B;
+      B = B * y + A[o + q];
+    }
+    Fxx = Fxx * x + 2.0 * Fx;
+    Fx = Fx * x + F;
+    F = F * x + B;
+    Fxy = Fxy * x + Fy;
+    Fy = Fy * x + B1;
+    Fyy = Fyy * x + B2;
+  }
+}
+
 // sag (zernike.py:133-161; sets range_error on |x/R_norm| > 1 or |y/R_norm| > 1,
 // :234-246) and, with want_normal, the normal (zernike.py:163-231; the normal omits the
 // normalisation constant: reference quirk)
 template <class T, class S, class PD, class PZ>
 ORT_INLINE T sagnorm_zernike(const T& x, const T& y, const S& R, const S& k, double Rn, PZ Tm,
                              int t0, int nt, PD coef, const ZSeed& zs, bool want_normal,
-                             bool& range_error, T& nx, T& ny, T& nz) {
+                             bool& range_error, T& nx, T& ny, T& nz, int zm_off = 0,
+                             int zm_deg = -1) {
+  if constexpr (IsPlain<T>::value && IsPlain<S>::value) {
+    if (zm_deg >= 0) {
+      // Cartesian form: the sag from As, the normal's slopes from An's gradient mapped
+      // through the reference's eps-guarded chain rule, d/dx = dF/drho drho/dx + dF/dphi
+      // dphi/dx with dF/drho = (xn Fx + yn Fy) / rho and dF/dphi = xn Fy - yn Fx
+      double xn, yn;
+      div2(x, y, Rn, xn, yn);
+      if (::fabs(xn) > 1.0 || ::fabs(yn) > 1.0) range_error = true;
+      const double r2 = x * x + y * y;
+      const double q = sqrt(1.0 - (1.0 + k) * r2 / (R * R));
+      const double z = r2 / (R * (1.0 + q));
+      const int K = (zm_deg + 1) * (zm_deg + 2) / 2;
+      const PD As = coef + zm_off;
+      const double F = zmono_value(As, zm_deg, xn, yn);
+      if (want_normal) {
+        double G, Gx, Gy;
+        zmono_grad(As + K, zm_deg, xn, yn, G, Gx, Gy);
+        double dzdx, dzdy;
+        div2(x, y, R * q, dzdx, dzdy);
+        const double eps = 1e-14;
+        const double rho = sqrt(xn * xn + yn * yn);
+        double xr, yr, drho_dx, drho_dy, qy, qx;
+        div2(x, y, Rn * Rn, xr, yr);
+        div2(xr, yr, rho + eps, drho_dx, drho_dy);
+        div2(-(yn), xn, rho * rho + eps, qy, qx);
+        const double inv_rn = 1.0 / Rn;
+        const double G1 = xn * Gx + yn * Gy, G2 = xn * Gy - yn * Gx;
+        const double Fr = rho > 0.0 ? G1 / rho : 0.0;
+        dzdx = dzdx + (Fr * drho_dx + G2 * (qy * inv_rn));
+        dzdy = dzdy + (Fr * drho_dy + G2 * (qx * inv_rn));
+        double norm = sqrt(dzdx * dzdx + dzdy * dzdy + 1.0);
+        norm = norm < eps ? 1.0 : norm;
+        unit_normal3(dzdx, dzdy, norm, nx, ny, nz);
+      }
+      return z + F;
+    }
+  }
   T xn, yn;
   div2(x, y, Rn, xn, yn);
   if (::fabs(vv(xn)) > 1.0 || ::fabs(vv(yn)) > 1.0) range_error = true;
@@ -1135,7 +1241,7 @@ struct SurfJet {
 
 template <class PD, class PZ>
 ORT_INLINE void zernike_jet(double x, double y, double R, double k, double Rn, PZ Tm, int t0,
-                            int nt, PD coef, SurfJet& J) {
+                            int nt, PD coef, SurfJet& J, int zm_off = 0, int zm_deg = -1) {
   // base conic (standard.py:73-87, 154-167): z = r2 / (R (1 + q)), slope x / (R q)
   const double r2 = x * x + y * y;
   const double q = sqrt(1.0 - (1.0 + k) * r2 / (R * R));
@@ -1148,6 +1254,23 @@ ORT_INLINE void zernike_jet(double x, double y, double R, double k, double Rn, P
   J.sxy = h * x * y;
   J.syy = iRq + h * y * y;
   const double xn = x / Rn, yn = y / Rn;
+  if (zm_deg >= 0) {  // Cartesian form (zmono_*): exact derivatives of both polynomials
+    const int K = (zm_deg + 1) * (zm_deg + 2) / 2;
+    const double iRn = 1.0 / Rn;
+    double F, Fx, Fy, G, Gx, Gy, Gxx, Gxy, Gyy;
+    zmono_grad(coef + zm_off, zm_deg, xn, yn, F, Fx, Fy);
+    zmono_hess(coef + zm_off + K, zm_deg, xn, yn, G, Gx, Gy, Gxx, Gxy, Gyy);
+    J.z += F;
+    J.zx = J.sx + Fx * iRn;
+    J.zy = J.sy + Fy * iRn;
+    J.sx += Gx * iRn;
+    J.sy += Gy * iRn;
+    const double iRn2 = iRn * iRn;
+    J.sxx += Gxx * iRn2;
+    J.sxy += Gxy * iRn2;
+    J.syy += Gyy * iRn2;
+    return;
+  }
   const double rho = sqrt(xn * xn + yn * yn);
   double c1 = 1.0, s1 = 0.0;  // cos / sin phi (atan2(0, 0) = 0)
   if (rho > 0.0) {
@@ -1643,7 +1766,7 @@ ORT_INLINE T newton_sagnorm(const ort_surface& s, const S& R, const S& K, PD coe
   if constexpr ((KM & KM_ZERN) != 0) {
     if ((KM & ~KM_ZERN) == 0 || s.geometry == ORT_GEOM_ZERNIKE)
       return sagnorm_zernike(x, y, R, K, s.norm_radius, zern, s.coef_off, s.n_coef, coef, zs,
-                             want_normal, range_error, nx, ny, nz);
+                             want_normal, range_error, nx, ny, nz, s.zm_off, s.zm_deg);
   }
   if constexpr ((KM & KM_FREE) != 0) {
     switch (s.geometry) {

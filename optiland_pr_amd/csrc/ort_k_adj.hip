@@ -131,3 +131,49 @@ extern "C" int ort_newton_fixup(const ort_lens* lens, int64_t n_groups,
                      prev_flag, flag, next_stats, next_status);
   return hipGetLastError() == hipSuccess ? ORT_OK : ORT_ERR_LAUNCH;
 }
+
+// ---- device-resident Zernike coefficients (ort_patch_zernike) ------------------------
+// One workgroup: the patched coefficients into the term table, then every Cartesian block
+// of the lens re-formed from it (As / An = sum_j c_j Ms[j] / Mn[j], term order, no FMA:
+// the host's order in geometries.zernike_monomial_block, so a device-resident coefficient
+// gives the same bits as the same value uploaded from the host).
+namespace ortk {
+__global__ __launch_bounds__(kBlock) void patch_zernike_kernel(const ort_surface* surf,
+                                                               int32_t n_surf,
+                                                               ort_zernike_term* zern,
+                                                               double* coef, const double* c,
+                                                               const int64_t* rows, int64_t n) {
+  for (int64_t i = threadIdx.x; i < n; i += kBlock) zern[rows[i]].c = c[i];
+  __threadfence();
+  __syncthreads();
+  for (int si = 0; si < n_surf; ++si) {
+    const ort_surface s = surf[si];
+    if (s.geometry != ORT_GEOM_ZERNIKE || s.zm_deg < 0) continue;
+    const int K = (s.zm_deg + 1) * (s.zm_deg + 2) / 2;
+    const int nt = s.n_coef;
+    const double* Ms = coef + s.zm_off + 2 * K;
+    const double* Mn = Ms + (int64_t)nt * K;
+    for (int k = threadIdx.x; k < 2 * K; k += kBlock) {
+      const double* M = k < K ? Ms : Mn;
+      const int kk = k < K ? k : k - K;
+      double acc = 0.0;
+      for (int jt = 0; jt < nt; ++jt) acc = acc + zern[s.coef_off + jt].c * M[(int64_t)jt * K + kk];
+      coef[s.zm_off + k] = acc;
+    }
+  }
+}
+}  // namespace ortk
+
+extern "C" int ort_patch_zernike(const ort_lens* lens, const double* c, const int64_t* rows,
+                                 int64_t n, void* stream) {
+  using namespace ortk;
+  if (!lens || n < 0 || (n > 0 && (!c || !rows))) return ORT_ERR_ARG;
+  if (lens->n_surfaces < 1 || lens->n_surfaces > ORT_MAX_SURFACES || !lens->surfaces ||
+      !lens->zern || !lens->coef)
+    return ORT_ERR_ARG;
+  hipLaunchKernelGGL(patch_zernike_kernel, dim3(1), dim3(kBlock), 0, (hipStream_t)stream,
+                     lens->surfaces, lens->n_surfaces,
+                     const_cast<ort_zernike_term*>(lens->zern), const_cast<double*>(lens->coef),
+                     c, rows, n);
+  return hipGetLastError() == hipSuccess ? ORT_OK : ORT_ERR_LAUNCH;
+}

@@ -464,7 +464,7 @@ ORT_INLINE void adj_ray(const KArgs& a, const AArgs& j, Lane& ln, int64_t rid, b
       if (KM == ort::KM_ZERN || s.geometry == ORT_GEOM_ZERNIKE) {
         ort::SurfJet J;
         ort::zernike_jet(x, y, s.radius, s.conic, s.norm_radius, cst(a.zern), s.coef_off,
-                         s.n_coef, cst(a.coef), J);
+                         s.n_coef, cst(a.coef), J, s.zm_off, s.zm_deg);
         ort::jet_normal(J, nx, ny, nz);
         D z(J.z);
         z.d[0] = J.zx;

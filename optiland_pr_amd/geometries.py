@@ -279,6 +279,79 @@ def radial_coefficients(n, m_abs):
     return tuple(a), tuple(d)
 
 
+# Radial orders up to which a Zernike surface's term sum is also lowered in Cartesian
+# (monomial) form and evaluated that way by the Newton kernels (ort_core.h zmono_*): the
+# expansion's coefficients grow with the order (cancellation ~ eps x sum |coefficient|),
+# so higher orders keep the polar recurrence.
+ZM_MAX_DEG = 6
+
+
+@functools.lru_cache(maxsize=None)
+def zernike_monomials(n, m):
+    """R_n^|m|(rho) * {cos m phi | sin |m| phi} (zernike/base.py:42-68, 228-253) as a
+    polynomial in the normalised coordinates (xn, yn): {(p, q): coefficient of xn^p yn^q}.
+    rho^a cos(a phi) = Re (xn + i yn)^a, rho^a sin(a phi) = Im (xn + i yn)^a and
+    rho^2 = xn^2 + yn^2, with the reference's radial weights a_k (radial_coefficients):
+    integers, so every coefficient here is an exact double."""
+    a = abs(m)
+    ak, _ = radial_coefficients(n, a)
+    ang = {}
+    for j in range(a + 1):  # binomial expansion of (xn + i yn)^a
+        c = math.comb(a, j) * (-1) ** (j // 2)
+        if (j % 2 == 0) == (m >= 0):
+            ang[(a - j, j)] = c
+    out = {}
+    for k, w in enumerate(ak):
+        e = (n - 2 * k - a) // 2  # rho^(n - 2k) = rho^a (rho^2)^e
+        for i in range(e + 1):
+            ce = math.comb(e, i)
+            for (p, q), cz in ang.items():
+                key = (p + 2 * i, q + 2 * (e - i))
+                out[key] = out.get(key, 0.0) + w * ce * cz
+    return out
+
+
+def monomial_index(N):
+    """(p, q) -> position in the p-major triangular block of degree N (ort_core.h)."""
+    idx, k = {}, 0
+    for p in range(N + 1):
+        for q in range(N - p + 1):
+            idx[(p, q)] = k
+            k += 1
+    return idx
+
+
+def zernike_monomial_block(terms, on_device):
+    """The Cartesian block of a Zernike surface (ort_surface.zm_off / zm_deg): degree N,
+    then [As (K)] [An (K)] [Ms (nt x K)] [Mn (nt x K)] with K = (N+1)(N+2)/2:
+    Mn[j] the monomials of term j, Ms[j] = norm_j * Mn[j]; As / An their sums weighted by
+    the coefficients -- the sag's (normalised) and the normal's (the reference's normal
+    omits the normalisation constant, zernike.py:163-231) -- formed in term order as
+    acc = acc + c_j * M[j][k], the order ort_patch_zernike uses on the device (zeros when
+    the coefficients live on the device and are patched there). None above ZM_MAX_DEG."""
+    if not terms:
+        return None
+    N = max(int(t[2]) for t in terms)
+    if N > ZM_MAX_DEG:
+        return None
+    idx = monomial_index(N)
+    K = len(idx)
+    Mn = np.zeros((len(terms), K))
+    Ms = np.zeros((len(terms), K))
+    for j, (c, norm, n, m, _a, _d) in enumerate(terms):
+        for key, v in zernike_monomials(int(n), int(m)).items():
+            Mn[j, idx[key]] = v
+        Ms[j] = np.float64(norm) * Mn[j]
+    As, An = [0.0] * K, [0.0] * K
+    if not on_device:
+        for j, t in enumerate(terms):
+            c = float(t[0])
+            for k in range(K):
+                As[k] = As[k] + c * float(Ms[j, k])
+                An[k] = An[k] + c * float(Mn[j, k])
+    return N, As + An + [float(v) for v in Ms.ravel()] + [float(v) for v in Mn.ravel()]
+
+
 @functools.lru_cache(maxsize=None)
 def _zernike_structure(kind, n_c):
     """(norm, n, m, a_k, d_k) of the first n_c terms of a scheme: value-independent, so

@@ -24,7 +24,8 @@ import numpy as np
 
 from . import _abi
 from .apertures import RadialAperture, program_depth
-from .geometries import NewtonRaphsonGeometry, ZernikePolynomialGeometry, scalar
+from .geometries import (NewtonRaphsonGeometry, ZernikePolynomialGeometry, scalar,
+                         zernike_monomial_block)
 from .surfaces import ObjectSurface
 
 
@@ -199,6 +200,7 @@ def lower_surface_group(surface_group, wavelengths, record=False, skip_object=Tr
         g = s.geometry
         R, k, tol, max_iter, norm_radius, cc = g.lower_params()
         row = rows[si]
+        row["zm_deg"] = -1
         row["geometry"] = g.geometry_id
         row["radius"] = R
         row["conic"] = k
@@ -251,6 +253,11 @@ def lower_surface_group(surface_group, wavelengths, record=False, skip_object=Tr
                 zern.append((c, norm, n, m, len(coef), len(a)))
                 coef.extend(a)
                 coef.extend(d)
+            blk = zernike_monomial_block(terms, on_device)
+            if blk is not None:
+                row["zm_off"] = len(coef)
+                row["zm_deg"] = blk[0]
+                coef.extend(blk[1])
         else:
             row["coef_off"] = len(coef)
             row["n_coef"] = len(cc)

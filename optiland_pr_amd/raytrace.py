@@ -183,23 +183,22 @@ class DeviceLens:
 
     def patch_coefficients(self, device_coeffs):
         """Write device-resident Zernike coefficients into the uploaded term table
-        (ort_zernike_term.c, the first double of each 32-byte row): a device-to-device
-        copy ordered on the current stream, no host round trip."""
-        rows = self.zern.view(torch.float64).view(-1, _abi.ZERNIKE_TERM.itemsize // 8)
+        (ort_zernike_term.c) and re-form the surfaces' Cartesian blocks from them
+        (ort_patch_zernike: one launch, after one concatenation when several surfaces
+        hold device coefficients), ordered on the current stream, no host round trip."""
         vals = [t.detach().reshape(-1).to(device=self.device, dtype=torch.float64)
                 for _, t in device_coeffs]
-        if len(vals) == 1:
-            rows[device_coeffs[0][0]:device_coeffs[0][0] + vals[0].numel(), 0].copy_(vals[0])
-            return
-        # several surfaces: one concatenation and one indexed copy instead of one strided
-        # copy per surface (the row indices cached per layout)
         key = tuple((off, v.numel()) for (off, _), v in zip(device_coeffs, vals))
         idx = self._patch_index.get(key)
-        if idx is None:
+        if idx is None:  # the term rows of this layout, cached
             idx = torch.as_tensor(np.concatenate([np.arange(o, o + n) for o, n in key]),
                                   dtype=torch.int64, device=self.device)
             self._patch_index[key] = idx
-        rows[:, 0].index_copy_(0, idx, torch.cat(vals))
+        c = vals[0].contiguous() if len(vals) == 1 else torch.cat(vals)
+        lib = _native.load()
+        rc = lib.ort_patch_zernike(C.byref(self.c), _ptr(c), _ptr(idx), int(c.numel()),
+                                   _stream_handle())
+        _native.check(rc, "ort_patch_zernike")
 
     # -- Newton schedule speculate / verify ---------------------------------------------
     def initial_schedule(self, keys):
