@@ -133,33 +133,44 @@ extern "C" int ort_newton_fixup(const ort_lens* lens, int64_t n_groups,
 }
 
 // ---- device-resident Zernike coefficients (ort_patch_zernike) ------------------------
-// One workgroup: the patched coefficients into the term table, then every Cartesian block
-// of the lens re-formed from it (As / An = sum_j c_j Ms[j] / Mn[j], term order, no FMA:
-// the host's order in geometries.zernike_monomial_block, so a device-resident coefficient
-// gives the same bits as the same value uploaded from the host).
+// One workgroup per traced surface (the Zernike ones work, the others leave): the surface's
+// coefficients gathered into LDS from the term table, the patched ones written over them
+// (and into the table), then the surface's Cartesian block re-formed from LDS (As / An =
+// sum_j c_j Ms[j] / Mn[j], term order, no FMA: the host's order in
+// geometries.zernike_monomial_block, so a device-resident coefficient gives the same bits
+// as the same value uploaded from the host). A surface of more than kPatchTerms terms
+// gets its coefficients written into the table only (it has no block: radial order 6
+// holds 28 terms).
 namespace ortk {
+constexpr int kPatchTerms = 1024;
+
 __global__ __launch_bounds__(kBlock) void patch_zernike_kernel(const ort_surface* surf,
-                                                               int32_t n_surf,
                                                                ort_zernike_term* zern,
                                                                double* coef, const double* c,
                                                                const int64_t* rows, int64_t n) {
-  for (int64_t i = threadIdx.x; i < n; i += kBlock) zern[rows[i]].c = c[i];
-  __threadfence();
+  __shared__ double cs[kPatchTerms];
+  const ort_surface s = surf[blockIdx.x];
+  if (s.geometry != ORT_GEOM_ZERNIKE) return;
+  const int t0 = s.coef_off, nt = s.n_coef;
+  for (int jt = threadIdx.x; jt < nt && jt < kPatchTerms; jt += kBlock) cs[jt] = zern[t0 + jt].c;
   __syncthreads();
-  for (int si = 0; si < n_surf; ++si) {
-    const ort_surface s = surf[si];
-    if (s.geometry != ORT_GEOM_ZERNIKE || s.zm_deg < 0) continue;
-    const int K = (s.zm_deg + 1) * (s.zm_deg + 2) / 2;
-    const int nt = s.n_coef;
-    const double* Ms = coef + s.zm_off + 2 * K;
-    const double* Mn = Ms + (int64_t)nt * K;
-    for (int k = threadIdx.x; k < 2 * K; k += kBlock) {
-      const double* M = k < K ? Ms : Mn;
-      const int kk = k < K ? k : k - K;
-      double acc = 0.0;
-      for (int jt = 0; jt < nt; ++jt) acc = acc + zern[s.coef_off + jt].c * M[(int64_t)jt * K + kk];
-      coef[s.zm_off + k] = acc;
-    }
+  for (int64_t i = threadIdx.x; i < n; i += kBlock) {
+    const int64_t r = rows[i];
+    if (r < t0 || r >= t0 + nt) continue;  // another surface's term
+    zern[r].c = c[i];
+    if (r - t0 < kPatchTerms) cs[r - t0] = c[i];
+  }
+  __syncthreads();
+  if (s.zm_deg < 0 || nt > kPatchTerms) return;
+  const int K = (s.zm_deg + 1) * (s.zm_deg + 2) / 2;
+  const double* Ms = coef + s.zm_off + 2 * K;
+  const double* Mn = Ms + (int64_t)nt * K;
+  for (int k = threadIdx.x; k < 2 * K; k += kBlock) {
+    const double* M = k < K ? Ms : Mn;
+    const int kk = k < K ? k : k - K;
+    double acc = 0.0;
+    for (int jt = 0; jt < nt; ++jt) acc = acc + cs[jt] * M[(int64_t)jt * K + kk];
+    coef[s.zm_off + k] = acc;
   }
 }
 }  // namespace ortk
@@ -171,8 +182,8 @@ extern "C" int ort_patch_zernike(const ort_lens* lens, const double* c, const in
   if (lens->n_surfaces < 1 || lens->n_surfaces > ORT_MAX_SURFACES || !lens->surfaces ||
       !lens->zern || !lens->coef)
     return ORT_ERR_ARG;
-  hipLaunchKernelGGL(patch_zernike_kernel, dim3(1), dim3(kBlock), 0, (hipStream_t)stream,
-                     lens->surfaces, lens->n_surfaces,
+  hipLaunchKernelGGL(patch_zernike_kernel, dim3((unsigned)lens->n_surfaces), dim3(kBlock), 0,
+                     (hipStream_t)stream, lens->surfaces,
                      const_cast<ort_zernike_term*>(lens->zern), const_cast<double*>(lens->coef),
                      c, rows, n);
   return hipGetLastError() == hipSuccess ? ORT_OK : ORT_ERR_LAUNCH;
