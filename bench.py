@@ -404,13 +404,32 @@ def config5(args, dev, rank, world, torch):
         kernel="adj_kernel<KM_ZERN, 2> (ort_trace_pupil_vjp, adjoint mode)", launches=None,
         bytes_per_launch=None, flops_per_ray=None, pmc_file="hbm_traffic_c5.json", rays=R,
         state=state, vjp_timer=vjp_timer, eager_step=eager_step,
-        # the taped forward writes the tape, the adjoint only reads it: S x kTapeRows
-        # (ort_sweep.h) doubles per ray
-        tape_bytes_per_launch=S * 11 * 8 * R,
+        # the taped forward writes the tape, the adjoint only reads it: per traced surface the
+        # incoming ray and t (7 rows) plus, for a Newton surface, the min(U, 4) iterates it
+        # replays (ort_sweep.h adj_ray), with U the verified schedule -- read after the run
+        tape_bytes_per_launch=lambda: _tape_read_bytes(lens, R),
         # the adjoint launch's algorithmic HBM bytes: the tape read, the pupil samples
         # (16 B/ray), the primal outputs it reads (L, M, N, i: 32 B/ray), the cotangents
         # (x, y: 16 B/ray) and the wave partials written (30 Zernike slots + 1 per 64 rays)
-        algorithmic_bytes_per_launch=S * 11 * 8 * R + (16 + 32 + 16) * R + 31 * 8 * (R // 64))
+        algorithmic_bytes_per_launch=lambda: (_tape_read_bytes(lens, R) + (16 + 32 + 16) * R
+                                              + 31 * 8 * (R // 64)))
+
+
+def _tape_read_bytes(lens, R):
+    """Tape bytes the adjoint reads per launch: 7 rows per traced surface plus min(U, kHist)
+    Newton iterates per Newton surface (the rows the taped forward writes)."""
+    from optiland_pr_amd import _abi
+
+    dl = next(iter(getattr(lens, "_lowered", {}).values()), None)
+    if dl is None:
+        return None
+    U = dl.sched_cache.get("_default")
+    rows = 0
+    for si, srow in enumerate(dl.table.surfaces):
+        rows += 7
+        if int(srow["geometry"]) in _abi.NEWTON_GEOMETRIES:
+            rows += min(int(U[si]) if U is not None else 4, 4)
+    return rows * 8 * R
 
 
 def vjp_timer(step, steps, torch):
@@ -588,6 +607,10 @@ def main():
         dist.destroy_process_group()
 
 
+def _val(v):
+    return v() if callable(v) else v
+
+
 def _roofline(w, kern_ms):
     if getattr(w, "spot", False):
         return {"bound": "launch", "achieved": None, "peak": None, "unit": None, "frac": None,
@@ -605,8 +628,8 @@ def _roofline(w, kern_ms):
                 "frac": None if achieved is None else achieved / SPEC_FP64_VEC_TFLOPS,
                 "traffic": pmc.get("bytes_per_launch"), "kernel": w.kernel,
                 "kernel_ms": w.vjp_ms, "step_device_ms": kern_ms,
-                "tape_bytes_per_launch": w.tape_bytes_per_launch,
-                "algorithmic_bytes_per_launch": w.algorithmic_bytes_per_launch,
+                "tape_bytes_per_launch": _val(w.tape_bytes_per_launch),
+                "algorithmic_bytes_per_launch": _val(w.algorithmic_bytes_per_launch),
                 "hbm_frac": None if pmc.get("bytes_per_launch") is None else
                 pmc["bytes_per_launch"] / (w.vjp_ms * 1e-3) / 1e9 / (SPEC_HBM_TBPS * 1e3),
                 "note": "achieved = hardware-counted FP64 FLOPs of adj_kernel "

@@ -46,3 +46,23 @@ def test_config5_adjoint_roofline():
 def test_launch_bound_spot_config_has_null_rates():
     r = bench._roofline(_w(spot=True), 0.023)
     assert ROOFLINE_KEYS <= set(r) and r["achieved"] is None and r["bound"] == "launch"
+
+
+def test_config5_tape_bytes_follow_the_schedule():
+    """The adjoint reads 7 tape rows per traced surface plus min(U, 4) Newton iterates per
+    Newton surface (the rows the taped forward writes): the TMA with one update per mirror
+    reads 31 rows x 8 B per ray."""
+    from types import SimpleNamespace
+
+    import numpy as np
+
+    from optiland_pr_amd.lowering import lower_surface_group
+    from optiland_pr_amd.samples import ThreeMirrorAnastigmat
+
+    lens = ThreeMirrorAnastigmat()
+    table = lower_surface_group(lens.surface_group, [0.587])
+    S = table.n_surfaces
+    U = np.array([1 if g == 4 else 0 for g in table.surfaces["geometry"]])
+    lens._lowered = {"k": SimpleNamespace(table=table, sched_cache={"_default": U})}
+    assert bench._tape_read_bytes(lens, 1_000_000) == (7 * S + int((U > 0).sum())) * 8 * 1_000_000
+    assert bench._tape_read_bytes(lens, 1_000_000) == 31 * 8 * 1_000_000
