@@ -493,6 +493,9 @@ ORT_INLINE void adj_ray(const KArgs& a, const AArgs& j, Lane& ln, int64_t rid, b
                       double w_sag, double bnx, double bny, double bnz, double nxv,
                       double nyv, double nzv) {
     if constexpr ((KM & ort::KM_ZERN) != 0) {
+#ifdef ORT_ADJ_NO_COEF  // timing builds only (A/B of the coefficient adjoint's cost)
+      return;
+#endif
       if (s.geometry == ORT_GEOM_ZERNIKE && j.zparam) {
         const double bn = bnx * nxv + bny * nyv + bnz * nzv;
         const double bdx = -nzv * (bnx - nxv * bn);
