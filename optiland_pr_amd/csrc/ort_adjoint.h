@@ -19,8 +19,10 @@ namespace ortk {
 // rocprofv3 A/B per adjoint launch on the MI355X, round 4, with the plain-double Zernike
 // jet): 2 waves per SIMD (184 VGPRs, no scratch) 755-757 us, 3 waves (168 VGPRs, 56 B of
 // scratch) 582-588 us, 4 waves (128 VGPRs, 216 B) 591-595 us -- the compiler's choice is
-// the slowest. Other kernels keep the compiler's choice. ORT_ADJ_WAVES overrides the target
-// for A/B builds.
+// the slowest. Re-measured after the Cartesian Zernike form (177 VGPRs uncapped): 3 waves
+// (168, 24 B) 437 us, 4 waves (128, 164 B) 446-452 us per ort_trace_pupil_vjp sequence.
+// Other kernels keep the compiler's choice. ORT_ADJ_WAVES overrides the target for A/B
+// builds.
 template <uint32_t KM, int P>
 struct AdjWaves {
   static constexpr int value = (P == 2 && (KM & ort::KM_ZERN) != 0 && KM < ort::KM_FREE) ? 3 : 1;

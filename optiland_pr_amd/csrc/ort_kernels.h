@@ -385,8 +385,9 @@ __device__ inline void interact(const KArgs& a, const ort_surface& s, ort::Ray& 
 // waves: 313 us). The even-asphere kernels already fit 6 waves; the rest keep the
 // compiler's choice. ORT_TRACE_WAVES overrides the target for A/B builds.
 // The taping forward (F_TAPE: the hist registers and 11 rows of stores per surface) runs
-// best unspilled at 4 waves: TMA 1M rays, taped trace 374 / 328 / 300 us at 6 / 5 / 4
-// waves per SIMD (rocprofv3 A/B).
+// best at 4 waves: TMA 1M rays, taped trace 374 / 328 / 300 us at 6 / 5 / 4 waves per
+// SIMD (rocprofv3 A/B); re-measured with the Cartesian Zernike form (131 VGPRs uncapped),
+// config 5 step 0.750-0.761 / 0.732-0.733 / 0.774-0.775 ms at 3 / 4 / 5 waves.
 // The Newton kernels' deferred-check pass (FAST = true in trace_ray) is compiled for the
 // lenses whose Newton surfaces are even / odd aspheres (the kinds ort_fastpath.h has
 // sequences for) without interactions, per-ray wavelengths or a tape; ORT_NO_NEWTON_FAST

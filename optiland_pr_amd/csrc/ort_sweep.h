@@ -493,7 +493,10 @@ ORT_INLINE void adj_ray(const KArgs& a, const AArgs& j, Lane& ln, int64_t rid, b
                       double w_sag, double bnx, double bny, double bnz, double nxv,
                       double nyv, double nzv) {
     if constexpr ((KM & ort::KM_ZERN) != 0) {
-#ifdef ORT_ADJ_NO_COEF  // timing builds only (A/B of the coefficient adjoint's cost)
+#ifdef ORT_ADJ_NO_COEF  // timing builds only (A/B of the coefficient adjoint's cost): one
+      // contribution per call instead of the term pass, so the sweep's data flow stays live
+      if (s.geometry == ORT_GEOM_ZERNIKE && j.zparam)
+        ln.zemit(3 * a.n_surf + s.coef_off, 0, on ? x * w_sag + y * bnx + bny + bnz : 0.0, first);
       return;
 #endif
       if (s.geometry == ORT_GEOM_ZERNIKE && j.zparam) {

@@ -25,7 +25,7 @@ def torch():
     import torch
 
     if not torch.cuda.is_available():
-        pytest.skip("no GPU")
+        pytest.fail("GPU tests need the MI355X (torch.cuda.is_available() is False)")
     return torch
 
 
