@@ -225,7 +225,8 @@ __device__ inline double grid_distance(const KArgs& a, const ort_surface& s, int
 // for operation, the propagated point Surface.trace takes the normal at
 // (standard_surface.py:215-225, homogeneous.py:45-47), so that normal is the
 // interaction's normal: one sag + normal evaluation per Newton surface saved.
-// F_TAPE: hist[m] = the iterate before the m-th last update (t_{U-1-m}), 0 beyond U, as
+// F_TAPE: tape (this ray's tape rows of surface si, nullptr for inactive lanes) gets row
+// 7 + m = the iterate before the m-th last update (t_{U-1-m}) for m < min(U, kHist), as
 // the adjoint's replay_distance tapes it.
 // FAST (trace_kernel's deferred-check pass): the initial conic guess, the even / odd
 // asphere evaluations and the updates on ort_fastpath.h's sequences, range failures ORed
@@ -263,13 +264,9 @@ __device__ inline __attribute__((always_inline)) double newton_distance(const KA
                                          const ort::Ray& r, bool active, int64_t group,
                                          bool group_uniform, int& range_bits, bool& hn,
                                          double& nnx, double& nny, double& nnz,
-                                         double (&hist)[kHist], const int32_t* sched,
+                                         double* tape, const int32_t* sched,
                                          bool& bad) {
   hn = false;
-  if constexpr ((FEAT & F_TAPE) != 0) {
-#pragma unroll
-    for (int h = 0; h < kHist; ++h) hist[h] = 0.0;
-  }
   if constexpr ((FEAT & ort::KM_FREE) != 0) {
     if (s.geometry == ORT_GEOM_GRID_SAG)
       return grid_distance<FEAT>(a, s, si, r, active, group, group_uniform, sched);
@@ -327,9 +324,10 @@ __device__ inline __attribute__((always_inline)) double newton_distance(const KA
       if (!conv) last_bad = j;
       if (upd) {
         if constexpr ((FEAT & F_TAPE) != 0) {
-#pragma unroll
-          for (int h = kHist - 1; h > 0; --h) hist[h] = hist[h - 1];
-          hist[0] = t;
+          // the iterate before the m-th last update, m = U - 1 - j, straight into its tape
+          // row (the adjoint replays m < min(U, kHist): adj_ray)
+          const int m = U - 1 - j;
+          if (m < kHist && tape) tape[(int64_t)(7 + m) * a.n_rays] = t;
         }
         if constexpr (FAST)
           t = ort::fast::newton_step(r, t, f, nx, ny, nz, bad);
@@ -384,7 +382,7 @@ __device__ inline void interact(const KArgs& a, const ort_surface& s, ort::Ray& 
 // forward runs 9% faster on the MI355X (334 -> 305 us per 1M-ray launch, rocprofv3; 5
 // waves: 313 us). The even-asphere kernels already fit 6 waves; the rest keep the
 // compiler's choice. ORT_TRACE_WAVES overrides the target for A/B builds.
-// The taping forward (F_TAPE: the hist registers and 11 rows of stores per surface) runs
+// The taping forward (F_TAPE: up to 11 rows of stores per surface) runs
 // best at 4 waves: TMA 1M rays, taped trace 374 / 328 / 300 us at 6 / 5 / 4 waves per
 // SIMD (rocprofv3 A/B); re-measured with the Cartesian Zernike form (131 VGPRs uncapped),
 // config 5 step 0.750-0.761 / 0.732-0.733 / 0.774-0.775 ms at 3 / 4 / 5 waves.
@@ -566,7 +564,6 @@ __device__ inline __attribute__((always_inline)) ort::Ray trace_ray(const KArgs&
     double t;
     bool hn = false;  // (hnx, hny, hnz): the Newton geometry's normal at t
     double hnx = 0.0, hny = 0.0, hnz = 0.0;
-    double hist[kHist];
     const bool radius_inf = (s.flags & ORT_SURF_RADIUS_INF) != 0;
     if (!known_geometry(s.geometry)) range_bits |= ORT_STATUS_BAD_GEOMETRY;
     if (s.geometry == ORT_GEOM_PLANE) {
@@ -582,16 +579,7 @@ __device__ inline __attribute__((always_inline)) ort::Ray trace_ray(const KArgs&
     } else {
       if constexpr ((FEAT & F_KM) != 0) {
         t = newton_distance<FEAT, FAST>(a, s, si, r, active, group, group_uniform, range_bits,
-                                        hn, hnx, hny, hnz, hist, sched, bad);
-        if constexpr ((FEAT & F_TAPE) != 0) {
-          if (active) {
-            // only the iterates the adjoint replays (m < min(U, kHist), adj_ray) are written
-            const int U = sched ? sched[group * a.n_surf + si] : s.max_iter;
-#pragma unroll
-            for (int h = 0; h < kHist; ++h)
-              if (h < U) tp[(7 + h) * a.n_rays] = hist[h];
-          }
-        }
+                                        hn, hnx, hny, hnz, active ? tp : nullptr, sched, bad);
       } else {
         t = __builtin_nan("");  // unreachable: the host sets geometry_mask
       }
@@ -829,7 +817,6 @@ __global__ __launch_bounds__(kBlock) ORT_TRACE_OCC void trace_kernel(const KArgs
     double t;
     bool hn = false;  // (hnx, hny, hnz): the Newton geometry's normal at t
     double hnx = 0.0, hny = 0.0, hnz = 0.0;
-    double hist[kHist];
     if (!known_geometry(s.geometry)) range_bits |= ORT_STATUS_BAD_GEOMETRY;
     if (s.geometry == ORT_GEOM_PLANE) {
       t = ort::distance_plane(r);
@@ -839,16 +826,7 @@ __global__ __launch_bounds__(kBlock) ORT_TRACE_OCC void trace_kernel(const KArgs
       if constexpr ((FEAT & F_KM) != 0) {
         bool unused = false;
         t = newton_distance<FEAT>(a, s, si, r, active, group, group_uniform, range_bits, hn,
-                                  hnx, hny, hnz, hist, sched, unused);
-        if constexpr ((FEAT & F_TAPE) != 0) {
-          if (active) {
-            // only the iterates the adjoint replays (m < min(U, kHist), adj_ray) are written
-            const int U = sched ? sched[group * a.n_surf + si] : s.max_iter;
-#pragma unroll
-            for (int h = 0; h < kHist; ++h)
-              if (h < U) tp[(7 + h) * a.n_rays] = hist[h];
-          }
-        }
+                                  hnx, hny, hnz, active ? tp : nullptr, sched, unused);
       } else {
         t = __builtin_nan("");  // unreachable: the host sets geometry_mask
       }
@@ -1295,9 +1273,9 @@ __global__ __launch_bounds__(kBlock) void geom_kernel(const KArgs a, const GArgs
     } else {
       if constexpr (KM != 0) {
         bool hn, bad = false;
-        double hnx, hny, hnz, hist[kHist];
+        double hnx, hny, hnz;
         t = newton_distance<KM>(a, s, g.surface, r, active, 0, true, range_bits, hn, hnx, hny,
-                                hnz, hist, a.sched, bad);
+                                hnz, nullptr, a.sched, bad);
       } else {
         t = __builtin_nan("");
       }
