@@ -1169,18 +1169,30 @@ ORT_INLINE void zernike_coef_adjoint(double x, double y, double Rn, PZ Tm, int t
   div2(-(yn), xn, rho2e, qy, qx);
   const double dphi_dx = qy * inv_rn;
   const double dphi_dy = qx * inv_rn;
+  // cos / sin(am phi), rho^am, rho^(am - 1) of the previous term: the recurrence resumes
+  // from there when |m| does not decrease (Z(n, +-m) pairs share it), else restarts --
+  // the same products in the same order as a restart from am = 0 (the values are equal)
+  int prev_am = 0;
+  double cm = 1.0, sm = 0.0, pm = 1.0, pm1 = 1.0;
   for (int j = 0; j < nt; ++j) {
     const ort_zernike_term t = Tm[t0 + j];
     const int am = t.m >= 0 ? t.m : -t.m;
-    double cm = 1.0, sm = 0.0, pm = 1.0, pm1 = 1.0;
+    if (am < prev_am) {
+      cm = 1.0;
+      sm = 0.0;
+      pm = 1.0;
+      pm1 = 1.0;
+      prev_am = 0;
+    }
 #pragma unroll 1
-    for (int qq = 0; qq < am; ++qq) {
+    for (int qq = prev_am; qq < am; ++qq) {
       const double cn = cm * c1 - sm * s1;
       sm = sm * c1 + cm * s1;
       cm = cn;
       pm1 = pm;
       pm = pm * rho;
     }
+    prev_am = am;
     const PD a = coef + t.rad_off;
     double P = a[0];
 #pragma unroll 1
