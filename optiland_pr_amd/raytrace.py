@@ -163,6 +163,8 @@ class DeviceLens:
         self._async_plans: dict = {}  # (keys, rounds) -> the rounds' launch arguments
         self._patch_index: dict = {}  # device-coefficient layout -> term-row indices
         self.pending: list = []        # device-verified launches whose flags are unread
+        if table.device_coeffs:  # coefficients held in HBM: into the table and its blocks
+            self.patch_coefficients(table.device_coeffs)
 
     def resident(self, slot, arr):
         """A read-only HBM copy of a small host array, reused while its bytes are
@@ -310,13 +312,13 @@ def lens_for(optic_or_group, wavelengths, record=False, image_record=False):
     hit = cache.get(key)
     if hit is None or hit.fingerprint != fp:
         old = hit
-        hit = DeviceLens(table)
+        hit = DeviceLens(table)  # (patches device-resident coefficients itself)
         hit.fingerprint = fp
         if old is not None and old.table.surfaces.shape == table.surfaces.shape:
             # an edited lens starts from the previous Newton schedules (verified anyway)
             hit.sched_cache = old.sched_cache
         cache[key] = hit
-    if table.device_coeffs:
+    elif table.device_coeffs:  # the cached upload: this call's coefficient values
         hit.patch_coefficients(table.device_coeffs)
     return hit
 
