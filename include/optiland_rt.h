@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define ORT_ABI_VERSION 16
+#define ORT_ABI_VERSION 17
 #define ORT_MAX_SURFACES 64
 
 /* ---- geometry kinds ----------------------------------- */
@@ -615,6 +615,11 @@ int ort_trace_sequential_vjp(const ort_lens* lens, const ort_rays* rays_in,
  * coefficients held in HBM. */
 int ort_patch_zernike(const ort_lens* lens, const double* c, const int64_t* rows, int64_t n,
                       void* stream);
+/* The same patch with the coefficients read through a device array of n pointers
+ * (c_ptrs[i] -> the value for term row rows[i]): the optimiser's separate parameter
+ * tensors are read where they live, without a concatenation launch first (ABI v17). */
+int ort_patch_zernike_ptrs(const ort_lens* lens, const double* const* c_ptrs,
+                           const int64_t* rows, int64_t n, void* stream);
 
 int ort_surface_sag_normal(const ort_lens* lens, int32_t surface, const double* x,
                            const double* y, int64_t n, double* sag, double* nx, double* ny,
@@ -640,6 +645,21 @@ int ort_newton_fixup(const ort_lens* lens, int64_t n_groups, const ort_newton_st
                      void* stream);
 /* next_stats / next_status (nullable): when *flag becomes 1 they are initialised for the
  * re-launch (launch it with ORT_OPT_NO_INIT), so a round costs two launches. */
+
+/* The last launch of `rounds` verify-and-re-trace rounds (ABI v17) on per-call buffers
+ * stats [rounds + 1][n_groups][n_surfaces], flags [rounds + 1], statuses [rounds + 1]:
+ * ort_newton_fixup's check of the last round (stats[rounds], sched; prev_flag =
+ * flags[rounds - 1], flag = flags[rounds]), then the state the next call on the same
+ * buffers starts from -- *status_out = statuses[r] of the last round r that ran (round 0,
+ * or the largest r with flags[r - 1] == 1), every statuses[r] = 0, every stats entry 0xFF
+ * bytes (conv_mask all ones, last_bad = max_updates = -1) -- and, when sched_copy is not
+ * NULL, the settled schedule copied to it (device int32 [n_groups][n_surfaces]). One
+ * single-block launch in place of the final fixup, the two initialisations and the copy
+ * of every call; the first call's buffers are initialised by the caller. */
+int ort_newton_finish(const ort_lens* lens, int64_t n_groups, ort_newton_stat* stats,
+                      int32_t rounds, int32_t conv_base, int32_t* sched, int32_t* flags,
+                      int32_t* statuses, int32_t* status_out, int32_t* sched_copy,
+                      void* stream);
 
 /* Pupil coordinates of a distribution on the device: px[k], py[k] for k < n_points
  * (distribution.py:72-408; the grid kinds bit-identical to NumPy, cos / sin correctly

@@ -126,7 +126,8 @@ EXPORTS = ("ort_abi_version", "ort_trace_sequential", "ort_trace_pupil", "ort_tr
            "ort_surface_sag_normal", "ort_surface_distance", "ort_generate_rays",
            "ort_material_nk", "ort_spot_workspace_size", "ort_spot_stats", "ort_trace_spot", "ort_spot_partials",
            "ort_rms_spot_workspace_size", "ort_rms_spot", "ort_rms_spot_vjp",
-           "ort_wavefront_workspace_size", "ort_wavefront_opd", "ort_patch_zernike")
+           "ort_wavefront_workspace_size", "ort_wavefront_opd", "ort_patch_zernike",
+           "ort_patch_zernike_ptrs", "ort_newton_finish")
 
 _lib = None
 
@@ -174,6 +175,13 @@ def load(path: str | None = None):
     lib.ort_patch_zernike.restype = C.c_int
     lib.ort_patch_zernike.argtypes = [P(ort_lens), C.c_void_p, C.c_void_p, C.c_int64,
                                       C.c_void_p]
+    lib.ort_patch_zernike_ptrs.restype = C.c_int
+    lib.ort_patch_zernike_ptrs.argtypes = [P(ort_lens), C.c_void_p, C.c_void_p, C.c_int64,
+                                           C.c_void_p]
+    lib.ort_newton_finish.restype = C.c_int
+    lib.ort_newton_finish.argtypes = [P(ort_lens), C.c_int64, C.c_void_p, C.c_int32, C.c_int32,
+                                      C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                      C.c_void_p, C.c_void_p]
     lib.ort_surface_sag_normal.restype = C.c_int
     lib.ort_surface_sag_normal.argtypes = [P(ort_lens), C.c_int32, C.c_void_p, C.c_void_p,
                                            C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p,

@@ -257,17 +257,21 @@ class CapturedStep:
 
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
+        loss = None
         with torch.cuda.stream(side):
             for _ in range(self.warmup):
-                self.eager()
+                loss = self.eager()
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         raytrace.check_all_pending()  # the warm-up's Newton flags, before the capture
         self.opt.zero_grad(set_to_none=True)
+        # the backward's seed d loss / d loss = 1 as a static tensor made before the capture
+        # (loss.backward() would fill a fresh one inside every replay: one launch per step)
+        seed = None if loss is None else torch.ones_like(loss)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             loss = self.loss_fn()
-            loss.backward()
+            loss.backward(seed)
             self.opt.step()
         self.graph, self.loss = g, loss.detach()
 

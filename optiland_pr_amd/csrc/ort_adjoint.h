@@ -50,6 +50,11 @@ struct AdjWaves {
 #define ORT_ADJ_ZACC 16
 #endif
 constexpr int kZAcc = ORT_ADJ_ZACC;
+// Block partials (AArgs.block_partials, n_slot <= kBlockSlots): a wave's slot sums are added
+// into bpart[slot][wave of the block] in LDS and the block's four waves combined in a fixed
+// order at the end of the launch -- partial[slot][block], a quarter of the columns the
+// parameter reduce reads, and no global read-modify-write per emit.
+constexpr int kBlockSlots = 128;
 
 struct DevLane {
   const AArgs& j;
@@ -58,10 +63,15 @@ struct DevLane {
   int64_t wave;
   bool active;
   double (*zacc)[kBlock];      // __shared__ [kZAcc][kBlock] (kZAcc > 0)
+  double (*bpart)[kBlock / 64];  // __shared__ [kBlockSlots][4] (used with block_partials)
 
   __device__ inline void emit(int slot, double v, bool first) {
     if (!cst(j.need)[slot]) return;  // uniform
     const double w = wave_sum(active ? v : 0.0);
+    if (j.block_partials) {  // uniform (a kernel argument)
+      if ((threadIdx.x & 63) == 0) bpart[slot][threadIdx.x >> 6] += w;
+      return;
+    }
     if ((threadIdx.x & 63) == 0) {
       double* dst = j.partial + (int64_t)slot * j.n_wave + wave;
       if (first)
@@ -107,13 +117,28 @@ template <uint32_t KM, int P, bool RES>
 __global__ __launch_bounds__(kBlock) ORT_ADJ_OCC void adj_kernel(const KArgs a, const AArgs j) {
   const int64_t rid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool active = rid < a.n_rays;
+  __shared__ double bpart_s[kBlockSlots][kBlock / 64];
+  if (j.block_partials) {  // uniform
+    for (int k = threadIdx.x; k < j.n_slot * (kBlock / 64); k += kBlock)
+      bpart_s[k / (kBlock / 64)][k % (kBlock / 64)] = 0.0;
+    __syncthreads();
+  }
   if constexpr (kZAcc > 0 && (KM & ort::KM_ZERN) != 0) {
     __shared__ double zacc[kZAcc > 0 ? kZAcc : 1][kBlock];
-    DevLane ln{j, active ? rid : 0, a.n_rays, rid >> 6, active, zacc};
+    DevLane ln{j, active ? rid : 0, a.n_rays, rid >> 6, active, zacc, bpart_s};
     adj_ray<KM, P, RES>(a, j, ln, rid, active);
   } else {
-    DevLane ln{j, active ? rid : 0, a.n_rays, rid >> 6, active, nullptr};
+    DevLane ln{j, active ? rid : 0, a.n_rays, rid >> 6, active, nullptr, bpart_s};
     adj_ray<KM, P, RES>(a, j, ln, rid, active);
+  }
+  if (j.block_partials) {  // the block's waves combined in index order
+    __syncthreads();
+    for (int slot = threadIdx.x; slot < j.n_slot; slot += kBlock) {
+      if (!cst(j.need)[slot]) continue;
+      double v = bpart_s[slot][0];
+      for (int w = 1; w < kBlock / 64; ++w) v += bpart_s[slot][w];
+      j.partial[(int64_t)slot * j.n_wave + blockIdx.x] = v;
+    }
   }
 }
 

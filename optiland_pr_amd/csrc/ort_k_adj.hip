@@ -115,7 +115,59 @@ __global__ __launch_bounds__(kBlock) void newton_fixup_kernel(
   }
 }
 
+// The last launch of the device-verified rounds (ort_newton_finish): the final fixup's
+// check, then the per-call state reset for the next call on the same buffers -- the
+// status of the last round that ran into *status_out, every round's status word zeroed and
+// statistics set to 0xFF bytes, the settled schedule copied out -- in place of two fills
+// and a copy per call.
+__global__ __launch_bounds__(kBlock) void newton_finish_kernel(
+    const ort_surface* surf, int32_t n_surf, int64_t n_groups, ort_newton_stat* stats,
+    int32_t rounds, int32_t conv_base, int32_t* sched, int32_t* flags, int32_t* statuses,
+    int32_t* status_out, int32_t* sched_copy) {
+  __shared__ int32_t codes[kBlock / 64];
+  const int64_t ngs = n_groups * n_surf;
+  const int32_t prev = flags[rounds - 1];
+  if (prev == 1) {  // the last round ran: check its statistics (block-uniform branch)
+    const int c = newton_decide(surf, n_surf, n_groups, stats + (int64_t)rounds * ngs,
+                                conv_base, sched, codes);
+    if (threadIdx.x == 0) flags[rounds] = c;
+  } else if (threadIdx.x == 0) {
+    flags[rounds] = prev;  // settled (0) or undecidable (2) stays so
+  }
+  int32_t st = 0;
+  if (threadIdx.x == 0) {
+    int last = 0;  // round 0 always runs; round r ran when flags[r - 1] == 1
+    for (int r = 1; r <= rounds; ++r)
+      if (flags[r - 1] == 1) last = r;
+    st = statuses[last];
+  }
+  __syncthreads();  // every read of stats / statuses / sched is done
+  if (threadIdx.x == 0) *status_out = st;
+  for (int r = threadIdx.x; r <= rounds; r += kBlock) statuses[r] = 0;
+  const int64_t words = (int64_t)(rounds + 1) * ngs * (int64_t)(sizeof(ort_newton_stat) / 8);
+  uint64_t* w = reinterpret_cast<uint64_t*>(stats);
+  for (int64_t k = threadIdx.x; k < words; k += kBlock) w[k] = ~0ull;
+  if (sched_copy)
+    for (int64_t k = threadIdx.x; k < ngs; k += kBlock) sched_copy[k] = sched[k];
+}
+
 }  // namespace ortk
+
+extern "C" int ort_newton_finish(const ort_lens* lens, int64_t n_groups, ort_newton_stat* stats,
+                                 int32_t rounds, int32_t conv_base, int32_t* sched,
+                                 int32_t* flags, int32_t* statuses, int32_t* status_out,
+                                 int32_t* sched_copy, void* stream) {
+  using namespace ortk;
+  if (!lens || !stats || !sched || !flags || !statuses || !status_out || n_groups < 1 ||
+      rounds < 1 || conv_base < 0)
+    return ORT_ERR_ARG;
+  if (lens->n_surfaces < 1 || lens->n_surfaces > ORT_MAX_SURFACES || !lens->surfaces)
+    return ORT_ERR_ARG;
+  hipLaunchKernelGGL(newton_finish_kernel, dim3(1), dim3(kBlock), 0, (hipStream_t)stream,
+                     lens->surfaces, lens->n_surfaces, n_groups, stats, rounds, conv_base, sched,
+                     flags, statuses, status_out, sched_copy);
+  return hipGetLastError() == hipSuccess ? ORT_OK : ORT_ERR_LAUNCH;
+}
 
 extern "C" int ort_newton_fixup(const ort_lens* lens, int64_t n_groups,
                                 const ort_newton_stat* stats, int32_t conv_base,
@@ -147,6 +199,7 @@ constexpr int kPatchTerms = 1024;
 __global__ __launch_bounds__(kBlock) void patch_zernike_kernel(const ort_surface* surf,
                                                                ort_zernike_term* zern,
                                                                double* coef, const double* c,
+                                                               const double* const* cp,
                                                                const int64_t* rows, int64_t n) {
   __shared__ double cs[kPatchTerms];
   const ort_surface s = surf[blockIdx.x];
@@ -157,8 +210,9 @@ __global__ __launch_bounds__(kBlock) void patch_zernike_kernel(const ort_surface
   for (int64_t i = threadIdx.x; i < n; i += kBlock) {
     const int64_t r = rows[i];
     if (r < t0 || r >= t0 + nt) continue;  // another surface's term
-    zern[r].c = c[i];
-    if (r - t0 < kPatchTerms) cs[r - t0] = c[i];
+    const double v = cp ? *cp[i] : c[i];  // ort_patch_zernike_ptrs: through the pointers
+    zern[r].c = v;
+    if (r - t0 < kPatchTerms) cs[r - t0] = v;
   }
   __syncthreads();
   if (s.zm_deg < 0 || nt > kPatchTerms) return;
@@ -185,6 +239,20 @@ extern "C" int ort_patch_zernike(const ort_lens* lens, const double* c, const in
   hipLaunchKernelGGL(patch_zernike_kernel, dim3((unsigned)lens->n_surfaces), dim3(kBlock), 0,
                      (hipStream_t)stream, lens->surfaces,
                      const_cast<ort_zernike_term*>(lens->zern), const_cast<double*>(lens->coef),
-                     c, rows, n);
+                     c, nullptr, rows, n);
+  return hipGetLastError() == hipSuccess ? ORT_OK : ORT_ERR_LAUNCH;
+}
+
+extern "C" int ort_patch_zernike_ptrs(const ort_lens* lens, const double* const* c_ptrs,
+                                      const int64_t* rows, int64_t n, void* stream) {
+  using namespace ortk;
+  if (!lens || n < 0 || (n > 0 && (!c_ptrs || !rows))) return ORT_ERR_ARG;
+  if (lens->n_surfaces < 1 || lens->n_surfaces > ORT_MAX_SURFACES || !lens->surfaces ||
+      !lens->zern || !lens->coef)
+    return ORT_ERR_ARG;
+  hipLaunchKernelGGL(patch_zernike_kernel, dim3((unsigned)lens->n_surfaces), dim3(kBlock), 0,
+                     (hipStream_t)stream, lens->surfaces,
+                     const_cast<ort_zernike_term*>(lens->zern), const_cast<double*>(lens->coef),
+                     nullptr, c_ptrs, rows, n);
   return hipGetLastError() == hipSuccess ? ORT_OK : ORT_ERR_LAUNCH;
 }

@@ -313,7 +313,8 @@ struct AArgs {
   int32_t n_zern;
   int32_t n_slot;           // 3 n_surf + n_zern + 1
   int32_t n_surf;
-  int64_t n_wave;           // waves of the main launch
+  int64_t n_wave;           // partial columns: waves of the main launch, or its blocks
+                            // (block_partials)
   ort_rays cot;             // cotangents of the outputs (NULL field: zero)
   // cotangents of the per-surface record buffer [n_rec][8][n_rays] (NULL: zero) and the
   // primal's record buffer (its intensity rows weight the absorption adjoint)
@@ -330,6 +331,8 @@ struct AArgs {
   ort_rays primal;          // the final ray state read from its outputs (L, M, N, i)
   double* grad;             // [n_param], accumulated (grad_store: overwritten)
   int32_t grad_store;
+  int32_t block_partials;   // GPU: the waves of a block combined in LDS, partial
+                            // [n_slot][blocks] (n_slot <= kBlockSlots)
 };
 
 // d(slot) / d(parameter p)

@@ -66,6 +66,7 @@ class HostLens:
         self.newton = table.newton_surfaces
         self.last_schedule = None
         self.last_schedule_dev = None
+        self.last_schedule_private = False
         self._resident: dict = {}
 
     def resident(self, slot, arr):

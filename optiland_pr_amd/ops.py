@@ -221,7 +221,8 @@ def trace_sequential(lens: int, rays: list[torch.Tensor], w: torch.Tensor | None
                per_ray_w=bool(per_ray_w))
     sched = dl.last_schedule
     if dl.last_schedule_dev is not None:  # device-verified: the settled device schedule
-        sched_t = dl.last_schedule_dev.clone()
+        sched_t = (dl.last_schedule_dev if dl.last_schedule_private  # a per-call copy
+                   else dl.last_schedule_dev.clone())
     elif sched is None:
         sched_t = torch.empty(0, dtype=torch.int32, device=dev)
     else:
@@ -411,7 +412,8 @@ def trace_pupil(plan: int, px: torch.Tensor, py: torch.Tensor, params: list[torc
            pupil_per_ray=p.pupil_per_ray, newton_mode=p.newton_mode, tape=p.tape)
     sched = dl.last_schedule
     if dl.last_schedule_dev is not None:  # device-verified: the settled device schedule
-        sched_t = dl.last_schedule_dev.clone()
+        sched_t = (dl.last_schedule_dev if dl.last_schedule_private  # a per-call copy
+                   else dl.last_schedule_dev.clone())
     elif sched is None:
         sched_t = torch.empty(0, dtype=torch.int32, device=dl.device)
     else:

@@ -158,6 +158,7 @@ class DeviceLens:
         self._resident: dict = {}
         self.last_schedule = None      # host [n_groups][S] of the last verified launch
         self.last_schedule_dev = None  # device int32 [n_groups * S] (device-verified launches)
+        self.last_schedule_private = False  # last_schedule_dev is a per-call copy (no clone)
         self._dev_sched: dict = {}     # keys -> the device-resident schedule (device mode)
         self._async_bufs: dict = {}
         self._async_plans: dict = {}  # (keys, rounds) -> the rounds' launch arguments
@@ -186,8 +187,8 @@ class DeviceLens:
     def patch_coefficients(self, device_coeffs):
         """Write device-resident Zernike coefficients into the uploaded term table
         (ort_zernike_term.c) and re-form the surfaces' Cartesian blocks from them
-        (ort_patch_zernike: one launch, after one concatenation when several surfaces
-        hold device coefficients), ordered on the current stream, no host round trip."""
+        (ort_patch_zernike: one launch; ort_patch_zernike_ptrs when several parameter
+        tensors are read in place), ordered on the current stream, no host round trip."""
         vals = [t.detach().reshape(-1).to(device=self.device, dtype=torch.float64)
                 for _, t in device_coeffs]
         key = tuple((off, v.numel()) for (off, _), v in zip(device_coeffs, vals))
@@ -196,10 +197,26 @@ class DeviceLens:
             idx = torch.as_tensor(np.concatenate([np.arange(o, o + n) for o, n in key]),
                                   dtype=torch.int64, device=self.device)
             self._patch_index[key] = idx
-        c = vals[0].contiguous() if len(vals) == 1 else torch.cat(vals)
         lib = _native.load()
-        rc = lib.ort_patch_zernike(C.byref(self.c), _ptr(c), _ptr(idx), int(c.numel()),
-                                   _stream_handle())
+        n = int(idx.numel())
+        if len(vals) > 1 and all(v.is_contiguous() and v.data_ptr() == t.data_ptr()
+                                 for v, (_, t) in zip(vals, device_coeffs)):
+            # the parameter tensors themselves (float64, contiguous, on this device): read
+            # through a cached device table of element pointers (ort_patch_zernike_ptrs),
+            # no concatenation launch -- the optimiser updates them in place
+            pkey = (key, tuple(v.data_ptr() for v in vals))
+            ptrs = self._patch_index.get(pkey)
+            if ptrs is None:
+                ptrs = torch.as_tensor(np.concatenate(
+                    [v.data_ptr() + 8 * np.arange(v.numel(), dtype=np.int64) for v in vals]),
+                    dtype=torch.int64, device=self.device)
+                self._patch_index[pkey] = ptrs
+            rc = lib.ort_patch_zernike_ptrs(C.byref(self.c), _ptr(ptrs), _ptr(idx), n,
+                                            _stream_handle())
+            _native.check(rc, "ort_patch_zernike_ptrs")
+            return
+        c = vals[0].contiguous() if len(vals) == 1 else torch.cat(vals)
+        rc = lib.ort_patch_zernike(C.byref(self.c), _ptr(c), _ptr(idx), n, _stream_handle())
         _native.check(rc, "ort_patch_zernike")
 
     # -- Newton schedule speculate / verify ---------------------------------------------
@@ -363,16 +380,26 @@ def check_pending(dlens: DeviceLens, block=False):
         p["event"].synchronize()
         dlens.pending.pop(0)
         host = p["host"].numpy()
-        flags, status = host[:R + 1], host[R + 1:2 * R + 2]
+        flags = host[:R + 1]
         a, b = p["sched"]
         dlens.remember(p["keys"], host[a:b].reshape(len(p["keys"]), -1))
-        ran = [0] + [r for r in range(1, R + 1) if flags[r - 1] == 1]
         if flags[R] != 0:
             raise NewtonScheduleError(
                 "the Newton schedule did not settle in the device-verified rounds "
                 f"(flag {int(flags[R])}): trace again with newton_mode='reference'")
         if p["status"]:
-            _raise_status_value(int(status[ran[-1]]))
+            _raise_status_value(_last_status(host, R, p["fused"]))
+
+
+def _last_status(host, R, fused):
+    """The status word of the last launch that ran, from the rounds' small buffer: the
+    one ort_newton_finish stored (fused rounds), or statuses[r] of the last round r that
+    ran (round 0, or the largest r with flags[r - 1] == 1)."""
+    if fused:
+        return int(host[2 * R + 2])
+    flags, status = host[:R + 1], host[R + 1:2 * R + 2]
+    ran = [0] + [r for r in range(1, R + 1) if flags[r - 1] == 1]
+    return int(status[ran[-1]])
 
 
 def check_graph_flags(dlens: DeviceLens):
@@ -385,16 +412,15 @@ def check_graph_flags(dlens: DeviceLens):
         return
     R = p["rounds"]
     host = p["small"].cpu().numpy()
-    flags, status = host[:R + 1], host[R + 1:2 * R + 2]
+    flags = host[:R + 1]
     a, b = p["sched"]
     dlens.remember(p["keys"], host[a:b].reshape(len(p["keys"]), -1))
-    ran = [0] + [r for r in range(1, R + 1) if flags[r - 1] == 1]
     if flags[R] != 0:
         raise NewtonScheduleError(
             "the Newton schedule did not settle in the captured device-verified rounds "
             f"(flag {int(flags[R])}): re-capture after a trace with newton_mode='reference'")
     if p["status"]:
-        _raise_status_value(int(status[ran[-1]]))
+        _raise_status_value(_last_status(host, R, p["fused"]))
 
 
 def check_all_pending():
@@ -412,10 +438,13 @@ def _run_device(dlens: DeviceLens, launch, n_rays, group_len, keys, need_status)
     launch runs the cached schedule; device_rounds() verify-and-re-trace launches
     (ort_options.verify_*: each checks the previous launch's statistics with
     ort_newton_fixup's rule in every workgroup and re-traces only on a corrected schedule)
-    settle it, and a last ort_newton_fixup checks the final launch; the flags, statuses
-    and the settled schedule are copied to pinned host memory (one copy) and read by a
-    later check_pending. Schedules larger than ORT_VERIFY_MAX_SCHED entries take the
-    two-launch rounds (ort_newton_fixup + a run_if re-launch)."""
+    settle it, and ort_newton_finish checks the final launch, stores the status of the last
+    launch that ran, copies the settled schedule out for the backward and leaves the
+    statistics and status words initialised for the next call (so a call issues no fills
+    and no copy of its own); the flags, that status and the settled schedule are copied to
+    pinned host memory (one copy) and read by a later check_pending. Schedules larger than
+    ORT_VERIFY_MAX_SCHED entries take the two-launch rounds (ort_newton_fixup + a run_if
+    re-launch) and initialise their buffers per call."""
     lib = _native.load()
     dev = dlens.device
     S = dlens.table.n_surfaces
@@ -425,18 +454,20 @@ def _run_device(dlens: DeviceLens, launch, n_rays, group_len, keys, need_status)
     ngs = n_groups * S
     fused = ngs <= VERIFY_MAX_SCHED
     nb = ngs * _abi.NEWTON_STAT.itemsize
+    # small: flags [R + 1], statuses [R + 1], the finished status word + 1 pad, then the
+    # schedule (two slots with the fused rounds: each round reads one and publishes the
+    # other) -- one buffer, so one device-to-host copy per call reads all of it
+    base = 2 * R + 4
     bufs = dlens._async_bufs.get((kk, R))
     if bufs is None:
-        stats = torch.empty((R + 1, nb), dtype=torch.uint8, device=dev)
-        # flags [R + 1], statuses [R + 1], then the schedule (two slots with the fused
-        # rounds: each round reads one and publishes the other): one buffer, so one
-        # device-to-host copy per call reads all of it
-        small = torch.zeros(2 * R + 2 + (2 if fused else 1) * ngs, dtype=torch.int32,
-                            device=dev)
+        # statistics 0xFF bytes and statuses 0 once here; afterwards every fused call's
+        # ort_newton_finish leaves them so for the next one
+        stats = torch.full((R + 1, nb), 255, dtype=torch.uint8, device=dev)
+        small = torch.zeros(base + (2 if fused else 1) * ngs, dtype=torch.int32, device=dev)
         bufs = [stats, small, 0]  # [2]: the slot holding the current schedule
         dlens._async_bufs[(kk, R)] = bufs
     stats, small, cur = bufs
-    slots = [small[2 * R + 2 + k * ngs:2 * R + 2 + (k + 1) * ngs] for k in range(2 if fused else 1)]
+    slots = [small[base + k * ngs:base + (k + 1) * ngs] for k in range(2 if fused else 1)]
     sched_dev = slots[cur]
     prev = dlens._dev_sched.get(kk)
     if prev is None or prev.data_ptr() != sched_dev.data_ptr():
@@ -464,6 +495,7 @@ def _run_device(dlens: DeviceLens, launch, n_rays, group_len, keys, need_status)
                     opt.sched_out = slots[(cur + r) % 2].data_ptr()
                 rounds.append((None, opt, stats[r], status[r]))
             last = slots[(cur + R) % 2]
+            final = (_ptr(stats), _ptr(last), _ptr(flags), _ptr(status), _ptr(small[2 * R + 2]))
         else:
             for r in range(R + 1):
                 fix = None
@@ -476,49 +508,53 @@ def _run_device(dlens: DeviceLens, launch, n_rays, group_len, keys, need_status)
                                           None if r == 0 else flags[r - 1].data_ptr())
                 rounds.append((fix, opt, stats[r], status[r]))
             last = sched_dev
-        final = (_ptr(stats[R]), _ptr(last), _ptr(flags[R - 1]), _ptr(flags[R]))
-        plan = (rounds, final, last, (cur + R) % 2 if fused else cur,
-                small[R + 1:2 * R + 2])
+            final = (_ptr(stats[R]), _ptr(last), _ptr(flags[R - 1]), _ptr(flags[R]))
+        plan = (rounds, final, last, (cur + R) % 2 if fused else cur)
         dlens._async_plans[(kk, R, cur)] = plan
-    rounds, final, last, new_cur, statuses = plan
-    if fused:  # every round's statistics and status initialised up front (two fills)
-        stats.fill_(255)
-        statuses.zero_()
+    rounds, final, last, new_cur = plan
     for fix, opt, st, stt in rounds:
         if fix is not None:
             rc = lib.ort_newton_fixup(lens_c, n_groups, fix[0], 0, fix[1], fix[2], fix[3],
                                       fix[4], fix[5], stream)
             _native.check(rc, "ort_newton_fixup")
         launch(opt, st, stt if need_status else None)
-    rc = lib.ort_newton_fixup(lens_c, n_groups, final[0], 0, final[1], final[2], final[3],
-                              None, None, stream)
-    _native.check(rc, "ort_newton_fixup")
+    if fused:
+        # the settled schedule the backward keeps: written by the finish launch (no clone)
+        sched_copy = torch.empty(ngs, dtype=torch.int32, device=dev)
+        rc = lib.ort_newton_finish(lens_c, n_groups, final[0], R, 0, final[1], final[2],
+                                   final[3], final[4], _ptr(sched_copy), stream)
+        _native.check(rc, "ort_newton_finish")
+    else:
+        sched_copy = None
+        rc = lib.ort_newton_fixup(lens_c, n_groups, final[0], 0, final[1], final[2], final[3],
+                                  None, None, stream)
+        _native.check(rc, "ort_newton_fixup")
     bufs[2] = new_cur
     dlens._dev_sched[kk] = last
-    off = 2 * R + 2 + (new_cur * ngs if fused else 0)
+    off = base + (new_cur * ngs if fused else 0)
+    flag_rec = dict(keys=list(keys), status=need_status, rounds=R, sched=(off, off + ngs),
+                    fused=fused)
+    dlens.last_schedule = None
+    # the settled device schedule: a private copy (fused) or the live slot (ops clone it)
+    dlens.last_schedule_dev = sched_copy if fused else last
+    dlens.last_schedule_private = fused
     if torch.cuda.is_current_stream_capturing():
         # captured into a HIP graph (e.g. a whole optimisation step): no host bookkeeping
         # is replayed, so the flags stay on the device; check_graph_flags() reads them
         # after the replays (once, with one synchronisation)
-        dlens.graph_flags = dict(small=small, keys=list(keys), status=need_status, rounds=R,
-                                 sched=(off, off + ngs))
-        dlens.last_schedule = None
-        dlens.last_schedule_dev = last
+        dlens.graph_flags = dict(small=small, **flag_rec)
         return
     host = torch.empty(small.numel(), dtype=torch.int32, pin_memory=True)
     host.copy_(small, non_blocking=True)
     ev = torch.cuda.Event()
     ev.record(torch.cuda.current_stream())
-    dlens.pending.append(dict(event=ev, host=host, keys=list(keys), status=need_status,
-                              rounds=R, sched=(off, off + ngs)))
+    dlens.pending.append(dict(event=ev, host=host, **flag_rec))
     global _PENDING_LENSES
     if _PENDING_LENSES is None:
         import weakref
 
         _PENDING_LENSES = weakref.WeakSet()
     _PENDING_LENSES.add(dlens)
-    dlens.last_schedule = None
-    dlens.last_schedule_dev = last
 
 
 def _run(dlens: DeviceLens, launch, n_rays, group_len, keys, newton_mode="reference",
@@ -531,6 +567,7 @@ def _run(dlens: DeviceLens, launch, n_rays, group_len, keys, newton_mode="refere
     if dlens.pending and not torch.cuda.is_current_stream_capturing():
         check_pending(dlens)  # (a capture only records launches: no event queries in it)
     dlens.last_schedule_dev = None
+    dlens.last_schedule_private = False
     S = dlens.table.n_surfaces
     n_groups = max(1, -(-n_rays // group_len))
     need_status = with_status and dlens.table.has_range_check

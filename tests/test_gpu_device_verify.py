@@ -133,3 +133,72 @@ def test_device_mode_range_error_surfaces_at_check(torch):
     with pytest.raises(ValueError, match="Zernike coordinates must be normalized"):
         _trace(lens, "device", n=64, wl=0.587)
         raytrace.check_all_pending()
+
+
+def test_newton_finish_state_for_the_next_call(torch):
+    """ort_newton_finish (ABI v17) on hand-made round buffers: the status of the last round
+    that ran lands in status_out, every status word is zeroed, every statistics byte is
+    0xFF and the schedule is copied out -- the state the next call's rounds start from."""
+    import ctypes as C
+
+    from optiland_pr_amd import _native
+    from optiland_pr_amd.raytrace import _ptr, _stream_handle
+    from tests._cases import build_lens
+
+    lens = build_lens("rt_asph")
+    _trace(lens, "reference")
+    dl = _dlens(lens, 0.5876)
+    S = dl.table.n_surfaces
+    R, n_groups = 3, 2
+    nb = n_groups * S * 24
+    stats = torch.randint(0, 255, (R + 1, nb), dtype=torch.uint8, device="cuda")
+    # round 1 ran (flags[0] == 1), round 2 did not (flags[1] == 0): the last status is [1]
+    flags = torch.tensor([1, 0, 0, 9], dtype=torch.int32, device="cuda")
+    statuses = torch.tensor([4, 1, 2, 8], dtype=torch.int32, device="cuda")
+    status_out = torch.full((1,), -1, dtype=torch.int32, device="cuda")
+    sched = torch.arange(n_groups * S, dtype=torch.int32, device="cuda")
+    copy = torch.full((n_groups * S,), -7, dtype=torch.int32, device="cuda")
+    rc = _native.load().ort_newton_finish(C.byref(dl.c), n_groups, _ptr(stats), R, 0,
+                                          _ptr(sched), _ptr(flags), _ptr(statuses),
+                                          _ptr(status_out), _ptr(copy), _stream_handle())
+    _native.check(rc, "ort_newton_finish")
+    torch.cuda.synchronize()
+    assert int(status_out) == 1
+    assert flags.tolist() == [1, 0, 0, 0]  # flags[R] = flags[R - 1]: nothing ran to check
+    assert statuses.tolist() == [0, 0, 0, 0]
+    assert bool((stats == 255).all())
+    assert torch.equal(copy, sched)
+
+
+def test_device_rounds_reuse_their_buffers(torch):
+    """Consecutive device-verified calls on the same round buffers (ort_newton_finish leaves
+    them initialised for the next call, no per-call fills): three wrong warm schedules in a
+    row, each settled to the reference's, each call's rays equal to the host-verified
+    trace, and the settled schedule the backward keeps is each call's own copy."""
+    from optiland_pr_amd import raytrace
+    from tests._cases import build_lens
+
+    ref_lens, lens = build_lens("rt_asph"), build_lens("rt_asph")
+    ref = _trace(ref_lens, "reference")
+    _trace(lens, "reference")
+    dl = _dlens(lens, 0.5876)
+    good = {k: v.copy() for k, v in dl.sched_cache.items() if k != "_default"}
+    copies = []
+    for offset in (+5, -1, +2, 0):
+        for k, v in good.items():
+            bad = v.copy()
+            for s in dl.newton:
+                bad[s] = max(0, int(v[s]) + offset)
+            dl.sched_cache[k] = bad
+        dl._dev_sched.clear()
+        got = _trace(lens, "device")
+        assert dl.last_schedule_private
+        copies.append(dl.last_schedule_dev)
+        raytrace.check_all_pending()
+        for a in ref:
+            np.testing.assert_array_equal(got[a], ref[a], err_msg=f"{a} offset {offset}")
+        for k, v in good.items():
+            assert np.array_equal(dl.sched_cache[k], v), (offset, k, dl.sched_cache[k], v)
+    assert len({c.data_ptr() for c in copies}) == len(copies)  # one live copy per call
+    for c in copies:
+        assert torch.equal(c, copies[0])
