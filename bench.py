@@ -410,9 +410,9 @@ def config5(args, dev, rank, world, torch):
         tape_bytes_per_launch=lambda: _tape_read_bytes(lens, R),
         # the adjoint launch's algorithmic HBM bytes: the tape read, the pupil samples
         # (16 B/ray), the primal outputs it reads (L, M, N, i: 32 B/ray), the cotangents
-        # (x, y: 16 B/ray) and the wave partials written (30 Zernike slots + 1 per 64 rays)
+        # (x, y: 16 B/ray) and the block partials written (30 Zernike slots + 1 per 256 rays)
         algorithmic_bytes_per_launch=lambda: (_tape_read_bytes(lens, R) + (16 + 32 + 16) * R
-                                              + 31 * 8 * (R // 64)))
+                                              + 31 * 8 * (R // 256)))
 
 
 def _tape_read_bytes(lens, R):

@@ -524,7 +524,10 @@ int ort_trace_pupil(const ort_lens* lens, const double* px, const double* py,
  *   distance differentiated through its implicit equation; equals the unrolled
  *   derivative to the Newton residual when the Newton slope is the sag's derivative --
  *   not for standard / noll Zernike normals, which omit the normalisation constant).
- *   Needs n_zern and a device workspace of ort_vjp_workspace_size() bytes. */
+ *   Needs n_zern and a device workspace of ort_vjp_workspace_size() bytes, and at most
+ *   ORT_VJP_ADJOINT_MAX_SLOTS parameter slots, 3 n_surfaces + n_zern + 1 (v17: the
+ *   slots' per-block partial sums live in LDS); beyond that use ORT_VJP_UNROLLED. */
+#define ORT_VJP_ADJOINT_MAX_SLOTS 512
 enum ort_vjp_mode { ORT_VJP_UNROLLED = 0, ORT_VJP_ADJOINT = 1 };
 typedef struct ort_vjp_params {
   int32_t n_param;

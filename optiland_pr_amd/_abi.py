@@ -211,3 +211,5 @@ OPT_EXACT = 2  # ort_options.flags: ORT_OPT_EXACT (no deferred-check pass)
 CONV_WINDOW = 128  # stop indices per conv_mask window (ort_options.conv_base)
 
 RAY_FIELDS = ("x", "y", "z", "L", "M", "N", "i", "opd")
+
+VJP_ADJOINT_MAX_SLOTS = 512  # ORT_VJP_ADJOINT_MAX_SLOTS: 3 S + n_zern + 1 at most

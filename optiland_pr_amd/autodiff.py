@@ -114,11 +114,14 @@ def vjp_mode(table):
     not its sag's derivative -- the standard / noll normal omits the normalisation
     constant (zernike.py:163-231), so the unrolled iteration's derivative only converges
     linearly to the implicit one there and the forward-mode ORT_VJP_UNROLLED keeps the
-    reference's semantics. ORT_VJP_MODE=unrolled|adjoint overrides (A/B checks)."""
+    reference's semantics -- or the lens has more parameter slots than the adjoint holds
+    (ORT_VJP_ADJOINT_MAX_SLOTS). ORT_VJP_MODE=unrolled|adjoint overrides (A/B checks)."""
     env = os.environ.get("ORT_VJP_MODE", "").lower()
     if env in ("unrolled", "adjoint"):
         return _abi.VJP_UNROLLED if env == "unrolled" else _abi.VJP_ADJOINT
     z = table.zern
+    if 3 * table.n_surfaces + len(z) + 1 > _abi.VJP_ADJOINT_MAX_SLOTS:
+        return _abi.VJP_UNROLLED  # more parameter slots than the adjoint's LDS partials hold
     live = z["c"] != 0.0
     for off, t in getattr(table, "device_coeffs", ()):  # values not on the host
         live[off:off + int(t.numel())] = True

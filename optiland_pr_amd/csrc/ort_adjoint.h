@@ -50,11 +50,13 @@ struct AdjWaves {
 #define ORT_ADJ_ZACC 16
 #endif
 constexpr int kZAcc = ORT_ADJ_ZACC;
-// Block partials (AArgs.block_partials, n_slot <= kBlockSlots): a wave's slot sums are added
-// into bpart[slot][wave of the block] in LDS and the block's four waves combined in a fixed
-// order at the end of the launch -- partial[slot][block], a quarter of the columns the
-// parameter reduce reads, and no global read-modify-write per emit.
-constexpr int kBlockSlots = 128;
+// Block partials: a wave's slot sums are added into bpart[slot][wave of the block] in LDS and
+// the block's four waves combined in a fixed order at the end of the launch --
+// partial[slot][block], a quarter of the columns the parameter reduce reads, no global
+// read-modify-write per emit, and fewer registers than a per-wave global store path (the
+// TMA adjoint's scratch 24 -> 20 B). n_slot <= kBlockSlots (16 KB of LDS per block); the
+// host takes the forward-mode VJP above that (autodiff.vjp_mode).
+constexpr int kBlockSlots = ORT_VJP_ADJOINT_MAX_SLOTS;
 
 struct DevLane {
   const AArgs& j;
@@ -63,22 +65,13 @@ struct DevLane {
   int64_t wave;
   bool active;
   double (*zacc)[kBlock];      // __shared__ [kZAcc][kBlock] (kZAcc > 0)
-  double (*bpart)[kBlock / 64];  // __shared__ [kBlockSlots][4] (used with block_partials)
+  double (*bpart)[kBlock / 64];  // __shared__ [kBlockSlots][4], zeroed at the kernel start
 
   __device__ inline void emit(int slot, double v, bool first) {
     if (!cst(j.need)[slot]) return;  // uniform
     const double w = wave_sum(active ? v : 0.0);
-    if (j.block_partials) {  // uniform (a kernel argument)
-      if ((threadIdx.x & 63) == 0) bpart[slot][threadIdx.x >> 6] += w;
-      return;
-    }
-    if ((threadIdx.x & 63) == 0) {
-      double* dst = j.partial + (int64_t)slot * j.n_wave + wave;
-      if (first)
-        *dst = w;
-      else
-        *dst += w;
-    }
+    (void)first;  // the LDS entries start at zero: 0 + w == w
+    if ((threadIdx.x & 63) == 0) bpart[slot][threadIdx.x >> 6] += w;
   }
   __device__ inline double* tape(int si) const {
     return j.tape + (int64_t)si * kTapeRows * n_rays + r_ld;
@@ -118,11 +111,9 @@ __global__ __launch_bounds__(kBlock) ORT_ADJ_OCC void adj_kernel(const KArgs a, 
   const int64_t rid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool active = rid < a.n_rays;
   __shared__ double bpart_s[kBlockSlots][kBlock / 64];
-  if (j.block_partials) {  // uniform
-    for (int k = threadIdx.x; k < j.n_slot * (kBlock / 64); k += kBlock)
-      bpart_s[k / (kBlock / 64)][k % (kBlock / 64)] = 0.0;
-    __syncthreads();
-  }
+  for (int k = threadIdx.x; k < j.n_slot * (kBlock / 64); k += kBlock)
+    bpart_s[k / (kBlock / 64)][k % (kBlock / 64)] = 0.0;
+  __syncthreads();
   if constexpr (kZAcc > 0 && (KM & ort::KM_ZERN) != 0) {
     __shared__ double zacc[kZAcc > 0 ? kZAcc : 1][kBlock];
     DevLane ln{j, active ? rid : 0, a.n_rays, rid >> 6, active, zacc, bpart_s};
@@ -131,14 +122,12 @@ __global__ __launch_bounds__(kBlock) ORT_ADJ_OCC void adj_kernel(const KArgs a, 
     DevLane ln{j, active ? rid : 0, a.n_rays, rid >> 6, active, nullptr, bpart_s};
     adj_ray<KM, P, RES>(a, j, ln, rid, active);
   }
-  if (j.block_partials) {  // the block's waves combined in index order
-    __syncthreads();
-    for (int slot = threadIdx.x; slot < j.n_slot; slot += kBlock) {
-      if (!cst(j.need)[slot]) continue;
-      double v = bpart_s[slot][0];
-      for (int w = 1; w < kBlock / 64; ++w) v += bpart_s[slot][w];
-      j.partial[(int64_t)slot * j.n_wave + blockIdx.x] = v;
-    }
+  __syncthreads();  // the block's waves combined in index order
+  for (int slot = threadIdx.x; slot < j.n_slot; slot += kBlock) {
+    if (!cst(j.need)[slot]) continue;
+    double v = bpart_s[slot][0];
+    for (int w = 1; w < kBlock / 64; ++w) v += bpart_s[slot][w];
+    j.partial[(int64_t)slot * j.n_wave + blockIdx.x] = v;
   }
 }
 

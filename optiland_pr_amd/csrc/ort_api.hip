@@ -166,17 +166,6 @@ extern "C" {
 // ORT_VJP_ADJOINT workspace: tape [S][kTapeRows][n_rays], partial [n_slot][n_wave],
 // slot_sum [n_slot], need [n_slot] (each 256-byte aligned).
 // ORT_VJP_UNROLLED workspace: the block partials [n_block][4] of one tangent chunk.
-// the adjoint's block partials (ort_adjoint.h kBlockSlots); ORT_ADJ_WAVE_PARTIALS (A/B
-// builds) keeps one partial column per wave
-static bool block_partials(int32_t n_slot) {
-#ifdef ORT_ADJ_WAVE_PARTIALS
-  (void)n_slot;
-  return false;
-#else
-  return n_slot <= kBlockSlots;
-#endif
-}
-
 struct AdjLayout {
   int32_t n_slot;
   int64_t n_wave, tape, partial, slot_sum, need, total;
@@ -196,8 +185,9 @@ static bool adj_layout(const ort_lens* lens, const ort_batch* batch,
     return true;
   }
   L.n_slot = (int32_t)(3 * S + params->n_zern + 1);
-  // partial columns: one per block when the block's waves combine in LDS, else per wave
-  L.n_wave = (n + kBlock - 1) / kBlock * (block_partials(L.n_slot) ? 1 : kBlock / 64);
+  // partial columns: one per block (its waves combined in LDS, ort_adjoint.h)
+  if (L.n_slot > kBlockSlots) return false;  // the forward-mode VJP serves such lenses
+  L.n_wave = (n + kBlock - 1) / kBlock;
   L.tape = 0;
   // a tape the primal wrote (params->tape) lives outside the workspace
   const int64_t tape_bytes = params->tape ? 0 : S * kTapeRows * n * (int64_t)sizeof(double);
@@ -279,7 +269,6 @@ static int vjp_run(const ort_lens* lens, const double* px, const double* py,
     aj.n_slot = L.n_slot;
     aj.n_surf = lens->n_surfaces;
     aj.n_wave = L.n_wave;
-    aj.block_partials = block_partials(L.n_slot);
     aj.cot = *cotangent;
     aj.rec_cot = rec_cotangent;
     aj.rec = rec;

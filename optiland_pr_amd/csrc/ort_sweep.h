@@ -305,6 +305,15 @@ ORT_INLINE void globalize(const KArgs& a, const ort_surface& s, ort::RayT<T>& r)
 // propagation distance) goes to lane.emit(slot, v, first); the per-parameter gradient is
 // the sum over rays of its slots weighted by the tangent tables (slot_weight).
 // =====================================================================================
+// The adjoint's tape rows are read once: ORT_NT_LOAD (A/B builds) reads them non-temporal
+// on the device -- measured no gain (config 5 adjoint 428 / 428 vs 436 / 430 us, A/B on the
+// MI355X), so plain loads are the default.
+#if defined(__HIP_DEVICE_COMPILE__) && defined(ORT_NT_LOAD)
+#define ORT_TAPE_LD(x) __builtin_nontemporal_load(&(x))
+#else
+#define ORT_TAPE_LD(x) (x)
+#endif
+
 struct AArgs {
   const int32_t* zparam;    // [n_zern] parameter per Zernike term (< 0: constant)
   const double* tan_surf;   // [n_param][n_surf][3]: d radius, d conic, d vertex z
@@ -313,8 +322,7 @@ struct AArgs {
   int32_t n_zern;
   int32_t n_slot;           // 3 n_surf + n_zern + 1
   int32_t n_surf;
-  int64_t n_wave;           // partial columns: waves of the main launch, or its blocks
-                            // (block_partials)
+  int64_t n_wave;           // partial columns (GPU: one per block of the main launch)
   ort_rays cot;             // cotangents of the outputs (NULL field: zero)
   // cotangents of the per-surface record buffer [n_rec][8][n_rays] (NULL: zero) and the
   // primal's record buffer (its intensity rows weight the absorption adjoint)
@@ -331,8 +339,6 @@ struct AArgs {
   ort_rays primal;          // the final ray state read from its outputs (L, M, N, i)
   double* grad;             // [n_param], accumulated (grad_store: overwritten)
   int32_t grad_store;
-  int32_t block_partials;   // GPU: the waves of a block combined in LDS, partial
-                            // [n_slot][blocks] (n_slot <= kBlockSlots)
 };
 
 // d(slot) / d(parameter p)
@@ -643,16 +649,16 @@ ORT_INLINE void adj_ray(const KArgs& a, const AArgs& j, Lane& ln, int64_t rid, b
     }
     const double* tp = ln.tape(si);
     ort::Ray q;
-    q.x = tp[0];
-    q.y = tp[TS];
-    q.z = tp[2 * TS];
-    q.L = tp[3 * TS];
-    q.M = tp[4 * TS];
-    q.N = tp[5 * TS];
+    q.x = ORT_TAPE_LD(tp[0]);
+    q.y = ORT_TAPE_LD(tp[TS]);
+    q.z = ORT_TAPE_LD(tp[2 * TS]);
+    q.L = ORT_TAPE_LD(tp[3 * TS]);
+    q.M = ORT_TAPE_LD(tp[4 * TS]);
+    q.N = ORT_TAPE_LD(tp[5 * TS]);
     q.i = 1.0;
     q.opd = 0.0;
     q.att = 0.0;
-    const double t = tp[6 * TS];
+    const double t = ORT_TAPE_LD(tp[6 * TS]);
     localize(a, s, q);
     const double x1 = q.x + t * q.L;
     const double y1 = q.y + t * q.M;
@@ -738,7 +744,7 @@ ORT_INLINE void adj_ray(const KArgs& a, const AArgs& j, Lane& ln, int64_t rid, b
       double tb = bt;
       for (int m = 0; m < m_end; ++m) {
         const bool on = m < Uk;
-        const double tk = tp[(7 + m) * TS];
+        const double tk = ORT_TAPE_LD(tp[(7 + m) * TS]);
         const double xk = q.x + tk * q.L, yk = q.y + tk * q.M, zk = q.z + tk * q.N;
         D kx, ky, kz;
         const D sk = sagnorm(s, xk, yk, kx, ky, kz);
@@ -779,7 +785,7 @@ ORT_INLINE void adj_ray(const KArgs& a, const AArgs& j, Lane& ln, int64_t rid, b
       // initial guess: the base conic's closed form (newton_raphson.py:131-135). More than
       // kHist updates: the earlier ones are dropped -- their share is scaled by the
       // products of f f'' / f'^2 over the kept updates, i.e. by converged residuals
-      const double t0 = U == 0 ? t : tp[(int64_t)(7 + (U <= kHist ? U - 1 : 0)) * TS];
+      const double t0 = U == 0 ? t : ORT_TAPE_LD(tp[(int64_t)(7 + (U <= kHist ? U - 1 : 0)) * TS]);
       closed_adj(s, q, t0, U <= kHist ? tb : 0.0, b, bR, bk);
     }
 

@@ -2,7 +2,7 @@
 the closed-form kernel's, ort_k_closed.hip): compile that TU with extra -D flags and link
 it with the main build's other objects. Measurement tooling (tools/ab.sh), not product.
 
-usage: python tools/build_variant.py NAME [--tu ort_k_trace.hip] [-DFLAG ...]
+usage: python tools/build_variant.py NAME [--tu ort_k_trace.hip[,ort_k_closed.hip,...]] [-DFLAG ...]
        -> optiland_pr_amd/lib/variants/NAME.so
 """
 import glob
@@ -22,11 +22,16 @@ build.build()  # the main objects must be current
 obj_main = os.path.join(build.LIB_DIR, "obj")
 vdir = os.path.join(build.LIB_DIR, "variants")
 os.makedirs(vdir, exist_ok=True)
-tu = os.path.join(build.CSRC, tu_name)
-obj = os.path.join(vdir, f"obj_{name}_{tu_name.split('.')[0]}.o")
-subprocess.run([build.hipcc(), *build.HIPCC_FLAGS, *flags, "-I", os.path.join(REPO, "include"),
-                "-c", "-o", obj, tu], check=True)
-objs = [o for o in glob.glob(os.path.join(obj_main, "*.o")) if os.path.basename(o) != tu_name + ".o"] + [obj]
+tus = tu_name.split(",")
+new = []
+for t in tus:  # each swapped TU compiled with the extra flags
+    obj = os.path.join(vdir, f"obj_{name}_{t.split('.')[0]}.o")
+    subprocess.run([build.hipcc(), *build.HIPCC_FLAGS, *flags, "-I",
+                    os.path.join(REPO, "include"), "-c", "-o", obj,
+                    os.path.join(build.CSRC, t)], check=True)
+    new.append(obj)
+objs = [o for o in glob.glob(os.path.join(obj_main, "*.o"))
+        if os.path.basename(o) not in {t + ".o" for t in tus}] + new
 out = os.path.join(vdir, name + ".so")
 subprocess.run([build.hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out, *objs],
                check=True)
