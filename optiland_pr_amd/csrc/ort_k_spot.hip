@@ -30,6 +30,13 @@ namespace {
 constexpr int kSpotThreads = kRedThreads;
 constexpr int64_t kSpotMaxChunks = 256;  // chunks per pair at most: a chunk is 256 rays
                                          // times ceil(n_pupil / (256 * 256)) per thread
+// ort_rms_spot (one pair, 1M points in config 5): more, shorter chunks -- 256 blocks of 16
+// points per thread leave the two passes latency-bound; every pass-2 block re-reduces the
+// pass-1 rows (24 B per chunk), so the count stays moderate. ORT_RMS_CHUNKS: A/B builds.
+#ifndef ORT_RMS_CHUNKS
+#define ORT_RMS_CHUNKS 1024
+#endif
+constexpr int64_t kRmsMaxChunks = ORT_RMS_CHUNKS;
 
 struct SpotArgs {
   const double* x;
@@ -320,26 +327,32 @@ using namespace ortk;
 
 extern "C" {
 
-static int64_t spot_per_thread(const ort_spot_layout* lay) {
-  const int64_t cap = kSpotMaxChunks * kSpotThreads;
+// max_chunks: chunks per pair at most (kSpotMaxChunks for the spot diagram's statistics,
+// kRmsMaxChunks for ort_rms_spot's one pair of up to millions of points)
+static int64_t spot_per_thread(const ort_spot_layout* lay, int64_t max_chunks = kSpotMaxChunks) {
+  const int64_t cap = max_chunks * kSpotThreads;
   return lay->n_pupil > cap ? (lay->n_pupil + cap - 1) / cap : 1;
 }
-static int64_t spot_chunks(const ort_spot_layout* lay) {
-  const int64_t chunk = spot_per_thread(lay) * kSpotThreads;
+static int64_t spot_chunks(const ort_spot_layout* lay, int64_t max_chunks = kSpotMaxChunks) {
+  const int64_t chunk = spot_per_thread(lay, max_chunks) * kSpotThreads;
   return lay->n_pupil > 0 ? (lay->n_pupil + chunk - 1) / chunk : 1;
 }
 
-int64_t ort_spot_workspace_size(const ort_spot_layout* lay) {
+static int64_t spot_workspace_size(const ort_spot_layout* lay, int64_t max_chunks) {
   if (!lay || lay->n_pupil < 0 || lay->n_fields < 0 || lay->n_wl < 1) return ORT_ERR_ARG;
   const int64_t pairs = (int64_t)lay->n_fields * lay->n_wl;
-  return pairs * spot_chunks(lay) * 3 * 2 * (int64_t)sizeof(double);
+  return pairs * spot_chunks(lay, max_chunks) * 3 * 2 * (int64_t)sizeof(double);
+}
+
+int64_t ort_spot_workspace_size(const ort_spot_layout* lay) {
+  return spot_workspace_size(lay, kSpotMaxChunks);
 }
 
 static int spot_args(const ort_rays* rays, const ort_spot_layout* lay, void* workspace,
                      int64_t workspace_size, double* out, SpotArgs& a, int64_t& pairs,
-                     int64_t& chunks) {
+                     int64_t& chunks, int64_t max_chunks = kSpotMaxChunks) {
   if (!rays || !lay || !out) return ORT_ERR_ARG;
-  const int64_t need = ort_spot_workspace_size(lay);
+  const int64_t need = spot_workspace_size(lay, max_chunks);
   if (need < 0) return (int)need;
   if (lay->ref_wl < 0 || lay->ref_wl >= lay->n_wl) return ORT_ERR_ARG;
   if (lay->n_local_ops < 0 || (lay->n_local_ops > 0 && !lay->local_ops)) return ORT_ERR_ARG;
@@ -348,8 +361,8 @@ static int spot_args(const ort_rays* rays, const ort_spot_layout* lay, void* wor
   if (!workspace || workspace_size < need) return ORT_ERR_ARG;
   if (lay->n_pupil > 0 && (!rays->x || !rays->y || !rays->i)) return ORT_ERR_ARG;
   if (lay->n_pupil > 0 && lay->n_local_ops > 0 && !rays->z) return ORT_ERR_ARG;
-  chunks = spot_chunks(lay);
-  if (spot_per_thread(lay) > 0x7fffffff || pairs > 65535) return ORT_ERR_ARG;
+  chunks = spot_chunks(lay, max_chunks);
+  if (spot_per_thread(lay, max_chunks) > 0x7fffffff || pairs > 65535) return ORT_ERR_ARG;
   a.x = rays->x;
   a.y = rays->y;
   a.z = rays->z;
@@ -360,7 +373,7 @@ static int spot_args(const ort_rays* rays, const ort_spot_layout* lay, void* wor
   a.n_ops = lay->n_local_ops;
   a.ops = lay->local_ops;
   a.n_chunks = (int32_t)chunks;
-  a.per_thread = (int32_t)spot_per_thread(lay);
+  a.per_thread = (int32_t)spot_per_thread(lay, max_chunks);
   a.part1 = (double*)workspace;
   a.part2 = a.part1 + pairs * chunks * 3;
   a.out = out;
@@ -411,7 +424,7 @@ int64_t ort_rms_spot_workspace_size(int64_t n) {
   lay.n_pupil = n;
   lay.n_fields = 1;
   lay.n_wl = 1;
-  return ort_spot_workspace_size(&lay);
+  return spot_workspace_size(&lay, kRmsMaxChunks);
 }
 
 int ort_rms_spot(const double* x, const double* y, int64_t n, void* workspace,
@@ -427,7 +440,8 @@ int ort_rms_spot(const double* x, const double* y, int64_t n, void* workspace,
   r.i = (double*)x;  // validated as present, then replaced by "no mask" below
   SpotArgs a{};
   int64_t pairs = 0, chunks = 0;
-  int rc = spot_args(&r, &lay, workspace, workspace_size, stats, a, pairs, chunks);
+  int rc = spot_args(&r, &lay, workspace, workspace_size, stats, a, pairs, chunks,
+                     kRmsMaxChunks);
   if (rc) return rc;
   a.i = nullptr;  // every point counts (the operand does not mask vignetted rays)
   a.rms_out = rms;
