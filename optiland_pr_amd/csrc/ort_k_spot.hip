@@ -316,8 +316,13 @@ __global__ __launch_bounds__(kSpotThreads) void rms_spot_vjp_kernel(
   if (i >= n) return;
   const double cx = stats[1], cy = stats[2];
   const double w = *grad_out / (stats[0] * stats[3]);
+#ifndef ORT_TEMPORAL_STORE  // written once, read by the trace's VJP launch (ORT_ST's rule)
+  __builtin_nontemporal_store((x[i] - cx) * w, &gx[i]);
+  __builtin_nontemporal_store((y[i] - cy) * w, &gy[i]);
+#else
   gx[i] = (x[i] - cx) * w;
   gy[i] = (y[i] - cy) * w;
+#endif
 }
 
 }  // namespace
