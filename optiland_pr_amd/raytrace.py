@@ -163,6 +163,7 @@ class DeviceLens:
         self._async_bufs: dict = {}
         self._async_plans: dict = {}  # (keys, rounds) -> the rounds' launch arguments
         self._patch_index: dict = {}  # device-coefficient layout -> term-row indices
+        self._patch_ptrs: dict = {}    # (layout, tensor addresses) -> element pointer table
         self.pending: list = []        # device-verified launches whose flags are unread
         if table.device_coeffs:  # coefficients held in HBM: into the table and its blocks
             self.patch_coefficients(table.device_coeffs)
@@ -199,18 +200,21 @@ class DeviceLens:
             self._patch_index[key] = idx
         lib = _native.load()
         n = int(idx.numel())
-        if len(vals) > 1 and all(v.is_contiguous() and v.data_ptr() == t.data_ptr()
-                                 for v, (_, t) in zip(vals, device_coeffs)):
+        pkey = (key, tuple(v.data_ptr() for v in vals))
+        ptrs = self._patch_ptrs.get(pkey)
+        if ptrs is None and len(vals) > 1 and len(self._patch_ptrs) < 64 and all(
+                v.is_contiguous() and v.data_ptr() == t.data_ptr()
+                for v, (_, t) in zip(vals, device_coeffs)):
             # the parameter tensors themselves (float64, contiguous, on this device): read
-            # through a cached device table of element pointers (ort_patch_zernike_ptrs),
-            # no concatenation launch -- the optimiser updates them in place
-            pkey = (key, tuple(v.data_ptr() for v in vals))
-            ptrs = self._patch_index.get(pkey)
-            if ptrs is None:
-                ptrs = torch.as_tensor(np.concatenate(
-                    [v.data_ptr() + 8 * np.arange(v.numel(), dtype=np.int64) for v in vals]),
-                    dtype=torch.int64, device=self.device)
-                self._patch_index[pkey] = ptrs
+            # through a device table of element pointers (ort_patch_zernike_ptrs), no
+            # concatenation launch -- the optimiser updates them in place. Tables are never
+            # freed (a captured graph may hold one); past 64 tensor sets (new tensors every
+            # call) the concatenation path below serves instead.
+            ptrs = torch.as_tensor(np.concatenate(
+                [v.data_ptr() + 8 * np.arange(v.numel(), dtype=np.int64) for v in vals]),
+                dtype=torch.int64, device=self.device)
+            self._patch_ptrs[pkey] = ptrs
+        if ptrs is not None:
             rc = lib.ort_patch_zernike_ptrs(C.byref(self.c), _ptr(ptrs), _ptr(idx), n,
                                             _stream_handle())
             _native.check(rc, "ort_patch_zernike_ptrs")
