@@ -409,7 +409,10 @@ __device__ inline void interact(const KArgs& a, const ort_surface& s, ort::Ray& 
 // per wave in all), so the launch time is the exact pass's: 7.15-7.17 ms at 6 waves per
 // SIMD (80 VGPRs) vs 7.16-7.20 ms exact-only (79 VGPRs); at the compiler's 99 VGPRs
 // (5 waves) 7.29-7.31 ms. TraceWaves: 6 for the wave-uniform-row (F_MONO) kernels
-// measured here, the compiler's choice for the others.
+// measured here, the compiler's choice for the others. The taped Zernike forward (config
+// 5): 5 waves (96 VGPRs, 96 B of scratch) vs 4 (123 VGPRs) after the non-temporal tape
+// stores, config 5 step 0.689 / 0.679 vs 0.692 / 0.694 ms (A/B, r04_ab_occupancy_c5.log;
+// the adjoint at 4 waves instead of 3 measured 540 vs 417 us there).
 template <uint32_t FEAT>
 constexpr bool kNewtonFast =
 #ifdef ORT_NO_NEWTON_FAST
@@ -423,7 +426,7 @@ template <uint32_t FEAT>
 struct TraceWaves {
   static constexpr int value =
       ((FEAT & ort::KM_ZERN) != 0 && (FEAT & (ort::KM_FREE | F_IA)) == 0)
-          ? ((FEAT & F_TAPE) != 0 ? 4 : 6)
+          ? ((FEAT & F_TAPE) != 0 ? 5 : 6)
           : ((kNewtonFast<FEAT> && (FEAT & F_MONO) != 0) ? 6 : 1);
 };
 #ifdef ORT_TRACE_WAVES
