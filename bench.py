@@ -82,7 +82,10 @@ def _flops_per_ray(table, sched=None):
 
 
 class Workload:
-    """One bench configuration: step() is the timed unit; units = intersections/step."""
+    """One bench configuration: step() is the timed unit; units = intersections/step;
+    ramp_steps = untimed steps that keep the GPU busy ~0.5 s before the warmup."""
+
+    ramp_steps = 64
 
     def __init__(self, **kw):
         self.__dict__.update(kw)
@@ -145,7 +148,7 @@ def config1(args, dev, rank, world, torch):
         kernel="trace_closed_kernel<F_GEN|F_SPOT> + spot_dev + spot_final (graph)",
         launches=3,
         bytes_per_launch=None, flops_per_ray=None, pmc_file=None, rays=n, state=state,
-        spot=True, data="synthetic (the reference's uniform 128 pupil grid)")
+        spot=True, data="synthetic (the reference's uniform 128 pupil grid)", ramp_steps=24000)
 
 
 def config2(args, dev, rank, world, torch):
@@ -177,7 +180,7 @@ def config2(args, dev, rank, world, torch):
             "parallelism": f"dp{world} (ray shards, no collective)"},
         kernel="trace_closed_kernel<F_GEN> (ort_trace_pupil)", launches=1,
         bytes_per_launch=R * (16 + 64), flops_per_ray=flops, pmc_file="hbm_traffic.json",
-        rays=R)
+        rays=R, ramp_steps=max(64, 90_000_000_000 // max(1, R * S)))
 
 
 def config3(args, dev, rank, world, torch):
@@ -258,9 +261,9 @@ def config4(args, dev, rank, world, torch):
     # N > 1: the image-plane gather into rank 0 (send / receive buffers allocated here,
     # once), pipelined with the trace: 7 chunks of 7 pairs, each chunk's x, y traced into
     # the send slab and gathered asynchronously (RCCL on its own stream) while the next
-    # chunk traces (distributed.PipelinedImageTrace). The gathered shards stay in rank 0's
-    # receive slabs (the reference-order reassembly is ImageGather.finish(assemble=True),
-    # outside the step)
+    # chunk traces (distributed.PipelinedImageTrace); rank 0 lays each chunk out in the
+    # reference's pair-major order as soon as that chunk has arrived (inside the step, as
+    # in rounds 1-3; round 4 had left the reassembly out of the timed step)
     gather = pipe = None
     if world > 1:
         gather = distributed.ImageGather(len(pairs), n_p, dev)
@@ -268,7 +271,7 @@ def config4(args, dev, rank, world, torch):
 
     def step():
         if pipe is not None:
-            pipe.run(assemble=False)
+            pipe.run(assemble=True)
         else:
             trace_pupil(dl, seg_dev, px, py, out, n, n_loc, n, pupil_per_ray=True)
 
@@ -311,13 +314,16 @@ def config4(args, dev, rank, world, torch):
             return float(t.item()) * 1e3
 
         g_ms = timed(lambda: gather.finish(gather.gather_pairs(0, len(pairs)), assemble=False))
+        a_ms = timed(lambda: gather.finish([], assemble=True))
         t_ms = timed(pipe.trace_only)
-        s_ms = timed(lambda: pipe.run(assemble=False))
+        s_ms = timed(lambda: pipe.run(assemble=True))
         recv = torch.tensor([gather.bytes_received], dtype=torch.float64, device=dev)
         dist.all_reduce(recv, op=dist.ReduceOp.MAX)
         return {"gather_bytes_per_rank": gather.send.numel() * 8,
                 "gather_bytes_into_rank0": int(recv.item()), "gather_ms": g_ms,
-                "trace_ms": t_ms, "pipelined_step_ms": s_ms,
+                "assemble_ms": a_ms, "trace_ms": t_ms, "pipelined_step_ms": s_ms,
+                "step_includes": "trace + gather + rank 0's reassembly into the reference's "
+                                 "pair-major order",
                 "gather_exposed_ms": max(0.0, s_ms - t_ms),
                 "gather_hidden_ms": max(0.0, g_ms - max(0.0, s_ms - t_ms)),
                 "gather_chunks": len(pipe.chunks), "gather_zero_copy": pipe.zero_copy}
@@ -403,7 +409,7 @@ def config5(args, dev, rank, world, torch):
                               if use_graph else "eager (torch ops + ctypes launches)"},
         kernel="adj_kernel<KM_ZERN, 2> (ort_trace_pupil_vjp, adjoint mode)", launches=None,
         bytes_per_launch=None, flops_per_ray=None, pmc_file="hbm_traffic_c5.json", rays=R,
-        state=state, vjp_timer=vjp_timer, eager_step=eager_step,
+        state=state, vjp_timer=vjp_timer, eager_step=eager_step, ramp_steps=720,
         # the taped forward writes the tape, the adjoint only reads it: per traced surface the
         # incoming ray and t (7 rows) plus, for a Newton surface, the min(U, 4) iterates it
         # replays (ort_sweep.h adj_ray), with U the verified schedule -- read after the run
@@ -472,10 +478,11 @@ def main():
     ap.add_argument("--cpu-rays", type=int, default=1_000_000)
     ap.add_argument("--cpu-seconds", type=float, default=1.5,
                     help="wall time of the multi-process CPU baseline leg")
-    ap.add_argument("--ramp-seconds", type=float, default=0.5,
-                    help="untimed steps before the warmup until the GPU clock has ramped "
+    ap.add_argument("--ramp-steps", type=int, default=None,
+                    help="untimed steps before the warmup so the GPU clock has ramped "
                          "(MI355X power management raises the engine clock only under "
-                         "sustained load: the first ~50 ms of launches run up to 15%% slower)")
+                         "sustained load: the first ~50 ms of launches run up to 15%% "
+                         "slower); default: the config's own count, ~0.5 s of its steps")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process group for N > 1 (nccl = RCCL, one GPU per rank); gloo "
                          "lets several ranks share a GPU (rank r on device r mod count) to "
@@ -509,13 +516,15 @@ def main():
     _native.load()
     w = CONFIGS[args.config](args, dev, rank, world, torch)
 
-    # clock ramp (untimed): keep the GPU busy until its engine clock has risen, then the
-    # W warmup steps
-    t_ramp = time.perf_counter()
-    while time.perf_counter() - t_ramp < args.ramp_seconds:
-        for _ in range(8):
-            w.step()
-        torch.cuda.synchronize()
+    # clock ramp (untimed): keep the GPU busy until its engine clock has risen (~0.5 s of
+    # load), then the W warmup steps. A FIXED number of ramp steps per config (not a wall
+    # time), so the work before the timed region -- and config 5's optimisation trajectory,
+    # hence its final_loss -- is the same on every run
+    n_ramp = args.ramp_steps if args.ramp_steps is not None else w.ramp_steps
+    for k in range(n_ramp):
+        w.step()
+        if k % 8 == 7:
+            torch.cuda.synchronize()
     for _ in range(args.warmup):
         w.step()
     torch.cuda.synchronize()
@@ -546,6 +555,18 @@ def main():
 
     value = w.units * args.steps / elapsed
     ms_per_step = elapsed / args.steps * 1e3
+    # results of the timed steps themselves, read before anything else runs: the captured
+    # step's device-verified Newton flags (config 5: vjp_timer's eager steps below share
+    # the flag buffers and would overwrite them) and the last timed step's loss
+    final_loss = None
+    if getattr(w, "state", None) and not getattr(w, "spot", False):
+        from optiland_pr_amd import raytrace
+
+        raytrace.check_all_pending()  # device-verified Newton schedules: raise here
+        if "check" in w.state:
+            w.state["check"]()
+        loss = w.state.get("loss")
+        final_loss = None if loss is None else float(loss)
     extra = w.extra() if getattr(w, "extra", None) else None  # every rank (collectives)
     if getattr(w, "vjp_timer", None):
         w.vjp_ms = w.vjp_timer(getattr(w, "eager_step", w.step), max(3, min(args.steps, 20)),
@@ -569,7 +590,7 @@ def main():
             "data": getattr(w, "data", "synthetic (random pupil rays, numpy default_rng seed = rank)"),
             "config": w.config,
             "roofline": _roofline(w, kern_ms),
-            "timing": {"clock_ramp_s": args.ramp_seconds,
+            "timing": {"clock_ramp_steps": n_ramp,
                        "device_ms_per_step": step_dev_ms,
                        "kernel_time": "HIP events at both ends of the timed region / steps"
                        + ("; roofline kernel_ms = the trace launch alone (events around "
@@ -591,13 +612,8 @@ def main():
             line["config"]["rms_spot_radius_mm"] = [float(v) for v in st[:, 3]]
             line["config"]["geo_spot_radius_mm"] = [float(v) for v in st[:, 4]]
         elif getattr(w, "state", None):
-            from optiland_pr_amd import raytrace
-
-            raytrace.check_all_pending()  # device-verified Newton schedules: raise here
-            if "check" in w.state:
-                w.state["check"]()
-            loss = w.state.get("loss")
-            line["config"]["final_loss"] = None if loss is None else float(loss)
+            line["config"]["final_loss"] = final_loss
+            line["config"]["steps_before_timed"] = n_ramp + args.warmup
         if extra:
             line["config"].update(extra)
         line["cpu_baseline"] = cpu_line

@@ -3,7 +3,8 @@
  * of the torch custom op torch.ops.ort.trace_sequential and of its VJP (SURVEY.md 8b:
  * "registered for the CUDA(HIP) and CPU dispatch keys").
  *
- * It replaces the same reference interface as ort_trace_sequential (optiland_rt.h):
+ * It replaces the same reference interfaces as ort_trace_sequential / ort_trace_pupil /
+ * ort_rms_spot (optiland_rt.h):
  *   optiland/surfaces/surface_group.py:232-244      SurfaceGroup.trace(rays, skip)
  *   optiland/surfaces/standard_surface.py:186-233   Surface.trace (real-ray branch)
  * for rays held in HOST memory -- the reference's own default (backend/torch_backend.py:
@@ -29,7 +30,7 @@
 extern "C" {
 #endif
 
-#define ORT_HOST_ABI_VERSION 1
+#define ORT_HOST_ABI_VERSION 2
 
 int ort_host_abi_version(void);
 
@@ -52,6 +53,31 @@ int ort_host_trace_sequential_vjp(const ort_lens* lens, const ort_rays* rays_in,
                                   const ort_vjp_params* params, const ort_rays* cotangent,
                                   const double* rec_cotangent, const double* rec,
                                   double* grad, const ort_rays* grad_in);
+
+/* ort_trace_pupil on host memory (v2): rays generated from the pupil samples px, py by the
+ * batch's segments (ray r of segment r / seg_len; pupil sample r with pupil_per_ray, else
+ * r - segment * seg_len; ray_generator.py:28-106 through the GPU's generate_ray), then
+ * traced in Newton groups of batch->group_len rays with the reference's stop rule as in
+ * ort_host_trace_sequential (updates: [n_groups][n_surfaces]). No records, no start surface,
+ * no per-ray wavelengths; n_rays must be n_seg * seg_len. Replaces RealRayTracer.trace
+ * (raytrace/real_ray_tracer.py:37-97) for host tensors. */
+int ort_host_trace_pupil(const ort_lens* lens, const double* px, const double* py,
+                         ort_rays* rays_out, const ort_batch* batch, const ort_options* opt,
+                         int32_t* updates, int32_t* status);
+
+/* ort_trace_pupil_vjp on host memory (v2): the adjoint / forward-mode sweeps of the pupil
+ * trace (generation included, not differentiated), opt->sched = the primal's updates. */
+int ort_host_trace_pupil_vjp(const ort_lens* lens, const double* px, const double* py,
+                             const ort_batch* batch, const ort_options* opt,
+                             const ort_vjp_params* params, const ort_rays* cotangent,
+                             double* grad);
+
+/* ort_rms_spot / ort_rms_spot_vjp on host memory (v2): RayOperand.rms_spot_size
+ * (optimization/operand/ray.py:300-340), stats = n, mean x, mean y, rms, max radius; sums in
+ * index order. */
+int ort_host_rms_spot(const double* x, const double* y, int64_t n, double* stats, double* rms);
+int ort_host_rms_spot_vjp(const double* x, const double* y, int64_t n, const double* stats,
+                          const double* grad_out, double* gx, double* gy);
 
 /* threads used by the calls (OpenMP; <= 0: the OpenMP default) */
 void ort_host_set_threads(int32_t n);

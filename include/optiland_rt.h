@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define ORT_ABI_VERSION 17
+#define ORT_ABI_VERSION 18
 #define ORT_MAX_SURFACES 64
 
 /* ---- geometry kinds ----------------------------------- */
@@ -552,6 +552,17 @@ typedef struct ort_vjp_params {
    * ray state from `primal` (that launch's outputs: L, M, N and i are read). */
   const double* tape;
   ort_rays primal;
+  /* ADJOINT (v18): Zernike coefficient adjoints in the Cartesian monomial basis. 0: one
+   * slot per Zernike term (as before v18). Otherwise the number of monomial slots of the
+   * lens, sum over its Zernike surfaces with a Cartesian block (zm_deg >= 0) of
+   * (zm_deg + 1)(zm_deg + 2) -- two per monomial: the sag's and the normal slopes' --
+   * appended after the final-thickness slot in surface order (n_slot = 3 n_surfaces +
+   * n_zern + 1 + n_mono); the kernel sums per-ray monomial values over the rays and the
+   * parameter reduction applies the surfaces' term matrices (Ms / Mn of the block) once
+   * per launch. A value that is not the lens's count disables the basis (per-term slots
+   * serve; the workspace is still sized with it). Requires zern_param. slot_need, when
+   * given, covers all n_slot slots. */
+  int32_t n_mono;
 } ort_vjp_params;
 
 /* Workspace bytes params->mode needs for this lens, batch and parameter set (ADJOINT:

@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import numpy as np
 
-ABI_VERSION = 17
+ABI_VERSION = 18
 VJP_UNROLLED = 0
 VJP_ADJOINT = 1
 AP_RADIAL = 1

@@ -69,6 +69,7 @@ class ort_vjp_params(C.Structure):  # field 7 ("grad_init") was "reserved" befor
         ("slot_need", C.c_void_p),
         ("tape", C.c_void_p),
         ("primal", ort_rays),
+        ("n_mono", C.c_int32),  # v18
     ]
 
 
@@ -239,8 +240,9 @@ def load(path: str | None = None):
 
 
 HOST_EXPORTS = ("ort_host_abi_version", "ort_host_trace_sequential",
-                "ort_host_trace_sequential_vjp", "ort_host_set_threads")
-HOST_ABI_VERSION = 1  # include/optiland_host.h ORT_HOST_ABI_VERSION
+                "ort_host_trace_sequential_vjp", "ort_host_trace_pupil", "ort_host_trace_pupil_vjp",
+                "ort_host_rms_spot", "ort_host_rms_spot_vjp", "ort_host_set_threads")
+HOST_ABI_VERSION = 2  # include/optiland_host.h ORT_HOST_ABI_VERSION
 
 _host = None
 
@@ -268,6 +270,18 @@ def load_host(path: str | None = None):
                                                   P(ort_options), P(ort_vjp_params),
                                                   P(ort_rays), C.c_void_p, C.c_void_p,
                                                   C.c_void_p, P(ort_rays)]
+    lib.ort_host_trace_pupil.restype = C.c_int
+    lib.ort_host_trace_pupil.argtypes = [P(ort_lens), C.c_void_p, C.c_void_p, P(ort_rays),
+                                         P(ort_batch), P(ort_options), C.c_void_p, C.c_void_p]
+    lib.ort_host_trace_pupil_vjp.restype = C.c_int
+    lib.ort_host_trace_pupil_vjp.argtypes = [P(ort_lens), C.c_void_p, C.c_void_p, P(ort_batch),
+                                             P(ort_options), P(ort_vjp_params), P(ort_rays),
+                                             C.c_void_p]
+    lib.ort_host_rms_spot.restype = C.c_int
+    lib.ort_host_rms_spot.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p]
+    lib.ort_host_rms_spot_vjp.restype = C.c_int
+    lib.ort_host_rms_spot_vjp.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p,
+                                          C.c_void_p, C.c_void_p, C.c_void_p]
     lib.ort_host_set_threads.restype = None
     lib.ort_host_set_threads.argtypes = [C.c_int32]
     v = lib.ort_host_abi_version()

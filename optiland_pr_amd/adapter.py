@@ -549,8 +549,9 @@ def _trace_on_mi355x(group, rays, skip):
             except NotImplementedError as e:  # no derivative kernels: the reference loop
                 raise Unsupported(str(e)) from e
     start = max(int(skip) - 1, 0)
+    lens, meta, ft, key = ops.lens_args(dl)
     outs = torch.ops.ort.trace_sequential(
-        ops.handle(dl), fields, w if per_ray else None, [t for _, _, t in params],
+        lens, meta, ft, key, fields, w if per_ray else None, [t for _, _, t in params],
         ops.encode_spec([(k, si) for k, si, _ in params]), start, per_ray)
     STATS[x.device.type] += 1
     conv = (lambda t: t.numpy()) if as_numpy else (lambda t: t)

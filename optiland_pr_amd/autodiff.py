@@ -119,8 +119,10 @@ def vjp_mode(table):
     env = os.environ.get("ORT_VJP_MODE", "").lower()
     if env in ("unrolled", "adjoint"):
         return _abi.VJP_UNROLLED if env == "unrolled" else _abi.VJP_ADJOINT
+    from .ops import mono_slot_count
+
     z = table.zern
-    if 3 * table.n_surfaces + len(z) + 1 > _abi.VJP_ADJOINT_MAX_SLOTS:
+    if 3 * table.n_surfaces + len(z) + 1 + mono_slot_count(table, z) > _abi.VJP_ADJOINT_MAX_SLOTS:
         return _abi.VJP_UNROLLED  # more parameter slots than the adjoint's LDS partials hold
     live = z["c"] != 0.0
     for off, t in getattr(table, "device_coeffs", ()):  # values not on the host
@@ -176,6 +178,10 @@ def vjp(dlens, seg_dev, px, py, n, seg_len, sched_dev, tables, n_param, cot, gra
     params = _native.ort_vjp_params(int(n_param), int(mode), _ptr(zp).value, _ptr(st).value,
                                     _ptr(ft).value, 0 if zp is None else int(zp.numel()),
                                     int(bool(overwrite)), None, 0, _ptr(need).value)
+    if mode == _abi.VJP_ADJOINT:
+        from .ops import mono_slot_count
+
+        params.n_mono = mono_slot_count(dlens.table, zp)
     if tape is not None and mode == _abi.VJP_ADJOINT:
         # the forward wrote the tape (ort_options.tape): reverse sweep only, the final
         # state read from the forward's outputs
@@ -215,8 +221,12 @@ def trace_pupil_grad(optic, dlens, seg_dev, px, py, n, seg_len, wavelength, keys
                       and vjp_mode(dlens.table) == _abi.VJP_ADJOINT
                       and not dlens.table.interaction_mask & ~(1 << _abi.IA_REFRACT_REFLECT)
                       and not np.any(dlens.table.surfaces["geometry"] == _abi.GEOM_GRID_SAG))
-    outs = torch.ops.ort.trace_pupil(ops.handle(plan), px, py, [t for _, _, t in params],
-                                     ops.encode_spec([(k, si) for k, si, _ in params]))
+    lens, meta, ft, key = ops.lens_args(dlens)
+    seg, apod, pmeta, pkey = ops.plan_args(plan)
+    outs = torch.ops.ort.trace_pupil(lens, meta, ft, key, seg, apod, px, py,
+                                     [t for _, _, t in params],
+                                     ops.encode_spec([(k, si) for k, si, _ in params]), pmeta,
+                                     pkey)
     return outs[:8]
 
 
@@ -271,12 +281,20 @@ class CapturedStep:
         # the backward's seed d loss / d loss = 1 as a static tensor made before the capture
         # (loss.backward() would fill a fresh one inside every replay: one launch per step)
         seed = None if loss is None else torch.ones_like(loss)
+        # drop the last warm-up loss before capturing: its autograd graph holds the leaves'
+        # AccumulateGrad nodes, which remember the warm-up stream, and the captured backward
+        # would reuse them on the capture stream (torch warns that the AccumulateGrad
+        # node's stream does not match). Freed here, the capture builds its own nodes; the
+        # capture also runs on the warm-up's stream.
+        del loss
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with torch.cuda.graph(g, stream=side):
             loss = self.loss_fn()
             loss.backward(seed)
             self.opt.step()
+        torch.cuda.current_stream().wait_stream(side)
         self.graph, self.loss = g, loss.detach()
+        del loss
 
     def __call__(self):
         if self.graph is None:

@@ -46,8 +46,12 @@ struct AdjWaves {
 // the wave once per surface -- one DPP wave sum per term and surface instead of one per
 // term and evaluation (32 KB of LDS per block; TMA 1M rays: 582 -> 551 us per adjoint
 // launch, rocprofv3 A/B). ORT_ADJ_ZACC=0 (A/B builds): a wave sum per evaluation.
+// Round 5: surfaces with a Cartesian block take the monomial-basis slots (mono_put below)
+// and need no per-lane term accumulators; the LDS they took (32 KB per block) held the
+// kernel at 3 blocks per CU, so the per-evaluation wave sums serve the polar surfaces
+// (radial order > 6) by default.
 #ifndef ORT_ADJ_ZACC
-#define ORT_ADJ_ZACC 16
+#define ORT_ADJ_ZACC 0
 #endif
 constexpr int kZAcc = ORT_ADJ_ZACC;
 // Block partials: a wave's slot sums are added into bpart[slot][wave of the block] in LDS and
@@ -58,6 +62,26 @@ constexpr int kZAcc = ORT_ADJ_ZACC;
 // host takes the forward-mode VJP above that (autodiff.vjp_mode).
 constexpr int kBlockSlots = ORT_VJP_ADJOINT_MAX_SLOTS;
 
+// Monomial-basis slots (AArgs.n_mono): one evaluation's 2 K values per lane are summed over
+// the wave eight slots at a time through a per-wave LDS transpose -- lane l writes its
+// value for slot row r to scr[r][l]; lane l then adds up row l / 8's entries l % 8,
+// l % 8 + 8, ... (eight of them) and the eight lanes of a row combine by DPP (quad xor 1, 2,
+// row_half_mirror) -- so a chunk of eight slots costs 8 LDS writes, 8 reads and ~16 VALU
+// per lane instead of eight full wave sums (~20 VALU each). The row stride of 72 doubles
+// puts the eight rows' reads on different LDS banks (2-way at most for 64-bit reads).
+constexpr int kMonoStride = 72;
+
+__device__ inline double group8_sum(double v) {
+  if (__builtin_amdgcn_read_exec() == ~0ull) {
+    v += dpp_step<0xB1, 0xf>(v);   // quad_perm [1,0,3,2]
+    v += dpp_step<0x4E, 0xf>(v);   // quad_perm [2,3,0,1]
+    v += dpp_step<0x141, 0xf>(v);  // row_half_mirror: lane i <- lane 7 - i of its 8
+    return v;
+  }
+  for (int o = 1; o < 8; o <<= 1) v += __shfl_xor(v, o, 64);  // the same sums, same order
+  return v;
+}
+
 struct DevLane {
   const AArgs& j;
   int64_t r_ld;                // this lane's ray (0 for the idle tail lanes)
@@ -66,6 +90,27 @@ struct DevLane {
   bool active;
   double (*zacc)[kBlock];      // __shared__ [kZAcc][kBlock] (kZAcc > 0)
   double (*bpart)[kBlock / 64];  // __shared__ [kBlockSlots][4], zeroed at the kernel start
+  double (*mscr)[kMonoStride];   // __shared__ this wave's [8][kMonoStride] transpose rows
+
+  // slot base + i of one evaluation's monomial values (i counts from 0: the chunk of eight
+  // rows is reduced when its last row is written, i known at compile time after unrolling)
+  __device__ inline void mono_put(int base, int i, double v) {
+    mscr[i & 7][threadIdx.x & 63] = active ? v : 0.0;
+    if ((i & 7) == 7) mono_chunk(base + (i & ~7), 8);
+  }
+  __device__ inline void mono_flush(int base, int n) {
+    if (n & 7) mono_chunk(base + (n & ~7), n & 7);
+  }
+  __device__ inline void mono_chunk(int slot, int rows) {
+    const int lane = threadIdx.x & 63, row = lane >> 3, c0 = lane & 7;
+    __builtin_amdgcn_wave_barrier();  // (LDS operations of a wave complete in order)
+    double v = 0.0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v += mscr[row][c0 + 8 * k];
+    v = group8_sum(v);
+    if (c0 == 0 && row < rows) bpart[slot + row][threadIdx.x >> 6] += v;
+    __builtin_amdgcn_wave_barrier();
+  }
 
   __device__ inline void emit(int slot, double v, bool first) {
     if (!cst(j.need)[slot]) return;  // uniform
@@ -114,13 +159,23 @@ __global__ __launch_bounds__(kBlock) ORT_ADJ_OCC void adj_kernel(const KArgs a, 
   for (int k = threadIdx.x; k < j.n_slot * (kBlock / 64); k += kBlock)
     bpart_s[k / (kBlock / 64)][k % (kBlock / 64)] = 0.0;
   __syncthreads();
-  if constexpr (kZAcc > 0 && (KM & ort::KM_ZERN) != 0) {
-    __shared__ double zacc[kZAcc > 0 ? kZAcc : 1][kBlock];
-    DevLane ln{j, active ? rid : 0, a.n_rays, rid >> 6, active, zacc, bpart_s};
-    adj_ray<KM, P, RES>(a, j, ln, rid, active);
+  AArgs jm = j;
+  jm.mono_on = mono_enabled(j);
+  if constexpr ((KM & ort::KM_ZERN) != 0) {
+    __shared__ double mscr[kBlock / 64][8][kMonoStride];
+    if constexpr (kZAcc > 0) {
+      __shared__ double zacc[kZAcc > 0 ? kZAcc : 1][kBlock];
+      DevLane ln{jm, active ? rid : 0, a.n_rays, rid >> 6, active, zacc, bpart_s,
+                 mscr[threadIdx.x >> 6]};
+      adj_ray<KM, P, RES>(a, jm, ln, rid, active);
+    } else {
+      DevLane ln{jm, active ? rid : 0, a.n_rays, rid >> 6, active, nullptr, bpart_s,
+                 mscr[threadIdx.x >> 6]};
+      adj_ray<KM, P, RES>(a, jm, ln, rid, active);
+    }
   } else {
-    DevLane ln{j, active ? rid : 0, a.n_rays, rid >> 6, active, nullptr, bpart_s};
-    adj_ray<KM, P, RES>(a, j, ln, rid, active);
+    DevLane ln{jm, active ? rid : 0, a.n_rays, rid >> 6, active, nullptr, bpart_s, nullptr};
+    adj_ray<KM, P, RES>(a, jm, ln, rid, active);
   }
   __syncthreads();  // the block's waves combined in index order
   for (int slot = threadIdx.x; slot < j.n_slot; slot += kBlock) {

@@ -184,7 +184,8 @@ static bool adj_layout(const ort_lens* lens, const ort_batch* batch,
     L.total = al(L.n_wave * 4 * (int64_t)sizeof(double));
     return true;
   }
-  L.n_slot = (int32_t)(3 * S + params->n_zern + 1);
+  if (params->n_mono < 0 || (params->n_mono > 0 && !params->zern_param)) return false;
+  L.n_slot = (int32_t)(3 * S + params->n_zern + 1 + params->n_mono);
   // partial columns: one per block (its waves combined in LDS, ort_adjoint.h)
   if (L.n_slot > kBlockSlots) return false;  // the forward-mode VJP serves such lenses
   L.n_wave = (n + kBlock - 1) / kBlock;
@@ -288,6 +289,10 @@ static int vjp_run(const ort_lens* lens, const double* px, const double* py,
     aj.zero_partials = opt->start_surface > 0;
     aj.grad = grad;
     aj.grad_store = params->grad_init != 0;
+    aj.n_mono = params->n_mono;
+    aj.surf = lens->surfaces;
+    aj.zern = lens->zern;
+    aj.coef = lens->coef;
     // radius / conic tangents need duals seeded on them too
     return adj_run(a, aj, (int32_t*)(w + L.need), params->surf_tangent ? 4 : 2, km, resident,
                    blocks, s);

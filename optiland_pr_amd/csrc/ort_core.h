@@ -950,8 +950,79 @@ struct IsPlain<double> {
   static constexpr bool value = true;
 };
 
+// The loops below take the degree N at run time; the block's entries A[o + q] are then
+// scalar loads inside a loop with a run-time trip count, each waited for before its
+// multiply (a dependent load chain per Newton evaluation). The degrees that occur (radial
+// orders 2..6) are dispatched to copies with N a template parameter, fully unrolled: the
+// same operations in the same order (bit-identical), with the block's loads issued up
+// front. Other degrees (0, 1) keep the loop.
+template <int N, class PD>
+ORT_INLINE double zmono_value_n(PD A, double x, double y) {
+  double F = 0.0;
+#pragma unroll
+  for (int p = N; p >= 0; --p) {
+    const int o = p * (N + 1) - p * (p - 1) / 2, L = N - p;
+    double B = A[o + L];
+#pragma unroll
+    for (int q = L - 1; q >= 0; --q) B = B * y + A[o + q];
+    F = F * x + B;
+  }
+  return F;
+}
+
+template <int N, class PD>
+ORT_INLINE void zmono_grad_n(PD A, double x, double y, double& F, double& Fx, double& Fy) {
+  F = 0.0;
+  Fx = 0.0;
+  Fy = 0.0;
+#pragma unroll
+  for (int p = N; p >= 0; --p) {
+    const int o = p * (N + 1) - p * (p - 1) / 2, L = N - p;
+    double B = A[o + L], B1 = 0.0;
+#pragma unroll
+    for (int q = L - 1; q >= 0; --q) {
+      B1 = B1 * y + B;
+      B = B * y + A[o + q];
+    }
+    Fx = Fx * x + F;
+    F = F * x + B;
+    Fy = Fy * x + B1;
+  }
+}
+
+template <int N, class PD>
+ORT_INLINE void zmono_hess_n(PD A, double x, double y, double& F, double& Fx, double& Fy,
+                             double& Fxx, double& Fxy, double& Fyy) {
+  F = Fx = Fy = Fxx = Fxy = Fyy = 0.0;
+#pragma unroll
+  for (int p = N; p >= 0; --p) {
+    const int o = p * (N + 1) - p * (p - 1) / 2, L = N - p;
+    double B = A[o + L], B1 = 0.0, B2 = 0.0;
+#pragma unroll
+    for (int q = L - 1; q >= 0; --q) {
+      B2 = B2 * y + 2.0 * B1;
+      B1 = B1 * y + B;
+      B = B * y + A[o + q];
+    }
+    Fxx = Fxx * x + 2.0 * Fx;
+    Fx = Fx * x + F;
+    F = F * x + B;
+    Fxy = Fxy * x + Fy;
+    Fy = Fy * x + B1;
+    Fyy = Fyy * x + B2;
+  }
+}
+
 template <class PD>
 ORT_INLINE double zmono_value(PD A, int N, double x, double y) {
+  switch (N) {
+    case 2: return zmono_value_n<2>(A, x, y);
+    case 3: return zmono_value_n<3>(A, x, y);
+    case 4: return zmono_value_n<4>(A, x, y);
+    case 5: return zmono_value_n<5>(A, x, y);
+    case 6: return zmono_value_n<6>(A, x, y);
+    default: break;
+  }
   double F = 0.0;
   for (int p = N; p >= 0; --p) {
     const int o = p * (N + 1) - p * (p - 1) / 2, L = N - p;
@@ -965,6 +1036,14 @@ ORT_INLINE double zmono_value(PD A, int N, double x, double y) {
 template <class PD>
 ORT_INLINE void zmono_grad(PD A, int N, double x, double y, double& F, double& Fx,
                            double& Fy) {
+  switch (N) {
+    case 2: return zmono_grad_n<2>(A, x, y, F, Fx, Fy);
+    case 3: return zmono_grad_n<3>(A, x, y, F, Fx, Fy);
+    case 4: return zmono_grad_n<4>(A, x, y, F, Fx, Fy);
+    case 5: return zmono_grad_n<5>(A, x, y, F, Fx, Fy);
+    case 6: return zmono_grad_n<6>(A, x, y, F, Fx, Fy);
+    default: break;
+  }
   F = 0.0;
   Fx = 0.0;
   Fy = 0.0;
@@ -984,6 +1063,14 @@ ORT_INLINE void zmono_grad(PD A, int N, double x, double y, double& F, double& F
 template <class PD>
 ORT_INLINE void zmono_hess(PD A, int N, double x, double y, double& F, double& Fx, double& Fy,
                            double& Fxx, double& Fxy, double& Fyy) {
+  switch (N) {
+    case 2: return zmono_hess_n<2>(A, x, y, F, Fx, Fy, Fxx, Fxy, Fyy);
+    case 3: return zmono_hess_n<3>(A, x, y, F, Fx, Fy, Fxx, Fxy, Fyy);
+    case 4: return zmono_hess_n<4>(A, x, y, F, Fx, Fy, Fxx, Fxy, Fyy);
+    case 5: return zmono_hess_n<5>(A, x, y, F, Fx, Fy, Fxx, Fxy, Fyy);
+    case 6: return zmono_hess_n<6>(A, x, y, F, Fx, Fy, Fxx, Fxy, Fyy);
+    default: break;
+  }
   F = Fx = Fy = Fxx = Fxy = Fyy = 0.0;
   for (int p = N; p >= 0; --p) {
     const int o = p * (N + 1) - p * (p - 1) / 2, L = N - p;

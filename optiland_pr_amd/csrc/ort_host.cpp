@@ -249,9 +249,11 @@ struct HostLane {
   int uniform_max(int v) const { return v; }
   void zemit(int slot, int, double v, bool first) { emit(slot, v, first); }
   void zflush(int, int) {}
+  void mono_put(int base, int i, double v) { acc[base + i] += v; }
+  void mono_flush(int, int) {}
 };
 
-template <uint32_t KM, int P>
+template <uint32_t KM, int P, bool RES = true>
 void adj_chunks(const KArgs& a, const AArgs& j, std::vector<double>& part, int64_t n_chunk) {
   const int nt = threads_for(a.n_rays);
 #pragma omp parallel num_threads(nt)
@@ -262,7 +264,7 @@ void adj_chunks(const KArgs& a, const AArgs& j, std::vector<double>& part, int64
       double* acc = part.data() + c * j.n_slot;
       HostLane ln{j, acc, tape.data()};
       const int64_t e = std::min(a.n_rays, (c + 1) * kChunk);
-      for (int64_t rid = c * kChunk; rid < e; ++rid) adj_ray<KM, P, true>(a, j, ln, rid, true);
+      for (int64_t rid = c * kChunk; rid < e; ++rid) adj_ray<KM, P, RES>(a, j, ln, rid, true);
     }
   }
 }
@@ -320,30 +322,17 @@ int ort_host_trace_sequential(const ort_lens* lens, const ort_rays* rays_in,
   return ORT_OK;
 }
 
-int ort_host_trace_sequential_vjp(const ort_lens* lens, const ort_rays* rays_in,
-                                  const ort_batch* batch, const ort_options* opt,
-                                  const ort_vjp_params* params, const ort_rays* cotangent,
-                                  const double* rec_cotangent, const double* rec,
-                                  double* grad, const ort_rays* grad_in) {
-  if (!batch || !cotangent || !params || params->n_param < 0 || !rays_in || !opt)
-    return ORT_ERR_ARG;
+}  // extern "C"
+
+namespace {
+
+// The shared body of the two host VJPs: resident rays (rays_in, RES) or rays generated from
+// pupil samples (a.px / a.py, the batch's segments: ort_trace_pupil_vjp's counterpart)
+template <bool RES>
+int host_vjp(KArgs& a, const ort_lens* lens, const ort_vjp_params* params,
+             const ort_rays* cotangent, const double* rec_cotangent, const double* rec,
+             double* grad, const ort_rays* grad_in, bool want_in) {
   const int32_t n_param = params->n_param;
-  const bool want_in = grad_in && (grad_in->x || grad_in->y || grad_in->z || grad_in->L ||
-                                   grad_in->M || grad_in->N || grad_in->i || grad_in->opd);
-  if (n_param > 0 && !grad) return ORT_ERR_ARG;
-  if (params->grad_init && n_param > 0)
-    for (int p = 0; p < n_param; ++p) grad[p] = 0.0;
-  if (batch->n_rays == 0 || (n_param == 0 && !want_in)) return ORT_OK;
-  if (rec_cotangent && !rec) return ORT_ERR_ARG;
-  if (opt->verify_stats || opt->tape || params->tape) return ORT_ERR_ARG;
-  KArgs a{};
-  uint32_t feat = 0;
-  int rc = fill_args(a, lens, batch, opt, nullptr, nullptr, nullptr, feat);
-  if (rc) return rc;
-  if (params->zern_param && (feat & ort::KM_ZERN) == 0) return ORT_ERR_ARG;
-  if (feat & F_IA) return ORT_ERR_ARG;  // no derivative code for thin-lens / phase / grating
-  if (lens->geometry_mask & (1u << ORT_GEOM_GRID_SAG)) return ORT_ERR_ARG;  // nor grid sags
-  a.in = *rays_in;
   const int64_t n_chunk = (a.n_rays + kChunk - 1) / kChunk;
   if (params->mode == ORT_VJP_ADJOINT) {
     AArgs j{};
@@ -352,8 +341,14 @@ int ort_host_trace_sequential_vjp(const ort_lens* lens, const ort_rays* rays_in,
     j.tan_final = params->final_tangent;
     j.n_param = n_param;
     j.n_zern = params->n_zern;
-    j.n_slot = 3 * a.n_surf + params->n_zern + 1;
+    if (params->n_mono < 0 || (params->n_mono > 0 && !params->zern_param)) return ORT_ERR_ARG;
+    j.n_slot = 3 * a.n_surf + params->n_zern + 1 + params->n_mono;
     j.n_surf = a.n_surf;
+    j.n_mono = params->n_mono;
+    j.surf = lens->surfaces;
+    j.zern = lens->zern;
+    j.coef = lens->coef;
+    j.mono_on = mono_enabled(j);
     j.cot = *cotangent;
     j.rec_cot = rec_cotangent;
     j.rec = rec;
@@ -369,9 +364,9 @@ int ort_host_trace_sequential_vjp(const ort_lens* lens, const ort_rays* rays_in,
     j.need = need.data();
     std::vector<double> part((size_t)n_chunk * j.n_slot, 0.0);
     if (params->surf_tangent)
-      adj_chunks<kAllKinds, 4>(a, j, part, n_chunk);
+      adj_chunks<kAllKinds, 4, RES>(a, j, part, n_chunk);
     else
-      adj_chunks<kAllKinds, 2>(a, j, part, n_chunk);
+      adj_chunks<kAllKinds, 2, RES>(a, j, part, n_chunk);
     // grad[p] += sum over slots of d slot / d p * (the chunks' sums in index order)
     std::vector<double> slot_sum(j.n_slot, 0.0);
     for (int slot = 0; slot < j.n_slot; ++slot) {
@@ -383,7 +378,7 @@ int ort_host_trace_sequential_vjp(const ort_lens* lens, const ort_rays* rays_in,
     for (int p = 0; p < n_param; ++p) {
       double g = 0.0;
       for (int slot = 0; slot < j.n_slot; ++slot) {
-        const double w = slot_weight(j, slot, p);
+        const double w = need[slot] ? slot_weight(j, slot, p) : 0.0;
         if (w != 0.0) g += slot_sum[slot] * w;
       }
       grad[p] += g;
@@ -409,6 +404,167 @@ int ort_host_trace_sequential_vjp(const ort_lens* lens, const ort_rays* rays_in,
       for (int64_t c = 0; c < n_chunk; ++c) v += part[(size_t)c * 4 + k];
       grad[p0 + k] += v;
     }
+  }
+  return ORT_OK;
+}
+
+// rays of a pupil trace generated on the host (ray_generator.py:28-106 via ort::generate_ray,
+// the GPU's source): ray r of segment r / seg_len at pupil sample r (pupil_per_ray) or
+// r - segment * seg_len
+void generate_host(const KArgs& a, const double* px, const double* py, std::vector<double>& buf,
+                   ort_rays& rays) {
+  const int64_t n = a.n_rays;
+  buf.assign((size_t)n * 8, 0.0);
+  double* f[8];
+  for (int k = 0; k < 8; ++k) f[k] = buf.data() + (size_t)k * n;
+  rays = ort_rays{f[0], f[1], f[2], f[3], f[4], f[5], f[6], f[7]};
+  const int nt = threads_for(n);
+#pragma omp parallel for num_threads(nt) schedule(static)
+  for (int64_t r = 0; r < n; ++r) {
+    const int64_t sidx = r / a.seg_len;
+    const ort_segment sg = a.seg[sidx];
+    const int64_t p = a.pupil_per_ray ? r : r - sidx * a.seg_len;
+    const Ray q = ort::generate_ray(sg, px[p], py[p], a.apod);
+    f[0][r] = q.x;
+    f[1][r] = q.y;
+    f[2][r] = q.z;
+    f[3][r] = q.L;
+    f[4][r] = q.M;
+    f[5][r] = q.N;
+    f[6][r] = ort::intensity(q);
+    f[7][r] = q.opd;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int ort_host_trace_sequential_vjp(const ort_lens* lens, const ort_rays* rays_in,
+                                  const ort_batch* batch, const ort_options* opt,
+                                  const ort_vjp_params* params, const ort_rays* cotangent,
+                                  const double* rec_cotangent, const double* rec,
+                                  double* grad, const ort_rays* grad_in) {
+  if (!batch || !cotangent || !params || params->n_param < 0 || !rays_in || !opt)
+    return ORT_ERR_ARG;
+  const int32_t n_param = params->n_param;
+  const bool want_in = grad_in && (grad_in->x || grad_in->y || grad_in->z || grad_in->L ||
+                                   grad_in->M || grad_in->N || grad_in->i || grad_in->opd);
+  if (n_param > 0 && !grad) return ORT_ERR_ARG;
+  if (params->grad_init && n_param > 0)
+    for (int p = 0; p < n_param; ++p) grad[p] = 0.0;
+  if (batch->n_rays == 0 || (n_param == 0 && !want_in)) return ORT_OK;
+  if (rec_cotangent && !rec) return ORT_ERR_ARG;
+  if (opt->verify_stats || opt->tape || params->tape) return ORT_ERR_ARG;
+  KArgs a{};
+  uint32_t feat = 0;
+  int rc = fill_args(a, lens, batch, opt, nullptr, nullptr, nullptr, feat);
+  if (rc) return rc;
+  if (params->zern_param && (feat & ort::KM_ZERN) == 0) return ORT_ERR_ARG;
+  if (feat & F_IA) return ORT_ERR_ARG;  // no derivative code for thin-lens / phase / grating
+  if (lens->geometry_mask & (1u << ORT_GEOM_GRID_SAG)) return ORT_ERR_ARG;  // nor grid sags
+  a.in = *rays_in;
+  return host_vjp<true>(a, lens, params, cotangent, rec_cotangent, rec, grad, grad_in, want_in);
+}
+
+int ort_host_trace_pupil(const ort_lens* lens, const double* px, const double* py,
+                         ort_rays* rays_out, const ort_batch* batch, const ort_options* opt,
+                         int32_t* updates, int32_t* status) {
+  if (!px || !py || !rays_out || !batch || !batch->seg || batch->n_seg < 1 || batch->w)
+    return ORT_ERR_ARG;
+  const ort_options dflt{ORT_NEWTON_SCHEDULE, 0, nullptr, 0, 0};
+  if (!opt) opt = &dflt;
+  if (opt->tape || opt->verify_stats || opt->run_if || opt->start_surface) return ORT_ERR_ARG;
+  KArgs a{};
+  uint32_t feat = 0;
+  int rc = fill_args(a, lens, batch, opt, nullptr, nullptr, status, feat);
+  if (rc) return rc;
+  if (batch->n_rays != (int64_t)batch->n_seg * batch->seg_len) return ORT_ERR_ARG;
+  a.out = *rays_out;
+  if (status) *status = 0;
+  if (a.n_rays == 0) return ORT_OK;
+  std::vector<double> buf;
+  ort_rays gen;
+  generate_host(a, px, py, buf, gen);
+  a.in = gen;
+  const int64_t n_groups = (a.n_rays + a.group_len - 1) / a.group_len;
+  int st = 0;
+  if (a.apod && (uint32_t)a.apod->kind > (uint32_t)ORT_APOD_TUKEY) st |= ORT_STATUS_BAD_APODIZATION;
+  for (int64_t g = 0; g < n_groups; ++g) {
+    const int64_t r0 = g * a.group_len, r1 = std::min(a.n_rays, r0 + a.group_len);
+    int32_t* up = updates ? updates + g * a.n_surf : nullptr;
+    if (up)
+      for (int s = 0; s < a.n_surf; ++s) up[s] = 0;
+    trace_group(a, r0, r1, up, st);
+  }
+  if (status) *status = st;
+  return ORT_OK;
+}
+
+int ort_host_trace_pupil_vjp(const ort_lens* lens, const double* px, const double* py,
+                             const ort_batch* batch, const ort_options* opt,
+                             const ort_vjp_params* params, const ort_rays* cotangent,
+                             double* grad) {
+  if (!px || !py || !batch || !batch->seg || batch->w || !cotangent || !params ||
+      params->n_param < 0 || !opt)
+    return ORT_ERR_ARG;
+  const int32_t n_param = params->n_param;
+  if (n_param > 0 && !grad) return ORT_ERR_ARG;
+  if (params->grad_init && n_param > 0)
+    for (int p = 0; p < n_param; ++p) grad[p] = 0.0;
+  if (batch->n_rays == 0 || n_param == 0) return ORT_OK;
+  if (opt->verify_stats || opt->tape || params->tape || opt->start_surface) return ORT_ERR_ARG;
+  KArgs a{};
+  uint32_t feat = 0;
+  int rc = fill_args(a, lens, batch, opt, nullptr, nullptr, nullptr, feat);
+  if (rc) return rc;
+  if (params->zern_param && (feat & ort::KM_ZERN) == 0) return ORT_ERR_ARG;
+  if (feat & F_IA) return ORT_ERR_ARG;
+  if (lens->geometry_mask & (1u << ORT_GEOM_GRID_SAG)) return ORT_ERR_ARG;
+  a.px = px;
+  a.py = py;
+  return host_vjp<false>(a, lens, params, cotangent, nullptr, nullptr, grad, nullptr, false);
+}
+
+// RayOperand.rms_spot_size (optimization/operand/ray.py:300-340) on host memory: the mean
+// of x and y over all n points, then sqrt(mean((x - mx)^2 + (y - my)^2)); sums in index
+// order (one thread: the value does not depend on a thread count). stats: n, mean x,
+// mean y, rms, max radius (the ort_rms_spot layout).
+int ort_host_rms_spot(const double* x, const double* y, int64_t n, double* stats, double* rms) {
+  if (n < 0 || !stats || !rms || (n > 0 && (!x || !y))) return ORT_ERR_ARG;
+  double sx = 0.0, sy = 0.0;
+  for (int64_t k = 0; k < n; ++k) {
+    sx += x[k];
+    sy += y[k];
+  }
+  const double mx = sx / (double)n, my = sy / (double)n;
+  double s2 = 0.0, rmax = 0.0;
+  for (int64_t k = 0; k < n; ++k) {
+    const double dx = x[k] - mx, dy = y[k] - my;
+    const double r2 = dx * dx + dy * dy;
+    s2 += r2;
+    const double r = sqrt(r2);
+    if (r > rmax || r != r) rmax = r;
+  }
+  const double v = sqrt(s2 / (double)n);
+  stats[0] = (double)n;
+  stats[1] = mx;
+  stats[2] = my;
+  stats[3] = v;
+  stats[4] = rmax;
+  *rms = v;
+  return ORT_OK;
+}
+
+// its VJP: d rms / d (x_k, y_k) = (x_k - mx, y_k - my) / (n rms), times grad_out
+int ort_host_rms_spot_vjp(const double* x, const double* y, int64_t n, const double* stats,
+                          const double* grad_out, double* gx, double* gy) {
+  if (n < 0 || !stats || !grad_out || (n > 0 && (!x || !y || !gx || !gy))) return ORT_ERR_ARG;
+  const double mx = stats[1], my = stats[2];
+  const double s = grad_out[0] / (stats[0] * stats[3]);
+  for (int64_t k = 0; k < n; ++k) {
+    gx[k] = (x[k] - mx) * s;
+    gy[k] = (y[k] - my) * s;
   }
   return ORT_OK;
 }

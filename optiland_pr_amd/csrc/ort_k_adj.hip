@@ -7,9 +7,11 @@ namespace ortk {
 
 // need[slot]: some parameter depends on the slot (skips its wave sums); used when the
 // caller passes no ort_vjp_params.slot_need
-__global__ void adj_need_kernel(const AArgs j, int32_t* need) {
+__global__ void adj_need_kernel(const AArgs j0, int32_t* need) {
   const int slot = blockIdx.x * blockDim.x + threadIdx.x;
-  if (slot >= j.n_slot) return;
+  if (slot >= j0.n_slot) return;
+  AArgs j = j0;
+  j.mono_on = mono_enabled(j0);
   int nd = 0;
   for (int p = 0; p < j.n_param && !nd; ++p) nd = slot_weight(j, slot, p) != 0.0;
   need[slot] = nd;
@@ -23,15 +25,18 @@ __global__ void adj_need_kernel(const AArgs j, int32_t* need) {
 // one dependent table load per slot, and each thread's strided partial loads are issued
 // eight at a time ahead of their (in-order) additions: 27 -> see DESIGN for the TMA's 43
 // slots x 30 parameters.
-__global__ __launch_bounds__(kBlock) void adj_param_reduce_kernel(const AArgs j) {
+__global__ __launch_bounds__(kBlock) void adj_param_reduce_kernel(const AArgs j0) {
   const int p = blockIdx.x;
+  AArgs j = j0;
+  j.mono_on = mono_enabled(j0);
   __shared__ double ws[kBlock / 64];
   __shared__ double wt[kBlock];
   double g = 0.0;  // meaningful in thread 0
   for (int base = 0; base < j.n_slot; base += kBlock) {
     const int my = base + threadIdx.x;
     __syncthreads();  // the previous pass's wt reads are done
-    wt[threadIdx.x] = my < j.n_slot ? slot_weight(j, my, p) : 0.0;
+    // (a slot the launch did not sum -- need == 0 -- has no partials to read)
+    wt[threadIdx.x] = (my < j.n_slot && cst(j.need)[my]) ? slot_weight(j, my, p) : 0.0;
     __syncthreads();
     const int end = min(kBlock, j.n_slot - base);
     for (int c = 0; c < end; ++c) {

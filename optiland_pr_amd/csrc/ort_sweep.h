@@ -339,14 +339,95 @@ struct AArgs {
   ort_rays primal;          // the final ray state read from its outputs (L, M, N, i)
   double* grad;             // [n_param], accumulated (grad_store: overwritten)
   int32_t grad_store;
+  // Zernike coefficient adjoints in the Cartesian monomial basis (ort_vjp_params.n_mono,
+  // ABI v18): every Zernike surface with a Cartesian block (zm_deg >= 0) owns 2 K slots
+  // after the final-thickness slot -- S_k = sum w_sag m_k and D_k = sum (a_x dm_k/dxn +
+  // a_y dm_k/dyn) over its evaluations, m_k = xn^p yn^q in the block's order -- and the
+  // parameter reduce applies the term matrices Ms / Mn once per launch (mono_weight).
+  // mono_on: n_mono equals that count (mono_slots); otherwise the per-term slots serve.
+  int32_t n_mono;
+  int32_t mono_on;
+  const ort_surface* surf;  // the lens tables the reduce reads the term matrices from
+  const ort_zernike_term* zern;
+  const double* coef;
 };
+
+// monomials of a Cartesian block of degree N
+ORT_INLINE int mono_count(int N) { return (N + 1) * (N + 2) / 2; }
+// slots of a surface in the monomial basis (0: none)
+ORT_INLINE int mono_slots(const ort_surface& s) {
+  return (s.geometry == ORT_GEOM_ZERNIKE && s.zm_deg >= 0) ? 2 * mono_count(s.zm_deg) : 0;
+}
+// the lens's monomial slot count (every surface, in order)
+ORT_INLINE int mono_total(const ort_surface* surf, int n_surf) {
+  int t = 0;
+  for (int si = 0; si < n_surf; ++si) t += mono_slots(cst(surf)[si]);
+  return t;
+}
+
+// the monomial slots serve (AArgs.mono_on): the caller's n_mono is the lens's count
+ORT_INLINE bool mono_enabled(const AArgs& j) {
+  return j.n_mono > 0 && j.zparam && j.surf && j.coef && j.zern &&
+         mono_total(j.surf, j.n_surf) == j.n_mono;
+}
+
+// the traced surface whose Zernike terms include row `row` of lens.zern (-1: none)
+ORT_INLINE int term_surface(const AArgs& j, int row) {
+  for (int si = 0; si < j.n_surf; ++si) {
+    const ort_surface s = cst(j.surf)[si];
+    if (s.geometry == ORT_GEOM_ZERNIKE && row >= s.coef_off && row < s.coef_off + s.n_coef)
+      return si;
+  }
+  return -1;
+}
+
+// d(monomial slot m) / d(parameter p): slot m (0-based after the final-thickness slot) is
+// S_k or D_k of some surface; its weight is the sum over the surface's terms j that are
+// parameter p of Ms[j][k] (the sag: d sag / d c_j = sum_k Ms[j][k] m_k) resp. Mn[j][k] (the
+// normal's slopes; zero for c_j == 0, whose term the reference's normal skips,
+// zernike.py:213-214)
+ORT_INLINE double mono_weight(const AArgs& j, int m, int p) {
+  int base = 0;
+  for (int si = 0; si < j.n_surf; ++si) {
+    const ort_surface s = cst(j.surf)[si];
+    const int ms = mono_slots(s);
+    if (m < base + ms) {
+      const int K = mono_count(s.zm_deg), r = m - base;
+      const bool sag = r < K;
+      const int k = sag ? r : r - K;
+      const int nt = s.n_coef;
+      const double* Ms = j.coef + s.zm_off + 2 * K;
+      const double* Mn = Ms + (int64_t)nt * K;
+      double w = 0.0;
+      for (int jt = 0; jt < nt; ++jt) {
+        if (!j.zparam || j.zparam[s.coef_off + jt] != p) continue;
+        if (sag)
+          w = w + Ms[(int64_t)jt * K + k];
+        else if (j.zern[s.coef_off + jt].c != 0.0)
+          w = w + Mn[(int64_t)jt * K + k];
+      }
+      return w;
+    }
+    base += ms;
+  }
+  return 0.0;
+}
 
 // d(slot) / d(parameter p)
 ORT_INLINE double slot_weight(const AArgs& j, int slot, int p) {
   const int ns = 3 * j.n_surf;
   if (slot < ns) return j.tan_surf ? j.tan_surf[(int64_t)p * ns + slot] : 0.0;
-  if (slot < ns + j.n_zern) return (j.zparam && j.zparam[slot - ns] == p) ? 1.0 : 0.0;
-  return j.tan_final ? j.tan_final[p] : 0.0;
+  if (slot < ns + j.n_zern) {
+    if (!j.zparam || j.zparam[slot - ns] != p) return 0.0;
+    // a term of a surface served by the monomial slots has no per-term slot of its own
+    if (j.mono_on) {
+      const int si = term_surface(j, slot - ns);
+      if (si >= 0 && mono_slots(cst(j.surf)[si]) > 0) return 0.0;
+    }
+    return 1.0;
+  }
+  if (slot == ns + j.n_zern) return j.tan_final ? j.tan_final[p] : 0.0;
+  return j.mono_on ? mono_weight(j, slot - ns - j.n_zern - 1, p) : 0.0;
 }
 
 // adjoint of a coordinate-system op: rotations transpose (sin -> -sin), translations
@@ -385,6 +466,60 @@ ORT_INLINE double replay_distance(const KArgs& a, const ort_surface& s, int si,
   return t;
 }
 
+// One evaluation's Zernike coefficient adjoint in the monomial basis of a degree-N block
+// (see AArgs.n_mono): at the normalised point (xn, yn) the sag's weight ws adds ws m_k to
+// S_k (SAG; without it -- the hit point, where the sag has no adjoint -- the S slots are
+// left alone) and the slopes' weights (ax, ay) -- the adjoint of the block gradient
+// (Gx, Gy) the Cartesian normal is formed from -- add ax dm_k/dxn + ay dm_k/dyn to D_k;
+// handed to the lane value by value (mono_put(base, i, v): slot base + i, i counting from
+// 0), then mono_flush(base, n)
+template <int N, bool SAG, class Lane>
+ORT_INLINE void zmono_adjoint(Lane& ln, int slot0, double xn, double yn, double ws, double ax,
+                              double ay) {
+  constexpr int K = (N + 1) * (N + 2) / 2;
+  double xp[N + 1], yp[N + 1];
+  xp[0] = yp[0] = 1.0;
+#pragma unroll
+  for (int p = 1; p <= N; ++p) {
+    xp[p] = xp[p - 1] * xn;
+    yp[p] = yp[p - 1] * yn;
+  }
+  const int base = SAG ? slot0 : slot0 + K;
+  int i = 0;
+  if constexpr (SAG) {
+#pragma unroll
+    for (int p = 0; p <= N; ++p) {
+#pragma unroll
+      for (int q = 0; q <= N - p; ++q) ln.mono_put(base, i++, ws * (xp[p] * yp[q]));
+    }
+  }
+#pragma unroll
+  for (int p = 0; p <= N; ++p) {
+#pragma unroll
+    for (int q = 0; q <= N - p; ++q) {
+      double d = 0.0;
+      if (p > 0) d = ax * ((double)p * (xp[p - 1] * yp[q]));
+      if (q > 0) d = d + ay * ((double)q * (xp[p] * yp[q - 1]));
+      ln.mono_put(base, i++, d);
+    }
+  }
+  ln.mono_flush(base, i);
+}
+
+template <bool SAG, class Lane>
+ORT_INLINE void zmono_adjoint_deg(Lane& ln, int deg, int slot0, double xn, double yn, double ws,
+                                  double ax, double ay) {
+  switch (deg) {
+    case 0: zmono_adjoint<0, SAG>(ln, slot0, xn, yn, ws, ax, ay); break;
+    case 1: zmono_adjoint<1, SAG>(ln, slot0, xn, yn, ws, ax, ay); break;
+    case 2: zmono_adjoint<2, SAG>(ln, slot0, xn, yn, ws, ax, ay); break;
+    case 3: zmono_adjoint<3, SAG>(ln, slot0, xn, yn, ws, ax, ay); break;
+    case 4: zmono_adjoint<4, SAG>(ln, slot0, xn, yn, ws, ax, ay); break;
+    case 5: zmono_adjoint<5, SAG>(ln, slot0, xn, yn, ws, ax, ay); break;
+    default: zmono_adjoint<6, SAG>(ln, slot0, xn, yn, ws, ax, ay); break;
+  }
+}
+
 // The lane policy (Lane) adj_ray is written against:
 //   void   emit(int slot, double v, bool first)  add the ray's v to parameter slot `slot`
 //                                                 (first: the slot's first contribution
@@ -396,6 +531,9 @@ ORT_INLINE double replay_distance(const KArgs& a, const ort_surface& s, int si,
 //                                                 a Zernike term's contribution (term j of
 //                                                 the surface; first: the surface's first);
 //                                                 zflush after the surface's last one
+//   void   mono_put(int slot0, int i, double v), mono_flush(int slot0, int n)
+//                                                 one evaluation's monomial-basis values,
+//                                                 v to slot slot0 + i (zmono_adjoint)
 // RES = false: rays generated from pupil samples (ort_trace_pupil_vjp);
 // RES = true: resident input rays a.in (ort_trace_sequential_vjp, SurfaceGroup.trace under
 // autograd), optionally with per-ray wavelengths (a.w), and the cotangents of the input
@@ -496,6 +634,11 @@ ORT_INLINE void adj_ray(const KArgs& a, const AArgs& j, Lane& ln, int64_t rid, b
     }
   };
 
+  // monomial-basis coefficient slots (AArgs.n_mono): the current surface's first slot
+  // (mono_base, -1: per-term slots), walking back from the end of the slot table
+  int mono_base = -1;
+  int mono_end = 3 * a.n_surf + j.n_zern + 1 + (j.mono_on ? j.n_mono : 0);
+
   // Zernike coefficients at local (x, y): w_sag * d sag / d c plus the slopes' share of
   // the normal's adjoint bn (n = (dzdx, dzdy, -1) / q, q = -1 / nz)
   auto zern_adj = [&](const ort_surface& s, bool on, bool first, double x, double y,
@@ -512,6 +655,33 @@ ORT_INLINE void adj_ray(const KArgs& a, const AArgs& j, Lane& ln, int64_t rid, b
         const double bn = bnx * nxv + bny * nyv + bnz * nzv;
         const double bdx = -nzv * (bnx - nxv * bn);
         const double bdy = -nzv * (bny - nyv * bn);
+        if (mono_base >= 0) {
+          // the Cartesian normal's slopes (sagnorm_zernike): dzdx += Fr drho_dx + G2 qy / Rn,
+          // dzdy += Fr drho_dy + G2 qx / Rn with Fr = (xn Gx + yn Gy) / rho (0 at rho = 0)
+          // and G2 = xn Gy - yn Gx: their adjoints (bdx, bdy) pulled back to (Gx, Gy)
+          double xn, yn;
+          ort::div2(x, y, s.norm_radius, xn, yn);
+          const double eps = 1e-14;
+          const double rho = sqrt(xn * xn + yn * yn);
+          const double Rn = s.norm_radius;
+          double xr, yr, drx, dry, qy, qx;
+          ort::div2(x, y, Rn * Rn, xr, yr);
+          ort::div2(xr, yr, rho + eps, drx, dry);
+          ort::div2(-(yn), xn, rho * rho + eps, qy, qx);
+          const double inv_rn = 1.0 / Rn;
+          double cx = 0.0, cy = 0.0;  // xn / rho, yn / rho (Fr's factors)
+          if (rho > 0.0) ort::div2(xn, yn, rho, cx, cy);
+          const double fr = bdx * drx + bdy * dry;        // adjoint of Fr
+          const double g2 = (bdx * qy + bdy * qx) * inv_rn;  // adjoint of G2
+          const double ax = fr * cx - g2 * yn;
+          const double ay = fr * cy + g2 * xn;
+          const double wx = on ? ax : 0.0, wy = on ? ay : 0.0;
+          if (first)  // the hit point: the normal only (w_sag == 0)
+            zmono_adjoint_deg<false>(ln, s.zm_deg, mono_base, xn, yn, 0.0, wx, wy);
+          else
+            zmono_adjoint_deg<true>(ln, s.zm_deg, mono_base, xn, yn, on ? w_sag : 0.0, wx, wy);
+          return;
+        }
         const int base = 3 * a.n_surf;
         ort::zernike_coef_adjoint(x, y, s.norm_radius, cst(a.zern), s.coef_off, s.n_coef,
                                   cst(a.coef), w_sag, bdx, bdy,
@@ -632,6 +802,16 @@ ORT_INLINE void adj_ray(const KArgs& a, const AArgs& j, Lane& ln, int64_t rid, b
   for (int si = a.n_surf - 1; si >= a.start_surface; --si) {
     const ort_surface s = cst(a.surf)[si];
     const ort_surface_optics o = optics_of(s, si);
+    if constexpr ((KM & ort::KM_ZERN) != 0) {
+      mono_base = -1;  // this surface's monomial slots (uniform), walking back from the end
+      if (j.mono_on) {
+        const int ms = mono_slots(s);
+        if (ms > 0) {
+          mono_end -= ms;
+          mono_base = mono_end;
+        }
+      }
+    }
     // cotangent of this surface's record (the state after its globalize): the adjoint of
     // the state there gains it; its intensity row through att (d I / d att = I, the
     // primal's recorded value)
@@ -790,7 +970,8 @@ ORT_INLINE void adj_ray(const KArgs& a, const AArgs& j, Lane& ln, int64_t rid, b
     }
 
     if constexpr ((KM & ort::KM_ZERN) != 0) {
-      if (s.geometry == ORT_GEOM_ZERNIKE && j.zparam) ln.zflush(3 * a.n_surf + s.coef_off, s.n_coef);
+      if (s.geometry == ORT_GEOM_ZERNIKE && j.zparam && mono_base < 0)
+        ln.zflush(3 * a.n_surf + s.coef_off, s.n_coef);
     }
 
     // localize adjoint: the op list transposed in reverse, then - cs_t

@@ -269,10 +269,15 @@ class PipelinedImageTrace:
                 trace_pupil(self.dl, seg_dev, pxc, pyc, sub, nc, nl, nc, pupil_per_ray=True)
             if self.gather.world > 1:
                 cols = () if self.zero_copy else (self.out.x, self.out.y)
-                works += self.gather.gather_pairs(lo, hi, *cols)
+                works.append((lo, hi, self.gather.gather_pairs(lo, hi, *cols)))
         if self.gather.world == 1:
             return self.gather.gather(self.out.x, self.out.y)
-        return self.gather.finish(works, assemble=assemble)
+        # chunk by chunk: the compute stream waits for chunk k's gather only, so dst lays
+        # chunk k out in the reference's order while chunk k + 1 is still on xGMI
+        planes = None
+        for lo, hi, w in works:
+            planes = self.gather.finish(w, lo, hi, assemble=assemble)
+        return planes
 
 
 def gather_image_plane(x, y, n_loc_pairs, n_pairs, n_p, group=None, dst=0):

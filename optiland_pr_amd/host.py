@@ -63,11 +63,21 @@ class HostLens:
             mask, table.interaction_mask, table.final_thickness, _p(mats), _p(lambdas),
             table.frame_flags)
         self._keep = keep
+        # the same nine tables as torch CPU tensors sharing these arrays' memory (the lens as
+        # the torch ops take it: ops.lens_args)
+        self._tensors = [torch.from_numpy(a.view(np.uint8) if a.dtype.fields else a)
+                         for a in (surfaces, cs_ops, coef, zern, n_tab.reshape(-1),
+                                   alpha_tab.reshape(-1), optics.reshape(-1), mats, lambdas)]
         self.newton = table.newton_surfaces
         self.last_schedule = None
         self.last_schedule_dev = None
         self.last_schedule_private = False
         self._resident: dict = {}
+
+    def lens_tensors(self):
+        """[surfaces, cs_ops, coef, zern, n_tab, alpha_tab, optics, materials, wavelengths]
+        as CPU tensors (structured tables as their bytes)."""
+        return self._tensors
 
     def resident(self, slot, arr):
         """A CPU tensor copy of a small host table, reused while its bytes are unchanged
@@ -138,6 +148,9 @@ def trace_sequential_vjp(hl: HostLens, rays_in, w, per_ray_w, start_surface, sch
     zp, st, ft = tabs
     params = _native.ort_vjp_params(int(n_param), int(mode), _p(zp), _p(st), _p(ft),
                                     0 if zp is None else int(zp.numel()), 0, None, 0, _p(need))
+    from .ops import mono_slot_count
+
+    params.n_mono = mono_slot_count(hl.table, None if zp is None else zp.numpy())
     rc = lib.ort_host_trace_sequential_vjp(
         C.byref(hl.c), C.byref(_rays_c(rays_in)), C.byref(batch), C.byref(opt),
         C.byref(params), C.byref(_rays_c(cot)), _p(rec_cot),
@@ -145,3 +158,69 @@ def trace_sequential_vjp(hl: HostLens, rays_in, w, per_ray_w, start_surface, sch
         C.byref(_rays_c(gin if gin is not None else [None] * 8)))
     _native.check(rc, "ort_host_trace_sequential_vjp")
     del w_keep
+
+
+def trace_pupil(hl: HostLens, seg, px, py, n, seg_len, pupil_per_ray, apod=None):
+    """ort_host_trace_pupil: rays generated from the pupil samples by the segments (SEGMENT
+    records as a uint8 CPU tensor) and traced as one reference trace call (one Newton
+    group); returns the 8 output tensors and the update counts [S] (int32)."""
+    from .raytrace import _raise_status_value
+
+    lib = _native.load_host()
+    n_seg = seg.numel() // _abi.SEGMENT.itemsize
+    outs = [torch.empty(n, dtype=torch.float64) for _ in range(8)]
+    # one Newton group: the whole call, as RealRayTracer.trace traces every field of a
+    # wavelength in one SurfaceGroup.trace (real_ray_tracer.py:37-97)
+    batch = _native.ort_batch(n, max(seg_len, 1), max(n, 1), n_seg, int(pupil_per_ray),
+                              seg.data_ptr())
+    batch.apod = None if apod is None else apod.data_ptr()
+    S = hl.table.n_surfaces
+    n_groups = 1 if n else 0
+    updates = torch.zeros(max(1, n_groups) * S, dtype=torch.int32)
+    status = np.zeros(1, dtype=np.int32)
+    opt = _native.ort_options(_abi.NEWTON_SCHEDULE, 0, None)
+    out_c = _rays_c(outs)
+    rc = lib.ort_host_trace_pupil(C.byref(hl.c), _p(px), _p(py), C.byref(out_c), C.byref(batch),
+                                  C.byref(opt), _p(updates), _p(status))
+    _native.check(rc, "ort_host_trace_pupil")
+    _raise_status_value(int(status[0]))
+    return outs, updates[:n_groups * S]
+
+
+def trace_pupil_vjp(hl: HostLens, seg, px, py, n, seg_len, pupil_per_ray, sched, tabs, need,
+                    n_param, mode, cot, grad, apod=None):
+    """ort_host_trace_pupil_vjp: grad = J^T cot of the pupil trace (grad overwritten)."""
+    from .ops import mono_slot_count
+
+    lib = _native.load_host()
+    n_seg = seg.numel() // _abi.SEGMENT.itemsize
+    batch = _native.ort_batch(n, max(seg_len, 1), max(n, 1), n_seg, int(pupil_per_ray),
+                              seg.data_ptr())
+    batch.apod = None if apod is None else apod.data_ptr()
+    sched_c = sched if sched is not None and sched.numel() else None
+    opt = _native.ort_options(_abi.NEWTON_SCHEDULE, 0, _p(sched_c))
+    zp, st, ft = tabs
+    params = _native.ort_vjp_params(int(n_param), int(mode), _p(zp), _p(st), _p(ft),
+                                    0 if zp is None else int(zp.numel()), 1, None, 0, _p(need))
+    params.n_mono = mono_slot_count(hl.table, None if zp is None else zp.numpy())
+    rc = lib.ort_host_trace_pupil_vjp(C.byref(hl.c), _p(px), _p(py), C.byref(batch), C.byref(opt),
+                                      C.byref(params), C.byref(_rays_c(cot)), _p(grad))
+    _native.check(rc, "ort_host_trace_pupil_vjp")
+
+
+def rms_spot(x, y):
+    """ort_host_rms_spot: (rms scalar, stats[5]) of contiguous float64 CPU tensors."""
+    lib = _native.load_host()
+    stats = torch.empty(5, dtype=torch.float64)
+    rms = torch.empty((), dtype=torch.float64)
+    rc = lib.ort_host_rms_spot(_p(x), _p(y), x.numel(), _p(stats), _p(rms))
+    _native.check(rc, "ort_host_rms_spot")
+    return rms, stats
+
+
+def rms_spot_vjp(x, y, stats, g):
+    lib = _native.load_host()
+    gx, gy = torch.empty_like(x), torch.empty_like(y)
+    rc = lib.ort_host_rms_spot_vjp(_p(x), _p(y), x.numel(), _p(stats), _p(g), _p(gx), _p(gy))
+    _native.check(rc, "ort_host_rms_spot_vjp")
+    return gx, gy

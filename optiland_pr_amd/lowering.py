@@ -134,13 +134,22 @@ def _device_tensor(v):
 # Material lowering results by material key (BaseMaterial.key(): the formula source or
 # the constants themselves, so equal keys mean equal materials) and by (key, wavelength):
 # the dispersion records and n / alpha at the lens's wavelengths are the same from one
-# trace call to the next.
+# trace call to the next. Keys that name an object rather than its parameters (the
+# adapter's ("ref", id(m)) for a custom reference material, which may be mutated, or a new
+# material created at a recycled id) are never cached: those are recomputed on every
+# lowering.
 _MAT_LOWER: dict = {}
 _MAT_N_ALPHA: dict = {}
 
 
+def _cacheable(key):
+    return not (isinstance(key, tuple) and key[:1] == ("ref",))
+
+
 def _material_lower(m):
     key = m.key()
+    if not _cacheable(key):
+        return m.lower()
     hit = _MAT_LOWER.get(key)
     if hit is None:
         if len(_MAT_LOWER) > 4096:
@@ -151,14 +160,15 @@ def _material_lower(m):
 
 def _material_n_alpha(m, w):
     key = (m.key(), w)
-    hit = _MAT_N_ALPHA.get(key)
+    hit = _MAT_N_ALPHA.get(key) if _cacheable(key[0]) else None
     if hit is None:
         if len(_MAT_N_ALPHA) > 65536:
             _MAT_N_ALPHA.clear()
         kv = m.k_scalar(w)
         # homogeneous.py:49-54: applied only when k > 0; alpha = 4*pi*k/w
         hit = (m.n_scalar(w), (4 * np.pi * np.float64(kv) / np.float64(w)) if kv > 0 else 0.0)
-        _MAT_N_ALPHA[key] = hit
+        if _cacheable(key[0]):
+            _MAT_N_ALPHA[key] = hit
     return hit
 
 

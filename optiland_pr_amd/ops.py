@@ -39,6 +39,8 @@ from __future__ import annotations
 import ctypes as C
 import weakref
 
+import os
+
 import numpy as np
 import torch
 
@@ -141,19 +143,49 @@ def tangent_tables(table, pairs, params):
     return zp, surf, final, n_param
 
 
+# ORT_ADJ_MONO=0 (A/B checks): Zernike coefficient adjoints in per-term slots instead of
+# the Cartesian monomial basis (ort_vjp_params.n_mono, ABI v18)
+ADJ_MONO = os.environ.get("ORT_ADJ_MONO", "1") != "0"
+
+
+def mono_slot_count(table, zp):
+    """ort_vjp_params.n_mono: the monomial-basis slots of the lens's Zernike surfaces with a
+    Cartesian block (2 K = (zm_deg + 1)(zm_deg + 2) each, in surface order), 0 without
+    Zernike parameters (or with ORT_ADJ_MONO=0)."""
+    if zp is None or not ADJ_MONO:
+        return 0
+    s = table.surfaces
+    d = s["zm_deg"][(s["geometry"] == _abi.GEOM_ZERNIKE) & (s["zm_deg"] >= 0)].astype(np.int64)
+    return int(np.sum((d + 1) * (d + 2)))
+
+
 def slot_need(table, zp, surf, final):
     """ort_vjp_params.slot_need of the tangent tables: nonzero for every slot (radius,
-    conic, vertex z of each surface; each Zernike term; the final thickness) some
-    parameter depends on. Host NumPy, kept resident with the tables."""
+    conic, vertex z of each surface; each Zernike term; the final thickness; the monomial
+    slots of the Cartesian Zernike surfaces) some parameter depends on. Host NumPy, kept
+    resident with the tables."""
     S = table.n_surfaces
     n_z = 0 if zp is None else len(zp)
-    need = np.zeros(3 * S + n_z + 1, dtype=np.int32)
+    n_mono = mono_slot_count(table, zp)
+    need = np.zeros(3 * S + n_z + 1 + n_mono, dtype=np.int32)
     if surf is not None:
         need[:3 * S] = np.any(surf != 0.0, axis=0).reshape(-1)
     if zp is not None:
         need[3 * S:3 * S + n_z] = zp >= 0
     if final is not None:
-        need[-1] = np.any(final != 0.0)
+        need[3 * S + n_z] = np.any(final != 0.0)
+    if n_mono:
+        off = 3 * S + n_z + 1
+        for row in table.surfaces:
+            if int(row["geometry"]) != _abi.GEOM_ZERNIKE or int(row["zm_deg"]) < 0:
+                continue
+            d = int(row["zm_deg"])
+            c0, nt = int(row["coef_off"]), int(row["n_coef"])
+            if np.any(zp[c0:c0 + nt] >= 0):
+                need[off:off + (d + 1) * (d + 2)] = 1
+                # the per-term slots of this surface are not summed (the monomials are)
+                need[3 * S + c0:3 * S + c0 + nt] = 0
+            off += (d + 1) * (d + 2)
     return need
 
 
@@ -192,10 +224,89 @@ def _ray_struct(ts):
 
 
 # --------------------------------------------------------------------------------------
+# the lens as the ops take it (the op is self-describing)
+# --------------------------------------------------------------------------------------
+# lens_meta: the host-side scalars of the ort_lens struct, in this order
+LENS_META = ("n_surfaces", "n_lambda", "n_mat", "final_mat", "geometry_mask",
+             "interaction_mask", "frame_flags", "n_rec", "newton")
+NEWTON_MODES = ("reference", "device", "wave")
+
+
+def lens_args(dl):
+    """(lens, lens_meta, final_thickness, lens_key) of a DeviceLens / HostLens: the nine
+    lowered tables as tensors on the lens's device -- surfaces, cs_ops, zern, optics and
+    materials as their bytes (uint8), coef, n_tab, alpha_tab and the wavelengths as float64
+    -- the ort_lens scalars, the image-space thickness and the handle of the object that
+    holds the host-side state (Newton schedule caches), used only as a cache key."""
+    t = dl.table
+    meta = [int(t.n_surfaces), len(t.wavelengths), int(t.n_tab.shape[1]), int(t.final_mat),
+            int(dl.geometry_mask), int(t.interaction_mask), int(t.frame_flags), int(t.n_rec),
+            1 if dl.newton else 0]
+    return dl.lens_tensors(), meta, float(t.final_thickness), handle(dl)
+
+
+# lenses rebuilt from their tensors (a handle that names no live object of those tensors:
+# e.g. a traced graph run in another process), keyed by the tables' addresses
+_REBUILT: "weakref.WeakValueDictionary[tuple, object]" = weakref.WeakValueDictionary()
+
+
+def _table_from_tensors(lens, meta, final_thickness):
+    from .lowering import LensTable
+
+    def raw(t, dt):
+        return np.frombuffer(t.detach().cpu().numpy().tobytes(), dtype=dt).copy()
+
+    S, n_lambda, n_mat = meta[0], meta[1], meta[2]
+    surfaces = raw(lens[0], _abi.SURFACE)
+    rec = [i for i in range(S) if int(surfaces[i]["flags"]) & _abi.SURF_RECORD]
+    mats = raw(lens[7], _abi.MATERIAL)
+    return LensTable(
+        surfaces=surfaces, cs_ops=raw(lens[1], _abi.CS_OP),
+        coef=lens[2].detach().cpu().numpy().astype(np.float64).copy(),
+        zern=raw(lens[3], _abi.ZERNIKE_TERM),
+        n_tab=lens[4].detach().cpu().numpy().reshape(n_lambda, n_mat).copy(),
+        alpha_tab=lens[5].detach().cpu().numpy().reshape(n_lambda, n_mat).copy(),
+        wavelengths=[float(v) for v in lens[8].detach().cpu().numpy()],
+        final_mat=int(meta[3]), final_thickness=float(final_thickness), mat_table=mats,
+        n_rec=int(meta[7]), rec_surfaces=rec)
+
+
+def _resolve(lens, meta, final_thickness, key):
+    """The DeviceLens / HostLens these tensors are: the object named by `key` when it holds
+    exactly these tables, else one rebuilt from the tensors (cached by their addresses)."""
+    obj = _HANDLES.get(int(key))
+    if obj is not None and hasattr(obj, "lens_tensors"):
+        mine = obj.lens_tensors()
+        if all(a.data_ptr() == b.data_ptr() and a.device == b.device
+               for a, b in zip(mine, lens, strict=True)):
+            return obj
+    ck = tuple((t.device.type, t.data_ptr()) for t in lens)
+    hit = _REBUILT.get(ck)
+    if hit is None:
+        table = _table_from_tensors(lens, meta, final_thickness)
+        if lens[0].device.type == "cpu":
+            from .host import HostLens
+
+            hit = HostLens(table)
+        else:
+            from .raytrace import DeviceLens
+
+            hit = DeviceLens(table, device=lens[0].device)
+        hit._source_tensors = list(lens)  # the rebuilt object keeps its source alive
+        _REBUILT[ck] = hit
+    return hit
+
+
+def _opt(t):
+    return None if t is None else t
+
+
+# --------------------------------------------------------------------------------------
 # ort::trace_sequential
 # --------------------------------------------------------------------------------------
 @torch.library.custom_op("ort::trace_sequential", mutates_args=(), device_types="cuda")
-def trace_sequential(lens: int, rays: list[torch.Tensor], w: torch.Tensor | None,
+def trace_sequential(lens: list[torch.Tensor], lens_meta: list[int], final_thickness: float,
+                     lens_key: int, rays: list[torch.Tensor], w: torch.Tensor | None,
                      params: list[torch.Tensor], spec: list[int], start_surface: int,
                      per_ray_w: bool) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor,
                                                torch.Tensor, torch.Tensor, torch.Tensor,
@@ -203,7 +314,7 @@ def trace_sequential(lens: int, rays: list[torch.Tensor], w: torch.Tensor | None
                                                torch.Tensor]:
     from .raytrace import RealRays, trace_rays
 
-    dl = _lookup(lens)
+    dl = _resolve(lens, lens_meta, final_thickness, lens_key)
     if len(rays) != 8:
         raise ValueError("rays: x, y, z, L, M, N, i, opd")
     n = rays[0].numel()
@@ -231,14 +342,16 @@ def trace_sequential(lens: int, rays: list[torch.Tensor], w: torch.Tensor | None
 
 
 @trace_sequential.register_kernel("cpu")
-def _trace_sequential_cpu(lens, rays, w, params, spec, start_surface, per_ray_w):
-    """The CPU dispatch key: the host build of the trace core on a HostLens (host.py)."""
+def _trace_sequential_cpu(lens, lens_meta, final_thickness, lens_key, rays, w, params, spec,
+                          start_surface, per_ray_w):
+    """The CPU dispatch key: the host build of the trace core (host.py) on the lens's CPU
+    tensors."""
     from . import host
 
-    hl = _lookup(lens)
+    hl = _resolve(lens, lens_meta, final_thickness, lens_key)
     if not isinstance(hl, host.HostLens):
-        raise RuntimeError("ort::trace_sequential: CPU tensors need a HostLens handle "
-                           f"(got {type(hl).__name__})")
+        raise RuntimeError("ort::trace_sequential: CPU rays need the lens's tables on the CPU "
+                           f"(got a {type(hl).__name__})")
     if len(rays) != 8:
         raise ValueError("rays: x, y, z, L, M, N, i, opd")
     n = rays[0].numel()
@@ -255,18 +368,19 @@ def _trace_sequential_cpu(lens, rays, w, params, spec, start_surface, per_ray_w)
 
 
 @trace_sequential.register_fake
-def _(lens, rays, w, params, spec, start_surface, per_ray_w):
-    dl = _lookup(lens)
+def _(lens, lens_meta, final_thickness, lens_key, rays, w, params, spec, start_surface,
+      per_ray_w):
     n = rays[0].numel()
     outs = [rays[0].new_empty(n, dtype=torch.float64) for _ in range(8)]
-    rec = rays[0].new_empty(dl.table.n_rec * 8 * n, dtype=torch.float64)
-    ns = dl.table.n_surfaces if dl.newton else 0
+    rec = rays[0].new_empty(lens_meta[7] * 8 * n, dtype=torch.float64)
+    ns = lens_meta[0] if lens_meta[8] else 0
     return (*outs, rec, rays[0].new_empty(ns, dtype=torch.int32))
 
 
 def _seq_setup(ctx, inputs, output):
-    lens, rays, w, params, spec, start_surface, per_ray_w = inputs
-    ctx.dlens = _lookup(lens)  # a strong reference for the backward
+    lens, meta, ft, key, rays, w, params, spec, start_surface, per_ray_w = inputs
+    ctx.lens_meta, ctx.final_thickness, ctx.lens_key = list(meta), float(ft), int(key)
+    ctx.n_lens = len(lens)
     ctx.pairs = _spec_pairs(spec)
     ctx.start_surface = int(start_surface)
     ctx.per_ray_w = bool(per_ray_w)
@@ -275,7 +389,7 @@ def _seq_setup(ctx, inputs, output):
     ctx.ray_meta = [(r.shape, r.dtype) for r in rays]
     ctx.set_materialize_grads(False)
     rec, sched = output[8], output[9]
-    saved = [r.detach() for r in rays] + [rec, sched]
+    saved = list(lens) + [r.detach() for r in rays] + [rec, sched]
     if w is not None:
         saved.append(w.detach())
     ctx.has_w = w is not None
@@ -284,44 +398,48 @@ def _seq_setup(ctx, inputs, output):
 
 def _seq_backward(ctx, *grads):
     saved = ctx.saved_tensors
-    rays_in, rec, sched = saved[:8], saved[8], saved[9]
-    w = saved[10] if ctx.has_w else None
-    dl = ctx.dlens
+    nl = ctx.n_lens
+    lens = list(saved[:nl])
+    rays_in, rec, sched = list(saved[nl:nl + 8]), saved[nl + 8], saved[nl + 9]
+    w = saved[nl + 10] if ctx.has_w else None
+    dl = _resolve(lens, ctx.lens_meta, ctx.final_thickness, ctx.lens_key)
     table = dl.table
-    n = rays_in[0].numel()
-    dev = dl.device
-    # list inputs: needs_input_grad holds one bool per list element
-    want_rays = any(ctx.needs_input_grad[1])
-    want_params = any(ctx.needs_input_grad[3]) and len(ctx.shapes) > 0
+    want_rays = any(ctx.needs_input_grad[4])  # list inputs: one bool per element
+    want_params = any(ctx.needs_input_grad[6]) and len(ctx.shapes) > 0
     cot = [None if g is None else g.detach().to(torch.float64).reshape(-1).contiguous()
            for g in grads[:8]]
     rec_cot = grads[8]
     if rec_cot is not None:
         rec_cot = rec_cot.detach().to(torch.float64).reshape(-1).contiguous()
-    # Tensor-list arguments take a list of Nones; the int list `spec` is one leaf of the
-    # argument structure, except when empty (then it reads as an empty tensor list)
+    # Tensor-list arguments take a list of Nones; the int lists are one leaf each, except an
+    # empty `spec` (then it reads as an empty tensor list)
     none_rays, none_params = [None] * 8, [None] * len(ctx.shapes)
     none_spec = [] if ctx.n_spec == 0 else None
+    nothing = ([None] * ctx.n_lens, None, None, None)
     if not (want_rays or want_params) or (all(c is None for c in cot) and rec_cot is None):
-        return None, none_rays, None, none_params, none_spec, None, None
+        return (*nothing, none_rays, None, none_params, none_spec, None, None)
     _check_differentiable(table)
     params_like = [torch.empty(s, dtype=d, device="meta") for s, d, _ in ctx.shapes]
     zp, st, ft, n_param = tangent_tables(table, ctx.pairs, params_like)
-    g = torch.zeros(max(1, n_param), dtype=torch.float64, device=dev)
-    gin = [torch.zeros(n, dtype=torch.float64, device=dev) if want_rays else None
-           for _ in range(8)]
     from .autodiff import vjp_mode
 
     mode = vjp_mode(table)
-    if want_params and n_param:
-        _seq_vjp(dl, rays_in, w, ctx.per_ray_w, ctx.start_surface, sched, zp, st, ft,
-                 n_param, cot, rec_cot, rec, g, gin if mode == _abi.VJP_ADJOINT else None,
-                 mode)
-    if want_rays and not (want_params and n_param and mode == _abi.VJP_ADJOINT):
-        # input-ray cotangents come from the reverse-mode pass (forward mode carries only
-        # the parameter tangents): one adjoint launch with no parameters
-        _seq_vjp(dl, rays_in, w, ctx.per_ray_w, ctx.start_surface, sched, None, None, None,
-                 0, cot, rec_cot, rec, None, gin, _abi.VJP_ADJOINT)
+    if not (want_params and n_param):
+        zp = st = ft = None
+        n_param = 0
+        mode = _abi.VJP_ADJOINT  # input-ray cotangents: the reverse-mode pass
+    tabs = _tables_cpu(zp, st, ft, slot_need(table, zp, st, ft) if mode == _abi.VJP_ADJOINT
+                       else None)
+    g, gin = torch.ops.ort.trace_sequential_vjp(
+        lens, ctx.lens_meta, ctx.final_thickness, ctx.lens_key, rays_in, w, sched, rec, cot,
+        rec_cot, tabs, n_param, int(mode), ctx.start_surface, ctx.per_ray_w, bool(want_rays))
+    if want_rays and mode != _abi.VJP_ADJOINT:
+        # input-ray cotangents come from the reverse-mode pass (forward mode carries only the
+        # parameter tangents): one adjoint launch with no parameters
+        _, gin = torch.ops.ort.trace_sequential_vjp(
+            lens, ctx.lens_meta, ctx.final_thickness, ctx.lens_key, rays_in, w, sched, rec,
+            cot, rec_cot, [None, None, None, None], 0, int(_abi.VJP_ADJOINT),
+            ctx.start_surface, ctx.per_ray_w, True)
     ray_grads = none_rays
     if want_rays:
         ray_grads = [gi.reshape(s).to(d) for gi, (s, d) in zip(gin, ctx.ray_meta, strict=True)]
@@ -333,21 +451,85 @@ def _seq_backward(ctx, *grads):
             k = int(np.prod(shape)) if len(shape) else 1
             param_grads.append(g[off:off + k].reshape(shape).to(device=pdev, dtype=dtype))
             off += k
-    return None, ray_grads, None, param_grads, none_spec, None, None
+    return (*nothing, ray_grads, None, param_grads, none_spec, None, None)
+
+
+def _tables_cpu(zp, st, ft, need):
+    """The tangent tables as host tensors (the VJP ops' `tables` argument)."""
+    return [None if a is None else torch.from_numpy(np.ascontiguousarray(a))
+            for a in (zp, st, ft, need)]
+
+
+trace_sequential.register_autograd(_seq_backward, setup_context=_seq_setup)
+
+
+# --------------------------------------------------------------------------------------
+# ort::trace_sequential_vjp -- the backward as its own op (traceable: fake + kernels)
+# --------------------------------------------------------------------------------------
+@torch.library.custom_op("ort::trace_sequential_vjp", mutates_args=(), device_types="cuda")
+def trace_sequential_vjp(lens: list[torch.Tensor], lens_meta: list[int], final_thickness: float,
+                         lens_key: int, rays_in: list[torch.Tensor], w: torch.Tensor | None,
+                         sched: torch.Tensor, rec: torch.Tensor,
+                         cot: list[torch.Tensor | None], rec_cot: torch.Tensor | None,
+                         tables: list[torch.Tensor | None], n_param: int, mode: int,
+                         start_surface: int, per_ray_w: bool,
+                         want_rays: bool) -> tuple[torch.Tensor, list[torch.Tensor]]:
+    """ort_trace_sequential_vjp: (grad [max(1, n_param)] = J^T cot w.r.t. the parameters of
+    the tangent tables (zern_param, surf_tangent, final_tangent, slot_need), the input-ray
+    cotangents [8][n] when want_rays, else [])."""
+    dl = _resolve(lens, lens_meta, final_thickness, lens_key)
+    return _seq_vjp_run(dl, rays_in, w, sched, rec, cot, rec_cot, tables, n_param, mode,
+                        start_surface, per_ray_w, want_rays)
+
+
+@trace_sequential_vjp.register_kernel("cpu")
+def _trace_sequential_vjp_cpu(lens, lens_meta, final_thickness, lens_key, rays_in, w, sched, rec,
+                              cot, rec_cot, tables, n_param, mode, start_surface, per_ray_w,
+                              want_rays):
+    dl = _resolve(lens, lens_meta, final_thickness, lens_key)
+    return _seq_vjp_run(dl, rays_in, w, sched, rec, cot, rec_cot, tables, n_param, mode,
+                        start_surface, per_ray_w, want_rays)
+
+
+@trace_sequential_vjp.register_fake
+def _(lens, lens_meta, final_thickness, lens_key, rays_in, w, sched, rec, cot, rec_cot, tables,
+      n_param, mode, start_surface, per_ray_w, want_rays):
+    n = rays_in[0].numel()
+    g = rays_in[0].new_empty(max(1, n_param), dtype=torch.float64)
+    gin = [rays_in[0].new_empty(n, dtype=torch.float64) for _ in range(8)] if want_rays else []
+    return g, gin
+
+
+def _seq_vjp_run(dl, rays_in, w, sched, rec, cot, rec_cot, tables, n_param, mode,
+                 start_surface, per_ray_w, want_rays):
+    dev = dl.device
+    n = rays_in[0].numel()
+    rays_in = [t.detach().to(device=dev, dtype=torch.float64).reshape(-1).contiguous()
+               for t in rays_in]
+    cot = [None if c is None else c.detach().to(device=dev, dtype=torch.float64).reshape(-1)
+           .contiguous() for c in cot]
+    g = torch.zeros(max(1, n_param), dtype=torch.float64, device=dev)
+    gin = [torch.zeros(n, dtype=torch.float64, device=dev) for _ in range(8)] if want_rays else None
+    zp, st, ft, need = (None if t is None else t.detach().cpu().numpy() for t in tables)
+    _seq_vjp(dl, rays_in, w, per_ray_w, start_surface, sched, zp, st, ft, n_param, cot,
+             rec_cot, rec, g if n_param else None, gin, mode, need)
+    return g, (gin if want_rays else [])
 
 
 def _seq_vjp(dl, rays_in, w, per_ray_w, start_surface, sched, zp, st, ft, n_param, cot,
-             rec_cot, rec, grad, gin, mode):
+             rec_cot, rec, grad, gin, mode, need=None):
     """One ort_trace_sequential_vjp call (grad += J^T cot, gin = input-ray cotangents); on
     a HostLens the host library's ort_host_trace_sequential_vjp."""
     from . import host
     from .raytrace import _ptr, _stream_handle
 
+    if need is None and mode == _abi.VJP_ADJOINT and zp is not None:
+        need = slot_need(dl.table, zp, st, ft)
     if isinstance(dl, host.HostLens):
         tabs = [None if a is None else dl.resident(("seq_tangent", i), a)
                 for i, a in enumerate((zp, st, ft))]
-        need = dl.resident("seq_need", slot_need(dl.table, zp, st, ft))
-        host.trace_sequential_vjp(dl, rays_in, w, per_ray_w, start_surface, sched, tabs, need,
+        need_t = None if need is None else dl.resident("seq_need", need)
+        host.trace_sequential_vjp(dl, rays_in, w, per_ray_w, start_surface, sched, tabs, need_t,
                                   n_param, mode, cot, rec_cot, rec, grad, gin)
         return
 
@@ -364,11 +546,12 @@ def _seq_vjp(dl, rays_in, w, per_ray_w, start_surface, sched, zp, st, ft, n_para
                               None if sched_dev is None else sched_dev.data_ptr())
     tabs = [None if a is None else dl.resident(("seq_tangent", i), a)
             for i, a in enumerate((zp, st, ft))]
-    need = dl.resident("seq_need", slot_need(dl.table, zp, st, ft))
+    need_t = None if need is None else dl.resident("seq_need", need)
     params = _native.ort_vjp_params(int(n_param), int(mode), _ptr(tabs[0]).value,
                                     _ptr(tabs[1]).value, _ptr(tabs[2]).value,
                                     0 if tabs[0] is None else int(tabs[0].numel()), 0, None, 0,
-                                    need.data_ptr())
+                                    _ptr(need_t).value)
+    params.n_mono = mono_slot_count(dl.table, zp) if mode == _abi.VJP_ADJOINT else 0
     # both modes take a workspace (ABI v15: the unrolled mode's block partials)
     size = lib.ort_vjp_workspace_size(C.byref(dl.c), C.byref(batch), C.byref(params))
     _native.check(int(size) if size < 0 else 0, "ort_vjp_workspace_size")
@@ -386,30 +569,56 @@ def _seq_vjp(dl, rays_in, w, per_ray_w, start_surface, sched, zp, st, ft, n_para
     del w_keep, tabs  # ordered on the stream before any reuse of their memory
 
 
-trace_sequential.register_autograd(_seq_backward, setup_context=_seq_setup)
-
-
 # --------------------------------------------------------------------------------------
 # ort::trace_pupil
 # --------------------------------------------------------------------------------------
+def plan_args(plan):
+    """(seg, apod, plan_meta, plan_key) of a PupilPlan: the segment descriptors (SEGMENT
+    records as bytes on the lens's device), the apodization record (or None), [n, seg_len,
+    pupil_per_ray, newton mode index, want_tape] and the plan's handle (its Newton schedule
+    cache keys; a cache key only)."""
+    dl = plan.dlens
+    seg = plan.seg_dev
+    if not torch.is_tensor(seg):
+        seg = dl.resident("segments", np.asarray(seg, dtype=_abi.SEGMENT))
+    apod = getattr(dl, "apod", None)
+    if apod is None and getattr(dl.table, "apod", None) is not None and dl.device.type == "cpu":
+        apod = dl.resident("apod", dl.table.apod)
+    meta = [plan.n, plan.seg_len, int(plan.pupil_per_ray),
+            NEWTON_MODES.index(plan.newton_mode), int(bool(plan.want_tape))]
+    return seg, apod, meta, handle(plan)
+
+
+def _plan_keys(plan_key):
+    """The Newton schedule cache keys of the plan (raytrace._run falls back to per-group
+    keys when there are none)."""
+    p = _HANDLES.get(int(plan_key))
+    return list(getattr(p, "keys", ()) or ())
+
+
 @torch.library.custom_op("ort::trace_pupil", mutates_args=(), device_types="cuda")
-def trace_pupil(plan: int, px: torch.Tensor, py: torch.Tensor, params: list[torch.Tensor],
-                spec: list[int]) -> tuple[
+def trace_pupil(lens: list[torch.Tensor], lens_meta: list[int], final_thickness: float,
+                lens_key: int, seg: torch.Tensor, apod: torch.Tensor | None, px: torch.Tensor,
+                py: torch.Tensor, params: list[torch.Tensor], spec: list[int],
+                plan_meta: list[int], plan_key: int) -> tuple[
         torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor,
-        torch.Tensor, torch.Tensor, torch.Tensor]:
+        torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]:
+    """Optic.trace's fused generation + trace (ort_trace_pupil): outputs the 8 ray columns,
+    the verified Newton schedule and the adjoint tape (empty unless plan_meta asks for it:
+    the backward is then the reverse sweep only)."""
     from .raytrace import RealRays
     from .raytrace import trace_pupil as _trace
 
-    p = _lookup(plan)
-    dl = p.dlens
+    dl = _resolve(lens, lens_meta, final_thickness, lens_key)
+    n, seg_len, ppr, mode, want_tape = plan_meta
     out = RealRays.__new__(RealRays)
     for a in _abi.RAY_FIELDS:
-        setattr(out, a, torch.empty(p.n, dtype=torch.float64, device=dl.device))
-    p.tape = None
-    if p.want_tape:  # the forward writes the adjoint tape: the backward is the reverse sweep
-        p.tape = torch.empty(tape_doubles(dl, p.n), dtype=torch.float64, device=dl.device)
-    _trace(dl, p.seg_dev, px, py, out, p.n, p.seg_len, p.n, keys=p.keys,
-           pupil_per_ray=p.pupil_per_ray, newton_mode=p.newton_mode, tape=p.tape)
+        setattr(out, a, torch.empty(n, dtype=torch.float64, device=dl.device))
+    tape = torch.empty(tape_doubles(dl, n) if want_tape else 0, dtype=torch.float64,
+                       device=dl.device)
+    _trace(dl, seg, px, py, out, n, seg_len, n, keys=_plan_keys(plan_key),
+           pupil_per_ray=bool(ppr), newton_mode=NEWTON_MODES[mode],
+           tape=tape if want_tape else None)
     sched = dl.last_schedule
     if dl.last_schedule_dev is not None:  # device-verified: the settled device schedule
         sched_t = (dl.last_schedule_dev if dl.last_schedule_private  # a per-call copy
@@ -418,59 +627,133 @@ def trace_pupil(plan: int, px: torch.Tensor, py: torch.Tensor, params: list[torc
         sched_t = torch.empty(0, dtype=torch.int32, device=dl.device)
     else:
         sched_t = dl.resident("sched", sched.reshape(-1)).clone()
-    return (*(getattr(out, a) for a in _abi.RAY_FIELDS), sched_t)
+    return (*(getattr(out, a) for a in _abi.RAY_FIELDS), sched_t, tape)
+
+
+@trace_pupil.register_kernel("cpu")
+def _trace_pupil_cpu(lens, lens_meta, final_thickness, lens_key, seg, apod, px, py, params,
+                     spec, plan_meta, plan_key):
+    """The CPU dispatch key: rays generated and traced by the host build (host.py), the
+    Newton stop rule evaluated exactly per (field, wavelength) group; no tape (the host
+    backward re-traces)."""
+    from . import host
+
+    hl = _resolve(lens, lens_meta, final_thickness, lens_key)
+    n, seg_len, ppr, _, _ = plan_meta
+    outs, updates = host.trace_pupil(hl, seg, px.detach().contiguous(), py.detach().contiguous(),
+                                     n, seg_len, bool(ppr), apod)
+    sched = updates if hl.newton else torch.empty(0, dtype=torch.int32)
+    return (*outs, sched, torch.empty(0, dtype=torch.float64))
 
 
 @trace_pupil.register_fake
-def _(plan, px, py, params, spec):
-    p = _lookup(plan)
-    ref = px
-    outs = [ref.new_empty(p.n, dtype=torch.float64) for _ in range(8)]
-    ns = p.dlens.table.n_surfaces if p.dlens.newton else 0
-    return (*outs, ref.new_empty(ns, dtype=torch.int32))
+def _(lens, lens_meta, final_thickness, lens_key, seg, apod, px, py, params, spec, plan_meta,
+      plan_key):
+    n, seg_len, _, _, want_tape = plan_meta
+    outs = [px.new_empty(n, dtype=torch.float64) for _ in range(8)]
+    S = lens_meta[0]
+    ns = S if lens_meta[8] else 0  # one Newton group per call (group_len = n)
+    nt = S * 11 * n if (want_tape and px.device.type != "cpu") else 0  # kTapeRows = 11
+    return (*outs, px.new_empty(ns, dtype=torch.int32), px.new_empty(nt, dtype=torch.float64))
 
 
 def _pupil_setup(ctx, inputs, output):
-    plan, px, py, params, spec = inputs
-    ctx.plan = _lookup(plan)
+    lens, meta, ft, key, seg, apod, px, py, params, spec, plan_meta, plan_key = inputs
+    ctx.lens_meta, ctx.final_thickness, ctx.lens_key = list(meta), float(ft), int(key)
+    ctx.plan_meta, ctx.plan_key = list(plan_meta), int(plan_key)
+    ctx.n_lens = len(lens)
     ctx.pairs = _spec_pairs(spec)
     ctx.n_spec = len(spec)
     ctx.shapes = [(p.shape, p.dtype, p.device) for p in params]
+    ctx.has_apod = apod is not None
     ctx.set_materialize_grads(False)
-    ctx.save_for_backward(output[8], *output[:8])
+    saved = [*lens, seg, px.detach(), py.detach(), output[8], output[9], *output[:8]]
+    if apod is not None:
+        saved.append(apod)
+    ctx.save_for_backward(*saved)
 
 
 def _pupil_backward(ctx, *grads):
-    from .autodiff import vjp
-
-    sched, *primal = ctx.saved_tensors
-    p = ctx.plan
-    dl = p.dlens
+    saved = ctx.saved_tensors
+    nl = ctx.n_lens
+    lens = list(saved[:nl])
+    seg, px, py, sched, tape = saved[nl:nl + 5]
+    primal = list(saved[nl + 5:nl + 13])
+    apod = saved[nl + 13] if ctx.has_apod else None
     none_spec = [] if ctx.n_spec == 0 else None  # see _seq_backward
-    if not any(ctx.needs_input_grad[3]) or not ctx.shapes:
-        return None, None, None, [None] * len(ctx.shapes), none_spec
+    nothing = ([None] * ctx.n_lens, None, None, None, None, None, None, None)
+    if not any(ctx.needs_input_grad[8]) or not ctx.shapes:
+        return (*nothing, [None] * len(ctx.shapes), none_spec, None, None)
+    dl = _resolve(lens, ctx.lens_meta, ctx.final_thickness, ctx.lens_key)
     _check_differentiable(dl.table)
     params_like = [torch.empty(s, dtype=d, device="meta") for s, d, _ in ctx.shapes]
     zp, st, ft, n_param = tangent_tables(dl.table, ctx.pairs, params_like)
-    tables = tuple(None if a is None else dl.resident(("tangent", i), a)
-                   for i, a in enumerate((zp, st, ft)))
-    tables = (*tables, dl.resident("tangent_need", slot_need(dl.table, zp, st, ft)))
-    g = torch.empty(n_param, dtype=torch.float64, device=dl.device)  # overwritten
+    from .autodiff import vjp_mode
+
+    mode = vjp_mode(dl.table)
+    tabs = _tables_cpu(zp, st, ft, slot_need(dl.table, zp, st, ft))
     cot = [None if gr is None else gr.to(torch.float64).contiguous() for gr in grads[:8]]
-    vjp(dl, p.seg_dev, p.px, p.py, p.n, p.seg_len, sched if sched.numel() else None, tables,
-        n_param, cot, g, pupil_per_ray=p.pupil_per_ray,
-        tape=p.tape, primal=primal if p.tape is not None else None, overwrite=True)
-    p.tape = None  # one backward per forward: release the tape
+    g = torch.ops.ort.trace_pupil_vjp(lens, ctx.lens_meta, ctx.final_thickness, ctx.lens_key,
+                                      seg, apod, px, py, sched, tape, primal, cot, tabs,
+                                      n_param, int(mode), ctx.plan_meta)
     res = []
     off = 0
     for shape, dtype, pdev in ctx.shapes:
         k = int(np.prod(shape)) if len(shape) else 1
         res.append(g[off:off + k].reshape(shape).to(device=pdev, dtype=dtype))
         off += k
-    return None, None, None, res, none_spec
+    return (*nothing, res, none_spec, None, None)
 
 
 trace_pupil.register_autograd(_pupil_backward, setup_context=_pupil_setup)
+
+
+@torch.library.custom_op("ort::trace_pupil_vjp", mutates_args=(), device_types="cuda")
+def trace_pupil_vjp(lens: list[torch.Tensor], lens_meta: list[int], final_thickness: float,
+                    lens_key: int, seg: torch.Tensor, apod: torch.Tensor | None,
+                    px: torch.Tensor, py: torch.Tensor, sched: torch.Tensor, tape: torch.Tensor,
+                    primal: list[torch.Tensor], cot: list[torch.Tensor | None],
+                    tables: list[torch.Tensor | None], n_param: int, mode: int,
+                    plan_meta: list[int]) -> torch.Tensor:
+    """ort_trace_pupil_vjp: grad [n_param] = J^T cot (the reverse sweep over `tape` when the
+    forward wrote one, else with its own re-trace)."""
+    from .autodiff import vjp
+
+    dl = _resolve(lens, lens_meta, final_thickness, lens_key)
+    n, seg_len, ppr, _, _ = plan_meta
+    dev = dl.device
+    tabs = tuple(None if t is None else dl.resident(("tangent", i), t.detach().cpu().numpy())
+                 for i, t in enumerate(tables))
+    g = torch.empty(max(1, n_param), dtype=torch.float64, device=dev)  # overwritten
+    cot = [None if c is None else c.detach().to(device=dev, dtype=torch.float64).contiguous()
+           for c in cot]
+    taped = tape.numel() > 0 and mode == _abi.VJP_ADJOINT
+    vjp(dl, seg, px, py, n, seg_len, sched if sched.numel() else None, tabs, n_param, cot, g,
+        pupil_per_ray=bool(ppr), mode=mode, tape=tape if taped else None,
+        primal=primal if taped else None, overwrite=True)
+    return g
+
+
+@trace_pupil_vjp.register_kernel("cpu")
+def _trace_pupil_vjp_cpu(lens, lens_meta, final_thickness, lens_key, seg, apod, px, py, sched,
+                         tape, primal, cot, tables, n_param, mode, plan_meta):
+    from . import host
+
+    hl = _resolve(lens, lens_meta, final_thickness, lens_key)
+    n, seg_len, ppr, _, _ = plan_meta
+    zp, st, ft, need = (None if t is None else t.detach().contiguous() for t in tables)
+    g = torch.empty(max(1, n_param), dtype=torch.float64)
+    cot = [None if c is None else c.detach().to(torch.float64).contiguous() for c in cot]
+    host.trace_pupil_vjp(hl, seg, px.detach().contiguous(), py.detach().contiguous(), n,
+                         seg_len, bool(ppr), sched, (zp, st, ft),
+                         need if mode == _abi.VJP_ADJOINT else None, n_param, mode, cot, g, apod)
+    return g
+
+
+@trace_pupil_vjp.register_fake
+def _(lens, lens_meta, final_thickness, lens_key, seg, apod, px, py, sched, tape, primal, cot,
+      tables, n_param, mode, plan_meta):
+    return px.new_empty(max(1, n_param), dtype=torch.float64)
 
 
 # --------------------------------------------------------------------------------------
@@ -516,6 +799,15 @@ def rms_spot(x: torch.Tensor, y: torch.Tensor) -> tuple[torch.Tensor, torch.Tens
     return rms, stats
 
 
+@rms_spot.register_kernel("cpu")
+def _rms_spot_cpu(x, y):
+    """The CPU dispatch key: the same formula in the host library (sums in index order)."""
+    from . import host
+
+    _check_rms_inputs(x, y)
+    return host.rms_spot(x.detach().reshape(-1).contiguous(), y.detach().reshape(-1).contiguous())
+
+
 def _check_rms_inputs(x, y):
     """The kernels read x and y as n doubles each on one device: refuse anything else
     (a shorter y would be read past its end, a float32 record read as doubles)."""
@@ -544,20 +836,43 @@ def _rms_setup(ctx, inputs, output):
 
 
 def _rms_backward(ctx, g_rms, g_stats):
-    from .raytrace import _ptr, _stream_handle
-
     if g_rms is None:
         return None, None
     x, y, stats = ctx.saved_tensors
-    xf = x.reshape(-1).contiguous()
-    yf = y.reshape(-1).contiguous()
-    g = g_rms.detach().to(torch.float64).contiguous()
-    gx = torch.empty_like(xf)
-    gy = torch.empty_like(yf)
-    rc = _native.load().ort_rms_spot_vjp(_ptr(xf), _ptr(yf), xf.numel(), _ptr(stats), _ptr(g),
-                                         _ptr(gx), _ptr(gy), _stream_handle())
-    _native.check(rc, "ort_rms_spot_vjp")
+    gx, gy = torch.ops.ort.rms_spot_vjp(x, y, stats, g_rms.detach().to(torch.float64))
     return gx.reshape(ctx.shapes[0]), gy.reshape(ctx.shapes[1])
 
 
 rms_spot.register_autograd(_rms_backward, setup_context=_rms_setup)
+
+
+@torch.library.custom_op("ort::rms_spot_vjp", mutates_args=(), device_types="cuda")
+def rms_spot_vjp(x: torch.Tensor, y: torch.Tensor, stats: torch.Tensor,
+                 g: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """ort_rms_spot_vjp: g (x - mean x, y - mean y) / (n rms) (one kernel)."""
+    from .raytrace import _ptr, _stream_handle
+
+    xf = x.detach().reshape(-1).contiguous()
+    yf = y.detach().reshape(-1).contiguous()
+    gg = g.detach().to(torch.float64).contiguous()
+    gx = torch.empty_like(xf)
+    gy = torch.empty_like(yf)
+    rc = _native.load().ort_rms_spot_vjp(_ptr(xf), _ptr(yf), xf.numel(), _ptr(stats), _ptr(gg),
+                                         _ptr(gx), _ptr(gy), _stream_handle())
+    _native.check(rc, "ort_rms_spot_vjp")
+    return gx, gy
+
+
+@rms_spot_vjp.register_kernel("cpu")
+def _rms_spot_vjp_cpu(x, y, stats, g):
+    from . import host
+
+    return host.rms_spot_vjp(x.detach().reshape(-1).contiguous(), y.detach().reshape(-1)
+                             .contiguous(), stats.contiguous(), g.detach().to(torch.float64)
+                             .reshape(1).contiguous())
+
+
+@rms_spot_vjp.register_fake
+def _(x, y, stats, g):
+    return (x.new_empty(x.numel(), dtype=torch.float64),
+            y.new_empty(y.numel(), dtype=torch.float64))

@@ -168,6 +168,13 @@ class DeviceLens:
         if table.device_coeffs:  # coefficients held in HBM: into the table and its blocks
             self.patch_coefficients(table.device_coeffs)
 
+    def lens_tensors(self):
+        """[surfaces, cs_ops, coef, zern, n_tab, alpha_tab, optics, materials, wavelengths]:
+        the uploaded tables (structured ones as bytes) -- the lens as the torch ops take it
+        (ops.lens_args)."""
+        return [self.surfaces, self.cs_ops, self.coef, self.zern, self.n_tab.reshape(-1),
+                self.alpha_tab.reshape(-1), self.optics, self.mats, self.lambdas]
+
     def resident(self, slot, arr):
         """A read-only HBM copy of a small host array, reused while its bytes are
         unchanged: segment descriptors, Newton schedules and tangent tables are the same

@@ -1,7 +1,12 @@
-"""Multi-process (gloo, world_size 2, CPU) tests of the sharding and the consumer
-collectives (optiland_pr_amd/distributed.py). The trace itself needs the GPU; here the
-per-rank "image-plane rays" are synthetic, so only the data movement and the reductions
-are under test."""
+"""Multi-process (gloo, CPU) tests of the sharding and the consumer collectives
+(optiland_pr_amd/distributed.py) at world sizes 2, 3 and 8 -- 8 is the driver's scaling
+run (one rank per GPU of a node); 101 pupil samples per pair make every shard layout
+uneven (101 = 34 + 34 + 33; 5 x 13 + 3 x 12), so the padded slabs, the shorter shards'
+tails and seven concurrent receives into rank 0 are exercised before any 8-GPU run. The
+trace itself needs the GPU; here the per-rank "image-plane rays" are synthetic, so only
+the data movement and the reductions are under test."""
+
+import pytest
 
 import os
 import socket
@@ -49,28 +54,38 @@ def _spot_reference(x, y, i):
     return rms, geo
 
 
-def test_gloo_world2_gather_and_stats(tmp_path):
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_gloo_gather_and_stats(tmp_path, world):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
                OMP_NUM_THREADS="1")
-    outs = [tmp_path / f"r{r}.npz" for r in range(2)]
+    outs = [tmp_path / f"r{r}.npz" for r in range(world)]
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dist_worker_gloo.py"),
-                               str(r), "2", str(outs[r])], env=env) for r in range(2)]
-    for p in procs:
-        assert p.wait(timeout=120) == 0
+                               str(r), str(world), str(outs[r])], env=env)
+             for r in range(world)]
+    try:
+        for p in procs:
+            assert p.wait(timeout=300) == 0
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
     x, y, i = full_rays()
-    r0, r1 = np.load(outs[0]), np.load(outs[1])
+    rs = [np.load(o) for o in outs]
+    r0 = rs[0]
     for rep in range(2):  # gathered into rank 0 only, reassembled in the reference order
         np.testing.assert_array_equal(r0[f"X{rep}"], x.reshape(-1))
         np.testing.assert_array_equal(r0[f"Y{rep}"], y.reshape(-1))
     # pipelined: chunks of pairs gathered asynchronously, finished chunk by chunk
     np.testing.assert_array_equal(r0["Xc"], x.reshape(-1))
     np.testing.assert_array_equal(r0["Yc"], y.reshape(-1))
-    assert "X0" not in r1.files
-    loc = -(-N_P // 2)  # the padded slab: fields x pairs x ceil(n_p / world) doubles
-    assert int(r1["sent"]) == 2 * N_FIELDS * N_WL * loc * 8 and int(r1["received"]) == 0
-    assert int(r0["received"]) == int(r1["sent"]) and int(r0["sent"]) == 0
+    loc = -(-N_P // world)  # the padded slab: fields x pairs x ceil(n_p / world) doubles
+    for r in rs[1:]:
+        assert "X0" not in r.files
+        assert int(r["sent"]) == 2 * N_FIELDS * N_WL * loc * 8 and int(r["received"]) == 0
+    # rank 0 receives world - 1 slabs (the seven concurrent receives at world 8)
+    assert int(r0["received"]) == (world - 1) * int(rs[1]["sent"]) and int(r0["sent"]) == 0
     rms, geo = _spot_reference(x, y, i)
-    for r in (r0, r1):
+    for r in rs:
         np.testing.assert_array_equal(r["rows"], r0["rows"])  # every rank: the same bits
         np.testing.assert_allclose(r["rms"], rms, rtol=1e-13)
         np.testing.assert_allclose(r["geo"], geo, rtol=1e-15)

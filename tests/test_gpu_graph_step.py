@@ -4,6 +4,8 @@ capturable Adam -- bench.py config 5's step) against the same step run eagerly: 
 same losses and the same coefficient trajectory, bit for bit (every kernel on the path
 is deterministic, so a replay computes exactly what the eager launches compute)."""
 
+import warnings
+
 import numpy as np
 import pytest
 
@@ -59,8 +61,15 @@ def test_captured_step_equals_eager_steps(torch):
     # the captured run: 3 eager warm-up steps (inside the first call), then one replay per
     # call; the eager run: the same number of eager steps
     losses_g = []
-    for _ in range(steps):
-        losses_g.append(float(step_g()))  # (a synchronising read per step: test only)
+    with warnings.catch_warnings(record=True) as caught:
+        warnings.simplefilter("always")
+        for _ in range(steps):
+            losses_g.append(float(step_g()))  # (a synchronising read per step: test only)
+    # the captured backward must not reuse the warm-up's AccumulateGrad nodes (a stream
+    # mismatch inside the capture)
+    stream_warnings = [str(w.message) for w in caught if "AccumulateGrad" in str(w.message)
+                       or "stream does not match" in str(w.message)]
+    assert not stream_warnings, stream_warnings
     step_g.check()
     losses_e = []
     for k in range(3 + steps):
