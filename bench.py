@@ -349,36 +349,53 @@ def config5(args, dev, rank, world, torch):
 
     R = args.rays
     _, _, d = _pupil(rank, R, dev, torch)
-    lens = ThreeMirrorAnastigmat()
-    # Newton schedules verified on the device once warm (ort_newton_fixup): the same
-    # schedules and results as the host check, without its per-step host round trip;
-    # range errors / unsettled schedules surface at raytrace.check_all_pending (below)
-    lens.newton_mode = "device"
-    leaves = []
-    for si in (1, 2, 3):
-        g = lens.surface_group.surfaces[si].geometry
-        # device-resident parameters: the uploaded lens table is patched on the device,
-        # the gradient and the Adam state stay in HBM (no per-step host round trip)
-        t = torch.tensor(np.asarray(g.coefficients), dtype=torch.float64, device=dev,
-                         requires_grad=True)
-        g.coefficients = t
-        leaves.append(t)
-    # one fused Adam kernel for the 30 coefficients (instead of the foreach sequence);
-    # capturable: its step count lives on the device, so the step can be a graph replay
     use_graph = not args.eager
-    opt = torch.optim.Adam(leaves, lr=1e-7, fused=True, capturable=use_graph)
     S = 4
+
+    def problem(capturable):
+        """The TMA with device-resident coefficient leaves, its Adam and loss."""
+        lens = ThreeMirrorAnastigmat()
+        # Newton schedules verified on the device once warm (ort_newton_fixup): the same
+        # schedules and results as the host check, without its per-step host round trip;
+        # range errors / unsettled schedules surface at raytrace.check_all_pending (below)
+        lens.newton_mode = "device"
+        leaves = []
+        for si in (1, 2, 3):
+            g = lens.surface_group.surfaces[si].geometry
+            # device-resident parameters: the uploaded lens table is patched on the device,
+            # the gradient and the Adam state stay in HBM (no per-step host round trip)
+            t = torch.tensor(np.asarray(g.coefficients), dtype=torch.float64, device=dev,
+                             requires_grad=True)
+            g.coefficients = t
+            leaves.append(t)
+        # one fused Adam kernel for the 30 coefficients (instead of the foreach sequence);
+        # capturable: its step count lives on the device, so the step can be a graph replay
+        opt = torch.optim.Adam(leaves, lr=1e-7, fused=True, capturable=capturable)
+
+        def loss_fn():
+            return RayOperand.rms_spot_size(lens, -1, 0.0, 1.0, R, 0.587, d)
+
+        return lens, opt, loss_fn
+
+    lens, opt, loss_fn = problem(use_graph)
     state = {}
 
-    def eager_step():
-        opt.zero_grad()
-        loss = loss_fn()
-        loss.backward()
-        opt.step()
-        state["loss"] = loss.detach()  # read once after the timed region (no per-step sync)
+    def eager_step_of(opt, loss_fn, keep):
+        def step():
+            opt.zero_grad()
+            loss = loss_fn()
+            loss.backward()
+            opt.step()
+            if keep:
+                state["loss"] = loss.detach()  # read once after the timed region
+        return step
 
-    def loss_fn():
-        return RayOperand.rms_spot_size(lens, -1, 0.0, 1.0, R, 0.587, d)
+    eager_step = eager_step_of(opt, loss_fn, True)
+    # the backward's device time (vjp_timer) is measured on eager steps of a SECOND copy of
+    # the problem: eager steps of the captured lens itself would overwrite the replays'
+    # Newton flags and reuse the autograd nodes the capture's outputs keep alive
+    _, opt_t, loss_t = problem(False) if use_graph else (lens, opt, loss_fn)
+    timer_step = eager_step_of(opt_t, loss_t, False) if use_graph else eager_step
 
     # the whole optimisation step -- coefficient patch, taped trace with its device-verified
     # Newton rounds, rms_spot, the adjoint VJP, the fused Adam update -- as ONE HIP graph
@@ -409,7 +426,7 @@ def config5(args, dev, rank, world, torch):
                               if use_graph else "eager (torch ops + ctypes launches)"},
         kernel="adj_kernel<KM_ZERN, 2> (ort_trace_pupil_vjp, adjoint mode)", launches=None,
         bytes_per_launch=None, flops_per_ray=None, pmc_file="hbm_traffic_c5.json", rays=R,
-        state=state, vjp_timer=vjp_timer, eager_step=eager_step, ramp_steps=720,
+        state=state, vjp_timer=vjp_timer, eager_step=timer_step, ramp_steps=720,
         # the taped forward writes the tape, the adjoint only reads it: per traced surface the
         # incoming ray and t (7 rows) plus, for a Newton surface, the min(U, 4) iterates it
         # replays (ort_sweep.h adj_ray), with U the verified schedule -- read after the run

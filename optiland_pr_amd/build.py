@@ -108,20 +108,37 @@ def build(force=False, verbose=False, out=None, extra_flags=(), jobs=None):
     jobs = jobs or min(len(SOURCES), max(1, os.cpu_count() or 1), 16)
     pending = list(SOURCES)
     failed = None
+    # a translation unit is recompiled when it or a header is newer than its object, or when
+    # the flags changed (force: every unit)
+    flag_file = os.path.join(obj_dir, "flags.txt")
+    flags_now = " ".join([*HIPCC_FLAGS, *extra_flags])
+    same_flags = os.path.exists(flag_file) and open(flag_file).read() == flags_now
+    newest_hdr = max(os.path.getmtime(h) for h in HEADERS)
+
+    def fresh(src, obj):
+        return (not force and same_flags and os.path.exists(obj)
+                and os.path.getmtime(obj) > max(os.path.getmtime(src), newest_hdr))
+
     while pending or procs:
         while pending and len(procs) < jobs:
             src = pending.pop(0)
             obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
             objs.append(obj)
+            if fresh(src, obj):
+                continue
             cmd = [cc, *HIPCC_FLAGS, *extra_flags, *inc, "-c", "-o", obj, src]
             if verbose:
                 print(" ".join(cmd), file=sys.stderr)
             procs.append((subprocess.Popen(cmd), src))
+        if not procs:
+            continue
         p, src = procs.pop(0)
         if p.wait() != 0:
             failed = src
     if failed:
         raise subprocess.CalledProcessError(1, f"hipcc {failed}")
+    with open(flag_file, "w") as f:
+        f.write(flags_now)
     tmp = out + ".tmp"
     cmd = [cc, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", tmp, *objs]
     if verbose:

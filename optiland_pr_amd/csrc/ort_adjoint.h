@@ -5,8 +5,8 @@
 // shared with the host build (ort_host.cpp). This file holds its GPU side: one ray per
 // lane, each parameter-slot contribution summed over the wave into partial[slot][wave]
 // (every needed (slot, wave) entry written by the launch: no memset), then
-// adj_param_reduce_kernel sums, per parameter, the waves of its slots in a fixed order
-// (deterministic) weighted by the tangent tables.
+// adj_slot_reduce_kernel / adj_grad_kernel sum each slot's partials, then per parameter the
+// slot sums weighted by the tangent tables, in fixed orders (deterministic).
 #pragma once
 
 #include "ort_kernels.h"  // (and ort_sweep.h: adj_ray, AArgs)

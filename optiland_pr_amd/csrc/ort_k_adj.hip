@@ -17,54 +17,60 @@ __global__ void adj_need_kernel(const AArgs j0, int32_t* need) {
   need[slot] = nd;
 }
 
-// One block per PARAMETER: grad[p] += sum over the slots p depends on of
-// d slot / d p * (the slot's wave partials summed in index order) -- the reduction and
-// the contraction with the tangent tables in one launch, deterministic (a fixed order,
-// no atomics; a slot shared by several parameters is summed once per parameter). The
-// slot weights are read by all threads at once (256 slots per pass into LDS) rather than
-// one dependent table load per slot, and each thread's strided partial loads are issued
-// eight at a time ahead of their (in-order) additions: 27 -> see DESIGN for the TMA's 43
-// slots x 30 parameters.
-__global__ __launch_bounds__(kBlock) void adj_param_reduce_kernel(const AArgs j0) {
+// The parameter reduction in two launches (round 5: with the monomial-basis slots a
+// parameter depends on a few dozen slots, and one block per parameter re-reading every
+// slot's partials cost 46 us per launch for the TMA's 30 parameters x 30 slots each):
+//   adj_slot_reduce_kernel  one block per SLOT: slot_sum[slot] = its per-block partials
+//                           summed in index order (each partial read once);
+//   adj_grad_kernel         one block per PARAMETER: grad[p] (+)= sum over the slots of
+//                           d slot / d p * slot_sum[slot], slots in index order.
+// Deterministic (fixed orders, no atomics). The slot weights come from the tangent tables
+// and, for the monomial slots, the lens's term matrices (slot_weight / mono_weight).
+__global__ __launch_bounds__(kBlock) void adj_slot_reduce_kernel(const AArgs j) {
+  const int slot = blockIdx.x;
+  __shared__ double ws[kBlock / 64];
+  if (!cst(j.need)[slot]) {  // uniform: the launch did not sum this slot
+    if (threadIdx.x == 0) j.slot_sum[slot] = 0.0;
+    return;
+  }
+  const double* src = j.partial + (int64_t)slot * j.n_wave;
+  double v = 0.0;
+  int64_t k = threadIdx.x;
+  for (; k + 7 * kBlock < j.n_wave; k += 8 * kBlock) {
+    double x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) x[u] = src[k + u * kBlock];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v += x[u];
+  }
+  for (; k < j.n_wave; k += kBlock) v += src[k];
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double sum = 0.0;
+    for (int q = 0; q < kBlock / 64; ++q) sum += ws[q];
+    j.slot_sum[slot] = sum;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void adj_grad_kernel(const AArgs j0) {
   const int p = blockIdx.x;
   AArgs j = j0;
   j.mono_on = mono_enabled(j0);
   __shared__ double ws[kBlock / 64];
-  __shared__ double wt[kBlock];
-  double g = 0.0;  // meaningful in thread 0
-  for (int base = 0; base < j.n_slot; base += kBlock) {
-    const int my = base + threadIdx.x;
-    __syncthreads();  // the previous pass's wt reads are done
-    // (a slot the launch did not sum -- need == 0 -- has no partials to read)
-    wt[threadIdx.x] = (my < j.n_slot && cst(j.need)[my]) ? slot_weight(j, my, p) : 0.0;
-    __syncthreads();
-    const int end = min(kBlock, j.n_slot - base);
-    for (int c = 0; c < end; ++c) {
-      const double w = wt[c];  // uniform
-      if (w == 0.0) continue;
-      const double* src = j.partial + (int64_t)(base + c) * j.n_wave;
-      double v = 0.0;
-      int64_t k = threadIdx.x;
-      for (; k + 7 * kBlock < j.n_wave; k += 8 * kBlock) {
-        double x[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) x[u] = src[k + u * kBlock];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) v += x[u];
-      }
-      for (; k < j.n_wave; k += kBlock) v += src[k];
-      v = wave_sum(v);
-      if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = v;
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        double s = 0.0;
-        for (int q = 0; q < kBlock / 64; ++q) s += ws[q];
-        g += s * w;
-      }
-      __syncthreads();
-    }
+  double v = 0.0;
+  for (int slot = threadIdx.x; slot < j.n_slot; slot += kBlock) {
+    if (!cst(j.need)[slot]) continue;
+    const double w = slot_weight(j, slot, p);
+    if (w != 0.0) v += w * j.slot_sum[slot];
   }
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = v;
+  __syncthreads();
   if (threadIdx.x == 0) {
+    double g = 0.0;
+    for (int q = 0; q < kBlock / 64; ++q) g += ws[q];
     if (j.grad_store)
       j.grad[p] = g;
     else
@@ -87,9 +93,11 @@ int adj_run(const KArgs& a, AArgs j, int32_t* need_ws, int tangents, uint32_t km
     j.need = need_ws;
   }
   hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(kBlock), 0, stream, a, j);
-  if (j.n_param > 0)
-    hipLaunchKernelGGL(adj_param_reduce_kernel, dim3((unsigned)j.n_param), dim3(kBlock), 0,
+  if (j.n_param > 0) {
+    hipLaunchKernelGGL(adj_slot_reduce_kernel, dim3((unsigned)j.n_slot), dim3(kBlock), 0,
                        stream, j);
+    hipLaunchKernelGGL(adj_grad_kernel, dim3((unsigned)j.n_param), dim3(kBlock), 0, stream, j);
+  }
   return hipGetLastError() == hipSuccess ? ORT_OK : ORT_ERR_LAUNCH;
 }
 
