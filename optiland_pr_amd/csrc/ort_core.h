@@ -613,28 +613,64 @@ ORT_INLINE T ipow(const T& x, int p) {
 // sag alone (the convergence check after the last update).
 
 // even_asphere.py:82-98 (sag) + :100-129 (normal)
+// The even asphere's term sums by Horner in r^2 (round 5):
+//   P = C0 + r2 (C1 + r2 (C2 + ...)),  z = conic + r2 P
+//   D = 2 C0 + r2 (4 C1 + r2 (6 C2 + ...)),  dz/dx = x / (R q) + x D  (dz/dy likewise)
+// The reference adds C_i * r2 ** (i + 1) term by term through libm pow (even_asphere.py:
+// 95-96, 119-121); this build already formed the powers as products (not the reference's
+// bits), and Newton surfaces are held to 1e-9 mm with the reference's update counts, not to
+// bit-exactness. Horner takes 2 operations per term for the sag and 3 for both slopes
+// (was 3 and 9). The common term counts are unrolled at compile time (the coefficients'
+// scalar loads issued together instead of one dependent load per loop trip).
+template <int NC, class T, class PD>
+ORT_INLINE void even_horner_n(const T& r2, PD C, T& P, T& D) {
+  P = T(C[NC - 1]);
+  D = T(2.0 * (double)NC * C[NC - 1]);
+#pragma unroll
+  for (int i = NC - 2; i >= 0; --i) {
+    P = P * r2 + C[i];
+    D = D * r2 + 2.0 * (double)(i + 1) * C[i];
+  }
+}
+
+template <class T, class PD>
+ORT_INLINE void even_horner(const T& r2, PD C, int nc, T& P, T& D) {
+  switch (nc) {
+    case 1: return even_horner_n<1>(r2, C, P, D);
+    case 2: return even_horner_n<2>(r2, C, P, D);
+    case 3: return even_horner_n<3>(r2, C, P, D);
+    case 4: return even_horner_n<4>(r2, C, P, D);
+    case 5: return even_horner_n<5>(r2, C, P, D);
+    case 6: return even_horner_n<6>(r2, C, P, D);
+    default: break;
+  }
+  if (nc <= 0) {
+    P = T(0.0);
+    D = T(0.0);
+    return;
+  }
+  P = T(C[nc - 1]);
+  D = T(2.0 * (double)nc * C[nc - 1]);
+  for (int i = nc - 2; i >= 0; --i) {
+    P = P * r2 + C[i];
+    D = D * r2 + 2.0 * (double)(i + 1) * C[i];
+  }
+}
+
 template <class T, class S, class PD>
 ORT_INLINE T sagnorm_even(const T& x, const T& y, const S& R, const S& k, PD C, int nc,
                           bool want_normal, T& nx, T& ny, T& nz) {
   const T r2 = x * x + y * y;
   const T q = sqrt(1.0 - (1.0 + k) * r2 / (R * R));
-  T z = r2 / (R * (1.0 + q));
-  T rp = r2;  // r2 ** (i + 1)
-  for (int i = 0; i < nc; ++i) {
-    z = z + C[i] * rp;
-    rp = rp * r2;
-  }
+  T P, D;
+  even_horner(r2, C, nc, P, D);
+  const T z = r2 / (R * (1.0 + q)) + r2 * P;
   if (want_normal) {
     const T denom = R * q;
     T dfdx, dfdy;
     div2(x, y, denom, dfdx, dfdy);
-    T rq = T(1.0);  // r2 ** i
-    for (int i = 0; i < nc; ++i) {
-      const double f = 2.0 * (double)(i + 1);
-      dfdx = dfdx + f * x * C[i] * rq;
-      dfdy = dfdy + f * y * C[i] * rq;
-      rq = rq * r2;
-    }
+    dfdx = dfdx + x * D;
+    dfdy = dfdy + y * D;
     const T mag = sqrt(dfdx * dfdx + dfdy * dfdy + 1.0);
     unit_normal3(dfdx, dfdy, mag, nx, ny, nz);
   }

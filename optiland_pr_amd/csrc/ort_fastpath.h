@@ -381,23 +381,15 @@ ORT_INLINE double sagnorm_even(double x, double y, const ort_surface& s, PD C,
   const double q = sqrt(1.0 - quot_pos(a, rr), bad);
   const SharedDiv dz = shared_div(R * (1.0 + q), bad);
   ORT_CHK(bad, !num_ok0(r2));
-  double z = quot_signed(r2, dz);
-  double rp = r2;  // r2 ** (i + 1)
-  for (int i = 0; i < nc; ++i) {
-    z = z + C[i] * rp;
-    rp = rp * r2;
-  }
+  double P, D;  // the term sums by Horner in r2 (ort_core.h even_horner)
+  ort::even_horner(r2, C, nc, P, D);
+  const double z = quot_signed(r2, dz) + r2 * P;
   const SharedDiv dd = shared_div(R * q, bad);
   ORT_CHK(bad, !(num_ok0(x) && num_ok0(y)));
   double dfdx = quot_signed(x, dd);
   double dfdy = quot_signed(y, dd);
-  double rq = 1.0;  // r2 ** i
-  for (int i = 0; i < nc; ++i) {
-    const double f = 2.0 * (double)(i + 1);
-    dfdx = dfdx + f * x * C[i] * rq;
-    dfdy = dfdy + f * y * C[i] * rq;
-    rq = rq * r2;
-  }
+  dfdx = dfdx + x * D;
+  dfdy = dfdy + y * D;
   const double mag = sqrt_ge1(dfdx * dfdx + dfdy * dfdy + 1.0, bad);
   const SharedDiv dm = shared_div_ge1(mag, bad);
   ORT_CHK(bad, !(num_ok0(dfdx) && num_ok0(dfdy)));

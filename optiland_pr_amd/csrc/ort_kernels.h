@@ -412,7 +412,10 @@ __device__ inline void interact(const KArgs& a, const ort_surface& s, ort::Ray& 
 // measured here, the compiler's choice for the others. The taped Zernike forward (config
 // 5): 5 waves (96 VGPRs, 96 B of scratch) vs 4 (123 VGPRs) after the non-temporal tape
 // stores, config 5 step 0.689 / 0.679 vs 0.692 / 0.694 ms (A/B, r04_ab_occupancy_c5.log;
-// the adjoint at 4 waves instead of 3 measured 540 vs 417 us there).
+// the adjoint at 4 waves instead of 3 measured 540 vs 417 us there). Round 5, with the
+// degree-specialised Horner schemes: 4 waves (123 VGPRs, no scratch) 0.5259 / 0.5267 ms,
+// 5 waves (96 VGPRs, 100 B of scratch) 0.5275 / 0.5227, 6 waves (80, 164 B) 0.567 / 0.593
+// (profiles/r05_ab_fwd_occupancy.log): 4 waves, the same time without the spill traffic.
 template <uint32_t FEAT>
 constexpr bool kNewtonFast =
 #ifdef ORT_NO_NEWTON_FAST
@@ -426,7 +429,7 @@ template <uint32_t FEAT>
 struct TraceWaves {
   static constexpr int value =
       ((FEAT & ort::KM_ZERN) != 0 && (FEAT & (ort::KM_FREE | F_IA)) == 0)
-          ? ((FEAT & F_TAPE) != 0 ? 5 : 6)
+          ? ((FEAT & F_TAPE) != 0 ? 4 : 6)
           : ((kNewtonFast<FEAT> && (FEAT & F_MONO) != 0) ? 6 : 1);
 };
 #ifdef ORT_TRACE_WAVES

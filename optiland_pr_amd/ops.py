@@ -271,10 +271,25 @@ def _table_from_tensors(lens, meta, final_thickness):
         n_rec=int(meta[7]), rec_surfaces=rec)
 
 
+def _has_data(t):
+    """False for tensors without storage (fake / functional tensors while tracing)."""
+    try:
+        t.data_ptr()
+        return True
+    except RuntimeError:
+        return False
+
+
 def _resolve(lens, meta, final_thickness, key):
     """The DeviceLens / HostLens these tensors are: the object named by `key` when it holds
-    exactly these tables, else one rebuilt from the tensors (cached by their addresses)."""
+    exactly these tables, else one rebuilt from the tensors (cached by their addresses).
+    While tracing (fake tensors: no data to compare or rebuild from), the object the key
+    names -- the backward formulas only read its host-side tables."""
     obj = _HANDLES.get(int(key))
+    if not _has_data(lens[0]):
+        if obj is None or not hasattr(obj, "lens_tensors"):
+            raise RuntimeError("ort op traced with a lens key that names no live lens")
+        return obj
     if obj is not None and hasattr(obj, "lens_tensors"):
         mine = obj.lens_tensors()
         if all(a.data_ptr() == b.data_ptr() and a.device == b.device

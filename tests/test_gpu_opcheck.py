@@ -1,0 +1,121 @@
+"""torch.library.opcheck of the custom ops on the CUDA (HIP) key (tests/test_ops_opcheck.py
+runs the CPU key): schema, fake tensors against the HIP kernels' real outputs, autograd
+registration and AOT dispatch (the backward through ort::trace_*_vjp / ort::rms_spot_vjp),
+plus torch.compile(fullgraph=True) of a trace on the device."""
+
+import numpy as np
+import pytest
+
+from tests.test_ops_opcheck import FIELDS, _traced
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need the MI355X (torch.cuda.is_available() is False)")
+    from optiland_pr_amd import _native
+
+    _native.load()
+    return torch
+
+
+def _leaves_cuda(torch, lens, spec):
+    from tests.test_gpu_adjoint import _leaves
+
+    leaves = _leaves(torch, lens, list(spec))
+    out = []
+    for (kind, si), t in zip(spec, leaves, strict=True):
+        if kind == "zernike":  # device-resident coefficients, as config 5 holds them
+            c = t.detach().cuda().requires_grad_(True)
+            lens.surface_group.surfaces[si].geometry.coefficients = c
+            out.append(c)
+        else:
+            out.append(t)
+    return out
+
+
+def _seq_args(torch, name, spec=(), n_rays=8):
+    from optiland_pr_amd import ops
+    from optiland_pr_amd.lowering import lower_surface_group
+    from optiland_pr_amd.raytrace import DeviceLens
+    from tests._cases import build_lens
+    from tests.test_seam_adapter import _generated
+
+    lens = build_lens(name)
+    leaves = _leaves_cuda(torch, lens, spec)
+    table = lower_surface_group(lens.surface_group, [lens.primary_wavelength], record=True)
+    table.final_mat = -1
+    dl = DeviceLens(table, device=torch.device("cuda"))
+    L, meta, ft, key = ops.lens_args(dl)
+    rays = _generated(torch, lens, 0.0, 1.0, lens.primary_wavelength, n_rays, "cuda",
+                      "hexapolar")
+    fields = [getattr(rays, a).detach().clone().requires_grad_(True) for a in FIELDS]
+    return dl, (L, meta, ft, key, fields, None, leaves, ops.encode_spec(_traced(spec)), 0,
+                False)
+
+
+def _check(torch, op, args):
+    res = torch.library.opcheck(op, args)
+    assert all(v == "SUCCESS" for v in res.values()), res
+
+
+@pytest.mark.parametrize("name,spec", [
+    ("dg", ()),
+    ("cooke", (("radius", 1), ("thickness", 2))),
+    ("tma_fringe", (("zernike", 1), ("zernike", 2))),
+])
+def test_opcheck_trace_sequential_cuda(torch, name, spec):
+    dl, args = _seq_args(torch, name, spec)
+    _check(torch, torch.ops.ort.trace_sequential.default, args)
+
+
+@pytest.mark.parametrize("name,spec", [("cooke", ()),
+                                       ("tma_fringe", (("zernike", 1), ("zernike", 3)))])
+def test_opcheck_trace_pupil_cuda(torch, name, spec):
+    from optiland_pr_amd import _abi, ops
+    from optiland_pr_amd.distribution import RandomDistribution
+    from optiland_pr_amd.lowering import segment_params
+    from optiland_pr_amd.raytrace import lens_for
+    from tests._cases import build_lens
+
+    lens = build_lens(name)
+    leaves = _leaves_cuda(torch, lens, spec)
+    dl = lens_for(lens, [lens.primary_wavelength])
+    L, meta, ft, key = ops.lens_args(dl)
+    seg = np.stack([segment_params(lens, 0.0, h, 0) for h in (0.0, 1.0)]).astype(_abi.SEGMENT)
+    seg_t = dl.resident("segments", seg)
+    d = RandomDistribution(seed=3)
+    d.generate_points(64)
+    px = torch.as_tensor(np.asarray(d.x, dtype=np.float64), device="cuda")
+    py = torch.as_tensor(np.asarray(d.y, dtype=np.float64), device="cuda")
+    n = 64 * len(seg)
+    want_tape = 1 if spec else 0
+    args = (L, meta, ft, key, seg_t, None, px, py, leaves, ops.encode_spec(_traced(spec)),
+            [n, 64, 0, 0, want_tape], 0)
+    _check(torch, torch.ops.ort.trace_pupil.default, args)
+
+
+def test_opcheck_rms_spot_cuda(torch):
+    g = np.random.default_rng(2)
+    x = torch.as_tensor(g.normal(size=1000), device="cuda").requires_grad_(True)
+    y = torch.as_tensor(g.normal(size=1000), device="cuda").requires_grad_(True)
+    _check(torch, torch.ops.ort.rms_spot.default, (x, y))
+
+
+def test_compile_fullgraph_trace_sequential_cuda(torch):
+    dl, args = _seq_args(torch, "dg", ())
+    L, meta, ft, key, fields, *_ = args
+    fields = [f.detach() for f in fields]
+
+    def f(L, fields):
+        out = torch.ops.ort.trace_sequential(L, meta, ft, key, fields, None, [], [], 0, False)
+        return out[0].sum() + out[1].square().sum(), out[7]
+
+    eager = f(L, fields)
+    compiled = torch.compile(f, fullgraph=True, backend="aot_eager")(L, fields)
+    for u, v in zip(eager, compiled, strict=True):
+        assert torch.equal(u, v)
