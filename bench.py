@@ -345,6 +345,7 @@ def config4(args, dev, rank, world, torch):
 def config5(args, dev, rank, world, torch):
     from optiland_pr_amd.autodiff import CapturedStep
     from optiland_pr_amd.operands import RayOperand
+    from optiland_pr_amd.optim import ZernikeAdam
     from optiland_pr_amd.samples import ThreeMirrorAnastigmat
 
     R = args.rays
@@ -368,9 +369,14 @@ def config5(args, dev, rank, world, torch):
                              requires_grad=True)
             g.coefficients = t
             leaves.append(t)
-        # one fused Adam kernel for the 30 coefficients (instead of the foreach sequence);
-        # capturable: its step count lives on the device, so the step can be a graph replay
-        opt = torch.optim.Adam(leaves, lr=1e-7, fused=True, capturable=capturable)
+        # torch.optim.Adam's update fused with the lens-table patch (optim.ZernikeAdam: ONE
+        # launch for torch's two fused-Adam kernels and the next trace's patch; the same bits,
+        # tests/test_gpu_optim.py); --torch-adam: torch.optim.Adam(fused=True) + the patch.
+        # Capturable either way: step counts on the device, so the step can be a graph replay
+        if args.torch_adam:
+            opt = torch.optim.Adam(leaves, lr=1e-7, fused=True, capturable=capturable)
+        else:
+            opt = ZernikeAdam(leaves, [lens], lr=1e-7)
 
         def loss_fn():
             return RayOperand.rms_spot_size(lens, -1, 0.0, 1.0, R, 0.587, d)
@@ -420,6 +426,8 @@ def config5(args, dev, rank, world, torch):
         config={"workload": "TMA (Tutorial_7d), 3 fringe-Zernike mirrors x 10 coefficients, "
                             "1M random rays, Hy=1, lambda 0.587: lens update + trace + "
                             "rms_spot_size + backward (VJP) + Adam",
+                "optimizer": "torch.optim.Adam(fused=True) + patch" if args.torch_adam else
+                             "optim.ZernikeAdam (torch Adam's update + the lens patch, one launch)",
                 "rays_per_gpu": R, "surfaces": S, "parameters": 30,
                 "parallelism": f"dp{world} (independent replicas)",
                 "step_issue": "one HIP graph replay per step (captured after 3 eager steps)"
@@ -489,6 +497,9 @@ def main():
                          "per-wavefront stop (within the Newton tolerance)")
     ap.add_argument("--gather-chunks", type=int, default=7,
                     help="config 4 at N > 1: pair chunks of the pipelined trace + gather")
+    ap.add_argument("--torch-adam", action="store_true",
+                    help="config 5: torch.optim.Adam(fused=True) and the trace's own coefficient "
+                         "patch instead of the fused optim.ZernikeAdam launch")
     ap.add_argument("--eager", action="store_true",
                     help="config 5: issue the optimisation step eagerly instead of as one HIP "
                          "graph replay")

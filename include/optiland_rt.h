@@ -635,6 +635,31 @@ int ort_patch_zernike(const ort_lens* lens, const double* c, const int64_t* rows
 int ort_patch_zernike_ptrs(const ort_lens* lens, const double* const* c_ptrs,
                            const int64_t* rows, int64_t n, void* stream);
 
+/* One Adam step of device-resident Zernike coefficients fused with the patch of the lens's
+ * term table and Cartesian blocks (v18): torch.optim.Adam's update (amsgrad and maximize
+ * off; weight_decay the L2 form: grad + weight_decay * param) of up to ORT_ADAM_MAX_TENSORS
+ * parameter tensors, each the coefficients of term rows [row0, row0 + count) of
+ * lens->zern, then every touched surface re-formed as ort_patch_zernike does -- one launch
+ * for the optimiser's two and the patch. step: device doubles [n_surfaces], the Adam step
+ * count of each surface's coefficients (incremented here, before the update, as torch does).
+ * Pointers by value (no device pointer table): a HIP graph captures the launch as is.
+ * Replaces the optimiser step of optimization/optimizer/torch/base.py:116-132 for
+ * ZernikeCoefficientVariables followed by the lens update of the next trace. */
+#define ORT_ADAM_MAX_TENSORS 16
+typedef struct ort_adam_params {
+  int32_t n_tensors;
+  int32_t reserved;
+  double* param[ORT_ADAM_MAX_TENSORS];
+  const double* grad[ORT_ADAM_MAX_TENSORS];
+  double* exp_avg[ORT_ADAM_MAX_TENSORS];
+  double* exp_avg_sq[ORT_ADAM_MAX_TENSORS];
+  int64_t row0[ORT_ADAM_MAX_TENSORS];
+  int64_t count[ORT_ADAM_MAX_TENSORS];
+  double* step;
+  double lr, beta1, beta2, eps, weight_decay;
+} ort_adam_params;
+int ort_adam_patch_zernike(const ort_lens* lens, const ort_adam_params* p, void* stream);
+
 int ort_surface_sag_normal(const ort_lens* lens, int32_t surface, const double* x,
                            const double* y, int64_t n, double* sag, double* nx, double* ny,
                            double* nz, int32_t* status, void* stream);

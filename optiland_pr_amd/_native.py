@@ -73,6 +73,28 @@ class ort_vjp_params(C.Structure):  # field 7 ("grad_init") was "reserved" befor
     ]
 
 
+ADAM_MAX_TENSORS = 16  # include/optiland_rt.h ORT_ADAM_MAX_TENSORS
+
+
+class ort_adam_params(C.Structure):  # v18
+    _fields_ = [
+        ("n_tensors", C.c_int32),
+        ("reserved", C.c_int32),
+        ("param", C.c_void_p * ADAM_MAX_TENSORS),
+        ("grad", C.c_void_p * ADAM_MAX_TENSORS),
+        ("exp_avg", C.c_void_p * ADAM_MAX_TENSORS),
+        ("exp_avg_sq", C.c_void_p * ADAM_MAX_TENSORS),
+        ("row0", C.c_int64 * ADAM_MAX_TENSORS),
+        ("count", C.c_int64 * ADAM_MAX_TENSORS),
+        ("step", C.c_void_p),
+        ("lr", C.c_double),
+        ("beta1", C.c_double),
+        ("beta2", C.c_double),
+        ("eps", C.c_double),
+        ("weight_decay", C.c_double),
+    ]
+
+
 class ort_pupil(C.Structure):
     _fields_ = [
         ("kind", C.c_int32),
@@ -128,7 +150,7 @@ EXPORTS = ("ort_abi_version", "ort_trace_sequential", "ort_trace_pupil", "ort_tr
            "ort_material_nk", "ort_spot_workspace_size", "ort_spot_stats", "ort_trace_spot", "ort_spot_partials",
            "ort_rms_spot_workspace_size", "ort_rms_spot", "ort_rms_spot_vjp",
            "ort_wavefront_workspace_size", "ort_wavefront_opd", "ort_patch_zernike",
-           "ort_patch_zernike_ptrs", "ort_newton_finish")
+           "ort_patch_zernike_ptrs", "ort_newton_finish", "ort_adam_patch_zernike")
 
 _lib = None
 
@@ -176,6 +198,8 @@ def load(path: str | None = None):
     lib.ort_patch_zernike.restype = C.c_int
     lib.ort_patch_zernike.argtypes = [P(ort_lens), C.c_void_p, C.c_void_p, C.c_int64,
                                       C.c_void_p]
+    lib.ort_adam_patch_zernike.restype = C.c_int
+    lib.ort_adam_patch_zernike.argtypes = [P(ort_lens), P(ort_adam_params), C.c_void_p]
     lib.ort_patch_zernike_ptrs.restype = C.c_int
     lib.ort_patch_zernike_ptrs.argtypes = [P(ort_lens), C.c_void_p, C.c_void_p, C.c_int64,
                                            C.c_void_p]

@@ -269,3 +269,93 @@ extern "C" int ort_patch_zernike_ptrs(const ort_lens* lens, const double* const*
                      nullptr, c_ptrs, rows, n);
   return hipGetLastError() == hipSuccess ? ORT_OK : ORT_ERR_LAUNCH;
 }
+
+// ---- fused Adam step + coefficient patch (ort_adam_patch_zernike) --------------------
+// One workgroup per traced surface, as patch_zernike_kernel: the surface's coefficients in
+// LDS, the Adam update of those that are parameters (torch.optim.Adam's fused kernel math
+// for doubles, FusedAdamKernel / fused_adam_utils: exp_avg = beta1 exp_avg + (1 - beta1) g,
+// exp_avg_sq = beta2 exp_avg_sq + (1 - beta2) g g, step_size = lr / (1 - beta1^t),
+// denom = sqrt(exp_avg_sq) / sqrt(1 - beta2^t) + eps, param -= step_size exp_avg / denom;
+// compiled with the same contraction as that kernel's build, hipcc's default), the new
+// value into the term table and LDS, then the surface's Cartesian blocks re-formed in term
+// order (patch_zernike_kernel's loop). Each parameter element belongs to one surface, so one
+// workgroup updates it; the step count is kept per surface (no cross-workgroup race).
+namespace ortk {
+__device__ inline void adam_update(const ort_adam_params& p, double t, double& param, double g,
+                                   double& m, double& v) {
+#pragma clang fp contract(fast)
+  if (p.weight_decay != 0.0) g = g + param * p.weight_decay;
+  m = p.beta1 * m + (1 - p.beta1) * g;
+  v = p.beta2 * v + (1 - p.beta2) * g * g;
+  const double bias_correction1 = 1 - ::pow(p.beta1, t);
+  const double bias_correction2 = 1 - ::pow(p.beta2, t);
+  const double bias_correction2_sqrt = ::sqrt(bias_correction2);
+  const double step_size = p.lr / bias_correction1;
+  const double denom = (::sqrt(v) / bias_correction2_sqrt) + p.eps;
+  param -= step_size * m / denom;
+}
+
+__global__ __launch_bounds__(kBlock) void adam_patch_zernike_kernel(const ort_surface* surf,
+                                                                    ort_zernike_term* zern,
+                                                                    double* coef,
+                                                                    const ort_adam_params p) {
+  __shared__ double cs[kPatchTerms];
+  __shared__ int touched;
+  const ort_surface s = surf[blockIdx.x];
+  if (s.geometry != ORT_GEOM_ZERNIKE) return;
+  const int t0 = s.coef_off, nt = s.n_coef;
+  if (threadIdx.x == 0) touched = 0;
+  for (int jt = threadIdx.x; jt < nt && jt < kPatchTerms; jt += kBlock) cs[jt] = zern[t0 + jt].c;
+  __syncthreads();
+  // this surface's step count, incremented before the update (torch: step += 1 first)
+  const double t = p.step[blockIdx.x] + 1.0;
+  for (int k = 0; k < p.n_tensors; ++k) {
+    const int64_t lo = p.row0[k] > t0 ? p.row0[k] : t0;
+    const int64_t hi = (p.row0[k] + p.count[k] < t0 + nt) ? p.row0[k] + p.count[k] : t0 + nt;
+    for (int64_t r = lo + threadIdx.x; r < hi; r += kBlock) {
+      const int64_t e = r - p.row0[k];
+      double param = p.param[k][e], m = p.exp_avg[k][e], v = p.exp_avg_sq[k][e];
+      adam_update(p, t, param, p.grad[k][e], m, v);
+      p.param[k][e] = param;
+      p.exp_avg[k][e] = m;
+      p.exp_avg_sq[k][e] = v;
+      zern[r].c = param;
+      if (r - t0 < kPatchTerms) cs[r - t0] = param;
+      touched = 1;  // (a benign race: every writer stores 1)
+    }
+  }
+  __syncthreads();
+  if (!touched) return;
+  if (threadIdx.x == 0) p.step[blockIdx.x] = t;
+  if (s.zm_deg < 0 || nt > kPatchTerms) return;
+  const int K = (s.zm_deg + 1) * (s.zm_deg + 2) / 2;
+  const double* Ms = coef + s.zm_off + 2 * K;
+  const double* Mn = Ms + (int64_t)nt * K;
+  for (int k = threadIdx.x; k < 2 * K; k += kBlock) {
+    const double* M = k < K ? Ms : Mn;
+    const int kk = k < K ? k : k - K;
+    double acc = 0.0;
+    for (int jt = 0; jt < nt; ++jt) acc = acc + cs[jt] * M[(int64_t)jt * K + kk];
+    coef[s.zm_off + k] = acc;
+  }
+}
+}  // namespace ortk
+
+extern "C" int ort_adam_patch_zernike(const ort_lens* lens, const ort_adam_params* p,
+                                      void* stream) {
+  using namespace ortk;
+  if (!lens || !p || p->n_tensors < 0 || p->n_tensors > ORT_ADAM_MAX_TENSORS || !p->step)
+    return ORT_ERR_ARG;
+  if (lens->n_surfaces < 1 || lens->n_surfaces > ORT_MAX_SURFACES || !lens->surfaces ||
+      !lens->zern || !lens->coef)
+    return ORT_ERR_ARG;
+  for (int k = 0; k < p->n_tensors; ++k)
+    if (!p->param[k] || !p->grad[k] || !p->exp_avg[k] || !p->exp_avg_sq[k] || p->row0[k] < 0 ||
+        p->count[k] < 0)
+      return ORT_ERR_ARG;
+  hipLaunchKernelGGL(adam_patch_zernike_kernel, dim3((unsigned)lens->n_surfaces), dim3(kBlock), 0,
+                     (hipStream_t)stream, lens->surfaces,
+                     const_cast<ort_zernike_term*>(lens->zern), const_cast<double*>(lens->coef),
+                     *p);
+  return hipGetLastError() == hipSuccess ? ORT_OK : ORT_ERR_LAUNCH;
+}

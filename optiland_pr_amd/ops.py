@@ -620,7 +620,8 @@ def trace_pupil(lens: list[torch.Tensor], lens_meta: list[int], final_thickness:
         torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]:
     """Optic.trace's fused generation + trace (ort_trace_pupil): outputs the 8 ray columns,
     the verified Newton schedule and the adjoint tape (empty unless plan_meta asks for it:
-    the backward is then the reverse sweep only)."""
+    the backward is then the reverse sweep only; rows the backward never reads are left
+    unwritten)."""
     from .raytrace import RealRays
     from .raytrace import trace_pupil as _trace
 

@@ -192,11 +192,27 @@ class DeviceLens:
         self._resident[slot] = (raw, a.dtype, t)
         return t
 
+    @staticmethod
+    def _coeff_stamp(device_coeffs):
+        return tuple((off, t.data_ptr(), t._version) for off, t in device_coeffs)
+
+    def coefficients_current(self):
+        """The uploaded tables hold the present values of the device-resident coefficient
+        tensors (optim.ZernikeAdam patched them in its own launch): the next
+        patch_coefficients of the same, unchanged tensors is skipped. Any in-place edit of a
+        tensor through torch bumps its version and brings the patch back."""
+        self._patched = self._coeff_stamp(self.table.device_coeffs)
+
     def patch_coefficients(self, device_coeffs):
         """Write device-resident Zernike coefficients into the uploaded term table
         (ort_zernike_term.c) and re-form the surfaces' Cartesian blocks from them
         (ort_patch_zernike: one launch; ort_patch_zernike_ptrs when several parameter
-        tensors are read in place), ordered on the current stream, no host round trip."""
+        tensors are read in place), ordered on the current stream, no host round trip.
+        Skipped when the tables already hold these tensors' values (coefficients_current)."""
+        stamp = self._coeff_stamp(device_coeffs)
+        if stamp == getattr(self, "_patched", None):
+            return
+        self._patched = None
         vals = [t.detach().reshape(-1).to(device=self.device, dtype=torch.float64)
                 for _, t in device_coeffs]
         key = tuple((off, v.numel()) for (off, _), v in zip(device_coeffs, vals))

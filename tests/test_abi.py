@@ -26,6 +26,7 @@ STRUCTS = {
     "ort_batch": (None, _native.ort_batch),
     "ort_options": (None, _native.ort_options),
     "ort_vjp_params": (None, _native.ort_vjp_params),
+    "ort_adam_params": (None, _native.ort_adam_params),
     "ort_pupil": (None, _native.ort_pupil),
     "ort_spot_layout": (None, _native.ort_spot_layout),
     "ort_wavefront_ref": (None, _native.ort_wavefront_ref),

@@ -1,0 +1,97 @@
+"""optim.ZernikeAdam (one fused launch: torch.optim.Adam's update of the device-resident
+Zernike coefficients + the lens-table patch, ort_adam_patch_zernike) against
+torch.optim.Adam(fused=True) followed by the trace's own patch: 20 optimisation steps of the
+TMA's 30 coefficients, the same losses and coefficient trajectory bit for bit; and the same
+step captured as one HIP graph (autodiff.CapturedStep) against its eager run."""
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need the MI355X (torch.cuda.is_available() is False)")
+    from optiland_pr_amd import _native
+
+    _native.load()
+    return torch
+
+
+def _problem(torch, n_rays, fused_patch, lr=1e-5, weight_decay=0.0):
+    from optiland_pr_amd.distribution import RandomDistribution
+    from optiland_pr_amd.operands import RayOperand
+    from optiland_pr_amd.optim import ZernikeAdam
+    from optiland_pr_amd.samples import ThreeMirrorAnastigmat
+
+    d = RandomDistribution(seed=5)
+    d.generate_points(n_rays)
+    lens = ThreeMirrorAnastigmat()
+    lens.newton_mode = "device"
+    leaves = []
+    for si in (1, 2, 3):
+        g = lens.surface_group.surfaces[si].geometry
+        t = torch.tensor(np.asarray(g.coefficients), dtype=torch.float64, device="cuda",
+                         requires_grad=True)
+        g.coefficients = t
+        leaves.append(t)
+    if fused_patch:
+        opt = ZernikeAdam(leaves, [lens], lr=lr, weight_decay=weight_decay)
+    else:
+        opt = torch.optim.Adam(leaves, lr=lr, fused=True, capturable=True,
+                               weight_decay=weight_decay)
+
+    def loss_fn():
+        return RayOperand.rms_spot_size(lens, -1, 0.0, 1.0, n_rays, 0.587, d)
+
+    return lens, leaves, opt, loss_fn
+
+
+def _run(torch, opt, loss_fn, steps):
+    from optiland_pr_amd import raytrace
+
+    losses = []
+    for _ in range(steps):
+        opt.zero_grad()
+        loss = loss_fn()
+        loss.backward()
+        opt.step()
+        losses.append(float(loss))
+    raytrace.check_all_pending()
+    return losses
+
+
+@pytest.mark.parametrize("weight_decay", [0.0, 0.1])
+def test_zernike_adam_equals_torch_fused_adam(torch, weight_decay):
+    n_rays, steps = 16384, 20
+    _, leaves_t, opt_t, loss_t = _problem(torch, n_rays, False, weight_decay=weight_decay)
+    _, leaves_z, opt_z, loss_z = _problem(torch, n_rays, True, weight_decay=weight_decay)
+    lt = _run(torch, opt_t, loss_t, steps)
+    lz = _run(torch, opt_z, loss_z, steps)
+    np.testing.assert_array_equal(np.array(lz), np.array(lt))
+    for a, b in zip(leaves_z, leaves_t, strict=True):
+        np.testing.assert_array_equal(a.detach().cpu().numpy(), b.detach().cpu().numpy())
+        sa, sb = opt_z.state[a], opt_t.state[b]
+        np.testing.assert_array_equal(sa["exp_avg"].cpu().numpy(), sb["exp_avg"].cpu().numpy())
+        np.testing.assert_array_equal(sa["exp_avg_sq"].cpu().numpy(),
+                                      sb["exp_avg_sq"].cpu().numpy())
+    assert len(set(lz)) > 1  # the steps did something
+
+
+def test_zernike_adam_captured_step(torch):
+    """The fused step inside a captured optimisation step: replays equal eager steps."""
+    from optiland_pr_amd.autodiff import CapturedStep
+
+    n_rays, steps = 16384, 6
+    _, leaves_e, opt_e, loss_e = _problem(torch, n_rays, True)
+    _, leaves_g, opt_g, loss_g = _problem(torch, n_rays, True)
+    step_g = CapturedStep(loss_g, opt_g, warmup=3)
+    lg = [float(step_g()) for _ in range(steps)]
+    le = _run(torch, opt_e, loss_e, 3 + steps)[3:]
+    np.testing.assert_array_equal(np.array(lg), np.array(le))
+    for a, b in zip(leaves_g, leaves_e, strict=True):
+        np.testing.assert_array_equal(a.detach().cpu().numpy(), b.detach().cpu().numpy())
