@@ -444,6 +444,12 @@ typedef struct ort_options {
   const int32_t* verify_prev_flag;
   int32_t* verify_flag;
   int32_t* sched_out;
+  /* ort_trace_pupil with a tape (v18; nullable): every workgroup of 256 rays also writes
+   * rms_part[workgroup][4] = { rays, sum x, sum y, sum of (x - mx)^2 + (y - my)^2 about the
+   * workgroup's own mean } of its final (image) points -- RayOperand.rms_spot_size's
+   * reduction (optimization/operand/ray.py:300-340) on the rays still in registers; then
+   * ort_rms_finish combines the rows. ceil(n_rays / 256) rows. */
+  double* rms_part;
 } ort_options;
 #define ORT_VERIFY_MAX_SCHED 1024
 enum ort_option_flags { ORT_OPT_NO_INIT = 1, ORT_OPT_EXACT = 2 };
@@ -563,6 +569,14 @@ typedef struct ort_vjp_params {
    * serve; the workspace is still sized with it). Requires zern_param. slot_need, when
    * given, covers all n_slot slots. */
   int32_t n_mono;
+  int32_t reserved;
+  /* ADJOINT with params->tape (v18; nullable): the cotangents of the x and y outputs gain
+   * those of an rms spot size rms = sqrt(mean((x - mx)^2 + (y - my)^2)) over all rays:
+   * g (x - mx) / (n rms), g (y - my) / (n rms) -- ort_rms_spot_vjp folded into the sweep's
+   * cotangent load (the primal's x, y read from params->primal). rms_stats: the 5 doubles
+   * of ort_rms_spot / ort_rms_finish (n, mx, my, rms, ...); rms_grad: g (one double). */
+  const double* rms_stats;
+  const double* rms_grad;
 } ort_vjp_params;
 
 /* Workspace bytes params->mode needs for this lens, batch and parameter set (ADJOINT:
@@ -767,6 +781,13 @@ int ort_rms_spot(const double* x, const double* y, int64_t n, void* workspace,
                  int64_t workspace_size, double* stats, double* rms, void* stream);
 int ort_rms_spot_vjp(const double* x, const double* y, int64_t n, const double* stats,
                      const double* grad_out, double* gx, double* gy, void* stream);
+/* The rms spot size from the workgroup rows a taped ort_trace_pupil wrote (ort_options.
+ * rms_part, n_rows = ceil(n_rays / 256)), one launch (v18): the mean mx, my and
+ * sum (x - mx)^2 + (y - my)^2 by Chan's pairwise combination of the rows in index order
+ * (deterministic; the same quantity as ort_rms_spot's two passes up to rounding).
+ * stats[5] = n, mx, my, rms, NaN (no max radius); *rms = stats[3]. */
+int ort_rms_finish(const double* part, int64_t n_rows, double* stats, double* rms,
+                   void* stream);
 
 /* Sharded spot statistics: rays holds THIS rank's slice of every pair (layout->n_pupil
  * rays per pair, the same pair order on every rank). Two phases, each two launches:

@@ -70,6 +70,9 @@ class ort_vjp_params(C.Structure):  # field 7 ("grad_init") was "reserved" befor
         ("tape", C.c_void_p),
         ("primal", ort_rays),
         ("n_mono", C.c_int32),  # v18
+        ("reserved", C.c_int32),
+        ("rms_stats", C.c_void_p),
+        ("rms_grad", C.c_void_p),
     ]
 
 
@@ -123,6 +126,7 @@ class ort_options(C.Structure):
         ("verify_prev_flag", C.c_void_p),
         ("verify_flag", C.c_void_p),
         ("sched_out", C.c_void_p),
+        ("rms_part", C.c_void_p),  # v18
     ]
 
 
@@ -150,7 +154,8 @@ EXPORTS = ("ort_abi_version", "ort_trace_sequential", "ort_trace_pupil", "ort_tr
            "ort_material_nk", "ort_spot_workspace_size", "ort_spot_stats", "ort_trace_spot", "ort_spot_partials",
            "ort_rms_spot_workspace_size", "ort_rms_spot", "ort_rms_spot_vjp",
            "ort_wavefront_workspace_size", "ort_wavefront_opd", "ort_patch_zernike",
-           "ort_patch_zernike_ptrs", "ort_newton_finish", "ort_adam_patch_zernike")
+           "ort_patch_zernike_ptrs", "ort_newton_finish", "ort_adam_patch_zernike",
+           "ort_rms_finish")
 
 _lib = None
 
@@ -198,6 +203,8 @@ def load(path: str | None = None):
     lib.ort_patch_zernike.restype = C.c_int
     lib.ort_patch_zernike.argtypes = [P(ort_lens), C.c_void_p, C.c_void_p, C.c_int64,
                                       C.c_void_p]
+    lib.ort_rms_finish.restype = C.c_int
+    lib.ort_rms_finish.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p]
     lib.ort_adam_patch_zernike.restype = C.c_int
     lib.ort_adam_patch_zernike.argtypes = [P(ort_lens), P(ort_adam_params), C.c_void_p]
     lib.ort_patch_zernike_ptrs.restype = C.c_int

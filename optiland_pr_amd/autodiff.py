@@ -154,10 +154,11 @@ def _workspace(device, nbytes):
 
 
 def vjp(dlens, seg_dev, px, py, n, seg_len, sched_dev, tables, n_param, cot, grad,
-        pupil_per_ray=False, mode=None, tape=None, primal=None, overwrite=False):
+        pupil_per_ray=False, mode=None, tape=None, primal=None, overwrite=False, rms=None):
     """grad += J^T cot through ort_trace_pupil_vjp (overwrite: grad = J^T cot, grad need
     not be initialised). tables: device tensors (zern_param, surf_tangent,
-    final_tangent), each possibly None; cot: 8 tensors / None."""
+    final_tangent), each possibly None; cot: 8 tensors / None; rms: (stats[5], g[1]) of an
+    rms spot size of the outputs, folded into the x, y cotangent load (adjoint mode)."""
     from .raytrace import _ptr, _stream_handle
 
     if np.any(dlens.table.surfaces["geometry"] == _abi.GEOM_GRID_SAG):
@@ -187,6 +188,10 @@ def vjp(dlens, seg_dev, px, py, n, seg_len, sched_dev, tables, n_param, cot, gra
         # state read from the forward's outputs
         params.tape = tape.data_ptr()
         params.primal = _native.ort_rays(*(t.data_ptr() for t in primal))
+    if rms is not None:
+        if mode != _abi.VJP_ADJOINT:
+            raise ValueError("vjp: the rms cotangent fold is the adjoint mode's")
+        params.rms_stats, params.rms_grad = rms[0].data_ptr(), rms[1].data_ptr()
     # both modes take a workspace (ABI v15: the unrolled mode's block partials)
     size = lib.ort_vjp_workspace_size(C.byref(dlens.c), C.byref(batch), C.byref(params))
     _native.check(int(size) if size < 0 else 0, "ort_vjp_workspace_size")
@@ -208,10 +213,12 @@ def vjp(dlens, seg_dev, px, py, n, seg_len, sched_dev, tables, n_param, cot, gra
 
 
 def trace_pupil_grad(optic, dlens, seg_dev, px, py, n, seg_len, wavelength, keys,
-                     newton_mode="reference"):
+                     newton_mode="reference", want_rms=False):
     """Differentiable fused trace: returns the 8 output tensors connected to the
     parameter tensors of parameters(optic), through the torch.ops.ort.trace_pupil custom
-    op (ops.py) whose autograd formula is ort_trace_pupil_vjp."""
+    op (ops.py) whose autograd formula is ort_trace_pupil_vjp, and a 9th: the rms spot size
+    of the final points (a 0-dim tensor) when want_rms and the forward is taped with one
+    wavelength row (F_RMS), else an empty tensor."""
     from . import ops
 
     params = parameters(optic)
@@ -221,13 +228,14 @@ def trace_pupil_grad(optic, dlens, seg_dev, px, py, n, seg_len, wavelength, keys
                       and vjp_mode(dlens.table) == _abi.VJP_ADJOINT
                       and not dlens.table.interaction_mask & ~(1 << _abi.IA_REFRACT_REFLECT)
                       and not np.any(dlens.table.surfaces["geometry"] == _abi.GEOM_GRID_SAG))
+    plan.want_rms = bool(want_rms and plan.want_tape and len(dlens.table.wavelengths) == 1)
     lens, meta, ft, key = ops.lens_args(dlens)
     seg, apod, pmeta, pkey = ops.plan_args(plan)
     outs = torch.ops.ort.trace_pupil(lens, meta, ft, key, seg, apod, px, py,
                                      [t for _, _, t in params],
                                      ops.encode_spec([(k, si) for k, si, _ in params]), pmeta,
                                      pkey)
-    return outs[:8]
+    return (*outs[:8], outs[10])
 
 
 class CapturedStep:

@@ -43,8 +43,16 @@ int launch(const KArgs& a_in, uint32_t feat, hipStream_t stream) {
   if (!fn) return ORT_ERR_ARG;
   const int bs = closed ? closed_block() : kBlock;
   // F_SPOT: one block per (pair, chunk) of seg_len rays
-  const int64_t blocks = (feat & F_SPOT) != 0 ? (int64_t)a_in.n_seg * a_in.spot_chunks
-                                              : (a_in.n_rays + bs - 1) / bs;
+  int64_t blocks = (feat & F_SPOT) != 0 ? (int64_t)a_in.n_seg * a_in.spot_chunks
+                                        : (a_in.n_rays + bs - 1) / bs;
+  // a verify-and-re-trace round (statistics to check, or a run_if flag) of a kernel with a
+  // grid-stride form (F_STRIDE): at most kVerifyGrid workgroups
+  if (!closed && (feat & F_IA) == 0 && (a_in.vstats || a_in.run_if) && blocks > kVerifyGrid) {
+    if (KernelFn fs = select_trace((feat | F_STRIDE) & ~F_AXIAL)) {
+      fn = fs;
+      blocks = kVerifyGrid;
+    }
+  }
   if (blocks > 0x7fffffff) return ORT_ERR_ARG;
   KArgs a = a_in;
   // Newton kernels on generated rays whose segments share one pupil: chunk-major block
@@ -95,7 +103,7 @@ int ort_trace_sequential(const ort_lens* lens, const ort_rays* rays_in, ort_rays
                          ort_newton_stat* newton_stat, int32_t* status, void* stream) {
   if (!rays_in || !rays_out || !batch) return ORT_ERR_ARG;
   if (batch->n_rays == 0) return ORT_OK;
-  if (opt && opt->tape) return ORT_ERR_ARG;  // the tape is ort_trace_pupil's
+  if (opt && (opt->tape || opt->rms_part)) return ORT_ERR_ARG;  // ort_trace_pupil's
   KArgs a{};
   uint32_t feat = 0;
   int rc = fill_args(a, lens, batch, opt, rec, newton_stat, status, feat);
@@ -140,6 +148,10 @@ int trace_pupil_impl(const ort_lens* lens, const double* px, const double* py,
         opt->newton_mode != ORT_NEWTON_SCHEDULE || opt->start_surface != 0)
       return ORT_ERR_ARG;
     feat |= F_TAPE;
+  }
+  if (opt->rms_part) {  // the rms spot size's workgroup rows in the taped kernel's epilogue
+    if ((feat & F_TAPE) == 0 || (feat & F_MONO) == 0 || fuse) return ORT_ERR_ARG;
+    feat |= F_RMS;
   }
   // ort_trace_spot: spot pass 1 in the closed-form kernel's epilogue when its blocks can be
   // the spot chunks (one ray per thread, each (field, lambda) segment one pair)
@@ -293,12 +305,19 @@ static int vjp_run(const ort_lens* lens, const double* px, const double* py,
     aj.surf = lens->surfaces;
     aj.zern = lens->zern;
     aj.coef = lens->coef;
+    // an rms spot size's cotangent folded into the x, y cotangent load
+    if ((params->rms_stats != nullptr) != (params->rms_grad != nullptr)) return ORT_ERR_ARG;
+    if (params->rms_stats && aj.tape_ready && (!params->primal.x || !params->primal.y))
+      return ORT_ERR_ARG;
+    aj.rms_stats = params->rms_stats;
+    aj.rms_grad = params->rms_grad;
     // radius / conic tangents need duals seeded on them too
     return adj_run(a, aj, (int32_t*)(w + L.need), params->surf_tangent ? 4 : 2, km, resident,
                    blocks, s);
   }
   if (params->mode != ORT_VJP_UNROLLED) return ORT_ERR_ARG;
   if (want_in) return ORT_ERR_ARG;  // forward mode carries parameter tangents only
+  if (params->rms_stats || params->rms_grad) return ORT_ERR_ARG;  // the adjoint's fold only
   AdjLayout L;
   if (!adj_layout(lens, batch, params, L)) return ORT_ERR_ARG;
   if (!params->workspace || params->workspace_size < L.total) return ORT_ERR_ARG;

@@ -349,6 +349,9 @@ int host_vjp(KArgs& a, const ort_lens* lens, const ort_vjp_params* params,
     j.zern = lens->zern;
     j.coef = lens->coef;
     j.mono_on = mono_enabled(j);
+    if ((params->rms_stats != nullptr) != (params->rms_grad != nullptr)) return ORT_ERR_ARG;
+    j.rms_stats = params->rms_stats;  // replayed: the final point is the traced state
+    j.rms_grad = params->rms_grad;
     j.cot = *cotangent;
     j.rec_cot = rec_cotangent;
     j.rec = rec;
@@ -387,6 +390,7 @@ int host_vjp(KArgs& a, const ort_lens* lens, const ort_vjp_params* params,
   }
   if (params->mode != ORT_VJP_UNROLLED) return ORT_ERR_ARG;
   if (want_in) return ORT_ERR_ARG;  // forward mode carries parameter tangents only
+  if (params->rms_stats || params->rms_grad) return ORT_ERR_ARG;  // the adjoint's fold only
   JArgs j{};
   j.zparam = params->zern_param;
   j.tan_surf = params->surf_tangent;

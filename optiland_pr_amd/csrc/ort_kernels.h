@@ -46,6 +46,14 @@ namespace ortk {
 
 
 constexpr int kBlock = 256;
+// workgroups of a verify-and-re-trace round of trace_kernel (a multiple of 8, so the
+// grid-stride loop keeps each block on its XCD): 4 per CU, the taped kernel's full
+// occupancy at 4 waves per SIMD. ORT_VERIFY_GRID: A/B builds.
+#ifndef ORT_VERIFY_GRID
+#define ORT_VERIFY_GRID 1024
+#endif
+constexpr int64_t kVerifyGrid = ORT_VERIFY_GRID;
+static_assert(kVerifyGrid % 8 == 0, "XCD-preserving stride");
 // trace_closed_kernel's block size (ort_k_closed.hip; its launch asks closed_block()):
 // a per-TU constant so A/B builds of that TU alone can change it
 #ifndef ORT_CLOSED_BLOCK
@@ -71,6 +79,9 @@ int trace_pupil_impl(const ort_lens* lens, const double* px, const double* py,
 // the F_SPOT epilogue (ort_reduce.h): every thread of the block calls it
 template <uint32_t FEAT>
 __device__ void spot_epilogue(const KArgs& a, const ort::Ray& r, double inten, bool active);
+// the F_RMS epilogue (ort_reduce.h): every thread of the block calls it
+__device__ inline void rms_epilogue(const KArgs& a, const ort::Ray& r, bool active,
+                                    int64_t vb);
 
 // Ray of this thread when every (field, lambda) segment traces the SAME pupil samples
 // (real_ray_tracer.py:74-77 field-major layout: ray = segment * seg_len + p): block b
@@ -81,9 +92,11 @@ __device__ void spot_epilogue(const KArgs& a, const ort::Ray& r, double inten, b
 // each of its pupil chunks once and serves all segments from its L2. Any dispatch order
 // gives the same results (a bijection over blocks); only the traffic depends on it.
 // Requires n_rays == n_seg * seg_len and seg_len % kBlock == 0 (host-checked).
-__device__ inline int64_t pair_major_ray(const KArgs& a) {
-  const int64_t B = gridDim.x;
-  const int64_t b = blockIdx.x;
+// vb / nb: the workgroup's (virtual) block of the launch's nb blocks (trace_kernel's
+// grid-stride loop keeps vb % 8 == blockIdx.x % 8: its grids are multiples of 8 or nb)
+__device__ inline int64_t pair_major_ray(const KArgs& a, int64_t vb, int64_t nb) {
+  const int64_t B = nb;
+  const int64_t b = vb;
   const int64_t x = b & 7, local = b >> 3;
   int64_t start = 0;
   for (int64_t y = 0; y < x; ++y) start += (B - y + 7) >> 3;  // blocks of the lower XCD slots
@@ -704,41 +717,12 @@ __device__ inline __attribute__((always_inline)) ort::Ray trace_ray(const KArgs&
   return r;
 }
 
+// The rays of (virtual) block vb of nb: the body of trace_kernel's grid-stride loop
 template <uint32_t FEAT>
-__global__ __launch_bounds__(kBlock) ORT_TRACE_OCC void trace_kernel(const KArgs a) {
-  if (a.run_if && *cst(a.run_if) != 1) return;  // a device-side re-trace that is not needed
-  // verify-and-re-trace (ort_options.verify_*): every workgroup derives the decision of
-  // ort_newton_fixup from the previous launch's statistics into its own copy of the
-  // schedule, workgroup 0 publishes it (verify_flag, sched_out), and the rays are traced
-  // on that copy only when the schedule was corrected
-  const int32_t* sched = a.sched;
-  __shared__ int32_t vsched[ORT_VERIFY_MAX_SCHED];
-  __shared__ int32_t vcodes[kBlock / 64];
-  if constexpr ((FEAT & F_KM) != 0) {
-    if (a.vstats) {
-      const int prev = a.vprev ? *a.vprev : 1;
-      const int64_t ng = (a.n_rays + a.group_len - 1) / a.group_len;
-      const int nsch = (int)ng * a.n_surf;  // <= ORT_VERIFY_MAX_SCHED (host-checked)
-      if (prev != 1) {  // the previous launch did not run: nothing to verify
-        if (blockIdx.x == 0) {
-          for (int k = threadIdx.x; k < nsch; k += kBlock) a.sched_out[k] = a.sched[k];
-          if (threadIdx.x == 0) *a.vflag = prev;
-        }
-        return;
-      }
-      for (int k = threadIdx.x; k < nsch; k += kBlock) vsched[k] = a.sched[k];
-      __syncthreads();
-      const int c = newton_decide(a.surf, a.n_surf, ng, a.vstats, a.conv_base, vsched, vcodes);
-      if (blockIdx.x == 0) {
-        for (int k = threadIdx.x; k < nsch; k += kBlock) a.sched_out[k] = vsched[k];
-        if (threadIdx.x == 0) *a.vflag = c;
-      }
-      if (c != 1) return;
-      sched = vsched;
-    }
-  }
+__device__ __forceinline__ void trace_block(const KArgs& a, const int32_t* sched, int64_t vb,
+                                            int64_t nb) {
   const int64_t rid =
-      a.block_remap ? pair_major_ray(a) : (int64_t)blockIdx.x * kBlock + threadIdx.x;
+      a.block_remap ? pair_major_ray(a, vb, nb) : vb * kBlock + threadIdx.x;
   const bool active = rid < a.n_rays;
   const int64_t r_ld = active ? rid : 0;  // inactive lanes compute on ray 0, store nothing
   // kNewtonFast: first the whole ray on ort_fastpath.h's deferred-check sequences; the
@@ -923,9 +907,55 @@ __global__ __launch_bounds__(kBlock) ORT_TRACE_OCC void trace_kernel(const KArgs
   }
 
   if (range_bits && active && a.status) atomicOr(a.status, range_bits);
+  if constexpr ((FEAT & F_RMS) != 0) rms_epilogue(a, r, active, vb);
   if (!active) return;
   store_ray(a, rid, r);
+}
 
+template <uint32_t FEAT>
+__global__ __launch_bounds__(kBlock) ORT_TRACE_OCC void trace_kernel(const KArgs a) {
+  if (a.run_if && *cst(a.run_if) != 1) return;  // a device-side re-trace that is not needed
+  // verify-and-re-trace (ort_options.verify_*): every workgroup derives the decision of
+  // ort_newton_fixup from the previous launch's statistics into its own copy of the
+  // schedule, workgroup 0 publishes it (verify_flag, sched_out), and the rays are traced
+  // on that copy only when the schedule was corrected
+  const int32_t* sched = a.sched;
+  __shared__ int32_t vsched[ORT_VERIFY_MAX_SCHED];
+  __shared__ int32_t vcodes[kBlock / 64];
+  if constexpr ((FEAT & F_KM) != 0) {
+    if (a.vstats) {
+      const int prev = a.vprev ? *a.vprev : 1;
+      const int64_t ng = (a.n_rays + a.group_len - 1) / a.group_len;
+      const int nsch = (int)ng * a.n_surf;  // <= ORT_VERIFY_MAX_SCHED (host-checked)
+      if (prev != 1) {  // the previous launch did not run: nothing to verify
+        if (blockIdx.x == 0) {
+          for (int k = threadIdx.x; k < nsch; k += kBlock) a.sched_out[k] = a.sched[k];
+          if (threadIdx.x == 0) *a.vflag = prev;
+        }
+        return;
+      }
+      for (int k = threadIdx.x; k < nsch; k += kBlock) vsched[k] = a.sched[k];
+      __syncthreads();
+      const int c = newton_decide(a.surf, a.n_surf, ng, a.vstats, a.conv_base, vsched, vcodes);
+      if (blockIdx.x == 0) {
+        for (int k = threadIdx.x; k < nsch; k += kBlock) a.sched_out[k] = vsched[k];
+        if (threadIdx.x == 0) *a.vflag = c;
+      }
+      if (c != 1) return;
+      sched = vsched;
+    }
+  }
+  const int64_t nb = (a.n_rays + kBlock - 1) / kBlock;
+  if constexpr ((FEAT & F_STRIDE) != 0) {
+    // a verify-and-re-trace round: at most kVerifyGrid workgroups stride over the nb
+    // blocks of rays (the usual outcome is "nothing to re-trace", so the round costs the
+    // dispatch of a chip's worth of workgroups, not one per 256 rays). Its own
+    // instantiation: the loop raises the register pressure of the body, and the first
+    // launch of a call runs the loop-free kernel.
+    for (int64_t vb = blockIdx.x; vb < nb; vb += gridDim.x) trace_block<FEAT>(a, sched, vb, nb);
+  } else {
+    trace_block<FEAT>(a, sched, blockIdx.x, nb);
+  }
 }
 
 // Closed-form lenses (planes, spheres, conics: no Newton surface) -- the DoubleGauss /

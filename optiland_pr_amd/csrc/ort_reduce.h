@@ -17,9 +17,9 @@ __device__ inline double wave_max(double v) {
   return v;
 }
 
-// block-wide sums of NV values (lanes by xor butterfly, then waves 0..3 in order); every
-// thread gets the totals. lds: >= 4 * NV doubles; safe to call back to back.
-template <int NV>
+// block-wide sums of NV values (lanes by xor butterfly, then waves 0..NT/64-1 in order);
+// every thread gets the totals. lds: >= NT / 64 * NV doubles; safe to call back to back.
+template <int NV, int NT = kRedThreads>
 __device__ inline void block_sum(double (&v)[NV], double* lds) {
 #pragma unroll
   for (int k = 0; k < NV; ++k) v[k] = wave_sum_xor(v[k]);
@@ -32,7 +32,7 @@ __device__ inline void block_sum(double (&v)[NV], double* lds) {
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     double s = 0.0;
-    for (int ww = 0; ww < kRedThreads / 64; ++ww) s += lds[ww * NV + k];
+    for (int ww = 0; ww < NT / 64; ++ww) s += lds[ww * NV + k];
     v[k] = s;
   }
 }
@@ -75,6 +75,38 @@ __device__ void spot_epilogue(const KArgs& a, const ort::Ray& r, double inten, b
     o[0] = v[0];
     o[1] = v[1];
     o[2] = v[2];
+  }
+}
+
+// F_RMS epilogue of the taped Newton kernel (RayOperand.rms_spot_size on the traced
+// points, optimization/operand/ray.py:300-340): block vb's row {count, sum x, sum y,
+// sum of (x - mx)^2 + (y - my)^2 about the block's own centroid (mx, my)}, each by
+// block_sum in its fixed order; rms_finish_kernel (ort_k_spot.hip) combines the rows
+// (Chan et al.'s pairwise update: the second moments re-centred on the total centroid),
+// so the rms leaves the forward without a second read of the points
+__device__ inline void rms_epilogue(const KArgs& a, const ort::Ray& r, bool active,
+                                    int64_t vb) {
+  static_assert(kBlock == kRedThreads, "one row per trace workgroup");
+  double v[3] = {0.0, 0.0, 0.0};
+  if (active) {
+    v[0] = 1.0;
+    v[1] = r.x;
+    v[2] = r.y;
+  }
+  __shared__ double lds[4 * 3];
+  block_sum<3>(v, lds);
+  double d[1] = {0.0};
+  if (active) {
+    const double dx = r.x - v[1] / v[0], dy = r.y - v[2] / v[0];
+    d[0] = dx * dx + dy * dy;
+  }
+  block_sum<1>(d, lds);
+  if (threadIdx.x == 0) {
+    double* o = a.rms_part + vb * 4;
+    o[0] = v[0];
+    o[1] = v[1];
+    o[2] = v[2];
+    o[3] = d[0];
   }
 }
 

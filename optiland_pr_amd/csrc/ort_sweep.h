@@ -57,6 +57,10 @@ enum : uint32_t {
   F_AXIAL = 1u << 9, // ORT_LENS_AXIAL: every frame a +z translation (closed-form kernels)
   F_TAPE = 1u << 10, // write the adjoint tape as the trace runs (ort_options.tape)
   F_SPOT = 1u << 11, // closed-form kernel: spot pass 1 in the epilogue (ort_trace_spot)
+  F_RMS = 1u << 12,  // taped Newton kernel: the rms spot size's workgroup rows in the
+                     // epilogue (ort_options.rms_part)
+  F_STRIDE = 1u << 13,  // Newton kernel of a verify-and-re-trace round: a grid of at most
+                        // kVerifyGrid workgroups strides over the blocks of rays
 };
 
 // Adjoint tape (adj_ray): per traced surface, rows of n_rays doubles -- the incoming
@@ -127,6 +131,7 @@ struct KArgs {
   const ort_cs_op* spot_ops;
   int32_t spot_n_ops;
   int32_t spot_chunks;
+  double* rms_part;  // F_RMS: [workgroup][4] (ort_options.rms_part)
 };
 
 // KArgs from the C ABI structs (argument checks included) and the kernel feature bits the
@@ -169,6 +174,7 @@ inline int fill_args(KArgs& a, const ort_lens* lens, const ort_batch* batch,
   a.no_init = (opt->flags & ORT_OPT_NO_INIT) != 0;
   a.exact_only = (opt->flags & ORT_OPT_EXACT) != 0;
   a.tape = opt->tape;
+  a.rms_part = opt->rms_part;
   if (opt->conv_base < 0) return ORT_ERR_ARG;
   // geometry ids this library knows (enum ort_geometry): anything else is refused here
   // rather than traced as some other kind
@@ -350,6 +356,9 @@ struct AArgs {
   const ort_surface* surf;  // the lens tables the reduce reads the term matrices from
   const ort_zernike_term* zern;
   const double* coef;
+  // an rms spot size's cotangent folded into the x, y cotangents (ort_vjp_params.rms_*)
+  const double* rms_stats;
+  const double* rms_grad;
 };
 
 // monomials of a Cartesian block of degree N
@@ -785,6 +794,16 @@ ORT_INLINE void adj_ray(const KArgs& a, const AArgs& j, Lane& ln, int64_t rid, b
     if (j.cot.N) b.N = j.cot.N[rid];
     if (j.cot.opd) bopd = j.cot.opd[rid];
     if (j.cot.i) batt = j.cot.i[rid] * (RES ? i_in * ort::intensity(r) : ort::intensity(r));
+    if (j.rms_stats) {
+      // d rms / d (x, y) = (x - mx, y - my) / (n rms) times the upstream gradient: the
+      // ort_rms_spot_vjp kernel's operations, on the final point (the primal's outputs, or
+      // the replayed state after the image-space propagate: the same values)
+      const double px = replay ? r.x : j.primal.x[r_ld];
+      const double py = replay ? r.y : j.primal.y[r_ld];
+      const double w = cst(j.rms_grad)[0] / (cst(j.rms_stats)[0] * cst(j.rms_stats)[3]);
+      b.x = b.x + (px - cst(j.rms_stats)[1]) * w;
+      b.y = b.y + (py - cst(j.rms_stats)[2]) * w;
+    }
   }
   const double factor_f = ort::intensity(r);  // RES: d i_out / d i_in
   // image-space propagate (real_ray_tracer.py:84-89): x = x' + d L, ...

@@ -188,8 +188,10 @@ def trace_pupil(hl: HostLens, seg, px, py, n, seg_len, pupil_per_ray, apod=None)
 
 
 def trace_pupil_vjp(hl: HostLens, seg, px, py, n, seg_len, pupil_per_ray, sched, tabs, need,
-                    n_param, mode, cot, grad, apod=None):
-    """ort_host_trace_pupil_vjp: grad = J^T cot of the pupil trace (grad overwritten)."""
+                    n_param, mode, cot, grad, apod=None, rms=None):
+    """ort_host_trace_pupil_vjp: grad = J^T cot of the pupil trace (grad overwritten).
+    rms: (stats[5], g[1]) of an rms spot size of the outputs, folded into the x, y
+    cotangents (ort_vjp_params.rms_stats / rms_grad; the adjoint mode)."""
     from .ops import mono_slot_count
 
     lib = _native.load_host()
@@ -203,6 +205,8 @@ def trace_pupil_vjp(hl: HostLens, seg, px, py, n, seg_len, pupil_per_ray, sched,
     params = _native.ort_vjp_params(int(n_param), int(mode), _p(zp), _p(st), _p(ft),
                                     0 if zp is None else int(zp.numel()), 1, None, 0, _p(need))
     params.n_mono = mono_slot_count(hl.table, None if zp is None else zp.numpy())
+    if rms is not None:
+        params.rms_stats, params.rms_grad = _p(rms[0]), _p(rms[1])
     rc = lib.ort_host_trace_pupil_vjp(C.byref(hl.c), _p(px), _p(py), C.byref(batch), C.byref(opt),
                                       C.byref(params), C.byref(_rays_c(cot)), _p(grad))
     _native.check(rc, "ort_host_trace_pupil_vjp")

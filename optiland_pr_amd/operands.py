@@ -4,11 +4,20 @@ RayOperand.rms_spot_size (optimization/operand/ray.py:300-340) is the loss of co
 (torch-autograd step): it reads the image record after Optic.trace. With torch-tensor
 Zernike coefficients that require grad, Optic.trace runs the differentiable trace
 (autodiff.py) and the value returned here back-propagates to the coefficients through
-ort_trace_pupil_vjp. The reduction is the custom op torch.ops.ort.rms_spot (ops.py:
-ort_rms_spot's two deterministic passes, ort_rms_spot_vjp for its gradient).
+ort_trace_pupil_vjp. On the image surface of a taped single-wavelength trace the
+reduction runs inside the trace: the taped kernel's epilogue writes per-workgroup rows
+(count, sums, second moment about the workgroup centroid), one ort_rms_finish launch
+combines them, and the gradient folds into the adjoint's x, y cotangent load
+(raytrace.fused_rms; ORT_FUSED_RMS=0 turns it off). Otherwise the reduction is the custom
+op torch.ops.ort.rms_spot (ops.py: ort_rms_spot's two deterministic passes,
+ort_rms_spot_vjp for its gradient).
 """
 
 from __future__ import annotations
+
+import os
+
+FUSED_RMS = os.environ.get("ORT_FUSED_RMS", "1") != "0"
 
 try:
     import torch
@@ -33,7 +42,15 @@ class RayOperand:
             mx, my = torch.mean(xs[k]), torch.mean(ys[k])
             r2 = [(x - mx) ** 2 + (y - my) ** 2 for x, y in zip(xs, ys, strict=True)]
             return torch.sqrt(torch.mean(torch.cat(r2)))
-        optic.trace(Hx, Hy, wavelength, num_rays, distribution)
+        if FUSED_RMS and surface_number in (-1, len(optic.surface_group.surfaces) - 1):
+            from . import raytrace
+
+            with raytrace.fused_rms() as req:
+                optic.trace(Hx, Hy, wavelength, num_rays, distribution)
+            if req.get("rms") is not None:
+                return req["rms"]
+        else:
+            optic.trace(Hx, Hy, wavelength, num_rays, distribution)
         x = _record_row(optic.surface_group, "x", surface_number)
         y = _record_row(optic.surface_group, "y", surface_number)
         if torch.is_tensor(x) and x.is_cuda:

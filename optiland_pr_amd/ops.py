@@ -82,6 +82,7 @@ class PupilPlan:
         self.pupil_per_ray = bool(pupil_per_ray)
         self.newton_mode = newton_mode
         self.want_tape = False  # set by the caller when the backward is an adjoint sweep
+        self.want_rms = False  # the rms spot size in the taped forward's epilogue (F_RMS)
         self.tape = None
 
 
@@ -590,8 +591,8 @@ def _seq_vjp(dl, rays_in, w, per_ray_w, start_surface, sched, zp, st, ft, n_para
 def plan_args(plan):
     """(seg, apod, plan_meta, plan_key) of a PupilPlan: the segment descriptors (SEGMENT
     records as bytes on the lens's device), the apodization record (or None), [n, seg_len,
-    pupil_per_ray, newton mode index, want_tape] and the plan's handle (its Newton schedule
-    cache keys; a cache key only)."""
+    pupil_per_ray, newton mode index, want_tape, want_rms] and the plan's handle (its Newton
+    schedule cache keys; a cache key only)."""
     dl = plan.dlens
     seg = plan.seg_dev
     if not torch.is_tensor(seg):
@@ -600,8 +601,14 @@ def plan_args(plan):
     if apod is None and getattr(dl.table, "apod", None) is not None and dl.device.type == "cpu":
         apod = dl.resident("apod", dl.table.apod)
     meta = [plan.n, plan.seg_len, int(plan.pupil_per_ray),
-            NEWTON_MODES.index(plan.newton_mode), int(bool(plan.want_tape))]
+            NEWTON_MODES.index(plan.newton_mode), int(bool(plan.want_tape)),
+            int(bool(plan.want_rms))]
     return seg, apod, meta, handle(plan)
+
+
+def _want_rms(plan_meta):
+    """plan_meta's want_rms entry (absent: 0)"""
+    return int(plan_meta[5]) if len(plan_meta) > 5 else 0
 
 
 def _plan_keys(plan_key):
@@ -617,24 +624,31 @@ def trace_pupil(lens: list[torch.Tensor], lens_meta: list[int], final_thickness:
                 py: torch.Tensor, params: list[torch.Tensor], spec: list[int],
                 plan_meta: list[int], plan_key: int) -> tuple[
         torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor,
-        torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]:
+        torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]:
     """Optic.trace's fused generation + trace (ort_trace_pupil): outputs the 8 ray columns,
-    the verified Newton schedule and the adjoint tape (empty unless plan_meta asks for it:
+    the verified Newton schedule, the adjoint tape (empty unless plan_meta asks for it:
     the backward is then the reverse sweep only; rows the backward never reads are left
-    unwritten)."""
+    unwritten), and RayOperand.rms_spot_size of the final points with its stats[5] (empty
+    unless plan_meta's want_rms: the rows in the taped kernel's epilogue, ort_rms_finish;
+    its gradient folds into the backward's x, y cotangents)."""
     from .raytrace import RealRays
     from .raytrace import trace_pupil as _trace
 
     dl = _resolve(lens, lens_meta, final_thickness, lens_key)
-    n, seg_len, ppr, mode, want_tape = plan_meta
+    n, seg_len, ppr, mode, want_tape = plan_meta[:5]
+    want_rms = _want_rms(plan_meta)
+    if want_rms and not want_tape:
+        raise ValueError("ort::trace_pupil: want_rms needs the taped forward (want_tape)")
     out = RealRays.__new__(RealRays)
     for a in _abi.RAY_FIELDS:
         setattr(out, a, torch.empty(n, dtype=torch.float64, device=dl.device))
     tape = torch.empty(tape_doubles(dl, n) if want_tape else 0, dtype=torch.float64,
                        device=dl.device)
+    rms = torch.empty(() if want_rms else 0, dtype=torch.float64, device=dl.device)
+    rms_stats = torch.empty(5 if want_rms else 0, dtype=torch.float64, device=dl.device)
     _trace(dl, seg, px, py, out, n, seg_len, n, keys=_plan_keys(plan_key),
            pupil_per_ray=bool(ppr), newton_mode=NEWTON_MODES[mode],
-           tape=tape if want_tape else None)
+           tape=tape if want_tape else None, rms=(rms, rms_stats) if want_rms else None)
     sched = dl.last_schedule
     if dl.last_schedule_dev is not None:  # device-verified: the settled device schedule
         sched_t = (dl.last_schedule_dev if dl.last_schedule_private  # a per-call copy
@@ -643,7 +657,7 @@ def trace_pupil(lens: list[torch.Tensor], lens_meta: list[int], final_thickness:
         sched_t = torch.empty(0, dtype=torch.int32, device=dl.device)
     else:
         sched_t = dl.resident("sched", sched.reshape(-1)).clone()
-    return (*(getattr(out, a) for a in _abi.RAY_FIELDS), sched_t, tape)
+    return (*(getattr(out, a) for a in _abi.RAY_FIELDS), sched_t, tape, rms, rms_stats)
 
 
 @trace_pupil.register_kernel("cpu")
@@ -651,26 +665,33 @@ def _trace_pupil_cpu(lens, lens_meta, final_thickness, lens_key, seg, apod, px, 
                      spec, plan_meta, plan_key):
     """The CPU dispatch key: rays generated and traced by the host build (host.py), the
     Newton stop rule evaluated exactly per (field, wavelength) group; no tape (the host
-    backward re-traces)."""
+    backward re-traces); want_rms: ort_host_rms_spot of the outputs."""
     from . import host
 
     hl = _resolve(lens, lens_meta, final_thickness, lens_key)
-    n, seg_len, ppr, _, _ = plan_meta
+    n, seg_len, ppr = plan_meta[:3]
     outs, updates = host.trace_pupil(hl, seg, px.detach().contiguous(), py.detach().contiguous(),
                                      n, seg_len, bool(ppr), apod)
     sched = updates if hl.newton else torch.empty(0, dtype=torch.int32)
-    return (*outs, sched, torch.empty(0, dtype=torch.float64))
+    if _want_rms(plan_meta):
+        rms, rms_stats = host.rms_spot(outs[0], outs[1])
+    else:
+        rms, rms_stats = (torch.empty(0, dtype=torch.float64) for _ in range(2))
+    return (*outs, sched, torch.empty(0, dtype=torch.float64), rms, rms_stats)
 
 
 @trace_pupil.register_fake
 def _(lens, lens_meta, final_thickness, lens_key, seg, apod, px, py, params, spec, plan_meta,
       plan_key):
-    n, seg_len, _, _, want_tape = plan_meta
+    n, seg_len, _, _, want_tape = plan_meta[:5]
+    want_rms = _want_rms(plan_meta)
     outs = [px.new_empty(n, dtype=torch.float64) for _ in range(8)]
     S = lens_meta[0]
     ns = S if lens_meta[8] else 0  # one Newton group per call (group_len = n)
     nt = S * 11 * n if (want_tape and px.device.type != "cpu") else 0  # kTapeRows = 11
-    return (*outs, px.new_empty(ns, dtype=torch.int32), px.new_empty(nt, dtype=torch.float64))
+    return (*outs, px.new_empty(ns, dtype=torch.int32), px.new_empty(nt, dtype=torch.float64),
+            px.new_empty(() if want_rms else 0, dtype=torch.float64),
+            px.new_empty(5 if want_rms else 0, dtype=torch.float64))
 
 
 def _pupil_setup(ctx, inputs, output):
@@ -683,7 +704,9 @@ def _pupil_setup(ctx, inputs, output):
     ctx.shapes = [(p.shape, p.dtype, p.device) for p in params]
     ctx.has_apod = apod is not None
     ctx.set_materialize_grads(False)
-    saved = [*lens, seg, px.detach(), py.detach(), output[8], output[9], *output[:8]]
+    ctx.mark_non_differentiable(output[8], output[9], output[11])
+    saved = [*lens, seg, px.detach(), py.detach(), output[8], output[9], output[11],
+             *output[:8]]
     if apod is not None:
         saved.append(apod)
     ctx.save_for_backward(*saved)
@@ -693,9 +716,9 @@ def _pupil_backward(ctx, *grads):
     saved = ctx.saved_tensors
     nl = ctx.n_lens
     lens = list(saved[:nl])
-    seg, px, py, sched, tape = saved[nl:nl + 5]
-    primal = list(saved[nl + 5:nl + 13])
-    apod = saved[nl + 13] if ctx.has_apod else None
+    seg, px, py, sched, tape, rms_stats = saved[nl:nl + 6]
+    primal = list(saved[nl + 6:nl + 14])
+    apod = saved[nl + 14] if ctx.has_apod else None
     none_spec = [] if ctx.n_spec == 0 else None  # see _seq_backward
     nothing = ([None] * ctx.n_lens, None, None, None, None, None, None, None)
     if not any(ctx.needs_input_grad[8]) or not ctx.shapes:
@@ -709,9 +732,15 @@ def _pupil_backward(ctx, *grads):
     mode = vjp_mode(dl.table)
     tabs = _tables_cpu(zp, st, ft, slot_need(dl.table, zp, st, ft))
     cot = [None if gr is None else gr.to(torch.float64).contiguous() for gr in grads[:8]]
+    g_rms = grads[10] if _want_rms(ctx.plan_meta) else None  # (AOT: zeros of an empty output)
+    if g_rms is not None:
+        g_rms = g_rms.detach().to(torch.float64).reshape(1)
+    if all(c is None for c in cot) and g_rms is None:
+        return (*nothing, [None] * len(ctx.shapes), none_spec, None, None)
     g = torch.ops.ort.trace_pupil_vjp(lens, ctx.lens_meta, ctx.final_thickness, ctx.lens_key,
                                       seg, apod, px, py, sched, tape, primal, cot, tabs,
-                                      n_param, int(mode), ctx.plan_meta)
+                                      n_param, int(mode), ctx.plan_meta,
+                                      rms_stats if g_rms is not None else None, g_rms)
     res = []
     off = 0
     for shape, dtype, pdev in ctx.shapes:
@@ -730,13 +759,16 @@ def trace_pupil_vjp(lens: list[torch.Tensor], lens_meta: list[int], final_thickn
                     px: torch.Tensor, py: torch.Tensor, sched: torch.Tensor, tape: torch.Tensor,
                     primal: list[torch.Tensor], cot: list[torch.Tensor | None],
                     tables: list[torch.Tensor | None], n_param: int, mode: int,
-                    plan_meta: list[int]) -> torch.Tensor:
+                    plan_meta: list[int], rms_stats: torch.Tensor | None = None,
+                    g_rms: torch.Tensor | None = None) -> torch.Tensor:
     """ort_trace_pupil_vjp: grad [n_param] = J^T cot (the reverse sweep over `tape` when the
-    forward wrote one, else with its own re-trace)."""
+    forward wrote one, else with its own re-trace). rms_stats / g_rms: the forward's rms
+    spot size (its stats[5]) and its upstream gradient [1], folded into the x, y cotangents
+    of the adjoint (ort_vjp_params.rms_stats / rms_grad)."""
     from .autodiff import vjp
 
     dl = _resolve(lens, lens_meta, final_thickness, lens_key)
-    n, seg_len, ppr, _, _ = plan_meta
+    n, seg_len, ppr = plan_meta[:3]
     dev = dl.device
     tabs = tuple(None if t is None else dl.resident(("tangent", i), t.detach().cpu().numpy())
                  for i, t in enumerate(tables))
@@ -744,31 +776,39 @@ def trace_pupil_vjp(lens: list[torch.Tensor], lens_meta: list[int], final_thickn
     cot = [None if c is None else c.detach().to(device=dev, dtype=torch.float64).contiguous()
            for c in cot]
     taped = tape.numel() > 0 and mode == _abi.VJP_ADJOINT
+    rms = None
+    if g_rms is not None:
+        if rms_stats is None or mode != _abi.VJP_ADJOINT:
+            raise ValueError("ort::trace_pupil_vjp: g_rms needs rms_stats and the adjoint mode")
+        rms = (rms_stats.detach().to(dev).contiguous(), g_rms.detach().to(dev).contiguous())
     vjp(dl, seg, px, py, n, seg_len, sched if sched.numel() else None, tabs, n_param, cot, g,
         pupil_per_ray=bool(ppr), mode=mode, tape=tape if taped else None,
-        primal=primal if taped else None, overwrite=True)
+        primal=primal if taped else None, overwrite=True, rms=rms)
     return g
 
 
 @trace_pupil_vjp.register_kernel("cpu")
 def _trace_pupil_vjp_cpu(lens, lens_meta, final_thickness, lens_key, seg, apod, px, py, sched,
-                         tape, primal, cot, tables, n_param, mode, plan_meta):
+                         tape, primal, cot, tables, n_param, mode, plan_meta, rms_stats=None,
+                         g_rms=None):
     from . import host
 
     hl = _resolve(lens, lens_meta, final_thickness, lens_key)
-    n, seg_len, ppr, _, _ = plan_meta
+    n, seg_len, ppr = plan_meta[:3]
     zp, st, ft, need = (None if t is None else t.detach().contiguous() for t in tables)
     g = torch.empty(max(1, n_param), dtype=torch.float64)
     cot = [None if c is None else c.detach().to(torch.float64).contiguous() for c in cot]
     host.trace_pupil_vjp(hl, seg, px.detach().contiguous(), py.detach().contiguous(), n,
                          seg_len, bool(ppr), sched, (zp, st, ft),
-                         need if mode == _abi.VJP_ADJOINT else None, n_param, mode, cot, g, apod)
+                         need if mode == _abi.VJP_ADJOINT else None, n_param, mode, cot, g, apod,
+                         rms=None if g_rms is None else (rms_stats.detach().contiguous(),
+                                                         g_rms.detach().contiguous()))
     return g
 
 
 @trace_pupil_vjp.register_fake
 def _(lens, lens_meta, final_thickness, lens_key, seg, apod, px, py, sched, tape, primal, cot,
-      tables, n_param, mode, plan_meta):
+      tables, n_param, mode, plan_meta, rms_stats=None, g_rms=None):
     return px.new_empty(max(1, n_param), dtype=torch.float64)
 
 

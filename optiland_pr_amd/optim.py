@@ -73,8 +73,12 @@ class ZernikeAdam(torch.optim.Optimizer):
             a.exp_avg_sq[k] = st["exp_avg_sq"].data_ptr()
             a.row0[k] = int(off)
             a.count[k] = p.numel()
-        steps = self.state.setdefault(("steps", id(dl)), torch.zeros(
-            dl.table.n_surfaces, dtype=torch.float64, device=dl.device))
+        # (made once: a plan built inside a graph capture -- new grad tensors -- must not
+        # capture a fill that every replay would repeat)
+        steps = self.state.get(("steps", id(dl)))
+        if steps is None:
+            steps = torch.zeros(dl.table.n_surfaces, dtype=torch.float64, device=dl.device)
+            self.state[("steps", id(dl))] = steps
         a.step = steps.data_ptr()
         a.lr, a.beta1, a.beta2, a.eps, a.weight_decay = hyper
         hit = (a, [p for _, p in items])

@@ -390,6 +390,29 @@ class NewtonScheduleError(RuntimeError):
     pass
 
 
+# RayOperand.rms_spot_size's request for the fused rms (operands.py): while a dict, the
+# differentiable single-wavelength trace (RealRayTracer._trace_grad) computes the rms of
+# its final points in the taped forward's epilogue and leaves the autograd-connected
+# scalar under "rms" (first trace only); the operand falls back to ort::rms_spot otherwise
+RMS_REQUEST = None
+
+
+class fused_rms:
+    """with fused_rms() as req: optic.trace(...) -> req.get("rms"): the rms spot size of
+    the traced image points when the trace could fuse it, else None."""
+
+    def __enter__(self):
+        global RMS_REQUEST
+        self._prev = RMS_REQUEST
+        RMS_REQUEST = {}
+        return RMS_REQUEST
+
+    def __exit__(self, *exc):
+        global RMS_REQUEST
+        RMS_REQUEST = self._prev
+        return False
+
+
 _PENDING_LENSES: "weakref.WeakSet" = None
 
 
@@ -675,11 +698,14 @@ def upload_segments(segments: np.ndarray, device):
 
 def trace_pupil(dlens: DeviceLens, segments, px, py, out: RealRays, n_rays,
                 seg_len, group_len, pupil_per_ray=False, keys=(), rec=None,
-                newton_mode="reference", start_surface=0, tape=None, exact_only=False):
+                newton_mode="reference", start_surface=0, tape=None, exact_only=False, rms=None):
     """Generate + trace in one launch (ort_trace_pupil). `segments` is a host SEGMENT array
     or the device tensor returned by upload_segments (no per-call copy). tape: a device
     buffer of ort_vjp_tape_size bytes the launch writes the adjoint tape into (Newton
-    lenses; the backward then runs the reverse sweep only)."""
+    lenses; the backward then runs the reverse sweep only). rms: (rms [], stats [5]) device
+    tensors that receive RayOperand.rms_spot_size of the final points: the taped kernel's
+    epilogue writes its workgroup rows (ort_options.rms_part), one ort_rms_finish launch
+    combines them (needs the tape and one wavelength)."""
     lib = _native.load()
     seg_dev = (segments if torch.is_tensor(segments) else
                dlens.resident("segments", np.asarray(segments, dtype=_abi.SEGMENT)))
@@ -691,16 +717,27 @@ def trace_pupil(dlens: DeviceLens, segments, px, py, out: RealRays, n_rays,
     stream = _stream_handle()  # one stream for all the launches of this call
     args = (C.byref(dlens.c), _ptr(px), _ptr(py), C.byref(out_c), C.byref(batch))
     rec_p, tape_p = _ptr(rec), _addr(tape)
+    rows = -(-int(n_rays) // 256)  # one row per trace workgroup (kBlock)
+    part = None
+    if rms is not None:
+        if tape is None:
+            raise ValueError("trace_pupil: the fused rms spot size needs the taped forward")
+        part = torch.empty(rows * 4, dtype=torch.float64, device=dlens.device)
+    part_p = _addr(part)
 
     def launch(opt, stats, status):
         opt.start_surface = start_surface
         opt.tape = tape_p
+        opt.rms_part = part_p
         if exact_only:
             opt.flags |= _abi.OPT_EXACT
         rc = lib.ort_trace_pupil(*args, C.byref(opt), rec_p, _ptr(stats), _ptr(status), stream)
         _native.check(rc, "ort_trace_pupil")
 
     _run(dlens, launch, n_rays, group_len, list(keys), newton_mode)
+    if rms is not None and n_rays > 0:
+        rc = lib.ort_rms_finish(_ptr(part), rows, _ptr(rms[1]), _ptr(rms[0]), stream)
+        _native.check(rc, "ort_rms_finish")
     return seg_dev
 
 
@@ -954,8 +991,12 @@ class RealRayTracer:
         # per step, and no launch for it inside a captured step)
         w = dlens.resident(("w_const", float(wavelength)),
                            np.array([float(wavelength)])).expand(n)
+        want_rms = RMS_REQUEST is not None and RMS_REQUEST.get("rms") is None
         outs = autodiff.trace_pupil_grad(self.optic, dlens, seg_dev, px, py, n, n_p,
-                                         wavelength, keys, newton_mode)
+                                         wavelength, keys, newton_mode, want_rms=want_rms)
+        if want_rms and outs[8].dim() == 0:  # the trace took it (the taped single-λ path)
+            RMS_REQUEST["rms"] = outs[8]
+        outs = outs[:8]
         out = RealRays.__new__(RealRays)
         for a, t in zip(_abi.RAY_FIELDS, outs, strict=True):
             setattr(out, a, t)

@@ -202,3 +202,54 @@ def test_device_rounds_reuse_their_buffers(torch):
     assert len({c.data_ptr() for c in copies}) == len(copies)  # one live copy per call
     for c in copies:
         assert torch.equal(c, copies[0])
+
+
+@pytest.mark.parametrize("offset", [+5, -1])
+def test_taped_rounds_stride_and_correct(torch, offset):
+    """The config-5 step (taped forward, fused rms) with more rays than one grid of the
+    verify rounds covers (kVerifyGrid = 1024 workgroups = 262,144 rays; 600,000 here, so
+    the F_STRIDE kernels loop): a wrong warm schedule is corrected by re-traces in those
+    rounds, and loss and gradients equal the host-verified step bit for bit."""
+    from optiland_pr_amd import raytrace
+    from optiland_pr_amd.distribution import RandomDistribution
+    from optiland_pr_amd.operands import RayOperand
+    from optiland_pr_amd.samples import ThreeMirrorAnastigmat
+
+    n = 600_000
+    d = RandomDistribution(seed=5)
+    d.generate_points(n)
+    res = {}
+    for mode in ("reference", "device"):
+        lens = ThreeMirrorAnastigmat()
+        lens.newton_mode = mode
+        leaves = []
+        for si in (1, 2, 3):
+            g = lens.surface_group.surfaces[si].geometry
+            t = torch.tensor(np.asarray(g.coefficients), dtype=torch.float64, device="cuda",
+                             requires_grad=True)
+            g.coefficients = t
+            leaves.append(t)
+
+        def step():
+            for t in leaves:
+                t.grad = None
+            loss = RayOperand.rms_spot_size(lens, -1, 0.0, 1.0, n, 0.587, d)
+            loss.backward()
+            return loss
+
+        step()  # warm (host-verified)
+        if mode == "device":
+            dl = _dlens(lens, 0.587)
+            for k, v in list(dl.sched_cache.items()):
+                if k == "_default":
+                    continue
+                bad = v.copy()
+                for s in dl.newton:
+                    bad[s] = max(0, int(v[s]) + offset)
+                dl.sched_cache[k] = bad
+            dl._dev_sched.clear()
+        loss = step()
+        raytrace.check_all_pending()
+        res[mode] = (float(loss), np.concatenate([t.grad.cpu().numpy() for t in leaves]))
+    assert res["device"][0] == res["reference"][0]
+    np.testing.assert_array_equal(res["device"][1], res["reference"][1])

@@ -139,3 +139,29 @@ def test_compile_fullgraph_trace_sequential_cpu():
     compiled = torch.compile(f, fullgraph=True, backend="aot_eager")(L, fields)
     for u, v in zip(eager, compiled, strict=True):
         assert torch.equal(u, v)
+
+
+def test_trace_pupil_fused_rms_cpu():
+    """plan_meta's want_rms (the rms spot size computed by the trace op, its gradient folded
+    into the trace's VJP as ort_vjp_params.rms_stats / rms_grad) against the same trace
+    followed by ort::rms_spot: value and coefficient gradients agree."""
+    spec = (("zernike", 1), ("zernike", 3))
+    _, args = _pupil_args("tma_fringe", spec, n_p=53)
+    L, meta, ft, key, seg_t, apod, px, py, leaves, sp, pmeta, pkey = args
+    fused = torch.ops.ort.trace_pupil(L, meta, ft, key, seg_t, apod, px, py, leaves, sp,
+                                      pmeta + [1], pkey)
+    assert fused[10].dim() == 0 and fused[11].numel() == 5
+    g_fused = torch.autograd.grad(fused[10], leaves)
+    plain = torch.ops.ort.trace_pupil(*args)
+    assert plain[10].numel() == 0
+    rms = torch.ops.ort.rms_spot(plain[0], plain[1])[0]
+    g_plain = torch.autograd.grad(rms, leaves)
+    np.testing.assert_allclose(float(fused[10]), float(rms), rtol=1e-14)
+    for a, b in zip(g_fused, g_plain, strict=True):
+        np.testing.assert_allclose(a.numpy(), b.numpy(), rtol=1e-12, atol=1e-18)
+
+
+def test_opcheck_trace_pupil_fused_rms_cpu():
+    _, args = _pupil_args("tma_fringe", (("zernike", 1),), n_p=29)
+    args = (*args[:10], args[10] + [1], args[11])
+    _assert_opcheck(torch.ops.ort.trace_pupil.default, args)
