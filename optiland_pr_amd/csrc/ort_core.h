@@ -346,6 +346,40 @@ ORT_INLINE void unit_normal3(const T& dzdx, const T& dzdy, const T& norm, T& nx,
   nz = sdiv(-1.0, sd);
 }
 
+// What a Newton geometry's evaluation returns besides the sag (want_normal):
+//   kNoNormal  the sag alone;
+//   kNormal    the unit normal (nx, ny, nz) of the interaction (and of the reference's
+//              update, newton_raphson.py:150-157);
+//   kSlope     the update's slopes (fx, fy, -1): the reference forms fx = -nx / nz_safe,
+//              fy = -ny / nz_safe from the unit normal (nz_safe = nz floored at 1e-14 in
+//              magnitude). With n = (dz/dx, dz/dy, -1) / norm that is dz/dx, dz/dy up to
+//              the rounding of the normalisation, so the update takes the slopes directly
+//              -- no norm, no four quotients -- while norm < 1e14 (norm^2 < 1e28). A
+//              steeper normal (where the floor matters) or NaN: the even / odd / Zernike
+//              kinds return the unit normal itself (nz != -1 tells it apart: nz = -1 / norm),
+//              the freeform kinds the reference's (fx, fy, -1) from it; newton_step_any
+//              and normal_of take either. Newton surfaces are held to 1e-9 mm and the
+//              reference's update counts, not to bit-exactness (the stop rule compares
+//              |f| with tol, far from the rounding of one step).
+enum : int { kNoNormal = 0, kNormal = 1, kSlope = 2 };
+
+// (fx, fy, -1) of the reference's update from a unit normal
+template <class T>
+ORT_INLINE void slope_from_normal(T& nx, T& ny, T& nz) {
+  const T nzs = ::fabs(vv(nz)) > 1e-14 ? nz : T(1e-14);
+  T fx, fy;
+  div2(T(-nx), T(-ny), nzs, fx, fy);
+  nx = fx;
+  ny = fy;
+  nz = T(-1.0);
+}
+
+// kSlope's direct form applies (norm^2 = dz/dx^2 + dz/dy^2 + 1 < 1e28, not NaN)
+template <class T>
+ORT_INLINE bool slope_direct(const T& dzdx, const T& dzdy) {
+  return vv(dzdx * dzdx + dzdy * dzdy + 1.0) < 1e28;
+}
+
 // Zernike coefficient tangent seeds for the derivative kernels: term j (global index in
 // lens.zern) is parameter param[j] (< 0: not differentiated); tangent slot k of this
 // launch is parameter p0 + k.
@@ -659,7 +693,7 @@ ORT_INLINE void even_horner(const T& r2, PD C, int nc, T& P, T& D) {
 
 template <class T, class S, class PD>
 ORT_INLINE T sagnorm_even(const T& x, const T& y, const S& R, const S& k, PD C, int nc,
-                          bool want_normal, T& nx, T& ny, T& nz) {
+                          int want_normal, T& nx, T& ny, T& nz) {
   const T r2 = x * x + y * y;
   const T q = sqrt(1.0 - (1.0 + k) * r2 / (R * R));
   T P, D;
@@ -671,6 +705,12 @@ ORT_INLINE T sagnorm_even(const T& x, const T& y, const S& R, const S& k, PD C, 
     div2(x, y, denom, dfdx, dfdy);
     dfdx = dfdx + x * D;
     dfdy = dfdy + y * D;
+    if (want_normal == kSlope && slope_direct(dfdx, dfdy)) {
+      nx = dfdx;
+      ny = dfdy;
+      nz = T(-1.0);
+      return z;
+    }
     const T mag = sqrt(dfdx * dfdx + dfdy * dfdy + 1.0);
     unit_normal3(dfdx, dfdy, mag, nx, ny, nz);
   }
@@ -681,7 +721,7 @@ ORT_INLINE T sagnorm_even(const T& x, const T& y, const S& R, const S& k, PD C, 
 // :112-122)
 template <class T, class S, class PD>
 ORT_INLINE T sagnorm_odd(const T& x, const T& y, const S& R, const S& k, PD C, int nc,
-                         bool want_normal, T& nx, T& ny, T& nz) {
+                         int want_normal, T& nx, T& ny, T& nz) {
   const T r2 = x * x + y * y;
   const T r = sqrt(r2);
   const T q = sqrt(1.0 - (1.0 + k) * r2 / (R * R));
@@ -705,6 +745,12 @@ ORT_INLINE T sagnorm_odd(const T& x, const T& y, const S& R, const S& k, PD C, i
       rq = (i == 0) ? T(1.0) : (i == 1 ? r : rq * r);
       dfdx = dfdx + xt;
       dfdy = dfdy + yt;
+    }
+    if (want_normal == kSlope && slope_direct(dfdx, dfdy)) {
+      nx = dfdx;
+      ny = dfdy;
+      nz = T(-1.0);
+      return z;
     }
     const T mag = sqrt(dfdx * dfdx + dfdy * dfdy + 1.0);
     unit_normal3(dfdx, dfdy, mag, nx, ny, nz);
@@ -1130,7 +1176,7 @@ ORT_INLINE void zmono_hess(PD A, int N, double x, double y, double& F, double& F
 // normalisation constant: reference quirk)
 template <class T, class S, class PD, class PZ>
 ORT_INLINE T sagnorm_zernike(const T& x, const T& y, const S& R, const S& k, double Rn, PZ Tm,
-                             int t0, int nt, PD coef, const ZSeed& zs, bool want_normal,
+                             int t0, int nt, PD coef, const ZSeed& zs, int want_normal,
                              bool& range_error, T& nx, T& ny, T& nz, int zm_off = 0,
                              int zm_deg = -1) {
   if constexpr (IsPlain<T>::value && IsPlain<S>::value) {
@@ -1163,6 +1209,12 @@ ORT_INLINE T sagnorm_zernike(const T& x, const T& y, const S& R, const S& k, dou
         const double Fr = rho > 0.0 ? G1 / rho : 0.0;
         dzdx = dzdx + (Fr * drho_dx + G2 * (qy * inv_rn));
         dzdy = dzdy + (Fr * drho_dy + G2 * (qx * inv_rn));
+        if (want_normal == kSlope && slope_direct(dzdx, dzdy)) {
+          nx = dzdx;
+          ny = dzdy;
+          nz = -1.0;
+          return z + F;
+        }
         double norm = sqrt(dzdx * dzdx + dzdy * dzdy + 1.0);
         norm = norm < eps ? 1.0 : norm;
         unit_normal3(dzdx, dzdy, norm, nx, ny, nz);
@@ -1253,6 +1305,12 @@ ORT_INLINE T sagnorm_zernike(const T& x, const T& y, const S& R, const S& k, dou
     }
   }
   if (want_normal) {
+    if (want_normal == kSlope && slope_direct(dzdx, dzdy)) {
+      nx = dzdx;
+      ny = dzdy;
+      nz = T(-1.0);
+      return z + total;
+    }
     T norm = sqrt(dzdx * dzdx + dzdy * dzdy + 1.0);
     norm = vv(norm) < eps ? T(1.0) : norm;
     unit_normal3(dzdx, dzdy, norm, nx, ny, nz);
@@ -1887,7 +1945,7 @@ enum : unsigned { KM_EVEN = 1u, KM_ODD = 2u, KM_ZERN = 4u, KM_FREE = 8u };
 // R, K: the surface's radius and conic (double, or seeded duals in the derivative kernels)
 template <unsigned KM, class T, class S, class PD, class PZ>
 ORT_INLINE T newton_sagnorm(const ort_surface& s, const S& R, const S& K, PD coef, PZ zern,
-                            const ZSeed& zs, const T& x, const T& y, bool want_normal,
+                            const ZSeed& zs, const T& x, const T& y, int want_normal,
                             bool& range_error, T& nx, T& ny, T& nz) {
   const PD C = coef + s.coef_off;
   if constexpr ((KM & KM_EVEN) != 0) {
@@ -1904,35 +1962,44 @@ ORT_INLINE T newton_sagnorm(const ort_surface& s, const S& R, const S& K, PD coe
                              want_normal, range_error, nx, ny, nz, s.zm_off, s.zm_deg);
   }
   if constexpr ((KM & KM_FREE) != 0) {
+    // the freeform kinds form the unit normal; kSlope's (fx, fy, -1) from it
+    const bool wn = want_normal != kNoNormal;
+    T z;
     switch (s.geometry) {
       case ORT_GEOM_POLYNOMIAL:
-        return sagnorm_poly(x, y, R, K, C, want_normal, nx, ny, nz);
+        z = sagnorm_poly(x, y, R, K, C, wn, nx, ny, nz);
+        break;
       case ORT_GEOM_CHEBYSHEV: {
         bool cerr = false;
-        const T z = sagnorm_cheb(x, y, R, K, C, want_normal, cerr, nx, ny, nz);
+        z = sagnorm_cheb(x, y, R, K, C, wn, cerr, nx, ny, nz);
         if (cerr) range_error = true;
-        return z;
+        break;
       }
       case ORT_GEOM_BICONIC:
-        return sagnorm_biconic(x, y, C, want_normal, nx, ny, nz);
+        z = sagnorm_biconic(x, y, C, wn, nx, ny, nz);
+        break;
       case ORT_GEOM_FORBES_QBFS:
-        return sagnorm_qbfs(x, y, R, K, (s.flags & ORT_SURF_RADIUS_INF) != 0, C, want_normal,
-                            nx, ny, nz);
+        z = sagnorm_qbfs(x, y, R, K, (s.flags & ORT_SURF_RADIUS_INF) != 0, C, wn, nx, ny, nz);
+        break;
       case ORT_GEOM_FORBES_Q2D:
-        return sagnorm_q2d(x, y, R, K, (s.flags & ORT_SURF_RADIUS_INF) != 0, C, want_normal,
-                           nx, ny, nz);
+        z = sagnorm_q2d(x, y, R, K, (s.flags & ORT_SURF_RADIUS_INF) != 0, C, wn, nx, ny, nz);
+        break;
       case ORT_GEOM_GRID_SAG:  // primal kernels only (no derivative kernels for grids)
         if constexpr (std::is_same<T, double>::value) {
-          return sagnorm_grid(grid_view(C), x, y, want_normal, nx, ny, nz);
+          z = sagnorm_grid(grid_view(C), x, y, wn, nx, ny, nz);
         } else {
-          nx = ny = nz = T(NAN);
-          return T(NAN);
+          nx = ny = nz = z = T(NAN);
         }
-      case ORT_GEOM_TOROIDAL:
-        return sagnorm_toroidal(x, y, C, want_normal, nx, ny, nz);
-      default:  // an id this library does not know: NaN, never another kind's sag
         break;
+      case ORT_GEOM_TOROIDAL:
+        z = sagnorm_toroidal(x, y, C, wn, nx, ny, nz);
+        break;
+      default:  // an id this library does not know: NaN, never another kind's sag
+        nx = ny = nz = T(NAN);
+        return T(NAN);
     }
+    if (want_normal == kSlope) slope_from_normal(nx, ny, nz);
+    return z;
   }
   nx = ny = nz = T(NAN);
   return T(NAN);
@@ -1949,7 +2016,7 @@ ORT_INLINE void newton_normal(const ort_surface& s, const S& R, const S& K, PD c
 // and, with want_normal, the normal at P(t) for the update.
 template <unsigned KM, class T, class S, class PD, class PZ>
 ORT_INLINE T newton_eval(const ort_surface& s, const S& R, const S& K, PD coef, PZ zern,
-                         const ZSeed& zs, const RayT<T>& r, const T& t, bool want_normal,
+                         const ZSeed& zs, const RayT<T>& r, const T& t, int want_normal,
                          bool& range_error, T& nx, T& ny, T& nz) {
   const T xi = r.x + t * r.L;
   const T yi = r.y + t * r.M;
@@ -1958,16 +2025,29 @@ ORT_INLINE T newton_eval(const ort_surface& s, const S& R, const S& K, PD coef, 
                             nz) - zi;
 }
 
-// newton_raphson.py:154-166: t_new = t - f / f'(t) from the normal at P(t)
+// newton_raphson.py:154-166: t_new = t - f / f'(t) from the update's slopes (fx, fy) at
+// P(t) (an evaluation with want_normal = kSlope)
 template <class T>
-ORT_INLINE T newton_step(const RayT<T>& r, const T& t, const T& f, const T& nx, const T& ny,
-                         const T& nz) {
-  const T nzs = ::fabs(vv(nz)) > 1e-14 ? nz : T(1e-14);
-  T fx, fy;
-  div2(T(-nx), T(-ny), nzs, fx, fy);
+ORT_INLINE T newton_step_slope(const RayT<T>& r, const T& t, const T& f, const T& fx,
+                               const T& fy) {
   const T df = fx * r.L + fy * r.M - r.N;
   const T dfs = ::fabs(vv(df)) > 1e-14 ? df : T(1e-14);
   return t - f / dfs;
+}
+
+// the same from a unit normal (the reference's own form)
+template <class T>
+ORT_INLINE T newton_step(const RayT<T>& r, const T& t, const T& f, T nx, T ny, T nz) {
+  slope_from_normal(nx, ny, nz);
+  return newton_step_slope(r, t, f, nx, ny);
+}
+
+// the update from a kSlope evaluation: its slopes (nz == -1) or its unit normal
+template <class T>
+ORT_INLINE T newton_step_any(const RayT<T>& r, const T& t, const T& f, const T& nx,
+                             const T& ny, const T& nz) {
+  if (vv(nz) == -1.0) return newton_step_slope(r, t, f, nx, ny);
+  return newton_step(r, t, f, nx, ny, nz);
 }
 
 // ---------------------------------------------------------------------------------

@@ -368,11 +368,34 @@ ORT_INLINE double quot_signed(double a, const SharedDiv& d) {
 // numerator in range or an exact zero of either sign (quot_signed / quot_pos keep its sign)
 ORT_INLINE bool num_ok0(double a) { return num_ok(a) || a == 0.0; }
 
+// kSlope's direct slopes (ort_core.h): norm^2 < 1e28 checked (a steeper normal or NaN
+// takes the exact path, which forms the reference's expression from the unit normal)
+ORT_INLINE void slope_out(double dfdx, double dfdy, double& nx, double& ny, double& nz,
+                          bool& bad) {
+  ORT_CHK(bad, !(dfdx * dfdx + dfdy * dfdy + 1.0 < 1e28));
+  nx = dfdx;
+  ny = dfdy;
+  nz = -1.0;
+}
+
+// the unit normal (dz/dx, dz/dy, -1) / norm from kSlope's direct slopes (norm^2 < 1e28
+// checked by slope_out): the tail of the kNormal evaluations, operation for operation
+ORT_INLINE void unit_normal_from_slope(double dfdx, double dfdy, double& nx, double& ny,
+                                       double& nz, bool& bad) {
+  const double mag = sqrt_ge1(dfdx * dfdx + dfdy * dfdy + 1.0, bad);
+  const SharedDiv dm = shared_div_ge1(mag, bad);
+  ORT_CHK(bad, !(num_ok0(dfdx) && num_ok0(dfdy)));
+  nx = quot_pos(dfdx, dm);
+  ny = quot_pos(dfdy, dm);
+  nz = quot(-1.0, dm);
+}
+
 // even_asphere.py:82-129 (ort_core.h sagnorm_even): the same operations in the same order,
-// the divisions and square roots as the deferred-check sequences
+// the divisions and square roots as the deferred-check sequences; mode: kNormal or kSlope
 template <class PD>
 ORT_INLINE double sagnorm_even(double x, double y, const ort_surface& s, PD C,
-                               int nc, double& nx, double& ny, double& nz, bool& bad) {
+                               int nc, int mode, double& nx, double& ny, double& nz,
+                               bool& bad) {
   const double R = s.radius;
   const double r2 = x * x + y * y;
   const double a = ORT_ONE_PLUS_K(s) * r2;  // (1 + k) r2: +-0 at the vertex
@@ -390,6 +413,10 @@ ORT_INLINE double sagnorm_even(double x, double y, const ort_surface& s, PD C,
   double dfdy = quot_signed(y, dd);
   dfdx = dfdx + x * D;
   dfdy = dfdy + y * D;
+  if (mode == kSlope) {
+    slope_out(dfdx, dfdy, nx, ny, nz, bad);
+    return z;
+  }
   const double mag = sqrt_ge1(dfdx * dfdx + dfdy * dfdy + 1.0, bad);
   const SharedDiv dm = shared_div_ge1(mag, bad);
   ORT_CHK(bad, !(num_ok0(dfdx) && num_ok0(dfdy)));
@@ -402,7 +429,8 @@ ORT_INLINE double sagnorm_even(double x, double y, const ort_surface& s, PD C,
 // odd_asphere.py:73-130 (ort_core.h sagnorm_odd); non-finite per-term slopes zeroed
 template <class PD>
 ORT_INLINE double sagnorm_odd(double x, double y, const ort_surface& s, PD C,
-                              int nc, double& nx, double& ny, double& nz, bool& bad) {
+                              int nc, int mode, double& nx, double& ny, double& nz,
+                              bool& bad) {
   const double R = s.radius;
   const double r2 = x * x + y * y;
   const double r = sqrt(r2, bad);  // the vertex itself (r2 = 0) takes the exact path
@@ -434,6 +462,10 @@ ORT_INLINE double sagnorm_odd(double x, double y, const ort_surface& s, PD C,
     dfdx = dfdx + xt;
     dfdy = dfdy + yt;
   }
+  if (mode == kSlope) {
+    slope_out(dfdx, dfdy, nx, ny, nz, bad);
+    return z;
+  }
   const double mag = sqrt_ge1(dfdx * dfdx + dfdy * dfdy + 1.0, bad);
   const SharedDiv dm = shared_div_ge1(mag, bad);
   ORT_CHK(bad, !(num_ok0(dfdx) && num_ok0(dfdy)));
@@ -441,6 +473,16 @@ ORT_INLINE double sagnorm_odd(double x, double y, const ort_surface& s, PD C,
   ny = quot_pos(dfdy, dm);
   nz = quot(-1.0, dm);
   return z;
+}
+
+// newton_raphson.py:154-166 from kSlope's slopes (ort_core.h newton_step_slope)
+ORT_INLINE double newton_step_slope(const Ray& r, double t, double f, double fx, double fy,
+                                    bool& bad) {
+  const double df = fx * r.L + fy * r.M - r.N;
+  const double dfs = ::fabs(df) > 1e-14 ? df : 1e-14;
+  const SharedDiv dd = shared_div(dfs, bad);
+  ORT_CHK(bad, !num_ok0(f));
+  return t - quot_signed(f, dd);
 }
 
 // newton_raphson.py:154-166 (ort_core.h newton_step)

@@ -164,7 +164,8 @@ void trace_group(const KArgs& a, int64_t r0, int64_t r1, int32_t* updates, int& 
         for (int64_t k = 0; k < n; ++k) {
           bool rerr = false;
           f[k] = ort::newton_eval<kAllKinds>(s, s.radius, s.conic, a.coef, a.zern, kNoSeed,
-                                             rays[k], t[k], true, rerr, nx[k], ny[k], nz[k]);
+                                             rays[k], t[k], ort::kSlope, rerr, nx[k], ny[k],
+                                             nz[k]);
           // the reference evaluates the sag at j = 0 .. max_iter - 1 only
           if (rerr && j < s.max_iter) rbits |= rb;
           const double v = fabs(f[k]);
@@ -177,7 +178,7 @@ void trace_group(const KArgs& a, int64_t r0, int64_t r1, int32_t* updates, int& 
         if (j >= s.max_iter || (!nan && fmax < s.tol)) break;
 #pragma omp parallel for num_threads(nt) schedule(static)
         for (int64_t k = 0; k < n; ++k)
-          t[k] = ort::newton_step(rays[k], t[k], f[k], nx[k], ny[k], nz[k]);
+          t[k] = ort::newton_step_any(rays[k], t[k], f[k], nx[k], ny[k], nz[k]);
       }
       if (updates) updates[si] = j;
     }

@@ -138,30 +138,48 @@ __global__ __launch_bounds__(kBlock) void newton_finish_kernel(
     int32_t rounds, int32_t conv_base, int32_t* sched, int32_t* flags, int32_t* statuses,
     int32_t* status_out, int32_t* sched_copy) {
   __shared__ int32_t codes[kBlock / 64];
+  __shared__ int32_t ran_last;
   const int64_t ngs = n_groups * n_surf;
+  // the flags, the statuses and (the usual case: the last round did not run) the settled
+  // schedule are loaded together up front: one memory round trip, not a chain of them
+  const int t = threadIdx.x;
   const int32_t prev = flags[rounds - 1];
+  const bool ran = t >= 1 && t <= rounds && flags[t - 1] == 1;  // round t ran
+  const int32_t st_t = t <= rounds ? statuses[t] : 0;
+  constexpr int kPre = 4;
+  int32_t sc[kPre];
+#pragma unroll
+  for (int q = 0; q < kPre; ++q) {
+    const int64_t k = t + (int64_t)q * kBlock;
+    sc[q] = k < ngs ? sched[k] : 0;
+  }
+  if (t == 0) ran_last = 0;  // round 0 always runs
+  __syncthreads();
+  if (ran) atomicMax(&ran_last, t);  // the last round that ran (order-free: a max)
   if (prev == 1) {  // the last round ran: check its statistics (block-uniform branch)
     const int c = newton_decide(surf, n_surf, n_groups, stats + (int64_t)rounds * ngs,
                                 conv_base, sched, codes);
-    if (threadIdx.x == 0) flags[rounds] = c;
-  } else if (threadIdx.x == 0) {
+    if (t == 0) flags[rounds] = c;
+  } else if (t == 0) {
     flags[rounds] = prev;  // settled (0) or undecidable (2) stays so
   }
-  int32_t st = 0;
-  if (threadIdx.x == 0) {
-    int last = 0;  // round 0 always runs; round r ran when flags[r - 1] == 1
-    for (int r = 1; r <= rounds; ++r)
-      if (flags[r - 1] == 1) last = r;
-    st = statuses[last];
-  }
   __syncthreads();  // every read of stats / statuses / sched is done
-  if (threadIdx.x == 0) *status_out = st;
-  for (int r = threadIdx.x; r <= rounds; r += kBlock) statuses[r] = 0;
+  if (t == ran_last) *status_out = st_t;
+  for (int r = t; r <= rounds; r += kBlock) statuses[r] = 0;
   const int64_t words = (int64_t)(rounds + 1) * ngs * (int64_t)(sizeof(ort_newton_stat) / 8);
   uint64_t* w = reinterpret_cast<uint64_t*>(stats);
-  for (int64_t k = threadIdx.x; k < words; k += kBlock) w[k] = ~0ull;
-  if (sched_copy)
-    for (int64_t k = threadIdx.x; k < ngs; k += kBlock) sched_copy[k] = sched[k];
+  for (int64_t k = t; k < words; k += kBlock) w[k] = ~0ull;
+  if (sched_copy) {
+    if (prev != 1 && ngs <= kPre * kBlock) {  // the schedule was not changed here
+#pragma unroll
+      for (int q = 0; q < kPre; ++q) {
+        const int64_t k = t + (int64_t)q * kBlock;
+        if (k < ngs) sched_copy[k] = sc[q];
+      }
+    } else {
+      for (int64_t k = t; k < ngs; k += kBlock) sched_copy[k] = sched[k];
+    }
+  }
 }
 
 }  // namespace ortk
@@ -176,6 +194,7 @@ extern "C" int ort_newton_finish(const ort_lens* lens, int64_t n_groups, ort_new
     return ORT_ERR_ARG;
   if (lens->n_surfaces < 1 || lens->n_surfaces > ORT_MAX_SURFACES || !lens->surfaces)
     return ORT_ERR_ARG;
+  if (rounds >= kBlock) return ORT_ERR_ARG;  // one thread per round's flag and status
   hipLaunchKernelGGL(newton_finish_kernel, dim3(1), dim3(kBlock), 0, (hipStream_t)stream,
                      lens->surfaces, lens->n_surfaces, n_groups, stats, rounds, conv_base, sched,
                      flags, statuses, status_out, sched_copy);

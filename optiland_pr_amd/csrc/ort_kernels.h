@@ -260,8 +260,8 @@ __device__ inline double grid_distance(const KArgs& a, const ort_surface& s, int
 // then are bit-identical to the exact path's, and the exact pass reports the bad lanes
 template <uint32_t FEAT, bool FAST>
 __device__ inline __attribute__((always_inline)) double newton_eval_fast(const KArgs& a, const ort_surface& s,
-                                          const ort::Ray& r, double t, bool& rerr, double& nx,
-                                          double& ny, double& nz, bool& bad) {
+                                          const ort::Ray& r, double t, int mode, bool& rerr,
+                                          double& nx, double& ny, double& nz, bool& bad) {
   constexpr uint32_t KM = FEAT & F_KM;
   if constexpr (FAST && (KM & (ort::KM_EVEN | ort::KM_ODD)) != 0) {
     const double xi = r.x + t * r.L;
@@ -269,18 +269,20 @@ __device__ inline __attribute__((always_inline)) double newton_eval_fast(const K
     const double zi = r.z + t * r.N;
     double sag;
     if ((KM & ort::KM_EVEN) != 0 && (KM == ort::KM_EVEN || s.geometry == ORT_GEOM_EVEN_ASPHERE))
-      sag = ort::fast::sagnorm_even(xi, yi, s, cst(a.coef) + s.coef_off, s.n_coef, nx, ny, nz, bad);
+      sag = ort::fast::sagnorm_even(xi, yi, s, cst(a.coef) + s.coef_off, s.n_coef, mode, nx, ny,
+                                    nz, bad);
     else if ((KM & ort::KM_ODD) != 0 && ((KM & ~ort::KM_ODD) == 0 || s.geometry == ORT_GEOM_ODD_ASPHERE))
-      sag = ort::fast::sagnorm_odd(xi, yi, s, cst(a.coef) + s.coef_off, s.n_coef, nx, ny, nz, bad);
+      sag = ort::fast::sagnorm_odd(xi, yi, s, cst(a.coef) + s.coef_off, s.n_coef, mode, nx, ny,
+                                   nz, bad);
     else
       sag = ort::newton_sagnorm<KM>(s, s.radius, s.conic, cst(a.coef), cst(a.zern), kNoSeed, xi,
-                                    yi, true, rerr, nx, ny, nz);
+                                    yi, mode, rerr, nx, ny, nz);
     const double f = sag - zi;
     ORT_CHK(bad, !(::fabs(f) < 0x1p1000));
     return f;
   } else {
     return ort::newton_eval<KM>(s, s.radius, s.conic, cst(a.coef), cst(a.zern), kNoSeed, r, t,
-                                true, rerr, nx, ny, nz);
+                                mode, rerr, nx, ny, nz);
   }
 }
 
@@ -307,22 +309,23 @@ __device__ inline __attribute__((always_inline)) double newton_distance(const KA
   if (a.newton_mode == ORT_NEWTON_WAVE) {
     // Per-wave global rule: every lane of the wave does the same number of updates,
     // the wave stops at the first j where all its (non-NaN) lanes have |f| < tol.
+    // (the evaluations give the update's slopes; the unit normal once at the stop)
     int j = 0;
     for (; j < max_iter; ++j) {
       bool rerr = false;
       double nx, ny, nz;
       const double f = ort::newton_eval<(FEAT & F_KM)>(s, s.radius, s.conic, cst(a.coef), cst(a.zern), kNoSeed, r,
-                                                      t, true, rerr, nx, ny, nz);
+                                                      t, ort::kSlope, rerr, nx, ny, nz);
       if (active && rerr) range_bits |= range_bit(s);
       const bool conv = !active || !(fabs(f) >= tol);
       if (__all(conv)) {
+        bool rerr2 = false;
+        (void)ort::newton_eval<(FEAT & F_KM)>(s, s.radius, s.conic, cst(a.coef), cst(a.zern),
+                                              kNoSeed, r, t, ort::kNormal, rerr2, nnx, nny, nnz);
         hn = true;
-        nnx = nx;
-        nny = ny;
-        nnz = nz;
         break;
       }
-      t = ort::newton_step(r, t, f, nx, ny, nz);
+      t = ort::newton_step_any(r, t, f, nx, ny, nz);
     }
     if (a.stats && (threadIdx.x & 63) == 0)
       max_if_changes(&a.stats[(group_uniform ? group : 0) * a.n_surf + si].max_updates, j);
@@ -332,15 +335,26 @@ __device__ inline __attribute__((always_inline)) double newton_distance(const KA
   const int U = sched ? sched[group * a.n_surf + si] : max_iter;
   ConvBits mask;
   int last_bad = -1;
+  // Every evaluation is one call site (the kernel's code size is its hot loop): at j < U
+  // sag + the update's slopes at P(t) (kSlope) and the update; at j = U (the stop test)
+  // the same evaluation, the interaction's unit normal formed from those slopes -- for the
+  // even / odd / Zernike kinds (n = (dz/dx, dz/dy, -1) / norm, the same operations as their
+  // kNormal evaluation). Kernels with freeform kinds, and ORT_NO_SLOPE A/B builds, evaluate
+  // the unit normal and update with the reference's -n / nz_safe.
+#ifdef ORT_NO_SLOPE
+  constexpr bool kSl = false;
+#else
+  constexpr bool kSl = ((FEAT & F_KM) & ~(ort::KM_EVEN | ort::KM_ODD | ort::KM_ZERN)) == 0;
+#endif
   for (int j = 0;; ++j) {
     const bool lane_on = active && j <= U;
     if (!__any(lane_on)) break;
     if (lane_on) {
       bool rerr = false;
       double nx, ny, nz;
-      const bool upd = j < U;  // sag + normal at P(t): for the update, or (j == U) for the
-                               // interaction at the returned t
-      const double f = newton_eval_fast<FEAT, FAST>(a, s, r, t, rerr, nx, ny, nz, bad);
+      const bool upd = j < U;
+      const double f = newton_eval_fast<FEAT, FAST>(a, s, r, t, kSl ? ort::kSlope : ort::kNormal,
+                                                    rerr, nx, ny, nz, bad);
       // the reference evaluates sag at j = 0..U-1 always, and at j = U only when the
       // loop broke there (U < max_iter)
       if (rerr && (j < U || U < max_iter) && !(FAST && bad)) range_bits |= range_bit(s);
@@ -354,11 +368,25 @@ __device__ inline __attribute__((always_inline)) double newton_distance(const KA
           const int m = U - 1 - j;
           if (m < kHist && tape) ORT_ST(tape[(int64_t)(7 + m) * a.n_rays], t);
         }
-        if constexpr (FAST)
-          t = ort::fast::newton_step(r, t, f, nx, ny, nz, bad);
-        else
-          t = ort::newton_step(r, t, f, nx, ny, nz);
-      } else {
+        if constexpr (!kSl) {
+          if constexpr (FAST)
+            t = ort::fast::newton_step(r, t, f, nx, ny, nz, bad);
+          else
+            t = ort::newton_step(r, t, f, nx, ny, nz);
+        } else if constexpr (FAST) {
+          t = ort::fast::newton_step_slope(r, t, f, nx, ny, bad);  // (steep: bad)
+        } else {
+          t = ort::newton_step_any(r, t, f, nx, ny, nz);
+        }
+      } else if constexpr (!kSl) {
+        nnx = nx;
+        nny = ny;
+        nnz = nz;
+      } else if constexpr (FAST) {
+        ort::fast::unit_normal_from_slope(nx, ny, nnx, nny, nnz, bad);
+      } else if (nz == -1.0) {  // the slopes: their unit normal, as kNormal forms it
+        ort::unit_normal3(nx, ny, ort::sqrt(nx * nx + ny * ny + 1.0), nnx, nny, nnz);
+      } else {  // steep or NaN: the evaluation returned the unit normal itself
         nnx = nx;
         nny = ny;
         nnz = nz;
@@ -924,17 +952,35 @@ __global__ __launch_bounds__(kBlock) ORT_TRACE_OCC void trace_kernel(const KArgs
   __shared__ int32_t vcodes[kBlock / 64];
   if constexpr ((FEAT & F_KM) != 0) {
     if (a.vstats) {
-      const int prev = a.vprev ? *a.vprev : 1;
       const int64_t ng = (a.n_rays + a.group_len - 1) / a.group_len;
       const int nsch = (int)ng * a.n_surf;  // <= ORT_VERIFY_MAX_SCHED (host-checked)
+      // the schedule's loads issued together with the flag's, so either path below waits
+      // for one memory round trip, not two (the no-op rounds after a settled one are
+      // mostly that wait)
+      constexpr int kPre = ORT_VERIFY_MAX_SCHED / kBlock;
+      int32_t pre[kPre];
+#pragma unroll
+      for (int q = 0; q < kPre; ++q) {
+        const int k = threadIdx.x + q * kBlock;
+        pre[q] = k < nsch ? a.sched[k] : 0;
+      }
+      const int prev = a.vprev ? *a.vprev : 1;
       if (prev != 1) {  // the previous launch did not run: nothing to verify
         if (blockIdx.x == 0) {
-          for (int k = threadIdx.x; k < nsch; k += kBlock) a.sched_out[k] = a.sched[k];
+#pragma unroll
+          for (int q = 0; q < kPre; ++q) {
+            const int k = threadIdx.x + q * kBlock;
+            if (k < nsch) a.sched_out[k] = pre[q];
+          }
           if (threadIdx.x == 0) *a.vflag = prev;
         }
         return;
       }
-      for (int k = threadIdx.x; k < nsch; k += kBlock) vsched[k] = a.sched[k];
+#pragma unroll
+      for (int q = 0; q < kPre; ++q) {
+        const int k = threadIdx.x + q * kBlock;
+        if (k < nsch) vsched[k] = pre[q];
+      }
       __syncthreads();
       const int c = newton_decide(a.surf, a.n_surf, ng, a.vstats, a.conv_base, vsched, vcodes);
       if (blockIdx.x == 0) {

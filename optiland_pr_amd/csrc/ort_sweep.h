@@ -468,8 +468,8 @@ ORT_INLINE double replay_distance(const KArgs& a, const ort_surface& s, int si,
       hist[0] = t;
       double nx, ny, nz;
       const double f = ort::newton_eval<KM>(s, s.radius, s.conic, cst(a.coef), cst(a.zern),
-                                            kNoSeed, r, t, true, rerr, nx, ny, nz);
-      t = ort::newton_step(r, t, f, nx, ny, nz);
+                                            kNoSeed, r, t, ort::kSlope, rerr, nx, ny, nz);
+      t = ort::newton_step_any(r, t, f, nx, ny, nz);
     }
   }
   return t;
@@ -1133,8 +1133,8 @@ ORT_INLINE void vjp_ray(const KArgs& a, const JArgs& j, int64_t rid, bool active
           for (int it = 0; it < U; ++it) {
             D nx, ny, nz;
             const D f = ort::newton_eval<KM>(s, R, K, cst(a.coef), cst(a.zern), zs, r, t,
-                                             true, rerr, nx, ny, nz);
-            t = ort::newton_step(r, t, f, nx, ny, nz);
+                                             ort::kSlope, rerr, nx, ny, nz);
+            t = ort::newton_step_any(r, t, f, nx, ny, nz);
           }
         }
       }

@@ -390,6 +390,18 @@ class NewtonScheduleError(RuntimeError):
     pass
 
 
+_SIDE_STREAMS = {}
+
+
+def _side_stream(dev):
+    """A second stream of the device (parallel branches of a captured step)."""
+    st = _SIDE_STREAMS.get(dev)
+    if st is None:
+        st = torch.cuda.Stream(device=dev)
+        _SIDE_STREAMS[dev] = st
+    return st
+
+
 # RayOperand.rms_spot_size's request for the fused rms (operands.py): while a dict, the
 # differentiable single-wavelength trace (RealRayTracer._trace_grad) computes the rms of
 # its final points in the taped forward's epilogue and leaves the autograd-connected
@@ -483,7 +495,8 @@ def check_all_pending():
 VERIFY_MAX_SCHED = 1024  # include/optiland_rt.h ORT_VERIFY_MAX_SCHED
 
 
-def _run_device(dlens: DeviceLens, launch, n_rays, group_len, keys, need_status):
+def _run_device(dlens: DeviceLens, launch, n_rays, group_len, keys, need_status,
+                epilogue=None):
     """The warm-schedule path of newton_mode="device": no host synchronisation. The first
     launch runs the cached schedule; device_rounds() verify-and-re-trace launches
     (ort_options.verify_*: each checks the previous launch's statistics with
@@ -568,6 +581,15 @@ def _run_device(dlens: DeviceLens, launch, n_rays, group_len, keys, need_status)
                                       fix[4], fix[5], stream)
             _native.check(rc, "ort_newton_fixup")
         launch(opt, st, stt if need_status else None)
+    side = None
+    if epilogue is not None and fused:
+        # the epilogue reads the last round's outputs only: it runs beside the finish
+        # launch on a side stream (a parallel branch of a captured graph)
+        side = _side_stream(dev)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            epilogue()
+        epilogue = None
     if fused:
         # the settled schedule the backward keeps: written by the finish launch (no clone)
         sched_copy = torch.empty(ngs, dtype=torch.int32, device=dev)
@@ -579,6 +601,10 @@ def _run_device(dlens: DeviceLens, launch, n_rays, group_len, keys, need_status)
         rc = lib.ort_newton_fixup(lens_c, n_groups, final[0], 0, final[1], final[2], final[3],
                                   None, None, stream)
         _native.check(rc, "ort_newton_fixup")
+    if side is not None:
+        torch.cuda.current_stream().wait_stream(side)
+    if epilogue is not None:
+        epilogue()
     bufs[2] = new_cur
     dlens._dev_sched[kk] = last
     off = base + (new_cur * ngs if fused else 0)
@@ -608,11 +634,20 @@ def _run_device(dlens: DeviceLens, launch, n_rays, group_len, keys, need_status)
 
 
 def _run(dlens: DeviceLens, launch, n_rays, group_len, keys, newton_mode="reference",
-         with_status=True):
+         with_status=True, epilogue=None):
     """Run `launch(opt, stats, status)` under the Newton speculate-and-verify protocol.
     newton_mode "reference": verified on the host (one read per launch); "device": the
     same rule checked on the device once the schedules are warm (no host round trip,
-    errors surface at a later check_pending); "wave": per-wavefront stop."""
+    errors surface at a later check_pending); "wave": per-wavefront stop. epilogue():
+    launches that read the final launch's outputs, issued once they are final (beside
+    the device rounds' finish launch)."""
+    if not _run_protocol(dlens, launch, n_rays, group_len, keys, newton_mode, with_status,
+                         epilogue) and epilogue is not None:
+        epilogue()
+
+
+def _run_protocol(dlens, launch, n_rays, group_len, keys, newton_mode, with_status, epilogue):
+    """_run's body; True when the device rounds issued the epilogue themselves"""
     dev = dlens.device
     if dlens.pending and not torch.cuda.is_current_stream_capturing():
         check_pending(dlens)  # (a capture only records launches: no event queries in it)
@@ -629,18 +664,18 @@ def _run(dlens: DeviceLens, launch, n_rays, group_len, keys, newton_mode="refere
         opt = _native.ort_options(_abi.NEWTON_SCHEDULE, 0, None)
         launch(opt, None, status)
         _raise_status(status)
-        return
+        return False
     if newton_mode == "wave":
         stats = torch.empty(n_groups * S * _abi.NEWTON_STAT.itemsize, dtype=torch.uint8, device=dev)
         opt = _native.ort_options(_abi.NEWTON_WAVE, 0, None)
         launch(opt, stats, status)
         _raise_status(status)
-        return
+        return False
     if len(keys) != n_groups:
         keys = [("group", g) for g in range(n_groups)]
     if newton_mode == "device" and all(k in dlens.sched_cache for k in keys):
-        _run_device(dlens, launch, n_rays, group_len, keys, need_status)
-        return
+        _run_device(dlens, launch, n_rays, group_len, keys, need_status, epilogue)
+        return True
     sched = dlens.initial_schedule(keys)
     # the Newton statistics and the status word share one buffer: the host reads both
     # with the one copy the schedule check needs (no second synchronising read)
@@ -668,7 +703,7 @@ def _run(dlens: DeviceLens, launch, n_rays, group_len, keys, newton_mode="refere
             dlens.last_schedule = sched
             if need_status:
                 _raise_status_value(int(host[nb:nb + 4].view(np.int32)[0]))
-            return
+            return False
         sched = new
     raise RuntimeError("Newton schedule did not settle")
 
@@ -734,10 +769,14 @@ def trace_pupil(dlens: DeviceLens, segments, px, py, out: RealRays, n_rays,
         rc = lib.ort_trace_pupil(*args, C.byref(opt), rec_p, _ptr(stats), _ptr(status), stream)
         _native.check(rc, "ort_trace_pupil")
 
-    _run(dlens, launch, n_rays, group_len, list(keys), newton_mode)
-    if rms is not None and n_rays > 0:
-        rc = lib.ort_rms_finish(_ptr(part), rows, _ptr(rms[1]), _ptr(rms[0]), stream)
+    def finish_rms():
+        # (on a side stream the read of `part` is ordered before its memory's reuse by the
+        # main stream's wait on that stream, issued before this call returns)
+        rc = lib.ort_rms_finish(_ptr(part), rows, _ptr(rms[1]), _ptr(rms[0]), _stream_handle())
         _native.check(rc, "ort_rms_finish")
+
+    _run(dlens, launch, n_rays, group_len, list(keys), newton_mode,
+         epilogue=finish_rms if rms is not None and n_rays > 0 else None)
     return seg_dev
 
 
