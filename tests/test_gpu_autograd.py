@@ -265,11 +265,15 @@ def test_device_resident_coefficients(torch):
 
 
 @pytest.mark.parametrize("name", ["tma_fringe", "rt_asph"])
-def test_taped_forward_gradients_bit_identical(torch, name):
+def test_taped_forward_gradients_bit_identical(torch, name, monkeypatch):
     """The forward writes the adjoint tape (F_TAPE) and the backward runs only the reverse
     sweep: the same tape values as the adjoint's own re-trace, so the same gradients to
-    the last bit (and the same loss)."""
-    from optiland_pr_amd import autodiff
+    the last bit (and the same loss). Both runs take the two-pass ort::rms_spot (the
+    untaped trace cannot fuse the rms; test_fused_rms_matches_unfused compares the two
+    reductions)."""
+    from optiland_pr_amd import autodiff, operands
+
+    monkeypatch.setattr(operands, "FUSED_RMS", False)
     from optiland_pr_amd.distribution import RandomDistribution
     from optiland_pr_amd.operands import RayOperand
     from tests._cases import build_lens
