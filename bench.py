@@ -225,7 +225,7 @@ def config3(args, dev, rank, world, torch):
                 "parallelism": f"dp{world} (ray shards, no collective)"},
         kernel="trace_kernel<F_GEN|KM_EVEN> (ort_trace_pupil)", launches=1,
         bytes_per_launch=n_p * 16 + n * 64, flops_per_ray=flops, pmc_file="hbm_traffic_c3.json",
-        compute_pmc_file="r04_config3_pmc_compute.json", rays=n)
+        compute_pmc_file="r05_config3_pmc_compute.json", rays=n)
 
 
 def config4(args, dev, rank, world, torch):

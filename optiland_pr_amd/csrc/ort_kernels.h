@@ -457,6 +457,10 @@ __device__ inline void interact(const KArgs& a, const ort_surface& s, ort::Ray& 
 // degree-specialised Horner schemes: 4 waves (123 VGPRs, no scratch) 0.5259 / 0.5267 ms,
 // 5 waves (96 VGPRs, 100 B of scratch) 0.5275 / 0.5227, 6 waves (80, 164 B) 0.567 / 0.593
 // (profiles/r05_ab_fwd_occupancy.log): 4 waves, the same time without the spill traffic.
+// The deferred-check even / odd kernels after the round-5 slope-form updates: 6 waves (80
+// VGPRs, 56 B of scratch whose stores reach HBM: config 3 WRITE_SIZE 5.54 GB per launch for
+// 3.84 GB of outputs) 6.89-6.91 ms, 5 waves (96 VGPRs, no scratch) 6.73-6.75 ms, 4 waves
+// 7.01-7.02 ms (tools/gpu_r05p.sh, profiles/r05_ab_c3_occupancy.log): 5.
 template <uint32_t FEAT>
 constexpr bool kNewtonFast =
 #ifdef ORT_NO_NEWTON_FAST
@@ -466,12 +470,16 @@ constexpr bool kNewtonFast =
     (FEAT & (F_IA | F_WRAY | F_TAPE)) == 0;
 #endif
 
+// The verify rounds' grid-stride form (F_STRIDE) usually returns at once and re-traces
+// only after a schedule correction: 2 waves per SIMD, so it carries no scratch (its
+// dispatch sets up no spill space).
 template <uint32_t FEAT>
 struct TraceWaves {
   static constexpr int value =
-      ((FEAT & ort::KM_ZERN) != 0 && (FEAT & (ort::KM_FREE | F_IA)) == 0)
+      (FEAT & F_STRIDE) != 0 ? 2
+      : ((FEAT & ort::KM_ZERN) != 0 && (FEAT & (ort::KM_FREE | F_IA)) == 0)
           ? ((FEAT & F_TAPE) != 0 ? 4 : 6)
-          : ((kNewtonFast<FEAT> && (FEAT & F_MONO) != 0) ? 6 : 1);
+          : ((kNewtonFast<FEAT> && (FEAT & F_MONO) != 0) ? 5 : 1);
 };
 #ifdef ORT_TRACE_WAVES
 #define ORT_TRACE_OCC __attribute__((amdgpu_waves_per_eu(ORT_TRACE_WAVES)))

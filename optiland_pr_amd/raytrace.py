@@ -390,18 +390,6 @@ class NewtonScheduleError(RuntimeError):
     pass
 
 
-_SIDE_STREAMS = {}
-
-
-def _side_stream(dev):
-    """A second stream of the device (parallel branches of a captured step)."""
-    st = _SIDE_STREAMS.get(dev)
-    if st is None:
-        st = torch.cuda.Stream(device=dev)
-        _SIDE_STREAMS[dev] = st
-    return st
-
-
 # RayOperand.rms_spot_size's request for the fused rms (operands.py): while a dict, the
 # differentiable single-wavelength trace (RealRayTracer._trace_grad) computes the rms of
 # its final points in the taped forward's epilogue and leaves the autograd-connected
@@ -581,15 +569,10 @@ def _run_device(dlens: DeviceLens, launch, n_rays, group_len, keys, need_status,
                                       fix[4], fix[5], stream)
             _native.check(rc, "ort_newton_fixup")
         launch(opt, st, stt if need_status else None)
-    side = None
-    if epilogue is not None and fused:
-        # the epilogue reads the last round's outputs only: it runs beside the finish
-        # launch on a side stream (a parallel branch of a captured graph)
-        side = _side_stream(dev)
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            epilogue()
-        epilogue = None
+    # (the epilogue reads the last round's outputs only; run beside the finish launch on a
+    # side stream -- a parallel branch of the captured graph -- it measured slower: the
+    # two queues' hand-offs cost ~15 us per step against 8.5 us of the two launches in
+    # order, so it runs after the finish on the same stream)
     if fused:
         # the settled schedule the backward keeps: written by the finish launch (no clone)
         sched_copy = torch.empty(ngs, dtype=torch.int32, device=dev)
@@ -601,8 +584,6 @@ def _run_device(dlens: DeviceLens, launch, n_rays, group_len, keys, need_status,
         rc = lib.ort_newton_fixup(lens_c, n_groups, final[0], 0, final[1], final[2], final[3],
                                   None, None, stream)
         _native.check(rc, "ort_newton_fixup")
-    if side is not None:
-        torch.cuda.current_stream().wait_stream(side)
     if epilogue is not None:
         epilogue()
     bufs[2] = new_cur
@@ -639,8 +620,8 @@ def _run(dlens: DeviceLens, launch, n_rays, group_len, keys, newton_mode="refere
     newton_mode "reference": verified on the host (one read per launch); "device": the
     same rule checked on the device once the schedules are warm (no host round trip,
     errors surface at a later check_pending); "wave": per-wavefront stop. epilogue():
-    launches that read the final launch's outputs, issued once they are final (beside
-    the device rounds' finish launch)."""
+    launches that read the final launch's outputs, issued once they are final (after the
+    device rounds' finish launch)."""
     if not _run_protocol(dlens, launch, n_rays, group_len, keys, newton_mode, with_status,
                          epilogue) and epilogue is not None:
         epilogue()
@@ -770,8 +751,6 @@ def trace_pupil(dlens: DeviceLens, segments, px, py, out: RealRays, n_rays,
         _native.check(rc, "ort_trace_pupil")
 
     def finish_rms():
-        # (on a side stream the read of `part` is ordered before its memory's reuse by the
-        # main stream's wait on that stream, issued before this call returns)
         rc = lib.ort_rms_finish(_ptr(part), rows, _ptr(rms[1]), _ptr(rms[0]), _stream_handle())
         _native.check(rc, "ort_rms_finish")
 
