@@ -714,6 +714,16 @@ int ort_newton_finish(const ort_lens* lens, int64_t n_groups, ort_newton_stat* s
                       int32_t* statuses, int32_t* status_out, int32_t* sched_copy,
                       void* stream);
 
+/* ort_newton_finish and ort_rms_finish in ONE launch (v18): a second workgroup combines
+ * the taped forward's rms rows (ort_options.rms_part, rms_rows of them) into rms_stats[5]
+ * and *rms (nullable) beside the check -- the rows are final once the rounds are. The
+ * device-verified rounds of RayOperand.rms_spot_size's trace end with it. */
+int ort_newton_finish_rms(const ort_lens* lens, int64_t n_groups, ort_newton_stat* stats,
+                          int32_t rounds, int32_t conv_base, int32_t* sched, int32_t* flags,
+                          int32_t* statuses, int32_t* status_out, int32_t* sched_copy,
+                          const double* rms_part, int64_t rms_rows, double* rms_stats,
+                          double* rms, void* stream);
+
 /* Pupil coordinates of a distribution on the device: px[k], py[k] for k < n_points
  * (distribution.py:72-408; the grid kinds bit-identical to NumPy, cos / sin correctly
  * rounded). Feeds ort_trace_pupil without host-side sampling or a host-to-device copy. */

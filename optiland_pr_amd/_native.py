@@ -155,7 +155,7 @@ EXPORTS = ("ort_abi_version", "ort_trace_sequential", "ort_trace_pupil", "ort_tr
            "ort_rms_spot_workspace_size", "ort_rms_spot", "ort_rms_spot_vjp",
            "ort_wavefront_workspace_size", "ort_wavefront_opd", "ort_patch_zernike",
            "ort_patch_zernike_ptrs", "ort_newton_finish", "ort_adam_patch_zernike",
-           "ort_rms_finish")
+           "ort_rms_finish", "ort_newton_finish_rms")
 
 _lib = None
 
@@ -214,6 +214,11 @@ def load(path: str | None = None):
     lib.ort_newton_finish.argtypes = [P(ort_lens), C.c_int64, C.c_void_p, C.c_int32, C.c_int32,
                                       C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                       C.c_void_p, C.c_void_p]
+    lib.ort_newton_finish_rms.restype = C.c_int
+    lib.ort_newton_finish_rms.argtypes = [P(ort_lens), C.c_int64, C.c_void_p, C.c_int32,
+                                          C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
+                                          C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64,
+                                          C.c_void_p, C.c_void_p, C.c_void_p]
     lib.ort_surface_sag_normal.restype = C.c_int
     lib.ort_surface_sag_normal.argtypes = [P(ort_lens), C.c_int32, C.c_void_p, C.c_void_p,
                                            C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p,

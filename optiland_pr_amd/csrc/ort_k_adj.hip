@@ -2,6 +2,7 @@
 // tangent tables, and the launch sequence (kernel templates: ort_adjoint.h)
 
 #include "ort_adjoint.h"
+#include "ort_reduce.h"
 
 namespace ortk {
 
@@ -133,10 +134,25 @@ __global__ __launch_bounds__(kBlock) void newton_fixup_kernel(
 // status of the last round that ran into *status_out, every round's status word zeroed and
 // statistics set to 0xFF bytes, the settled schedule copied out -- in place of two fills
 // and a copy per call.
+// ort_newton_finish_rms: a second workgroup finishes the rms spot size from the F_RMS rows
+// beside the check (one launch for both; the rows are final once the rounds are)
+struct RmsFinish {
+  const double* part;
+  int32_t n_rows;
+  double* stats;
+  double* rms;
+};
+
 __global__ __launch_bounds__(kBlock) void newton_finish_kernel(
     const ort_surface* surf, int32_t n_surf, int64_t n_groups, ort_newton_stat* stats,
     int32_t rounds, int32_t conv_base, int32_t* sched, int32_t* flags, int32_t* statuses,
-    int32_t* status_out, int32_t* sched_copy) {
+    int32_t* status_out, int32_t* sched_copy, const RmsFinish rf) {
+  if (blockIdx.x == 1) {  // (launched with 2 workgroups only when rf.part is set)
+    static_assert(kBlock == kRmsFinThreads, "ort_rms_finish's workgroup shape");
+    __shared__ double lds[kBlock / 64 * 3];
+    rms_finish_block<kRmsFinThreads, kRmsFinRows>(rf.part, rf.n_rows, rf.stats, rf.rms, lds);
+    return;
+  }
   __shared__ int32_t codes[kBlock / 64];
   __shared__ int32_t ran_last;
   const int64_t ngs = n_groups * n_surf;
@@ -184,10 +200,10 @@ __global__ __launch_bounds__(kBlock) void newton_finish_kernel(
 
 }  // namespace ortk
 
-extern "C" int ort_newton_finish(const ort_lens* lens, int64_t n_groups, ort_newton_stat* stats,
-                                 int32_t rounds, int32_t conv_base, int32_t* sched,
-                                 int32_t* flags, int32_t* statuses, int32_t* status_out,
-                                 int32_t* sched_copy, void* stream) {
+static int newton_finish_launch(const ort_lens* lens, int64_t n_groups, ort_newton_stat* stats,
+                                int32_t rounds, int32_t conv_base, int32_t* sched,
+                                int32_t* flags, int32_t* statuses, int32_t* status_out,
+                                int32_t* sched_copy, const ortk::RmsFinish& rf, void* stream) {
   using namespace ortk;
   if (!lens || !stats || !sched || !flags || !statuses || !status_out || n_groups < 1 ||
       rounds < 1 || conv_base < 0)
@@ -195,10 +211,32 @@ extern "C" int ort_newton_finish(const ort_lens* lens, int64_t n_groups, ort_new
   if (lens->n_surfaces < 1 || lens->n_surfaces > ORT_MAX_SURFACES || !lens->surfaces)
     return ORT_ERR_ARG;
   if (rounds >= kBlock) return ORT_ERR_ARG;  // one thread per round's flag and status
-  hipLaunchKernelGGL(newton_finish_kernel, dim3(1), dim3(kBlock), 0, (hipStream_t)stream,
-                     lens->surfaces, lens->n_surfaces, n_groups, stats, rounds, conv_base, sched,
-                     flags, statuses, status_out, sched_copy);
+  hipLaunchKernelGGL(newton_finish_kernel, dim3(rf.part ? 2 : 1), dim3(kBlock), 0,
+                     (hipStream_t)stream, lens->surfaces, lens->n_surfaces, n_groups, stats,
+                     rounds, conv_base, sched, flags, statuses, status_out, sched_copy, rf);
   return hipGetLastError() == hipSuccess ? ORT_OK : ORT_ERR_LAUNCH;
+}
+
+extern "C" int ort_newton_finish(const ort_lens* lens, int64_t n_groups, ort_newton_stat* stats,
+                                 int32_t rounds, int32_t conv_base, int32_t* sched,
+                                 int32_t* flags, int32_t* statuses, int32_t* status_out,
+                                 int32_t* sched_copy, void* stream) {
+  return newton_finish_launch(lens, n_groups, stats, rounds, conv_base, sched, flags, statuses,
+                              status_out, sched_copy, ortk::RmsFinish{}, stream);
+}
+
+extern "C" int ort_newton_finish_rms(const ort_lens* lens, int64_t n_groups,
+                                     ort_newton_stat* stats, int32_t rounds, int32_t conv_base,
+                                     int32_t* sched, int32_t* flags, int32_t* statuses,
+                                     int32_t* status_out, int32_t* sched_copy,
+                                     const double* rms_part, int64_t rms_rows,
+                                     double* rms_stats, double* rms, void* stream) {
+  if (!rms_part || !rms_stats || rms_rows < 1 || rms_rows > ((int64_t)1 << 28))
+    return ORT_ERR_ARG;
+  return newton_finish_launch(lens, n_groups, stats, rounds, conv_base, sched, flags, statuses,
+                              status_out, sched_copy,
+                              ortk::RmsFinish{rms_part, (int32_t)rms_rows, rms_stats, rms},
+                              stream);
 }
 
 extern "C" int ort_newton_fixup(const ort_lens* lens, int64_t n_groups,

@@ -325,63 +325,17 @@ __global__ __launch_bounds__(kSpotThreads) void rms_spot_vjp_kernel(
 #endif
 }
 
-// ort_rms_finish: the taped forward's F_RMS rows (ort_reduce.h rms_epilogue) -> the rms
-// spot size. One workgroup of 1024 threads, each holding up to kFinRows rows in registers
-// (config 5: 4096 rows, so one load round trip): the counts and sums in index order give
-// the centroid (mx, my), then M2 = sum over rows of [M2_b + n_b ((sx_b / n_b - mx)^2 +
-// (sy_b / n_b - my)^2)] (a row with n_b = 0 adds nothing), rms = sqrt(M2 / n); stats as
-// ort_rms_spot's row (n, mean x, mean y, rms) with the geometric radius, which this pass
-// has no data for, NaN. Rows past kFinThreads * kFinRows are re-read in the second sum.
-constexpr int kFinThreads = 1024;
-constexpr int kFinRows = 4;
-
-__device__ inline double rms_row_m2(const double* p, double mx, double my) {
-  const double nb = p[0];
-  if (!(nb > 0.0)) return 0.0;
-  const double dx = p[1] / nb - mx, dy = p[2] / nb - my;
-  return p[3] + nb * (dx * dx + dy * dy);
-}
+// ort_rms_finish: the taped forward's F_RMS rows -> the rms spot size (ort_reduce.h
+// rms_finish_block), one workgroup of 256 threads holding up to 16 rows each in registers
+// (config 5: 4096 rows, one load round trip) -- the same workgroup shape and order as
+// ort_newton_finish_rms's second workgroup, so both give the same bits
+constexpr int kFinThreads = kRmsFinThreads;
 
 __global__ __launch_bounds__(kFinThreads) void rms_finish_kernel(const double* part,
                                                                  int n_rows, double* stats,
                                                                  double* rms) {
   __shared__ double lds[kFinThreads / 64 * 3];
-  double row[kFinRows][4];
-#pragma unroll
-  for (int k = 0; k < kFinRows; ++k) {
-    const int c = threadIdx.x + k * kFinThreads;
-#pragma unroll
-    for (int f = 0; f < 4; ++f) row[k][f] = c < n_rows ? part[c * 4 + f] : 0.0;
-  }
-  double v[3] = {0.0, 0.0, 0.0};
-#pragma unroll
-  for (int k = 0; k < kFinRows; ++k) {
-    v[0] += row[k][0];
-    v[1] += row[k][1];
-    v[2] += row[k][2];
-  }
-  for (int c = threadIdx.x + kFinRows * kFinThreads; c < n_rows; c += kFinThreads) {
-    v[0] += part[c * 4 + 0];
-    v[1] += part[c * 4 + 1];
-    v[2] += part[c * 4 + 2];
-  }
-  block_sum<3, kFinThreads>(v, lds);
-  const double mx = v[1] / v[0], my = v[2] / v[0];
-  double m[1] = {0.0};
-#pragma unroll
-  for (int k = 0; k < kFinRows; ++k) m[0] += rms_row_m2(row[k], mx, my);
-  for (int c = threadIdx.x + kFinRows * kFinThreads; c < n_rows; c += kFinThreads)
-    m[0] += rms_row_m2(part + c * 4, mx, my);
-  block_sum<1, kFinThreads>(m, lds);
-  if (threadIdx.x == 0) {
-    const double r = ::sqrt(m[0] / v[0]);
-    stats[0] = v[0];
-    stats[1] = mx;
-    stats[2] = my;
-    stats[3] = r;
-    stats[4] = __builtin_nan("");
-    if (rms) *rms = r;
-  }
+  rms_finish_block<kFinThreads, kRmsFinRows>(part, n_rows, stats, rms, lds);
 }
 
 }  // namespace

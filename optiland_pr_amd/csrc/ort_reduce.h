@@ -110,4 +110,62 @@ __device__ inline void rms_epilogue(const KArgs& a, const ort::Ray& r, bool acti
   }
 }
 
+// The rms spot size from the F_RMS rows (ort_rms_finish, and the second workgroup of
+// ort_newton_finish_rms): one workgroup of NT threads, each holding up to ROWS rows in
+// registers (rows past NT * ROWS re-read in the second sum). The counts and sums in index
+// order give the centroid (mx, my); then M2 = sum over rows of [M2_b + n_b ((sx_b / n_b -
+// mx)^2 + (sy_b / n_b - my)^2)] (a row with n_b = 0 adds nothing: Chan et al.'s pairwise
+// update), rms = sqrt(M2 / n); stats as ort_rms_spot's row (n, mean x, mean y, rms) with the
+// geometric radius, which this pass has no data for, NaN. lds: >= NT / 64 * 3 doubles.
+__device__ inline double rms_row_m2(const double* p, double mx, double my) {
+  const double nb = p[0];
+  if (!(nb > 0.0)) return 0.0;
+  const double dx = p[1] / nb - mx, dy = p[2] / nb - my;
+  return p[3] + nb * (dx * dx + dy * dy);
+}
+
+constexpr int kRmsFinThreads = 256;  // the one workgroup shape of both finish launches
+constexpr int kRmsFinRows = 16;
+
+template <int NT, int ROWS>
+__device__ inline void rms_finish_block(const double* part, int n_rows, double* stats,
+                                        double* rms, double* lds) {
+  double row[ROWS][4];
+#pragma unroll
+  for (int k = 0; k < ROWS; ++k) {
+    const int c = threadIdx.x + k * NT;
+#pragma unroll
+    for (int f = 0; f < 4; ++f) row[k][f] = c < n_rows ? part[(int64_t)c * 4 + f] : 0.0;
+  }
+  double v[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+  for (int k = 0; k < ROWS; ++k) {
+    v[0] += row[k][0];
+    v[1] += row[k][1];
+    v[2] += row[k][2];
+  }
+  for (int c = threadIdx.x + ROWS * NT; c < n_rows; c += NT) {
+    v[0] += part[(int64_t)c * 4 + 0];
+    v[1] += part[(int64_t)c * 4 + 1];
+    v[2] += part[(int64_t)c * 4 + 2];
+  }
+  block_sum<3, NT>(v, lds);
+  const double mx = v[1] / v[0], my = v[2] / v[0];
+  double m[1] = {0.0};
+#pragma unroll
+  for (int k = 0; k < ROWS; ++k) m[0] += rms_row_m2(row[k], mx, my);
+  for (int c = threadIdx.x + ROWS * NT; c < n_rows; c += NT)
+    m[0] += rms_row_m2(part + (int64_t)c * 4, mx, my);
+  block_sum<1, NT>(m, lds);
+  if (threadIdx.x == 0) {
+    const double r = ::sqrt(m[0] / v[0]);
+    stats[0] = v[0];
+    stats[1] = mx;
+    stats[2] = my;
+    stats[3] = r;
+    stats[4] = __builtin_nan("");
+    if (rms) *rms = r;
+  }
+}
+
 }  // namespace ortk

@@ -483,8 +483,7 @@ def check_all_pending():
 VERIFY_MAX_SCHED = 1024  # include/optiland_rt.h ORT_VERIFY_MAX_SCHED
 
 
-def _run_device(dlens: DeviceLens, launch, n_rays, group_len, keys, need_status,
-                epilogue=None):
+def _run_device(dlens: DeviceLens, launch, n_rays, group_len, keys, need_status, rms=None):
     """The warm-schedule path of newton_mode="device": no host synchronisation. The first
     launch runs the cached schedule; device_rounds() verify-and-re-trace launches
     (ort_options.verify_*: each checks the previous launch's statistics with
@@ -569,23 +568,32 @@ def _run_device(dlens: DeviceLens, launch, n_rays, group_len, keys, need_status,
                                       fix[4], fix[5], stream)
             _native.check(rc, "ort_newton_fixup")
         launch(opt, st, stt if need_status else None)
-    # (the epilogue reads the last round's outputs only; run beside the finish launch on a
-    # side stream -- a parallel branch of the captured graph -- it measured slower: the
-    # two queues' hand-offs cost ~15 us per step against 8.5 us of the two launches in
-    # order, so it runs after the finish on the same stream)
     if fused:
-        # the settled schedule the backward keeps: written by the finish launch (no clone)
+        # the settled schedule the backward keeps: written by the finish launch (no clone);
+        # the rms rows of a fused rms spot size (the last round's outputs) are finished by a
+        # second workgroup of the same launch (ort_newton_finish_rms). (Run beside the
+        # finish on a side stream -- a parallel branch of the captured graph -- the two
+        # queues' hand-offs measured ~25 us from the last round to the adjoint against
+        # ~10 us for the two launches in order.)
         sched_copy = torch.empty(ngs, dtype=torch.int32, device=dev)
-        rc = lib.ort_newton_finish(lens_c, n_groups, final[0], R, 0, final[1], final[2],
-                                   final[3], final[4], _ptr(sched_copy), stream)
+        if rms is not None:
+            part, rows, stats_t, rms_t = rms
+            rc = lib.ort_newton_finish_rms(lens_c, n_groups, final[0], R, 0, final[1],
+                                           final[2], final[3], final[4], _ptr(sched_copy),
+                                           _ptr(part), rows, _ptr(stats_t), _ptr(rms_t),
+                                           stream)
+            rms = None
+        else:
+            rc = lib.ort_newton_finish(lens_c, n_groups, final[0], R, 0, final[1], final[2],
+                                       final[3], final[4], _ptr(sched_copy), stream)
         _native.check(rc, "ort_newton_finish")
     else:
         sched_copy = None
         rc = lib.ort_newton_fixup(lens_c, n_groups, final[0], 0, final[1], final[2], final[3],
                                   None, None, stream)
         _native.check(rc, "ort_newton_fixup")
-    if epilogue is not None:
-        epilogue()
+    if rms is not None:  # (the two-launch rounds: finished after them)
+        _rms_finish(lib, rms, stream)
     bufs[2] = new_cur
     dlens._dev_sched[kk] = last
     off = base + (new_cur * ngs if fused else 0)
@@ -614,21 +622,27 @@ def _run_device(dlens: DeviceLens, launch, n_rays, group_len, keys, need_status,
     _PENDING_LENSES.add(dlens)
 
 
+def _rms_finish(lib, rms, stream):
+    part, rows, stats_t, rms_t = rms
+    rc = lib.ort_rms_finish(_ptr(part), rows, _ptr(stats_t), _ptr(rms_t), stream)
+    _native.check(rc, "ort_rms_finish")
+
+
 def _run(dlens: DeviceLens, launch, n_rays, group_len, keys, newton_mode="reference",
-         with_status=True, epilogue=None):
+         with_status=True, rms=None):
     """Run `launch(opt, stats, status)` under the Newton speculate-and-verify protocol.
     newton_mode "reference": verified on the host (one read per launch); "device": the
     same rule checked on the device once the schedules are warm (no host round trip,
-    errors surface at a later check_pending); "wave": per-wavefront stop. epilogue():
-    launches that read the final launch's outputs, issued once they are final (after the
-    device rounds' finish launch)."""
+    errors surface at a later check_pending); "wave": per-wavefront stop. rms: (rows,
+    n_rows, stats, rms) of a fused rms spot size, finished from the final launch's rows
+    (by the device rounds' finish launch, or after the protocol)."""
     if not _run_protocol(dlens, launch, n_rays, group_len, keys, newton_mode, with_status,
-                         epilogue) and epilogue is not None:
-        epilogue()
+                         rms) and rms is not None:
+        _rms_finish(_native.load(), rms, _stream_handle())
 
 
-def _run_protocol(dlens, launch, n_rays, group_len, keys, newton_mode, with_status, epilogue):
-    """_run's body; True when the device rounds issued the epilogue themselves"""
+def _run_protocol(dlens, launch, n_rays, group_len, keys, newton_mode, with_status, rms):
+    """_run's body; True when the device rounds finished the rms themselves"""
     dev = dlens.device
     if dlens.pending and not torch.cuda.is_current_stream_capturing():
         check_pending(dlens)  # (a capture only records launches: no event queries in it)
@@ -655,7 +669,7 @@ def _run_protocol(dlens, launch, n_rays, group_len, keys, newton_mode, with_stat
     if len(keys) != n_groups:
         keys = [("group", g) for g in range(n_groups)]
     if newton_mode == "device" and all(k in dlens.sched_cache for k in keys):
-        _run_device(dlens, launch, n_rays, group_len, keys, need_status, epilogue)
+        _run_device(dlens, launch, n_rays, group_len, keys, need_status, rms)
         return True
     sched = dlens.initial_schedule(keys)
     # the Newton statistics and the status word share one buffer: the host reads both
@@ -720,8 +734,9 @@ def trace_pupil(dlens: DeviceLens, segments, px, py, out: RealRays, n_rays,
     buffer of ort_vjp_tape_size bytes the launch writes the adjoint tape into (Newton
     lenses; the backward then runs the reverse sweep only). rms: (rms [], stats [5]) device
     tensors that receive RayOperand.rms_spot_size of the final points: the taped kernel's
-    epilogue writes its workgroup rows (ort_options.rms_part), one ort_rms_finish launch
-    combines them (needs the tape and one wavelength)."""
+    epilogue writes its workgroup rows (ort_options.rms_part), combined by the second
+    workgroup of the device rounds' finish launch (ort_newton_finish_rms) or by one
+    ort_rms_finish launch (needs the tape and one wavelength)."""
     lib = _native.load()
     seg_dev = (segments if torch.is_tensor(segments) else
                dlens.resident("segments", np.asarray(segments, dtype=_abi.SEGMENT)))
@@ -750,12 +765,8 @@ def trace_pupil(dlens: DeviceLens, segments, px, py, out: RealRays, n_rays,
         rc = lib.ort_trace_pupil(*args, C.byref(opt), rec_p, _ptr(stats), _ptr(status), stream)
         _native.check(rc, "ort_trace_pupil")
 
-    def finish_rms():
-        rc = lib.ort_rms_finish(_ptr(part), rows, _ptr(rms[1]), _ptr(rms[0]), _stream_handle())
-        _native.check(rc, "ort_rms_finish")
-
     _run(dlens, launch, n_rays, group_len, list(keys), newton_mode,
-         epilogue=finish_rms if rms is not None and n_rays > 0 else None)
+         rms=(part, rows, rms[1], rms[0]) if rms is not None and n_rays > 0 else None)
     return seg_dev
 
 
