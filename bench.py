@@ -440,10 +440,19 @@ def config5(args, dev, rank, world, torch):
         # replays (ort_sweep.h adj_ray), with U the verified schedule -- read after the run
         tape_bytes_per_launch=lambda: _tape_read_bytes(lens, R),
         # the adjoint launch's algorithmic HBM bytes: the tape read, the pupil samples
-        # (16 B/ray), the primal outputs it reads (L, M, N, i: 32 B/ray), the cotangents
-        # (x, y: 16 B/ray) and the block partials written (30 Zernike slots + 1 per 256 rays)
-        algorithmic_bytes_per_launch=lambda: (_tape_read_bytes(lens, R) + (16 + 32 + 16) * R
-                                              + 31 * 8 * (R // 256)))
+        # (16 B/ray), the primal outputs it reads (L, M, N, i and, for the rms gradient
+        # folded into its cotangent load, x, y: 48 B/ray; no cotangent buffers) and the
+        # block partials written (the monomial slots of the Zernike surfaces, per 256 rays)
+        algorithmic_bytes_per_launch=lambda: (_tape_read_bytes(lens, R) + (16 + 48) * R
+                                              + _mono_slots(lens) * 8 * (R // 256)))
+
+
+def _mono_slots(lens):
+    """The adjoint's monomial-basis slots (ops.mono_slot_count) of the lowered lens."""
+    from optiland_pr_amd import ops
+
+    dl = next(iter(getattr(lens, "_lowered", {}).values()), None)
+    return 0 if dl is None else ops.mono_slot_count(dl.table, True)
 
 
 def _tape_read_bytes(lens, R):
