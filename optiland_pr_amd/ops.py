@@ -646,6 +646,9 @@ def trace_pupil(lens: list[torch.Tensor], lens_meta: list[int], final_thickness:
                        device=dl.device)
     rms = torch.empty(() if want_rms else 0, dtype=torch.float64, device=dl.device)
     rms_stats = torch.empty(5 if want_rms else 0, dtype=torch.float64, device=dl.device)
+    if want_rms and n == 0:  # the mean over no points: NaN (no finish launch runs)
+        rms.fill_(float("nan"))
+        rms_stats.fill_(float("nan"))
     _trace(dl, seg, px, py, out, n, seg_len, n, keys=_plan_keys(plan_key),
            pupil_per_ray=bool(ppr), newton_mode=NEWTON_MODES[mode],
            tape=tape if want_tape else None, rms=(rms, rms_stats) if want_rms else None)
