@@ -204,13 +204,19 @@ def test_device_rounds_reuse_their_buffers(torch):
         assert torch.equal(c, copies[0])
 
 
+@pytest.mark.parametrize("path", ["verify_retrace", "fixup_run_if"])
 @pytest.mark.parametrize("offset", [+5, -1])
-def test_taped_rounds_stride_and_correct(torch, offset):
+def test_taped_rounds_stride_and_correct(torch, offset, path, monkeypatch):
     """The config-5 step (taped forward, fused rms) with more rays than one grid of the
     verify rounds covers (kVerifyGrid = 1024 workgroups = 262,144 rays; 600,000 here, so
     the F_STRIDE kernels loop): a wrong warm schedule is corrected by re-traces in those
-    rounds, and loss and gradients equal the host-verified step bit for bit."""
+    rounds -- the verify-and-re-trace launches, or the two-launch rounds (ort_newton_fixup +
+    a run_if re-launch, also on the grid-stride kernel) -- and loss and gradients equal the
+    host-verified step bit for bit."""
     from optiland_pr_amd import raytrace
+
+    if path == "fixup_run_if":
+        monkeypatch.setattr(raytrace, "VERIFY_MAX_SCHED", 0)
     from optiland_pr_amd.distribution import RandomDistribution
     from optiland_pr_amd.operands import RayOperand
     from optiland_pr_amd.samples import ThreeMirrorAnastigmat
