@@ -858,12 +858,6 @@ ORT_INLINE void adj_ray(const KArgs& a, const AArgs& j, Lane& ln, int64_t rid, b
     q.opd = 0.0;
     q.att = 0.0;
     const double t = ORT_TAPE_LD(tp[6 * TS]);
-#ifdef ORT_ADJ_TK_PREFETCH
-    // the newest taped Newton iterate (m = 0), loaded with the surface's rows: one memory
-    // round trip per surface instead of two when it replays one update (A/B builds)
-    const bool newton_s = s.geometry != ORT_GEOM_PLANE && s.geometry != ORT_GEOM_STANDARD;
-    const double tk0 = newton_s ? ORT_TAPE_LD(tp[7 * TS]) : 0.0;
-#endif
     localize(a, s, q);
     const double x1 = q.x + t * q.L;
     const double y1 = q.y + t * q.M;
@@ -949,11 +943,10 @@ ORT_INLINE void adj_ray(const KArgs& a, const AArgs& j, Lane& ln, int64_t rid, b
       double tb = bt;
       for (int m = 0; m < m_end; ++m) {
         const bool on = m < Uk;
-#ifdef ORT_ADJ_TK_PREFETCH
-        const double tk = m == 0 ? tk0 : ORT_TAPE_LD(tp[(7 + m) * TS]);
-#else
+        // (loaded here, a second round trip per surface; loading the newest iterate with
+        // the surface's rows measured the same: config 5 step 0.4917 / 0.4953 vs 0.4925 /
+        // 0.4929 ms, tools/gpu_r05u.sh)
         const double tk = ORT_TAPE_LD(tp[(7 + m) * TS]);
-#endif
         const double xk = q.x + tk * q.L, yk = q.y + tk * q.M, zk = q.z + tk * q.N;
         D kx, ky, kz;
         const D sk = sagnorm(s, xk, yk, kx, ky, kz);
