@@ -363,6 +363,10 @@ ORT_INLINE void unit_normal3(const T& dzdx, const T& dzdy, const T& norm, T& nx,
 //              |f| with tol, far from the rounding of one step).
 enum : int { kNoNormal = 0, kNormal = 1, kSlope = 2 };
 
+// The Cartesian Zernike slopes are Gx / Rn off the disc rho^2 < kZernChainRho2 (normalised
+// coordinates), the reference's eps-guarded polar chain on it (sagnorm_zernike)
+constexpr double kZernChainRho2 = 1e-4;
+
 // (fx, fy, -1) of the reference's update from a unit normal
 template <class T>
 ORT_INLINE void slope_from_normal(T& nx, T& ny, T& nz) {
@@ -1199,16 +1203,37 @@ ORT_INLINE T sagnorm_zernike(const T& x, const T& y, const S& R, const S& k, dou
         double dzdx, dzdy;
         div2(x, y, R * q, dzdx, dzdy);
         const double eps = 1e-14;
-        const double rho = sqrt(xn * xn + yn * yn);
-        double xr, yr, drho_dx, drho_dy, qy, qx;
-        div2(x, y, Rn * Rn, xr, yr);
-        div2(xr, yr, rho + eps, drho_dx, drho_dy);
-        div2(-(yn), xn, rho * rho + eps, qy, qx);
-        const double inv_rn = 1.0 / Rn;
-        const double G1 = xn * Gx + yn * Gy, G2 = xn * Gy - yn * Gx;
-        const double Fr = rho > 0.0 ? G1 / rho : 0.0;
-        dzdx = dzdx + (Fr * drho_dx + G2 * (qy * inv_rn));
-        dzdy = dzdy + (Fr * drho_dy + G2 * (qx * inv_rn));
+        // The term sum's slopes. The reference forms them through (rho, phi) with eps guards
+        // (zernike.py:190-214): dF/drho drho/dx + dF/dphi dphi/dx with drho/dx = (x / Rn^2) /
+        // (rho + eps), dphi/dx = -yn / (rho^2 + eps) / Rn, dF/drho = (xn Gx + yn Gy) / rho,
+        // dF/dphi = xn Gy - yn Gx (G: the block's Cartesian gradient). Without the guards
+        // that is exactly Gx / Rn; with them it differs by ~eps / rho^2 relative, which
+        // matters only near the axis (rho^2 < 1e-4: the guards bend the reference's normal
+        // there, and its value on the axis is 0). So off that disc the slopes are Gx / Rn,
+        // Gy / Rn (2 products instead of a square root and four divisions; < 1e-10
+        // relative from the reference's), on it the reference's own chain. The adjoint's
+        // pull-back (ort_sweep.h zern_adj) takes the same branch. (ORT_ZERN_POLAR_CHAIN,
+        // A/B builds: the chain everywhere.)
+        const double rho2n = xn * xn + yn * yn;
+#ifndef ORT_ZERN_POLAR_CHAIN
+        if (rho2n >= kZernChainRho2) {
+          const double inv_rn = 1.0 / Rn;
+          dzdx = dzdx + Gx * inv_rn;
+          dzdy = dzdy + Gy * inv_rn;
+        } else
+#endif
+        {
+          const double rho = sqrt(rho2n);
+          double xr, yr, drho_dx, drho_dy, qy, qx;
+          div2(x, y, Rn * Rn, xr, yr);
+          div2(xr, yr, rho + eps, drho_dx, drho_dy);
+          div2(-(yn), xn, rho * rho + eps, qy, qx);
+          const double inv_rn = 1.0 / Rn;
+          const double G1 = xn * Gx + yn * Gy, G2 = xn * Gy - yn * Gx;
+          const double Fr = rho > 0.0 ? G1 / rho : 0.0;
+          dzdx = dzdx + (Fr * drho_dx + G2 * (qy * inv_rn));
+          dzdy = dzdy + (Fr * drho_dy + G2 * (qx * inv_rn));
+        }
         if (want_normal == kSlope && slope_direct(dzdx, dzdy)) {
           nx = dzdx;
           ny = dzdy;

@@ -665,25 +665,37 @@ ORT_INLINE void adj_ray(const KArgs& a, const AArgs& j, Lane& ln, int64_t rid, b
         const double bdx = -nzv * (bnx - nxv * bn);
         const double bdy = -nzv * (bny - nyv * bn);
         if (mono_base >= 0) {
-          // the Cartesian normal's slopes (sagnorm_zernike): dzdx += Fr drho_dx + G2 qy / Rn,
-          // dzdy += Fr drho_dy + G2 qx / Rn with Fr = (xn Gx + yn Gy) / rho (0 at rho = 0)
-          // and G2 = xn Gy - yn Gx: their adjoints (bdx, bdy) pulled back to (Gx, Gy)
+          // the Cartesian normal's slopes (sagnorm_zernike): their adjoints (bdx, bdy)
+          // pulled back to the block gradient (Gx, Gy)
           double xn, yn;
           ort::div2(x, y, s.norm_radius, xn, yn);
-          const double eps = 1e-14;
-          const double rho = sqrt(xn * xn + yn * yn);
-          const double Rn = s.norm_radius;
-          double xr, yr, drx, dry, qy, qx;
-          ort::div2(x, y, Rn * Rn, xr, yr);
-          ort::div2(xr, yr, rho + eps, drx, dry);
-          ort::div2(-(yn), xn, rho * rho + eps, qy, qx);
-          const double inv_rn = 1.0 / Rn;
-          double cx = 0.0, cy = 0.0;  // xn / rho, yn / rho (Fr's factors)
-          if (rho > 0.0) ort::div2(xn, yn, rho, cx, cy);
-          const double fr = bdx * drx + bdy * dry;        // adjoint of Fr
-          const double g2 = (bdx * qy + bdy * qx) * inv_rn;  // adjoint of G2
-          const double ax = fr * cx - g2 * yn;
-          const double ay = fr * cy + g2 * xn;
+          // sagnorm_zernike's slopes: Gx / Rn, Gy / Rn off the disc rho^2 < kZernChainRho2
+          // (their adjoint: (bdx, bdy) / Rn), the reference's chain on it
+          const double rho2n = xn * xn + yn * yn;
+          double ax, ay;
+#ifndef ORT_ZERN_POLAR_CHAIN
+          if (rho2n >= ort::kZernChainRho2) {
+            const double inv_rn = 1.0 / s.norm_radius;
+            ax = bdx * inv_rn;
+            ay = bdy * inv_rn;
+          } else
+#endif
+          {
+            const double eps = 1e-14;
+            const double rho = sqrt(rho2n);
+            const double Rn = s.norm_radius;
+            double xr, yr, drx, dry, qy, qx;
+            ort::div2(x, y, Rn * Rn, xr, yr);
+            ort::div2(xr, yr, rho + eps, drx, dry);
+            ort::div2(-(yn), xn, rho * rho + eps, qy, qx);
+            const double inv_rn = 1.0 / Rn;
+            double cx = 0.0, cy = 0.0;  // xn / rho, yn / rho (Fr's factors)
+            if (rho > 0.0) ort::div2(xn, yn, rho, cx, cy);
+            const double fr = bdx * drx + bdy * dry;        // adjoint of Fr
+            const double g2 = (bdx * qy + bdy * qx) * inv_rn;  // adjoint of G2
+            ax = fr * cx - g2 * yn;
+            ay = fr * cy + g2 * xn;
+          }
           const double wx = on ? ax : 0.0, wy = on ? ay : 0.0;
           if (first)  // the hit point: the normal only (w_sag == 0)
             zmono_adjoint_deg<false>(ln, s.zm_deg, mono_base, xn, yn, 0.0, wx, wy);
