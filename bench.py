@@ -355,7 +355,7 @@ def config5(args, dev, rank, world, torch):
 
     def problem(capturable):
         """The TMA with device-resident coefficient leaves, its Adam and loss."""
-        lens = ThreeMirrorAnastigmat()
+        lens = ThreeMirrorAnastigmat(args.zernike_scheme)
         # Newton schedules verified on the device once warm (ort_newton_fixup): the same
         # schedules and results as the host check, without its per-step host round trip;
         # range errors / unsettled schedules surface at raytrace.check_all_pending (below)
@@ -423,9 +423,10 @@ def config5(args, dev, rank, world, torch):
         metric="TMA Zernike optimisation steps: ray-surface intersections/sec of forward + "
                "backward (d rms_spot / d coeff) at 1M rays",
         unit="intersections/s", units=world * R * S, step=step, scaling="weak",
-        config={"workload": "TMA (Tutorial_7d), 3 fringe-Zernike mirrors x 10 coefficients, "
-                            "1M random rays, Hy=1, lambda 0.587: lens update + trace + "
-                            "rms_spot_size + backward (VJP) + Adam",
+        config={"workload": f"TMA (Tutorial_7d), 3 {args.zernike_scheme}-Zernike mirrors x 10 "
+                            "coefficients, 1M random rays, Hy=1, lambda 0.587: lens update + "
+                            "trace + rms_spot_size + backward (VJP) + Adam",
+                "zernike_scheme": args.zernike_scheme,
                 "optimizer": "torch.optim.Adam(fused=True) + patch" if args.torch_adam else
                              "optim.ZernikeAdam (torch Adam's update + the lens patch, one launch)",
                 "rays_per_gpu": R, "surfaces": S, "parameters": 30,
@@ -509,6 +510,10 @@ def main():
     ap.add_argument("--torch-adam", action="store_true",
                     help="config 5: torch.optim.Adam(fused=True) and the trace's own coefficient "
                          "patch instead of the fused optim.ZernikeAdam launch")
+    ap.add_argument("--zernike-scheme", default="fringe", choices=["fringe", "standard", "noll"],
+                    help="config 5: the Zernike indexing of the TMA mirrors (SURVEY 8d.5 names "
+                         "fringe and standard; standard / noll normals omit the normalisation "
+                         "constant, zernike.py:162-231)")
     ap.add_argument("--eager", action="store_true",
                     help="config 5: issue the optimisation step eagerly instead of as one HIP "
                          "graph replay")
@@ -788,7 +793,7 @@ def _cpu_workload(args):
         segs = np.stack([segment_params(lens, 0.0, float(h), wi)
                          for h in np.linspace(0, 1, 7) for wi in range(7)])[:3]
         return table, segs, max(1, args.cpu_rays // 10), "ReverseTelephoto"
-    lens = samples.ThreeMirrorAnastigmat()
+    lens = samples.ThreeMirrorAnastigmat(getattr(args, "zernike_scheme", "fringe"))
     table = lower_surface_group(lens.surface_group, [0.587])
     segs = np.stack([segment_params(lens, 0.0, 1.0, 0)])
     return table, segs, max(1, args.cpu_rays // 10), "TMA (forward trace only: the oracle " \

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define ORT_ABI_VERSION 18
+#define ORT_ABI_VERSION 19
 #define ORT_MAX_SURFACES 64
 
 /* ---- geometry kinds ----------------------------------- */
@@ -77,8 +77,12 @@ enum ort_surface_flags {
   ORT_SURF_INV_R2 = 1u << 6,       /* inv_r2 holds RN(1 / (R * R)) (finite, normal range)  */
   ORT_SURF_ALPHA_ALL = 1u << 7,    /* optics.alpha_pre > 0 at every wavelength row: the     */
                                    /* absorption step runs unconditionally (homogeneous.py) */
-  ORT_SURF_ALPHA_NONE = 1u << 8    /* optics.alpha_pre == 0 at every row: no absorption     */
+  ORT_SURF_ALPHA_NONE = 1u << 8,   /* optics.alpha_pre == 0 at every row: no absorption     */
                                    /* (neither bit: decided per ray / row)                  */
+  /* (v19) the Newton slope is not the sag's derivative: a Zernike surface with a term whose
+   * normalisation is not 1 (standard / noll: zernike.py:163-231 omits it from the normal).
+   * The adjoint VJP then replays every Newton update, not only the last kHist (4). */
+  ORT_SURF_SLOPE_INEXACT = 1u << 9
 };
 
 /* ---- lens-wide frame facts (ort_lens.frame_flags) --------------------------------- */
@@ -425,10 +429,12 @@ typedef struct ort_options {
    * device; lenses with Newton surfaces only). With ort_newton_fixup this re-traces on a
    * corrected schedule without a host round trip. */
   const int32_t* run_if;
-  /* nullable device double [n_surfaces][11][n_rays] (ort_vjp_tape_size bytes): a
-   * ORT_NEWTON_SCHEDULE launch of ort_trace_pupil on a lens with Newton surfaces writes
+  /* nullable device double [rows][n_rays] (v19: rows = the sum over the surfaces of 7 for
+   * a plane / conic, 11 for a Newton surface, surface by surface; ort_vjp_tape_size bytes
+   * hold any lens's tape): a Newton-lens launch with this set writes
    * the adjoint tape of its own rays as it traces (each surface's incoming global ray,
-   * its distance t and the Newton iterates before the last four updates), so the
+   * its distance t and the Newton iterates before the last four updates, the initial
+   * guess in the iterate rows no update fills -- every row written), so the
    * backward (ort_vjp_params.tape) runs the reverse sweep only */
   double* tape;
   /* Verify-and-re-trace (ABI v14; nullable): with verify_stats set, the launch first
@@ -526,10 +532,14 @@ int ort_trace_pupil(const ort_lens* lens, const double* px, const double* py,
  *   it); one re-trace per 4 parameters. Needs a device workspace of
  *   ort_vjp_workspace_size() bytes (v15: the per-block partial sums, reduced in a fixed
  *   order -- the gradient is the same bits run to run).
- * mode ORT_VJP_ADJOINT: one reverse-mode pass whatever n_param (the intersection
- *   distance differentiated through its implicit equation; equals the unrolled
- *   derivative to the Newton residual when the Newton slope is the sag's derivative --
- *   not for standard / noll Zernike normals, which omit the normalisation constant).
+ * mode ORT_VJP_ADJOINT: one reverse-mode pass whatever n_param: closed-form
+ *   intersections through their implicit equations, Newton intersections through the
+ *   last kHist = 4 updates of the unrolled iteration (taped iterates) and the initial
+ *   guess -- the unrolled derivative exactly when a surface ran U <= 4 updates; with
+ *   U > 4 the older updates are dropped (their share is a product of converged
+ *   residuals) except on ORT_SURF_SLOPE_INEXACT surfaces (standard / noll Zernike, whose
+ *   Newton slope omits the normalisation constant and converges linearly), where U > 4
+ *   writes NaN into the gradient: take ORT_VJP_UNROLLED for such a schedule (v19).
  *   Needs n_zern and a device workspace of ort_vjp_workspace_size() bytes, and at most
  *   ORT_VJP_ADJOINT_MAX_SLOTS parameter slots, 3 n_surfaces + n_zern + 1 (v17: the
  *   slots' per-block partial sums live in LDS); beyond that use ORT_VJP_UNROLLED. */
@@ -583,7 +593,9 @@ typedef struct ort_vjp_params {
  * without the tape when params->tape is set). */
 int64_t ort_vjp_workspace_size(const ort_lens* lens, const ort_batch* batch,
                                const ort_vjp_params* params);
-/* Bytes of the adjoint tape of one trace (ort_options.tape, ort_vjp_params.tape). */
+/* Bytes that hold the adjoint tape of one trace of this lens (ort_options.tape,
+ * ort_vjp_params.tape): n_surfaces x 11 rows of n_rays doubles, the most any lens of
+ * n_surfaces surfaces writes (v19: the tape itself has 7 rows per plane / conic). */
 int64_t ort_vjp_tape_size(const ort_lens* lens, const ort_batch* batch);
 
 /* Backward of ort_trace_pupil: the vector-Jacobian product
@@ -654,8 +666,10 @@ int ort_patch_zernike_ptrs(const ort_lens* lens, const double* const* c_ptrs,
  * off; weight_decay the L2 form: grad + weight_decay * param) of up to ORT_ADAM_MAX_TENSORS
  * parameter tensors, each the coefficients of term rows [row0, row0 + count) of
  * lens->zern, then every touched surface re-formed as ort_patch_zernike does -- one launch
- * for the optimiser's two and the patch. step: device doubles [n_surfaces], the Adam step
- * count of each surface's coefficients (incremented here, before the update, as torch does).
+ * for the optimiser's two and the patch. step[k] (v19): a device double, tensor k's Adam
+ * step count (torch.optim.Adam's state["step"], incremented here before the update, as torch
+ * does); each tensor's rows lie within one Zernike surface, so one workgroup updates it and
+ * its count, once per call.
  * Pointers by value (no device pointer table): a HIP graph captures the launch as is.
  * Replaces the optimiser step of optimization/optimizer/torch/base.py:116-132 for
  * ZernikeCoefficientVariables followed by the lens update of the next trace. */
@@ -669,7 +683,7 @@ typedef struct ort_adam_params {
   double* exp_avg_sq[ORT_ADAM_MAX_TENSORS];
   int64_t row0[ORT_ADAM_MAX_TENSORS];
   int64_t count[ORT_ADAM_MAX_TENSORS];
-  double* step;
+  double* step[ORT_ADAM_MAX_TENSORS]; /* v19: per tensor (v18: one per surface) */
   double lr, beta1, beta2, eps, weight_decay;
 } ort_adam_params;
 int ort_adam_patch_zernike(const ort_lens* lens, const ort_adam_params* p, void* stream);

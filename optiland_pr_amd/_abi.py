@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import numpy as np
 
-ABI_VERSION = 18
+ABI_VERSION = 19
 VJP_UNROLLED = 0
 VJP_ADJOINT = 1
 AP_RADIAL = 1
@@ -55,6 +55,7 @@ SURF_APERTURE_PROG = 1 << 5
 SURF_INV_R2 = 1 << 6
 SURF_ALPHA_ALL = 1 << 7
 SURF_ALPHA_NONE = 1 << 8
+SURF_SLOPE_INEXACT = 1 << 9  # (v19) the Newton slope is not the sag's derivative
 LENS_AXIAL = 1 << 0  # ort_lens.frame_flags
 
 # enum ort_interaction / ort_phase_kind
@@ -212,4 +213,5 @@ CONV_WINDOW = 128  # stop indices per conv_mask window (ort_options.conv_base)
 
 RAY_FIELDS = ("x", "y", "z", "L", "M", "N", "i", "opd")
 
-VJP_ADJOINT_MAX_SLOTS = 512  # ORT_VJP_ADJOINT_MAX_SLOTS: 3 S + n_zern + 1 at most
+VJP_ADJOINT_MAX_SLOTS = 512
+ADJ_HIST = 4  # ort_sweep.h kHist: Newton iterates the adjoint tape keeps per surface  # ORT_VJP_ADJOINT_MAX_SLOTS: 3 S + n_zern + 1 at most

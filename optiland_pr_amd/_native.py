@@ -79,7 +79,7 @@ class ort_vjp_params(C.Structure):  # field 7 ("grad_init") was "reserved" befor
 ADAM_MAX_TENSORS = 16  # include/optiland_rt.h ORT_ADAM_MAX_TENSORS
 
 
-class ort_adam_params(C.Structure):  # v18
+class ort_adam_params(C.Structure):  # v19
     _fields_ = [
         ("n_tensors", C.c_int32),
         ("reserved", C.c_int32),
@@ -89,7 +89,7 @@ class ort_adam_params(C.Structure):  # v18
         ("exp_avg_sq", C.c_void_p * ADAM_MAX_TENSORS),
         ("row0", C.c_int64 * ADAM_MAX_TENSORS),
         ("count", C.c_int64 * ADAM_MAX_TENSORS),
-        ("step", C.c_void_p),
+        ("step", C.c_void_p * ADAM_MAX_TENSORS),
         ("lr", C.c_double),
         ("beta1", C.c_double),
         ("beta2", C.c_double),

@@ -109,13 +109,19 @@ def parameter_map(table, params):
     return zp, off
 
 
-def vjp_mode(table):
-    """ORT_VJP_ADJOINT (one reverse-mode pass) unless a Zernike surface's Newton slope is
-    not its sag's derivative -- the standard / noll normal omits the normalisation
-    constant (zernike.py:163-231), so the unrolled iteration's derivative only converges
-    linearly to the implicit one there and the forward-mode ORT_VJP_UNROLLED keeps the
-    reference's semantics -- or the lens has more parameter slots than the adjoint holds
-    (ORT_VJP_ADJOINT_MAX_SLOTS). ORT_VJP_MODE=unrolled|adjoint overrides (A/B checks)."""
+def vjp_mode(table, sched=None):
+    """ORT_VJP_ADJOINT (one reverse-mode pass) unless the lens has more parameter slots
+    than the adjoint holds (ORT_VJP_ADJOINT_MAX_SLOTS), or a surface whose Newton slope is
+    not its sag's derivative (SURF_SLOPE_INEXACT: the standard / noll Zernike normal omits
+    the normalisation constant, zernike.py:163-231, so the unrolled iteration converges
+    linearly) ran more updates than the adjoint tape keeps (ADJ_HIST): the forward-mode
+    ORT_VJP_UNROLLED then differentiates every update. With U <= ADJ_HIST the tape holds
+    every iterate and the adjoint is the unrolled derivative on any surface.
+
+    sched: the verified Newton schedule ([n_groups][S] update counts, host array or
+    tensor) when known, else None -- then the adjoint runs, and a schedule the device
+    raised past ADJ_HIST on such a surface poisons the gradient with NaN rather than
+    truncating it (ort_sweep.h). ORT_VJP_MODE=unrolled|adjoint overrides (A/B checks)."""
     env = os.environ.get("ORT_VJP_MODE", "").lower()
     if env in ("unrolled", "adjoint"):
         return _abi.VJP_UNROLLED if env == "unrolled" else _abi.VJP_ADJOINT
@@ -124,12 +130,42 @@ def vjp_mode(table):
     z = table.zern
     if 3 * table.n_surfaces + len(z) + 1 + mono_slot_count(table, z) > _abi.VJP_ADJOINT_MAX_SLOTS:
         return _abi.VJP_UNROLLED  # more parameter slots than the adjoint's LDS partials hold
-    live = z["c"] != 0.0
-    for off, t in getattr(table, "device_coeffs", ()):  # values not on the host
-        live[off:off + int(t.numel())] = True
-    if len(z) and np.any(live & (z["norm"] != 1.0)):
+    if sched is not None and inexact_updates(table, sched) > _abi.ADJ_HIST:
         return _abi.VJP_UNROLLED
     return _abi.VJP_ADJOINT
+
+
+def inexact_surfaces(table):
+    """bool [S]: the surfaces whose Newton slope is not the sag's derivative"""
+    return (table.surfaces["flags"] & _abi.SURF_SLOPE_INEXACT) != 0
+
+
+def inexact_updates(table, sched):
+    """The most Newton updates any SURF_SLOPE_INEXACT surface ran under `sched` (0: none)"""
+    mask = inexact_surfaces(table)
+    if not mask.any() or sched is None:
+        return 0
+    if torch is not None and torch.is_tensor(sched):
+        sched = sched.detach().cpu().numpy()
+    s = np.asarray(sched).reshape(-1, table.n_surfaces)
+    return int(s[:, mask].max()) if s.size else 0
+
+
+def schedule_for_mode(table, sched_t, hint=None):
+    """The schedule vjp_mode should see for a backward: nothing to read when the lens has
+    no SURF_SLOPE_INEXACT surface; else the saved schedule tensor (a host tensor, or a
+    device one copied back -- one small synchronising read, only for such lenses), or
+    while a HIP graph is being captured (no synchronisation allowed) `hint`, the host's
+    cached schedule the captured trace starts from."""
+    if not inexact_surfaces(table).any():
+        return None
+    if sched_t is None or sched_t.numel() == 0:
+        return hint
+    if sched_t.device.type == "cpu":
+        return sched_t
+    if torch.cuda.is_current_stream_capturing():
+        return hint
+    return sched_t.cpu()
 
 
 _WORKSPACE = {}
@@ -225,7 +261,7 @@ def trace_pupil_grad(optic, dlens, seg_dev, px, py, n, seg_len, wavelength, keys
     plan = ops.PupilPlan(dlens, seg_dev, px, py, n, seg_len, keys, newton_mode=newton_mode)
     # adjoint-mode backward of a Newton lens: let the forward write the tape
     plan.want_tape = (bool(params) and bool(dlens.newton) and TAPED_FORWARD
-                      and vjp_mode(dlens.table) == _abi.VJP_ADJOINT
+                      and vjp_mode(dlens.table, dlens.cached_schedule(keys)) == _abi.VJP_ADJOINT
                       and not dlens.table.interaction_mask & ~(1 << _abi.IA_REFRACT_REFLECT)
                       and not np.any(dlens.table.surfaces["geometry"] == _abi.GEOM_GRID_SAG))
     plan.want_rms = bool(want_rms and plan.want_tape and len(dlens.table.wavelengths) == 1)

@@ -37,7 +37,7 @@ struct AdjWaves {
 // summed over the wave and stored by lane 0 into partial[slot][wave] (one writer per slot
 // and wave; `first`: a plain store instead of a read-modify-write whose load the wave
 // would wait for -- the same value, 0 + w == w); the tape rows of the ray in HBM
-// ([S][kTapeRows][n_rays], coalesced). (Round 3 parked the adjoint state in LDS across the
+// ([rows][n_rays], coalesced). (Round 3 parked the adjoint state in LDS across the
 // Newton replay's dual-number Zernike evaluation; with the plain-double jet that costs
 // more than it saves: 657 vs 591 us at 4 waves, rocprofv3 A/B, so the state stays in
 // registers.)
@@ -118,9 +118,7 @@ struct DevLane {
     (void)first;  // the LDS entries start at zero: 0 + w == w
     if ((threadIdx.x & 63) == 0) bpart[slot][threadIdx.x >> 6] += w;
   }
-  __device__ inline double* tape(int si) const {
-    return j.tape + (int64_t)si * kTapeRows * n_rays + r_ld;
-  }
+  __device__ inline double* tape_at(int64_t row) const { return j.tape + row * n_rays + r_ld; }
   __device__ inline int64_t tape_stride() const { return n_rays; }
   __device__ inline int uniform_max(int v) const { return wave_max_i32(v); }
   // Zernike coefficient contributions of one surface (term j of the surface, slot `slot`):

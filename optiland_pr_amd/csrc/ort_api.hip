@@ -175,7 +175,7 @@ int trace_pupil_impl(const ort_lens* lens, const double* px, const double* py,
 
 extern "C" {
 
-// ORT_VJP_ADJOINT workspace: tape [S][kTapeRows][n_rays], partial [n_slot][n_wave],
+// ORT_VJP_ADJOINT workspace: tape [rows <= S kTapeRows][n_rays], partial [n_slot][n_wave],
 // slot_sum [n_slot], need [n_slot] (each 256-byte aligned).
 // ORT_VJP_UNROLLED workspace: the block partials [n_block][4] of one tangent chunk.
 struct AdjLayout {

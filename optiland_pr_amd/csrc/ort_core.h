@@ -307,6 +307,33 @@ ORT_INLINE double sdiv(double a, const SharedDiv& d) {
 #endif
 }
 
+// Quotients that only enter derivatives (the adjoint's reverse sweep and its local jets,
+// whose results are compared at rtol 1e-10, never bit for bit). IEEE by default; the
+// ORT_FAST_RDIV A/B builds take the reciprocal refined twice and one residual step
+// (within an ulp, no scale / fix-up steps) -- measured no faster on the config-5 adjoint
+// (one box, alternating: 268.97 / 261.66 us IEEE vs 273.28 / 267.99 us fast, the fast
+// build's scratch 76 -> 100 B; profiles/r06_ab_rdiv.log).
+ORT_INLINE double rrcp(double b) {
+#if defined(__HIP_DEVICE_COMPILE__) && defined(ORT_FAST_RDIV)
+  double y = __builtin_amdgcn_rcp(b);
+  double e = fma(-b, y, 1.0);
+  y = fma(y, e, y);
+  e = fma(-b, y, 1.0);
+  return fma(y, e, y);
+#else
+  return 1.0 / b;
+#endif
+}
+ORT_INLINE double rdiv(double a, double b) {
+#if defined(__HIP_DEVICE_COMPILE__) && defined(ORT_FAST_RDIV)
+  const double y = rrcp(b);
+  const double q0 = a * y;
+  return fma(fma(-b, q0, a), y, q0);
+#else
+  return a / b;
+#endif
+}
+
 template <int P>
 struct PlainDiv {
   Dual<P> b;
@@ -1454,7 +1481,9 @@ ORT_INLINE void zernike_coef_adjoint(double x, double y, double Rn, PZ Tm, int t
 struct SurfJet {
   double z, zx, zy;      // sag, d sag / dx, d sag / dy (the terms' normalisation included)
   double sx, sy;         // the normal's slopes
-  double sxx, sxy, syy;  // d sx / dx, d sx / dy (= d sy / dx), d sy / dy
+  double sxx, sxy, syy;  // d sx / dx, d sx / dy, d sy / dy
+  double syx;            // d sy / dx (= sxy for a gradient field; the eps-guarded chain of
+                         // the reference's normal near the Zernike axis is not one)
 };
 
 template <class PD, class PZ>
@@ -1462,38 +1491,83 @@ ORT_INLINE void zernike_jet(double x, double y, double R, double k, double Rn, P
                             int nt, PD coef, SurfJet& J, int zm_off = 0, int zm_deg = -1) {
   // base conic (standard.py:73-87, 154-167): z = r2 / (R (1 + q)), slope x / (R q)
   const double r2 = x * x + y * y;
-  const double q = sqrt(1.0 - (1.0 + k) * r2 / (R * R));
-  const double iRq = 1.0 / (R * q);
+  const double q = sqrt(1.0 - rdiv((1.0 + k) * r2, R * R));
+  const double iRq = rrcp(R * q);
   const double h = (1.0 + k) * iRq * iRq * iRq;  // (1 + k) / (R q)^3
-  J.z = r2 / (R * (1.0 + q));
+  J.z = rdiv(r2, R * (1.0 + q));
   J.sx = x * iRq;
   J.sy = y * iRq;
   J.sxx = iRq + h * x * x;
   J.sxy = h * x * y;
   J.syy = iRq + h * y * y;
-  const double xn = x / Rn, yn = y / Rn;
+  const double iRn = rrcp(Rn);
+  const double xn = x * iRn, yn = y * iRn;
   if (zm_deg >= 0) {  // Cartesian form (zmono_*): exact derivatives of both polynomials
     const int K = (zm_deg + 1) * (zm_deg + 2) / 2;
-    const double iRn = 1.0 / Rn;
     double F, Fx, Fy, G, Gx, Gy, Gxx, Gxy, Gyy;
     zmono_grad(coef + zm_off, zm_deg, xn, yn, F, Fx, Fy);
     zmono_hess(coef + zm_off + K, zm_deg, xn, yn, G, Gx, Gy, Gxx, Gxy, Gyy);
     J.z += F;
     J.zx = J.sx + Fx * iRn;
     J.zy = J.sy + Fy * iRn;
-    J.sx += Gx * iRn;
-    J.sy += Gy * iRn;
-    const double iRn2 = iRn * iRn;
-    J.sxx += Gxx * iRn2;
-    J.sxy += Gxy * iRn2;
-    J.syy += Gyy * iRn2;
+    const double rho2n = xn * xn + yn * yn;
+#ifndef ORT_ZERN_POLAR_CHAIN
+    // (ORT_JET_NO_DISC, A/B builds only: the unguarded derivatives on the disc too)
+#ifdef ORT_JET_NO_DISC
+    if (true) {
+#else
+    if (rho2n >= kZernChainRho2) {
+#endif
+      J.sx += Gx * iRn;
+      J.sy += Gy * iRn;
+      const double iRn2 = iRn * iRn;
+      J.sxx += Gxx * iRn2;
+      J.sxy += Gxy * iRn2;
+      J.syx = J.sxy;
+      J.syy += Gyy * iRn2;
+      return;
+    }
+#endif
+    // near the axis the forward's slopes are the reference's eps-guarded chain
+    // (sagnorm_zernike): S = Rn sx = a G1 u - c G2 v, T = Rn sy = a G1 v + c G2 u with
+    // u, v = xn, yn, a = 1 / (rho (rho + eps)), c = 1 / (rho^2 + eps), G1 = u Gx + v Gy,
+    // G2 = u Gy - v Gx -- differentiated as the reference's autograd does, the block's
+    // gradient carrying its Hessian (no symmetry: the guarded chain is no gradient field)
+    const double eps = 1e-14;
+    const double u = xn, v = yn;
+    const double rho = sqrt(rho2n);
+    if (rho > 0.0) {
+      const double a = rrcp(rho * (rho + eps)), c = rrcp(rho2n + eps);
+      const double ka = -a * a * rdiv(2.0 * rho + eps, rho), kc = -2.0 * c * c;  // a_u = ka u
+      const double G1 = u * Gx + v * Gy, G2 = u * Gy - v * Gx;
+      const double G1u = Gx + u * Gxx + v * Gxy, G1v = Gy + u * Gxy + v * Gyy;
+      const double G2u = Gy + u * Gxy - v * Gxx, G2v = u * Gyy - Gx - v * Gxy;
+      const double aG1 = a * G1, cG2 = c * G2;
+      const double pa = ka * G1, pc = kc * G2;  // d(a G1) = pa (u, v) + a dG1, likewise c
+      const double iRn2 = iRn * iRn;
+      const double E = pa * u - pc * v, H = pa * v + pc * u;
+      const double au = a * u, av = a * v, cu = c * u, cv = c * v;
+      J.sx += (aG1 * u - cG2 * v) * iRn;
+      J.sy += (aG1 * v + cG2 * u) * iRn;
+      J.sxx += (u * E + au * G1u - cv * G2u + aG1) * iRn2;
+      J.syx = J.sxy + (u * H + av * G1u + cu * G2u + cG2) * iRn2;
+      J.sxy += (v * E + au * G1v - cv * G2v - cG2) * iRn2;
+      J.syy += (v * H + av * G1v + cu * G2v + aG1) * iRn2;
+    } else {  // on the axis: the forward's slopes are 0 + the conic's (Fr = 0, G2 = 0)
+      const double iRn2 = iRn * iRn;
+      J.sxx += Gxx * iRn2;
+      J.sxy += Gxy * iRn2;
+      J.syx = J.sxy;
+      J.syy += Gyy * iRn2;
+    }
     return;
   }
   const double rho = sqrt(xn * xn + yn * yn);
   double c1 = 1.0, s1 = 0.0;  // cos / sin phi (atan2(0, 0) = 0)
   if (rho > 0.0) {
-    c1 = xn / rho;
-    s1 = yn / rho;
+    const double ir = rrcp(rho);
+    c1 = xn * ir;
+    s1 = yn * ir;
   }
   const double u = rho * rho;
   double Z = 0.0, Gr = 0.0, Gp = 0.0, Qr = 0.0, Qp = 0.0, Qrr = 0.0, Qrp = 0.0, Qpp = 0.0;
@@ -1530,9 +1604,9 @@ ORT_INLINE void zernike_jet(double x, double y, double R, double k, double Rn, P
       P1 = F;
       P2 = 2.0 * rho * (3.0 * H1 + 2.0 * u * H2);
     } else {
-      const double pw2 = pw / (rho * rho);  // rho^(am - 2) (rho > 0 here, else pw = 0)
+      const double pw2 = rdiv(pw, rho * rho);  // rho^(am - 2) (rho > 0 here, else pw = 0)
       P = H * pw;
-      P1 = rho > 0.0 ? F * (pw / rho) : 0.0;
+      P1 = rho > 0.0 ? F * rdiv(pw, rho) : 0.0;
       P2 = rho > 0.0 ? pw2 * ((am - 1.0) * F + 2.0 * u * ((2.0 + am) * H1 + 2.0 * u * H2))
                      : (am == 2 ? 2.0 * H : 0.0);
     }
@@ -1558,10 +1632,10 @@ ORT_INLINE void zernike_jet(double x, double y, double R, double k, double Rn, P
     Qpp -= cz * (double)(am * am) * P * A;
   }
   const double eps = 1e-14;
-  const double ir = 1.0 / ((rho + eps) * Rn);  // 1 / (rho R_n), guarded
-  const double rx = c1 / Rn, ry = s1 / Rn;     // d rho / dx, d rho / dy
+  const double ir = rrcp((rho + eps) * Rn);  // 1 / (rho R_n), guarded
+  const double rx = c1 * iRn, ry = s1 * iRn;  // d rho / dx, d rho / dy
   const double px = -s1 * ir, py = c1 * ir;    // d phi / dx, d phi / dy
-  const double rxx = s1 * s1 * ir / Rn, rxy = -c1 * s1 * ir / Rn, ryy = c1 * c1 * ir / Rn;
+  const double rxx = s1 * s1 * ir * iRn, rxy = -c1 * s1 * ir * iRn, ryy = c1 * c1 * ir * iRn;
   const double pxx = 2.0 * c1 * s1 * ir * ir, pxy = (s1 * s1 - c1 * c1) * ir * ir;
   J.z += Z;
   J.zx = J.sx + Gr * rx + Gp * px;
@@ -1571,6 +1645,7 @@ ORT_INLINE void zernike_jet(double x, double y, double R, double k, double Rn, P
   J.sxx += Qrr * rx * rx + 2.0 * Qrp * rx * px + Qpp * px * px + Qr * rxx + Qp * pxx;
   J.sxy += Qrr * rx * ry + Qrp * (rx * py + ry * px) + Qpp * px * py + Qr * rxy + Qp * pxy;
   J.syy += Qrr * ry * ry + 2.0 * Qrp * ry * py + Qpp * py * py + Qr * ryy - Qp * pxx;
+  J.syx = J.sxy;
 }
 
 // the unit normal n = (sx, sy, -1) / |(sx, sy, -1)| of a jet and its x / y derivatives:
@@ -1578,13 +1653,13 @@ ORT_INLINE void zernike_jet(double x, double y, double R, double k, double Rn, P
 template <int P>
 ORT_INLINE void jet_normal(const SurfJet& J, Dual<P>& nx, Dual<P>& ny, Dual<P>& nz) {
   const double g = sqrt(J.sx * J.sx + J.sy * J.sy + 1.0);
-  const double ig = 1.0 / g;
+  const double ig = rrcp(g);
   nx = Dual<P>(J.sx * ig);
   ny = Dual<P>(J.sy * ig);
   nz = Dual<P>(-ig);
-  const double ex = nx.v * J.sxx + ny.v * J.sxy, ey = nx.v * J.sxy + ny.v * J.syy;
+  const double ex = nx.v * J.sxx + ny.v * J.syx, ey = nx.v * J.sxy + ny.v * J.syy;
   nx.d[0] = (J.sxx - nx.v * ex) * ig;
-  ny.d[0] = (J.sxy - ny.v * ex) * ig;
+  ny.d[0] = (J.syx - ny.v * ex) * ig;
   nz.d[0] = -nz.v * ex * ig;
   nx.d[1] = (J.sxy - nx.v * ey) * ig;
   ny.d[1] = (J.syy - ny.v * ey) * ig;

@@ -236,7 +236,7 @@ void trace_group(const KArgs& a, int64_t r0, int64_t r1, int32_t* updates, int& 
 }
 
 // adj_ray's lane policy on the host (ort_sweep.h): one ray at a time, its tape in a
-// ray-local array [S][kTapeRows] (stride 1), slot contributions added to the chunk's
+// ray-local array of at most S kTapeRows rows (stride 1), slot contributions added to the chunk's
 // accumulator acc[slot] in the ray's order
 struct HostLane {
   const AArgs& j;
@@ -245,7 +245,7 @@ struct HostLane {
   void emit(int slot, double v, bool) {
     if (j.need[slot]) acc[slot] += v;
   }
-  double* tape(int si) const { return tp + (int64_t)si * kTapeRows; }
+  double* tape_at(int64_t row) const { return tp + row; }
   int64_t tape_stride() const { return 1; }
   int uniform_max(int v) const { return v; }
   void zemit(int slot, int, double v, bool first) { emit(slot, v, first); }

@@ -335,8 +335,8 @@ extern "C" int ort_patch_zernike_ptrs(const ort_lens* lens, const double* const*
 // denom = sqrt(exp_avg_sq) / sqrt(1 - beta2^t) + eps, param -= step_size exp_avg / denom;
 // compiled with the same contraction as that kernel's build, hipcc's default), the new
 // value into the term table and LDS, then the surface's Cartesian blocks re-formed in term
-// order (patch_zernike_kernel's loop). Each parameter element belongs to one surface, so one
-// workgroup updates it; the step count is kept per surface (no cross-workgroup race).
+// order (patch_zernike_kernel's loop). Each parameter tensor's rows lie within one surface,
+// so one workgroup updates it and its step count (no cross-workgroup race).
 namespace ortk {
 __device__ inline void adam_update(const ort_adam_params& p, double t, double& param, double g,
                                    double& m, double& v) {
@@ -357,18 +357,19 @@ __global__ __launch_bounds__(kBlock) void adam_patch_zernike_kernel(const ort_su
                                                                     double* coef,
                                                                     const ort_adam_params p) {
   __shared__ double cs[kPatchTerms];
-  __shared__ int touched;
   const ort_surface s = surf[blockIdx.x];
   if (s.geometry != ORT_GEOM_ZERNIKE) return;
   const int t0 = s.coef_off, nt = s.n_coef;
-  if (threadIdx.x == 0) touched = 0;
   for (int jt = threadIdx.x; jt < nt && jt < kPatchTerms; jt += kBlock) cs[jt] = zern[t0 + jt].c;
   __syncthreads();
-  // this surface's step count, incremented before the update (torch: step += 1 first)
-  const double t = p.step[blockIdx.x] + 1.0;
+  uint32_t mine = 0;  // the tensors with rows on this surface (uniform)
   for (int k = 0; k < p.n_tensors; ++k) {
     const int64_t lo = p.row0[k] > t0 ? p.row0[k] : t0;
     const int64_t hi = (p.row0[k] + p.count[k] < t0 + nt) ? p.row0[k] + p.count[k] : t0 + nt;
+    if (lo >= hi) continue;
+    mine |= 1u << k;
+    // the tensor's step count, incremented before the update (torch: step += 1 first)
+    const double t = *p.step[k] + 1.0;
     for (int64_t r = lo + threadIdx.x; r < hi; r += kBlock) {
       const int64_t e = r - p.row0[k];
       double param = p.param[k][e], m = p.exp_avg[k][e], v = p.exp_avg_sq[k][e];
@@ -378,12 +379,13 @@ __global__ __launch_bounds__(kBlock) void adam_patch_zernike_kernel(const ort_su
       p.exp_avg_sq[k][e] = v;
       zern[r].c = param;
       if (r - t0 < kPatchTerms) cs[r - t0] = param;
-      touched = 1;  // (a benign race: every writer stores 1)
     }
   }
-  __syncthreads();
-  if (!touched) return;
-  if (threadIdx.x == 0) p.step[blockIdx.x] = t;
+  __syncthreads();  // (every thread has read the step counts)
+  if (!mine) return;
+  if (threadIdx.x == 0)
+    for (int k = 0; k < p.n_tensors; ++k)
+      if (mine & (1u << k)) *p.step[k] = *p.step[k] + 1.0;
   if (s.zm_deg < 0 || nt > kPatchTerms) return;
   const int K = (s.zm_deg + 1) * (s.zm_deg + 2) / 2;
   const double* Ms = coef + s.zm_off + 2 * K;
@@ -401,14 +403,13 @@ __global__ __launch_bounds__(kBlock) void adam_patch_zernike_kernel(const ort_su
 extern "C" int ort_adam_patch_zernike(const ort_lens* lens, const ort_adam_params* p,
                                       void* stream) {
   using namespace ortk;
-  if (!lens || !p || p->n_tensors < 0 || p->n_tensors > ORT_ADAM_MAX_TENSORS || !p->step)
-    return ORT_ERR_ARG;
+  if (!lens || !p || p->n_tensors < 0 || p->n_tensors > ORT_ADAM_MAX_TENSORS) return ORT_ERR_ARG;
   if (lens->n_surfaces < 1 || lens->n_surfaces > ORT_MAX_SURFACES || !lens->surfaces ||
       !lens->zern || !lens->coef)
     return ORT_ERR_ARG;
   for (int k = 0; k < p->n_tensors; ++k)
-    if (!p->param[k] || !p->grad[k] || !p->exp_avg[k] || !p->exp_avg_sq[k] || p->row0[k] < 0 ||
-        p->count[k] < 0)
+    if (!p->param[k] || !p->grad[k] || !p->exp_avg[k] || !p->exp_avg_sq[k] || !p->step[k] ||
+        p->row0[k] < 0 || p->count[k] < 0)
       return ORT_ERR_ARG;
   hipLaunchKernelGGL(adam_patch_zernike_kernel, dim3((unsigned)lens->n_surfaces), dim3(kBlock), 0,
                      (hipStream_t)stream, lens->surfaces,

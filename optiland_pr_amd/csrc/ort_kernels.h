@@ -394,6 +394,15 @@ __device__ inline __attribute__((always_inline)) double newton_distance(const KA
     }
   }
   report_newton(a, si, active && !(FAST && bad), group, group_uniform, mask, last_bad);
+  if constexpr ((FEAT & F_TAPE) != 0) {
+    // the iterate rows no update fills (m >= U) get the root: every tape row is written
+    // (the tape is the trace op's output; the adjoint reads only m < min(U, kHist))
+    if (tape) {
+#pragma unroll
+      for (int m = 0; m < kHist; ++m)
+        if (m >= U) ORT_ST(tape[(int64_t)(7 + m) * a.n_rays], t);
+    }
+  }
   hn = true;  // every active lane evaluated j == U (inactive lanes store nothing)
   return t;
 }
@@ -617,7 +626,7 @@ __device__ inline __attribute__((always_inline)) ort::Ray trace_ray(const KArgs&
     const ort_surface_optics o = surface_optics<FEAT>(a, s, lam, si, wl);
     double* tp = nullptr;  // F_TAPE: this surface's tape rows of this ray
     if constexpr ((FEAT & F_TAPE) != 0) {
-      tp = a.tape + (int64_t)si * kTapeRows * a.n_rays + rid;
+      tp = a.tape + tape_row0(a.surf, si) * a.n_rays + rid;
       if (active) {
         ORT_ST(tp[0], r.x);
         ORT_ST(tp[a.n_rays], r.y);
@@ -841,7 +850,7 @@ __device__ __forceinline__ void trace_block(const KArgs& a, const int32_t* sched
     const ort_surface_optics o = surface_optics<FEAT>(a, s, lam, si, wl);
     double* tp = nullptr;  // F_TAPE: this surface's tape rows of this ray
     if constexpr ((FEAT & F_TAPE) != 0) {
-      tp = a.tape + (int64_t)si * kTapeRows * a.n_rays + rid;
+      tp = a.tape + tape_row0(a.surf, si) * a.n_rays + rid;
       if (active) {
         ORT_ST(tp[0], r.x);
         ORT_ST(tp[a.n_rays], r.y);

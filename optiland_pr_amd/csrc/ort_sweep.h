@@ -63,10 +63,23 @@ enum : uint32_t {
                         // kVerifyGrid workgroups strides over the blocks of rays
 };
 
-// Adjoint tape (adj_ray): per traced surface, rows of n_rays doubles -- the incoming
-// global x y z L M N, the distance t, the Newton iterates before the last kHist updates
-constexpr int kTapeRows = 11;
+// Adjoint tape (adj_ray): per surface, rows of n_rays doubles -- the incoming global
+// x y z L M N, the distance t (7 rows), and for a Newton surface kHist more: the iterates
+// before the last kHist updates, row 7 + m = t_{U-1-m} for m < min(U, kHist), the initial
+// guess t_0 in the rows m >= U (ABI v19: closed-form surfaces take no iterate rows, and
+// every row of the tape is written -- it is the trace op's output, ops.py)
+constexpr int kTapeRows = 11;  // the most rows of one surface
 constexpr int kHist = 4;
+
+// tape rows of surface s, and the first row of surface si (the surfaces before it)
+ORT_INLINE int tape_rows(const ort_surface& s) {
+  return (s.geometry == ORT_GEOM_PLANE || s.geometry == ORT_GEOM_STANDARD) ? 7 : kTapeRows;
+}
+ORT_INLINE int64_t tape_row0(const ort_surface* surf, int si) {
+  int64_t r = 0;
+  for (int k = 0; k < si; ++k) r += tape_rows(cst(surf)[k]);
+  return r;
+}
 
 struct KArgs {
   // lens
@@ -122,7 +135,7 @@ struct KArgs {
   const int32_t* vprev;
   int32_t* vflag;
   int32_t* sched_out;
-  double* tape;     // F_TAPE: [n_surf][kTapeRows][n_rays] (ort_options.tape)
+  double* tape;     // F_TAPE: [sum of tape_rows][n_rays] (ort_options.tape)
   // F_SPOT (ort_trace_spot): block b traces chunk b % spot_chunks of pair b / spot_chunks
   // (kClosedBlock rays of seg_len, the tail lanes idle) and writes the chunk's count, sum x,
   // sum y of its i > 0 image points, in the image frame, to spot_part1[b][3] -- the rows
@@ -301,7 +314,9 @@ ORT_INLINE void globalize(const KArgs& a, const ort_surface& s, ort::RayT<T>& r)
 // conic initial guess; with more updates the earliest are dropped (their share is
 // scaled by products of converged residuals). The standard / noll Zernike normal omits
 // the normalisation constant, so its Newton slope is not the sag's derivative and the
-// iteration converges linearly: the host keeps the forward-mode VJP for those lenses.
+// iteration converges linearly: on those surfaces (ORT_SURF_SLOPE_INEXACT) the sweep is
+// exact while U <= kHist (every iterate taped), and the host takes the forward-mode VJP
+// for a longer schedule (autodiff.vjp_mode).
 //
 // Local derivatives of the surface at the hit point (normal and sag w.r.t. x, y and,
 // with P = 4, the radius and conic) come from one forward-mode evaluation with dual
@@ -335,7 +350,7 @@ struct AArgs {
   const double* rec_cot;
   const double* rec;
   ort_rays gin;             // RES: d / d rays_in (NULL field: not wanted)
-  double* tape;             // [n_surf][kTapeRows][n_rays]
+  double* tape;             // [sum of tape_rows][n_rays]
   double* partial;          // [n_slot][n_wave]
   double* slot_sum;         // [n_slot]
   const int32_t* need;      // [n_slot]: some parameter depends on this slot
@@ -363,9 +378,16 @@ struct AArgs {
 
 // monomials of a Cartesian block of degree N
 ORT_INLINE int mono_count(int N) { return (N + 1) * (N + 2) / 2; }
+// the highest Cartesian-block degree with a specialised monomial adjoint (zmono_adjoint_deg;
+// the host lowers blocks up to geometries.ZM_MAX_DEG = 6). A block of a higher degree --
+// only through a hand-made ort_lens: the forward kernels evaluate any degree -- takes the
+// per-term slots, so its coefficient adjoint stays exact.
+constexpr int kMonoMaxDeg = 6;
 // slots of a surface in the monomial basis (0: none)
 ORT_INLINE int mono_slots(const ort_surface& s) {
-  return (s.geometry == ORT_GEOM_ZERNIKE && s.zm_deg >= 0) ? 2 * mono_count(s.zm_deg) : 0;
+  return (s.geometry == ORT_GEOM_ZERNIKE && s.zm_deg >= 0 && s.zm_deg <= kMonoMaxDeg)
+             ? 2 * mono_count(s.zm_deg)
+             : 0;
 }
 // the lens's monomial slot count (every surface, in order)
 ORT_INLINE int mono_total(const ort_surface* surf, int n_surf) {
@@ -525,7 +547,12 @@ ORT_INLINE void zmono_adjoint_deg(Lane& ln, int deg, int slot0, double xn, doubl
     case 3: zmono_adjoint<3, SAG>(ln, slot0, xn, yn, ws, ax, ay); break;
     case 4: zmono_adjoint<4, SAG>(ln, slot0, xn, yn, ws, ax, ay); break;
     case 5: zmono_adjoint<5, SAG>(ln, slot0, xn, yn, ws, ax, ay); break;
-    default: zmono_adjoint<6, SAG>(ln, slot0, xn, yn, ws, ax, ay); break;
+    case 6: zmono_adjoint<6, SAG>(ln, slot0, xn, yn, ws, ax, ay); break;
+    default:  // unreachable (mono_slots gives such a surface no monomial slots): never
+              // another degree's layout -- a NaN in the surface's first slot instead
+      ln.mono_put(slot0, 0, __builtin_nan(""));
+      ln.mono_flush(slot0, 1);
+      break;
   }
 }
 
@@ -533,7 +560,7 @@ ORT_INLINE void zmono_adjoint_deg(Lane& ln, int deg, int slot0, double xn, doubl
 //   void   emit(int slot, double v, bool first)  add the ray's v to parameter slot `slot`
 //                                                 (first: the slot's first contribution
 //                                                 from this ray / wave)
-//   double* tape(int si)                          this ray's tape rows of surface si
+//   double* tape_at(int64_t row)                  this ray's entry of tape row `row`
 //   int64_t tape_stride()                         distance between two tape rows
 //   int    uniform_max(int v)                     max over the rays sharing control flow
 //   void   zemit(int slot, int j, double v, bool first), zflush(int slot0, int nt)
@@ -666,16 +693,15 @@ ORT_INLINE void adj_ray(const KArgs& a, const AArgs& j, Lane& ln, int64_t rid, b
         const double bdy = -nzv * (bny - nyv * bn);
         if (mono_base >= 0) {
           // the Cartesian normal's slopes (sagnorm_zernike): their adjoints (bdx, bdy)
-          // pulled back to the block gradient (Gx, Gy)
-          double xn, yn;
-          ort::div2(x, y, s.norm_radius, xn, yn);
+          // pulled back to the block gradient (Gx, Gy) (derivative-only quotients: rdiv)
+          const double inv_rn = ort::rrcp(s.norm_radius);
+          const double xn = x * inv_rn, yn = y * inv_rn;
           // sagnorm_zernike's slopes: Gx / Rn, Gy / Rn off the disc rho^2 < kZernChainRho2
           // (their adjoint: (bdx, bdy) / Rn), the reference's chain on it
           const double rho2n = xn * xn + yn * yn;
           double ax, ay;
 #ifndef ORT_ZERN_POLAR_CHAIN
           if (rho2n >= ort::kZernChainRho2) {
-            const double inv_rn = 1.0 / s.norm_radius;
             ax = bdx * inv_rn;
             ay = bdy * inv_rn;
           } else
@@ -683,14 +709,15 @@ ORT_INLINE void adj_ray(const KArgs& a, const AArgs& j, Lane& ln, int64_t rid, b
           {
             const double eps = 1e-14;
             const double rho = sqrt(rho2n);
-            const double Rn = s.norm_radius;
-            double xr, yr, drx, dry, qy, qx;
-            ort::div2(x, y, Rn * Rn, xr, yr);
-            ort::div2(xr, yr, rho + eps, drx, dry);
-            ort::div2(-(yn), xn, rho * rho + eps, qy, qx);
-            const double inv_rn = 1.0 / Rn;
+            const double ire = ort::rrcp(rho + eps), iq = ort::rrcp(rho * rho + eps);
+            const double drx = xn * inv_rn * ire, dry = yn * inv_rn * ire;
+            const double qy = -(yn)*iq, qx = xn * iq;
             double cx = 0.0, cy = 0.0;  // xn / rho, yn / rho (Fr's factors)
-            if (rho > 0.0) ort::div2(xn, yn, rho, cx, cy);
+            if (rho > 0.0) {
+              const double ir = ort::rrcp(rho);
+              cx = xn * ir;
+              cy = yn * ir;
+            }
             const double fr = bdx * drx + bdy * dry;        // adjoint of Fr
             const double g2 = (bdx * qy + bdy * qx) * inv_rn;  // adjoint of G2
             ax = fr * cx - g2 * yn;
@@ -728,7 +755,7 @@ ORT_INLINE void adj_ray(const KArgs& a, const AArgs& j, Lane& ln, int64_t rid, b
       GR = -2.0 * z;
       Gk = z * z;
     }
-    const double lm = -tb / (Gx * q.L + Gy * q.M + Gz * q.N);
+    const double lm = ort::rdiv(-tb, Gx * q.L + Gy * q.M + Gz * q.N);
     b.x += lm * Gx;
     b.y += lm * Gy;
     b.z += lm * Gz;
@@ -746,10 +773,12 @@ ORT_INLINE void adj_ray(const KArgs& a, const AArgs& j, Lane& ln, int64_t rid, b
   bool replay = true;
   if constexpr (!RES) replay = !j.tape_ready;
   if (replay) {
+    int64_t trow = tape_row0(a.surf, a.start_surface);
     for (int si = a.start_surface; si < a.n_surf; ++si) {
       const ort_surface s = cst(a.surf)[si];
       const ort_surface_optics o = optics_of(s, si);
-      double* tp = ln.tape(si);
+      double* tp = ln.tape_at(trow);
+      trow += tape_rows(s);
       if (active) {
         tp[0] = r.x;
         tp[TS] = r.y;
@@ -830,9 +859,12 @@ ORT_INLINE void adj_ray(const KArgs& a, const AArgs& j, Lane& ln, int64_t rid, b
   }
 
   // ---- reverse over the surfaces
+  int64_t trow_end = tape_row0(a.surf, a.n_surf);  // (this surface's rows end here)
   for (int si = a.n_surf - 1; si >= a.start_surface; --si) {
     const ort_surface s = cst(a.surf)[si];
     const ort_surface_optics o = optics_of(s, si);
+    trow_end -= tape_rows(s);
+    const int64_t trow = trow_end;
     if constexpr ((KM & ort::KM_ZERN) != 0) {
       mono_base = -1;  // this surface's monomial slots (uniform), walking back from the end
       if (j.mono_on) {
@@ -858,7 +890,7 @@ ORT_INLINE void adj_ray(const KArgs& a, const AArgs& j, Lane& ln, int64_t rid, b
       const double ci = rc[6 * NR];
       if (ci != 0.0) batt += ci * j.rec[((int64_t)s.rec_slot * 8 + 6) * NR + rid];
     }
-    const double* tp = ln.tape(si);
+    const double* tp = ln.tape_at(trow);
     ort::Ray q;
     q.x = ORT_TAPE_LD(tp[0]);
     q.y = ORT_TAPE_LD(tp[TS]);
@@ -907,7 +939,7 @@ ORT_INLINE void adj_ray(const KArgs& a, const AArgs& j, Lane& ln, int64_t rid, b
       bmx = b.L * fac;
       bmy = b.M * fac;
       bmz = b.N * fac;
-      bdot = bs * (u * u * dot / root - u);
+      bdot = bs * (ort::rdiv(u * u * dot, root) - u);
       b.L *= u;
       b.M *= u;
       b.N *= u;
@@ -952,7 +984,8 @@ ORT_INLINE void adj_ray(const KArgs& a, const AArgs& j, Lane& ln, int64_t rid, b
       const int U = a.sched ? a.sched[group * a.n_surf + si] : s.max_iter;
       const int Uk = U < kHist ? U : kHist;
       const int m_end = ln.uniform_max(active ? Uk : 0);
-      double tb = bt;
+      // (a linearly converging surface past the tape: NaN, see the initial guess below)
+      double tb = U > kHist && (s.flags & ORT_SURF_SLOPE_INEXACT) ? __builtin_nan("") : bt;
       for (int m = 0; m < m_end; ++m) {
         const bool on = m < Uk;
         // (loaded here, a second round trip per surface; loading the newest iterate with
@@ -965,16 +998,18 @@ ORT_INLINE void adj_ray(const KArgs& a, const AArgs& j, Lane& ln, int64_t rid, b
         const double f = sk.v - zk;
         const bool zg = fabs(kz.v) > 1e-14;
         const double nzs = zg ? kz.v : 1e-14;
-        const double fx = -kx.v / nzs, fy = -ky.v / nzs;
+        const double inzs = ort::rrcp(nzs);  // (derivative-only quotients: rdiv)
+        const double fx = -kx.v * inzs, fy = -ky.v * inzs;
         const double df = fx * q.L + fy * q.M - q.N;
         const bool dg = fabs(df) > 1e-14;
         const double dfs = dg ? df : 1e-14;
         const double tbo = on ? tb : 0.0;
-        const double bf = -tbo / dfs;
-        const double bdfs = dg ? tbo * f / (dfs * dfs) : 0.0;
+        const double idfs = ort::rrcp(dfs);
+        const double bf = -tbo * idfs;
+        const double bdfs = dg ? tbo * f * (idfs * idfs) : 0.0;
         const double bfx = bdfs * q.L, bfy = bdfs * q.M;
-        const double knx = -bfx / nzs, kny = -bfy / nzs;
-        const double knz = zg ? (bfx * kx.v + bfy * ky.v) / (nzs * nzs) : 0.0;
+        const double knx = -bfx * inzs, kny = -bfy * inzs;
+        const double knz = zg ? (bfx * kx.v + bfy * ky.v) * (inzs * inzs) : 0.0;
         if (on) {
           b.L += bdfs * fx;
           b.M += bdfs * fy;
@@ -998,9 +1033,15 @@ ORT_INLINE void adj_ray(const KArgs& a, const AArgs& j, Lane& ln, int64_t rid, b
       }
       // initial guess: the base conic's closed form (newton_raphson.py:131-135). More than
       // kHist updates: the earlier ones are dropped -- their share is scaled by the
-      // products of f f'' / f'^2 over the kept updates, i.e. by converged residuals
+      // products of f f'' / f'^2 over the kept updates, i.e. by converged residuals. Not so
+      // where the Newton slope is not the sag's derivative (ORT_SURF_SLOPE_INEXACT: standard
+      // / noll Zernike, linear convergence): the host takes the forward-mode VJP when it
+      // knows of such a schedule (autodiff.vjp_mode), and a schedule only the device saw
+      // (a device-verified round raised it) poisons the gradient with NaN instead of
+      // truncating it silently
       const double t0 = U == 0 ? t : ORT_TAPE_LD(tp[(int64_t)(7 + (U <= kHist ? U - 1 : 0)) * TS]);
-      closed_adj(s, q, t0, U <= kHist ? tb : 0.0, b, bR, bk);
+      closed_adj(s, q, t0, U <= kHist || (s.flags & ORT_SURF_SLOPE_INEXACT) ? tb : 0.0, b, bR,
+                 bk);
     }
 
     if constexpr ((KM & ort::KM_ZERN) != 0) {

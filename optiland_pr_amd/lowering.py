@@ -263,6 +263,10 @@ def lower_surface_group(surface_group, wavelengths, record=False, skip_object=Tr
                 zern.append((c, norm, n, m, len(coef), len(a)))
                 coef.extend(a)
                 coef.extend(d)
+            if any(t[1] != 1.0 for t in terms):
+                # the normal omits the normalisation (zernike.py:163-231): the Newton slope
+                # is not the sag's derivative, the adjoint replays every update
+                row["flags"] |= _abi.SURF_SLOPE_INEXACT
             blk = zernike_monomial_block(terms, on_device)
             if blk is not None:
                 row["zm_off"] = len(coef)

@@ -9,22 +9,28 @@ Here the whole trace is ONE dispatcher op whose CUDA (HIP) kernel is the fused t
 forward-mode) VJP of the trace core (ort_trace_sequential_vjp / ort_trace_pupil_vjp), so
 autograd sees one node per trace call:
 
-  ort::trace_sequential(lens, rays[8], w, params, spec, start_surface, per_ray_w)
+  ort::trace_sequential(lens, lens_meta, final_thickness, lens_key, rays[8], w, params,
+                        spec, start_surface, per_ray_w)
       -> (x, y, z, L, M, N, i, opd, rec, sched)
       resident rays in (SurfaceGroup.trace, the drop-in seam); rec = every traced
       surface's record [S][8][n] (standard_surface.py:266-286); differentiable w.r.t. the
       input rays, the record buffer's cotangents included, and the lens parameters in
       `params`.
-  ort::trace_pupil(plan, px, py, params, spec) -> (x, y, z, L, M, N, i, opd, sched)
+  ort::trace_pupil(lens, lens_meta, final_thickness, lens_key, seg, apod, px, py, params,
+                   spec, plan_meta, plan_key)
+      -> (x, y, z, L, M, N, i, opd, sched, tape, rms, rms_stats)
       rays generated from pupil samples in the same launch (Optic.trace's fused path,
       raytrace/real_ray_tracer.py:37-97); differentiable w.r.t. the lens parameters.
 
-``lens`` / ``plan`` are integer handles of host objects (the uploaded lens tables, the
-pupil samples and segment descriptors): the dispatcher passes ints, and the tables they
-name are a few KB that the kernels read from HBM. ``params`` are the lens-parameter
-tensors that require grad and ``spec`` says which lens value each one is, as flattened
-(kind, traced-surface index) pairs with kind in SPEC_KINDS: the forward ignores their
-values (the lowered lens already holds them), the backward returns d loss / d each.
+The ops are self-describing: ``lens`` is the lowered lens as tensors (lens_args: the nine
+uploaded tables, a few KB the kernels read from HBM) with its scalars in ``lens_meta``;
+``seg`` / ``apod`` / ``plan_meta`` describe the pupil plan the same way. ``lens_key`` /
+``plan_key`` are integer cache keys only -- the handle of the live host object holding the
+Newton schedule caches; a key that names no live object of these tensors makes the op
+rebuild the lens from the tensors. ``params`` are the lens-parameter tensors that require
+grad and ``spec`` says which lens value each one is, as flattened (kind, traced-surface
+index) pairs with kind in SPEC_KINDS: the forward ignores their values (the lowered lens
+already holds them), the backward returns d loss / d each.
 
 ort::trace_sequential has two kernels, one per dispatch key (SURVEY.md 8b): CUDA (HIP) runs
 the fused GPU trace on a DeviceLens handle, CPU runs the host build of the same per-ray
@@ -156,7 +162,9 @@ def mono_slot_count(table, zp):
     if zp is None or not ADJ_MONO:
         return 0
     s = table.surfaces
-    d = s["zm_deg"][(s["geometry"] == _abi.GEOM_ZERNIKE) & (s["zm_deg"] >= 0)].astype(np.int64)
+    # (blocks above ort_sweep.h kMonoMaxDeg = 6 take the per-term slots)
+    d = s["zm_deg"][(s["geometry"] == _abi.GEOM_ZERNIKE) & (s["zm_deg"] >= 0)
+                    & (s["zm_deg"] <= 6)].astype(np.int64)
     return int(np.sum((d + 1) * (d + 2)))
 
 
@@ -190,13 +198,19 @@ def slot_need(table, zp, surf, final):
     return need
 
 
+def tape_rows(table):
+    """Rows of the adjoint tape per ray (ort_options.tape, ABI v19): 7 per plane / conic
+    surface, 11 per Newton surface -- every one written by the taped trace."""
+    g = table.surfaces["geometry"]
+    closed = (g == _abi.GEOM_PLANE) | (g == _abi.GEOM_STANDARD)
+    return int(7 * len(g) + 4 * np.count_nonzero(~closed))
+
+
 def tape_doubles(dl, n):
-    """Doubles of the adjoint tape of an n-ray trace of this lens (ort_vjp_tape_size)."""
-    lib = _native.load()
-    batch = _native.ort_batch(n, max(n, 1), max(n, 1), 0, 0, None)
-    size = int(lib.ort_vjp_tape_size(C.byref(dl.c), C.byref(batch)))
-    _native.check(size if size < 0 else 0, "ort_vjp_tape_size")
-    return size // 8
+    """Doubles of the adjoint tape of an n-ray trace of this lens: exactly the rows the
+    taped trace writes (ort_vjp_tape_size bytes bound it for any lens of this many
+    surfaces)."""
+    return tape_rows(dl.table) * int(n)
 
 
 def _check_differentiable(table):
@@ -229,7 +243,7 @@ def _ray_struct(ts):
 # --------------------------------------------------------------------------------------
 # lens_meta: the host-side scalars of the ort_lens struct, in this order
 LENS_META = ("n_surfaces", "n_lambda", "n_mat", "final_mat", "geometry_mask",
-             "interaction_mask", "frame_flags", "n_rec", "newton")
+             "interaction_mask", "frame_flags", "n_rec", "newton", "tape_rows")
 NEWTON_MODES = ("reference", "device", "wave")
 
 
@@ -242,7 +256,7 @@ def lens_args(dl):
     t = dl.table
     meta = [int(t.n_surfaces), len(t.wavelengths), int(t.n_tab.shape[1]), int(t.final_mat),
             int(dl.geometry_mask), int(t.interaction_mask), int(t.frame_flags), int(t.n_rec),
-            1 if dl.newton else 0]
+            1 if dl.newton else 0, tape_rows(t)]
     return dl.lens_tensors(), meta, float(t.final_thickness), handle(dl)
 
 
@@ -437,9 +451,9 @@ def _seq_backward(ctx, *grads):
     _check_differentiable(table)
     params_like = [torch.empty(s, dtype=d, device="meta") for s, d, _ in ctx.shapes]
     zp, st, ft, n_param = tangent_tables(table, ctx.pairs, params_like)
-    from .autodiff import vjp_mode
+    from .autodiff import schedule_for_mode, vjp_mode
 
-    mode = vjp_mode(table)
+    mode = vjp_mode(table, schedule_for_mode(table, sched))
     if not (want_params and n_param):
         zp = st = ft = None
         n_param = 0
@@ -627,8 +641,8 @@ def trace_pupil(lens: list[torch.Tensor], lens_meta: list[int], final_thickness:
         torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]:
     """Optic.trace's fused generation + trace (ort_trace_pupil): outputs the 8 ray columns,
     the verified Newton schedule, the adjoint tape (empty unless plan_meta asks for it:
-    the backward is then the reverse sweep only; rows the backward never reads are left
-    unwritten), and RayOperand.rms_spot_size of the final points with its stats[5] (empty
+    the backward is then the reverse sweep only; every row written, tape_rows per ray),
+    and RayOperand.rms_spot_size of the final points with its stats[5] (empty
     unless plan_meta's want_rms: the rows in the taped kernel's epilogue, ort_rms_finish;
     its gradient folds into the backward's x, y cotangents)."""
     from .raytrace import RealRays
@@ -691,7 +705,7 @@ def _(lens, lens_meta, final_thickness, lens_key, seg, apod, px, py, params, spe
     outs = [px.new_empty(n, dtype=torch.float64) for _ in range(8)]
     S = lens_meta[0]
     ns = S if lens_meta[8] else 0  # one Newton group per call (group_len = n)
-    nt = S * 11 * n if (want_tape and px.device.type != "cpu") else 0  # kTapeRows = 11
+    nt = lens_meta[9] * n if (want_tape and px.device.type != "cpu") else 0  # tape_rows
     return (*outs, px.new_empty(ns, dtype=torch.int32), px.new_empty(nt, dtype=torch.float64),
             px.new_empty(() if want_rms else 0, dtype=torch.float64),
             px.new_empty(5 if want_rms else 0, dtype=torch.float64))
@@ -730,9 +744,12 @@ def _pupil_backward(ctx, *grads):
     _check_differentiable(dl.table)
     params_like = [torch.empty(s, dtype=d, device="meta") for s, d, _ in ctx.shapes]
     zp, st, ft, n_param = tangent_tables(dl.table, ctx.pairs, params_like)
-    from .autodiff import vjp_mode
+    from .autodiff import schedule_for_mode, vjp_mode
 
-    mode = vjp_mode(dl.table)
+    hint = None
+    if hasattr(dl, "cached_schedule"):
+        hint = dl.cached_schedule(_plan_keys(ctx.plan_key))
+    mode = vjp_mode(dl.table, schedule_for_mode(dl.table, sched, hint))
     tabs = _tables_cpu(zp, st, ft, slot_need(dl.table, zp, st, ft))
     cot = [None if gr is None else gr.to(torch.float64).contiguous() for gr in grads[:8]]
     g_rms = grads[10] if _want_rms(ctx.plan_meta) else None  # (AOT: zeros of an empty output)

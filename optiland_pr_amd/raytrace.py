@@ -198,10 +198,17 @@ class DeviceLens:
 
     def coefficients_current(self):
         """The uploaded tables hold the present values of the device-resident coefficient
-        tensors (optim.ZernikeAdam patched them in its own launch): the next
-        patch_coefficients of the same, unchanged tensors is skipped. Any in-place edit of a
-        tensor through torch bumps its version and brings the patch back."""
+        tensors (optim.ZernikeAdam patched them in its own launch): the NEXT
+        patch_coefficients of the same, unchanged tensors is skipped (once: later ones patch
+        again). An in-place edit through torch bumps the tensor's version and brings the
+        patch back; an edit through `.data` does not, and is seen from the second trace after
+        a ZernikeAdam step on (the first one trusts the step)."""
         self._patched = self._coeff_stamp(self.table.device_coeffs)
+
+    def invalidate_patch(self):
+        """The device-resident coefficient tensors changed behind the tables' back (another
+        lowered lens's ZernikeAdam launch updated them): the next trace patches."""
+        self._patched = None
 
     def patch_coefficients(self, device_coeffs):
         """Write device-resident Zernike coefficients into the uploaded term table
@@ -211,6 +218,7 @@ class DeviceLens:
         Skipped when the tables already hold these tensors' values (coefficients_current)."""
         stamp = self._coeff_stamp(device_coeffs)
         if stamp == getattr(self, "_patched", None):
+            self._patched = None  # trusted once (coefficients_current)
             return
         self._patched = None
         vals = [t.detach().reshape(-1).to(device=self.device, dtype=torch.float64)
@@ -323,6 +331,13 @@ class DeviceLens:
             k = base + W
         return None, None
 
+    def cached_schedule(self, keys):
+        """The verified schedules cached for `keys` ([n_groups][S]), or None when any key
+        has none yet (a cold trace: its schedule is only known once verified)."""
+        if not keys or not all(k in self.sched_cache for k in keys):
+            return None
+        return np.stack([self.sched_cache[k] for k in keys])
+
     def remember(self, keys, sched):
         for g, k in enumerate(keys):
             self.sched_cache[k] = sched[g].copy()
@@ -362,7 +377,8 @@ def lens_for(optic_or_group, wavelengths, record=False, image_record=False):
             # an edited lens starts from the previous Newton schedules (verified anyway)
             hit.sched_cache = old.sched_cache
         cache[key] = hit
-    elif table.device_coeffs:  # the cached upload: this call's coefficient values
+    elif table.device_coeffs:  # the cached upload: this call's coefficient tensors + values
+        hit.table.device_coeffs = table.device_coeffs
         hit.patch_coefficients(table.device_coeffs)
     return hit
 

@@ -6,8 +6,12 @@ Test infrastructure only, run in the build container (never on the GPU box):
     PYTHONPATH=tests/golden/shims:/root/reference PYTHONDONTWRITEBYTECODE=1 \
         python tests/golden/gen_autograd_golden.py
 
-Writes tests/golden/autograd_tma.npz (and with --full, autograd_tma_1m.json: config 5's
-own 1M-ray loss and gradient, see full_size):
+Writes tests/golden/autograd_tma.npz (fringe) and autograd_tma_standard.npz /
+autograd_tma_noll.npz (the same loss and weights with the standard and noll schemes,
+whose Newton slope omits the normalisation constant, zernike.py:162-231; SURVEY 8d.5's
+"standard" variant), and with --full autograd_tma_1m.json (fringe; --full --scheme
+standard|noll: autograd_tma_{scheme}_1m.json), config 5's own 1M-ray loss and gradient,
+see full_size:
   rms_*      RayOperand.rms_spot_size(optic, -1, 0, 1, 32, 0.587, "uniform")
              (operand/ray.py:300-340) and d rms / d c for the coefficients of the three
              Zernike mirrors (surfaces 1-3, 10 fringe coefficients each)
@@ -57,19 +61,19 @@ def _leaf_coefficients(lens):
     return leaves
 
 
-def main():
+def main(scheme="fringe"):
     be.set_backend("torch")
     be.set_precision("float64")
     out = {}
 
-    lens = gen_golden.tma("fringe")
+    lens = gen_golden.tma(scheme)
     leaves = _leaf_coefficients(lens)
     rms = RayOperand.rms_spot_size(lens, -1, 0.0, 1.0, 32, 0.587, "uniform")
     rms.backward()
     out["rms_value"] = np.array(float(rms))
     out["rms_grad"] = np.stack([t.grad.numpy().copy() for t in leaves])
 
-    lens = gen_golden.tma("fringe")
+    lens = gen_golden.tma(scheme)
     leaves = _leaf_coefficients(lens)
     d = create_distribution("uniform")
     d.generate_points(32)
@@ -88,10 +92,12 @@ def main():
         out[f"wsum_w_{f}"] = w[f]
     out["Px"] = px
     out["Py"] = py
-    np.savez_compressed(os.path.join(HERE, "autograd_tma.npz"), **out)
-    print("rms", out["rms_value"], "wsum", out["wsum_value"])
+    name = "autograd_tma" if scheme == "fringe" else f"autograd_tma_{scheme}"
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+    print(scheme, "rms", out["rms_value"], "wsum", out["wsum_value"])
     print(out["rms_grad"])
-    shape_params()
+    if scheme == "fringe":
+        shape_params()
 
 
 def _cooke_leaves(thickness_surface):
@@ -135,7 +141,7 @@ def shape_params():
     np.savez_compressed(os.path.join(HERE, "autograd_cooke.npz"), **out)
 
 
-def full_size():
+def full_size(scheme="fringe"):
     """Config 5 at its own size (VERDICT r02 item 6 for config 5): the TMA loss
     rms_spot_size(optic, -1, 0, 1, 1M, 0.587, RandomDistribution(seed=0)) -- the bench's
     workload -- and d rms / d c for the 30 coefficients, from the reference's torch
@@ -153,7 +159,7 @@ def full_size():
     be.set_backend("torch")
     be.set_precision("float64")
     d.x, d.y = torch.as_tensor(px), torch.as_tensor(py)
-    lens = gen_golden.tma("fringe")
+    lens = gen_golden.tma(scheme)
     leaves = _leaf_coefficients(lens)
     t0 = time.perf_counter()
     rms = RayOperand.rms_spot_size(lens, -1, 0.0, 1.0, 1_000_000, 0.587, d)
@@ -161,13 +167,18 @@ def full_size():
     res = dict(rms=float(rms), grad=[[float(v) for v in t.grad.numpy()] for t in leaves],
                seconds=time.perf_counter() - t0, n=int(px.size),
                px_sum=float(np.sum(px)), py_sum=float(np.sum(py)))
-    with open(os.path.join(HERE, "autograd_tma_1m.json"), "w") as f:
+    name = "autograd_tma_1m" if scheme == "fringe" else f"autograd_tma_{scheme}_1m"
+    with open(os.path.join(HERE, name + ".json"), "w") as f:
         json.dump(res, f, indent=1)
     print(res["rms"], res["seconds"])
 
 
 if __name__ == "__main__":
-    if "--full" in sys.argv:
-        full_size()
-    else:
-        main()
+    schemes = ("fringe", "standard", "noll")
+    if "--scheme" in sys.argv:
+        schemes = (sys.argv[sys.argv.index("--scheme") + 1],)
+    for sc in schemes:
+        if "--full" in sys.argv:
+            full_size(sc)
+        else:
+            main(sc)

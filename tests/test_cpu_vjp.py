@@ -94,3 +94,64 @@ def test_host_vjp_independent_of_threads(torch, mode):
     b = _grad(torch, "tma_fringe", spec, mode, num_rays=40, threads=4)
     assert np.all(np.isfinite(a))
     assert np.array_equal(a, b)
+
+
+def test_inexact_slope_past_the_tape_takes_unrolled(torch, monkeypatch):
+    """standard-scheme TMA with every Newton surface forced to U = 6 > ADJ_HIST updates
+    (tol 0, max_iter 6): the standard normal's slope omits the normalisation constant, so
+    the older updates keep a share (linear convergence) and the adjoint tape (4 iterates)
+    cannot hold them. The default mode sees the schedule and takes the forward-mode VJP;
+    the adjoint forced on it writes NaN (ort_sweep.h) rather than a truncated gradient."""
+    import optiland_pr_amd.samples as samples
+
+    orig = samples.ThreeMirrorAnastigmat.__init__
+
+    def forced(self, *a, **k):
+        orig(self, *a, **k)
+        for s in self.surface_group.surfaces[1:4]:
+            s.geometry.tol = 0.0
+            s.geometry.max_iter = 6
+
+    monkeypatch.setattr(samples.ThreeMirrorAnastigmat, "__init__", forced)
+    spec = [("zernike", 1), ("zernike", 3), ("radius", 2)]
+    gu = _grad(torch, "tma_standard", spec, "unrolled")
+    gd = _grad(torch, "tma_standard", spec, "")  # vjp_mode's choice
+    assert np.all(np.isfinite(gu))
+    np.testing.assert_array_equal(gd, gu)
+    ga = _grad(torch, "tma_standard", spec, "adjoint")
+    assert np.all(np.isnan(ga))
+    # the same lens at the reference's own tolerance (U = 1): the adjoint is the default
+    # and the unrolled derivative
+    monkeypatch.setattr(samples.ThreeMirrorAnastigmat, "__init__", orig)
+    np.testing.assert_allclose(_grad(torch, "tma_standard", spec, ""),
+                               _grad(torch, "tma_standard", spec, "unrolled"), rtol=1e-10)
+
+
+def test_block_above_degree_six_takes_per_term_slots(torch, monkeypatch):
+    """A Cartesian block of degree > 6 (only the host's ZM_MAX_DEG = 6 keeps them out: the
+    C ABI takes any ort_surface.zm_deg, and the forward kernels evaluate any degree) gets
+    no monomial-basis slots (ort_sweep.h kMonoMaxDeg, ops.mono_slot_count): its
+    coefficient adjoint runs per term, so the adjoint still equals the unrolled VJP."""
+    import optiland_pr_amd.geometries as geometries
+    import optiland_pr_amd.samples as samples
+    from optiland_pr_amd import _abi, ops
+    from optiland_pr_amd.lowering import lower_surface_group
+
+    monkeypatch.setattr(geometries, "ZM_MAX_DEG", 10)
+    coeffs = tuple(1e-5 * ((-1) ** k) / (1 + k) for k in range(25))
+    orig = samples.ThreeMirrorAnastigmat.__init__
+
+    def high(self, zernike_type="fringe", coefficients=None):
+        orig(self, zernike_type, coeffs)
+
+    monkeypatch.setattr(samples.ThreeMirrorAnastigmat, "__init__", high)
+    lens = samples.ThreeMirrorAnastigmat()
+    table = lower_surface_group(lens.surface_group, [lens.primary_wavelength])
+    deg = table.surfaces["zm_deg"][table.surfaces["geometry"] == _abi.GEOM_ZERNIKE]
+    assert np.all(deg > 6)
+    assert ops.mono_slot_count(table, np.zeros(1, np.int32)) == 0
+    spec = [("zernike", 1), ("zernike", 2), ("radius", 3)]
+    ga = _grad(torch, "tma_fringe", spec, "adjoint")
+    gu = _grad(torch, "tma_fringe", spec, "unrolled")
+    assert np.all(np.isfinite(ga))
+    np.testing.assert_allclose(ga, gu, rtol=1e-7, atol=1e-9 * np.max(np.abs(gu)))

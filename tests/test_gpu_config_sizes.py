@@ -133,27 +133,33 @@ def test_config3_pairs_at_4m_rays(torch, sizes, pair):
     np.testing.assert_allclose([x[-1], y[-1], opd[-1]], ref["last"], rtol=0, atol=1e-9)
 
 
-def test_config5_loss_and_gradient_at_1m_rays(torch):
+@pytest.mark.parametrize("scheme", ["fringe", "standard", "noll"])
+def test_config5_loss_and_gradient_at_1m_rays(torch, scheme):
     """Config 5 at its own size: the TMA loss rms_spot_size over 1M random pupil rays
-    (seed 0, Hy = 1, 0.587 um) and d rms / d c for the 30 fringe-Zernike coefficients, as
-    the reference's torch backend computes them (tests/golden/autograd_tma_1m.json,
-    gen_autograd_golden.py --full). The pupil sample is NumPy's stream (sums bit-exact);
-    the loss within rtol 1e-12 (reduction order), the gradient within rtol 1e-8 as the
-    smaller autograd goldens (adjoint vs torch's unrolled graph)."""
+    (seed 0, Hy = 1, 0.587 um) and d rms / d c for the 30 Zernike coefficients, as the
+    reference's torch backend computes them (tests/golden/autograd_tma_1m.json and
+    autograd_tma_{standard,noll}_1m.json, gen_autograd_golden.py --full): fringe, and
+    SURVEY 8d.5's "standard" variant (whose Newton slope omits the normalisation
+    constant; the adjoint serves it, every update taped). The pupil sample is NumPy's
+    stream (sums bit-exact); the loss within rtol 1e-12 (reduction order), the gradient
+    within rtol 1e-8 as the smaller autograd goldens (adjoint vs torch's unrolled
+    graph)."""
     import json
 
+    from optiland_pr_amd import autodiff
     from optiland_pr_amd.distribution import RandomDistribution
     from optiland_pr_amd.operands import RayOperand
     from optiland_pr_amd.samples import ThreeMirrorAnastigmat
 
-    path = os.path.join(HERE, "golden", "autograd_tma_1m.json")
+    name = "autograd_tma_1m" if scheme == "fringe" else f"autograd_tma_{scheme}_1m"
+    path = os.path.join(HERE, "golden", name + ".json")
     with open(path) as f:
         ref = json.load(f)
     d = RandomDistribution(seed=0)
     d.generate_points(1_000_000)
     assert float(np.sum(np.asarray(d.x))) == ref["px_sum"]
     assert float(np.sum(np.asarray(d.y))) == ref["py_sum"]
-    lens = ThreeMirrorAnastigmat()
+    lens = ThreeMirrorAnastigmat(scheme)
     leaves = []
     for si in (1, 2, 3):
         g = lens.surface_group.surfaces[si].geometry
@@ -161,8 +167,22 @@ def test_config5_loss_and_gradient_at_1m_rays(torch):
                          requires_grad=True)
         g.coefficients = t
         leaves.append(t)
-    rms = RayOperand.rms_spot_size(lens, -1, 0.0, 1.0, 1_000_000, 0.587, d)
-    rms.backward()
-    np.testing.assert_allclose(float(rms), ref["rms"], rtol=1e-12)
+    calls = []
+    real_vjp = autodiff.vjp
+
+    def spy(*a, **k):
+        calls.append(k.get("mode"))
+        return real_vjp(*a, **k)
+
+    autodiff.vjp = spy
+    try:
+        rms = RayOperand.rms_spot_size(lens, -1, 0.0, 1.0, 1_000_000, 0.587, d)
+        rms.backward()
+    finally:
+        autodiff.vjp = real_vjp
+    from optiland_pr_amd import _abi
+
+    assert calls == [_abi.VJP_ADJOINT]  # one reverse sweep, for every scheme
+    np.testing.assert_allclose(float(rms.detach()), ref["rms"], rtol=1e-12)
     got = np.stack([t.grad.cpu().numpy() for t in leaves])
     np.testing.assert_allclose(got, np.asarray(ref["grad"]), rtol=1e-8, atol=1e-12)

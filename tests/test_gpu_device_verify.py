@@ -114,7 +114,7 @@ def test_device_mode_gradients_equal_reference(torch):
             loss = RayOperand.rms_spot_size(lens, -1, 0.0, 1.0, 65536, 0.587, d)
             loss.backward()
         raytrace.check_all_pending()
-        res[mode] = (float(loss), np.concatenate([t.grad.cpu().numpy() for t in leaves]))
+        res[mode] = (float(loss.detach()), np.concatenate([t.grad.cpu().numpy() for t in leaves]))
     assert res["device"][0] == res["reference"][0]
     np.testing.assert_array_equal(res["device"][1], res["reference"][1])
 
@@ -256,6 +256,6 @@ def test_taped_rounds_stride_and_correct(torch, offset, path, monkeypatch):
             dl._dev_sched.clear()
         loss = step()
         raytrace.check_all_pending()
-        res[mode] = (float(loss), np.concatenate([t.grad.cpu().numpy() for t in leaves]))
+        res[mode] = (float(loss.detach()), np.concatenate([t.grad.cpu().numpy() for t in leaves]))
     assert res["device"][0] == res["reference"][0]
     np.testing.assert_array_equal(res["device"][1], res["reference"][1])

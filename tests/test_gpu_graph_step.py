@@ -75,7 +75,7 @@ def test_captured_step_equals_eager_steps(torch):
     for k in range(3 + steps):
         loss = step_e.eager()
         if k >= 3:
-            losses_e.append(float(loss))
+            losses_e.append(float(loss.detach()))
     raytrace.check_all_pending()
     torch.cuda.synchronize()
     np.testing.assert_array_equal(np.array(losses_g), np.array(losses_e))

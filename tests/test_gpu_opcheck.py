@@ -73,9 +73,17 @@ def test_opcheck_trace_sequential_cuda(torch, name, spec):
     _check(torch, torch.ops.ort.trace_sequential.default, args)
 
 
-@pytest.mark.parametrize("name,spec", [("cooke", ()),
-                                       ("tma_fringe", (("zernike", 1), ("zernike", 3)))])
-def test_opcheck_trace_pupil_cuda(torch, name, spec):
+@pytest.mark.parametrize("name,spec,want_tape", [
+    ("cooke", (), 0),
+    ("tma_fringe", (("zernike", 1), ("zernike", 3)), 0),
+    ("tma_fringe", (("zernike", 1), ("zernike", 3)), 1),
+    ("rt_asph", (("radius", 2), ("thickness", 4)), 1),
+])
+def test_opcheck_trace_pupil_cuda(torch, name, spec, want_tape):
+    """The default differentiable path writes the adjoint tape as an op output (want_tape):
+    every row is written (ABI v19: 7 rows per plane / conic surface, 11 per Newton surface,
+    the root in the iterate rows no update fills), so opcheck's
+    eager-vs-compiled comparisons cover it."""
     from optiland_pr_amd import _abi, ops
     from optiland_pr_amd.distribution import RandomDistribution
     from optiland_pr_amd.lowering import segment_params
@@ -93,11 +101,6 @@ def test_opcheck_trace_pupil_cuda(torch, name, spec):
     px = torch.as_tensor(np.asarray(d.x, dtype=np.float64), device="cuda")
     py = torch.as_tensor(np.asarray(d.y, dtype=np.float64), device="cuda")
     n = 64 * len(seg)
-    # without the adjoint tape: its rows the backward never reads (iterates past min(U, 4),
-    # rows 7-10 of closed-form surfaces) are left unwritten, so two runs differ there and
-    # opcheck's eager-vs-compiled output comparison would flag them; the taped path is what
-    # every other autograd test runs
-    want_tape = 0
     args = (L, meta, ft, key, seg_t, None, px, py, leaves, ops.encode_spec(_traced(spec)),
             [n, 64, 0, 0, want_tape], 0)
     _check(torch, torch.ops.ort.trace_pupil.default, args)

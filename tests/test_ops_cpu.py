@@ -33,7 +33,7 @@ def test_ops_registered():
     assert "Tensor seg" in s2 and "Tensor? apod" in s2
     for name in ("trace_sequential_vjp", "trace_pupil_vjp", "rms_spot", "rms_spot_vjp"):
         assert hasattr(torch.ops.ort, name)
-    assert len(ops.LENS_META) == 9
+    assert len(ops.LENS_META) == 10
 
 
 def test_rms_spot_refuses_mismatched_inputs():

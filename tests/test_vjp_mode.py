@@ -1,16 +1,33 @@
 """CPU: which VJP mode a lens gets (host logic; the kernels run in test_gpu_adjoint.py)."""
 
 
-def test_standard_zernike_keeps_unrolled_mode():
+def test_standard_zernike_takes_adjoint_within_the_tape():
+    """standard / noll Zernike surfaces carry SURF_SLOPE_INEXACT (their Newton slope omits
+    the normalisation constant, zernike.py:163-231); the adjoint is exact on them while
+    every surface's schedule fits the tape (U <= ADJ_HIST), the forward-mode VJP serves a
+    longer one. Surfaces with an exact slope keep the adjoint whatever U."""
+    import numpy as np
+
     from optiland_pr_amd import _abi, autodiff
     from tests._cases import build_lens
     from optiland_pr_amd.lowering import lower_surface_group
 
-    for name, want in (("tma_standard", _abi.VJP_UNROLLED), ("tma_noll", _abi.VJP_UNROLLED),
-                       ("tma_fringe", _abi.VJP_ADJOINT), ("cooke", _abi.VJP_ADJOINT)):
+    for name, inexact in (("tma_standard", True), ("tma_noll", True), ("tma_fringe", False),
+                          ("rt_asph", False), ("cooke", False)):
         lens = build_lens(name)
         table = lower_surface_group(lens.surface_group, [lens.primary_wavelength])
-        assert autodiff.vjp_mode(table) == want, name
+        flags = (table.surfaces["flags"] & _abi.SURF_SLOPE_INEXACT) != 0
+        geo = table.surfaces["geometry"]
+        assert np.array_equal(flags, inexact & (geo == _abi.GEOM_ZERNIKE)), name
+        assert autodiff.vjp_mode(table) == _abi.VJP_ADJOINT, name
+        S = table.n_surfaces
+        newton = geo >= _abi.GEOM_EVEN_ASPHERE
+        for U in (0, 1, _abi.ADJ_HIST, _abi.ADJ_HIST + 1, 100):
+            sched = np.where(newton, U, -1).astype(np.int32).reshape(1, S).repeat(3, 0)
+            want = (_abi.VJP_UNROLLED if inexact and U > _abi.ADJ_HIST
+                    else _abi.VJP_ADJOINT)
+            assert autodiff.vjp_mode(table, sched) == want, (name, U)
+        assert autodiff.inexact_updates(table, None) == 0
 
 
 def test_more_slots_than_the_adjoint_holds_take_unrolled_mode():
