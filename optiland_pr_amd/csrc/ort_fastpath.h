@@ -136,10 +136,17 @@ ORT_INLINE SharedDiv shared_div(double b, bool& bad) {
 }
 
 // the divisor is known to lie in [1, inf) unless NaN (a norm of (., ., 1))
+// (no test: the divisor is a norm sqrt(s), s = a^2 + b^2 + 1 >= 1, so it is at most
+// sqrt(DBL_MAX) < 2^512 -- its refined reciprocal >= 2^-512 is accurate and the quotients
+// of the checked numerators (|a| >= 2^-300 or +-0, and -1) stay normal -- or, with s
+// overflowed, +inf, whose zero reciprocal makes every quotient NaN for state_ok; NaN
+// likewise. Round 6: the b <= 2^300 test this had was one of those that cannot fail on a
+// finite result.)
 ORT_INLINE SharedDiv shared_div_ge1(double b, bool& bad) {
   SharedDiv d;
   d.b = b;
   d.ok = true;
+  (void)bad;
 #if defined(__HIP_DEVICE_COMPILE__)
   double y = __builtin_amdgcn_rcp(b);
   double e = fma(-b, y, 1.0);
@@ -147,7 +154,6 @@ ORT_INLINE SharedDiv shared_div_ge1(double b, bool& bad) {
   e = fma(-b, y, 1.0);
   y = fma(y, e, y);
   d.y = y;
-  ORT_CHK(bad, !(b <= 0x1p300));
 #else
   (void)bad;
   d.y = 0.0;
@@ -368,6 +374,21 @@ ORT_INLINE double quot_signed(double a, const SharedDiv& d) {
 // numerator in range or an exact zero of either sign (quot_signed / quot_pos keep its sign)
 ORT_INLINE bool num_ok0(double a) { return num_ok(a) || a == 0.0; }
 
+// The asphere formulas divide by R (1 + q) and R q with q = sqrt(...) >= 0: the sign of a
+// nonzero divisor is the radius's, a lens constant. With sR = +-1 that sign and the
+// divisor's magnitude |R| (1 + q), |R| q (the same products: IEEE multiplication is
+// sign-symmetric), a / b = (sR a) / |b| is quot_pos's form on a positive divisor -- the
+// same IEEE quotient, signed zeros included (sR a flips an exact zero's sign exactly when
+// b < 0) -- without quot_signed's two quotients and select. A zero divisor (q = 0)
+// gives an infinite reciprocal and non-finite quotients, as the signed form does.
+// |R| <= 2^149 (so |R| (1 + q) <= 2^150, R^2 <= 2^298: inside shared_div's range) is
+// tested once per evaluation (lens_range) instead of a test per divisor.
+ORT_INLINE SharedDiv shared_div_pos(double b) {
+  bool unused = false;
+  return shared_div_ge1(b, unused);  // (the same refinement, no test of its own)
+}
+ORT_INLINE bool lens_range(double R) { return ::fabs(R) <= 0x1p149; }
+
 // kSlope's direct slopes (ort_core.h): norm^2 < 1e28 checked (a steeper normal or NaN
 // takes the exact path, which forms the reference's expression from the unit normal)
 ORT_INLINE void slope_out(double dfdx, double dfdy, double& nx, double& ny, double& nz,
@@ -397,20 +418,22 @@ ORT_INLINE double sagnorm_even(double x, double y, const ort_surface& s, PD C,
                                int nc, int mode, double& nx, double& ny, double& nz,
                                bool& bad) {
   const double R = s.radius;
+  const double aR = ::fabs(R), sR = R > 0.0 ? 1.0 : -1.0;  // (lens constants)
+  ORT_CHK(bad, !lens_range(R));
   const double r2 = x * x + y * y;
   const double a = ORT_ONE_PLUS_K(s) * r2;  // (1 + k) r2: +-0 at the vertex
-  const SharedDiv rr = shared_div(ORT_R_SQ(s), bad);
+  const SharedDiv rr = shared_div_pos(ORT_R_SQ(s));
   ORT_CHK(bad, !num_ok0(a));
   const double q = sqrt(1.0 - quot_pos(a, rr), bad);
-  const SharedDiv dz = shared_div(R * (1.0 + q), bad);
+  const SharedDiv dz = shared_div_pos(aR * (1.0 + q));
   ORT_CHK(bad, !num_ok0(r2));
   double P, D;  // the term sums by Horner in r2 (ort_core.h even_horner)
   ort::even_horner(r2, C, nc, P, D);
-  const double z = quot_signed(r2, dz) + r2 * P;
-  const SharedDiv dd = shared_div(R * q, bad);
+  const double z = quot_pos(sR * r2, dz) + r2 * P;
+  const SharedDiv dd = shared_div_pos(aR * q);
   ORT_CHK(bad, !(num_ok0(x) && num_ok0(y)));
-  double dfdx = quot_signed(x, dd);
-  double dfdy = quot_signed(y, dd);
+  double dfdx = quot_pos(sR * x, dd);
+  double dfdy = quot_pos(sR * y, dd);
   dfdx = dfdx + x * D;
   dfdy = dfdy + y * D;
   if (mode == kSlope) {
@@ -432,24 +455,26 @@ ORT_INLINE double sagnorm_odd(double x, double y, const ort_surface& s, PD C,
                               int nc, int mode, double& nx, double& ny, double& nz,
                               bool& bad) {
   const double R = s.radius;
+  const double aR = ::fabs(R), sR = R > 0.0 ? 1.0 : -1.0;  // (lens constants)
+  ORT_CHK(bad, !lens_range(R));
   const double r2 = x * x + y * y;
   const double r = sqrt(r2, bad);  // the vertex itself (r2 = 0) takes the exact path
   const double a = ORT_ONE_PLUS_K(s) * r2;
-  const SharedDiv rr = shared_div(ORT_R_SQ(s), bad);
+  const SharedDiv rr = shared_div_pos(ORT_R_SQ(s));
   ORT_CHK(bad, !num_ok0(a));
   const double q = sqrt(1.0 - quot_pos(a, rr), bad);
-  const SharedDiv dz = shared_div(R * (1.0 + q), bad);
+  const SharedDiv dz = shared_div_pos(aR * (1.0 + q));
   ORT_CHK(bad, !num_ok0(r2));
-  double z = quot_signed(r2, dz);
+  double z = quot_pos(sR * r2, dz);
   double rp = r;
   for (int i = 0; i < nc; ++i) {
     z = z + C[i] * rp;
     rp = rp * r;
   }
-  const SharedDiv dd = shared_div(R * q, bad);
+  const SharedDiv dd = shared_div_pos(aR * q);
   ORT_CHK(bad, !(num_ok0(x) && num_ok0(y)));
-  double dfdx = quot_signed(x, dd);
-  double dfdy = quot_signed(y, dd);
+  double dfdx = quot_pos(sR * x, dd);
+  double dfdy = quot_pos(sR * y, dd);
   const SharedDiv dr = shared_div(r, bad);
   double rq = quot_pos(1.0, dr);  // 1 / r
   for (int i = 0; i < nc; ++i) {

@@ -180,10 +180,45 @@ struct ConvBits {
 };
 
 // Newton statistics of one (group, surface): AND of the per-update convergence bits and
-// the max non-converged index (see ort_newton_stat), read-before-atomic
+// the max non-converged index (see ort_newton_stat), read-before-atomic. The lane's
+// evaluated stop indices are j_lo .. U (its bits outside stay 0, last_bad is the largest
+// of them that did not converge). A group-uniform wave whose indices all fall in the
+// mask window (conv_base 0, U < 128) forms the wave's AND and max from one ballot per
+// index -- bit j of the AND is set iff no reporting lane missed j, and the max is the
+// last j some reporting lane missed: the same values as the shuffle reductions (six
+// dependent cross-lane steps each, three reductions per Newton surface) at a fraction of
+// the instructions and latency (#ifndef ORT_SHFL_REPORT, A/B builds)
 __device__ inline void report_newton(const KArgs& a, int si, bool active, int64_t group,
-                                     bool group_uniform, ConvBits m, int last_bad) {
+                                     bool group_uniform, ConvBits m, int last_bad, int U = -1,
+                                     int j_lo = 0) {
   if (!a.stats) return;
+#ifndef ORT_SHFL_REPORT
+  if (group_uniform && a.conv_base == 0) {
+    const int Uw = __builtin_amdgcn_readfirstlane(U);
+    if (Uw >= 0 && Uw < 128) {
+      if (__ballot(active) == 0) return;  // no reporting lane: nothing changes
+      uint64_t w0 = 0, w1 = 0;
+      int lb = -1;
+      for (int j = j_lo; j <= Uw; ++j) {
+        const bool bit = ((j < 64 ? m.w0 >> j : m.w1 >> (j - 64)) & 1) != 0;
+        if (__ballot(active && !bit) == 0) {
+          if (j < 64)
+            w0 |= 1ull << j;
+          else
+            w1 |= 1ull << (j - 64);
+        } else {
+          lb = j;
+        }
+      }
+      if ((threadIdx.x & 63) != 0) return;
+      ort_newton_stat* st = &a.stats[group * a.n_surf + si];
+      if (w0 != ~0ull) and_if_changes(&st->conv_mask[0], w0);
+      if (w1 != ~0ull) and_if_changes(&st->conv_mask[1], w1);
+      if (lb >= 0) max_if_changes(&st->last_bad, lb);
+      return;
+    }
+  }
+#endif
   if (!active) {
     m.w0 = m.w1 = ~0ull;
     last_bad = -1;
@@ -240,7 +275,7 @@ __device__ inline double grid_distance(const KArgs& a, const ort_surface& s, int
       if (!conv) last_bad = j + 1;
     }
   }
-  report_newton(a, si, active, group, group_uniform, mask, last_bad);
+  report_newton(a, si, active, group, group_uniform, mask, last_bad, U, 1);
   return ort::grid_final(g, r, t);
 }
 
@@ -393,7 +428,7 @@ __device__ inline __attribute__((always_inline)) double newton_distance(const KA
       }
     }
   }
-  report_newton(a, si, active && !(FAST && bad), group, group_uniform, mask, last_bad);
+  report_newton(a, si, active && !(FAST && bad), group, group_uniform, mask, last_bad, U);
   if constexpr ((FEAT & F_TAPE) != 0) {
     // the iterate rows no update fills (m >= U) get the root: every tape row is written
     // (the tape is the trace op's output; the adjoint reads only m < min(U, kHist))

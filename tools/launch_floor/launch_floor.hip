@@ -83,6 +83,25 @@ __global__ __launch_bounds__(256) void k_chain(const int* prev_flag, int* my_fla
   }
 }
 
+// the flag test in front of a LARGE body (~10K instructions, as the trace kernels'): does
+// the code size of a kernel cost its no-op launches anything (instruction fetch)?
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+void k_huge(const int* flag, const double* in, double* out) {
+  if (*flag != 1) return;
+  double acc[32];
+  const int t = blockIdx.x * 256 + threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < 32; ++k) acc[k] = in[t + k * 4096];
+#pragma unroll
+  for (int it = 0; it < 300; ++it)
+#pragma unroll
+    for (int k = 0; k < 32; ++k) acc[k] = acc[k] * acc[(k + it) % 32] + in[(it * 32 + k) & 4095];
+  double s = 0.0;
+#pragma unroll
+  for (int k = 0; k < 32; ++k) s += acc[k];
+  out[t] = s;
+}
+
 template <class F>
 static double per_launch_us(F launch, int N, int R, hipStream_t st) {
   hipGraph_t g;
@@ -132,12 +151,13 @@ int main() {
   bool first = true;
   for (unsigned G : grids) {
     struct V { const char* name; double us; };
-    V v[5];
+    V v[6];
     v[0] = {"empty", per_launch_us([&](hipStream_t s) { hipLaunchKernelGGL(k_empty, dim3(G), dim3(256), 0, s, flag); }, N, R, st)};
     v[1] = {"flag", per_launch_us([&](hipStream_t s) { hipLaunchKernelGGL(k_flag, dim3(G), dim3(256), 0, s, flag, out); }, N, R, st)};
     v[2] = {"big_args", per_launch_us([&](hipStream_t s) { hipLaunchKernelGGL(k_big, dim3(G), dim3(256), 0, s, big); }, N, R, st)};
     v[3] = {"lds_prefetch", per_launch_us([&](hipStream_t s) { hipLaunchKernelGGL(k_lds, dim3(G), dim3(256), 0, s, flag, sched, out); }, N, R, st)};
     v[4] = {"heavy_regs", per_launch_us([&](hipStream_t s) { hipLaunchKernelGGL(k_heavy, dim3(G), dim3(256), 0, s, flag, din, dout); }, N, R, st)};
+    v[5] = {"huge_code", per_launch_us([&](hipStream_t s) { hipLaunchKernelGGL(k_huge, dim3(G), dim3(256), 0, s, flag, din, dout); }, N, R, st)};
     for (auto& x : v) {
       std::printf("%s {\"grid\": %u, \"kernel\": \"%s\", \"us_per_launch\": %.3f}", first ? " " : ",\n ", G, x.name, x.us);
       first = false;
