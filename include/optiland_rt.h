@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define ORT_ABI_VERSION 19
+#define ORT_ABI_VERSION 20
 #define ORT_MAX_SURFACES 64
 
 /* ---- geometry kinds ----------------------------------- */
@@ -44,7 +44,8 @@ enum ort_geometry { /* see optiland/geometries */
   ORT_GEOM_TOROIDAL = 8,     /* toroidal.py:75-233                                 */
   ORT_GEOM_FORBES_QBFS = 9,  /* forbes/geometry.py:183-330 + forbes/qpoly.py       */
   ORT_GEOM_FORBES_Q2D = 10,  /* forbes/geometry.py:333-640 + forbes/qpoly.py       */
-  ORT_GEOM_GRID_SAG = 11     /* grid_sag.py:61-149: bilinear sag grid, own Newton   */
+  ORT_GEOM_GRID_SAG = 11,    /* grid_sag.py:61-149: bilinear sag grid, own Newton   */
+  ORT_GEOM_NURBS = 12        /* nurbs/nurbs_geometry.py:606-822 (v20): (u, v) solve */
 };
 /* Coefficient blocks in lens.coef at ort_surface.coef_off (n_coef doubles):
  *   GRID_SAG            nx, ny, x_0 .. x_(nx-1), y_0 .. y_(ny-1), sag[ny][nx] (row = y);
@@ -64,6 +65,12 @@ enum ort_geometry { /* see optiland/geometries */
  *                       (m = 0 part, as FORBES_QBFS), M, then for m = 1 .. M two
  *                       Clenshaw records (cosine, then sine): L, d_0 .. d_{L-1},
  *                       A_0 .. A_{L-1}, B_0 .. B_{L-1}, C_0 .. C_{L-1} (L = 0: no terms)
+ *   NURBS               p, q, nu, nv, U[nu + p + 1], V[nv + q + 1], Pw[4][nu][nv]
+ *                       (x w, y w, z w, w); clamped knots, degrees 1 .. 5. Not a Newton
+ *                       surface of the schedule: each ray solves its own (u, v) 2 x 2
+ *                       iteration (ort_nurbs.h) to its own |r| < tol (tol / max_iter from
+ *                       the surface record); no derivative kernels (the VJP entry points
+ *                       refuse it, as they refuse GRID_SAG)
  * ZERNIKE uses lens.zern[coef_off .. coef_off + n_coef) instead. */
 
 /* ---- surface flags ------------------------------------------------------------ */

@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import numpy as np
 
-ABI_VERSION = 19
+ABI_VERSION = 20
 VJP_UNROLLED = 0
 VJP_ADJOINT = 1
 AP_RADIAL = 1
@@ -41,6 +41,7 @@ GEOM_TOROIDAL = 8
 GEOM_FORBES_QBFS = 9
 GEOM_FORBES_Q2D = 10
 GEOM_GRID_SAG = 11
+GEOM_NURBS = 12  # ABI v20: own (u, v) solve per ray, not a Newton-in-t surface
 FREEFORM_GEOMETRIES = (GEOM_POLYNOMIAL, GEOM_CHEBYSHEV, GEOM_BICONIC, GEOM_TOROIDAL,
                        GEOM_FORBES_QBFS, GEOM_FORBES_Q2D, GEOM_GRID_SAG)
 NEWTON_GEOMETRIES = (GEOM_EVEN_ASPHERE, GEOM_ODD_ASPHERE, GEOM_ZERNIKE) + FREEFORM_GEOMETRIES

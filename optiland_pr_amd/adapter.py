@@ -47,6 +47,7 @@ from .geometries import (
     ForbesSurfaceConfig,
     OddAsphere,
     GridSagGeometry,
+    NurbsGeometry,
     Plane,
     PlaneGrating,
     PolynomialGeometry,
@@ -155,6 +156,15 @@ def _geometry(g):
     if name == "GridSagGeometry":
         return GridSagGeometry(cs, _np(g.x_grid), _np(g.y_grid), _np(g.sag_grid), g.tol,
                                g.max_iter)
+    if name == "NurbsGeometry":  # nurbs_geometry.py:86-269: the net as the reference holds it
+        if g.P is None:
+            raise ValueError("NURBS surface without a control net (call fit_surface())")
+        out = NurbsGeometry(cs, _f(g.radius), _f(g.k), g.nurbs_norm_x, g.nurbs_norm_y,
+                            _f(g.x_center), _f(g.y_center), _np(g.P), _np(g.W), int(g.p),
+                            int(g.q), _np(g.U), _np(g.V), tol=_f(g.tol),
+                            max_iter=int(g.max_iter))
+        out.is_fitted = bool(getattr(g, "is_fitted", False))
+        return out
     if name == "PlaneGrating":
         return PlaneGrating(cs, _f(g.grating_order), _f(g.grating_period),
                             _f(g.groove_orientation_angle))

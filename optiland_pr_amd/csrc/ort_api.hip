@@ -257,7 +257,8 @@ static int vjp_run(const ort_lens* lens, const double* px, const double* py,
   if (opt->newton_mode != ORT_NEWTON_SCHEDULE) return ORT_ERR_ARG;
   if (params->zern_param && (feat & ort::KM_ZERN) == 0) return ORT_ERR_ARG;
   if (feat & F_IA) return ORT_ERR_ARG;  // no derivative kernels for thin-lens / phase / grating
-  if (lens->geometry_mask & (1u << ORT_GEOM_GRID_SAG)) return ORT_ERR_ARG;  // nor grid sags
+  if (lens->geometry_mask & ((1u << ORT_GEOM_GRID_SAG) | (1u << ORT_GEOM_NURBS)))
+    return ORT_ERR_ARG;  // nor grid sags / NURBS (no derivative kernels)
   if (resident) {
     a.in = *rays_in;
   } else {

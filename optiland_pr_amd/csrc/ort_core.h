@@ -2034,13 +2034,18 @@ ORT_INLINE double grid_final(const GridView& g, const Ray& r, double t) {
   return off ? __builtin_nan("") : t;
 }
 
+// ---- NURBS: geometries/nurbs/nurbs_geometry.py (ort_nurbs.h) ----------------------------
+#include "ort_nurbs.h"
+
 // Sag and normal of a Newton-iterated geometry (EvenAsphere / OddAsphere / Zernike).
 // KM is a bitmask of the Newton kinds compiled in (KM_EVEN | KM_ODD | KM_ZERN): a lens
 // only pays registers for the kinds it contains.
 // KM_FREE covers the freeform kinds (XY polynomial, Chebyshev, biconic, toroidal, Forbes
-// Q-bfs / Q-2D) with a
-// runtime switch.
-enum : unsigned { KM_EVEN = 1u, KM_ODD = 2u, KM_ZERN = 4u, KM_FREE = 8u };
+// Q-bfs / Q-2D, grid sag) with a runtime switch; KM_NURBS the NURBS surfaces.
+// KM_NURBS (bit 16, clear of the kernels' other specialisation bits, ort_sweep.h): NURBS
+// surfaces, compiled only into the kernels of lenses that have one (ort_k_trace_ia.hip,
+// ort_k_geom.hip)
+enum : unsigned { KM_EVEN = 1u, KM_ODD = 2u, KM_ZERN = 4u, KM_FREE = 8u, KM_NURBS = 1u << 16 };
 
 // R, K: the surface's radius and conic (double, or seeded duals in the derivative kernels)
 template <unsigned KM, class T, class S, class PD, class PZ>
@@ -2060,6 +2065,19 @@ ORT_INLINE T newton_sagnorm(const ort_surface& s, const S& R, const S& K, PD coe
     if ((KM & ~KM_ZERN) == 0 || s.geometry == ORT_GEOM_ZERNIKE)
       return sagnorm_zernike(x, y, R, K, s.norm_radius, zern, s.coef_off, s.n_coef, coef, zs,
                              want_normal, range_error, nx, ny, nz, s.zm_off, s.zm_deg);
+  }
+  if constexpr ((KM & KM_NURBS) != 0) {  // primal kernels only (no derivative kernels)
+    if (s.geometry == ORT_GEOM_NURBS) {
+      if constexpr (std::is_same<T, double>::value) {
+        const T z = sagnorm_nurbs(nurbs_view(C), s.tol, s.max_iter, x, y,
+                                  want_normal != kNoNormal, nx, ny, nz);
+        if (want_normal == kSlope) slope_from_normal(nx, ny, nz);
+        return z;
+      } else {
+        nx = ny = nz = T(NAN);
+        return T(NAN);
+      }
+    }
   }
   if constexpr ((KM & KM_FREE) != 0) {
     // the freeform kinds form the unit normal; kSlope's (fx, fy, -1) from it

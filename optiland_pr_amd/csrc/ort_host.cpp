@@ -33,7 +33,8 @@ namespace {
 using namespace ortk;
 using ort::Ray;
 
-constexpr unsigned kAllKinds = ort::KM_EVEN | ort::KM_ODD | ort::KM_ZERN | ort::KM_FREE;
+constexpr unsigned kAllKinds =
+    ort::KM_EVEN | ort::KM_ODD | ort::KM_ZERN | ort::KM_FREE | ort::KM_NURBS;
 constexpr int64_t kChunk = 256;  // rays per reduction chunk (the GPU's block)
 constexpr int64_t kParMin = 2048;  // below this many rays a phase runs on one thread
 
@@ -44,7 +45,9 @@ int threads_for(int64_t n) {
   return g_threads > 0 ? g_threads : omp_get_max_threads();
 }
 
-bool is_newton(int g) { return g != ORT_GEOM_PLANE && g != ORT_GEOM_STANDARD; }
+bool is_newton(int g) {
+  return g != ORT_GEOM_PLANE && g != ORT_GEOM_STANDARD && g != ORT_GEOM_NURBS;
+}
 
 int range_bit(const ort_surface& s) {
   return s.geometry == ORT_GEOM_CHEBYSHEV ? (int)ORT_STATUS_CHEBYSHEV_RANGE
@@ -109,7 +112,7 @@ void trace_group(const KArgs& a, int64_t r0, int64_t r1, int32_t* updates, int& 
   for (int si = a.start_surface; si < a.n_surf; ++si) {
     const ort_surface s = a.surf[si];
     if (updates) updates[si] = 0;
-    const bool known = s.geometry >= ORT_GEOM_PLANE && s.geometry <= ORT_GEOM_GRID_SAG;
+    const bool known = s.geometry >= ORT_GEOM_PLANE && s.geometry <= ORT_GEOM_NURBS;
     if (!known) status |= ORT_STATUS_BAD_GEOMETRY;
     const bool grid = s.geometry == ORT_GEOM_GRID_SAG;
     // localize and the closed-form distance (the Newton kinds' initial guess)
@@ -122,6 +125,9 @@ void trace_group(const KArgs& a, int64_t r0, int64_t r1, int32_t* updates, int& 
         t[k] = ort::distance_plane(rays[k]);
       else if (grid)
         t[k] = 0.0;  // grid_sag.py:110
+      else if (s.geometry == ORT_GEOM_NURBS)  // per-ray (u, v) solve (ort_nurbs.h)
+        t[k] = ort::nurbs_distance(ort::nurbs_view(a.coef + s.coef_off), s.tol, s.max_iter,
+                                   rays[k]);
       else
         t[k] = ort::distance_conic(rays[k], s.radius, s.conic,
                                    (s.flags & ORT_SURF_RADIUS_INF) != 0);
@@ -467,7 +473,8 @@ int ort_host_trace_sequential_vjp(const ort_lens* lens, const ort_rays* rays_in,
   if (rc) return rc;
   if (params->zern_param && (feat & ort::KM_ZERN) == 0) return ORT_ERR_ARG;
   if (feat & F_IA) return ORT_ERR_ARG;  // no derivative code for thin-lens / phase / grating
-  if (lens->geometry_mask & (1u << ORT_GEOM_GRID_SAG)) return ORT_ERR_ARG;  // nor grid sags
+  if (lens->geometry_mask & ((1u << ORT_GEOM_GRID_SAG) | (1u << ORT_GEOM_NURBS)))
+    return ORT_ERR_ARG;  // nor grid sags / NURBS (no derivative kernels)
   a.in = *rays_in;
   return host_vjp<true>(a, lens, params, cotangent, rec_cotangent, rec, grad, grad_in, want_in);
 }
@@ -525,7 +532,7 @@ int ort_host_trace_pupil_vjp(const ort_lens* lens, const double* px, const doubl
   if (rc) return rc;
   if (params->zern_param && (feat & ort::KM_ZERN) == 0) return ORT_ERR_ARG;
   if (feat & F_IA) return ORT_ERR_ARG;
-  if (lens->geometry_mask & (1u << ORT_GEOM_GRID_SAG)) return ORT_ERR_ARG;
+  if (lens->geometry_mask & ((1u << ORT_GEOM_GRID_SAG) | (1u << ORT_GEOM_NURBS))) return ORT_ERR_ARG;
   a.px = px;
   a.py = py;
   return host_vjp<false>(a, lens, params, cotangent, nullptr, nullptr, grad, nullptr, false);

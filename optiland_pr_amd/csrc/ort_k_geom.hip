@@ -1,10 +1,12 @@
-// ort_k_geom.hip -- per-geometry primitive kernels (16 Newton-kind specialisations)
+// ort_k_geom.hip -- per-geometry primitive kernels (16 Newton-kind specialisations, and
+// one with every kind and the NURBS solves)
 // (kernel templates: ort_kernels.h; compiled as its own translation unit)
 
 #include "ort_kernels.h"
 
 namespace ortk {
 GeomFn select_geom(uint32_t km) {
+  if (km & ort::KM_NURBS) return geom_kernel<15u | ort::KM_NURBS>;  // NURBS: every kind
   switch (km) {
 #define ORT_G(K) \
   case (K):      \

@@ -159,7 +159,11 @@ __device__ inline double final_alpha(const KArgs& a, int lam, double w) {
 
 // geometry ids this library implements (enum ort_geometry); the kernels turn any other
 // id into NaN rays plus ORT_STATUS_BAD_GEOMETRY
-__device__ inline bool known_geometry(int g) { return g >= ORT_GEOM_PLANE && g <= ORT_GEOM_GRID_SAG; }
+__device__ inline bool known_geometry(int g) { return g >= ORT_GEOM_PLANE && g <= ORT_GEOM_NURBS; }
+// surfaces of the Newton schedule / statistics machinery (not plane, conic or NURBS)
+__device__ inline bool scheduled_geometry(int g) {
+  return g != ORT_GEOM_PLANE && g != ORT_GEOM_STANDARD && g != ORT_GEOM_NURBS;
+}
 
 // status bit of a normalisation-range error at surface s (zernike.py:234-246,
 // chebyshev.py:203-215: both raise ValueError in the reference)
@@ -333,6 +337,10 @@ __device__ inline __attribute__((always_inline)) double newton_distance(const KA
     if (s.geometry == ORT_GEOM_GRID_SAG)
       return grid_distance<FEAT>(a, s, si, r, active, group, group_uniform, sched);
   }
+  if constexpr ((FEAT & ort::KM_NURBS) != 0) {
+    if (s.geometry == ORT_GEOM_NURBS)  // its own per-ray (u, v) solve (ort_nurbs.h)
+      return ort::nurbs_distance(ort::nurbs_view(a.coef + s.coef_off), s.tol, s.max_iter, r);
+  }
   const bool rinf = (s.flags & ORT_SURF_RADIUS_INF) != 0;
   double t;
   if constexpr (FAST)
@@ -370,6 +378,22 @@ __device__ inline __attribute__((always_inline)) double newton_distance(const KA
   const int U = sched ? sched[group * a.n_surf + si] : max_iter;
   ConvBits mask;
   int last_bad = -1;
+  // Wave-level statistics (#ifndef ORT_LANE_STATS, A/B builds): a group-uniform wave whose
+  // stop indices fall in the mask window (conv_base 0, U < 128) forms the wave's AND of
+  // the convergence bits and its last non-converged index from one ballot per evaluation
+  // -- over the lanes reporting at that index, i.e. not yet out of range on the fast
+  // pass: their values up to there are the exact path's, which reports the same bits for
+  // them again if they turn bad later -- instead of per-lane 64-bit masks reduced at the
+  // end (report_newton). The bits, the index and the atomics are the same.
+#ifndef ORT_LANE_STATS
+  const bool wstat = a.stats && group_uniform && a.conv_base == 0 &&
+                     __builtin_amdgcn_readfirstlane(U) < 128;
+#else
+  constexpr bool wstat = false;
+#endif
+  uint64_t ws0 = 0, ws1 = 0;  // (wave-uniform)
+  int wlast = -1;
+  bool wany = false;
   // Every evaluation is one call site (the kernel's code size is its hot loop): at j < U
   // sag + the update's slopes at P(t) (kSlope) and the update; at j = U (the stop test)
   // the same evaluation, the interaction's unit normal formed from those slopes -- for the
@@ -384,6 +408,7 @@ __device__ inline __attribute__((always_inline)) double newton_distance(const KA
   for (int j = 0;; ++j) {
     const bool lane_on = active && j <= U;
     if (!__any(lane_on)) break;
+    bool rep = false, miss = false;  // wstat: this lane reports index j / did not converge
     if (lane_on) {
       bool rerr = false;
       double nx, ny, nz;
@@ -394,8 +419,13 @@ __device__ inline __attribute__((always_inline)) double newton_distance(const KA
       // loop broke there (U < max_iter)
       if (rerr && (j < U || U < max_iter) && !(FAST && bad)) range_bits |= range_bit(s);
       const bool conv = fabs(f) < tol;  // NaN never converges (np.max propagates NaN)
-      if (conv) mask.set(j, a.conv_base);
-      if (!conv) last_bad = j;
+      if (wstat) {
+        rep = !(FAST && bad);
+        miss = rep && !conv;
+      } else {
+        if (conv) mask.set(j, a.conv_base);
+        if (!conv) last_bad = j;
+      }
       if (upd) {
         if constexpr ((FEAT & F_TAPE) != 0) {
           // the iterate before the m-th last update, m = U - 1 - j, straight into its tape
@@ -427,8 +457,28 @@ __device__ inline __attribute__((always_inline)) double newton_distance(const KA
         nnz = nz;
       }
     }
+    if (wstat && __ballot(rep) != 0) {  // (uniform control flow: the state stays scalar)
+      wany = true;
+      if (__ballot(miss) == 0) {
+        if (j < 64)
+          ws0 |= 1ull << j;
+        else
+          ws1 |= 1ull << (j - 64);
+      } else {
+        wlast = j;
+      }
+    }
   }
-  report_newton(a, si, active && !(FAST && bad), group, group_uniform, mask, last_bad, U);
+  if (wstat) {
+    if (wany && (threadIdx.x & 63) == 0) {
+      ort_newton_stat* st = &a.stats[group * a.n_surf + si];
+      if (ws0 != ~0ull) and_if_changes(&st->conv_mask[0], ws0);
+      if (ws1 != ~0ull) and_if_changes(&st->conv_mask[1], ws1);
+      if (wlast >= 0) max_if_changes(&st->last_bad, wlast);
+    }
+  } else {
+    report_newton(a, si, active && !(FAST && bad), group, group_uniform, mask, last_bad, U);
+  }
   if constexpr ((FEAT & F_TAPE) != 0) {
     // the iterate rows no update fills (m >= U) get the root: every tape row is written
     // (the tape is the trace op's output; the adjoint reads only m < min(U, kHist))
@@ -546,7 +596,7 @@ __device__ inline int newton_decide(const ort_surface* surf, int32_t n_surf, int
   for (int64_t g = threadIdx.x; g < n_groups; g += kBlock) {
     for (int s = 0; s < n_surf; ++s) {
       const ort_surface sf = surf[s];
-      if (sf.geometry == ORT_GEOM_PLANE || sf.geometry == ORT_GEOM_STANDARD) continue;
+      if (!scheduled_geometry(sf.geometry)) continue;
       int32_t* U_p = sched + g * n_surf + s;
       const int U = *U_p;
       const int max_iter = sf.max_iter;

@@ -1,0 +1,270 @@
+// ort_nurbs.h -- NURBS surfaces (geometries/nurbs/nurbs_geometry.py, nurbs_basis_functions.py)
+// for the trace kernels, the geometry kernel and the host build. Included by ort_core.h
+// inside namespace ort (it uses Ray and ORT_INLINE from there).
+//
+// Block (lens.coef at coef_off, optiland_pr_amd/nurbs.py lowered_block):
+//   p, q, nu, nv, U[nu + p + 1], V[nv + q + 1], Pw[4][nu][nv] = (x w, y w, z w, w)
+// with clamped knot vectors (the first p + 1 and the last p + 1 knots equal; the host
+// refuses others) and degrees 1 .. kNurbsMaxDeg.
+//
+// The reference finds the parameters (u, v) of a ray's hit (distance: two planes through
+// the ray) or of the point above (x, y) (sag, surface_normal) by a 2 x 2 Newton iteration
+// from (0, 0), nurbs_geometry.py:606-822: residual r at (u, v), (u, v) -= inv(J) r, points
+// that left the unit square restarted, stop after the update made at the first iteration
+// whose max |r| over the call is below tol. Here each ray iterates on its own and stops
+// after the update made at its own first |r| < tol: once a ray's residual is below tol the
+// reference's further updates move (u, v) by O(|r|^2), below the rounding of its result.
+// Restart values come from restart_value (oracle/nurbs_np.py restates the same sequence);
+// the reference draws them from numpy.random, so a restarted point's path differs while its
+// root is the same.
+//
+// Basis functions: the non-zero ones of the knot span (NURBS Book A2.2's window), each by
+// the reference's own recurrence expression (eq. 2.5, nurbs_basis_functions.py:55-67, the
+// zero-denominator terms 0) -- the table entries it leaves out are exact zeros there.
+// Derivatives: eq. 2.9 from the degree p - 1 window (nurbs_basis_functions.py:119-132).
+// The surface sums run over the (p + 1)(q + 1) window of the control net; the reference's
+// matmul sums the same non-zero products in another order (the rounding differs at the
+// ulp level).
+
+constexpr int kNurbsMaxDeg = 5;
+
+// Compiled only into the kernels of lenses with NURBS surfaces (ort::KM_NURBS: the six
+// ort_k_trace_ia.hip specialisations and one geometry kernel) -- an out-of-line call in
+// the shared freeform kernels cost them half their occupancy (the call ABI's register
+// and scratch reservations: 150 -> 256 + 74 AGPRs, 400 B scratch, measured).
+#define ORT_NURBS_FN ORT_INLINE
+
+struct NurbsView {
+  const double* U;
+  const double* V;
+  const double* Pw;  // [4][nu][nv]
+  int p, q, nu, nv;
+};
+
+template <class PD>
+ORT_INLINE NurbsView nurbs_view(PD C) {
+  NurbsView g;
+  g.p = (int)C[0];
+  g.q = (int)C[1];
+  g.nu = (int)C[2];
+  g.nv = (int)C[3];
+  g.U = (const double*)(C + 4);
+  g.V = g.U + g.nu + g.p + 1;
+  g.Pw = g.V + g.nv + g.q + 1;
+  return g;
+}
+
+// the knot span k (p <= k <= n = n_ctrl - 1) with K[k] <= u < K[k + 1]; u == K[n + p + 1]
+// counts as the last span (nurbs_basis_functions.py:51-52); -1 outside [K[0], K[n + p + 1]]
+// and for NaN (every basis function is 0 there, the point 0 / 0)
+ORT_INLINE int nurbs_span(const double* K, int p, int n_ctrl, double u) {
+  const int n = n_ctrl - 1;
+  if (!(u >= K[0] && u <= K[n + p + 1])) return -1;
+  if (u == K[n + p + 1]) return n;
+  int lo = p, hi = n + 1;  // K[lo] <= u < K[hi]
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (K[mid] <= u)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+
+// values B[j] = N_{k-p+j, p}(u) and first derivatives D[j] of the span's basis functions
+ORT_INLINE void nurbs_basis(const double* K, int p, int k, double u, double B[kNurbsMaxDeg + 1],
+                            double D[kNurbsMaxDeg + 1]) {
+  double Bm[kNurbsMaxDeg + 1];  // degree p - 1
+#pragma unroll
+  for (int j = 0; j <= kNurbsMaxDeg; ++j) B[j] = Bm[j] = D[j] = 0.0;
+#pragma unroll
+  for (int j = 0; j <= kNurbsMaxDeg; ++j)
+    if (j == p) B[j] = 1.0;  // degree 0: N_{k,0} = 1
+#pragma unroll
+  for (int d = 1; d <= kNurbsMaxDeg; ++d) {
+    if (d > p) break;
+    if (d == p) {
+#pragma unroll
+      for (int j = 0; j <= kNurbsMaxDeg; ++j) Bm[j] = B[j];
+    }
+#pragma unroll
+    for (int j = 0; j <= kNurbsMaxDeg; ++j) {
+      if (j > p || j < p - d) continue;
+      const int i = k - p + j;
+      const double next = (j < p) ? B[j + 1] : 0.0;
+      const double d1 = K[i + d] - K[i];
+      const double d2 = K[i + d + 1] - K[i + 1];
+      const double n1 = d1 == 0.0 ? 0.0 : (u - K[i]) / d1 * B[j];
+      const double n2 = d2 == 0.0 ? 0.0 : (K[i + d + 1] - u) / d2 * next;
+      B[j] = n1 + n2;
+    }
+  }
+  // eq. 2.9: N'_{i,p} = p N_{i,p-1} / (K[i+p] - K[i]) - p N_{i+1,p-1} / (K[i+p+1] - K[i+1])
+  const double fp = (double)p;
+#pragma unroll
+  for (int j = 0; j <= kNurbsMaxDeg; ++j) {
+    if (j > p) continue;
+    const int i = k - p + j;
+    const double next = (j < p) ? Bm[j + 1] : 0.0;
+    const double d1 = K[i + p] - K[i];
+    const double d2 = K[i + p + 1] - K[i + 1];
+    const double n1 = d1 == 0.0 ? 0.0 : fp * Bm[j] / d1;
+    const double n2 = d2 == 0.0 ? 0.0 : fp * next / d2;
+    D[j] = n1 - n2;
+  }
+}
+
+// S(u, v) and, with want_d, S_u, S_v (nurbs_geometry.py:309-374, 455-583: the homogeneous
+// sums, then S = A / w, S_u = (A_u - w_u S) / w, S_v = (A_v - w_v S) / w)
+ORT_INLINE void nurbs_eval(const NurbsView& g, double u, double v, bool want_d, double S[3],
+                           double Su[3], double Sv[3]) {
+  const int ku = nurbs_span(g.U, g.p, g.nu, u);
+  const int kv = nurbs_span(g.V, g.q, g.nv, v);
+  if (ku < 0 || kv < 0) {
+    for (int c = 0; c < 3; ++c) S[c] = Su[c] = Sv[c] = __builtin_nan("");
+    return;
+  }
+  double Nu[kNurbsMaxDeg + 1], Du[kNurbsMaxDeg + 1], Nv[kNurbsMaxDeg + 1], Dv[kNurbsMaxDeg + 1];
+  nurbs_basis(g.U, g.p, ku, u, Nu, Du);
+  nurbs_basis(g.V, g.q, kv, v, Nv, Dv);
+  double A[4] = {0.0, 0.0, 0.0, 0.0}, Au[4] = {0.0, 0.0, 0.0, 0.0}, Av[4] = {0.0, 0.0, 0.0, 0.0};
+  const int64_t plane = (int64_t)g.nu * g.nv;
+#pragma unroll
+  for (int i = 0; i <= kNurbsMaxDeg; ++i) {
+    if (i > g.p) continue;
+    const double* row = g.Pw + (int64_t)(ku - g.p + i) * g.nv + (kv - g.q);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      double s = 0.0, sv = 0.0;
+#pragma unroll
+      for (int j = 0; j <= kNurbsMaxDeg; ++j) {
+        if (j > g.q) continue;
+        const double pw = row[c * plane + j];
+        s = s + pw * Nv[j];
+        sv = sv + pw * Dv[j];
+      }
+      A[c] = A[c] + s * Nu[i];
+      Au[c] = Au[c] + s * Du[i];
+      Av[c] = Av[c] + sv * Nu[i];
+    }
+  }
+  for (int c = 0; c < 3; ++c) S[c] = A[c] / A[3];
+  if (want_d) {
+    for (int c = 0; c < 3; ++c) {
+      Su[c] = (Au[c] - Au[3] * S[c]) / A[3];
+      Sv[c] = (Av[c] - Av[3] * S[c]) / A[3];
+    }
+  }
+}
+
+// restart value of iteration j, slot s (oracle/nurbs_np.py restart_value)
+ORT_INLINE double nurbs_restart_value(int j, int s) {
+  const double x = 0.5 + (double)(4 * j + s) * 0.6180339887498949;
+  return x - floor(x);
+}
+
+// nurbs_geometry.py:711-714: points that left the unit square restart
+ORT_INLINE void nurbs_restart(double& u, double& v, int j) {
+  if (u < 0.0 || v < 0.0) u = nurbs_restart_value(j, 0);
+  if (u < 0.0 || v < 0.0) v = nurbs_restart_value(j, 1);
+  if (u > 1.0 || v > 1.0) u = nurbs_restart_value(j, 2);
+  if (u > 1.0 || v > 1.0) v = nurbs_restart_value(j, 3);
+}
+
+// one correction of the 2 x 2 system J (du, dv) = r, J = [[a, b], [c, d]]
+// (nurbs_geometry.py:635-651: adj(J) / det(J) applied to r)
+ORT_INLINE void nurbs_update(double& u, double& v, double r1, double r2, double a, double b,
+                             double c, double d) {
+  const double det = a * d - b * c;
+  const double cu = (d / det) * r1 + (-b / det) * r2;
+  const double cv = (-c / det) * r1 + (a / det) * r2;
+  u = u - cu;
+  v = v - cv;
+}
+
+// (u, v) of the surface point above (x, y) (nurbs_geometry.py:653-718)
+ORT_INLINE void nurbs_solve_xy(const NurbsView& g, double x, double y, double tol, int max_iter,
+                               double& u, double& v) {
+  u = 0.0;
+  v = 0.0;
+  for (int j = 0; j < max_iter; ++j) {
+    double S[3], Su[3], Sv[3];
+    nurbs_eval(g, u, v, true, S, Su, Sv);
+    const double r1 = S[1] - y, r2 = S[0] - x;
+    nurbs_update(u, v, r1, r2, Su[1], Sv[1], Su[0], Sv[0]);
+    nurbs_restart(u, v, j);
+    if (fabs(r1) < tol && fabs(r2) < tol) break;  // NaN never passes
+  }
+}
+
+struct NurbsSagNormal {
+  double z, nx, ny, nz;
+};
+
+// sag(x, y) (nurbs_geometry.py:696-719) and the unit normal cross(S_u, S_v) / |.| at the
+// same (u, v) (nurbs_geometry.py:585-604, 796-822)
+ORT_NURBS_FN NurbsSagNormal nurbs_sag_normal(NurbsView g, double tol, int max_iter, double x,
+                                             double y) {
+  double u, v;
+  nurbs_solve_xy(g, x, y, tol, max_iter, u, v);
+  double S[3], Su[3], Sv[3];
+  nurbs_eval(g, u, v, true, S, Su, Sv);
+  const double cx = Su[1] * Sv[2] - Su[2] * Sv[1];
+  const double cy = Su[2] * Sv[0] - Su[0] * Sv[2];
+  const double cz = Su[0] * Sv[1] - Su[1] * Sv[0];
+  const double m = sqrt(cx * cx + cy * cy + cz * cz);
+  return NurbsSagNormal{S[2], cx / m, cy / m, cz / m};
+}
+
+ORT_INLINE double sagnorm_nurbs(const NurbsView& g, double tol, int max_iter, double x,
+                                double y, bool want_normal, double& nx, double& ny,
+                                double& nz) {
+  const NurbsSagNormal o = nurbs_sag_normal(g, tol, max_iter, x, y);
+  if (want_normal) {
+    nx = o.nx;
+    ny = o.ny;
+    nz = o.nz;
+  }
+  return o.z;
+}
+
+// distance(rays) (nurbs_geometry.py:721-794): the ray as the intersection of the planes
+// N1 . P + d1 = 0, N2 . P + d2 = 0; the result |S(u, v) - P0| (unsigned)
+ORT_NURBS_FN double nurbs_distance(NurbsView g, double tol, int max_iter, Ray r) {
+  double N1x, N1y, N1z;
+  if (r.L > r.M && r.L > r.N) {
+    const double s = sqrt(r.L * r.L + r.M * r.M);
+    N1x = r.M / s;
+    N1y = -r.L / s;
+    N1z = 0.0;
+  } else {
+    const double s = sqrt(r.N * r.N + r.M * r.M);
+    N1x = 0.0;
+    N1y = r.N / s;
+    N1z = -r.M / s;
+  }
+  const double N2x = N1y * r.N - N1z * r.M;
+  const double N2y = N1z * r.L - N1x * r.N;
+  const double N2z = N1x * r.M - N1y * r.L;
+  const double d1 = -(N1x * r.x + N1y * r.y + N1z * r.z);
+  const double d2 = -(N2x * r.x + N2y * r.y + N2z * r.z);
+  double u = 0.0, v = 0.0;
+  for (int j = 0; j < max_iter; ++j) {
+    double S[3], Su[3], Sv[3];
+    nurbs_eval(g, u, v, true, S, Su, Sv);
+    const double r1 = N1x * S[0] + N1y * S[1] + N1z * S[2] + d1;
+    const double r2 = N2x * S[0] + N2y * S[1] + N2z * S[2] + d2;
+    const double a = N1x * Su[0] + N1y * Su[1] + N1z * Su[2];
+    const double b = N1x * Sv[0] + N1y * Sv[1] + N1z * Sv[2];
+    const double c = N2x * Su[0] + N2y * Su[1] + N2z * Su[2];
+    const double d = N2x * Sv[0] + N2y * Sv[1] + N2z * Sv[2];
+    nurbs_update(u, v, r1, r2, a, b, c, d);
+    nurbs_restart(u, v, j);
+    if (fabs(r1) < tol && fabs(r2) < tol) break;
+  }
+  double S[3], Su[3], Sv[3];
+  nurbs_eval(g, u, v, false, S, Su, Sv);
+  const double dx = S[0] - r.x, dy = S[1] - r.y, dz = S[2] - r.z;
+  return sqrt(dx * dx + dy * dy + dz * dz);
+}

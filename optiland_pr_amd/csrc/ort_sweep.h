@@ -47,7 +47,7 @@ constexpr ort::ZSeed kNoSeed{nullptr, 0};
 // Kernel specialisation bits: bits 0-3 = Newton kinds present (ort::KM_*), bit 4 = rays
 // generated in-kernel from pupil coordinates.
 enum : uint32_t {
-  F_KM = 15u,
+  F_KM = 15u | ort::KM_NURBS,  // the kinds (bits 0-3 and KM_NURBS = bit 16)
   F_GEN = 1u << 4,
   F_REC = 1u << 5,   // some surfaces are recorded (standard_surface.py:266-286)
   F_MONO = 1u << 6,  // the wavelength row is wave-uniform (one wavelength in the lens
@@ -191,7 +191,7 @@ inline int fill_args(KArgs& a, const ort_lens* lens, const ort_batch* batch,
   if (opt->conv_base < 0) return ORT_ERR_ARG;
   // geometry ids this library knows (enum ort_geometry): anything else is refused here
   // rather than traced as some other kind
-  if (lens->geometry_mask & ~((2u << ORT_GEOM_GRID_SAG) - 1u)) return ORT_ERR_ARG;
+  if (lens->geometry_mask & ~((2u << ORT_GEOM_NURBS) - 1u)) return ORT_ERR_ARG;
   a.rec = rec;
   a.stats = stats;
   a.status = status;
@@ -204,6 +204,10 @@ inline int fill_args(KArgs& a, const ort_lens* lens, const ort_batch* batch,
                              (1u << ORT_GEOM_FORBES_QBFS) | (1u << ORT_GEOM_FORBES_Q2D) |
                              (1u << ORT_GEOM_GRID_SAG)))
     feat |= ort::KM_FREE;
+  // NURBS lenses take the all-kinds kernels of ort_k_trace_ia.hip (the only trace kernels
+  // with the NURBS solves compiled in)
+  if (lens->geometry_mask & (1u << ORT_GEOM_NURBS))
+    feat |= ort::KM_NURBS | F_IA | ort::KM_EVEN | ort::KM_ODD | ort::KM_ZERN | ort::KM_FREE;
   if (rec) feat |= F_REC;
   if (batch->w) {  // per-ray wavelengths: n, k from the material tables
     if (!lens->materials) return ORT_ERR_ARG;

@@ -583,3 +583,127 @@ class ForbesQ2dGeometry(_ForbesBase):
             block += q2d_order_block(ams[m - 1], m)
             block += q2d_order_block(bms[m - 1], m)
         return scalar(self.radius), scalar(self.k), self.tol, self.max_iter, 1.0, block
+
+
+class NurbsGeometry(BaseGeometry):
+    """geometries/nurbs/nurbs_geometry.py:29-932: a NURBS surface -- an explicit control
+    net (control_points (3, n+1, m+1), weights, degrees, knots) or, with no control points,
+    a bicubic least-squares fit of the conic (radius, conic) or of a plane over the window
+    [x_center +- nurbs_norm_x] x [y_center +- nurbs_norm_y] once fit_surface() is called
+    (the reference fits only then, nurbs_geometry.py:828-838). sag / surface_normal /
+    distance solve for (u, v) on the MI355X (ort_nurbs.h); get_value / get_derivative /
+    get_normals evaluate at given (u, v) on the host (nurbs.py)."""
+
+    geometry_id = _abi.GEOM_NURBS
+
+    def __init__(self, coordinate_system, radius=np.inf, conic=0.0, nurbs_norm_x=None,
+                 nurbs_norm_y=None, x_center=0.0, y_center=0.0, control_points=None,
+                 weights=None, u_degree=None, v_degree=None, u_knots=None, v_knots=None,
+                 n_points_u=4, n_points_v=4, tol=1e-10, max_iter=100):
+        from . import nurbs
+
+        super().__init__(coordinate_system)
+        self.radius = radius
+        self.k = conic
+        self.nurbs_norm_x = nurbs_norm_x
+        self.nurbs_norm_y = nurbs_norm_y
+        self.x_center = x_center
+        self.y_center = y_center
+        self.tol = tol
+        self.max_iter = max_iter
+        self.is_symmetric = False
+        self.P = None if control_points is None else np.asarray(control_points, np.float64)
+        self.W = None if weights is None else np.asarray(weights, np.float64)
+        self.p, self.q = u_degree, v_degree
+        self.U = None if u_knots is None else np.asarray(u_knots, np.float64)
+        self.V = None if v_knots is None else np.asarray(v_knots, np.float64)
+        if self.P is None:  # fitted on fit_surface()
+            self.is_fitted = True
+            self.ndim = 3
+            self.P_size_u = n_points_u + 1
+            self.P_size_v = n_points_v + 1
+            return
+        # nurbs_geometry.py:132-269: the missing parts of an explicit net take the
+        # reference's defaults (unit weights; degree = points - 1, i.e. Bezier; clamped
+        # uniform knots)
+        self.is_fitted = False
+        self.ndim = self.P.shape[0]
+        nu, nv = self.P.shape[1], self.P.shape[2]
+        self.P_size_u, self.P_size_v = nu, nv
+        if self.W is None:
+            self.W = np.ones((nu, nv))
+        if self.p is None and self.U is None:
+            self.p = nu - 1
+        if self.q is None and self.V is None:
+            self.q = nv - 1
+        if self.U is None:
+            self.U = nurbs.clamped_knots(nu, self.p)
+        if self.V is None:
+            self.V = nurbs.clamped_knots(nv, self.q)
+        if self.p is None:
+            self.p = len(self.U) - nu - 1
+        if self.q is None:
+            self.q = len(self.V) - nv - 1
+        self.surface_type = ("NURBS" if weights is not None else
+                             "Bezier" if u_knots is None and u_degree is None else "B-Spline")
+
+    def __str__(self):
+        return "NURBS"
+
+    def flip(self):
+        """nurbs_geometry.py:271-278."""
+        self.radius = -self.radius
+        self.P = self.P.copy()
+        self.P[2] = -self.P[2]
+
+    def fit_surface(self):
+        """nurbs_geometry.py:828-932: fit the conic (or, with an infinite radius, a plane)."""
+        from . import nurbs
+
+        nx, ny = float(self.nurbs_norm_x), float(self.nurbs_norm_y)
+        xc, yc = float(self.x_center), float(self.y_center)
+        if np.isinf(scalar(self.radius)):
+            P, W, p, q, U, V = nurbs.fit_plane(nx, ny, xc, yc, self.P_size_u, self.P_size_v)
+        else:
+            P, W, p, q, U, V = nurbs.fit_standard(scalar(self.radius), scalar(self.k), nx, ny,
+                                                  xc, yc, self.P_size_u, self.P_size_v)
+            self.P_size_u, self.P_size_v = P.shape[1], P.shape[2]
+        self.surface_type = "NURBS"
+        self.P, self.W, self.p, self.q, self.U, self.V = P, W, p, q, U, V
+
+    def _net(self):
+        if self.P is None:
+            raise ValueError("the NURBS surface has no control net yet: call fit_surface()")
+        return self.P, self.W, int(self.p), int(self.q), self.U, self.V
+
+    def get_value(self, u, v):
+        """nurbs_geometry.py:280-307: S(u, v), shape (3, ...) like u."""
+        from . import nurbs
+
+        u, v = np.asarray(u, np.float64), np.asarray(v, np.float64)
+        if u.size != v.size:
+            raise Exception("u and v must have the same size")
+        S = nurbs.surface_point(*self._net(), u.ravel(), v.ravel())
+        return S.reshape((S.shape[0],) + u.shape) if u.ndim > 1 else S
+
+    def get_derivative(self, u, v, order_u, order_v):
+        """nurbs_geometry.py:428-453: d^(order_u + order_v) S / du^order_u dv^order_v."""
+        from . import nurbs
+
+        u, v = np.asarray(u, np.float64), np.asarray(v, np.float64)
+        dS = nurbs.surface_derivatives(*self._net(), u.ravel(), v.ravel(), order_u,
+                                       order_v)[order_u][order_v]
+        return dS.reshape((dS.shape[0],) + u.shape) if u.ndim > 1 else dS
+
+    def get_normals(self, u, v):
+        """nurbs_geometry.py:585-604."""
+        from . import nurbs
+
+        return nurbs.surface_normals(*self._net(), np.asarray(u, np.float64),
+                                     np.asarray(v, np.float64))
+
+    def lower_params(self):
+        from . import nurbs
+
+        blk = nurbs.lowered_block(*self._net())
+        return scalar(self.radius), scalar(self.k), float(self.tol), int(self.max_iter), 1.0, blk

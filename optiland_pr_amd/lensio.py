@@ -29,6 +29,7 @@ from .geometries import (
     ForbesSolverConfig,
     ForbesSurfaceConfig,
     GridSagGeometry,
+    NurbsGeometry,
     OddAsphere,
     Plane,
     PlaneGrating,
@@ -76,6 +77,15 @@ def geometry_from_dict(d):
     tol, max_iter = _f(d.get("tol"), 1e-10), int(d.get("max_iter", 100))
     if t == "Plane":
         return Plane(cs)
+    if t == "NurbsGeometry":  # the control net as this module writes it (geometry_to_dict)
+        g = NurbsGeometry(cs, _f(d.get("radius"), np.inf), _f(d.get("conic")),
+                          d.get("nurbs_norm_x"), d.get("nurbs_norm_y"),
+                          _f(d.get("x_center")), _f(d.get("y_center")),
+                          d.get("control_points"), d.get("weights"), d.get("u_degree"),
+                          d.get("v_degree"), d.get("u_knots"), d.get("v_knots"),
+                          tol=_f(d.get("tol"), 1e-10), max_iter=int(d.get("max_iter", 100)))
+        g.is_fitted = bool(d.get("is_fitted", False))
+        return g
     if t == "GridSagGeometry":  # grid_sag.py:155-180
         return GridSagGeometry(cs, d["x_coordinates"], d["y_coordinates"], d["sag_values"],
                                _f(d.get("tol"), 1e-6), int(d.get("max_iter", 100)))
@@ -158,6 +168,19 @@ def geometry_to_dict(g):
         d["surface_config"] = {"radius": scalar(g.radius), "conic": scalar(g.k),
                                "norm_radius": g.norm_radius, "terms": terms}
         d["solver_config"] = {"tol": g.tol, "max_iter": g.max_iter}
+        return d
+    if isinstance(g, NurbsGeometry):  # the reference's NurbsGeometry has no to_dict of its
+        # own (geometries/base.py's writes no net): the control net, knots and fit window
+        net = g.P is not None
+        d.update(radius=scalar(g.radius), conic=scalar(g.k), tol=float(g.tol),
+                 max_iter=int(g.max_iter), nurbs_norm_x=g.nurbs_norm_x,
+                 nurbs_norm_y=g.nurbs_norm_y, x_center=float(g.x_center),
+                 y_center=float(g.y_center), is_fitted=bool(g.is_fitted),
+                 control_points=np.asarray(g.P).tolist() if net else None,
+                 weights=np.asarray(g.W).tolist() if net else None,
+                 u_degree=int(g.p) if net else None, v_degree=int(g.q) if net else None,
+                 u_knots=np.asarray(g.U).tolist() if net else None,
+                 v_knots=np.asarray(g.V).tolist() if net else None)
         return d
     if isinstance(g, GridSagGeometry):
         d.update(x_coordinates=g.x_grid.tolist(), y_coordinates=g.y_grid.tolist(),

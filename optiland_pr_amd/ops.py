@@ -134,7 +134,8 @@ def tangent_tables(table, pairs, params):
                 surf = np.zeros((n_param, S, 3), dtype=np.float64)
             g = int(row["geometry"])
             if kind in ("radius", "conic"):
-                if g in (_abi.GEOM_PLANE, _abi.GEOM_BICONIC, _abi.GEOM_TOROIDAL, _abi.GEOM_GRID_SAG):
+                if g in (_abi.GEOM_PLANE, _abi.GEOM_BICONIC, _abi.GEOM_TOROIDAL, _abi.GEOM_GRID_SAG,
+                         _abi.GEOM_NURBS):
                     raise NotImplementedError(f"surface {si}: {kind} of this geometry is not a "
                                               "differentiable parameter of the trace core")
                 surf[off, si, 0 if kind == "radius" else 1] = 1.0
@@ -216,6 +217,9 @@ def tape_doubles(dl, n):
 def _check_differentiable(table):
     if np.any(table.surfaces["geometry"] == _abi.GEOM_GRID_SAG):
         raise NotImplementedError("autograd through grid-sag surfaces is not implemented by "
+                                  "the trace core (no derivative kernels)")
+    if np.any(table.surfaces["geometry"] == _abi.GEOM_NURBS):
+        raise NotImplementedError("autograd through NURBS surfaces is not implemented by "
                                   "the trace core (no derivative kernels)")
     if table.interaction_mask & ~(1 << _abi.IA_REFRACT_REFLECT):
         raise NotImplementedError("autograd through thin-lens, phase or grating surfaces is "

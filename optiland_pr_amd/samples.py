@@ -436,6 +436,44 @@ class Grating(Optic):
         self.update_paraxial()
 
 
+def nurbs_back_net():
+    """The explicit rational back surface of NurbsLens: a 7 x 6 net over [-8, 8] x [-8, 8],
+    a concave bowl with an xy twist, non-uniform weights, u degree 3 / v degree 2 on
+    clamped non-uniform knots."""
+    xs = np.linspace(-8.0, 8.0, 7)
+    ys = np.linspace(-8.0, 8.0, 6)
+    X, Y = np.meshgrid(xs, ys, indexing="ij")
+    Z = -(X**2 + Y**2) / 140.0 + 0.002 * X * Y
+    W = 1.0 + 0.1 * np.cos(0.5 * X) * np.sin(0.4 * Y + 0.2)
+    U = [0.0, 0.0, 0.0, 0.0, 0.3, 0.5, 0.75, 1.0, 1.0, 1.0, 1.0]
+    V = [0.0, 0.0, 0.0, 0.2, 0.55, 0.8, 1.0, 1.0, 1.0]
+    return np.stack([X, Y, Z]), W, U, V
+
+
+class NurbsLens(Optic):
+    """A singlet with a bicubic NURBS fit of a conic in front (fit_surface) and an explicit
+    rational NURBS net behind (geometries/nurbs/nurbs_geometry.py)."""
+
+    def __init__(self):
+        super().__init__()
+        P, W, U, V = nurbs_back_net()
+        self.add_surface(index=0, thickness=np.inf)
+        self.add_surface(index=1, surface_type="nurbs", radius=40.0, conic=-0.5,
+                         nurbs_norm_x=8.0, nurbs_norm_y=8.0, n_points_u=8, n_points_v=8,
+                         thickness=4.0, material="SK16", is_stop=True)
+        self.add_surface(index=2, surface_type="nurbs", radius=-70.0, control_points=P,
+                         weights=W, u_degree=3, v_degree=2, u_knots=U, v_knots=V,
+                         thickness=45.0)
+        self.add_surface(index=3)
+        self.surface_group.surfaces[1].geometry.fit_surface()
+        self.set_aperture(aperture_type="EPD", value=10)
+        self.set_field_type(field_type="angle")
+        self.add_field(y=0)
+        self.add_field(y=5)
+        self.add_field(x=3, y=2)
+        self.add_wavelength(value=0.55, is_primary=True)
+
+
 class GridSagLens(Optic):
     """A singlet whose front surface is a 17 x 13 bilinear sag grid (grid_sag.py)."""
 
@@ -565,6 +603,7 @@ GOLDEN_LENSES = {
     "grating_reflective": lambda: Grating("reflective"),
     "grating_tilted": lambda: Grating("curved", angle=0.35),
     "grid_lens": GridSagLens,
+    "nurbs_lens": NurbsLens,
     "uv_projection": UVProjectionLens,
     "apod_gaussian": lambda: CookeTripletApodized("GaussianApodization", sigma=0.6),
     "apod_cos2": lambda: CookeTripletApodized("CosineSquaredApodization", R=0.9),

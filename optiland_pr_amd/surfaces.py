@@ -27,6 +27,7 @@ from .geometries import (
     OddAsphere,
     Plane,
     GridSagGeometry,
+    NurbsGeometry,
     PlaneGrating,
     PolynomialGeometry,
     StandardGratingGeometry,
@@ -176,6 +177,13 @@ def _make_geometry(surface_type, cs, kw):
         return GridSagGeometry(cs, kw.get("x_coordinates", []), kw.get("y_coordinates", []),
                                kw.get("sag_values", []), kw.get("tol", 1e-6),
                                kw.get("max_iter", 100))
+    if st == "nurbs":  # geometry_factory.py:316-337, NurbsConfig defaults
+        return NurbsGeometry(cs, radius, conic, kw.get("nurbs_norm_x", 0.0),
+                             kw.get("nurbs_norm_y", 0.0), kw.get("nurbs_x_center", 0.0),
+                             kw.get("nurbs_y_center", 0.0), kw.get("control_points"),
+                             kw.get("weights"), kw.get("u_degree", 3), kw.get("v_degree", 3),
+                             kw.get("u_knots"), kw.get("v_knots"), kw.get("n_points_u", 5),
+                             kw.get("n_points_v", 5), tol, max_iter)
     if st in ("forbes_qbfs", "forbes_q2d"):  # geometry_factory.py:282-314
         cfg = ForbesSurfaceConfig(
             radius=radius, conic=conic, norm_radius=kw.get("norm_radius", 1.0),
@@ -185,7 +193,8 @@ def _make_geometry(surface_type, cs, kw):
     raise ValueError(
         f"Surface type {st!r} is not lowered to the MI355X trace core (supported: "
         "standard, plane, paraxial, grating, even_asphere, odd_asphere, zernike, "
-        "polynomial, chebyshev, biconic, toroidal, forbes_qbfs, forbes_q2d, grid_sag).")
+        "polynomial, chebyshev, biconic, toroidal, forbes_qbfs, forbes_q2d, grid_sag, "
+        "nurbs).")
 
 
 _NAN_ROWS: dict = {}

@@ -47,7 +47,7 @@ CLOSED_FORM = ("cooke", "dg", "rt", "cooke_aperture", "cooke_shapes", "decentere
                "grating_tilted", "uv_projection", "apod_gaussian", "apod_cos2", "apod_hann",
                "apod_poly", "apod_supergauss", "apod_tukey", "apod_uniform", "cooke_abbe")
 NEWTON = ("rt_asph", "rt_odd", "tma_fringe", "tma_standard", "tma_noll", "freeform",
-          "forbes", "forbes_q2d", "phase_plate", "grid_lens")
+          "forbes", "forbes_q2d", "phase_plate", "grid_lens", "nurbs_lens")
 ALL_CASES = CLOSED_FORM + NEWTON
 
 FIELDS = _abi.RAY_FIELDS

@@ -429,6 +429,50 @@ def grid_lens():
     return lens
 
 
+def nurbs_back_net():
+    """The explicit rational back surface of nurbs_lens (shared with
+    optiland_pr_amd.samples.NurbsLens): a 7 x 6 net over [-8, 8] x [-8, 8], a concave bowl
+    with an xy twist, non-uniform weights, u degree 3 / v degree 2 on clamped non-uniform
+    knots."""
+    xs = np.linspace(-8.0, 8.0, 7)
+    ys = np.linspace(-8.0, 8.0, 6)
+    X, Y = np.meshgrid(xs, ys, indexing="ij")
+    Z = -(X**2 + Y**2) / 140.0 + 0.002 * X * Y
+    W = 1.0 + 0.1 * np.cos(0.5 * X) * np.sin(0.4 * Y + 0.2)
+    U = [0.0, 0.0, 0.0, 0.0, 0.3, 0.5, 0.75, 1.0, 1.0, 1.0, 1.0]
+    V = [0.0, 0.0, 0.0, 0.2, 0.55, 0.8, 1.0, 1.0, 1.0]
+    return np.stack([X, Y, Z]), W, U, V
+
+
+def nurbs_lens():
+    """A singlet whose front surface is a bicubic NURBS fit of a conic and whose back surface
+    is an explicit rational NURBS net (nurbs_geometry.py): covers the (u, v) solves of
+    distance and surface_normal inside a trace."""
+    np.random.seed(11)  # the reference's restarts draw from numpy.random
+    P, W, U, V = nurbs_back_net()
+    lens = ref_optic.Optic()
+    lens.add_surface(index=0, thickness=np.inf)
+    lens.add_surface(index=1, surface_type="nurbs", radius=40.0, conic=-0.5,
+                     nurbs_norm_x=8.0, nurbs_norm_y=8.0, n_points_u=8, n_points_v=8,
+                     thickness=4.0, material="SK16", is_stop=True)
+    lens.add_surface(index=2, surface_type="nurbs", radius=-70.0, control_points=P.tolist(),
+                     weights=W.tolist(), u_degree=3, v_degree=2, u_knots=U, v_knots=V,
+                     thickness=45.0)
+    lens.add_surface(index=3)
+    lens.surface_group.surfaces[1].geometry.fit_surface()
+    for si in (1, 2):  # the reference's NurbsGeometry keeps P / W / knots as given
+        g = lens.surface_group.surfaces[si].geometry
+        g.P, g.W = np.asarray(g.P, dtype=np.float64), np.asarray(g.W, dtype=np.float64)
+        g.U, g.V = np.asarray(g.U, dtype=np.float64), np.asarray(g.V, dtype=np.float64)
+    lens.set_aperture(aperture_type="EPD", value=10)
+    lens.set_field_type(field_type="angle")
+    lens.add_field(y=0)
+    lens.add_field(y=5)
+    lens.add_field(x=3, y=2)
+    lens.add_wavelength(value=0.55, is_primary=True)
+    return lens
+
+
 def cooke_apod(kind, **kwargs):
     """CookeTriplet with a pupil apodization (optic.set_apodization, optic.py:401-419;
     applied in ray_generator.py:91-95)."""
@@ -519,6 +563,7 @@ CASES = {
     "grating_tilted": (lambda: grating("curved", angle=0.35), [(0, 0), (0.2, 0.8)], [0.587],
                        "uniform", 24),
     "grid_lens": (grid_lens, [(0, 0), (0, 1), (0.6, 0.6)], [0.48, 0.55], "uniform", 24),
+    "nurbs_lens": (nurbs_lens, [(0, 0), (0, 1), (0.6, 0.6)], [0.48, 0.55], "uniform", 24),
     "cooke_abbe": (cooke_abbe, [(0, 0), (0, 1)], [0.48, 0.55, 0.65], "uniform", 24),
     "uv_projection": (uv_projection, [(0, 0), (0, 0.7), (0, 1)], [0.248], "uniform", 24),
     "apod_gaussian": (cooke_apod("GaussianApodization", sigma=0.6), [(0, 0), (0, 1)], [0.55],

@@ -59,13 +59,16 @@ static void globalize(const Lens& L, const ort_surface& s, Ray& r) {
   r.z = r.z + s.cs_t[2];
 }
 
-static bool is_newton(int g) { return g != ORT_GEOM_PLANE && g != ORT_GEOM_STANDARD; }
+static bool is_newton(int g) {
+  return g != ORT_GEOM_PLANE && g != ORT_GEOM_STANDARD && g != ORT_GEOM_NURBS;
+}
 
 // one reference trace call over rays [0, n) of a segment at wavelength row lam
 static int trace_segment(const Lens& L, std::vector<Ray>& rays, int lam, int start,
                          int32_t* updates, double* rec, int64_t rec_stride, int64_t rec_off,
                          int& status) {
-  constexpr unsigned KM = ort::KM_EVEN | ort::KM_ODD | ort::KM_ZERN | ort::KM_FREE;
+  constexpr unsigned KM =
+      ort::KM_EVEN | ort::KM_ODD | ort::KM_ZERN | ort::KM_FREE | ort::KM_NURBS;
   const double* coef = L.coef.data();
   const ort_zernike_term* zern = L.zern.data();
   const size_t n = rays.size();
@@ -79,6 +82,10 @@ static int trace_segment(const Lens& L, std::vector<Ray>& rays, int lam, int sta
       for (size_t k = 0; k < n; ++k) t[k] = ort::distance_plane(rays[k]);
     } else if (s.geometry == ORT_GEOM_GRID_SAG) {
       return 3;  // the grid sag's own Newton is not restated here
+    } else if (s.geometry == ORT_GEOM_NURBS) {  // its per-ray (u, v) solve (ort_nurbs.h)
+      for (size_t k = 0; k < n; ++k)
+        t[k] = ort::nurbs_distance(ort::nurbs_view(coef + s.coef_off), s.tol, s.max_iter,
+                                   rays[k]);
     } else {
       const bool rinf = (s.flags & ORT_SURF_RADIUS_INF) != 0;
       for (size_t k = 0; k < n; ++k) t[k] = ort::distance_conic(rays[k], s.radius, s.conic, rinf);

@@ -1,0 +1,86 @@
+"""GPU: NURBS surfaces (ort_nurbs.h) through the geometry API kernels against the reference's
+own outputs (tests/golden/nurbs.npz from tests/golden/gen_nurbs_golden.py: the inputs of its
+tests/test_nurbs_geometry.py plus seeded points and rays on five nets) and against the
+oracle (oracle/nurbs_np.py). The trace of a lens with a fitted and an explicit NURBS surface
+is pinned by test_gpu_parity.py's nurbs_lens case.
+
+Stated tolerances: sag and distance 1e-11 mm, normal components 1e-12 -- each ray iterates
+to its own |r| < tol (1e-10) instead of the call-wide stop, and the window sums of the
+control net run in another order than the reference's matmul."""
+
+import numpy as np
+import pytest
+
+from tests.test_nurbs_cpu import CASES, TOL, block, g, geometry
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need the MI355X (torch.cuda.is_available() is False)")
+    from optiland_pr_amd import _native
+
+    _native.load()
+    return torch
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_sag_normal_distance_vs_reference(torch, case):
+    from optiland_pr_amd.raytrace import RealRays
+
+    geo = geometry(case)
+    x = torch.as_tensor(g(case, "x"), device="cuda")
+    y = torch.as_tensor(g(case, "y"), device="cuda")
+    sag = geo.sag(x, y).cpu().numpy()
+    np.testing.assert_allclose(sag, g(case, "sag"), rtol=0, atol=1e-11)
+    rays = RealRays(x, y, torch.zeros_like(x), torch.zeros_like(x), torch.zeros_like(x),
+                    torch.ones_like(x), 1.0, 0.0)
+    n = np.stack([c.cpu().numpy() for c in geo.surface_normal(rays)])
+    np.testing.assert_allclose(n, g(case, "normal"), rtol=0, atol=1e-12)
+    r = RealRays(g(case, "rx"), g(case, "ry"), g(case, "rz"), g(case, "rL"), g(case, "rM"),
+                 g(case, "rN"), 1.0, 0.0)
+    t = geo.distance(r).cpu().numpy()
+    np.testing.assert_allclose(t, g(case, "distance"), rtol=0, atol=1e-11)
+
+
+def test_reference_test_expectations(torch):
+    """tests/test_nurbs_geometry.py:18-93 on the device: sag(0, 0) = 0, sag(10, 0) = 0.5,
+    normal (0, 0, 1) at the vertex, distance 10 from z = -10 along the axis."""
+    from optiland_pr_amd.raytrace import RealRays
+
+    geo = geometry("fit_conic")
+    s = geo.sag(torch.tensor([0.0, 10.0], device="cuda"),
+                torch.tensor([0.0, 0.0], device="cuda")).cpu().numpy()
+    np.testing.assert_allclose(s, [0.0, 0.5], atol=1e-4)
+    r = RealRays(np.zeros(1), np.zeros(1), np.full(1, -10.0), np.zeros(1), np.zeros(1),
+                 np.ones(1), 1.0, 0.0)
+    n = [float(c.cpu()[0]) for c in geo.surface_normal(r)]
+    np.testing.assert_allclose(n, [0.0, 0.0, 1.0], atol=1e-4)
+    np.testing.assert_allclose(geo.distance(r).cpu().numpy(), [10.0], atol=1e-4)
+
+
+def test_many_points_vs_oracle(torch):
+    """4096 seeded points / rays over the fitted paraboloid's window (restarts included:
+    the oracle and the kernels draw the same fixed restart sequence)."""
+    from oracle import nurbs_np
+    from optiland_pr_amd.raytrace import RealRays
+
+    rng = np.random.default_rng(3)
+    geo = geometry("fit_conic")
+    blk = block("fit_conic")
+    x, y = rng.uniform(-19.5, 19.5, size=(2, 4096))
+    sag = geo.sag(torch.as_tensor(x, device="cuda"),
+                  torch.as_tensor(y, device="cuda")).cpu().numpy()
+    np.testing.assert_allclose(sag, nurbs_np.sag(blk, x, y, TOL, 100), rtol=0, atol=1e-11)
+    n = 4096
+    L, M = rng.uniform(-0.05, 0.05, size=(2, n))
+    N = np.sqrt(1 - L * L - M * M)
+    px, py = rng.uniform(-16, 16, size=(2, n))
+    pz = rng.uniform(-8, -2, n)
+    t = geo.distance(RealRays(px, py, pz, L, M, N, 1.0, 0.0)).cpu().numpy()
+    np.testing.assert_allclose(t, nurbs_np.distance(blk, px, py, pz, L, M, N, TOL, 100),
+                               rtol=0, atol=1e-11)

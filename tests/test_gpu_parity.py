@@ -311,7 +311,7 @@ def test_unknown_geometry_id_fails_loudly(torch):
     lens = CookeTriplet()
     table = lens_for(lens, [0.55]).table
     table.surfaces = table.surfaces.copy()
-    table.surfaces[2]["geometry"] = 12
+    table.surfaces[2]["geometry"] = 13  # (12 is NURBS since ABI v20)
     seg = np.stack([segment_params(lens, 0.0, 1.0, 0)])
     n = 256
     px = torch.linspace(-0.5, 0.5, n, dtype=torch.float64, device="cuda")
@@ -320,7 +320,7 @@ def test_unknown_geometry_id_fails_loudly(torch):
     dl = DeviceLens(table)
     with pytest.raises(RuntimeError, match="ORT_ERR_ARG"):
         trace_pupil(dl, seg, px, py, out, n, n, n)
-    dl.c.geometry_mask = dl.geometry_mask & ~(1 << 12)  # a stale / inconsistent mask
+    dl.c.geometry_mask = dl.geometry_mask & ~(1 << 13)  # a stale / inconsistent mask
     trace_pupil(dl, seg, px, py, out, n, n, n)
     torch.cuda.synchronize()
     assert np.isnan(out.numpy()["x"]).all()  # the closed-form kernel: NaN rays

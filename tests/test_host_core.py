@@ -27,7 +27,7 @@ CLOSED = ("cooke", "dg", "rt", "cooke_aperture", "cooke_shapes", "decentered", "
           "cooke_pih", "finite_pih", "uv_projection", "apod_gaussian", "apod_tukey",
           "cooke_abbe")
 NEWTON = ("rt_asph", "rt_odd", "tma_fringe", "tma_standard", "tma_noll", "freeform",
-          "forbes", "forbes_q2d")
+          "forbes", "forbes_q2d", "nurbs_lens")
 
 
 def _build(tmp_path_factory, name, flags):

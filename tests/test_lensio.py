@@ -33,7 +33,7 @@ def test_round_trip_preserves_lowering(name):
 def test_unsupported_inputs_raise():
     data = optic_to_dict(build_lens("cooke"))
     bad = json.loads(json.dumps(data))
-    bad["surface_group"]["surfaces"][1]["geometry"]["type"] = "NurbsGeometry"
+    bad["surface_group"]["surfaces"][1]["geometry"]["type"] = "BogusGeometry"
     with pytest.raises(ValueError, match="geometry type"):
         optic_from_dict(bad)
     bad = json.loads(json.dumps(data))

@@ -5,7 +5,10 @@ The lens here is built with the native host API (optiland_pr_amd samples + lower
 so this also pins the lowering, the glass table and the paraxial host scalars.
 The oracle evaluates the same NumPy expressions in the same order as the reference, so
 every case -- Newton and Zernike included -- is pinned BIT-EXACT (the GPU kernel is held
-to the stated tolerance where it uses device libm / deferred absorption).
+to the stated tolerance where it uses device libm / deferred absorption). The exception is
+NURBS (nurbs_lens): the reference's own surface points change in the last bits with the
+memory layout of its control-point array (its matmul's BLAS summation order: a fitted net
+is a transposed view, nurbs_geometry.py:871-872), so that case is held to 1e-12 mm.
 """
 
 import numpy as np
@@ -14,6 +17,8 @@ import pytest
 from oracle import trace_np
 from tests._cases import ALL_CASES, FIELDS, native_case
 from tests.conftest import load_golden
+
+LAYOUT_DEPENDENT = ("nurbs_lens",)
 
 def run_oracle(name, meta, record=False):
     lens, table, segs = native_case(name, meta, record=record)
@@ -46,7 +51,10 @@ def test_image_plane(name, golden_index):
     for a in FIELDS:
         got, ref = cat(out, a), g[a]
         np.testing.assert_array_equal(np.isnan(got), np.isnan(ref), err_msg=f"{name}.{a} NaN mask")
-        np.testing.assert_array_equal(got, ref, err_msg=f"{name}.{a}")
+        if name in LAYOUT_DEPENDENT:
+            np.testing.assert_allclose(got, ref, rtol=0, atol=1e-12, err_msg=f"{name}.{a}")
+        else:
+            np.testing.assert_array_equal(got, ref, err_msg=f"{name}.{a}")
 
 
 @pytest.mark.parametrize("name", ALL_CASES)

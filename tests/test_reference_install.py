@@ -110,3 +110,25 @@ def test_torch_optimizer_trajectory_matches_reference(tmp_path, case):
     np.testing.assert_allclose(got["x"], ref["x"], rtol=1e-8, atol=1e-15)
     np.testing.assert_allclose(got["fun"], ref["fun"], rtol=1e-8)
     assert got["losses"][-1] < got["losses"][0]  # the optimiser made progress
+
+
+def test_reference_nurbs_lens_through_install(tmp_path):
+    """The reference's own NURBS lens (a fitted conic in front, an explicit rational net
+    behind) through install(): every trace served by the op's CPU kernel (no fallback), the
+    image planes equal to the reference's own trace within the Newton tolerances (its
+    (u, v) solves stop per call at tol 1e-6, ours per ray)."""
+    from optiland_pr_amd import _native
+
+    _native.load_host()
+    r = subprocess.run([sys.executable, os.path.join(REPO, "tests", "refrun", "nurbs_run.py")],
+                       cwd=str(tmp_path), env=_env(tmp_path), capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["stats"]["cpu"] == 3 and d["stats"]["fallback"] == 0, d["stats"]
+    for ref, got in zip(d["reference"], d["installed"], strict=True):
+        for a in ("x", "y", "z", "opd"):
+            np.testing.assert_allclose(got[a], ref[a], rtol=0, atol=1e-9, err_msg=a)
+        for a in ("L", "M", "N"):
+            np.testing.assert_allclose(got[a], ref[a], rtol=0, atol=1e-11, err_msg=a)
+        np.testing.assert_allclose(got["i"], ref["i"], rtol=1e-12, err_msg="i")
