@@ -549,7 +549,12 @@ int ort_trace_pupil(const ort_lens* lens, const double* px, const double* py,
  *   writes NaN into the gradient: take ORT_VJP_UNROLLED for such a schedule (v19).
  *   Needs n_zern and a device workspace of ort_vjp_workspace_size() bytes, and at most
  *   ORT_VJP_ADJOINT_MAX_SLOTS parameter slots, 3 n_surfaces + n_zern + 1 (v17: the
- *   slots' per-block partial sums live in LDS); beyond that use ORT_VJP_UNROLLED. */
+ *   slots' per-block partial sums live in LDS); beyond that use ORT_VJP_UNROLLED.
+ * Lenses with thin-lens / phase / grating surfaces (interaction_mask beyond
+ * REFRACT_REFLECT): ORT_VJP_UNROLLED only (v20: the forward-mode sweep carries the
+ * interaction models in duals; the adjoint refuses them with ORT_ERR_ARG, as both modes
+ * refuse GRID_SAG / NURBS surfaces). A grating surface's radius / conic take no tangent
+ * (its grating-vector constants are host-formed). */
 #define ORT_VJP_ADJOINT_MAX_SLOTS 512
 enum ort_vjp_mode { ORT_VJP_UNROLLED = 0, ORT_VJP_ADJOINT = 1 };
 typedef struct ort_vjp_params {

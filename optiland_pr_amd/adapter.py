@@ -555,7 +555,8 @@ def _trace_on_mi355x(group, rays, skip):
         fields = [t if _live(t, grad_mode, memo) else t.detach() for t in fields]
         if params or any(t.requires_grad for t in fields):
             try:
-                ops._check_differentiable(dl.table)
+                ops._check_differentiable(dl.table,
+                                          adjoint=any(t.requires_grad for t in fields))
             except NotImplementedError as e:  # no derivative kernels: the reference loop
                 raise Unsupported(str(e)) from e
     start = max(int(skip) - 1, 0)

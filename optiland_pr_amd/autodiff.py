@@ -122,6 +122,8 @@ def vjp_mode(table, sched=None):
     tensor) when known, else None -- then the adjoint runs, and a schedule the device
     raised past ADJ_HIST on such a surface poisons the gradient with NaN rather than
     truncating it (ort_sweep.h). ORT_VJP_MODE=unrolled|adjoint overrides (A/B checks)."""
+    if has_interactions(table):
+        return _abi.VJP_UNROLLED  # thin-lens / phase / grating: forward mode only (vjp_ray)
     env = os.environ.get("ORT_VJP_MODE", "").lower()
     if env in ("unrolled", "adjoint"):
         return _abi.VJP_UNROLLED if env == "unrolled" else _abi.VJP_ADJOINT
@@ -133,6 +135,13 @@ def vjp_mode(table, sched=None):
     if sched is not None and inexact_updates(table, sched) > _abi.ADJ_HIST:
         return _abi.VJP_UNROLLED
     return _abi.VJP_ADJOINT
+
+
+def has_interactions(table):
+    """The lens has thin-lens, phase or grating surfaces: its gradient is the forward-mode
+    VJP's (their interactions are carried in duals by vjp_ray; the adjoint has no reverse
+    for them)."""
+    return bool(table.interaction_mask & ~(1 << _abi.IA_REFRACT_REFLECT))
 
 
 def inexact_surfaces(table):
@@ -200,9 +209,10 @@ def vjp(dlens, seg_dev, px, py, n, seg_len, sched_dev, tables, n_param, cot, gra
     if np.any(dlens.table.surfaces["geometry"] == _abi.GEOM_GRID_SAG):
         raise NotImplementedError("autograd through grid-sag surfaces is not implemented by "
                                   "the trace core (no derivative kernels)")
-    if dlens.table.interaction_mask & ~(1 << _abi.IA_REFRACT_REFLECT):
-        raise NotImplementedError("autograd through thin-lens, phase or grating surfaces is "
-                                  "not implemented by the trace core (no derivative kernels)")
+    mode = vjp_mode(dlens.table) if mode is None else mode
+    if has_interactions(dlens.table) and mode != _abi.VJP_UNROLLED:
+        raise NotImplementedError("thin-lens, phase and grating surfaces are differentiated "
+                                  "by the forward-mode VJP only (ORT_VJP_UNROLLED)")
     lib = _native.load()
     n_seg = seg_dev.numel() // _abi.SEGMENT.itemsize
     batch = _native.ort_batch(n, seg_len, n, n_seg, int(pupil_per_ray), seg_dev.data_ptr())
@@ -211,7 +221,6 @@ def vjp(dlens, seg_dev, px, py, n, seg_len, sched_dev, tables, n_param, cot, gra
                               None if sched_dev is None else sched_dev.data_ptr())
     zp, st, ft = tables[:3]
     need = tables[3] if len(tables) > 3 else None  # ort_vjp_params.slot_need (resident)
-    mode = vjp_mode(dlens.table) if mode is None else mode
     params = _native.ort_vjp_params(int(n_param), int(mode), _ptr(zp).value, _ptr(st).value,
                                     _ptr(ft).value, 0 if zp is None else int(zp.numel()),
                                     int(bool(overwrite)), None, 0, _ptr(need).value)

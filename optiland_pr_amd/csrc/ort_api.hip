@@ -256,7 +256,9 @@ static int vjp_run(const ort_lens* lens, const double* px, const double* py,
   if (rc) return rc;
   if (opt->newton_mode != ORT_NEWTON_SCHEDULE) return ORT_ERR_ARG;
   if (params->zern_param && (feat & ort::KM_ZERN) == 0) return ORT_ERR_ARG;
-  if (feat & F_IA) return ORT_ERR_ARG;  // no derivative kernels for thin-lens / phase / grating
+  // thin-lens / phase / grating surfaces: the forward-mode VJP only (vjp_ray's all-kinds
+  // instantiation carries their interactions in duals; the adjoint has no reverse for them)
+  if ((feat & F_IA) && params->mode != ORT_VJP_UNROLLED) return ORT_ERR_ARG;
   if (lens->geometry_mask & ((1u << ORT_GEOM_GRID_SAG) | (1u << ORT_GEOM_NURBS)))
     return ORT_ERR_ARG;  // nor grid sags / NURBS (no derivative kernels)
   if (resident) {
@@ -267,7 +269,7 @@ static int vjp_run(const ort_lens* lens, const double* px, const double* py,
   }
   const int64_t blocks = (a.n_rays + kBlock - 1) / kBlock;
   if (blocks > 0x7fffffff) return ORT_ERR_ARG;
-  const uint32_t km = feat & F_KM;
+  const uint32_t km = (feat & F_IA) ? 15u : (feat & F_KM);  // (F_IA: every kind, vjp_ray)
   hipStream_t s = (hipStream_t)stream;
   if (params->mode == ORT_VJP_ADJOINT) {
     AdjLayout L;

@@ -472,7 +472,8 @@ int ort_host_trace_sequential_vjp(const ort_lens* lens, const ort_rays* rays_in,
   int rc = fill_args(a, lens, batch, opt, nullptr, nullptr, nullptr, feat);
   if (rc) return rc;
   if (params->zern_param && (feat & ort::KM_ZERN) == 0) return ORT_ERR_ARG;
-  if (feat & F_IA) return ORT_ERR_ARG;  // no derivative code for thin-lens / phase / grating
+  // thin-lens / phase / grating surfaces: the forward-mode VJP only (vjp_ray in duals)
+  if ((feat & F_IA) && params->mode != ORT_VJP_UNROLLED) return ORT_ERR_ARG;
   if (lens->geometry_mask & ((1u << ORT_GEOM_GRID_SAG) | (1u << ORT_GEOM_NURBS)))
     return ORT_ERR_ARG;  // nor grid sags / NURBS (no derivative kernels)
   a.in = *rays_in;
@@ -531,7 +532,7 @@ int ort_host_trace_pupil_vjp(const ort_lens* lens, const double* px, const doubl
   int rc = fill_args(a, lens, batch, opt, nullptr, nullptr, nullptr, feat);
   if (rc) return rc;
   if (params->zern_param && (feat & ort::KM_ZERN) == 0) return ORT_ERR_ARG;
-  if (feat & F_IA) return ORT_ERR_ARG;
+  if ((feat & F_IA) && params->mode != ORT_VJP_UNROLLED) return ORT_ERR_ARG;
   if (lens->geometry_mask & ((1u << ORT_GEOM_GRID_SAG) | (1u << ORT_GEOM_NURBS))) return ORT_ERR_ARG;
   a.px = px;
   a.py = py;

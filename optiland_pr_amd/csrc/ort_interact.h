@@ -11,6 +11,11 @@
 //
 // Parameter blocks (lens.coef at ort_surface.ia_off) are described in
 // include/optiland_rt.h at enum ort_interaction.
+//
+// T = double in the trace kernels; T = Dual<P> in the forward-mode VJP (vjp_ray), whose
+// values are the same operations (a dual's value is its double expression, divisions
+// plain IEEE) -- the derivatives follow every ray-dependent quantity, the parameter
+// blocks, indices and wavelengths are constants.
 
 #pragma once
 
@@ -19,9 +24,10 @@
 namespace ort {
 
 // rays/real_rays.py:503-509: L, M, N divided by sqrt(L**2 + M**2 + N**2)
-ORT_INLINE void normalize_dir(Ray& r) {
-  const double mag = sqrt(r.L * r.L + r.M * r.M + r.N * r.N);
-  const SharedDiv d = shared_div(mag);
+template <class T>
+ORT_INLINE void normalize_dir(RayT<T>& r) {
+  const T mag = sqrt(r.L * r.L + r.M * r.M + r.N * r.N);
+  const auto d = shared_div(mag);
   r.L = sdiv(r.L, d);
   r.M = sdiv(r.M, d);
   r.N = sdiv(r.N, d);
@@ -30,16 +36,17 @@ ORT_INLINE void normalize_dir(Ray& r) {
 // interactions/thin_lens_interaction_model.py:55-113: OPD of the paraxial phase
 // transformation, slopes u' = (n1 u - x / f) / n2 (n2 = -n1 on a mirror), direction
 // (u'x, u'y, 1) left unnormalised (the next propagation normalises it).
-ORT_INLINE void thin_lens(Ray& r, double f, double n1, double n2) {
+template <class T>
+ORT_INLINE void thin_lens(RayT<T>& r, double f, double n1, double n2) {
   r.opd = r.opd - (r.x * r.x + r.y * r.y) / (2.0 * f);
-  const SharedDiv dn = shared_div(r.N);
-  const double ux1 = sdiv(r.L, dn);
-  const double uy1 = sdiv(r.M, dn);
+  const auto dn = shared_div(r.N);
+  const T ux1 = sdiv(r.L, dn);
+  const T uy1 = sdiv(r.M, dn);
   const double inv_n2 = 1.0 / n2;
   const SharedDiv df = shared_div(f);
   r.L = inv_n2 * (n1 * ux1 - sdiv(r.x, df));
   r.M = inv_n2 * (n1 * uy1 - sdiv(r.y, df));
-  r.N = 1.0;
+  r.N = T(1.0);
 }
 
 // x**k for an integer k >= 1, rounded once: NumPy squares exactly for k == 2 and passes
@@ -59,70 +66,78 @@ ORT_INLINE double pow_k(double x, int k) {
   }
   return hi + lo;
 }
+// the dual power: the same value, d(x^k) = k x^(k-1) dx
+template <int P>
+ORT_INLINE Dual<P> pow_k(const Dual<P>& x, int k) {
+  Dual<P> r(pow_k(x.v, k));
+  const double dk = k == 1 ? 1.0 : (double)k * pow_k(x.v, k - 1);
+#pragma unroll
+  for (int q = 0; q < P; ++q) r.d[q] = dk * x.d[q];
+  return r;
+}
 
 // phase/*.py get_phase + get_gradient at (x, y); the z gradient is 0 for every profile
-template <class PD>
-ORT_INLINE void phase_profile(PD p, double x, double y, double& phase, double& gx,
-                              double& gy) {
+template <class PD, class T>
+ORT_INLINE void phase_profile(PD p, const T& x, const T& y, T& phase, T& gx, T& gy) {
   const int kind = (int)p[0];
   if (kind == ORT_PHASE_CONSTANT) {  // constant.py: full_like(x, phase), zero gradient
-    phase = p[2];
-    gx = 0.0;
-    gy = 0.0;
+    phase = T(p[2]);
+    gx = T(0.0);
+    gy = T(0.0);
   } else if (kind == ORT_PHASE_LINEAR) {  // linear_grating.py:60-92
     phase = p[2] * x + p[3] * y;
-    gx = p[2];
-    gy = p[3];
+    gx = T(p[2]);
+    gy = T(p[3]);
   } else {  // radial.py:26-75: phi = sum a_i r2**(i+1), d phi / dr = sum 2 (i+1) a_i r**(2i+1)
     const int n = (int)p[2];
-    const double r2 = x * x + y * y;
-    phase = 0.0;
+    const T r2 = x * x + y * y;
+    phase = T(0.0);
 #pragma unroll 1
     for (int i = 0; i < n; ++i) phase = phase + p[3 + i] * pow_k(r2, i + 1);
-    const double r = sqrt(r2);
-    double dr = 0.0;
+    const T r = sqrt(r2);
+    T dr = T(0.0);
 #pragma unroll 1
     for (int i = 0; i < n; ++i)
       dr = dr + p[3 + i] * 2.0 * (double)(i + 1) * pow_k(r, 2 * (i + 1) - 1);
-    const bool at0 = r == 0.0;
-    const double q = dr / (at0 ? 1.0 : r);
-    gx = at0 ? 0.0 : q * x;
-    gy = at0 ? 0.0 : q * y;
+    const bool at0 = vv(r) == 0.0;
+    const T q = dr / (at0 ? T(1.0) : r);
+    gx = at0 ? T(0.0) : q * x;
+    gy = at0 ? T(0.0) : q * y;
   }
 }
 
 // interactions/phase_interaction_model.py:45-132 (the normal is used as the geometry
 // returns it, not aligned with the ray)
-template <class PD>
-ORT_INLINE void phase_interact(Ray& r, PD p, double nx, double ny, double nz, double n1,
-                               double n2, bool reflective, double w) {
+template <class PD, class T>
+ORT_INLINE void phase_interact(RayT<T>& r, PD p, const T& nx, const T& ny, const T& nz,
+                               double n1, double n2, bool reflective, double w) {
   const double k0 = 6.283185307179586 / w;  // 2 * be.pi / rays.w
-  const double kix = n1 * k0 * r.L;
-  const double kiy = n1 * k0 * r.M;
-  const double kiz = n1 * k0 * r.N;
-  double phase, gx, gy;
+  const T kix = n1 * k0 * r.L;
+  const T kiy = n1 * k0 * r.M;
+  const T kiz = n1 * k0 * r.N;
+  T phase, gx, gy;
   phase_profile(p, r.x, r.y, phase, gx, gy);
   const double gz = 0.0;
-  const double gdn = gx * nx + gy * ny + gz * nz;
-  const double Gx = gx - gdn * nx, Gy = gy - gdn * ny, Gz = gz - gdn * nz;
-  const double kdn = kix * nx + kiy * ny + kiz * nz;
-  const double kx0 = kix - kdn * nx + Gx;
-  const double ky0 = kiy - kdn * ny + Gy;
-  const double kz0 = kiz - kdn * nz + Gz;
-  const double par2 = kx0 * kx0 + ky0 * ky0 + kz0 * kz0;
+  const T gdn = gx * nx + gy * ny + gz * nz;
+  const T Gx = gx - gdn * nx, Gy = gy - gdn * ny, Gz = gz - gdn * nz;
+  const T kdn = kix * nx + kiy * ny + kiz * nz;
+  const T kx0 = kix - kdn * nx + Gx;
+  const T ky0 = kiy - kdn * ny + Gy;
+  const T kz0 = kiz - kdn * nz + Gz;
+  const T par2 = kx0 * kx0 + ky0 * ky0 + kz0 * kz0;
   const double nk = n2 * k0;
-  double rsq = nk * nk - par2;
-  if (rsq < 0.0) {  // TIR / evanescent: rays.clip
-    r.i = 0.0;
-    r.att = 0.0;
+  T rsq = nk * nk - par2;
+  if (vv(rsq) < 0.0) {  // TIR / evanescent: rays.clip
+    r.i = T(0.0);
+    r.att = T(0.0);
   }
-  rsq = (0.0 >= rsq) ? 0.0 : rsq;  // np.maximum(0.0, R_sq): NaN propagates
-  const double alpha = (reflective ? -1.0 : 1.0) * sqrt(rsq);
-  const double kx = kx0 + alpha * nx;
-  const double ky = ky0 + alpha * ny;
-  const double kz = kz0 + alpha * nz;
-  const double mag = sqrt(kx * kx + ky * ky + kz * kz);
-  const SharedDiv dm = shared_div(mag);
+  rsq = (0.0 >= vv(rsq)) ? T(0.0) : rsq;  // np.maximum(0.0, R_sq): NaN propagates
+  const T alpha = (reflective ? -1.0 : 1.0) * sqrt(rsq);
+  const T kx = kx0 + alpha * nx;
+  const T ky = ky0 + alpha * ny;
+  const T kz = kz0 + alpha * nz;
+  const T mag = sqrt(kx * kx + ky * ky + kz * kz);
+  const auto dm = shared_div(mag);
   r.L = sdiv(kx, dm);
   r.M = sdiv(ky, dm);
   r.N = sdiv(kz, dm);
@@ -133,28 +148,28 @@ ORT_INLINE void phase_interact(Ray& r, PD p, double nx, double ny, double nz, do
 // Grating vector at the local hit point: constant for PlaneGrating
 // (plane_grating.py:105-124), from the groove tangent of the conic for
 // StandardGratingGeometry (standard_grating.py:93-146, 224-247; n = the unaligned normal)
-template <class PD>
-ORT_INLINE void grating_vector(PD p, double x, double y, double nx, double ny, double nz,
-                               double& fx, double& fy, double& fz) {
+template <class PD, class T>
+ORT_INLINE void grating_vector(PD p, const T& x, const T& y, const T& nx, const T& ny,
+                               const T& nz, T& fx, T& fy, T& fz) {
   if (p[2] == 0.0) {
-    fx = p[3];
-    fy = p[4];
-    fz = 0.0;
+    fx = T(p[3]);
+    fy = T(p[4]);
+    fz = T(0.0);
     return;
   }
   const double ta = p[3], R2 = p[4], R3 = p[5], kp1 = p[6];
-  const double r2 = x * x + y * y;
-  const double s = sqrt((R2 - kp1 * r2) / R2);
-  const double s1 = s + 1.0;
-  const double dzdx = (x + y * ta) * (2.0 * R2 * s * s1 + kp1 * r2) / (R3 * s * (s1 * s1));
-  const double nt = sqrt(1.0 + ta * ta + dzdx * dzdx);
-  const SharedDiv dt = shared_div(nt);
-  const double tx = sdiv(1.0, dt), ty = sdiv(ta, dt), tz = sdiv(dzdx, dt);
-  const double gx = ny * tz - nz * ty;
-  const double gy = -nx * tz + nz * tx;
-  const double gz = nx * ty - ny * tx;
-  const double mag = sqrt(gx * gx + gy * gy + gz * gz);
-  const SharedDiv dm = shared_div(mag);
+  const T r2 = x * x + y * y;
+  const T s = sqrt((R2 - kp1 * r2) / R2);
+  const T s1 = s + 1.0;
+  const T dzdx = (x + y * ta) * (2.0 * R2 * s * s1 + kp1 * r2) / (R3 * s * (s1 * s1));
+  const T nt = sqrt(1.0 + ta * ta + dzdx * dzdx);
+  const auto dt = shared_div(nt);
+  const T tx = sdiv(1.0, dt), ty = sdiv(T(ta), dt), tz = sdiv(dzdx, dt);
+  const T gx = ny * tz - nz * ty;
+  const T gy = -nx * tz + nz * tx;
+  const T gz = nx * ty - ny * tx;
+  const T mag = sqrt(gx * gx + gy * gy + gz * gz);
+  const auto dm = shared_div(mag);
   fx = -sdiv(gx, dm);
   fy = -sdiv(gy, dm);
   fz = -sdiv(gz, dm);
@@ -163,20 +178,21 @@ ORT_INLINE void grating_vector(PD p, double x, double y, double nx, double ny, d
 // real_rays.py:183-498 (gratingdiffract) as called by diffractive_model.py:28-61:
 // d = period / sqrt(fx**2 + fy**2), the normal aligned with the ray, the closed-form
 // diffracted direction (every term in the reference's order), then normalize().
-template <class PD>
-ORT_INLINE void diffract(Ray& r, PD p, double nx, double ny, double nz, double n1, double n2,
+template <class PD, class T>
+ORT_INLINE void diffract(RayT<T>& r, PD p, T nx, T ny, T nz, double n1, double n2,
                          bool reflective, double w) {
-  double fx, fy, fz;
+  T fx, fy, fz;
   grating_vector(p, r.x, r.y, nx, ny, nz, fx, fy, fz);
   const double m = p[0];
-  const double d = p[1] / sqrt(fx * fx + fy * fy);
-  const double L0 = r.L, M0 = r.M, N0 = r.N;
+  const T d = p[1] / sqrt(fx * fx + fy * fy);
+  const T L0 = r.L, M0 = r.M, N0 = r.N;
   align_normal(r, nx, ny, nz);
   const double n2c = reflective ? n2 * -1.0 : n2;
-  const double d2 = d * d, n12 = n1 * n1, m2 = m * m, w2 = w * w;
-  const double nx2 = nx * nx, ny2 = ny * ny, nz2 = nz * nz;
+  const double n12 = n1 * n1, m2 = m * m, w2 = w * w;
+  const T d2 = d * d;
+  const T nx2 = nx * nx, ny2 = ny * ny, nz2 = nz * nz;
   // clang-format off
-  const double D =
+  const T D =
       -(L0 * L0) * d2 * n12 * ny2
       - L0 * L0 * d2 * n12 * nz2
       + 2.0 * L0 * M0 * d2 * n12 * nx * ny
@@ -211,17 +227,17 @@ ORT_INLINE void diffract(Ray& r, PD p, double nx, double ny, double nz, double n
       - fz * fz * m2 * nx2 * w2
       - fz * fz * m2 * ny2 * w2;
   // clang-format on
-  const double sD = sqrt(D);
-  const double AL = L0 * d * n1 * ny2 + L0 * d * n1 * nz2 - M0 * d * n1 * nx * ny -
+  const T sD = sqrt(D);
+  const T AL = L0 * d * n1 * ny2 + L0 * d * n1 * nz2 - M0 * d * n1 * nx * ny -
                     N0 * d * n1 * nx * nz + fx * m * ny2 * w + fx * m * nz2 * w -
                     fy * m * nx * ny * w - fz * m * nx * nz * w;
-  const double AM = -L0 * d * n1 * nx * ny + M0 * d * n1 * nx2 + M0 * d * n1 * nz2 -
+  const T AM = -L0 * d * n1 * nx * ny + M0 * d * n1 * nx2 + M0 * d * n1 * nz2 -
                     N0 * d * n1 * ny * nz - fx * m * nx * ny * w + fy * m * nx2 * w +
                     fy * m * nz2 * w - fz * m * ny * nz * w;
-  const double PN = L0 * d * n1 * nx * nz + M0 * d * n1 * ny * nz - N0 * d * n1 * nx2 -
+  const T PN = L0 * d * n1 * nx * nz + M0 * d * n1 * ny * nz - N0 * d * n1 * nx2 -
                     N0 * d * n1 * ny2 + fx * m * nx * nz * w + fy * m * ny * nz * w -
                     fz * m * nx2 * w - fz * m * ny2 * w;
-  const SharedDiv dd = shared_div(d * n2c);
+  const auto dd = shared_div(d * n2c);
   if (reflective) {
     r.L = sdiv(AL - nx * sD, dd);
     r.M = sdiv(AM - ny * sD, dd);

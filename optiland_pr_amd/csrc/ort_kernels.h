@@ -378,22 +378,6 @@ __device__ inline __attribute__((always_inline)) double newton_distance(const KA
   const int U = sched ? sched[group * a.n_surf + si] : max_iter;
   ConvBits mask;
   int last_bad = -1;
-  // Wave-level statistics (#ifndef ORT_LANE_STATS, A/B builds): a group-uniform wave whose
-  // stop indices fall in the mask window (conv_base 0, U < 128) forms the wave's AND of
-  // the convergence bits and its last non-converged index from one ballot per evaluation
-  // -- over the lanes reporting at that index, i.e. not yet out of range on the fast
-  // pass: their values up to there are the exact path's, which reports the same bits for
-  // them again if they turn bad later -- instead of per-lane 64-bit masks reduced at the
-  // end (report_newton). The bits, the index and the atomics are the same.
-#ifndef ORT_LANE_STATS
-  const bool wstat = a.stats && group_uniform && a.conv_base == 0 &&
-                     __builtin_amdgcn_readfirstlane(U) < 128;
-#else
-  constexpr bool wstat = false;
-#endif
-  uint64_t ws0 = 0, ws1 = 0;  // (wave-uniform)
-  int wlast = -1;
-  bool wany = false;
   // Every evaluation is one call site (the kernel's code size is its hot loop): at j < U
   // sag + the update's slopes at P(t) (kSlope) and the update; at j = U (the stop test)
   // the same evaluation, the interaction's unit normal formed from those slopes -- for the
@@ -408,7 +392,6 @@ __device__ inline __attribute__((always_inline)) double newton_distance(const KA
   for (int j = 0;; ++j) {
     const bool lane_on = active && j <= U;
     if (!__any(lane_on)) break;
-    bool rep = false, miss = false;  // wstat: this lane reports index j / did not converge
     if (lane_on) {
       bool rerr = false;
       double nx, ny, nz;
@@ -419,13 +402,8 @@ __device__ inline __attribute__((always_inline)) double newton_distance(const KA
       // loop broke there (U < max_iter)
       if (rerr && (j < U || U < max_iter) && !(FAST && bad)) range_bits |= range_bit(s);
       const bool conv = fabs(f) < tol;  // NaN never converges (np.max propagates NaN)
-      if (wstat) {
-        rep = !(FAST && bad);
-        miss = rep && !conv;
-      } else {
-        if (conv) mask.set(j, a.conv_base);
-        if (!conv) last_bad = j;
-      }
+      if (conv) mask.set(j, a.conv_base);
+      if (!conv) last_bad = j;
       if (upd) {
         if constexpr ((FEAT & F_TAPE) != 0) {
           // the iterate before the m-th last update, m = U - 1 - j, straight into its tape
@@ -457,28 +435,8 @@ __device__ inline __attribute__((always_inline)) double newton_distance(const KA
         nnz = nz;
       }
     }
-    if (wstat && __ballot(rep) != 0) {  // (uniform control flow: the state stays scalar)
-      wany = true;
-      if (__ballot(miss) == 0) {
-        if (j < 64)
-          ws0 |= 1ull << j;
-        else
-          ws1 |= 1ull << (j - 64);
-      } else {
-        wlast = j;
-      }
-    }
   }
-  if (wstat) {
-    if (wany && (threadIdx.x & 63) == 0) {
-      ort_newton_stat* st = &a.stats[group * a.n_surf + si];
-      if (ws0 != ~0ull) and_if_changes(&st->conv_mask[0], ws0);
-      if (ws1 != ~0ull) and_if_changes(&st->conv_mask[1], ws1);
-      if (wlast >= 0) max_if_changes(&st->last_bad, wlast);
-    }
-  } else {
-    report_newton(a, si, active && !(FAST && bad), group, group_uniform, mask, last_bad, U);
-  }
+  report_newton(a, si, active && !(FAST && bad), group, group_uniform, mask, last_bad, U);
   if constexpr ((FEAT & F_TAPE) != 0) {
     // the iterate rows no update fills (m >= U) get the root: every tape row is written
     // (the tape is the trace op's output; the adjoint reads only m < min(U, kHist))

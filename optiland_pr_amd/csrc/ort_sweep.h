@@ -1166,6 +1166,7 @@ ORT_INLINE void vjp_ray(const KArgs& a, const JArgs& j, int64_t rid, bool active
   const int64_t group = r_ld / a.group_len;
   const ort::ZSeed zs{j.zparam, j.p0};
   const int64_t ts = (int64_t)a.n_surf * 3;
+  bool unnorm = false;  // a thin lens left the direction unnormalised (F_IA lenses)
 #pragma unroll
   for (int k = 0; k < P; ++k) acc[k] = 0.0;
 
@@ -1199,8 +1200,47 @@ ORT_INLINE void vjp_ray(const KArgs& a, const JArgs& j, int64_t rid, bool active
         }
       }
     }
-    ort::finish_surface<KM>(r, s, R, K, cst(a.coef), cst(a.zern), zs, t, o.n_pre, o.u,
-                            o.alpha_pre);
+    bool done = false;
+    if constexpr ((KM & 15u) == 15u) {
+      // thin-lens / phase / grating surfaces (F_IA lenses take the all-kinds kernels):
+      // trace_kernel<F_IA>'s surface step in duals -- propagate, the normalisation a thin
+      // lens left pending (homogeneous.py:55-57), OPD, clipping, the interaction model
+      if (s.interaction != ORT_IA_REFRACT_REFLECT || unnorm) {
+        ort::propagate(r, t, o.alpha_pre);
+        if (unnorm) {
+          ort::normalize_dir(r);
+          unnorm = false;
+        }
+        ort::add_opd(r, t, o.n_pre);
+        if (s.flags & ORT_SURF_APERTURE) ort::clip_radial(r, s.ap_rmax2, s.ap_rmin2);
+        if (s.flags & ORT_SURF_APERTURE_PROG) ort::clip_program(r, cst(a.coef) + s.ap_off, s.ap_len);
+        const bool refl = (s.flags & ORT_SURF_REFLECTIVE) != 0;
+        const PD ip = cst(a.coef) + s.ia_off;
+        if (s.interaction == ORT_IA_THIN_LENS) {
+          ort::thin_lens(r, ip[0], o.n_pre, refl ? -o.n_pre : o.n_post);
+          unnorm = true;
+        } else {
+          D nx, ny, nz;
+          ort::surface_normal<KM>(s, R, K, cst(a.coef), cst(a.zern), zs, r, nx, ny, nz);
+          if (s.interaction == ORT_IA_REFRACT_REFLECT) {
+            if (refl)
+              ort::reflect(r, nx, ny, nz);
+            else
+              ort::refract(r, nx, ny, nz, o.u);
+          } else {
+            const double w = a.w ? wl : (a.n_lambda == 1 ? cst(a.lambdas)[0] : a.lambdas[lam]);
+            if (s.interaction == ORT_IA_PHASE)
+              ort::phase_interact(r, ip, nx, ny, nz, o.n_pre, refl ? o.n_pre : o.n_post, refl, w);
+            else
+              ort::diffract(r, ip, nx, ny, nz, o.n_pre, o.n_post, refl, w);
+          }
+        }
+        done = true;
+      }
+    }
+    if (!done)
+      ort::finish_surface<KM>(r, s, R, K, cst(a.coef), cst(a.zern), zs, t, o.n_pre, o.u,
+                              o.alpha_pre);
     for (int c = 0; c < s.n_cs_glob; ++c) ort::apply_cs_op(r, cst(a.cs)[s.cs_glob_off + c]);
     r.x = r.x + s.cs_t[0];
     r.y = r.y + s.cs_t[1];
@@ -1217,10 +1257,14 @@ ORT_INLINE void vjp_ray(const KArgs& a, const JArgs& j, int64_t rid, bool active
       cot_acc(acc, rc + 7 * a.n_rays, rid, r.opd);
     }
   }
-  if (a.final_mat >= 0)
+  if (a.final_mat >= 0) {
     ort::propagate(r, seeded<P>(a.final_thickness, j.tan_final, 1, 0, j),
                    a.w ? ort::absorption_alpha(ort::material_k(cst(a.mats)[a.final_mat], a.coef, wl), wl)
                        : tab(a.alpha_tab, a.n_lambda, a.n_mat, lam, a.final_mat));
+    if constexpr ((KM & 15u) == 15u) {
+      if (unnorm) ort::normalize_dir(r);
+    }
+  }
 
   if (active) {
     cot_acc(acc, j.cot.x, rid, r.x);

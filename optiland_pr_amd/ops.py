@@ -138,6 +138,11 @@ def tangent_tables(table, pairs, params):
                          _abi.GEOM_NURBS):
                     raise NotImplementedError(f"surface {si}: {kind} of this geometry is not a "
                                               "differentiable parameter of the trace core")
+                if int(row["interaction"]) == _abi.IA_DIFFRACTIVE:
+                    # the grating vector's groove-tangent constants are formed from them on
+                    # the host (standard_grating.py:93-146): no tangent reaches them
+                    raise NotImplementedError(f"surface {si}: {kind} of a grating surface is not "
+                                              "a differentiable parameter of the trace core")
                 surf[off, si, 0 if kind == "radius" else 1] = 1.0
             elif kind == "vertex":
                 surf[off, si, 2] = 1.0
@@ -214,16 +219,20 @@ def tape_doubles(dl, n):
     return tape_rows(dl.table) * int(n)
 
 
-def _check_differentiable(table):
+def _check_differentiable(table, adjoint=False):
+    """Refuse what no derivative kernel covers. adjoint: the reverse-mode pass is needed
+    (input-ray cotangents), which has no reverse for thin-lens / phase / grating surfaces
+    (their parameter gradients come from the forward-mode VJP, autodiff.vjp_mode)."""
     if np.any(table.surfaces["geometry"] == _abi.GEOM_GRID_SAG):
         raise NotImplementedError("autograd through grid-sag surfaces is not implemented by "
                                   "the trace core (no derivative kernels)")
     if np.any(table.surfaces["geometry"] == _abi.GEOM_NURBS):
         raise NotImplementedError("autograd through NURBS surfaces is not implemented by "
                                   "the trace core (no derivative kernels)")
-    if table.interaction_mask & ~(1 << _abi.IA_REFRACT_REFLECT):
-        raise NotImplementedError("autograd through thin-lens, phase or grating surfaces is "
-                                  "not implemented by the trace core (no derivative kernels)")
+    if adjoint and table.interaction_mask & ~(1 << _abi.IA_REFRACT_REFLECT):
+        raise NotImplementedError("input-ray gradients through thin-lens, phase or grating "
+                                  "surfaces are not implemented by the trace core (the "
+                                  "forward-mode VJP carries parameter tangents only)")
 
 
 _WORKSPACE: dict = {}
@@ -452,7 +461,7 @@ def _seq_backward(ctx, *grads):
     nothing = ([None] * ctx.n_lens, None, None, None)
     if not (want_rays or want_params) or (all(c is None for c in cot) and rec_cot is None):
         return (*nothing, none_rays, None, none_params, none_spec, None, None)
-    _check_differentiable(table)
+    _check_differentiable(table, adjoint=want_rays)
     params_like = [torch.empty(s, dtype=d, device="meta") for s, d, _ in ctx.shapes]
     zp, st, ft, n_param = tangent_tables(table, ctx.pairs, params_like)
     from .autodiff import schedule_for_mode, vjp_mode

@@ -6,6 +6,10 @@ Test infrastructure only, run in the build container (never on the GPU box):
     PYTHONPATH=tests/golden/shims:/root/reference PYTHONDONTWRITEBYTECODE=1 \
         python tests/golden/gen_autograd_golden.py
 
+With --ia: tests/golden/autograd_ia.npz, d rms / d (radius, thickness) through the
+thin-lens, phase and grating surfaces of gen_golden.py's paraxial_lens, phase_plate and
+grating_curved (ia_params).
+
 Writes tests/golden/autograd_tma.npz (fringe) and autograd_tma_standard.npz /
 autograd_tma_noll.npz (the same loss and weights with the standard and noll schemes,
 whose Newton slope omits the normalisation constant, zernike.py:162-231; SURVEY 8d.5's
@@ -141,6 +145,46 @@ def shape_params():
     np.savez_compressed(os.path.join(HERE, "autograd_cooke.npz"), **out)
 
 
+# lenses with thin-lens / phase / grating surfaces (gen_golden.py builders): radius leaves
+# of their refractive (or grating) surfaces and the thickness after surface 1, rms spot
+# size at field (0, 1), uniform 16 -- the gradient flows through the interaction models
+# (thin_lens_interaction_model.py:55-113, phase_interaction_model.py:45-132,
+# diffractive_model.py:28-61)
+IA_CASES = {
+    "paraxial_lens": ((2, 3), 0.55),
+    "phase_plate": ((2, 3), 0.55),
+    "grating_curved": ((), 0.587),  # (a grating's own radius: not a core parameter)
+}
+
+
+def ia_params():
+    """d rms / d (radii, thickness 1) through thin-lens, phase and grating surfaces
+    (autograd_ia.npz)."""
+    be.set_backend("torch")
+    be.set_precision("float64")
+    builders = {"paraxial_lens": gen_golden.paraxial_lens, "phase_plate": gen_golden.phase_plate,
+                "grating_curved": lambda: gen_golden.grating("curved")}
+    out = {}
+    for name, (rsurf, wl) in IA_CASES.items():
+        lens = builders[name]()
+        leaves = []
+        for si in rsurf:
+            t = torch.tensor(float(lens.surface_group.surfaces[si].geometry.radius),
+                             dtype=torch.float64, requires_grad=True)
+            lens.set_radius(t, si)
+            leaves.append(t)
+        t = torch.tensor(float(lens.surface_group.surfaces[1].thickness), dtype=torch.float64,
+                         requires_grad=True)
+        lens.set_thickness(t, 1)
+        leaves.append(t)
+        rms = RayOperand.rms_spot_size(lens, -1, 0.0, 1.0, 16, wl, "uniform")
+        rms.backward()
+        out[f"{name}_value"] = np.array(float(rms))
+        out[f"{name}_grad"] = np.array([float(v.grad) for v in leaves])
+        print(name, float(rms), out[f"{name}_grad"])
+    np.savez_compressed(os.path.join(HERE, "autograd_ia.npz"), **out)
+
+
 def full_size(scheme="fringe"):
     """Config 5 at its own size (VERDICT r02 item 6 for config 5): the TMA loss
     rms_spot_size(optic, -1, 0, 1, 1M, 0.587, RandomDistribution(seed=0)) -- the bench's
@@ -174,6 +218,9 @@ def full_size(scheme="fringe"):
 
 
 if __name__ == "__main__":
+    if "--ia" in sys.argv:  # autograd_ia.npz only
+        ia_params()
+        sys.exit(0)
     schemes = ("fringe", "standard", "noll")
     if "--scheme" in sys.argv:
         schemes = (sys.argv[sys.argv.index("--scheme") + 1],)

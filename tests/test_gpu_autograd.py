@@ -349,3 +349,43 @@ def test_fused_rms_matches_unfused(torch, device, monkeypatch):
     assert res[True][0] == pytest.approx(res[False][0], rel=1e-13)
     scale = np.max(np.abs(res[False][1]))
     np.testing.assert_allclose(res[True][1], res[False][1], rtol=1e-10, atol=1e-12 * scale)
+
+
+# gen_autograd_golden.py IA_CASES: radius leaves (surfaces) and the wavelength per lens
+IA_CASES = {"paraxial_lens": ((2, 3), 0.55), "phase_plate": ((2, 3), 0.55),
+            "grating_curved": ((), 0.587)}
+
+
+@pytest.mark.parametrize("name", sorted(IA_CASES))
+def test_gradients_through_interaction_models(torch, name):
+    """d rms / d (radii, thickness after surface 1) through thin-lens, phase and grating
+    surfaces vs the reference's torch autograd (autograd_ia.npz, gen_autograd_golden.py
+    --ia): the forward-mode VJP carries the interaction models in duals (vjp_ray; the
+    adjoint has no reverse for them, autodiff.vjp_mode)."""
+    from optiland_pr_amd import _abi, autodiff
+    from optiland_pr_amd.operands import RayOperand
+    from tests._cases import build_lens
+    from tests.conftest import load_golden
+
+    rsurf, wl = IA_CASES[name]
+    g = load_golden("autograd_ia")
+    lens = build_lens(name)
+    leaves = []
+    for si in rsurf:
+        t = torch.tensor(float(lens.surface_group.surfaces[si].geometry.radius),
+                         dtype=torch.float64, requires_grad=True)
+        lens.set_radius(t, si)
+        leaves.append(t)
+    t = torch.tensor(float(lens.surface_group.surfaces[1].thickness), dtype=torch.float64,
+                     requires_grad=True)
+    lens.set_thickness(t, 1)
+    leaves.append(t)
+    loss = RayOperand.rms_spot_size(lens, -1, 0.0, 1.0, 16, wl, "uniform")
+    np.testing.assert_allclose(float(loss.detach()), float(g[f"{name}_value"]), rtol=1e-12)
+    loss.backward()
+    got = np.array([float(v.grad) for v in leaves])
+    np.testing.assert_allclose(got, g[f"{name}_grad"], rtol=1e-9, atol=1e-13)
+    from optiland_pr_amd.lowering import lower_surface_group
+
+    table = lower_surface_group(lens.surface_group, [wl])
+    assert autodiff.vjp_mode(table) == _abi.VJP_UNROLLED

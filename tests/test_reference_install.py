@@ -132,3 +132,26 @@ def test_reference_nurbs_lens_through_install(tmp_path):
         for a in ("L", "M", "N"):
             np.testing.assert_allclose(got[a], ref[a], rtol=0, atol=1e-11, err_msg=a)
         np.testing.assert_allclose(got["i"], ref["i"], rtol=1e-12, err_msg="i")
+
+
+def test_reference_gradients_through_interactions(tmp_path):
+    """d rms / d (radius, thickness) of the reference's thin-lens, phase-plate and grating
+    lenses with install() active: every trace served by the op's CPU kernel, the backward
+    by the host build's forward-mode VJP (the interaction models in duals), against the
+    uninstalled reference's torch autograd (tests/golden/autograd_ia.npz)."""
+    from optiland_pr_amd import _native
+    from tests.conftest import load_golden
+
+    _native.load_host()
+    r = subprocess.run([sys.executable, os.path.join(REPO, "tests", "refrun", "ia_grad_run.py")],
+                       cwd=str(tmp_path), env=_env(tmp_path), capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["stats"]["fallback"] == 0 and d["stats"]["cpu"] >= 3, d["stats"]
+    g = load_golden("autograd_ia")
+    for name, v in d["cases"].items():
+        np.testing.assert_allclose(v["value"], float(g[f"{name}_value"]), rtol=1e-12,
+                                   err_msg=name)
+        np.testing.assert_allclose(v["grad"], g[f"{name}_grad"], rtol=1e-9, atol=1e-13,
+                                   err_msg=name)
