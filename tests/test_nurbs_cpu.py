@@ -183,3 +183,62 @@ def test_reference_geometry_converts_through_the_adapter():
     assert isinstance(nat, NurbsGeometry)
     assert nat.lower_params()[5] == nurbs.lowered_block(ref.P, ref.W, ref.p, ref.q, ref.U,
                                                         ref.V)
+
+
+@pytest.fixture(scope="module")
+def nurbs_exe(tmp_path_factory):
+    import shutil
+    import subprocess
+
+    if not shutil.which("g++"):
+        pytest.skip("g++ not available")
+    src = os.path.join(HERE, "native", "nurbs_main.cpp")
+    out = tmp_path_factory.mktemp("nurbs") / "nurbs_main"
+    subprocess.run(["g++", "-std=c++17", "-O2", "-ffp-contract=off", "-o", str(out), src],
+                   check=True)
+    return str(out)
+
+
+def _net(p, q, seed):
+    rng = np.random.default_rng(seed)
+    nu, nv = p + 3, q + 4
+    X, Y = np.meshgrid(np.linspace(-6, 6, nu), np.linspace(-5, 5, nv), indexing="ij")
+    Z = (X**2 + Y**2) / 100.0 + 0.003 * X * Y + rng.uniform(-0.02, 0.02, X.shape)
+    W = rng.uniform(0.8, 1.2, X.shape)
+
+    def knots(n, d):
+        inner = np.sort(rng.uniform(0.1, 0.9, n - d - 1))
+        return np.concatenate([np.zeros(d + 1), inner, np.ones(d + 1)])
+
+    return np.stack([X, Y, Z]), W, knots(nu, p), knots(nv, q), rng
+
+
+@pytest.mark.parametrize("pq", [(1, 1), (1, 2), (2, 2), (3, 2), (4, 3), (5, 5), (5, 1)])
+def test_kernel_solves_match_oracle_every_degree(nurbs_exe, pq):
+    """ort_nurbs.h compiled for the host (the code the kernels inline): sag, normal and
+    distance on nets of degrees 1-5 against the oracle (global stop rule; the kernel code
+    stops per ray), plus the golden nets."""
+    import subprocess
+
+    from oracle import nurbs_np
+
+    p, q = pq
+    P, W, U, V, rng = _net(p, q, 10 * p + q)
+    B = np.asarray(nurbs.lowered_block(P, W, p, q, U, V))
+    n = 256
+    x, y = rng.uniform(-4.5, 4.5, size=(2, n))
+    L, M = rng.uniform(-0.05, 0.05, size=(2, n))
+    N = np.sqrt(1 - L * L - M * M)
+    px, py = rng.uniform(-4, 4, size=(2, n))
+    pz = rng.uniform(-6, -2, n)
+    inp = b"".join([np.int32(B.size).tobytes(), B.tobytes(), np.float64(TOL).tobytes(),
+                    np.int32(100).tobytes(), np.int32(n).tobytes(), x.tobytes(), y.tobytes(),
+                    np.concatenate([px, py, pz, L, M, N]).tobytes()])
+    r = subprocess.run([nurbs_exe], input=inp, capture_output=True, check=True)
+    out = np.frombuffer(r.stdout, dtype=np.float64).reshape(5, n)
+    blk = nurbs_np.unpack(B)
+    np.testing.assert_allclose(out[0], nurbs_np.sag(blk, x, y, TOL, 100), rtol=0, atol=1e-11)
+    np.testing.assert_allclose(out[1:4], np.stack(nurbs_np.surface_normal(blk, x, y, TOL, 100)),
+                               rtol=0, atol=1e-12)
+    np.testing.assert_allclose(out[4], nurbs_np.distance(blk, px, py, pz, L, M, N, TOL, 100),
+                               rtol=0, atol=1e-11)
