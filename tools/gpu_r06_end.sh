@@ -14,4 +14,6 @@ bash tools/bench_configs.sh prof || exit $?
 run r06e_c5_standard 400 python3 bench.py --config 5 --steps 100 --warmup 5 --zernike-scheme standard
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
 run r06e_prof_c2 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r06e_prof_c2 -o run -- python3 bench.py --no-cpu --steps 50 --warmup 5
+cd "$(dirname "$0")/.." 2>/dev/null || true
+AB_ARGS="--config 3 --steps 10 --warmup 2" run r06e_ab_slopemax 900 bash tools/ab.sh slopemax.so ../liboptiland_rt.so
 echo END_OK
