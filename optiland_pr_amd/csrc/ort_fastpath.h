@@ -393,9 +393,9 @@ ORT_INLINE bool lens_range(double R) { return ::fabs(R) <= 0x1p149; }
 // takes the exact path, which forms the reference's expression from the unit normal)
 ORT_INLINE void slope_out(double dfdx, double dfdy, double& nx, double& ny, double& nz,
                           bool& bad) {
-#ifndef ORT_SLOPE_NORM_CHK  // |dfdx|, |dfdy| < 7e13 implies the sum < 9.8e27 + 1 < 1e28:
-  // the same guarantee as the norm test (A/B builds), two compares instead of three fp64
-  // operations and one (round 6: profiles/r06_ab_slopemax.log)
+#ifdef ORT_SLOPE_MAXCHK  // (A/B builds) |dfdx|, |dfdy| < 7e13 implies the sum < 9.8e27 + 1
+  // < 1e28: the same guarantee in two compares -- no measurable gain on the MI355X
+  // (profiles/r06_ab_slopemax.log, r06_ab_c3_slope_opk.log)
   ORT_CHK(bad, !(::fabs(dfdx) < 7e13 && ::fabs(dfdy) < 7e13));
 #else
   ORT_CHK(bad, !(dfdx * dfdx + dfdy * dfdy + 1.0 < 1e28));
@@ -429,8 +429,7 @@ ORT_INLINE double sagnorm_even(double x, double y, const ort_surface& s, PD C,
   const double r2 = x * x + y * y;
   const double a = ORT_ONE_PLUS_K(s) * r2;  // (1 + k) r2: +-0 at the vertex
   const SharedDiv rr = shared_div_pos(ORT_R_SQ(s));
-  // (a lens constant 1 + k == 1 makes a == r2 to the bit: its test is r2's, below)
-  if (ORT_ONE_PLUS_K(s) != 1.0) ORT_CHK(bad, !num_ok0(a));
+  ORT_CHK(bad, !num_ok0(a));
   const double q = sqrt(1.0 - quot_pos(a, rr), bad);
   const SharedDiv dz = shared_div_pos(aR * (1.0 + q));
   ORT_CHK(bad, !num_ok0(r2));
@@ -468,7 +467,7 @@ ORT_INLINE double sagnorm_odd(double x, double y, const ort_surface& s, PD C,
   const double r = sqrt(r2, bad);  // the vertex itself (r2 = 0) takes the exact path
   const double a = ORT_ONE_PLUS_K(s) * r2;
   const SharedDiv rr = shared_div_pos(ORT_R_SQ(s));
-  if (ORT_ONE_PLUS_K(s) != 1.0) ORT_CHK(bad, !num_ok0(a));  // (1 + k == 1: a == r2)
+  ORT_CHK(bad, !num_ok0(a));
   const double q = sqrt(1.0 - quot_pos(a, rr), bad);
   const SharedDiv dz = shared_div_pos(aR * (1.0 + q));
   ORT_CHK(bad, !num_ok0(r2));

@@ -936,6 +936,7 @@ MIXED_W_CASES = {  # name -> (builder, field (Hx, Hy), pupil n, wavelength range
     "grating_curved": (lambda: grating("curved"), (0.2, 0.8), 20, (0.45, 0.70)),
     "grating_reflective": (lambda: grating("reflective"), (0.2, 0.8), 20, (0.45, 0.70)),
     "cooke_abbe": (cooke_abbe, (0.0, 0.7), 24, (0.42, 0.74)),
+    "nurbs_lens": (nurbs_lens, (0.3, 0.6), 20, (0.45, 0.70)),
 }
 
 

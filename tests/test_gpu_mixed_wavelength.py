@@ -72,7 +72,8 @@ def test_device_dispersion_matches_reference(torch, golden):
 
 
 @pytest.mark.parametrize("name", ["cooke", "dg", "freeform", "paraxial_lens", "phase_plate",
-                                  "grating_curved", "grating_reflective", "cooke_abbe"])
+                                  "grating_curved", "grating_reflective", "cooke_abbe",
+                                  "nurbs_lens"])
 def test_mixed_wavelength_surface_group_trace(torch, golden, name):
     from optiland_pr_amd.raytrace import RealRays
 
