@@ -119,8 +119,12 @@ ORT_INLINE void nurbs_basis(const double* K, int p, int k, double u, double B[kN
 // sums, then S = A / w, S_u = (A_u - w_u S) / w, S_v = (A_v - w_v S) / w)
 ORT_INLINE void nurbs_eval(const NurbsView& g, double u, double v, bool want_d, double S[3],
                            double Su[3], double Sv[3]) {
-  const int ku = nurbs_span(g.U, g.p, g.nu, u);
-  const int kv = nurbs_span(g.V, g.q, g.nv, v);
+  // (a block outside the lowered range -- degrees 1 .. kNurbsMaxDeg, at least p + 1 control
+  // points per direction -- evaluates to NaN rather than past its window)
+  const bool shape_ok = g.p >= 1 && g.p <= kNurbsMaxDeg && g.q >= 1 && g.q <= kNurbsMaxDeg &&
+                        g.nu > g.p && g.nv > g.q;
+  const int ku = shape_ok ? nurbs_span(g.U, g.p, g.nu, u) : -1;
+  const int kv = shape_ok ? nurbs_span(g.V, g.q, g.nv, v) : -1;
   if (ku < 0 || kv < 0) {
     for (int c = 0; c < 3; ++c) S[c] = Su[c] = Sv[c] = __builtin_nan("");
     return;

@@ -85,6 +85,8 @@ def geometry_from_dict(d):
                           d.get("v_degree"), d.get("u_knots"), d.get("v_knots"),
                           tol=_f(d.get("tol"), 1e-10), max_iter=int(d.get("max_iter", 100)))
         g.is_fitted = bool(d.get("is_fitted", False))
+        if "P_size_u" in d:  # the fit grid (fit_surface refits on it)
+            g.P_size_u, g.P_size_v = int(d["P_size_u"]), int(d["P_size_v"])
         return g
     if t == "GridSagGeometry":  # grid_sag.py:155-180
         return GridSagGeometry(cs, d["x_coordinates"], d["y_coordinates"], d["sag_values"],
@@ -180,7 +182,8 @@ def geometry_to_dict(g):
                  weights=np.asarray(g.W).tolist() if net else None,
                  u_degree=int(g.p) if net else None, v_degree=int(g.q) if net else None,
                  u_knots=np.asarray(g.U).tolist() if net else None,
-                 v_knots=np.asarray(g.V).tolist() if net else None)
+                 v_knots=np.asarray(g.V).tolist() if net else None,
+                 P_size_u=int(g.P_size_u), P_size_v=int(g.P_size_v))
         return d
     if isinstance(g, GridSagGeometry):
         d.update(x_coordinates=g.x_grid.tolist(), y_coordinates=g.y_grid.tolist(),

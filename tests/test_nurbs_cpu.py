@@ -242,3 +242,40 @@ def test_kernel_solves_match_oracle_every_degree(nurbs_exe, pq):
                                rtol=0, atol=1e-12)
     np.testing.assert_allclose(out[4], nurbs_np.distance(blk, px, py, pz, L, M, N, TOL, 100),
                                rtol=0, atol=1e-11)
+
+
+def test_kernel_solves_refuse_out_of_range_blocks(nurbs_exe):
+    """A hand-made block outside the lowered range (degree 6, or fewer control points than
+    degree + 1) evaluates to NaN instead of reading past its window (ort_nurbs.h)."""
+    import subprocess
+
+    P, W, U, V, _ = _net(3, 2, 1)
+    good = np.asarray(nurbs.lowered_block(P, W, 3, 2, U, V))
+    for bad in (6.0, 0.0):
+        B = good.copy()
+        B[0] = bad  # the u degree
+        n = 4
+        z = np.zeros(n)
+        inp = b"".join([np.int32(B.size).tobytes(), B.tobytes(), np.float64(TOL).tobytes(),
+                        np.int32(20).tobytes(), np.int32(n).tobytes(), z.tobytes(), z.tobytes(),
+                        np.concatenate([z, z, z - 3, z, z, z + 1]).tobytes()])
+        r = subprocess.run([nurbs_exe], input=inp, capture_output=True, check=True)
+        out = np.frombuffer(r.stdout, dtype=np.float64)
+        assert np.isnan(out).all(), bad
+
+
+def test_unfitted_surface_json_round_trip_keeps_the_fit_grid():
+    """lensio: a NURBS surface not fitted yet keeps its fit window and grid, so
+    fit_surface after from_dict gives the same net."""
+    import json
+
+    from optiland_pr_amd.lensio import geometry_from_dict, geometry_to_dict
+
+    geo = NurbsGeometry(CoordinateSystem(), radius=-50.0, conic=0.3, nurbs_norm_x=12.0,
+                        nurbs_norm_y=9.0, x_center=1.5, y_center=-2.0, n_points_u=6,
+                        n_points_v=8)
+    back = geometry_from_dict(json.loads(json.dumps(geometry_to_dict(geo))))
+    geo.fit_surface()
+    back.fit_surface()
+    np.testing.assert_array_equal(back.P, geo.P)
+    np.testing.assert_array_equal(back.P, g("fit_offcentre", "P"))
