@@ -664,8 +664,16 @@ __device__ inline __attribute__((always_inline)) ort::Ray trace_ray(const KArgs&
       range_bits |= ORT_STATUS_BAD_APODIZATION;
   }
 
+#ifdef ORT_PREFETCH_SURF  // (A/B builds) surface si + 1's record loaded during surface si
+  ort_surface s_next = cst(a.surf)[a.start_surface < a.n_surf ? a.start_surface : 0];
+#endif
   for (int si = a.start_surface; si < a.n_surf; ++si) {
+#ifdef ORT_PREFETCH_SURF
+    const ort_surface s = s_next;
+    s_next = cst(a.surf)[si + 1 < a.n_surf ? si + 1 : si];
+#else
     const ort_surface s = cst(a.surf)[si];
+#endif
     const ort_surface_optics o = surface_optics<FEAT>(a, s, lam, si, wl);
     double* tp = nullptr;  // F_TAPE: this surface's tape rows of this ray
     if constexpr ((FEAT & F_TAPE) != 0) {
@@ -888,8 +896,16 @@ __device__ __forceinline__ void trace_block(const KArgs& a, const int32_t* sched
       range_bits |= ORT_STATUS_BAD_APODIZATION;
   }
 
+#ifdef ORT_PREFETCH_SURF  // (A/B builds) surface si + 1's record loaded during surface si
+  ort_surface s_next = cst(a.surf)[a.start_surface < a.n_surf ? a.start_surface : 0];
+#endif
   for (int si = a.start_surface; si < a.n_surf; ++si) {
+#ifdef ORT_PREFETCH_SURF
+    const ort_surface s = s_next;
+    s_next = cst(a.surf)[si + 1 < a.n_surf ? si + 1 : si];
+#else
     const ort_surface s = cst(a.surf)[si];
+#endif
     const ort_surface_optics o = surface_optics<FEAT>(a, s, lam, si, wl);
     double* tp = nullptr;  // F_TAPE: this surface's tape rows of this ray
     if constexpr ((FEAT & F_TAPE) != 0) {
@@ -1116,8 +1132,16 @@ template <uint32_t FEAT, bool FAST>
 __device__ inline void closed_surfaces(const KArgs& a, ort::Ray& r, int lam, double wl,
                                        int64_t rid, bool active, bool& bad, bool& geom_bad,
                                        double apod = 1.0) {
+#ifdef ORT_PREFETCH_SURF  // (A/B builds) surface si + 1's record loaded during surface si
+  ort_surface s_next = cst(a.surf)[a.start_surface < a.n_surf ? a.start_surface : 0];
+#endif
   for (int si = a.start_surface; si < a.n_surf; ++si) {
+#ifdef ORT_PREFETCH_SURF
+    const ort_surface s = s_next;
+    s_next = cst(a.surf)[si + 1 < a.n_surf ? si + 1 : si];
+#else
     const ort_surface s = cst(a.surf)[si];
+#endif
     const ort_surface_optics o = surface_optics<FEAT>(a, s, lam, si, wl);
     if constexpr ((FEAT & F_AXIAL) != 0)
       r.z = r.z + -s.cs_t[2];  // x + -0 and y + -0 are identities
