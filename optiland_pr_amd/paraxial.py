@@ -69,7 +69,8 @@ class Paraxial:
     def f2(self):
         z_start = self.surfaces.positions[1] - 1
         y, u = self._trace_generic(1.0, 0.0, z_start, self.optic.primary_wavelength)
-        f2 = -y[0] / u[-1]
+        with np.errstate(divide="ignore"):  # an afocal system: inf, as the reference returns
+            f2 = -y[0] / u[-1]
         return np.abs(f2[0])
 
     # -- paraxial.py:207-230 --

@@ -30,7 +30,8 @@ def _seam_leaves(torch, lens, spec):
         t0 = float(sg.surfaces[si].thickness)
         t = torch.tensor(t0, dtype=torch.float64, requires_grad=True)
         for s in sg.surfaces[si + 1:]:
-            s.geometry.cs.z = float(s.geometry.cs.z) + (t - t0)
+            z = s.geometry.cs.z  # (as set_thickness: from the detached value)
+            s.geometry.cs.z = float(z.detach() if torch.is_tensor(z) else z) + (t - t0)
         leaves.append(t)
     return leaves
 

@@ -156,7 +156,7 @@ def test_trace_pupil_fused_rms_cpu():
     assert plain[10].numel() == 0
     rms = torch.ops.ort.rms_spot(plain[0], plain[1])[0]
     g_plain = torch.autograd.grad(rms, leaves)
-    np.testing.assert_allclose(float(fused[10]), float(rms.detach()), rtol=1e-14)
+    np.testing.assert_allclose(float(fused[10].detach()), float(rms.detach()), rtol=1e-14)
     for a, b in zip(g_fused, g_plain, strict=True):
         np.testing.assert_allclose(a.numpy(), b.numpy(), rtol=1e-12, atol=1e-18)
 
