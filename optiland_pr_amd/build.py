@@ -32,11 +32,13 @@ SOURCES = [os.path.join(CSRC, f) for f in (
 HEADERS = [os.path.join(CSRC, "ort_core.h"), os.path.join(CSRC, "ort_kernels.h"), os.path.join(CSRC, "ort_fastpath.h"),
            os.path.join(CSRC, "ort_adjoint.h"), os.path.join(CSRC, "ort_pupil.h"),
            os.path.join(CSRC, "ort_sincos_table.h"), os.path.join(CSRC, "ort_material.h"), os.path.join(CSRC, "ort_interact.h"), os.path.join(CSRC, "ort_reduce.h"),
-           os.path.join(CSRC, "ort_sweep.h"), os.path.join(REPO, "include", "optiland_rt.h")]
+           os.path.join(CSRC, "ort_sweep.h"), os.path.join(CSRC, "ort_nurbs.h"),
+           os.path.join(REPO, "include", "optiland_rt.h")]
 DEPS = SOURCES + HEADERS
 HOST_SOURCES = [os.path.join(CSRC, "ort_host.cpp")]
 HOST_DEPS = HOST_SOURCES + [os.path.join(CSRC, f) for f in ("ort_core.h", "ort_sweep.h",
-                                                           "ort_material.h", "ort_interact.h")] + [
+                                                           "ort_material.h", "ort_interact.h",
+                                                           "ort_nurbs.h")] + [
     os.path.join(REPO, "include", "optiland_rt.h"), os.path.join(REPO, "include", "optiland_host.h")]
 # the host build keeps the kernels' rounding: no contraction of a*b+c (as -ffp-contract=off
 # on hipcc), no fast-math

@@ -31,7 +31,10 @@ constexpr int kNurbsMaxDeg = 5;
 // Compiled only into the kernels of lenses with NURBS surfaces (ort::KM_NURBS: the six
 // ort_k_trace_ia.hip specialisations and one geometry kernel) -- an out-of-line call in
 // the shared freeform kernels cost them half their occupancy (the call ABI's register
-// and scratch reservations: 150 -> 256 + 74 AGPRs, 400 B scratch, measured).
+// and scratch reservations: 150 -> 256 + 74 AGPRs, 400 B scratch, measured). Inlined
+// even there: the NURBS kernels grow to ~100k instructions, but out-of-line solves
+// (364 VGPRs, 384 B scratch) traced the 1M-ray NURBS lens in 4.99 ms vs 2.76 ms
+// (profiles/r06_ab_nurbs_noinline.log).
 #define ORT_NURBS_FN ORT_INLINE
 
 struct NurbsView {
